@@ -1,0 +1,214 @@
+"""CPU fp32 oracle for the DFC-SA-Res training step.  TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+this module, and only as the checker (or the timed CPU baseline) -- never as part of the product
+path.  The product path (``dfc-sa-unet_amd/``) runs the HIP kernels of ``libdfcsa.so`` and fails
+loudly when they are missing.
+
+What it is: a functional restatement of the reference algorithm in eager PyTorch on the CPU
+(NCHW, fp32; autograd supplies the backward), keyed by the reference's ``state_dict`` names so
+that golden fixtures and our GPU modules can be fed to it directly.  It is *pinned* against
+golden vectors produced by running the reference itself in the build container
+(``tests/golden/make_golden.py``; ``tests/test_oracle_golden.py`` checks it).
+
+Reference functions restated (file:line under the reference checkout):
+  * LightSelfAttention.forward            models/unet_dfc_sa_res.py:20-39   -> light_self_attention
+  * DynamicFusionConvAttnBlock.forward    models/unet_dfc_sa_res.py:95-116  -> dfc_block
+  * UNetDFCSA.forward                     models/unet_dfc_sa_res.py:161-204 -> unet_dfc_sa_res
+  * dice_loss / BCEDiceLoss               utils/metrics.py:6-24, 52-78      -> bce_dice_loss
+  * calculate_metrics ('bce_dice')        utils/metrics.py:211-264          -> calculate_metrics
+  * train step (zero_grad, fwd, sigmoid, loss, backward, clip_grad_norm_(1.0), SGD)
+                                          utils/trainer.py:115-151, train.py:73-78 -> train_step
+"""
+import math
+
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-5
+BN_MOMENTUM = 0.1
+
+
+# ------------------------------------------------------------------------------------------
+# building blocks
+# ------------------------------------------------------------------------------------------
+def conv(x, sd, name, padding=0, bias=True):
+    w = sd[name + ".weight"]
+    b = sd.get(name + ".bias") if bias else None
+    return F.conv2d(x, w, b, padding=padding)
+
+
+def batch_norm(x, sd, name, training, bufs):
+    """nn.BatchNorm2d semantics: train mode normalises with the biased batch variance and
+    updates running stats with momentum 0.1 using the unbiased variance; eval mode uses the
+    running statistics.  ``bufs`` (dict) receives the updated running stats."""
+    rm = sd[name + ".running_mean"].clone()
+    rv = sd[name + ".running_var"].clone()
+    y = F.batch_norm(x, rm, rv, sd[name + ".weight"], sd[name + ".bias"], training,
+                     BN_MOMENTUM, BN_EPS)
+    if training and bufs is not None:
+        bufs[name + ".running_mean"] = rm
+        bufs[name + ".running_var"] = rv
+        nbt = sd.get(name + ".num_batches_tracked")
+        if nbt is not None:
+            bufs[name + ".num_batches_tracked"] = nbt + 1
+    return y
+
+
+def light_self_attention(a, sd, name, pool_size):
+    """models/unet_dfc_sa_res.py:20-39: pooled self-attention, no 1/sqrt(d) scale,
+    softmax over keys, bilinear (align_corners=False) back to H x W, gamma-scaled residual."""
+    B, C, H, W = a.shape
+    p = F.adaptive_avg_pool2d(a, (pool_size, pool_size))
+    N = pool_size * pool_size
+    q = conv(p, sd, name + ".query_conv").reshape(B, -1, N).permute(0, 2, 1)   # [B,N,C']
+    k = conv(p, sd, name + ".key_conv").reshape(B, -1, N)                      # [B,C',N]
+    att = torch.softmax(torch.bmm(q, k), dim=-1)                               # [B,N,N]
+    v = conv(p, sd, name + ".value_conv").reshape(B, C, N)                     # [B,C,N]
+    o = torch.bmm(v, att.permute(0, 2, 1)).reshape(B, C, pool_size, pool_size)
+    o = F.interpolate(o, size=(H, W), mode="bilinear", align_corners=False)
+    return sd[name + ".gamma"] * o + a
+
+
+def dfc_block(x, sd, name, pool_size, training, bufs):
+    """models/unet_dfc_sa_res.py:95-116 (DynamicFusionConvAttnBlock.forward)."""
+    local = F.relu(batch_norm(conv(x, sd, name + ".conv_branch.0", padding=1), sd,
+                              name + ".conv_branch.1", training, bufs))
+    a = F.relu(batch_norm(conv(x, sd, name + ".attn_branch.0"), sd, name + ".attn_branch.1",
+                          training, bufs))
+    attn = light_self_attention(a, sd, name + ".attn_branch.3", pool_size)
+    comb = torch.cat([local, attn], dim=1)
+    g = torch.sigmoid(batch_norm(conv(comb, sd, name + ".gate.0"), sd, name + ".gate.1",
+                                 training, bufs))
+    fused = g * local + (1 - g) * attn
+    out = F.relu(batch_norm(conv(torch.cat([fused, comb], dim=1), sd, name + ".fusion_conv.0"),
+                            sd, name + ".fusion_conv.1", training, bufs))
+    if (name + ".residual_conv.weight") in sd:
+        res = conv(x, sd, name + ".residual_conv", bias=False)
+    else:
+        res = x
+    return out + sd[name + ".res_scale"] * res
+
+
+def conv_transpose2x2(x, sd, name):
+    return F.conv_transpose2d(x, sd[name + ".weight"], sd[name + ".bias"], stride=2)
+
+
+def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None):
+    """models/unet_dfc_sa_res.py:161-204 (UNetDFCSA.forward; UNetDFCSARes adds nothing)."""
+    blk = lambda t, n: dfc_block(t, sd, n, pool_size, training, bufs)  # noqa: E731
+    d1 = blk(x, "down1")
+    d2 = blk(F.max_pool2d(d1, 2, 2), "down2")
+    d3 = blk(F.max_pool2d(d2, 2, 2), "down3")
+    d4 = blk(F.max_pool2d(d3, 2, 2), "down4")
+    u = blk(F.max_pool2d(d4, 2, 2), "bottleneck")
+    for lvl, skip in ((4, d4), (3, d3), (2, d2), (1, d1)):
+        u = conv_transpose2x2(u, sd, f"up{lvl}")
+        if u.shape[2:] != skip.shape[2:]:
+            u = F.interpolate(u, size=skip.shape[2:], mode="bilinear", align_corners=False)
+        u = blk(torch.cat([u, skip], dim=1), f"up_conv{lvl}")
+    return conv(u, sd, "final_conv")
+
+
+# ------------------------------------------------------------------------------------------
+# loss and metrics
+# ------------------------------------------------------------------------------------------
+def bce_dice_loss(p, t, w_bce=1.0, w_dice=1.0, smooth=1.0):
+    """utils/metrics.py:52-78 + :6-24: mean BCE (log clamped at -100 inside F.binary_cross_
+    entropy) + Dice loss over the whole flattened batch."""
+    bce = F.binary_cross_entropy(p, t)
+    pf, tf = p.reshape(-1), t.reshape(-1)
+    inter = (pf * tf).sum()
+    dice = (2.0 * inter + smooth) / (pf.sum() + tf.sum() + smooth)
+    return w_bce * bce + w_dice * (1 - dice)
+
+
+def calculate_metrics(p, t, loss_type="bce_dice", loss_params=None):
+    """utils/metrics.py:211-264 for loss_type 'bce_dice' (the only type any config uses).
+    Note the reference reads 'weight_bce'/'weight_dice' (defaults 1.0), NOT the yaml's
+    'bce_weight'/'dice_weight' keys."""
+    if loss_type != "bce_dice":
+        raise ValueError(f"oracle only restates loss_type 'bce_dice', got {loss_type!r}")
+    loss_params = loss_params or {}
+    b = (p > 0.5).float()
+    inter = (b * t).sum().item()
+    union = (b + t).sum().item() - inter
+    iou = inter / (union + 1e-7)
+    dice = (2.0 * inter) / (b.sum().item() + t.sum().item() + 1e-7)
+    loss = bce_dice_loss(p, t, loss_params.get("weight_bce", 1.0),
+                         loss_params.get("weight_dice", 1.0))
+    return {"loss": loss, "iou": iou, "dice": dice}
+
+
+# ------------------------------------------------------------------------------------------
+# the train step
+# ------------------------------------------------------------------------------------------
+def param_names(sd):
+    """Trainable entries of a DFC-SA-Res state_dict (everything but BN buffers)."""
+    return [k for k in sd if not (k.endswith("running_mean") or k.endswith("running_var")
+                                  or k.endswith("num_batches_tracked"))]
+
+
+def forward_backward(sd, x, t, pool_size, loss_params=None):
+    """fwd -> sigmoid -> calculate_metrics -> backward.  Returns (logits, metrics, grads,
+    updated BN buffers)."""
+    params = {k: (v.detach().clone().requires_grad_(True) if k in set(param_names(sd)) else v)
+              for k, v in sd.items()}
+    bufs = {}
+    logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs)
+    met = calculate_metrics(torch.sigmoid(logits), t, "bce_dice", loss_params)
+    met["loss"].backward()
+    grads = {k: params[k].grad.detach().clone() for k in param_names(sd)}
+    return logits.detach(), met, grads, bufs
+
+
+def clip_and_sgd(sd, grads, mom_bufs, lr=0.01, momentum=0.9, weight_decay=1e-4, max_norm=1.0):
+    """torch.nn.utils.clip_grad_norm_ (utils/trainer.py:149) + torch.optim.SGD step
+    (train.py:73-78): total L2 norm, coef = max_norm/(norm+1e-6) clamped to <= 1;
+    d = g + wd*w; buf = d on the first step else momentum*buf + d; w -= lr*buf."""
+    names = param_names(sd)
+    total = torch.linalg.vector_norm(torch.stack([torch.linalg.vector_norm(grads[k]) for k in names]))
+    coef = torch.clamp(max_norm / (total + 1e-6), max=1.0)
+    new_sd = dict(sd)
+    new_bufs = dict(mom_bufs)
+    clipped = {}
+    for k in names:
+        g = grads[k] * coef
+        clipped[k] = g
+        d = g + weight_decay * sd[k]
+        buf = d.clone() if k not in mom_bufs else momentum * mom_bufs[k] + d
+        new_bufs[k] = buf
+        new_sd[k] = sd[k] - lr * buf
+    return new_sd, new_bufs, total, clipped
+
+
+def train_step(sd, mom_bufs, x, t, pool_size, loss_params=None, lr=0.01, momentum=0.9,
+               weight_decay=1e-4):
+    logits, met, grads, bufs = forward_backward(sd, x, t, pool_size, loss_params)
+    new_sd, new_bufs, norm, clipped = clip_and_sgd(sd, grads, mom_bufs, lr, momentum, weight_decay)
+    new_sd.update(bufs)
+    return new_sd, new_bufs, {"logits": logits, "norm": norm, "grads": clipped, **met}
+
+
+def num_params(sd):
+    return sum(sd[k].numel() for k in param_names(sd))
+
+
+def gflop_per_image(features, H, pool_size):
+    """Analytic fwd conv+bmm FLOPs per image (2*MACs), for documentation cross-checks."""
+    f = features
+    chans = [(None, f[0]), (f[0], f[1]), (f[1], f[2]), (f[2], f[3]), (f[3], 2 * f[3]),
+             (2 * f[3], f[3]), (2 * f[2], f[2]), (2 * f[1], f[1]), (2 * f[0], f[0])]
+    sizes = [H, H // 2, H // 4, H // 8, H // 16, H // 8, H // 4, H // 2, H]
+    total = 0.0
+    for (cin, cout), s in zip(chans, sizes):
+        cin = 3 if cin is None else cin
+        px = s * s
+        total += px * cout * (9 * cin + cin + 2 * cout + 3 * cout + cin)
+        n = pool_size * pool_size
+        cq = cout // 8
+        total += n * cout * (2 * cq + cout) + n * n * (cq + cout)
+    for cin, s in ((2 * f[3], H // 16), (f[3], H // 8), (f[2], H // 4), (f[1], H // 2)):
+        total += s * s * cin * (cin // 2) * 4
+    total += H * H * f[0]
+    return 2 * total / 1e9

@@ -1,0 +1,286 @@
+"""Generate golden fixtures by running the REFERENCE implementation (CPU, fp32).
+
+Runs only in the build container, where the read-only reference checkout lives at
+/root/reference.  The reference itself never travels: only the .npz outputs written next to
+this script are committed and used by the tests (inputs + expected outputs, i.e. data).
+
+Reference files imported (file-by-file, via importlib, because the reference's package
+``__init__`` files import modules that do not exist):
+  * models/unet_dfc_sa_res.py   LightSelfAttention :5-39, DynamicFusionConvAttnBlock :41-116,
+                                UNetDFCSA :118-204, UNetDFCSARes :207-220
+  * utils/metrics.py            dice_loss :6-24, BCEDiceLoss :52-78, calculate_metrics :211-264
+  * models/unet.py              UNet :69-101 (config 1)
+The train-step semantics follow utils/trainer.py:115-151 and train.py:73-78.
+
+Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz, ~a few MB)
+"""
+import importlib.util
+import os
+import sys
+
+import numpy as np
+import torch
+
+REF = os.environ.get("DFCSA_REFERENCE", "/root/reference")
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _load(name, rel):
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, rel))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    return mod
+
+
+ref_res = _load("ref_unet_dfc_sa_res", "models/unet_dfc_sa_res.py")
+ref_metrics = _load("ref_metrics", "utils/metrics.py")
+ref_unet = _load("ref_unet", "models/unet.py")
+
+
+def np32(t):
+    return t.detach().cpu().numpy().astype(np.float32)
+
+
+def save(name, **arrays):
+    path = os.path.join(OUT, name)
+    np.savez_compressed(path, **{k: np.asarray(v) for k, v in arrays.items()})
+    print(f"wrote {name}: {sum(np.asarray(v).nbytes for v in arrays.values())/1e6:.2f} MB raw")
+
+
+def sd_arrays(module, prefix="sd."):
+    return {prefix + k: v.detach().cpu().numpy().copy() for k, v in module.state_dict().items()}
+
+
+def grad_arrays(module, prefix="grad."):
+    return {prefix + n: np32(p.grad) for n, p in module.named_parameters() if p.grad is not None}
+
+
+# ----------------------------------------------------------------------------------------
+# (1) LightSelfAttention forward/backward, gamma = 0.7 (gamma inits to 0, which would hide
+#     the attention path).  Non-divisible adaptive-pool windows at H=14 (P=4,8) and H=28 (P=8),
+#     and P > H (pool upsamples) at H=14, P=16/32.
+# ----------------------------------------------------------------------------------------
+def gen_lsa():
+    cases = [(8, 14, p) for p in (4, 8, 16, 32)] + [(8, 28, p) for p in (4, 8, 16, 32)] + \
+            [(8, 56, p) for p in (4, 8)] + [(64, 14, p) for p in (4, 8, 32)] + [(64, 28, 8)]
+    for (C, H, P) in cases:
+        torch.manual_seed(1000 + C * 7 + H * 3 + P)
+        m = ref_res.LightSelfAttention(C, pool_size=P, ablation_on_qk_channels=8)
+        with torch.no_grad():
+            m.gamma.fill_(0.7)
+        x = torch.randn(2, C, H, H, requires_grad=True)
+        y = m(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        save(f"lsa_C{C}_H{H}_P{P}.npz", x=np32(x), g=np32(g), y=np32(y), dx=np32(x.grad),
+             **sd_arrays(m), **grad_arrays(m))
+
+
+# ----------------------------------------------------------------------------------------
+# (2) DynamicFusionConvAttnBlock, train-mode forward + backward + BN running stats.
+# ----------------------------------------------------------------------------------------
+def gen_block():
+    for (cin, cout, H, P) in [(3, 8, 32, 4), (16, 8, 16, 8), (16, 16, 14, 4)]:
+        torch.manual_seed(2000 + cin * 11 + cout + H)
+        blk = ref_res.DynamicFusionConvAttnBlock(cin, cout, pool_size=P, ablation_on_qk_channels=8)
+        with torch.no_grad():
+            blk.attn_branch[3].gamma.fill_(0.7)
+        sd0 = sd_arrays(blk, "sd0.")
+        blk.train()
+        x = torch.randn(2, cin, H, H, requires_grad=True)
+        y = blk(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        save(f"block_{cin}to{cout}_H{H}_P{P}.npz", x=np32(x), g=np32(g), y=np32(y),
+             dx=np32(x.grad), **sd0, **sd_arrays(blk, "sd1."), **grad_arrays(blk))
+
+
+# ----------------------------------------------------------------------------------------
+# (3) Whole model: two full train steps exactly as Trainer.train_epoch + SGD do them.
+# ----------------------------------------------------------------------------------------
+LOSS_PARAMS = {"bce_weight": 0.5, "dice_weight": 0.5}  # as in the DFC yaml configs (ignored keys)
+
+
+def perturb_gammas(model):
+    with torch.no_grad():
+        for i, (n, p) in enumerate(sorted(model.named_parameters())):
+            if n.endswith("gamma"):
+                p.fill_(0.2 + 0.05 * (i % 9))
+
+
+def train_step(model, opt, x, t):
+    """utils/trainer.py:120-151."""
+    opt.zero_grad()
+    out = model(x)
+    prob = torch.sigmoid(out)
+    met = ref_metrics.calculate_metrics(prob, t, "bce_dice", LOSS_PARAMS)
+    loss = met["loss"]
+    loss.backward()
+    norm = torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+    grads = grad_arrays(model)  # post-clip grads
+    opt.step()
+    return out, met, norm, grads
+
+
+def base_model(P=4):
+    """The one initial model every whole-model fixture starts from (stored once, as sd0)."""
+    torch.manual_seed(3000)
+    model = ref_res.UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, ablation_on_qk_channels=8)
+    perturb_gammas(model)
+    sd = {k: v.clone() for k, v in model.state_dict().items()}
+    m = ref_res.UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=P, ablation_on_qk_channels=8)
+    m.load_state_dict(sd)  # pool_size does not change the parameter set
+    return m
+
+
+def batch(gen, shape):
+    x = torch.randn(*shape, generator=gen)
+    t = (torch.rand(shape[0], 1, shape[2], shape[3], generator=gen) > 0.5).float()
+    return x, t
+
+
+def gen_model():
+    # Two full train steps (P=4): step-1 post-clip grads, params + momentum after step 2.
+    model = base_model(4)
+    sd0 = sd_arrays(model, "sd0.")
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    model.train()
+    gen = torch.Generator().manual_seed(3001)
+    x1, t1 = batch(gen, (2, 3, 32, 32))
+    x2, t2 = batch(gen, (2, 3, 32, 32))
+    out1, met1, norm1, g1 = train_step(model, opt, x1, t1)
+    bn1 = {"bn1." + k: v.numpy().copy() for k, v in model.state_dict().items() if "running" in k or "num_batches" in k}
+    out2, met2, norm2, _ = train_step(model, opt, x2, t2)
+    sd2 = sd_arrays(model, "sd2.")
+    save("model_small.npz", x1=np32(x1), t1=np32(t1), x2=np32(x2), t2=np32(t2),
+         logits1=np32(out1), loss1=np32(met1["loss"]), iou1=np.float64(met1["iou"]),
+         dice1=np.float64(met1["dice"]), norm1=np32(norm1),
+         logits2=np32(out2), loss2=np32(met2["loss"]), iou2=np.float64(met2["iou"]),
+         dice2=np.float64(met2["dice"]), norm2=np32(norm2),
+         **sd0, **bn1, **sd2, **{"step1." + k: v for k, v in g1.items()})
+
+    # P=8 (non-divisible pool windows at 4x4/2x2 maps, P > H at the bottleneck): fwd + grads.
+    model = base_model(8)
+    model.train()
+    out = model(x1)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t1, "bce_dice", LOSS_PARAMS)
+    met["loss"].backward()
+    save("model_p8.npz", logits=np32(out), loss=np32(met["loss"]), iou=np.float64(met["iou"]),
+         dice=np.float64(met["dice"]), **grad_arrays(model))
+
+    # Non-divisible input (36 -> 18 -> 9 -> 4 -> 2): exercises the bilinear shape fix
+    # (unet_dfc_sa_res.py:180-199) and floor max-pooling of odd sizes.  Forward + grads.
+    model = base_model(4)
+    model.train()
+    gen = torch.Generator().manual_seed(3100)
+    x, t = batch(gen, (1, 3, 36, 36))
+    out = model(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
+    met["loss"].backward()
+    save("model_odd36.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+         iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), **grad_arrays(model))
+
+    # Eval-mode forward (BN running statistics) after perturbing the running stats.
+    model = base_model(4)
+    torch.manual_seed(3200)
+    with torch.no_grad():
+        for n, b in model.named_buffers():
+            if n.endswith("running_mean"):
+                b.normal_(0, 0.1)
+            elif n.endswith("running_var"):
+                b.uniform_(0.5, 1.5)
+    model.eval()
+    x = torch.randn(2, 3, 32, 32)
+    with torch.no_grad():
+        out = model(x)
+    save("model_eval.npz", x=np32(x), logits=np32(out),
+         **{"buf." + k: v.numpy() for k, v in model.state_dict().items() if "running" in k})
+
+
+# ----------------------------------------------------------------------------------------
+# (4) calculate_metrics edge cases (BCE log clamp at -100, p == 0.5 threshold, empty masks,
+#     the weight_bce/weight_dice vs bce_weight/dice_weight key gotcha).
+# ----------------------------------------------------------------------------------------
+def gen_metrics():
+    rng = np.random.default_rng(4000)
+    p = rng.uniform(0, 1, size=(2, 1, 16, 16)).astype(np.float32)
+    t = (rng.uniform(size=(2, 1, 16, 16)) > 0.5).astype(np.float32)
+    p_edge = p.copy()
+    p_edge[0, 0, 0, :4] = [0.0, 1.0, 0.5, 0.5]
+    t_edge = t.copy()
+    t_edge[0, 0, 0, :4] = [1.0, 0.0, 1.0, 0.0]
+    cases = {
+        "random_default": (p, t, {}),
+        "random_keygotcha": (p, t, {"bce_weight": 0.5, "dice_weight": 0.5}),
+        "random_weighted": (p, t, {"weight_bce": 0.3, "weight_dice": 2.0}),
+        "edge_clamp": (p_edge, t_edge, {}),
+        "empty_mask": (p, np.zeros_like(t), {}),
+        "all_low": (p * 0.4, t, {}),
+    }
+    out = {}
+    for k, (pp, tt, params) in cases.items():
+        pt = torch.tensor(pp, requires_grad=True)
+        tt_ = torch.tensor(tt)
+        met = ref_metrics.calculate_metrics(pt, tt_, "bce_dice", params)
+        met["loss"].backward()
+        out[k + ".p"] = pp
+        out[k + ".t"] = tt
+        out[k + ".wbce"] = np.float32(params.get("weight_bce", 1.0))
+        out[k + ".wdice"] = np.float32(params.get("weight_dice", 1.0))
+        out[k + ".loss"] = np32(met["loss"])
+        out[k + ".iou"] = np.float64(met["iou"])
+        out[k + ".dice"] = np.float64(met["dice"])
+        out[k + ".dp"] = np32(pt.grad)
+    save("metrics_bce_dice.npz", **out)
+
+
+# ----------------------------------------------------------------------------------------
+# (5) DDP parity target: mean over 4 shards (2 images each) of per-shard gradients (local BN,
+#     per-shard Dice), from identical initial weights.  Also 2 shards of 4.
+# ----------------------------------------------------------------------------------------
+def gen_ddp():
+    sd = {k: v.clone() for k, v in base_model(4).state_dict().items()}  # = model_small sd0
+    gen = torch.Generator().manual_seed(5001)
+    x, t = batch(gen, (8, 3, 32, 32))
+    res = {"x": np32(x), "t": np32(t)}
+    for world in (2, 4):
+        acc = None
+        per = x.shape[0] // world
+        for r in range(world):
+            m = ref_res.UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, ablation_on_qk_channels=8)
+            m.load_state_dict(sd)
+            m.train()
+            out = m(x[r * per:(r + 1) * per])
+            met = ref_metrics.calculate_metrics(torch.sigmoid(out), t[r * per:(r + 1) * per],
+                                                "bce_dice", LOSS_PARAMS)
+            met["loss"].backward()
+            g = grad_arrays(m)
+            acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
+        for k, v in acc.items():
+            res[f"w{world}.mean_{k}"] = v / world
+    save("ddp_shards.npz", **res)
+
+
+# ----------------------------------------------------------------------------------------
+# (6) Config 1 plumbing: plain UNet (widths hard-coded 64..1024) at 64x64, batch 2.
+# ----------------------------------------------------------------------------------------
+def gen_unet():
+    torch.manual_seed(6000)
+    m = ref_unet.UNet(3, 1, bilinear=False)
+    m.train()
+    x = torch.randn(2, 3, 20, 20)
+    t = (torch.rand(2, 1, 20, 20) > 0.5).float()
+    out = m(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", {})
+    met["loss"].backward()
+    n = sum(p.numel() for p in m.parameters())
+    save("unet_small.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+         nparams=np.int64(n))
+
+
+if __name__ == "__main__":
+    torch.set_num_threads(8)
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet"]
+    for w in which:
+        globals()["gen_" + w]()
+    print("torch", torch.__version__)

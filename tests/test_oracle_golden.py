@@ -1,0 +1,134 @@
+"""Pin the CPU oracle (oracle/dfcsa_oracle.py) against golden vectors produced by running the
+reference implementation itself (tests/golden/make_golden.py).  CPU only."""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import dfcsa_oracle as O
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def T(a):
+    return torch.from_numpy(np.asarray(a))
+
+
+def sd_from(fx, prefix):
+    return {k[len(prefix):]: T(v) for k, v in fx.items() if k.startswith(prefix)}
+
+
+def close(a, b, rtol=1e-5, atol=1e-5):
+    a = a.detach().numpy() if torch.is_tensor(a) else np.asarray(a)
+    np.testing.assert_allclose(a, np.asarray(b), rtol=rtol, atol=atol)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "lsa_*.npz"))),
+                         ids=os.path.basename)
+def test_lsa(path):
+    fx = dict(np.load(path))
+    P = int(os.path.basename(path).split("_P")[1].split(".")[0])
+    sd = {k[3:]: T(v).requires_grad_(True) for k, v in fx.items() if k.startswith("sd.")}
+    x = T(fx["x"]).requires_grad_(True)
+    sdp = {"m." + k: v for k, v in sd.items()}
+    y = O.light_self_attention(x, sdp, "m", P)
+    close(y, fx["y"])
+    y.backward(T(fx["g"]))
+    close(x.grad, fx["dx"], rtol=1e-4, atol=1e-5)
+    for k in sd:
+        close(sd[k].grad, fx["grad." + k], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "block_*.npz"))),
+                         ids=os.path.basename)
+def test_block(path):
+    fx = dict(np.load(path))
+    P = int(os.path.basename(path).split("_P")[1].split(".")[0])
+    sd0 = {"b." + k: v for k, v in sd_from(fx, "sd0.").items()}
+    params = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+              for k, v in sd0.items()}
+    x = T(fx["x"]).requires_grad_(True)
+    bufs = {}
+    y = O.dfc_block(x, params, "b", P, True, bufs)
+    close(y, fx["y"], rtol=1e-4, atol=1e-5)
+    y.backward(T(fx["g"]))
+    close(x.grad, fx["dx"], rtol=1e-4, atol=1e-4)
+    for k, v in fx.items():
+        if k.startswith("grad."):
+            close(params["b." + k[5:]].grad, v, rtol=1e-3, atol=1e-4)
+        if k.startswith("sd1.") and ("running" in k or "num_batches" in k):
+            close(bufs["b." + k[4:]], v, rtol=1e-5, atol=1e-6)
+
+
+def test_model_two_steps():
+    fx = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    sd = sd_from(fx, "sd0.")
+    lp = {"bce_weight": 0.5, "dice_weight": 0.5}
+    sd1, bufs, m1 = O.train_step(sd, {}, T(fx["x1"]), T(fx["t1"]), 4, lp)
+    close(m1["logits"], fx["logits1"], rtol=1e-4, atol=1e-5)
+    close(m1["loss"], fx["loss1"], rtol=1e-5, atol=1e-6)
+    assert abs(m1["iou"] - fx["iou1"]) < 1e-6 and abs(m1["dice"] - fx["dice1"]) < 1e-6
+    close(m1["norm"], fx["norm1"], rtol=1e-4)
+    for k in O.param_names(sd):
+        close(m1["grads"][k], fx["step1.grad." + k], rtol=1e-3, atol=1e-5)
+    for k, v in fx.items():
+        if k.startswith("bn1."):
+            close(sd1[k[4:]], v, rtol=1e-5, atol=1e-6)
+    sd2, bufs, m2 = O.train_step(sd1, bufs, T(fx["x2"]), T(fx["t2"]), 4, lp)
+    close(m2["loss"], fx["loss2"], rtol=1e-4, atol=1e-6)
+    for k in sd:
+        close(sd2[k], fx["sd2." + k], rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("name,P", [("model_p8.npz", 8), ("model_odd36.npz", 4)])
+def test_model_grads(name, P):
+    base = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    sd = sd_from(base, "sd0.")
+    fx = dict(np.load(os.path.join(GOLDEN, name)))
+    x = T(fx["x"]) if "x" in fx else T(base["x1"])
+    t = T(fx["t"]) if "t" in fx else T(base["t1"])
+    logits, met, grads, _ = O.forward_backward(sd, x, t, P, {"bce_weight": 0.5})
+    close(logits, fx["logits"], rtol=1e-4, atol=1e-5)
+    close(met["loss"], fx["loss"], rtol=1e-5)
+    for k in O.param_names(sd):
+        close(grads[k], fx["grad." + k], rtol=1e-3, atol=1e-5)
+
+
+def test_model_eval():
+    base = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    sd = sd_from(base, "sd0.")
+    fx = dict(np.load(os.path.join(GOLDEN, "model_eval.npz")))
+    sd.update(sd_from(fx, "buf."))
+    with torch.no_grad():
+        y = O.unet_dfc_sa_res(T(fx["x"]), sd, 4, training=False)
+    close(y, fx["logits"], rtol=1e-4, atol=1e-5)
+
+
+def test_metrics():
+    fx = dict(np.load(os.path.join(GOLDEN, "metrics_bce_dice.npz")))
+    cases = sorted({k.split(".")[0] for k in fx})
+    for c in cases:
+        p = T(fx[c + ".p"]).requires_grad_(True)
+        params = {"weight_bce": float(fx[c + ".wbce"]), "weight_dice": float(fx[c + ".wdice"])}
+        m = O.calculate_metrics(p, T(fx[c + ".t"]), "bce_dice", params)
+        close(m["loss"], fx[c + ".loss"], rtol=1e-6)
+        assert abs(m["iou"] - fx[c + ".iou"]) < 1e-9 and abs(m["dice"] - fx[c + ".dice"]) < 1e-9
+        m["loss"].backward()
+        close(p.grad, fx[c + ".dp"], rtol=1e-5, atol=1e-7)
+
+
+def test_ddp_shard_means():
+    base = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    sd = sd_from(base, "sd0.")
+    fx = dict(np.load(os.path.join(GOLDEN, "ddp_shards.npz")))
+    x, t = T(fx["x"]), T(fx["t"])
+    for world in (2, 4):
+        per = x.shape[0] // world
+        acc = None
+        for r in range(world):
+            _, _, g, _ = O.forward_backward(sd, x[r * per:(r + 1) * per], t[r * per:(r + 1) * per], 4)
+            acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
+        for k in acc:
+            close(acc[k] / world, fx[f"w{world}.mean_grad.{k}"], rtol=1e-3, atol=1e-5)
