@@ -1,0 +1,579 @@
+// DFC block elementwise stages and the train-mode BatchNorm machinery, NHWC, vectorised over
+// 8-channel chunks (16-B bf16 / 32-B f32 accesses).
+//
+// Reference (models/unet_dfc_sa_res.py):
+//   :57-62 local = ReLU(BN(conv3x3 x))           :65-69 a = ReLU(BN(conv1x1 x)) -> LSA
+//   :36-38 attn = gamma * bilinear(o) + a        :73-77 g = Sigmoid(BN(conv1x1 [local, attn]))
+//   :106  fused = g*local + (1-g)*attn           :80-84 ReLU(BN(conv1x1 [fused, local, attn]))
+//   :113-114 out = out + res_scale * residual_conv(x)
+// BatchNorm2d train semantics (torch.nn.BatchNorm2d, momentum 0.1, eps 1e-5): normalise with
+// the biased batch variance, update running_var with the unbiased one.  The statistics come
+// from the producing GEMM's epilogue (sums of the fp32 accumulator) so no extra pass is made.
+//
+// Backward: every BatchNorm backward is split into (1) an elementwise stage that forms
+// dz = dL/d(BN output) and per-tile per-channel partial sums (sum dz, sum dz*xhat, ...), (2) a
+// finalize that reduces the partial slabs in a fixed order (fp64) and (3) an apply stage
+// dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)) that also emits the conv-bias partial
+// sums.  Nothing uses float atomics: results are bitwise reproducible.
+#include <algorithm>
+#include <cstring>
+
+#include "common.h"
+#include "dfcsa_internal.h"
+
+namespace {
+
+enum {
+  EW_BN_ACT = 0,
+  EW_LOCAL_ATTN,
+  EW_GATE_FUSE,
+  EW_BLOCK_OUT,
+  EW_BWD_BLOCK_OUT,
+  EW_BWD_RELU_BN,
+  EW_BWD_GATE,
+  EW_BWD_ATTN_ENTRY,
+  EW_BN_BWD_APPLY,
+  EW_CHANNEL_SUM,
+};
+
+struct EwArgs {
+  int M, C, B, H, W, P, act;
+  const void* a0;
+  const void* a1;
+  const void* a2;
+  const void* a3;
+  void* o0;
+  void* o1;
+  void* o2;
+  void* o3;
+  const float* sc;
+  const float* sh;
+  const float* sc2;
+  const float* sh2;
+  const float* mean;
+  const float* invstd;
+  const float* gamma;
+  const float* coef;
+  const float* tbl;     // o (fp32 [B][P][P][C]) or dpooled
+  const float* scalar;  // gamma of LSA / res_scale
+  float* partial;
+  int tile_px;          // pixels per reduction tile
+};
+
+__device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
+
+// PyTorch upsample_bilinear2d (align_corners=False) source index/lambda for one axis.
+__device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  float scale = (float)in / (float)out;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+// ------------------------------- forward (no reductions) -------------------------------
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
+  const int cpp = a.C >> 3;
+  const int64_t total = (int64_t)a.M * cpp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int m = (int)(e / cpp);
+    const int c0 = (int)(e - (int64_t)m * cpp) * 8;
+    const size_t off = (size_t)m * a.C + c0;
+    float sc[8], sh[8], y[8], out[8];
+    if (a.a0) {
+      ld8f(a.sc + c0, sc);
+      ld8f(a.sh + c0, sh);
+      load8<T>((const T*)a.a0 + off, y);
+    }
+    if constexpr (MODE == EW_BN_ACT) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = y[q] * sc[q] + sh[q];
+        out[q] = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 2 ? sigm(v) : v);
+      }
+      store8<T>((T*)a.o0 + off, out);
+    } else if constexpr (MODE == EW_LOCAL_ATTN) {
+      // a0 = y1 (sc, sh), a1 = y2 (sc2, sh2); tbl = o [B][P][P][C]; o0 = local, o1 = attn
+      if (a.o0) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f);
+        store8<T>((T*)a.o0 + off, out);
+      }
+      float y2[8], sc2[8], sh2[8];
+      load8<T>((const T*)a.a1 + off, y2);
+      ld8f(a.sc2 + c0, sc2);
+      ld8f(a.sh2 + c0, sh2);
+      const int hw = a.H * a.W;
+      const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
+      int h0, h1, w0, w1;
+      float lh0, lh1, lw0, lw1;
+      bilin_axis(h, a.P, a.H, h0, h1, lh0, lh1);
+      bilin_axis(w, a.P, a.W, w0, w1, lw0, lw1);
+      const float* ob = a.tbl + (size_t)b * a.P * a.P * a.C + c0;
+      float o00[8], o01[8], o10[8], o11[8];
+      ld8f(ob + (size_t)(h0 * a.P + w0) * a.C, o00);
+      ld8f(ob + (size_t)(h0 * a.P + w1) * a.C, o01);
+      ld8f(ob + (size_t)(h1 * a.P + w0) * a.C, o10);
+      ld8f(ob + (size_t)(h1 * a.P + w1) * a.C, o11);
+      const float gm = *a.scalar;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float up = lh0 * (lw0 * o00[q] + lw1 * o01[q]) + lh1 * (lw0 * o10[q] + lw1 * o11[q]);
+        const float v = y2[q] * sc2[q] + sh2[q];
+        out[q] = gm * up + (a.act ? fmaxf(v, 0.f) : v);
+      }
+      store8<T>((T*)a.o1 + off, out);
+    } else if constexpr (MODE == EW_GATE_FUSE) {
+      float l[8], at[8];
+      load8<T>((const T*)a.a1 + off, l);
+      load8<T>((const T*)a.a2 + off, at);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float g = sigm(y[q] * sc[q] + sh[q]);
+        out[q] = g * l[q] + (1.f - g) * at[q];
+      }
+      store8<T>((T*)a.o0 + off, out);
+    } else if constexpr (MODE == EW_BLOCK_OUT) {
+      float r[8];
+      load8<T>((const T*)a.a1 + off, r);
+      const float rs = *a.scalar;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f) + rs * r[q];
+      store8<T>((T*)a.o0 + off, out);
+    }
+  }
+}
+
+// ------------------------- backward stages with per-channel partial sums ----------------
+template <int MODE> struct NSums { static constexpr int v = 2; };
+template <> struct NSums<EW_BWD_BLOCK_OUT> { static constexpr int v = 3; };
+template <> struct NSums<EW_BN_BWD_APPLY> { static constexpr int v = 1; };
+template <> struct NSums<EW_CHANNEL_SUM> { static constexpr int v = 1; };
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
+  constexpr int NS = NSums<MODE>::v;
+  const int cpp = a.C >> 3;                   // chunks per pixel (<= 256)
+  const int pl = 256 / cpp;                   // pixel lanes
+  const int tid = threadIdx.x;
+  const int lane_px = tid / cpp, ck = tid - lane_px * cpp;
+  const int c0 = ck * 8;
+  const bool active = lane_px < pl;
+  float acc[NS][8];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[s][q] = 0.f;
+
+  const int mbeg = blockIdx.x * a.tile_px;
+  const int mend = min(a.M, mbeg + a.tile_px);
+  float sc[8], sh[8], mu[8], is[8];
+  if (active) {
+    if (a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
+    if (a.mean) { ld8f(a.mean + c0, mu); ld8f(a.invstd + c0, is); }
+  }
+  if (active) {
+    for (int m = mbeg + lane_px; m < mend; m += pl) {
+      const size_t off = (size_t)m * a.C + c0;
+      if constexpr (MODE == EW_CHANNEL_SUM) {
+        float x[8];
+        load8<T>((const T*)a.a0 + off, x);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[0][q] += x[q];
+      } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
+        // a0 = dout, a1 = y4, a2 = res; o0 = dz4, o1 = dres
+        float d[8], y[8], r[8], dz[8], dr[8];
+        load8<T>((const T*)a.a0 + off, d);
+        load8<T>((const T*)a.a1 + off, y);
+        load8<T>((const T*)a.a2 + off, r);
+        const float rs = *a.scalar;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
+          dz[q] = z;
+          dr[q] = rs * d[q];
+          acc[0][q] += z;
+          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+          acc[2][q] += d[q] * r[q];
+        }
+        store8<T>((T*)a.o0 + off, dz);
+        store8<T>((T*)a.o1 + off, dr);
+      } else if constexpr (MODE == EW_BWD_RELU_BN) {
+        float d[8], y[8], dz[8];
+        load8<T>((const T*)a.a0 + off, d);
+        load8<T>((const T*)a.a1 + off, y);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
+          dz[q] = z;
+          acc[0][q] += z;
+          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+        }
+        store8<T>((T*)a.o0 + off, dz);
+      } else if constexpr (MODE == EW_BWD_GATE) {
+        // a0 = dfused, a1 = y3, a2 = local, a3 = attn; o0 = dlocal(+=), o1 = dattn(+=), o2 = dz3
+        float df[8], y[8], l[8], at[8], dl[8], da[8], dz[8];
+        load8<T>((const T*)a.a0 + off, df);
+        load8<T>((const T*)a.a1 + off, y);
+        load8<T>((const T*)a.a2 + off, l);
+        load8<T>((const T*)a.a3 + off, at);
+        load8<T>((const T*)a.o0 + off, dl);
+        load8<T>((const T*)a.o1 + off, da);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float g = sigm(y[q] * sc[q] + sh[q]);
+          float dg = df[q] * (l[q] - at[q]);
+          float z = dg * g * (1.f - g);
+          dz[q] = z;
+          dl[q] += df[q] * g;
+          da[q] += df[q] * (1.f - g);
+          acc[0][q] += z;
+          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+        }
+        store8<T>((T*)a.o0 + off, dl);
+        store8<T>((T*)a.o1 + off, da);
+        store8<T>((T*)a.o2 + off, dz);
+      } else if constexpr (MODE == EW_BWD_ATTN_ENTRY) {
+        // a0 = dattn, a1 = y2, tbl = dpooled [B][P][P][C]; o0 = dz2
+        float d[8], y[8], dz[8];
+        load8<T>((const T*)a.a0 + off, d);
+        load8<T>((const T*)a.a1 + off, y);
+        const int hw = a.H * a.W;
+        const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - h * a.W;
+        const int P = a.P;
+        // adaptive-avg-pool windows containing (h, w): rows [floor(i*H/P), ceil((i+1)*H/P))
+        const int pi0 = (h * P) / a.H, pi1 = ((h + 1) * P + a.H - 1) / a.H - 1;
+        const int pj0 = (w * P) / a.W, pj1 = ((w + 1) * P + a.W - 1) / a.W - 1;
+        float add[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+        for (int pi = pi0; pi <= pi1; ++pi) {
+          const int hs = (pi * a.H) / P, he = ((pi + 1) * a.H + P - 1) / P;
+          for (int pj = pj0; pj <= pj1; ++pj) {
+            const int ws = (pj * a.W) / P, we = ((pj + 1) * a.W + P - 1) / P;
+            const float inv = 1.f / (float)((he - hs) * (we - ws));
+            float v[8];
+            ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) add[q] += v[q] * inv;
+          }
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float z = (!a.act || y[q] * sc[q] + sh[q] > 0.f) ? (d[q] + add[q]) : 0.f;
+          dz[q] = z;
+          acc[0][q] += z;
+          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+        }
+        store8<T>((T*)a.o0 + off, dz);
+      } else if constexpr (MODE == EW_BN_BWD_APPLY) {
+        // a0 = dz, a1 = y; gamma, coef [2][C]; o0 = dy; sum dy (conv bias grad)
+        float dz[8], y[8], gm[8], k0[8], k1[8], dy[8];
+        load8<T>((const T*)a.a0 + off, dz);
+        load8<T>((const T*)a.a1 + off, y);
+        ld8f(a.gamma + c0, gm);
+        ld8f(a.coef + c0, k0);
+        ld8f(a.coef + a.C + c0, k1);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          float xh = (y[q] - mu[q]) * is[q];
+          float v = gm[q] * is[q] * (dz[q] - k0[q] - xh * k1[q]);
+          dy[q] = v;
+          acc[0][q] += v;
+        }
+        store8<T>((T*)a.o0 + off, dy);
+      }
+    }
+  }
+  // deterministic in-workgroup reduction over pixel lanes
+  __shared__ float red[256 * 8];
+  float* out = a.partial + (size_t)blockIdx.x * NS * a.C;
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[(lane_px * cpp + ck) * 8 + q] = acc[s][q];
+    }
+    __syncthreads();
+    for (int c = tid; c < a.C; c += 256) {
+      const int k = c >> 3, q = c & 7;
+      float v = 0.f;
+      for (int p = 0; p < pl; ++p) v += red[(p * cpp + k) * 8 + q];
+      out[s * a.C + c] = v;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(
+    const float* __restrict__ stats, int ntiles, int C, int ld, int count, const float* bias, const float* gamma,
+    const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
+    float* scale, float* shift, float* mean, float* invstd) {
+  __shared__ double rs[16][64], rq[16][64];
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0.0, q = 0.0;
+  if (training && c < C) {
+    for (int t = part; t < ntiles; t += 16) {
+      s += (double)stats[(size_t)t * 2 * ld + c];
+      q += (double)stats[(size_t)t * 2 * ld + ld + c];
+    }
+  }
+  rs[part][cl] = s;
+  rq[part][cl] = q;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    float mu, var, istd;
+    if (training) {
+      for (int p = 1; p < 16; ++p) { s += rs[p][cl]; q += rq[p][cl]; }
+      const double n = (double)count;
+      const double ma = s / n;
+      double v = q / n - ma * ma;
+      if (v < 0.0) v = 0.0;
+      const double b = bias ? (double)bias[c] : 0.0;
+      mu = (float)(ma + b);
+      var = (float)v;
+      istd = (float)(1.0 / sqrt(v + (double)eps));
+      const double unb = count > 1 ? v * n / (n - 1.0) : v;
+      rmean[c] = (1.f - momentum) * rmean[c] + momentum * mu;
+      rvar[c] = (float)((1.0 - momentum) * (double)rvar[c] + momentum * unb);
+    } else {
+      mu = rmean[c];
+      var = rvar[c];
+      istd = 1.f / sqrtf(var + eps);
+    }
+    const float sc = gamma[c] * istd;
+    scale[c] = sc;
+    shift[c] = beta[c] - mu * sc;
+    mean[c] = mu;
+    invstd[c] = istd;
+  }
+  if (training && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
+}
+
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ partial, int ntiles,
+                                                               int nsum, int C, int count, float* coef,
+                                                               float* dgamma, float* dbeta, float* third) {
+  __shared__ double r0[16][64], r1[16][64], r2[16][64];
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s0 = 0, s1 = 0, s2 = 0;
+  if (c < C) {
+    for (int t = part; t < ntiles; t += 16) {
+      const float* p = partial + (size_t)t * nsum * C + c;
+      s0 += p[0];
+      s1 += p[C];
+      if (nsum > 2) s2 += p[2 * C];
+    }
+  }
+  r0[part][cl] = s0; r1[part][cl] = s1; r2[part][cl] = s2;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    for (int p = 1; p < 16; ++p) { s0 += r0[p][cl]; s1 += r1[p][cl]; s2 += r2[p][cl]; }
+    coef[c] = (float)(s0 / count);
+    coef[C + c] = (float)(s1 / count);
+    if (dgamma) dgamma[c] += (float)s1;
+    if (dbeta) dbeta[c] += (float)s0;
+    if (third) third[c] = (float)s2;
+  }
+}
+
+__global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int C,
+                                                           float* out) {
+  __shared__ double r[16][64];
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double s = 0;
+  if (c < C)
+    for (int t = part; t < ntiles; t += 16) s += slab[(size_t)t * C + c];
+  r[part][cl] = s;
+  __syncthreads();
+  if (part == 0 && c < C) {
+    for (int p = 1; p < 16; ++p) s += r[p][cl];
+    out[c] += (float)s;
+  }
+}
+
+__global__ void __launch_bounds__(256) sum_scalar_kernel(const float* x, int n, float* out) {
+  __shared__ double r[256];
+  double s = 0;
+  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
+  r[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out += (float)r[0];
+}
+
+constexpr int kTilePx = 256;
+
+template <int MODE>
+int launch_fwd(int dtype, const EwArgs& a, hipStream_t st) {
+  if (a.C % 8 || a.M <= 0) return DFCSA_EINVAL;
+  int64_t chunks = (int64_t)a.M * (a.C / 8);
+  int blocks = (int)std::min<int64_t>((chunks + 255) / 256, 256 * 16);
+  if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_fwd_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((ew_fwd_kernel<float, MODE>), dim3(blocks), dim3(256), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <int MODE>
+int launch_red(int dtype, EwArgs a, hipStream_t st) {
+  if (a.C % 8 || a.C > 2048 || a.M <= 0) return DFCSA_EINVAL;
+  a.tile_px = kTilePx;
+  int blocks = (a.M + kTilePx - 1) / kTilePx;
+  if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_red_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);
+  else hipLaunchKernelGGL((ew_red_kernel<float, MODE>), dim3(blocks), dim3(256), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+EwArgs zargs(int M, int C) {
+  EwArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M;
+  a.C = C;
+  return a;
+}
+
+}  // namespace
+
+extern "C" int dfcsa_ew_ntiles(int M, int C) { (void)C; return (M + kTilePx - 1) / kTilePx; }
+
+extern "C" int dfcsa_bn_finalize(const float* stats, int ntiles, int C, int ld, int count, const float* conv_bias,
+                                 const float* gamma, const float* beta, float* running_mean, float* running_var,
+                                 int64_t* nbt, float momentum, float eps, int training, float* scale,
+                                 float* shift, float* mean, float* invstd, void* stream) {
+  if (C <= 0 || (training && (!stats || count <= 0))) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, stats, ntiles,
+                     C, ld, count, conv_bias, gamma, beta, running_mean, running_var, nbt, momentum, eps, training,
+                     scale, shift, mean, invstd);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_bn_act(int dtype, int M, int C, const void* y, const float* scale, const float* shift,
+                            int act, void* out, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = y; a.sc = scale; a.sh = shift; a.act = act; a.o0 = out;
+  return launch_fwd<EW_BN_ACT>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_block_local_attn(int dtype, int B, int H, int W, int C, const void* y1, const float* sc1,
+                                      const float* sh1, const void* y2, const float* sc2, const float* sh2,
+                                      const float* o, int P, const float* gamma, int relu, void* local,
+                                      void* attn, void* stream) {
+  EwArgs a = zargs(B * H * W, C);
+  a.B = B; a.H = H; a.W = W; a.P = P;
+  a.a0 = y1; a.sc = sc1; a.sh = sh1; a.a1 = y2; a.sc2 = sc2; a.sh2 = sh2; a.tbl = o; a.scalar = gamma;
+  a.o0 = y1 ? local : nullptr; a.o1 = attn; a.act = relu;
+  return launch_fwd<EW_LOCAL_ATTN>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_gate_fuse(int dtype, int M, int C, const void* y3, const float* sc3, const float* sh3,
+                               const void* local, const void* attn, void* fused, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = y3; a.sc = sc3; a.sh = sh3; a.a1 = local; a.a2 = attn; a.o0 = fused;
+  return launch_fwd<EW_GATE_FUSE>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_block_out(int dtype, int M, int C, const void* y4, const float* sc4, const float* sh4,
+                               const void* res, const float* res_scale, void* out, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = y4; a.sc = sc4; a.sh = sh4; a.a1 = res; a.scalar = res_scale; a.o0 = out;
+  return launch_fwd<EW_BLOCK_OUT>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, const void* y4, const float* sc4,
+                                   const float* sh4, const float* mean4, const float* invstd4, const void* res,
+                                   const float* res_scale, void* dz4, void* dres, float* partial, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = dout; a.a1 = y4; a.a2 = res; a.sc = sc4; a.sh = sh4; a.mean = mean4; a.invstd = invstd4;
+  a.scalar = res_scale; a.o0 = dz4; a.o1 = dres; a.partial = partial;
+  return launch_red<EW_BWD_BLOCK_OUT>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
+                                 const float* sh, const float* mean, const float* invstd, void* dz,
+                                 float* partial, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.o0 = dz; a.partial = partial;
+  return launch_red<EW_BWD_RELU_BN>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,
+                              const float* sh3, const float* mean3, const float* invstd3, const void* local,
+                              const void* attn, void* dlocal, void* dattn, void* dz3, float* partial,
+                              void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = dfused; a.a1 = y3; a.a2 = local; a.a3 = attn; a.sc = sc3; a.sh = sh3; a.mean = mean3;
+  a.invstd = invstd3; a.o0 = dlocal; a.o1 = dattn; a.o2 = dz3; a.partial = partial;
+  return launch_red<EW_BWD_GATE>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn,
+                                    const float* dpooled, int P, const void* y2, const float* sc2,
+                                    const float* sh2, const float* mean2, const float* invstd2, int relu,
+                                    void* dz2, float* partial, void* stream) {
+  EwArgs a = zargs(B * H * W, C);
+  a.B = B; a.H = H; a.W = W; a.P = P;
+  a.a0 = dattn; a.a1 = y2; a.tbl = dpooled; a.sc = sc2; a.sh = sh2; a.mean = mean2; a.invstd = invstd2;
+  a.o0 = dz2; a.partial = partial; a.act = relu;
+  return launch_red<EW_BWD_ATTN_ENTRY>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count, float* coef,
+                                     float* dgamma, float* dbeta, float* extra, void* stream) {
+  if (nsum < 2 || nsum > 3 || C <= 0) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  // the third per-channel sum (res_scale gradient) is reduced to a scalar afterwards; it is
+  // staged in the tail of `coef` ([3][C]) when requested
+  float* third = (nsum == 3 && extra) ? coef + 2 * C : nullptr;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, partial, ntiles, nsum, C,
+                     count, coef, dgamma, dbeta, third);
+  DFCSA_CHECK_LAUNCH();
+  if (third) {
+    hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, st, third, C, extra);
+    DFCSA_CHECK_LAUNCH();
+  }
+  return 0;
+}
+
+extern "C" int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
+                                  const float* invstd, const float* gamma, const float* coef, void* dy,
+                                  float* bias_partial, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = dz; a.a1 = y; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.coef = coef; a.o0 = dy;
+  a.partial = bias_partial;
+  return launch_red<EW_BN_BWD_APPLY>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream) {
+  if (C <= 0 || ntiles <= 0) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, ntiles,
+                     C, out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, void* stream) {
+  EwArgs a = zargs(M, C);
+  a.a0 = x; a.partial = partial;
+  return launch_red<EW_CHANNEL_SUM>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_sum_to_scalar(const float* x, int n, float* out, void* stream) {
+  if (n <= 0) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}

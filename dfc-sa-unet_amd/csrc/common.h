@@ -1,0 +1,112 @@
+// Shared device/host helpers for libdfcsa (gfx950 / CDNA4 only).
+//
+// Element types: activations and packed weights are stored as T in {float, bf16 (uint16_t)};
+// every reduction, accumulator and statistic is fp32 (fp64 where a whole-tensor sum is formed).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DFCSA_DT_F32 0
+#define DFCSA_DT_BF16 1
+
+typedef uint16_t bf16_t;
+
+// ---------------------------------------------------------------------------------------
+// bf16 <-> f32.  The cast lowers to v_cvt_pk_bf16_f32 (round-to-nearest-even, NaN-preserving).
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float bf2f(uint16_t v) { return __uint_as_float((uint32_t)v << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  __bf16 h = (__bf16)f;
+  return __builtin_bit_cast(uint16_t, h);
+}
+
+template <typename T> struct ElemTraits;
+template <> struct ElemTraits<float> {
+  static constexpr int kChunk = 4;  // elements per 16-byte chunk
+  __device__ __forceinline__ static float to_f(float v) { return v; }
+  __device__ __forceinline__ static float from_f(float v) { return v; }
+};
+template <> struct ElemTraits<bf16_t> {
+  static constexpr int kChunk = 8;
+  __device__ __forceinline__ static float to_f(bf16_t v) { return bf2f(v); }
+  __device__ __forceinline__ static bf16_t from_f(float v) { return f2bf(v); }
+};
+
+// 8 consecutive elements <-> 8 floats (16 B for bf16, 32 B for f32).  p must be 16-B aligned.
+template <typename T> __device__ __forceinline__ void load8(const T* p, float (&v)[8]);
+template <> __device__ __forceinline__ void load8<float>(const float* p, float (&v)[8]) {
+  float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
+  v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+}
+template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float (&v)[8]) {
+  uint4 u = *(const uint4*)p;
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8]);
+template <> __device__ __forceinline__ void store8<float>(float* p, const float (&v)[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
+__device__ __forceinline__ uint32_t pack2bf(float lo, float hi) {
+  return (uint32_t)f2bf(lo) | ((uint32_t)f2bf(hi) << 16);
+}
+template <> __device__ __forceinline__ void store8<bf16_t>(bf16_t* p, const float (&v)[8]) {
+  uint4 u;
+  u.x = pack2bf(v[0], v[1]); u.y = pack2bf(v[2], v[3]);
+  u.z = pack2bf(v[4], v[5]); u.w = pack2bf(v[6], v[7]);
+  *(uint4*)p = u;
+}
+
+// ---------------------------------------------------------------------------------------
+// Fast unsigned division by a runtime constant (valid for 0 <= n < 2^31).
+// ---------------------------------------------------------------------------------------
+struct DivMod {
+  int d;
+  uint32_t mul;
+  uint32_t shr;
+};
+
+static inline DivMod make_divmod(int d) {
+  DivMod r;
+  r.d = d;
+  if (d <= 1) {
+    r.mul = 0;
+    r.shr = 0;
+  } else {
+    uint32_t l = 0;
+    while ((1u << l) < (uint32_t)d) ++l;  // ceil(log2 d)
+    uint32_t p = 31 + l;
+    r.mul = (uint32_t)(((1ull << p) + (uint64_t)d - 1) / (uint64_t)d);
+    r.shr = p - 32;
+  }
+  return r;
+}
+
+__device__ __forceinline__ int dm_div(const DivMod& dm, int n) {
+  return dm.d == 1 ? n : (int)(__umulhi((uint32_t)n, dm.mul) >> dm.shr);
+}
+
+// ---------------------------------------------------------------------------------------
+// wave reductions (wave64)
+// ---------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+#define DFCSA_CHECK_LAUNCH() \
+  do {                       \
+    hipError_t e_ = hipGetLastError(); \
+    if (e_ != hipSuccess) return -(int)e_; \
+  } while (0)
+
+#define DFCSA_EINVAL (-10000)

@@ -1,0 +1,313 @@
+// Implicit-GEMM convolution on MFMA, NHWC, for gfx950.
+//
+//   C[m][n] = sum_k A[m][k] * Bw[n][k]   (+ bias[n]),  fp32 accumulation
+//
+// m enumerates output pixels (b, oh, ow) of an Ho x Wo grid; k enumerates (segment, channel)
+// with segment s = (source tensor, spatial shift dh/dw) and channel c in [0, Cseg):
+//   A[m][s*Cseg + c] = src_s[b, oh*stride + dh_s, ow*stride + dw_s, c]   (0 outside the image)
+// This one formulation covers every convolution of the training step:
+//   * 3x3 conv forward: 9 taps x (1 or 2 concatenated sources)  -> the skip concat is never
+//     materialised (reference models/unet_dfc_sa_res.py:182/188/194/200 torch.cat);
+//   * 1x1 convs over [local, attn] and [fused, local, attn] (reference :102, :109 cat);
+//   * 3x3 dgrad (shifts 1-kh, 1-kw) plus the 1x1 dgrads of the same input in ONE GEMM;
+//   * ConvTranspose2d(k2,s2) forward (epilogue pixel-shuffle) and its dgrad (stride-2 gather).
+// Epilogue: bias, optional accumulate into the destination, split of the N columns over up to
+// three destination tensors, and per-column partial sums (sum, sum of squares) of the fp32
+// accumulator for the following train-mode BatchNorm (one slab row per M tile: deterministic).
+//
+// Tiling: BM x BN workgroup tile, WM x WN waves (wave64), 128-byte K-stage (64 bf16 / 32 f32),
+// register-staged double-buffered LDS with an XOR swizzle that makes the ds_read_b128 fragment
+// reads conflict-free; mfma_f32_16x16x32_bf16 (bf16) or 8 x mfma_f32_16x16x4f32 (f32 parity
+// mode; exact f32 FMA chain).
+#include "common.h"
+#include "dfcsa_internal.h"
+
+namespace {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Frag;
+template <> struct Frag<bf16_t> { bf16x8_t v; };
+template <> struct Frag<float> { float v[8]; };
+
+__device__ __forceinline__ int swz(int r, int c) { return (c ^ ((r >> 1) & 7)); }
+
+template <typename T>
+__device__ __forceinline__ void read_frag(const char* lds_tile, int row, int g, int lane, Frag<T>& f);
+
+// 8 consecutive k at element offset 32*g + 8*(lane>>4) of row `row` (128-byte swizzled rows).
+template <>
+__device__ __forceinline__ void read_frag<bf16_t>(const char* t, int row, int g, int lane, Frag<bf16_t>& f) {
+  int chunk = 4 * g + (lane >> 4);
+  f.v = *(const bf16x8_t*)(t + row * 128 + swz(row, chunk) * 16);
+}
+template <>
+__device__ __forceinline__ void read_frag<float>(const char* t, int row, int g, int lane, Frag<float>& f) {
+  int chunk = 8 * g + 2 * (lane >> 4);
+  float4 a = *(const float4*)(t + row * 128 + swz(row, chunk) * 16);
+  float4 b = *(const float4*)(t + row * 128 + swz(row, chunk + 1) * 16);
+  f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w;
+  f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
+}
+
+__device__ __forceinline__ void mma(f32x4_t& acc, const Frag<bf16_t>& a, const Frag<bf16_t>& b) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a.v, b.v, acc, 0, 0, 0);
+}
+__device__ __forceinline__ void mma(f32x4_t& acc, const Frag<float>& a, const Frag<float>& b) {
+#pragma unroll
+  for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], acc, 0, 0, 0);
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM* WN * 64)
+conv_gemm_kernel(const ConvGemmArgs args) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int EPC = ElemTraits<T>::kChunk;     // elements per 16-B chunk
+  constexpr int KST = 128 / sizeof(T);           // elements per K stage
+  constexpr int NG = KST / 32;                   // 32-wide k groups per stage
+  constexpr int A_CH = BM * 8 / NT;              // A chunks per thread per stage
+  constexpr int B_CH = BN * 8 / NT;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  static_assert(A_CH >= 1 && B_CH >= 1, "tile too small for thread count");
+
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;  // padded output-tile row stride (bytes)
+  constexpr int SMEM_MAIN = 2 * (BM + BN) * 128, SMEM_OUT = BM * OSTR;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN > SMEM_OUT ? SMEM_MAIN : SMEM_OUT];
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  const int wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n_tile = blockIdx.x, m_tile = blockIdx.y;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int M = args.M, N = args.N;
+
+  // ---- per-thread A row info (rows fixed over the K loop) ----
+  const int cchunk = tid & 7;                  // chunk column handled by this thread
+  int a_b[A_CH], a_oh[A_CH], a_ow[A_CH];
+#pragma unroll
+  for (int i = 0; i < A_CH; ++i) {
+    int r = (tid >> 3) + i * (NT / 8);
+    int m = m0 + r;
+    if (m < M) {
+      int b = dm_div(args.dm_hw, m);
+      int rem = m - b * args.dm_hw.d;
+      int oh = dm_div(args.dm_w, rem);
+      a_b[i] = b;
+      a_oh[i] = oh * args.stride;
+      a_ow[i] = (rem - oh * args.dm_w.d) * args.stride;
+    } else {
+      a_b[i] = -1; a_oh[i] = 0; a_ow[i] = 0;
+    }
+  }
+
+  const int nk = args.Kpad / KST;
+  uint4 ra[A_CH], rb[B_CH];
+
+  auto load_stage = [&](int kt) {
+    const int kbase = kt * KST + cchunk * EPC;
+    // A: implicit im2col gather
+    int seg = dm_div(args.dm_cseg, kbase);
+    int ch = kbase - seg * args.Cseg;
+    bool kvalid = kbase < args.K;
+    const ConvSeg sg = args.seg[kvalid ? seg : 0];
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int ih = a_oh[i] + sg.dh, iw = a_ow[i] + sg.dw;
+      bool ok = kvalid && a_b[i] >= 0 && ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi;
+      if (ok) {
+        const T* p = (const T*)sg.ptr + ((size_t)((a_b[i] * args.Hi + ih) * args.Wi + iw) * args.Cseg + ch);
+        ra[i] = *(const uint4*)p;
+      } else {
+        ra[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+    // B: packed weights [N][Kpad]
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      int r = (tid >> 3) + i * (NT / 8);
+      int n = n0 + r;
+      if (n < N) {
+        const T* p = (const T*)args.Bw + ((size_t)n * args.Kpad + kbase);
+        rb[i] = *(const uint4*)p;
+      } else {
+        rb[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_stage = [&](int s) {
+    char* A = smem + s * (BM + BN) * 128;
+    char* B = A + BM * 128;
+#pragma unroll
+    for (int i = 0; i < A_CH; ++i) {
+      int r = (tid >> 3) + i * (NT / 8);
+      *(uint4*)(A + r * 128 + swz(r, cchunk) * 16) = ra[i];
+    }
+#pragma unroll
+    for (int i = 0; i < B_CH; ++i) {
+      int r = (tid >> 3) + i * (NT / 8);
+      *(uint4*)(B + r * 128 + swz(r, cchunk) * 16) = rb[i];
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  load_stage(0);
+  store_stage(0);
+  __syncthreads();
+
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) load_stage(kt + 1);
+    const char* A = smem + (kt & 1) * (BM + BN) * 128;
+    const char* B = A + BM * 128;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      Frag<T> fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) read_frag<T>(A, wm * WTM + i * 16 + (lane & 15), g, lane, fa[i]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) read_frag<T>(B, wn * WTN + j * 16 + (lane & 15), g, lane, fb[j]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
+    }
+    if (more) store_stage((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  // ---------------- epilogue ----------------
+  // (1) BatchNorm partial statistics of the raw accumulator, per column, rows m < M only.
+  float* red = (float*)smem;  // [WM][2][BN] after the main loop
+  if (args.stats) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          float v = (m < M) ? acc[i][j][r] : 0.f;
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        int col = wn * WTN + j * 16 + lane;
+        red[(wm * 2 + 0) * BN + col] = s;
+        red[(wm * 2 + 1) * BN + col] = q;
+      }
+    }
+    __syncthreads();
+    for (int c = tid; c < BN; c += NT) {
+      int n = n0 + c;
+      if (n < N) {
+        float s = 0.f, q = 0.f;
+        for (int w = 0; w < WM; ++w) { s += red[(w * 2) * BN + c]; q += red[(w * 2 + 1) * BN + c]; }
+        args.stats[(size_t)m_tile * 2 * N + n] = s;
+        args.stats[(size_t)m_tile * 2 * N + N + n] = q;
+      }
+    }
+    __syncthreads();
+  }
+
+  // (2) bias, convert, stage the tile through LDS, coalesced 16-B stores.
+  T* otile = (T*)smem;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    int col = wn * WTN + j * 16 + (lane & 15);
+    int n = n0 + col;
+    float bv = (args.bias && n < N) ? args.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        *(T*)((char*)otile + row * OSTR + col * sizeof(T)) = ElemTraits<T>::from_f(acc[i][j][r] + bv);
+      }
+  }
+  __syncthreads();
+  constexpr int OCH = BN / 8;                      // 8-element chunks per tile row
+  for (int e = tid; e < BM * OCH; e += NT) {
+    int row = e / OCH, cc = e % OCH;
+    int m = m0 + row, n = n0 + cc * 8;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    const T* src = (const T*)((const char*)otile + row * OSTR + cc * 8 * sizeof(T));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = ElemTraits<T>::to_f(src[q]);
+    T* dst;
+    if (args.mode == CONV_STORE_SHUFFLE2) {
+      // ConvTranspose2d(k=2, s=2): column n = (i*2 + j) * Cout + co  ->  pixel (2oh+i, 2ow+j)
+      int ij = n / args.Nd, co = n - ij * args.Nd;
+      int b = dm_div(args.dm_hw, m);
+      int rem = m - b * args.dm_hw.d;
+      int oh = dm_div(args.dm_w, rem);
+      int ow = rem - oh * args.dm_w.d;
+      int y = 2 * oh + (ij >> 1), x = 2 * ow + (ij & 1);
+      dst = (T*)args.dest[0] + ((size_t)((b * args.Hout + y) * args.Wout + x) * args.Nd + co);
+    } else {
+      int d = n / args.Nd, col = n - d * args.Nd;
+      dst = (T*)args.dest[d] + ((size_t)m * args.Nd + col);
+    }
+    if (args.accumulate) {
+      float o[8];
+      load8<T>(dst, o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += o[q];
+    }
+    store8<T>(dst, v);
+  }
+}
+
+template <typename T, int BM, int BN, int WM, int WN>
+int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
+  hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+template <typename T>
+int launch_t(const ConvGemmArgs& a, hipStream_t st) {
+  if (a.N <= 64) return launch_cfg<T, 128, 64, 4, 1>(a, st);
+  return launch_cfg<T, 128, 128, 2, 2>(a, st);
+}
+
+}  // namespace
+
+extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
+  if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->M <= 0 || d->N <= 0) return DFCSA_EINVAL;
+  const int chunk = d->dtype == DFCSA_DT_BF16 ? 8 : 4;
+  const int kst = d->dtype == DFCSA_DT_BF16 ? 64 : 32;
+  if (d->Cseg % chunk || d->Kpad % kst || d->Kpad < d->nseg * d->Cseg) return DFCSA_EINVAL;
+  if (d->ndest < 1 || d->ndest > 3 || d->Nd % 8 || (d->mode == CONV_STORE_PLAIN && d->Nd * d->ndest != d->N))
+    return DFCSA_EINVAL;
+  if (d->mode == CONV_STORE_SHUFFLE2 && (d->ndest != 1 || d->N != 4 * d->Nd)) return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  a.M = d->M; a.N = d->N; a.K = d->nseg * d->Cseg; a.Kpad = d->Kpad; a.Cseg = d->Cseg;
+  a.nseg = d->nseg;
+  for (int i = 0; i < d->nseg; ++i) { a.seg[i].ptr = d->seg_ptr[i]; a.seg[i].dh = d->seg_dh[i]; a.seg[i].dw = d->seg_dw[i]; }
+  a.Ho = d->Ho; a.Wo = d->Wo; a.Hi = d->Hi; a.Wi = d->Wi; a.stride = d->stride;
+  a.dm_hw = make_divmod(d->Ho * d->Wo);
+  a.dm_w = make_divmod(d->Wo);
+  a.dm_cseg = make_divmod(d->Cseg);
+  a.Bw = d->weight; a.bias = d->bias;
+  a.mode = d->mode; a.ndest = d->ndest; a.Nd = d->Nd;
+  for (int i = 0; i < 3; ++i) a.dest[i] = i < d->ndest ? d->dest[i] : nullptr;
+  a.accumulate = d->accumulate; a.stats = d->stats;
+  a.Hout = d->Hout; a.Wout = d->Wout;
+  hipStream_t st = (hipStream_t)stream;
+  return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
+}
+
+extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 128; }

@@ -1,0 +1,45 @@
+// Kernel-argument structs shared between translation units (device-side views of the public
+// descriptors in include/dfcsa.h).
+#pragma once
+#include "common.h"
+#include "dfcsa.h"
+
+struct ConvSeg {
+  const void* ptr;
+  int dh, dw;
+};
+
+struct ConvGemmArgs {
+  int M, N, K, Kpad, Cseg, nseg;
+  ConvSeg seg[DFCSA_MAX_SEG];
+  int Ho, Wo, Hi, Wi, stride;
+  DivMod dm_hw, dm_w, dm_cseg;
+  const void* Bw;
+  const float* bias;
+  int mode, ndest;
+  void* dest[3];
+  int Nd, accumulate;
+  float* stats;
+  int Hout, Wout;
+};
+
+struct WgradArgs {
+  int M, NI, NJ, Cg, ng;
+  const void* g_ptr[3];
+  int Cseg, nseg;
+  ConvSeg seg[DFCSA_MAX_SEG];
+  int Ho, Wo, Hi, Wi, stride;
+  DivMod dm_hw, dm_w, dm_cseg, dm_cg;
+  float* slab;
+  int mchunk;
+};
+
+// profiling hook (prof.cpp)
+struct ProfScope {
+  int cls;
+  hipStream_t st;
+  double flops;
+  bool on;
+  ProfScope(int cls, hipStream_t st, double flops);
+  ~ProfScope();
+};

@@ -1,0 +1,443 @@
+// LightSelfAttention (reference models/unet_dfc_sa_res.py:5-39) forward and backward.
+//
+// The attention itself runs on the P x P pooled map (N = P*P <= 1024 tokens), so it is tiny;
+// what costs HBM bandwidth is the full-resolution traffic around it: the adaptive average pool
+// (read once, BN+ReLU of the producing conv applied on the fly) and, in backward, the
+// transposed bilinear upsample (a weighted reduction of the full-resolution gradient onto the
+// P x P grid, done separably: first along W per image row, then along H).
+//
+// Semantics kept exactly: adaptive_avg_pool2d windows [floor(i*H/P), ceil((i+1)*H/P)) (they
+// overlap when P does not divide H, and repeat pixels when P > H); no 1/sqrt(d) scale on
+// q.k; softmax over keys; o = v @ A^T; F.interpolate(bilinear, align_corners=False) with the
+// source index clamped at 0; out = gamma * o + x (x added by the caller's fused stage).
+// Everything here is fp32 and deterministic (fixed-order reductions, no atomics).
+#include "common.h"
+#include "dfcsa_internal.h"
+
+namespace {
+
+__device__ __forceinline__ int win_lo(int i, int H, int P) { return (i * H) / P; }
+__device__ __forceinline__ int win_hi(int i, int H, int P) { return ((i + 1) * H + P - 1) / P; }
+
+__device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  float scale = (float)in / (float)out;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+// weight of source index `p` for destination `dst` along one axis
+__device__ __forceinline__ float bilin_w(int dst, int p, int in, int out) {
+  int i0, i1;
+  float l0, l1;
+  bilin_axis(dst, in, out, i0, i1, l0, l1);
+  return (i0 == p ? l0 : 0.f) + (i1 == p ? l1 : 0.f);
+}
+
+__device__ __forceinline__ float block_reduce_sum(float v, float* sh) {
+  v = wave_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = 0.f;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) r += sh[i];
+  return r;
+}
+__device__ __forceinline__ float block_reduce_max(float v, float* sh) {
+  v = wave_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) sh[w] = v;
+  __syncthreads();
+  float r = -INFINITY;
+  const int nw = blockDim.x >> 6;
+  for (int i = 0; i < nw; ++i) r = fmaxf(r, sh[i]);
+  return r;
+}
+
+int pool_splits(int H, int P) {
+  int maxwh = (H + P - 1) / P + 1;
+  int s = (maxwh + 3) / 4;
+  return s < 1 ? 1 : s;
+}
+
+// grid (S, N, B): row slice s of window n of image b
+template <typename T>
+__global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, const T* __restrict__ y2,
+                                                       const float* __restrict__ sc, const float* __restrict__ sh,
+                                                       int P, int S, int relu, float* __restrict__ partial) {
+  const int s = blockIdx.x, n = blockIdx.y, b = blockIdx.z;
+  const int pi = n / P, pj = n - pi * P;
+  const int hs = win_lo(pi, H, P), he = win_hi(pi, H, P);
+  const int ws = win_lo(pj, W, P), we = win_hi(pj, W, P);
+  const int wh = he - hs, ww = we - ws;
+  const int R = (wh + S - 1) / S;
+  const int r0 = hs + s * R, r1 = min(he, r0 + R);
+  const int cpp = C >> 3, pl = 256 / cpp;
+  const int tid = threadIdx.x, lp = tid / cpp, ck = tid - lp * cpp, c0 = ck * 8;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (lp < pl) {
+    float a[8], bb[8];
+    for (int q = 0; q < 8; ++q) { a[q] = sc[c0 + q]; bb[q] = sh[c0 + q]; }
+    const int npx = (r1 > r0 ? (r1 - r0) : 0) * ww;
+    for (int i = lp; i < npx; i += pl) {
+      const int h = r0 + i / ww, w = ws + i % ww;
+      float v[8];
+      load8<T>(y2 + ((size_t)(b * H + h) * W + w) * C + c0, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float t = v[q] * a[q] + bb[q];
+        acc[q] += relu ? fmaxf(t, 0.f) : t;
+      }
+    }
+  }
+  __shared__ float red[256 * 8];
+  if (lp < pl)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) red[tid * 8 + q] = acc[q];
+  __syncthreads();
+  float* out = partial + (((size_t)b * P * P + n) * S + s) * C;
+  for (int c = tid; c < C; c += 256) {
+    const int k = c >> 3, q = c & 7;
+    float v = 0.f;
+    for (int p = 0; p < pl; ++p) v += red[(p * cpp + k) * 8 + q];
+    out[c] = v;
+  }
+}
+
+// grid (ceil(J/256), ceil(N/16), B); J = 2Cq + C
+__global__ void __launch_bounds__(256) lsa_qkv_kernel(int H, int W, int C, int Cq, int P, int S,
+                                                      const float* __restrict__ partial,
+                                                      const float* __restrict__ wT, const float* __restrict__ bias,
+                                                      float* __restrict__ pooled, float* __restrict__ qkv) {
+  extern __shared__ float prow[];  // [16][C]
+  const int N = P * P, J = 2 * Cq + C;
+  const int b = blockIdx.z, n0 = blockIdx.y * 16, j = blockIdx.x * 256 + threadIdx.x;
+  const int nr = min(16, N - n0);
+  for (int e = threadIdx.x; e < nr * C; e += 256) {
+    const int r = e / C, c = e - r * C, n = n0 + r;
+    const int pi = n / P, pj = n - pi * P;
+    const float area = (float)((win_hi(pi, H, P) - win_lo(pi, H, P)) * (win_hi(pj, W, P) - win_lo(pj, W, P)));
+    const float* p = partial + (((size_t)b * N + n) * S) * C + c;
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += p[(size_t)k * C];
+    const float v = s / area;
+    prow[r * C + c] = v;
+    if (blockIdx.x == 0) pooled[((size_t)b * N + n) * C + c] = v;
+  }
+  __syncthreads();
+  if (j >= J) return;
+  float acc[16];
+  const float bj = bias[j];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = bj;
+  for (int c = 0; c < C; ++c) {
+    const float w = wT[(size_t)c * J + j];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] += prow[r * C + c] * w;
+  }
+  for (int r = 0; r < nr; ++r) qkv[((size_t)b * N + n0 + r) * J + j] = acc[r];
+}
+
+// grid (N, B): one query row per workgroup
+__global__ void __launch_bounds__(256) lsa_attn_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
+                                                       float* __restrict__ A, float* __restrict__ o) {
+  extern __shared__ float sm[];  // q [Cq] | e [N] | red [8]
+  float* q = sm;
+  float* e = sm + Cq;
+  float* red = e + N;
+  const int n = blockIdx.x, b = blockIdx.y, J = 2 * Cq + C;
+  const float* base = qkv + (size_t)b * N * J;
+  for (int c = threadIdx.x; c < Cq; c += 256) q[c] = base[(size_t)n * J + c];
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float* k = base + (size_t)m * J + Cq;
+    float s = 0.f;
+    for (int c = 0; c < Cq; ++c) s += q[c] * k[c];
+    e[m] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = block_reduce_max(mx, red);
+  float sum = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float v = __expf(e[m] - mx);
+    e[m] = v;
+    sum += v;
+  }
+  sum = block_reduce_sum(sum, red);
+  const float inv = 1.f / sum;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float v = e[m] * inv;
+    e[m] = v;
+    A[((size_t)b * N + n) * N + m] = v;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int m = 0; m < N; ++m) s += e[m] * base[(size_t)m * J + 2 * Cq + c];
+    o[((size_t)b * N + n) * C + c] = s;
+  }
+}
+
+// grid (H, B): rows[b][h][pj][c] = sum_w wx(pj, w) * dattn[b][h][w][c]
+template <typename T>
+__global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int C, const T* __restrict__ d, int P,
+                                                              float* __restrict__ rows) {
+  const int h = blockIdx.x, b = blockIdx.y;
+  const int cpp = C >> 3;
+  const T* row = d + ((size_t)b * H + h) * W * C;
+  for (int item = threadIdx.x; item < P * cpp; item += 256) {
+    const int pj = item / cpp, c0 = (item - pj * cpp) * 8;
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // source position of w is increasing in w: start a little before the first contributor
+    int w = (int)(((float)(pj - 1) + 0.5f) * (float)W / (float)P - 0.5f) - 2;
+    if (w < 0) w = 0;
+    for (; w < W; ++w) {
+      int i0, i1;
+      float l0, l1;
+      bilin_axis(w, P, W, i0, i1, l0, l1);
+      if (i0 > pj) break;
+      const float wt = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
+      if (wt == 0.f) continue;
+      float v[8];
+      load8<T>(row + (size_t)w * C + c0, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += wt * v[q];
+    }
+    float* out = rows + (((size_t)b * H + h) * P + pj) * C + c0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) out[q] = acc[q];
+  }
+}
+
+// grid (N, B): du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du
+__global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
+                                                              const float* __restrict__ o, const float* gamma,
+                                                              float* __restrict__ dO, float* __restrict__ gpart) {
+  __shared__ float red[8];
+  const int n = blockIdx.x, b = blockIdx.y, N = P * P;
+  const int pi = n / P, pj = n - pi * P;
+  const float gm = *gamma;
+  int hlo = (int)(((float)(pi - 1) + 0.5f) * (float)H / (float)P - 0.5f) - 2;
+  if (hlo < 0) hlo = 0;
+  float gsum = 0.f;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int h = hlo; h < H; ++h) {
+      int i0, i1;
+      float l0, l1;
+      bilin_axis(h, P, H, i0, i1, l0, l1);
+      if (i0 > pi) break;
+      const float wt = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
+      if (wt != 0.f) s += wt * rows[(((size_t)b * H + h) * P + pj) * C + c];
+    }
+    const size_t idx = ((size_t)b * N + n) * C + c;
+    gsum += o[idx] * s;
+    dO[idx] = gm * s;
+  }
+  gsum = block_reduce_sum(gsum, red);
+  if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
+}
+
+// grid (N, B): query row n -> dE[b][n][:], dq[b][n][:]
+__global__ void __launch_bounds__(256) lsa_attn_bwd_rows_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
+                                                                const float* __restrict__ A,
+                                                                const float* __restrict__ dO, float* __restrict__ dE,
+                                                                float* __restrict__ dqkv) {
+  extern __shared__ float sm[];  // dO row [C] | dA [N] | red [8]
+  float* dor = sm;
+  float* da = sm + C;
+  float* red = da + N;
+  const int n = blockIdx.x, b = blockIdx.y, J = 2 * Cq + C;
+  const float* base = qkv + (size_t)b * N * J;
+  const float* arow = A + ((size_t)b * N + n) * N;
+  for (int c = threadIdx.x; c < C; c += 256) dor[c] = dO[((size_t)b * N + n) * C + c];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int m = wave; m < N; m += 4) {
+    const float* v = base + (size_t)m * J + 2 * Cq;
+    float s = 0.f;
+    for (int c = lane; c < C; c += 64) s += dor[c] * v[c];
+    s = wave_sum(s);
+    if (lane == 0) da[m] = s;
+  }
+  __syncthreads();
+  float dot = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) dot += arow[m] * da[m];
+  dot = block_reduce_sum(dot, red);
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float g = arow[m] * (da[m] - dot);
+    da[m] = g;
+    dE[((size_t)b * N + n) * N + m] = g;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < Cq; c += 256) {
+    float s = 0.f;
+    for (int m = 0; m < N; ++m) s += da[m] * base[(size_t)m * J + Cq + c];
+    dqkv[((size_t)b * N + n) * J + c] = s;
+  }
+}
+
+// grid (N, B): key/value row m -> dk[b][m][:], dv[b][m][:]
+__global__ void __launch_bounds__(256) lsa_attn_bwd_cols_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
+                                                                const float* __restrict__ A,
+                                                                const float* __restrict__ dO,
+                                                                const float* __restrict__ dE, float* __restrict__ dqkv) {
+  extern __shared__ float sm[];  // dE col [N] | A col [N]
+  float* de = sm;
+  float* ac = sm + N;
+  const int m = blockIdx.x, b = blockIdx.y, J = 2 * Cq + C;
+  for (int n = threadIdx.x; n < N; n += 256) {
+    de[n] = dE[((size_t)b * N + n) * N + m];
+    ac[n] = A[((size_t)b * N + n) * N + m];
+  }
+  __syncthreads();
+  const float* base = qkv + (size_t)b * N * J;
+  float* out = dqkv + ((size_t)b * N + m) * J;
+  for (int c = threadIdx.x; c < Cq; c += 256) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += de[n] * base[(size_t)n * J + c];
+    out[Cq + c] = s;
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int n = 0; n < N; ++n) s += ac[n] * dO[((size_t)b * N + n) * C + c];
+    out[2 * Cq + c] = s;
+  }
+}
+
+// dW[j][c] += sum_bn dqkv[bn][j] * pooled[bn][c]; grid (ceil(C/256), J)
+__global__ void __launch_bounds__(256) lsa_proj_dw_kernel(int BN, int C, int Cq, const float* __restrict__ dqkv,
+                                                          const float* __restrict__ pooled, float* dWq, float* dWk,
+                                                          float* dWv) {
+  const int J = 2 * Cq + C;
+  const int j = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= C) return;
+  float s = 0.f;
+  for (int r = 0; r < BN; ++r) s += dqkv[(size_t)r * J + j] * pooled[(size_t)r * C + c];
+  if (j < Cq) dWq[(size_t)j * C + c] += s;
+  else if (j < 2 * Cq) dWk[(size_t)(j - Cq) * C + c] += s;
+  else dWv[(size_t)(j - 2 * Cq) * C + c] += s;
+}
+
+__global__ void __launch_bounds__(256) lsa_proj_db_kernel(int BN, int C, int Cq, const float* __restrict__ dqkv,
+                                                          float* dbq, float* dbk, float* dbv) {
+  const int J = 2 * Cq + C;
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  if (j >= J) return;
+  float s = 0.f;
+  for (int r = 0; r < BN; ++r) s += dqkv[(size_t)r * J + j];
+  if (j < Cq) dbq[j] += s;
+  else if (j < 2 * Cq) dbk[j - Cq] += s;
+  else dbv[j - 2 * Cq] += s;
+}
+
+// dpooled[bn][c] = sum_j dqkv[bn][j] * w[j][c]; grid (ceil(C/256), BN)
+__global__ void __launch_bounds__(256) lsa_proj_dx_kernel(int C, int Cq, const float* __restrict__ dqkv,
+                                                          const float* __restrict__ w, float* __restrict__ dpooled) {
+  extern __shared__ float drow[];
+  const int J = 2 * Cq + C;
+  const int r = blockIdx.y, c = blockIdx.x * 256 + threadIdx.x;
+  for (int j = threadIdx.x; j < J; j += 256) drow[j] = dqkv[(size_t)r * J + j];
+  __syncthreads();
+  if (c >= C) return;
+  float s = 0.f;
+  for (int j = 0; j < J; ++j) s += drow[j] * w[(size_t)j * C + c];
+  dpooled[(size_t)r * C + c] = s;
+}
+
+}  // namespace
+
+extern "C" int dfcsa_lsa_pool_splits(int H, int P) { return pool_splits(H, P); }
+
+extern "C" int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                              const float* sh2, int P, int relu, float* partial, void* stream) {
+  if (C % 8 || C > 2048 || P <= 0) return DFCSA_EINVAL;
+  const int S = pool_splits(H, P);
+  dim3 grid(S, P * P, B);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(lsa_pool_kernel<bf16_t>, grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2, sh2, P, S,
+                       relu, partial);
+  else
+    hipLaunchKernelGGL(lsa_pool_kernel<float>, grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2, P, S,
+                       relu, partial);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,
+                             const float* bias, float* pooled, float* qkv, void* stream) {
+  const int N = P * P, J = 2 * Cq + C;
+  size_t shm = (size_t)16 * C * sizeof(float);
+  if (shm > 64 * 1024) return DFCSA_EINVAL;
+  dim3 grid((J + 255) / 256, (N + 15) / 16, B);
+  hipLaunchKernelGGL(lsa_qkv_kernel, grid, dim3(256), shm, (hipStream_t)stream, H, W, C, Cq, P, pool_splits(H, P),
+                     partial, wT, bias, pooled, qkv);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream) {
+  size_t shm = (size_t)(Cq + N + 8) * sizeof(float);
+  hipLaunchKernelGGL(lsa_attn_kernel, dim3(N, B), dim3(256), shm, (hipStream_t)stream, N, C, Cq, qkv, A, o);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, const void* dattn, int P, float* rows,
+                                     void* stream) {
+  if (C % 8) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(lsa_up_bwd_rows_kernel<bf16_t>, dim3(H, B), dim3(256), 0, st, H, W, C, (const bf16_t*)dattn,
+                       P, rows);
+  else
+    hipLaunchKernelGGL(lsa_up_bwd_rows_kernel<float>, dim3(H, B), dim3(256), 0, st, H, W, C, (const float*)dattn, P,
+                       rows);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const float* o,
+                                     const float* gamma, float* dO, float* gpart, int* ngpart, void* stream) {
+  hipLaunchKernelGGL(lsa_up_bwd_cols_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, P, rows, o,
+                     gamma, dO, gpart);
+  DFCSA_CHECK_LAUNCH();
+  if (ngpart) *ngpart = B * P * P;
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv, const float* A, const float* dO,
+                                  float* dE, float* dqkv, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  size_t shm1 = (size_t)(C + N + 8) * sizeof(float);
+  hipLaunchKernelGGL(lsa_attn_bwd_rows_kernel, dim3(N, B), dim3(256), shm1, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  DFCSA_CHECK_LAUNCH();
+  size_t shm2 = (size_t)(2 * N) * sizeof(float);
+  hipLaunchKernelGGL(lsa_attn_bwd_cols_kernel, dim3(N, B), dim3(256), shm2, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_proj_bwd(int B, int N, int C, int Cq, const float* dqkv, const float* pooled,
+                                  const float* w, float* dWq, float* dWk, float* dWv, float* dbq, float* dbk,
+                                  float* dbv, float* dpooled, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int J = 2 * Cq + C, BN = B * N;
+  hipLaunchKernelGGL(lsa_proj_dw_kernel, dim3((C + 255) / 256, J), dim3(256), 0, st, BN, C, Cq, dqkv, pooled, dWq,
+                     dWk, dWv);
+  DFCSA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lsa_proj_db_kernel, dim3((J + 255) / 256), dim3(256), 0, st, BN, C, Cq, dqkv, dbq, dbk, dbv);
+  DFCSA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(lsa_proj_dx_kernel, dim3((C + 255) / 256, BN), dim3(256), (size_t)J * sizeof(float), st, C, Cq,
+                     dqkv, w, dpooled);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,570 @@
+// U-Net plumbing, weight packing and the loss/metric reduction.
+//
+// Reference call sites replaced (models/unet_dfc_sa_res.py unless noted):
+//   nn.MaxPool2d(2, 2)                       :132-141 (+ its backward)
+//   F.interpolate(bilinear) shape fix        :180-199 (only when a decoder size mismatches)
+//   final_conv 1x1 head                      :159, :203
+//   torch.sigmoid                            utils/trainer.py:124
+//   BCELoss + dice_loss + IoU/Dice counts    utils/metrics.py:6-24, 52-78, 228-236
+#include <algorithm>
+
+#include "common.h"
+#include "dfcsa_internal.h"
+
+namespace {
+
+inline int grid_for(int64_t n, int per = 256, int cap = 4096) {
+  int64_t b = (n + per - 1) / per;
+  return (int)std::max<int64_t>(1, std::min<int64_t>(b, cap));
+}
+
+// ---------------------------------------------------------------- max pooling 2x2 / 2
+template <typename T>
+__global__ void maxpool2_fwd_kernel(int B, int H, int W, int C, const T* __restrict__ x, T* __restrict__ y) {
+  const int Ho = H / 2, Wo = W / 2, cpp = C >> 3;
+  const int64_t total = (int64_t)B * Ho * Wo * cpp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ck = (int)(e % cpp);
+    int64_t p = e / cpp;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    float best[8], v[8];
+    const T* base = x + ((size_t)(b * H + 2 * oh) * W + 2 * ow) * C + ck * 8;
+    load8<T>(base, best);
+#pragma unroll
+    for (int t = 1; t < 4; ++t) {
+      load8<T>(base + ((size_t)(t >> 1) * W + (t & 1)) * C, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (v[q] > best[q] || isnan(v[q])) best[q] = v[q];
+    }
+    store8<T>(y + ((size_t)(b * Ho + oh) * Wo + ow) * C + ck * 8, best);
+  }
+}
+
+// dx += dout at the first maximum (scan order (0,0),(0,1),(1,0),(1,1); NaN wins), as ATen
+template <typename T>
+__global__ void maxpool2_bwd_kernel(int B, int H, int W, int C, const T* __restrict__ x, const T* __restrict__ dy,
+                                    T* __restrict__ dx) {
+  const int Ho = H / 2, Wo = W / 2, cpp = C >> 3;
+  const int64_t total = (int64_t)B * Ho * Wo * cpp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ck = (int)(e % cpp);
+    int64_t p = e / cpp;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    float best[8], v[8], g[8];
+    int arg[8];
+    const size_t base = ((size_t)(b * H + 2 * oh) * W + 2 * ow) * C + ck * 8;
+    load8<T>(x + base, best);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) arg[q] = 0;
+#pragma unroll
+    for (int t = 1; t < 4; ++t) {
+      load8<T>(x + base + ((size_t)(t >> 1) * W + (t & 1)) * C, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        if (v[q] > best[q] || isnan(v[q])) { best[q] = v[q]; arg[q] = t; }
+    }
+    load8<T>(dy + ((size_t)(b * Ho + oh) * Wo + ow) * C + ck * 8, g);
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      T* dst = dx + base + ((size_t)(t >> 1) * W + (t & 1)) * C;
+      float o[8];
+      load8<T>(dst, o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] += (arg[q] == t) ? g[q] : 0.f;
+      store8<T>(dst, o);
+    }
+  }
+}
+
+// ---------------------------------------------------------------- layout conversion
+template <typename T>
+__global__ void pack_input_kernel(int B, int Cin, int H, int W, const float* __restrict__ x, int Cpad,
+                                  T* __restrict__ out) {
+  const int64_t total = (int64_t)B * H * W;
+  for (int64_t p = (int64_t)blockIdx.x * 256 + threadIdx.x; p < total; p += (int64_t)gridDim.x * 256) {
+    const int hw = (int)(p % ((int64_t)H * W));
+    const int b = (int)(p / ((int64_t)H * W));
+    for (int c0 = 0; c0 < Cpad; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        int c = c0 + q;
+        v[q] = c < Cin ? x[((size_t)b * Cin + c) * H * W + hw] : 0.f;
+      }
+      store8<T>(out + (size_t)p * Cpad + c0, v);
+    }
+  }
+}
+
+__device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  float scale = (float)in / (float)out;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
+template <typename T>
+__global__ void resize_kernel(int B, int C, int Hi, int Wi, int Ho, int Wo, const T* __restrict__ x,
+                              T* __restrict__ y) {
+  const int cpp = C >> 3;
+  const int64_t total = (int64_t)B * Ho * Wo * cpp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ck = (int)(e % cpp);
+    int64_t p = e / cpp;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    bilin_axis(oh, Hi, Ho, h0, h1, lh0, lh1);
+    bilin_axis(ow, Wi, Wo, w0, w1, lw0, lw1);
+    const T* xb = x + (size_t)b * Hi * Wi * C + ck * 8;
+    float a[8], bq[8], c[8], d[8], o[8];
+    load8<T>(xb + ((size_t)h0 * Wi + w0) * C, a);
+    load8<T>(xb + ((size_t)h0 * Wi + w1) * C, bq);
+    load8<T>(xb + ((size_t)h1 * Wi + w0) * C, c);
+    load8<T>(xb + ((size_t)h1 * Wi + w1) * C, d);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) o[q] = lh0 * (lw0 * a[q] + lw1 * bq[q]) + lh1 * (lw0 * c[q] + lw1 * d[q]);
+    store8<T>(y + (size_t)e * 8, o);
+  }
+}
+
+template <typename T>
+__global__ void resize_bwd_kernel(int B, int C, int Hi, int Wi, int Ho, int Wo, const T* __restrict__ dy,
+                                  float* __restrict__ dx) {
+  const int cpp = C >> 3;
+  const int64_t total = (int64_t)B * Ho * Wo * cpp;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ck = (int)(e % cpp);
+    int64_t p = e / cpp;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    bilin_axis(oh, Hi, Ho, h0, h1, lh0, lh1);
+    bilin_axis(ow, Wi, Wo, w0, w1, lw0, lw1);
+    float g[8];
+    load8<T>(dy + (size_t)e * 8, g);
+    float* xb = dx + (size_t)b * Hi * Wi * C + ck * 8;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      atomicAdd(xb + ((size_t)h0 * Wi + w0) * C + q, lh0 * lw0 * g[q]);
+      atomicAdd(xb + ((size_t)h0 * Wi + w1) * C + q, lh0 * lw1 * g[q]);
+      atomicAdd(xb + ((size_t)h1 * Wi + w0) * C + q, lh1 * lw0 * g[q]);
+      atomicAdd(xb + ((size_t)h1 * Wi + w1) * C + q, lh1 * lw1 * g[q]);
+    }
+  }
+}
+
+template <typename T>
+__global__ void cast_f32_kernel(int64_t n, const float* __restrict__ x, T* __restrict__ out, int accumulate) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    float v = x[i];
+    if (accumulate) v += ElemTraits<T>::to_f(out[i]);
+    out[i] = ElemTraits<T>::from_f(v);
+  }
+}
+
+// ---------------------------------------------------------------- 1x1 head (N = Cout small)
+template <typename T>
+__global__ void head_fwd_kernel(int B, int HW, int C, int Cout, const T* __restrict__ x, const float* __restrict__ w,
+                                const float* __restrict__ bias, float* __restrict__ out) {
+  const int64_t M = (int64_t)B * HW;
+  for (int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x; m < M; m += (int64_t)gridDim.x * 256) {
+    const int b = (int)(m / HW), hw = (int)(m % HW);
+    for (int o = 0; o < Cout; ++o) {
+      float s = bias ? bias[o] : 0.f;
+      for (int c0 = 0; c0 < C; c0 += 8) {
+        float v[8];
+        load8<T>(x + (size_t)m * C + c0, v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) s += v[q] * w[(size_t)o * C + c0 + q];
+      }
+      out[((size_t)b * Cout + o) * HW + hw] = s;
+    }
+  }
+}
+
+// dx = dlogit @ w ; per-tile partial sums for dw and db (tile = 256 pixels)
+template <typename T>
+__global__ void __launch_bounds__(256) head_bwd_kernel(int B, int HW, int C, int Cout, const T* __restrict__ x,
+                                                       const float* __restrict__ w, const float* __restrict__ dl,
+                                                       T* __restrict__ dx, float* __restrict__ pw,
+                                                       float* __restrict__ pb) {
+  extern __shared__ float sred[];  // [256][Cout]
+  const int64_t M = (int64_t)B * HW;
+  const int64_t m = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  float g[8];
+  for (int o = 0; o < Cout && o < 8; ++o) g[o] = 0.f;
+  if (m < M) {
+    const int b = (int)(m / HW), hw = (int)(m % HW);
+    for (int o = 0; o < Cout; ++o) g[o] = dl[((size_t)b * Cout + o) * HW + hw];
+    for (int c0 = 0; c0 < C; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float s = 0.f;
+        for (int o = 0; o < Cout; ++o) s += g[o] * w[(size_t)o * C + c0 + q];
+        v[q] = s;
+      }
+      store8<T>(dx + (size_t)m * C + c0, v);
+    }
+  }
+  for (int o = 0; o < Cout; ++o) sred[threadIdx.x * Cout + o] = g[o];
+  __syncthreads();
+  // dw[o][c] partial over this tile's pixels: thread t handles (o, c) pairs
+  const int64_t m0 = (int64_t)blockIdx.x * 256;
+  const int np = (int)std::min<int64_t>(256, M - m0);
+  for (int e = threadIdx.x; e < Cout * C; e += 256) {
+    const int o = e / C, c = e % C;
+    float s = 0.f;
+    for (int p = 0; p < np; ++p) s += sred[p * Cout + o] * ElemTraits<T>::to_f(x[(size_t)(m0 + p) * C + c]);
+    pw[(size_t)blockIdx.x * Cout * C + e] = s;
+  }
+  for (int o = threadIdx.x; o < Cout; o += 256) {
+    float s = 0.f;
+    for (int p = 0; p < np; ++p) s += sred[p * Cout + o];
+    pb[(size_t)blockIdx.x * Cout + o] = s;
+  }
+}
+
+// ---------------------------------------------------------------- weight packing
+template <typename T>
+__global__ void pack_conv_w_kernel(const float* __restrict__ w, int Cout, int Cin, int ntaps, int Cpad, int Kpad,
+                                   int row0, T* __restrict__ out) {
+  const int64_t total = (int64_t)Cout * Kpad;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int co = (int)(e / Kpad), k = (int)(e % Kpad);
+    const int tap = k / Cpad, ci = k - tap * Cpad;
+    float v = 0.f;
+    if (tap < ntaps && ci < Cin) v = w[((size_t)co * Cin + ci) * ntaps + tap];
+    out[(size_t)(row0 + co) * Kpad + k] = ElemTraits<T>::from_f(v);
+  }
+}
+
+template <typename T>
+__global__ void pack_conv_w_t_kernel(const float* __restrict__ w, int Cout, int Cin, int ntaps, int Kpad, int col0,
+                                     T* __restrict__ out) {
+  const int64_t total = (int64_t)Cin * ntaps * Cout;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int co = (int)(e % Cout);
+    int64_t r = e / Cout;
+    const int tap = (int)(r % ntaps);
+    const int ci = (int)(r / ntaps);
+    out[(size_t)ci * Kpad + col0 + tap * Cout + co] = ElemTraits<T>::from_f(w[((size_t)co * Cin + ci) * ntaps + tap]);
+  }
+}
+
+template <typename T>
+__global__ void pack_convT_kernel(const float* __restrict__ w, const float* __restrict__ bias, int Cin, int Cout,
+                                  T* __restrict__ fwd, T* __restrict__ bwd, float* __restrict__ bias4) {
+  const int64_t total = (int64_t)Cin * Cout * 4;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ij = (int)(e & 3);
+    const int64_t r = e >> 2;
+    const int co = (int)(r % Cout), ci = (int)(r / Cout);
+    const T v = ElemTraits<T>::from_f(w[e]);
+    fwd[((size_t)ij * Cout + co) * Cin + ci] = v;
+    bwd[(size_t)ci * 4 * Cout + ij * Cout + co] = v;
+    if (ci == 0) bias4[ij * Cout + co] = bias[co];
+  }
+}
+
+// ---------------------------------------------------------------- sigmoid / loss
+__global__ void sigmoid_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ y) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+    y[i] = 1.f / (1.f + expf(-x[i]));
+}
+__global__ void sigmoid_bwd_kernel(int64_t n, const float* __restrict__ y, const float* __restrict__ dy,
+                                   float* __restrict__ dx) {
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float v = y[i];
+    dx[i] = dy[i] * (1.f - v) * v;
+  }
+}
+
+constexpr int kLossBlocks = 512;
+
+// partial[blk][6] = {sum bce, sum p*t, sum p, sum t, sum b*t, sum b}
+__global__ void __launch_bounds__(256) bce_dice_partial_kernel(int64_t n, const float* __restrict__ p,
+                                                               const float* __restrict__ t,
+                                                               float* __restrict__ partial) {
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float pv = p[i], tv = t[i];
+    const float lp = fmaxf(logf(pv), -100.f), l1p = fmaxf(log1pf(-pv), -100.f);
+    const float bce = -(tv * lp + (1.f - tv) * l1p);
+    const float b = pv > 0.5f ? 1.f : 0.f;
+    acc[0] += bce; acc[1] += pv * tv; acc[2] += pv; acc[3] += tv; acc[4] += b * tv; acc[5] += b;
+  }
+  __shared__ double red[6][256];
+  for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (threadIdx.x < o)
+      for (int k = 0; k < 6; ++k) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 6) partial[blockIdx.x * 6 + threadIdx.x] = (float)red[threadIdx.x][0];
+}
+
+__global__ void bce_dice_final_kernel(int64_t n, int nparts, const float* __restrict__ partial, float wbce,
+                                      float wdice, float* __restrict__ stats) {
+  __shared__ double red[6][64];
+  double acc[6] = {0, 0, 0, 0, 0, 0};
+  for (int i = threadIdx.x; i < nparts; i += 64)
+    for (int k = 0; k < 6; ++k) acc[k] += partial[i * 6 + k];
+  for (int k = 0; k < 6; ++k) red[k][threadIdx.x] = acc[k];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double s[6] = {0, 0, 0, 0, 0, 0};
+    for (int i = 0; i < 64; ++i)
+      for (int k = 0; k < 6; ++k) s[k] += red[k][i];
+    const float bce = (float)(s[0] / (double)n);
+    const float inter = (float)s[1], ps = (float)s[2], ts = (float)s[3];
+    const float dice = (2.f * inter + 1.f) / (ps + ts + 1.f);
+    const float loss = wbce * bce + wdice * (1.f - dice);
+    stats[0] = loss;
+    stats[1] = (float)s[0];
+    for (int k = 1; k < 6; ++k) stats[1 + k] = (float)s[k];
+    stats[7] = isfinite(loss) ? 1.f : 0.f;
+  }
+}
+
+// dp = dloss * (wbce * (p - t) / max((1 - p) p, 1e-12) / n + wdice * d(1 - dice)/dp)
+__global__ void bce_dice_bwd_kernel(int64_t n, const float* __restrict__ p, const float* __restrict__ t,
+                                    const float* __restrict__ stats, float wbce, float wdice,
+                                    const float* __restrict__ dloss, float* __restrict__ dp) {
+  const float g = dloss ? *dloss : 1.f;
+  const float inter = stats[2], den = stats[3] + stats[4] + 1.f;
+  const float num = 2.f * inter + 1.f;
+  for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+    const float pv = p[i], tv = t[i];
+    const float gb = (pv - tv) / fmaxf((1.f - pv) * pv, 1e-12f) / (float)n;
+    // dice = num/den; d(1-dice)/dp = -(2 t den - num) / den^2
+    const float gd = -(2.f * tv * den - num) / (den * den);
+    dp[i] = g * (wbce * gb + wdice * gd);
+  }
+}
+
+}  // namespace
+
+extern "C" int dfcsa_maxpool2_fwd(int dtype, int B, int H, int W, int C, const void* x, void* out, void* stream) {
+  if (C % 8) return DFCSA_EINVAL;
+  int64_t n = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       (const bf16_t*)x, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(maxpool2_fwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C, (const float*)x,
+                       (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_maxpool2_bwd(int dtype, int B, int H, int W, int C, const void* x, const void* dout, void* dx,
+                                  void* stream) {
+  if (C % 8) return DFCSA_EINVAL;
+  int64_t n = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C,
+                       (const bf16_t*)x, (const bf16_t*)dout, (bf16_t*)dx);
+  else
+    hipLaunchKernelGGL(maxpool2_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, H, W, C, (const float*)x,
+                       (const float*)dout, (float*)dx);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_input(int dtype, int B, int Cin, int H, int W, const float* x, int Cpad, void* out,
+                                void* stream) {
+  if (Cpad % 8 || Cpad < Cin) return DFCSA_EINVAL;
+  int64_t n = (int64_t)B * H * W;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(pack_input_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, Cin, H, W, x, Cpad,
+                       (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_input_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, Cin, H, W, x, Cpad,
+                       (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_resize_bilinear(int dtype, int B, int C, int Hi, int Wi, int Ho, int Wo, const void* x,
+                                     void* out, void* stream) {
+  if (C % 8) return DFCSA_EINVAL;
+  int64_t n = (int64_t)B * Ho * Wo * (C / 8);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(resize_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, C, Hi, Wi, Ho, Wo,
+                       (const bf16_t*)x, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(resize_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, C, Hi, Wi, Ho, Wo,
+                       (const float*)x, (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_resize_bilinear_bwd(int dtype, int B, int C, int Hi, int Wi, int Ho, int Wo, const void* dout,
+                                         float* dx32, void* stream) {
+  if (C % 8) return DFCSA_EINVAL;
+  int64_t n = (int64_t)B * Ho * Wo * (C / 8);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(resize_bwd_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, B, C, Hi, Wi, Ho, Wo,
+                       (const bf16_t*)dout, dx32);
+  else
+    hipLaunchKernelGGL(resize_bwd_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, B, C, Hi, Wi, Ho, Wo,
+                       (const float*)dout, dx32);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_cast_f32(int dtype, int64_t n, const float* x, void* out, int accumulate, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(cast_f32_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, n, x, (bf16_t*)out, accumulate);
+  else
+    hipLaunchKernelGGL(cast_f32_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, n, x, (float*)out, accumulate);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_head_fwd(int dtype, int B, int HW, int C, int Cout, const void* x, const float* w,
+                              const float* b, float* logits, void* stream) {
+  if (C % 8 || Cout < 1 || Cout > 8) return DFCSA_EINVAL;
+  int64_t M = (int64_t)B * HW;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid_for(M)), dim3(256), 0, st, B, HW, C, Cout,
+                       (const bf16_t*)x, w, b, logits);
+  else
+    hipLaunchKernelGGL(head_fwd_kernel<float>, dim3(grid_for(M)), dim3(256), 0, st, B, HW, C, Cout, (const float*)x,
+                       w, b, logits);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_head_bwd(int dtype, int B, int HW, int C, int Cout, const void* x, const float* w,
+                              const float* dlogit, void* dx, float* partial_w, float* partial_b, int* ntiles,
+                              void* stream) {
+  if (C % 8 || Cout < 1 || Cout > 8) return DFCSA_EINVAL;
+  int64_t M = (int64_t)B * HW;
+  int blocks = (int)((M + 255) / 256);
+  if (ntiles) *ntiles = blocks;
+  if (!partial_w) return 0;  // size query
+  hipStream_t st = (hipStream_t)stream;
+  size_t shm = (size_t)256 * Cout * sizeof(float);
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, B, HW, C, Cout, (const bf16_t*)x,
+                       w, dlogit, (bf16_t*)dx, partial_w, partial_b);
+  else
+    hipLaunchKernelGGL(head_bwd_kernel<float>, dim3(blocks), dim3(256), shm, st, B, HW, C, Cout, (const float*)x, w,
+                       dlogit, (float*)dx, partial_w, partial_b);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_conv_w(int dtype, const float* w, int Cout, int Cin, int ntaps, int Cpad, int Kpad,
+                                 int row0, void* out, void* stream) {
+  if (Cpad < Cin || Kpad < ntaps * Cpad) return DFCSA_EINVAL;
+  int64_t n = (int64_t)Cout * Kpad;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(pack_conv_w_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, w, Cout, Cin, ntaps, Cpad,
+                       Kpad, row0, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_conv_w_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, Cout, Cin, ntaps, Cpad,
+                       Kpad, row0, (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_conv_w_t(int dtype, const float* w, int Cout, int Cin, int ntaps, int Kpad, int col0,
+                                   void* out, void* stream) {
+  if (col0 + ntaps * Cout > Kpad) return DFCSA_EINVAL;
+  int64_t n = (int64_t)Cin * ntaps * Cout;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(pack_conv_w_t_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, w, Cout, Cin, ntaps, Kpad,
+                       col0, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_conv_w_t_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, Cout, Cin, ntaps, Kpad,
+                       col0, (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, int Cin, int Cout, void* out_fwd,
+                                  void* out_bwd, float* bias4, void* stream) {
+  int64_t n = (int64_t)Cin * Cout * 4;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(pack_convT_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, w, bias, Cin, Cout,
+                       (bf16_t*)out_fwd, (bf16_t*)out_bwd, bias4);
+  else
+    hipLaunchKernelGGL(pack_convT_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, bias, Cin, Cout,
+                       (float*)out_fwd, (float*)out_bwd, bias4);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_zero(void* p, int64_t bytes, void* stream) {
+  hipError_t e = hipMemsetAsync(p, 0, (size_t)bytes, (hipStream_t)stream);
+  return e == hipSuccess ? 0 : -(int)e;
+}
+
+extern "C" int dfcsa_sigmoid(int64_t n, const float* x, float* y, void* stream) {
+  hipLaunchKernelGGL(sigmoid_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, x, y);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_sigmoid_bwd(int64_t n, const float* y, const float* dy, float* dx, void* stream) {
+  hipLaunchKernelGGL(sigmoid_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, y, dy, dx);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_bce_dice_partial_count(int64_t n) {
+  return (int)std::max<int64_t>(1, std::min<int64_t>(kLossBlocks, (n + 255) / 256));
+}
+
+extern "C" int dfcsa_bce_dice_fwd(int64_t n, const float* p, const float* t, float* partial, float wbce, float wdice,
+                                  float* stats, void* stream) {
+  if (n <= 0) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  int nb = dfcsa_bce_dice_partial_count(n);
+  hipLaunchKernelGGL(bce_dice_partial_kernel, dim3(nb), dim3(256), 0, st, n, p, t, partial);
+  DFCSA_CHECK_LAUNCH();
+  hipLaunchKernelGGL(bce_dice_final_kernel, dim3(1), dim3(64), 0, st, n, nb, partial, wbce, wdice, stats);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_bce_dice_bwd(int64_t n, const float* p, const float* t, const float* stats, float wbce,
+                                  float wdice, const float* dloss, float* dp, void* stream) {
+  hipLaunchKernelGGL(bce_dice_bwd_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, n, p, t, stats, wbce,
+                     wdice, dloss, dp);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}

@@ -1,0 +1,309 @@
+// Convolution weight gradient on MFMA: a reduction over pixels.
+//
+//   slab[s][i][j] = sum_{m in chunk s} G[m][i] * X[m][j]
+//
+// G is an NHWC gradient tensor (possibly the channel-concat of up to three tensors), X is the
+// implicit im2col gather of the layer input (same segment/shift description as conv_gemm), so
+// the reduction axis m is the slow (row) axis of BOTH operands.  Tiles are staged in LDS as
+// [pixel][channel] images and the MFMA fragments (8 consecutive pixels per lane) are read with
+// the gfx950 hardware-transposing ds_read_b64_tr_b16 (bf16).  An XOR swizzle of the 16-column
+// blocks keeps those transposed reads bank-conflict-free.  The pixel axis is split into chunks
+// (split-K) with fp32 partial slabs reduced by dfcsa_wgrad_reduce in a fixed order
+// (deterministic, no float atomics), which also permutes into the reference weight layout.
+//
+// Replaces the weight half of ATen convolution_backward for the convolutions at reference
+// models/unet_dfc_sa_res.py:58, 66, 74, 81, 88 and ConvTranspose2d at :147-156.
+#include "common.h"
+#include "dfcsa_internal.h"
+
+namespace {
+
+typedef short bf16x8_t __attribute__((ext_vector_type(8)));
+typedef short v4s_t __attribute__((ext_vector_type(4)));
+typedef float f32x4_t __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) v4s_t lds_v4s;
+
+// physical 32-byte block of logical block `blk` in pixel row `r` (bf16 images)
+template <int BW>
+__device__ __forceinline__ int blk_swz(int r, int blk) {
+  if constexpr (BW == 128) return blk ^ ((r & 3) | (((r >> 3) & 1) << 2));
+  else return blk ^ (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
+}
+
+template <typename T, int BI>
+struct WgTile;
+
+// bf16: rows of BW channels = BW*2 bytes; chunk (8 channels) ch of row r
+template <int BW>
+__device__ __forceinline__ int chunk_off_bf16(int r, int ch) {
+  int blk = ch >> 1;
+  return r * (BW * 2) + ((blk_swz<BW>(r, blk) << 1) | (ch & 1)) * 16;
+}
+
+// transposed fragment read: 8 consecutive pixels (rows kb + 8*(lane>>4) ...) of column
+// col0 + (lane & 15)
+template <int BW>
+__device__ __forceinline__ bf16x8_t tr_frag(const char* img, int kb, int col0, int lane) {
+  const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+  const int blk = col0 >> 4;
+  int r0 = kb + 8 * g + q, r1 = r0 + 4;
+  const char* a0 = img + r0 * (BW * 2) + blk_swz<BW>(r0, blk) * 32 + 8 * p;
+  const char* a1 = img + r1 * (BW * 2) + blk_swz<BW>(r1, blk) * 32 + 8 * p;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+  bf16x8_t f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+// f32 fragment (parity mode): plain [pixel][BW] image, 8 scalar reads
+template <int BW>
+__device__ __forceinline__ void f32_frag(const char* img, int kb, int col0, int lane, float (&f)[8]) {
+  const float* t = (const float*)img;
+  const int col = col0 + (lane & 15), r = kb + 8 * (lane >> 4);
+#pragma unroll
+  for (int s = 0; s < 8; ++s) f[s] = t[(r + s) * BW + col];
+}
+
+template <typename T, int BI, int BJ>
+__global__ void __launch_bounds__(256) wgrad_kernel(const WgradArgs args) {
+  constexpr int EPC = ElemTraits<T>::kChunk;
+  constexpr int KMS = (sizeof(T) == 2) ? 64 : 32;    // pixels per stage
+  constexpr int NG = KMS / 32;
+  constexpr int CPR_G = BI * (int)sizeof(T) / 16;    // 16-B chunks per G row
+  constexpr int CPR_X = BJ * (int)sizeof(T) / 16;
+  constexpr int RPP_G = 256 / CPR_G, RPP_X = 256 / CPR_X;  // rows per pass
+  constexpr int NPG = KMS / RPP_G, NPX = KMS / RPP_X;       // passes per stage
+  constexpr int GB = KMS * BI * (int)sizeof(T), XB = KMS * BJ * (int)sizeof(T);
+  constexpr int WTM = BI / 2, WTN = BJ / 2;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+
+  __shared__ __attribute__((aligned(16))) char smem[2 * (GB + XB)];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI, split = blockIdx.z;
+  const int mbeg = split * args.mchunk;
+  const int mend = min(args.M, mbeg + args.mchunk);
+  if (mbeg >= mend) {
+    // still write zeros so the reduction can read every slab
+  }
+
+  // G loader: fixed channel chunk
+  const int gcc = tid % CPR_G, grow = tid / CPR_G;
+  const int gi = i0 + gcc * EPC;
+  const bool g_ok = gi < args.NI;
+  const T* gbase = nullptr;
+  int gC = args.Cg;
+  if (g_ok) {
+    int src = dm_div(args.dm_cg, gi);
+    gbase = (const T*)args.g_ptr[src] + (gi - src * args.Cg);
+  }
+  // X loader: fixed column chunk -> fixed segment
+  const int xcc = tid % CPR_X, xrow = tid / CPR_X;
+  const int xj = j0 + xcc * EPC;
+  const bool x_ok = xj < args.NJ;
+  ConvSeg xs = {nullptr, 0, 0};
+  int xch = 0;
+  if (x_ok) {
+    int seg = dm_div(args.dm_cseg, xj);
+    xch = xj - seg * args.Cseg;
+    xs = args.seg[seg];
+  }
+
+  uint4 rg[NPG], rx[NPX];
+  auto load_stage = [&](int kt) {
+    const int mb = mbeg + kt * KMS;
+#pragma unroll
+    for (int p = 0; p < NPG; ++p) {
+      int m = mb + grow + p * RPP_G;
+      if (g_ok && m < mend) rg[p] = *(const uint4*)(gbase + (size_t)m * gC);
+      else rg[p] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int p = 0; p < NPX; ++p) {
+      int m = mb + xrow + p * RPP_X;
+      uint4 v = make_uint4(0, 0, 0, 0);
+      if (x_ok && m < mend) {
+        int b = dm_div(args.dm_hw, m);
+        int rem = m - b * args.dm_hw.d;
+        int oh = dm_div(args.dm_w, rem);
+        int ow = rem - oh * args.dm_w.d;
+        int ih = oh * args.stride + xs.dh, iw = ow * args.stride + xs.dw;
+        if (ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi)
+          v = *(const uint4*)((const T*)xs.ptr + ((size_t)((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + xch));
+      }
+      rx[p] = v;
+    }
+  };
+  auto store_stage = [&](int s) {
+    char* G = smem + s * (GB + XB);
+    char* X = G + GB;
+#pragma unroll
+    for (int p = 0; p < NPG; ++p) {
+      int r = grow + p * RPP_G;
+      int off = (sizeof(T) == 2) ? chunk_off_bf16<BI>(r, gcc) : (r * BI * 4 + gcc * 16);
+      *(uint4*)(G + off) = rg[p];
+    }
+#pragma unroll
+    for (int p = 0; p < NPX; ++p) {
+      int r = xrow + p * RPP_X;
+      int off = (sizeof(T) == 2) ? chunk_off_bf16<BJ>(r, xcc) : (r * BJ * 4 + xcc * 16);
+      *(uint4*)(X + off) = rx[p];
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend > mbeg) ? (mend - mbeg + KMS - 1) / KMS : 0;
+  if (nk > 0) {
+    load_stage(0);
+    store_stage(0);
+  }
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const bool more = kt + 1 < nk;
+    if (more) load_stage(kt + 1);
+    const char* G = smem + (kt & 1) * (GB + XB);
+    const char* X = G + GB;
+#pragma unroll
+    for (int g = 0; g < NG; ++g) {
+      if constexpr (sizeof(T) == 2) {
+        bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) fa[i] = tr_frag<BI>(G, 32 * g, wm * WTM + i * 16, lane);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) fb[j] = tr_frag<BJ>(X, 32 * g, wn * WTN + j * 16, lane);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      } else {
+        float fa[FM][8], fb[FN][8];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) f32_frag<BI>(G, 32 * g, wm * WTM + i * 16, lane, fa[i]);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) f32_frag<BJ>(X, 32 * g, wn * WTN + j * 16, lane, fb[j]);
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+#pragma unroll
+            for (int s = 0; s < 8; ++s)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+      }
+    }
+    if (more) store_stage((kt + 1) & 1);
+    __syncthreads();
+  }
+
+  float* out = args.slab + (size_t)split * args.NI * args.NJ;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      int col = j0 + wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = i0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        if (row < args.NI && col < args.NJ) out[(size_t)row * args.NJ + col] = acc[i][j][r];
+      }
+    }
+}
+
+__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI, int NJ,
+                                    int layout, int ntaps, int Ctot, int Creal, int ndst,
+                                    float* d0, float* d1, float* d2) {
+  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  int64_t total = (int64_t)NI * NJ;
+  if (e >= total) return;
+  float s = 0.f;
+  for (int k = 0; k < splits; ++k) s += slab[(int64_t)k * total + e];
+  int i = (int)(e / NJ), j = (int)(e % NJ);
+  if (layout == 0) {
+    int rows = NI / ndst;
+    int d = i / rows, r = i - d * rows;
+    int tap = j / Ctot, cin = j - tap * Ctot;
+    if (cin >= Creal) return;
+    float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
+    dst[((int64_t)r * Creal + cin) * ntaps + tap] += s;
+  } else {
+    // ConvTranspose2d weight [Cin][Cout][2][2]; i = ci, j = ij*Cout + co (Ctot = Cout)
+    int ij = j / Ctot, co = j - ij * Ctot;
+    d0[((int64_t)i * Ctot + co) * 4 + ij] += s;
+  }
+}
+
+template <typename T, int BI>
+int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
+  constexpr int BJ = 128;
+  dim3 grid((a.NJ + BJ - 1) / BJ, (a.NI + BI - 1) / BI, splits);
+  hipLaunchKernelGGL((wgrad_kernel<T, BI, BJ>), grid, dim3(256), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
+extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk) {
+  if (M <= 0 || NI <= 0 || NJ <= 0 || !splits || !mchunk) return DFCSA_EINVAL;
+  const int kms = dtype == DFCSA_DT_BF16 ? 64 : 32;
+  const int BI = NI <= 64 ? 64 : 128;
+  const int tiles = ((NI + BI - 1) / BI) * ((NJ + 127) / 128);
+  int s = 1024 / tiles;
+  if (s < 1) s = 1;
+  int max_s = M / (4 * kms);  // keep >= 4 stages per chunk
+  if (max_s < 1) max_s = 1;
+  if (s > max_s) s = max_s;
+  // cap the slab at 256 MiB
+  int64_t per = (int64_t)NI * NJ * 4;
+  int64_t cap = ((int64_t)256 << 20) / per;
+  if (cap < 1) cap = 1;
+  if (s > cap) s = (int)cap;
+  int mc = (M + s - 1) / s;
+  mc = (mc + kms - 1) / kms * kms;
+  s = (M + mc - 1) / mc;
+  *splits = s;
+  *mchunk = mc;
+  return 0;
+}
+
+extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
+  if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->ng < 1 || d->ng > 3) return DFCSA_EINVAL;
+  if (d->Cg % 8 || d->Cseg % 8 || d->mchunk <= 0 || d->splits <= 0) return DFCSA_EINVAL;
+  const int kms = d->dtype == DFCSA_DT_BF16 ? 64 : 32;
+  if (d->mchunk % kms) return DFCSA_EINVAL;
+  WgradArgs a;
+  a.M = d->M; a.ng = d->ng; a.Cg = d->Cg; a.NI = d->ng * d->Cg;
+  for (int i = 0; i < 3; ++i) a.g_ptr[i] = i < d->ng ? d->g_ptr[i] : nullptr;
+  a.nseg = d->nseg; a.Cseg = d->Cseg; a.NJ = d->nseg * d->Cseg;
+  for (int i = 0; i < d->nseg; ++i) { a.seg[i].ptr = d->seg_ptr[i]; a.seg[i].dh = d->seg_dh[i]; a.seg[i].dw = d->seg_dw[i]; }
+  a.Ho = d->Ho; a.Wo = d->Wo; a.Hi = d->Hi; a.Wi = d->Wi; a.stride = d->stride;
+  a.dm_hw = make_divmod(d->Ho * d->Wo); a.dm_w = make_divmod(d->Wo);
+  a.dm_cseg = make_divmod(d->Cseg); a.dm_cg = make_divmod(d->Cg);
+  a.slab = d->slab; a.mchunk = d->mchunk;
+  hipStream_t st = (hipStream_t)stream;
+  double flops = 2.0 * a.M * a.NI * a.NJ;
+  ProfScope prof(DFCSA_PROF_WGRAD, st, flops);
+  if (d->dtype == DFCSA_DT_BF16)
+    return a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st) : launch_wgrad<bf16_t, 128>(a, d->splits, st);
+  return a.NI <= 64 ? launch_wgrad<float, 64>(a, d->splits, st) : launch_wgrad<float, 128>(a, d->splits, st);
+}
+
+extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
+                                  int Ctot, int Creal, int ndst, float* const* dst, void* stream) {
+  if (!slab || !dst || ndst < 1 || ndst > 3 || NI % ndst) return DFCSA_EINVAL;
+  int64_t total = (int64_t)NI * NJ;
+  int blocks = (int)((total + 255) / 256);
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, splits,
+                     NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
+                     ndst > 2 ? dst[2] : nullptr);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}

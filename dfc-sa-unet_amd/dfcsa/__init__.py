@@ -1,0 +1,28 @@
+"""dfcsa: MI355X-native runtime for the DFC-SA-Res U-Net training step.
+
+Importing this package loads libdfcsa.so (HIP kernels for gfx950) and fails loudly if it is
+missing.  Public pieces:
+  dfcsa.block       DFC block forward/backward on the kernels
+  dfcsa.functions   U-Net plumbing (pooling, transposed conv, head, ...)
+  dfcsa.loss        sigmoid + BCE/Dice loss and metrics
+  dfcsa.flat        flat fp32 parameter / gradient storage
+  dfcsa.optim       fused clip_grad_norm_ + momentum SGD
+  dfcsa.ddp         data parallelism over RCCL (torch.distributed 'nccl' backend)
+"""
+from ._lib import version  # noqa: F401
+
+PRECISIONS = {"bf16": "bfloat16", "bfloat16": "bfloat16", "fp32": "float32", "float32": "float32"}
+
+
+def resolve_dtype(precision):
+    import torch
+    if precision is None:
+        return torch.bfloat16
+    if isinstance(precision, torch.dtype):
+        if precision not in (torch.bfloat16, torch.float32):
+            raise ValueError(f"unsupported compute dtype {precision}")
+        return precision
+    key = str(precision).lower()
+    if key not in PRECISIONS:
+        raise ValueError(f"unsupported precision {precision!r} (use 'bf16' or 'fp32')")
+    return getattr(torch, PRECISIONS[key])

@@ -1,0 +1,107 @@
+"""ctypes binding of libdfcsa.so (the C ABI declared in include/dfcsa.h).
+
+The argument types of every entry point are derived from the header itself, so the header is
+the single source of truth for the boundary.  Loading fails loudly (ImportError) when the
+library is missing: there is no fallback path.  torch must be imported first so that the HIP
+runtime torch ships (soname libamdhip64.so.7) is the one libdfcsa binds to.
+"""
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must precede the library load, see above)
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.environ.get("DFCSA_LIB", os.path.join(PKG_DIR, "libdfcsa.so"))
+HEADER_PATH = os.path.join(REPO_DIR, "include", "dfcsa.h")
+
+MAX_SEG = 32
+DT_F32 = 0
+DT_BF16 = 1
+EINVAL = -10000
+
+
+class DfcsaError(RuntimeError):
+    pass
+
+
+def parse_header(path=HEADER_PATH):
+    """Return {name: (restype, [argtypes])} for every `dfcsa_*` prototype in the header."""
+    text = open(path).read()
+    text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
+    protos = {}
+    for m in re.finditer(r"\b(int|const\s+char\s*\*)\s*(dfcsa_\w+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+        ret, name, args = m.group(1), m.group(2), m.group(3)
+        restype = ctypes.c_char_p if "char" in ret else ctypes.c_int
+        argtypes = []
+        args = args.strip()
+        if args and args != "void":
+            for a in args.split(","):
+                a = " ".join(a.split())
+                if "*" in a:
+                    argtypes.append(ctypes.c_void_p)
+                elif a.startswith("int64_t"):
+                    argtypes.append(ctypes.c_int64)
+                elif a.startswith("int"):
+                    argtypes.append(ctypes.c_int)
+                elif a.startswith("float"):
+                    argtypes.append(ctypes.c_float)
+                elif a.startswith("double"):
+                    argtypes.append(ctypes.c_double)
+                else:
+                    raise DfcsaError(f"unparsed argument {a!r} of {name}")
+        protos[name] = (restype, argtypes)
+    return protos
+
+
+class ConvDesc(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int), ("M", ctypes.c_int), ("N", ctypes.c_int), ("Kpad", ctypes.c_int),
+                ("Cseg", ctypes.c_int), ("nseg", ctypes.c_int),
+                ("seg_ptr", ctypes.c_void_p * MAX_SEG), ("seg_dh", ctypes.c_int * MAX_SEG),
+                ("seg_dw", ctypes.c_int * MAX_SEG),
+                ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("Hi", ctypes.c_int), ("Wi", ctypes.c_int),
+                ("stride", ctypes.c_int), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
+                ("mode", ctypes.c_int), ("ndest", ctypes.c_int), ("dest", ctypes.c_void_p * 3),
+                ("Nd", ctypes.c_int), ("accumulate", ctypes.c_int), ("stats", ctypes.c_void_p),
+                ("Hout", ctypes.c_int), ("Wout", ctypes.c_int)]
+
+
+class WgradDesc(ctypes.Structure):
+    _fields_ = [("dtype", ctypes.c_int), ("M", ctypes.c_int), ("ng", ctypes.c_int), ("Cg", ctypes.c_int),
+                ("g_ptr", ctypes.c_void_p * 3), ("nseg", ctypes.c_int), ("Cseg", ctypes.c_int),
+                ("seg_ptr", ctypes.c_void_p * MAX_SEG), ("seg_dh", ctypes.c_int * MAX_SEG),
+                ("seg_dw", ctypes.c_int * MAX_SEG),
+                ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("Hi", ctypes.c_int), ("Wi", ctypes.c_int),
+                ("stride", ctypes.c_int), ("slab", ctypes.c_void_p), ("splits", ctypes.c_int),
+                ("mchunk", ctypes.c_int)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"libdfcsa.so not found at {LIB_PATH}: build it with `python -c 'import __graft_entry__ as g; "
+            f"g.build()'` (or `make -C dfc-sa-unet_amd/csrc`). The DFC-SA-UNet MI355X path has no fallback.")
+    lib = ctypes.CDLL(LIB_PATH)
+    protos = parse_header()
+    for name, (res, args) in protos.items():
+        fn = getattr(lib, name)  # AttributeError = exported symbol missing: fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    return lib, protos
+
+
+LIB, PROTOS = _load()
+
+
+def call(name, *args):
+    """Invoke an entry point; raise DfcsaError on a non-zero status."""
+    rc = getattr(LIB, name)(*args)
+    if rc != 0:
+        what = "invalid argument/shape" if rc == EINVAL else f"HIP error {-rc}"
+        raise DfcsaError(f"{name} failed: {what}")
+    return rc
+
+
+def version():
+    return LIB.dfcsa_version().decode()

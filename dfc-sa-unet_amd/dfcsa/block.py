@@ -1,0 +1,347 @@
+"""DynamicFusionConvAttnBlock forward and backward on the libdfcsa kernels.
+
+Reference: models/unet_dfc_sa_res.py:41-116 (block) and :5-39 (LightSelfAttention).  The
+backward is written out by hand (no autograd inside): every tensor the reference's autograd
+graph would touch is produced by one of our kernels, parameter gradients are accumulated
+straight into ``param.grad`` (fp32), and the block input gradient is one implicit GEMM that
+fuses the 3x3 dgrad with both 1x1 dgrads (attention entry + residual).
+
+Activation flow per block (NHWC, dtype T; M = B*H*W pixels; C = out channels):
+  GEMM 3x3            x -> y1 (+bias, BN1 stats)
+  GEMM 1x1 (N = 2C)   x -> [y2 (+bias, BN2 stats) | res]        (one launch)
+  LSA                 pool(relu(bn2 y2)) -> q,k,v -> softmax -> o      (pooled P x P, fp32)
+  EW                  local = relu(bn1 y1); attn = gamma*up(o) + relu(bn2 y2)
+  GEMM 1x1            [local, attn] -> y3 (+bias, BN3 stats)   (no concat materialised)
+  EW                  fused = s*local + (1-s)*attn, s = sigmoid(bn3 y3)
+  GEMM 1x1            [fused, local, attn] -> y4 (+bias, BN4 stats)
+  EW                  out = relu(bn4 y4) + res_scale * res
+"""
+import torch
+import torch.nn as nn
+
+from . import ops
+from ._lib import call
+from .ops import P, dt, rup, stream
+
+
+def grad_of(p):
+    """fp32 gradient buffer of a parameter (created zeroed if absent)."""
+    if p.grad is None:
+        p.grad = torch.zeros_like(p)
+    return p.grad
+
+
+def _conv3x3_segments(xs):
+    return [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xs]
+
+
+class _Saved:
+    pass
+
+
+def block_forward(blk, xs, pool_size, training, dtype):
+    B, H, W, Cs = xs[0].shape
+    nsrc = len(xs)
+    Cin_p = nsrc * Cs
+    conv1, bn1m = blk.conv_branch[0], blk.conv_branch[1]
+    conv2, bn2m = blk.attn_branch[0], blk.attn_branch[1]
+    lsa = blk.attn_branch[3]
+    conv3, bn3m = blk.gate[0], blk.gate[1]
+    conv4, bn4m = blk.fusion_conv[0], blk.fusion_conv[1]
+    has_res = not isinstance(blk.residual_conv, nn.Identity)
+    C = conv1.out_channels
+    Cin_real = conv1.in_channels
+    if Cin_real > Cin_p:
+        raise ValueError(f"block expects {Cin_real} input channels, got {Cin_p}")
+    if not has_res and (nsrc != 1 or Cs != C):
+        raise ValueError("identity residual needs a single source with out_channels channels")
+    M = B * H * W
+    dev = xs[0].device
+    nt = ops.ntiles_gemm(M)
+    s = _Saved()
+
+    # ---- weights -> GEMM operands (fp32 master -> dtype) ----
+    Kp1 = rup(9 * Cin_p, ops.KALIGN)
+    W1p = ops.pack_conv_w(dtype, conv1.weight, Cin_p, Kp1)
+    N2 = 2 * C if has_res else C
+    Kp2 = rup(Cin_p, ops.KALIGN)
+    W2p = torch.empty((N2, Kp2), dtype=dtype, device=dev)
+    ops.pack_conv_w(dtype, conv2.weight, Cin_p, Kp2, out=W2p, row0=0)
+    if has_res:
+        ops.pack_conv_w(dtype, blk.residual_conv.weight, Cin_p, Kp2, out=W2p, row0=C)
+        b2 = torch.cat([conv2.bias.detach(), torch.zeros(C, device=dev)])
+    else:
+        b2 = conv2.bias
+    Kp3, Kp4 = rup(2 * C, ops.KALIGN), rup(3 * C, ops.KALIGN)
+    W3p = ops.pack_conv_w(dtype, conv3.weight, 2 * C, Kp3)
+    W4p = ops.pack_conv_w(dtype, conv4.weight, 3 * C, Kp4)
+
+    def stats(n):
+        return torch.empty(nt * 2 * n, device=dev, dtype=torch.float32) if training else None
+
+    # ---- local branch conv + attention entry / residual ----
+    y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    st1 = stats(C)
+    ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
+                  bias=conv1.bias, stats=st1)
+    y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
+    st2 = stats(N2)
+    ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
+                  [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
+    bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt, C, C, M, training)
+    bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt, C, N2, M, training)
+
+    # ---- LightSelfAttention on the pooled map ----
+    Pp = pool_size
+    Cq = lsa.query_conv.out_channels
+    J, N = 2 * Cq + C, Pp * Pp
+    pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype)
+
+    local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
+         P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
+
+    # ---- gate + fusion ----
+    y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    st3 = stats(C)
+    ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
+                  bias=conv3.bias, stats=st3)
+    bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt, C, C, M, training)
+    fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
+         stream())
+    y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    st4 = stats(C)
+    ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C, [y4],
+                  C, bias=conv4.bias, stats=st4)
+    bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt, C, C, M, training)
+    out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    call("dfcsa_block_out", dt(dtype), M, C, P(y4), P(bn4.scale), P(bn4.shift), P(res), P(blk.res_scale), P(out),
+         stream())
+
+    s.shape = (B, H, W, C, Cs, nsrc, Cin_p, Cin_real, has_res, Pp, Cq, J, N)
+    s.xs = xs
+    s.y1, s.y2, s.res, s.local, s.attn, s.y3, s.fused, s.y4 = y1, y2, res, local, attn, y3, fused, y4
+    s.bn = (bn1, bn2, bn3, bn4)
+    s.pooled, s.qkv, s.A, s.o, s.Wqkv = pooled, qkv, A, o, Wqkv
+    return out, s
+
+
+def block_backward(blk, s, dout, need_dx, dtype):
+    B, H, W, C, Cs, nsrc, Cin_p, Cin_real, has_res, Pp, Cq, J, N = s.shape
+    conv1, bn1m = blk.conv_branch[0], blk.conv_branch[1]
+    conv2, bn2m = blk.attn_branch[0], blk.attn_branch[1]
+    lsa = blk.attn_branch[3]
+    conv3, bn3m = blk.gate[0], blk.gate[1]
+    conv4, bn4m = blk.fusion_conv[0], blk.fusion_conv[1]
+    bn1, bn2, bn3, bn4 = s.bn
+    M = B * H * W
+    dev = dout.device
+    T = dt(dtype)
+    grid, hw = (B, H, W), (H, W)
+    nte = ops.ntiles_ew(M, C)
+    f32 = torch.float32
+    dout = dout.contiguous()
+
+    # ---- block output: relu(bn4 y4) + res_scale * res ----
+    dz4 = torch.empty_like(s.y4)
+    dres = torch.empty_like(s.y4)
+    part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
+    call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean), P(bn4.invstd),
+         P(s.res), P(blk.res_scale), P(dz4), P(dres), P(part), stream())
+    coef = ops.bn_bwd_finalize(part, nte, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
+                               extra=grad_of(blk.res_scale))
+    dy4 = ops.bn_bwd_apply(dtype, dz4, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
+    del dz4
+    # fusion conv: dW4 and d[fused, local, attn]
+    ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                        [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
+    KpC = rup(C, ops.KALIGN)
+    W4t = torch.zeros((3 * C, KpC), dtype=dtype, device=dev)
+    ops.pack_conv_w_t(dtype, conv4.weight, KpC, W4t, 0)
+    dfused = torch.empty_like(s.y4)
+    dlocal = torch.empty_like(s.y4)
+    dattn = torch.empty_like(s.y4)
+    ops.conv_gemm(dtype, [(dy4, 0, 0)], C, grid, hw, W4t, KpC, 3 * C, [dfused, dlocal, dattn], C)
+    del dy4
+
+    # ---- gate: s = sigmoid(bn3 y3); fused = s*local + (1-s)*attn ----
+    dz3 = torch.empty_like(s.y3)
+    part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+    call("dfcsa_bwd_gate", T, M, C, P(dfused), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean), P(bn3.invstd),
+         P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+    del dfused
+    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
+    dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
+    del dz3
+    ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                        [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
+    W3t = torch.zeros((2 * C, KpC), dtype=dtype, device=dev)
+    ops.pack_conv_w_t(dtype, conv3.weight, KpC, W3t, 0)
+    ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
+    del dy3
+
+    # ---- LightSelfAttention ----
+    dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype)
+
+    # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
+    dz2 = torch.empty_like(s.y2)
+    call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale), P(bn2.shift),
+         P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part), stream())
+    del dattn
+    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+    dy2 = ops.bn_bwd_apply(dtype, dz2, s.y2, bn2, bn2m.weight, coef, grad_of(conv2.bias))
+    del dz2
+
+    # ---- local branch: relu(bn1 y1) ----
+    dz1 = torch.empty_like(s.y1)
+    call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
+         P(dz1), P(part), stream())
+    del dlocal
+    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
+    dy1 = ops.bn_bwd_apply(dtype, dz1, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
+    del dz1
+
+    # ---- weight gradients of the input-side convs ----
+    xs = s.xs
+    ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9, Cin_p,
+                        Cin_real)
+    if has_res:
+        ops.conv_wgrad_into(dtype, [dy2, dres], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
+                            [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
+    else:
+        ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw, [grad_of(conv2.weight)], 1,
+                            Cin_p, Cin_real)
+    if not need_dx:
+        return None
+
+    # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM ----
+    Kx = rup(11 * C, ops.KALIGN)
+    Wdx = torch.zeros((Cin_p, Kx), dtype=dtype, device=dev)
+    ops.pack_conv_w_t(dtype, conv1.weight, Kx, Wdx, 0)
+    ops.pack_conv_w_t(dtype, conv2.weight, Kx, Wdx, 9 * C)
+    if has_res:
+        ops.pack_conv_w_t(dtype, blk.residual_conv.weight, Kx, Wdx, 10 * C)
+    else:
+        Wdx[:, 10 * C:11 * C] = torch.eye(C, dtype=dtype, device=dev)  # identity residual
+    segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dy2, 0, 0), (dres, 0, 0)]
+    dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
+    ops.conv_gemm(dtype, segs, C, grid, hw, Wdx, Kx, Cin_p, dxs, Cs)
+    return dxs
+
+
+def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
+    """LightSelfAttention up to the pooled output o (unet_dfc_sa_res.py:24-34): pool of
+    act(y*scale + shift) -> q/k/v 1x1 convs -> softmax(q k^T) -> o = v A^T (all fp32)."""
+    B, H, W, C = y.shape
+    dev = y.device
+    f32 = torch.float32
+    Pp = pool_size
+    N = Pp * Pp
+    Cq = lsa.query_conv.out_channels
+    J = 2 * Cq + C
+    S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
+    part = torch.empty(B * N * S * C, device=dev, dtype=f32)
+    call("dfcsa_lsa_pool", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), stream())
+    Wqkv = torch.empty((J, C), device=dev, dtype=f32)
+    WqkvT = torch.empty((C, J), device=dev, dtype=f32)
+    for w, off in ((lsa.query_conv.weight, 0), (lsa.key_conv.weight, Cq), (lsa.value_conv.weight, 2 * Cq)):
+        ops.pack_conv_w(f32, w, C, C, out=Wqkv, row0=off)
+        ops.pack_conv_w_t(f32, w, J, WqkvT, col0=off)
+    bqkv = torch.cat([lsa.query_conv.bias.detach(), lsa.key_conv.bias.detach(), lsa.value_conv.bias.detach()])
+    pooled = torch.empty((B, N, C), device=dev, dtype=f32)
+    qkv = torch.empty((B, N, J), device=dev, dtype=f32)
+    call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
+    A = torch.empty((B, N, N), device=dev, dtype=f32)
+    o = torch.empty((B, N, C), device=dev, dtype=f32)
+    call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
+    return pooled, qkv, A, o, Wqkv
+
+
+def lsa_core_backward(lsa, saved, dattn, pool_size, dtype):
+    """Backward of gamma * bilinear(o) (unet_dfc_sa_res.py:36-38) through the attention core;
+    accumulates gamma/q/k/v parameter gradients and returns d(pooled) [B][N][C] fp32."""
+    pooled, qkv, A, o, Wqkv = saved
+    B, H, W, C = dattn.shape
+    dev = dattn.device
+    f32 = torch.float32
+    Pp = pool_size
+    N = Pp * Pp
+    Cq = lsa.query_conv.out_channels
+    J = 2 * Cq + C
+    rows = torch.empty(B * H * Pp * C, device=dev, dtype=f32)
+    call("dfcsa_lsa_up_bwd_rows", dt(dtype), B, H, W, C, P(dattn), Pp, P(rows), stream())
+    dO = torch.empty((B, N, C), device=dev, dtype=f32)
+    gpart = torch.empty(B * N, device=dev, dtype=f32)
+    call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None, stream())
+    call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
+    dE = torch.empty((B, N, N), device=dev, dtype=f32)
+    dqkv = torch.empty((B, N, J), device=dev, dtype=f32)
+    call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
+    dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
+    call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
+         P(grad_of(lsa.query_conv.weight)), P(grad_of(lsa.key_conv.weight)), P(grad_of(lsa.value_conv.weight)),
+         P(grad_of(lsa.query_conv.bias)), P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)),
+         P(dpooled), stream())
+    return dpooled
+
+
+class LSAFunction(torch.autograd.Function):
+    """Standalone LightSelfAttention on an NHWC tensor (no BatchNorm/ReLU in front)."""
+
+    @staticmethod
+    def forward(ctx, lsa, pool_size, dtype, x, *params):
+        B, H, W, C = x.shape
+        dev = x.device
+        one = torch.ones(C, device=dev)
+        zero = torch.zeros(C, device=dev)
+        saved = lsa_core_forward(lsa, x, one, zero, False, pool_size, dtype)
+        out = torch.empty_like(x)
+        call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, None, None, None, P(x), P(one), P(zero),
+             P(saved[3]), pool_size, P(lsa.gamma), 0, None, P(out), stream())
+        ctx.lsa, ctx.saved, ctx.ps, ctx.dtype, ctx.np = lsa, saved, pool_size, dtype, len(params)
+        ctx.x = x
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        g = g.contiguous()
+        x = ctx.x
+        B, H, W, C = x.shape
+        dev = x.device
+        dpooled = lsa_core_backward(ctx.lsa, ctx.saved, g, ctx.ps, ctx.dtype)
+        one = torch.ones(C, device=dev)
+        zero = torch.zeros(C, device=dev)
+        dx = torch.empty_like(x)
+        part = torch.empty(ops.ntiles_ew(B * H * W, C) * 2 * C, device=dev, dtype=torch.float32)
+        call("dfcsa_bwd_attn_entry", dt(ctx.dtype), B, H, W, C, P(g), P(dpooled), ctx.ps, P(x), P(one), P(zero),
+             P(zero), P(one), 0, P(dx), P(part), stream())
+        ctx.saved = None
+        return (None, None, None, dx, *([None] * ctx.np))
+
+
+def block_params(blk):
+    return [p for p in blk.parameters()]
+
+
+class DFCBlockFunction(torch.autograd.Function):
+    """autograd node for one DFC block: inputs = NHWC sources (+ the block's parameters, passed
+    only so the graph knows they are upstream; their gradients are accumulated in place)."""
+
+    @staticmethod
+    def forward(ctx, blk, pool_size, dtype, nsrc, *args):
+        xs = list(args[:nsrc])
+        training = blk.training
+        out, saved = block_forward(blk, xs, pool_size, training, dtype)
+        ctx.blk, ctx.saved, ctx.dtype, ctx.nsrc, ctx.nparams = blk, saved, dtype, nsrc, len(args) - nsrc
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        need_dx = any(ctx.needs_input_grad[4:4 + ctx.nsrc])
+        dxs = block_backward(ctx.blk, ctx.saved, dout, need_dx, ctx.dtype)
+        ctx.saved = None
+        grads = list(dxs) if dxs is not None else [None] * ctx.nsrc
+        return (None, None, None, None, *grads, *([None] * ctx.nparams))

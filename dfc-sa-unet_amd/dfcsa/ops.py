@@ -1,0 +1,185 @@
+"""Thin tensor-level wrappers over the libdfcsa C ABI.
+
+Every wrapper enqueues on torch's current HIP stream and takes/returns torch tensors that live
+on the GPU.  NHWC activations are torch tensors of shape [B, H, W, C] (dtype bf16 or fp32);
+all statistics / parameters / gradients are fp32.  Nothing here computes on the host and
+there is no fallback: a CPU tensor is rejected.
+"""
+import ctypes
+
+import torch
+
+from . import _lib
+from ._lib import call
+
+KALIGN = 64          # Kpad granularity (64 bf16 / 32 f32 per K stage -> 64 serves both)
+GEMM_MTILE = 128     # rows per conv_gemm stats tile
+
+
+def stream():
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def dt(dtype):
+    if dtype == torch.bfloat16:
+        return _lib.DT_BF16
+    if dtype == torch.float32:
+        return _lib.DT_F32
+    raise TypeError(f"dfcsa supports bf16/fp32 activations, got {dtype}")
+
+
+def P(t):
+    """device pointer of a tensor (None -> NULL); rejects host tensors."""
+    if t is None:
+        return None
+    if not t.is_cuda:
+        raise RuntimeError("dfcsa kernels need GPU tensors (MI355X/ROCm); got a CPU tensor")
+    return t.data_ptr()
+
+
+def rup(x, a):
+    return (x + a - 1) // a * a
+
+
+def ntiles_gemm(M):
+    return (M + GEMM_MTILE - 1) // GEMM_MTILE
+
+
+def ntiles_ew(M, C):
+    return _lib.LIB.dfcsa_ew_ntiles(M, C)
+
+
+# --------------------------------------------------------------------------- GEMMs
+def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=None, stride=1,
+              mode=0, accumulate=False, stats=None, out_hw=(0, 0)):
+    """segs: list of (tensor, dh, dw); grid: (B, Ho, Wo) output pixel grid; in_hw: (Hi, Wi)."""
+    B, Ho, Wo = grid
+    d = _lib.ConvDesc()
+    d.dtype = dt(dtype)
+    d.M, d.N, d.Kpad, d.Cseg, d.nseg = B * Ho * Wo, N, Kpad, Cseg, len(segs)
+    if len(segs) > _lib.MAX_SEG:
+        raise ValueError("too many GEMM segments")
+    for i, (t, dh, dw) in enumerate(segs):
+        d.seg_ptr[i] = P(t)
+        d.seg_dh[i] = dh
+        d.seg_dw[i] = dw
+    d.Ho, d.Wo = Ho, Wo
+    d.Hi, d.Wi = in_hw
+    d.stride = stride
+    d.weight = P(weight)
+    d.bias = P(bias)
+    d.mode = mode
+    d.ndest = len(dests)
+    for i, t in enumerate(dests):
+        d.dest[i] = P(t)
+    d.Nd = Nd
+    d.accumulate = int(bool(accumulate))
+    d.stats = P(stats)
+    d.Hout, d.Wout = out_hw
+    call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
+
+
+def wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride=1):
+    """Returns (slab, splits) with slab [splits][ng*Cg][nseg*Cseg] fp32."""
+    B, Ho, Wo = grid
+    M = B * Ho * Wo
+    NI, NJ = len(gs) * Cg, len(segs) * Cseg
+    splits, mchunk = ctypes.c_int(), ctypes.c_int()
+    call("dfcsa_wgrad_plan", M, NI, NJ, dt(dtype), ctypes.addressof(splits), ctypes.addressof(mchunk))
+    slab = torch.empty(splits.value * NI * NJ, device=gs[0].device, dtype=torch.float32)
+    d = _lib.WgradDesc()
+    d.dtype = dt(dtype)
+    d.M, d.ng, d.Cg = M, len(gs), Cg
+    for i, t in enumerate(gs):
+        d.g_ptr[i] = P(t)
+    d.nseg, d.Cseg = len(segs), Cseg
+    for i, (t, dh, dw) in enumerate(segs):
+        d.seg_ptr[i] = P(t)
+        d.seg_dh[i] = dh
+        d.seg_dw[i] = dw
+    d.Ho, d.Wo = Ho, Wo
+    d.Hi, d.Wi = in_hw
+    d.stride = stride
+    d.slab = P(slab)
+    d.splits, d.mchunk = splits.value, mchunk.value
+    call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
+    return slab, splits.value, NI, NJ
+
+
+def wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts):
+    arr = (ctypes.c_void_p * len(dsts))(*[P(t) for t in dsts])
+    call("dfcsa_wgrad_reduce", P(slab), splits, NI, NJ, layout, ntaps, Ctot, Creal, len(dsts),
+         ctypes.addressof(arr), stream())
+
+
+def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, Creal, layout=0, stride=1):
+    slab, splits, NI, NJ = wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
+    wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, grads)
+
+
+# --------------------------------------------------------------------------- packing
+def pack_conv_w(dtype, w, Cpad, Kpad, out=None, row0=0, rows=None):
+    Cout, Cin = w.shape[0], w.shape[1]
+    ntaps = w.shape[2] * w.shape[3] if w.dim() == 4 else 1
+    if out is None:
+        out = torch.empty((rows or Cout, Kpad), device=w.device, dtype=dtype)
+    call("dfcsa_pack_conv_w", dt(dtype), P(w), Cout, Cin, ntaps, Cpad, Kpad, row0, P(out), stream())
+    return out
+
+
+def pack_conv_w_t(dtype, w, Kpad, out, col0):
+    Cout, Cin = w.shape[0], w.shape[1]
+    ntaps = w.shape[2] * w.shape[3] if w.dim() == 4 else 1
+    call("dfcsa_pack_conv_w_t", dt(dtype), P(w), Cout, Cin, ntaps, Kpad, col0, P(out), stream())
+    return out
+
+
+def zeros(shape, dtype, device):
+    return torch.zeros(shape, dtype=dtype, device=device)
+
+
+# --------------------------------------------------------------------------- BatchNorm
+class BNState:
+    """Per-forward BatchNorm coefficients (fp32 [C] each)."""
+    __slots__ = ("scale", "shift", "mean", "invstd")
+
+    def __init__(self, C, device):
+        buf = torch.empty(4, C, device=device, dtype=torch.float32)
+        self.scale, self.shift, self.mean, self.invstd = buf[0], buf[1], buf[2], buf[3]
+
+
+def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
+    st = BNState(C, bn_mod.weight.device)
+    nbt = bn_mod.num_batches_tracked if training else None
+    call("dfcsa_bn_finalize", P(stats) if training else None, ntiles, C, ld, count, P(conv_bias),
+         P(bn_mod.weight), P(bn_mod.bias), P(bn_mod.running_mean), P(bn_mod.running_var), P(nbt),
+         float(bn_mod.momentum if bn_mod.momentum is not None else 0.1), float(bn_mod.eps), int(training),
+         P(st.scale), P(st.shift), P(st.mean), P(st.invstd), stream())
+    return st
+
+
+def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
+    coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
+    call("dfcsa_bn_bwd_finalize", P(partial), ntiles, nsum, C, count, P(coef), P(dgamma), P(dbeta), P(extra),
+         stream())
+    return coef
+
+
+def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
+    M, C = dz.numel() // dz.shape[-1], dz.shape[-1]
+    nt = ntiles_ew(M, C)
+    dy = torch.empty_like(dz)
+    part = torch.empty(nt * C, device=dz.device, dtype=torch.float32)
+    call("dfcsa_bn_bwd_apply", dt(dtype), M, C, P(dz), P(y), P(bn.mean), P(bn.invstd), P(gamma), P(coef), P(dy),
+         P(part), stream())
+    if bias_grad is not None:
+        call("dfcsa_slab_colsum", P(part), nt, C, P(bias_grad), stream())
+    return dy
+
+
+def channel_sum_into(dtype, x, out):
+    M, C = x.numel() // x.shape[-1], x.shape[-1]
+    nt = ntiles_ew(M, C)
+    part = torch.empty(nt * C, device=x.device, dtype=torch.float32)
+    call("dfcsa_channel_sum", dt(dtype), M, C, P(x), P(part), stream())
+    call("dfcsa_slab_colsum", P(part), nt, C, P(out), stream())

@@ -1,0 +1,88 @@
+"""Fused clip_grad_norm_ + momentum SGD over a model's flat parameter buffer.
+
+Replaces, in one device pass and without host synchronisation:
+  torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)   utils/trainer.py:149
+  torch.optim.SGD(lr, momentum, weight_decay).step()                  train.py:73-78, trainer.py:151
+with torch's semantics (weight decay added to the gradient before momentum; first step
+initialises the buffer to the gradient; p.grad holds the clipped gradient afterwards).
+"""
+import ctypes
+
+import torch
+
+from ._lib import LIB, call
+from .ops import P, stream
+
+
+class FusedSGD(torch.optim.Optimizer):
+    def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, dampening=0.0, nesterov=False):
+        if dampening != 0.0 or nesterov:
+            raise NotImplementedError("FusedSGD implements the reference's SGD (no dampening/nesterov)")
+        super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, dampening=0.0,
+                                      nesterov=False, maximize=False, foreach=None, differentiable=False,
+                                      fused=None))
+        if len(self.param_groups) != 1:
+            raise NotImplementedError("FusedSGD supports a single parameter group")
+        self._flat = None
+        self._mom = None
+        self._mom_init = None
+        self._partial = None
+        self.last_norm = None
+
+    # ------------------------------------------------------------------ helpers
+    def _resolve(self):
+        params = self.param_groups[0]["params"]
+        flat = getattr(params[0], "_dfcsa_flat", None)
+        if flat is None or not flat.valid() or len(flat.params) != len(params) or \
+                any(a is not b for a, b in zip(flat.params, params)):
+            raise RuntimeError("FusedSGD needs the parameters of a dfcsa model after its first forward "
+                               "(they live in one flat buffer); got foreign parameters")
+        if flat is not self._flat:
+            self._flat = flat
+            self._mom = torch.zeros_like(flat.data)
+            self._mom_init = torch.zeros(1, dtype=torch.int32, device=flat.device)
+            self._partial = torch.empty(LIB.dfcsa_sumsq_nparts(flat.numel), dtype=torch.float32,
+                                        device=flat.device)
+            self.last_norm = torch.zeros(1, dtype=torch.float32, device=flat.device)
+            for p, off in zip(flat.params, flat.offsets):
+                self.state[p]["momentum_buffer"] = self._mom[off:off + p.numel()].view_as(p)
+        return flat
+
+    def zero_grad(self, set_to_none=True):
+        flat = getattr(self.param_groups[0]["params"][0], "_dfcsa_flat", None)
+        if flat is not None and flat.valid():
+            flat.zero_grad()  # one memset; grads stay views of the flat buffer
+        else:
+            super().zero_grad(set_to_none)
+
+    @torch.no_grad()
+    def step(self, closure=None, max_norm=None, grad_scale=1.0, skip_if_nonfinite=None):
+        """max_norm: clip the global L2 norm first (None = no clipping).
+        grad_scale: multiply gradients first (1/world_size after an all-reduce sum).
+        skip_if_nonfinite: device scalar; the update is skipped on the device if it is NaN/inf."""
+        loss = closure() if closure is not None else None
+        flat = self._resolve()
+        g = self.param_groups[0]
+        n = flat.numel
+        if max_norm is not None:
+            call("dfcsa_sumsq_partial", ctypes.c_int64(n), P(flat.grad), P(self._partial), stream())
+            nparts, mn = self._partial.numel(), float(max_norm)
+        else:
+            nparts, mn = 0, float("inf")
+        call("dfcsa_clip_sgd", ctypes.c_int64(n), P(flat.data), P(flat.grad), P(self._mom), P(self._partial),
+             nparts, mn, float(grad_scale), float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
+             P(self._mom_init), P(skip_if_nonfinite), P(self.last_norm), stream())
+        return loss
+
+    def load_state_dict(self, state_dict):
+        super().load_state_dict(state_dict)
+        flat = getattr(self.param_groups[0]["params"][0], "_dfcsa_flat", None)
+        if flat is None:
+            return
+        bufs = [self.state[p].get("momentum_buffer") for p in flat.params]
+        if all(b is not None for b in bufs):
+            self._flat = None
+            self._resolve()
+            for p, b in zip(flat.params, bufs):
+                self.state[p]["momentum_buffer"].copy_(b)
+            self._mom_init.fill_(1)

@@ -1,0 +1,179 @@
+"""DFC-SA-Res U-Net on the MI355X kernels of libdfcsa.
+
+Drop-in for the reference's models/unet_dfc_sa_res.py:
+  * the module tree (attribute names, nn.Sequential indices, parameter shapes, creation order)
+    is the reference's, so ``state_dict`` keys (343 for features 64..512) and the default
+    initialisation under a given seed are identical -- checkpoints interoperate both ways;
+  * ``forward`` runs the hand-written HIP kernels (dfcsa.block / dfcsa.functions) on NHWC
+    activations in the compute dtype (bf16 by default, fp32 for parity runs) with fp32 master
+    parameters, gradients and statistics.  The nn.Conv2d / nn.BatchNorm2d submodules are only
+    parameter holders; their own forward is never called.
+
+Reference classes: LightSelfAttention :5-39, DynamicFusionConvAttnBlock :41-116,
+UNetDFCSA :118-204, UNetDFCSARes :207-220.
+"""
+import torch
+import torch.nn as nn
+
+import dfcsa
+from dfcsa.block import DFCBlockFunction, LSAFunction
+from dfcsa.flat import FlatParams
+from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPool2x2, ResizeBilinear
+from dfcsa.ops import rup
+
+
+def _nchw_to_nhwc(x, dtype):
+    return InputToNHWC.apply(x, dtype, rup(x.shape[1], 8))
+
+
+def _nhwc_to_nchw(y):
+    return y.permute(0, 3, 1, 2).float()
+
+
+class LightSelfAttention(nn.Module):
+    """Pooled self-attention (reference :5-39).  Parameters: query/key (C -> C // ratio),
+    value (C -> C) 1x1 convs and a scalar gamma initialised to 0."""
+
+    def __init__(self, channels, pool_size=8, ablation_on_qk_channels=8):
+        super().__init__()
+        self.pool_size = pool_size
+        reduced = channels // ablation_on_qk_channels
+        self.query_conv = nn.Conv2d(channels, reduced, kernel_size=1)
+        self.key_conv = nn.Conv2d(channels, reduced, kernel_size=1)
+        self.value_conv = nn.Conv2d(channels, channels, kernel_size=1)
+        self.gamma = nn.Parameter(torch.zeros(1))
+        self.compute_dtype = torch.bfloat16
+
+    def forward(self, x):
+        """x: [B, C, H, W] (any values) -> gamma * up(attn(pool(x))) + x, NCHW fp32."""
+        xh = _nchw_to_nhwc(x, self.compute_dtype)
+        y = LSAFunction.apply(self, self.pool_size, self.compute_dtype, xh, *self.parameters())
+        return _nhwc_to_nchw(y)
+
+
+class DynamicFusionConvAttnBlock(nn.Module):
+    """DFC block (reference :41-116): 3x3 conv branch, 1x1 -> pooled self-attention branch,
+    sigmoid fusion gate, 1x1 fusion conv, scaled 1x1 residual."""
+
+    def __init__(self, in_channels, out_channels, kernel_size=3, stride=1, padding=1, pool_size=8,
+                 ablation_on_qk_channels=8):
+        super().__init__()
+        if kernel_size != 3 or stride != 1 or padding != 1:
+            raise NotImplementedError("the DFC block kernels implement the reference's 3x3/s1/p1 local branch")
+        self.pool_size = pool_size
+        self.conv_branch = nn.Sequential(
+            nn.Conv2d(in_channels, out_channels, kernel_size=3, stride=1, padding=1),
+            nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True))
+        self.attn_branch = nn.Sequential(
+            nn.Conv2d(in_channels, out_channels, kernel_size=1),
+            nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True),
+            LightSelfAttention(out_channels, pool_size=pool_size, ablation_on_qk_channels=ablation_on_qk_channels))
+        self.gate = nn.Sequential(
+            nn.Conv2d(out_channels * 2, out_channels, kernel_size=1),
+            nn.BatchNorm2d(out_channels), nn.Sigmoid())
+        self.fusion_conv = nn.Sequential(
+            nn.Conv2d(out_channels * 3, out_channels, kernel_size=1),
+            nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True))
+        if in_channels != out_channels:
+            self.residual_conv = nn.Conv2d(in_channels, out_channels, kernel_size=1, bias=False)
+        else:
+            self.residual_conv = nn.Identity()
+        self.res_scale = nn.Parameter(torch.tensor(0.1))
+        self.compute_dtype = torch.bfloat16
+
+    def forward_nhwc(self, xs, dtype):
+        """xs: list of NHWC sources whose channel concat is the block input (skip concat
+        never materialised)."""
+        return DFCBlockFunction.apply(self, self.pool_size, dtype, len(xs), *xs, *self.parameters())
+
+    def forward(self, x):
+        """Standalone use on NCHW fp32 input (returns NCHW fp32)."""
+        y = self.forward_nhwc([_nchw_to_nhwc(x, self.compute_dtype)], self.compute_dtype)
+        return _nhwc_to_nchw(y)
+
+
+class UNetDFCSA(nn.Module):
+    """U-Net of DFC blocks (reference :118-204): 4 encoder blocks + 2x2 max pooling, a 2x-wide
+    bottleneck block, 4 x (ConvTranspose2d k2 s2 -> [bilinear fix] -> concat skip -> block),
+    1x1 head.  ``precision`` selects the activation dtype ('bf16' default, 'fp32')."""
+
+    def __init__(self, in_channels=3, out_channels=1, features=(64, 128, 256, 512), pool_size=8,
+                 ablation_on_qk_channels=8, precision=None):
+        super().__init__()
+        f = list(features)
+        for c in f:
+            if c % 8:
+                raise ValueError(f"feature widths must be multiples of 8 for the NHWC kernels, got {f}")
+        blk = lambda i, o: DynamicFusionConvAttnBlock(  # noqa: E731
+            i, o, kernel_size=3, stride=1, padding=1, pool_size=pool_size,
+            ablation_on_qk_channels=ablation_on_qk_channels)
+        self.pool_size = pool_size
+        self.in_channels = in_channels
+        self.down1 = blk(in_channels, f[0])
+        self.pool1 = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.down2 = blk(f[0], f[1])
+        self.pool2 = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.down3 = blk(f[1], f[2])
+        self.pool3 = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.down4 = blk(f[2], f[3])
+        self.pool4 = nn.MaxPool2d(kernel_size=2, stride=2)
+        self.bottleneck = blk(f[3], f[3] * 2)
+        self.up4 = nn.ConvTranspose2d(f[3] * 2, f[3], kernel_size=2, stride=2)
+        self.up_conv4 = blk(f[3] * 2, f[3])
+        self.up3 = nn.ConvTranspose2d(f[3], f[2], kernel_size=2, stride=2)
+        self.up_conv3 = blk(f[2] * 2, f[2])
+        self.up2 = nn.ConvTranspose2d(f[2], f[1], kernel_size=2, stride=2)
+        self.up_conv2 = blk(f[1] * 2, f[1])
+        self.up1 = nn.ConvTranspose2d(f[1], f[0], kernel_size=2, stride=2)
+        self.up_conv1 = blk(f[0] * 2, f[0])
+        self.final_conv = nn.Conv2d(f[0], out_channels, kernel_size=1)
+        self.compute_dtype = dfcsa.resolve_dtype(precision)
+        self._flat = None
+
+    # -------------------------------------------------------------- precision / storage
+    def set_precision(self, precision):
+        self.compute_dtype = dfcsa.resolve_dtype(precision)
+        return self
+
+    def _apply(self, fn, *args, **kwargs):
+        out = super()._apply(fn, *args, **kwargs)
+        self._flat = None  # parameters moved: re-flatten lazily on the next forward
+        return out
+
+    def flat_params(self):
+        """The FlatParams storage of this model (created on first use, on the params' device)."""
+        if self._flat is None or not self._flat.valid():
+            self._flat = FlatParams(self)
+        return self._flat
+
+    # -------------------------------------------------------------- forward
+    def forward(self, x):
+        """x: [B, in_channels, H, W] float -> logits [B, out_channels, H, W] fp32 (no sigmoid)."""
+        if not x.is_cuda:
+            raise RuntimeError("UNetDFCSARes runs on the MI355X kernels only; move model and input to 'cuda'")
+        flat = self.flat_params()
+        if torch.is_grad_enabled():
+            flat.attach_grads()
+        dt = self.compute_dtype
+        mp = lambda t: MaxPool2x2.apply(t, dt)  # noqa: E731
+        h = _nchw_to_nhwc(x, dt)
+        d1 = self.down1.forward_nhwc([h], dt)
+        d2 = self.down2.forward_nhwc([mp(d1)], dt)
+        d3 = self.down3.forward_nhwc([mp(d2)], dt)
+        d4 = self.down4.forward_nhwc([mp(d3)], dt)
+        u = self.bottleneck.forward_nhwc([mp(d4)], dt)
+        for up, block, skip in ((self.up4, self.up_conv4, d4), (self.up3, self.up_conv3, d3),
+                                (self.up2, self.up_conv2, d2), (self.up1, self.up_conv1, d1)):
+            u = ConvTranspose2x2.apply(u, up, dt, *up.parameters())
+            if u.shape[1:3] != skip.shape[1:3]:
+                u = ResizeBilinear.apply(u, tuple(skip.shape[1:3]), dt)
+            u = block.forward_nhwc([u, skip], dt)  # cat([up, skip]) order, never materialised
+        return Head1x1.apply(u, self.final_conv, dt, *self.final_conv.parameters())
+
+
+class UNetDFCSARes(UNetDFCSA):
+    """Reference :207-220 -- identical to UNetDFCSA (the residual lives inside each block)."""
+
+    def __init__(self, in_channels=3, out_channels=1, features=(64, 128, 256, 512), pool_size=8,
+                 ablation_on_qk_channels=8, precision=None):
+        super().__init__(in_channels, out_channels, features, pool_size, ablation_on_qk_channels, precision)

@@ -1,0 +1,222 @@
+"""Trainer (drop-in for the reference's utils/trainer.py:19-461).
+
+Same constructor (model, train_loader, val_loader, optimizer, device, config), same methods
+(train_epoch -> (loss, iou, dice), validate_epoch -> dict, save_checkpoint, load_checkpoint,
+train) and the same step semantics (trainer.py:115-151):
+
+    zero_grad -> forward -> sigmoid -> calculate_metrics -> [NaN loss: skip] -> backward
+    -> clip_grad_norm_(max_norm=1.0) -> optimizer.step()
+
+On the MI355X path the step is device-resident (``train_step``): the NaN check skips the SGD
+update on the device and the metrics stay on the device; the epoch loop reads them back once
+per batch for the running averages, as the reference's ``.item()`` calls do.  With a
+``dfcsa.optim.FusedSGD`` optimizer, clipping + SGD is one fused pass; with any other
+torch optimizer the reference's clip_grad_norm_ + step() are called.
+
+Differences kept deliberately small and listed: plots are written only when matplotlib is
+importable; best/worst validation samples are kept (tensors on the host) but image dumps
+(cv2 in the reference) are not written; ``train(resume_from)`` restores histories and the
+start epoch (the reference resets them, trainer.py:334-349 -- pass
+``training.reference_resume_semantics: true`` to keep that behaviour).
+"""
+import csv
+import os
+import time
+
+import torch
+
+from dfcsa.loss import metrics_from_stats, sigmoid
+from dfcsa.optim import FusedSGD
+from utils.metrics import calculate_metrics_device
+
+try:
+    from tqdm import tqdm
+except ImportError:  # pragma: no cover
+    def tqdm(it, **kw):
+        return it
+
+
+class Trainer:
+    def __init__(self, model, train_loader, val_loader, optimizer, device, config):
+        self.config = config
+        self.device = device
+        self.model = model.to(device)
+        self.optimizer = optimizer
+        self.train_loader = train_loader
+        self.val_loader = val_loader
+        self.loss_type = config["training"].get("loss", {}).get("type", "dice")
+        self.loss_params = config["training"].get("loss", {}).get("params", {}) or {}
+        print(f"使用損失函數: {self.loss_type}")
+        if self.loss_type == "bce_dice":
+            print(f"BCE+Dice 損失參數: weight_bce={self.loss_params.get('weight_bce', 1.0)}, "
+                  f"weight_dice={self.loss_params.get('weight_dice', 1.0)}")
+        self.train_losses, self.val_losses = [], []
+        self.train_dice_scores, self.val_dice_scores = [], []
+        self.train_iou_scores, self.val_iou_scores = [], []
+        self.epochs = []
+        self.log_dir = config["logging"]["log_dir"].replace("\\", "/")
+        self.images_dir = config["logging"]["images_dir"].replace("\\", "/")
+        os.makedirs(self.log_dir, exist_ok=True)
+        os.makedirs(self.images_dir, exist_ok=True)
+        self.best_model_path = os.path.join(self.log_dir, "best_model.pth").replace("\\", "/")
+        self.best_val_loss = float("inf")
+        self.checkpoint_dir = os.path.join(self.log_dir, "checkpoints").replace("\\", "/")
+        os.makedirs(self.checkpoint_dir, exist_ok=True)
+        self.start_time = time.time()
+        self.num_epochs = config["training"]["num_epochs"]
+        self.max_norm = 1.0
+        print(f"模型將在 {self.device} 上訓練")
+
+    # ------------------------------------------------------------------ one step
+    def train_step(self, images, masks):
+        """One device-resident training step.  Returns {'loss': 0-d tensor, 'stats': fp32[8]}
+        (see dfcsa.loss) without synchronising with the host."""
+        self.optimizer.zero_grad()
+        logits = self.model(images)
+        probs = sigmoid(logits)
+        met = calculate_metrics_device(probs, masks, self.loss_type, self.loss_params)
+        loss = met["loss"]
+        loss.backward()
+        if isinstance(self.optimizer, FusedSGD):
+            self.optimizer.step(max_norm=self.max_norm, skip_if_nonfinite=loss)
+        else:
+            if torch.isfinite(loss):  # host sync; reference behaviour with a foreign optimizer
+                torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm)
+                self.optimizer.step()
+        return met
+
+    def train_epoch(self, epoch):
+        self.model.train()
+        running_loss = running_iou = running_dice = 0.0
+        bar = tqdm(self.train_loader, desc=f"Epoch {epoch + 1}/{self.num_epochs} [Train]")
+        for batch_idx, batch in enumerate(bar):
+            images = batch["image"].to(self.device, non_blocking=True)
+            masks = batch["mask"].to(self.device, non_blocking=True)
+            met = self.train_step(images, masks)
+            loss = float(met["stats"][0].item())
+            if loss != loss:  # NaN: the device already skipped the update (trainer.py:134-139)
+                print(f"Warning: NaN loss detected at batch {batch_idx}\n  Skipping this batch...")
+                continue
+            if loss > 100:
+                print(f"Warning: Very large loss detected: {loss:.6f} at batch {batch_idx}")
+            iou, dice = metrics_from_stats(met["stats"])
+            running_loss += loss
+            running_iou += iou
+            running_dice += dice
+            if hasattr(bar, "set_postfix"):
+                bar.set_postfix({"loss": running_loss / (batch_idx + 1), "iou": running_iou / (batch_idx + 1),
+                                 "dice": running_dice / (batch_idx + 1)})
+        n = len(self.train_loader)
+        return running_loss / n, running_iou / n, running_dice / n
+
+    @torch.no_grad()
+    def validate_epoch(self, dataloader):
+        self.model.eval()
+        running_loss = running_iou = running_dice = 0.0
+        samples = []
+        for batch_idx, batch in enumerate(tqdm(dataloader, desc="Validation")):
+            images = batch["image"].to(self.device)
+            masks = batch["mask"].to(self.device)
+            probs = sigmoid(self.model(images))
+            met = calculate_metrics_device(probs, masks, self.loss_type, self.loss_params)
+            loss = float(met["stats"][0].item())
+            if loss != loss:
+                print(f"Warning: NaN loss detected in validation at batch {batch_idx}")
+                continue
+            iou, dice = metrics_from_stats(met["stats"])
+            running_loss += loss
+            running_iou += iou
+            running_dice += dice
+            names = batch.get("filename", [f"{batch_idx}_{i}" for i in range(images.shape[0])])
+            for i in range(images.shape[0]):
+                m = calculate_metrics_device(probs[i:i + 1], masks[i:i + 1], self.loss_type, self.loss_params)
+                si, sd = metrics_from_stats(m["stats"])
+                samples.append({"batch_idx": batch_idx, "sample_idx": i, "image": images[i].cpu(),
+                                "mask": masks[i].cpu(), "output": probs[i].cpu(), "filename": names[i],
+                                "metrics": {"loss": float(m["stats"][0].item()), "iou": si, "dice": sd}})
+        n = len(dataloader)
+        samples.sort(key=lambda s: s["metrics"]["dice"])
+        k = self.config["logging"].get("save_best_worst_samples", 0)
+        return {"loss": running_loss / n, "iou": running_iou / n, "dice": running_dice / n,
+                "best_samples": samples[-k:] if k else [], "worst_samples": samples[:k]}
+
+    # ------------------------------------------------------------------ checkpoints
+    def save_checkpoint(self, epoch, metrics, is_best=False):
+        ckpt = {"epoch": epoch, "model_state_dict": self.model.state_dict(),
+                "optimizer_state_dict": self.optimizer.state_dict(),
+                "train_losses": self.train_losses, "val_losses": self.val_losses,
+                "train_dice_scores": self.train_dice_scores, "val_dice_scores": self.val_dice_scores,
+                "train_iou_scores": self.train_iou_scores, "val_iou_scores": self.val_iou_scores,
+                "best_val_loss": self.best_val_loss,
+                "metrics": {k: v for k, v in metrics.items() if k not in ("best_samples", "worst_samples")}}
+        path = os.path.join(self.checkpoint_dir, f"checkpoint_epoch_{epoch + 1}.pth").replace("\\", "/")
+        torch.save(ckpt, path)
+        if is_best:
+            torch.save(self.model.state_dict(), self.best_model_path)
+            torch.save(ckpt, os.path.join(self.checkpoint_dir, "best_checkpoint.pth").replace("\\", "/"))
+
+    def load_checkpoint(self, checkpoint_path):
+        ckpt = torch.load(checkpoint_path.replace("\\", "/"), map_location=self.device, weights_only=True)
+        self.model.load_state_dict(ckpt["model_state_dict"])
+        self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        for k in ("train_losses", "val_losses", "train_dice_scores", "val_dice_scores", "train_iou_scores",
+                  "val_iou_scores", "best_val_loss"):
+            setattr(self, k, ckpt[k])
+        return ckpt["epoch"]
+
+    # ------------------------------------------------------------------ loop
+    def _write_history(self):
+        with open(os.path.join(self.images_dir, "metrics.csv"), "w", newline="") as f:
+            w = csv.writer(f)
+            w.writerow(["epoch", "train_loss", "val_loss", "train_dice", "val_dice", "train_iou", "val_iou"])
+            for row in zip(self.epochs, self.train_losses, self.val_losses, self.train_dice_scores,
+                           self.val_dice_scores, self.train_iou_scores, self.val_iou_scores):
+                w.writerow(row)
+        try:
+            import matplotlib
+            matplotlib.use("Agg")
+            import matplotlib.pyplot as plt
+        except ImportError:
+            return
+        for name, tr, va in (("loss", self.train_losses, self.val_losses),
+                             ("dice", self.train_dice_scores, self.val_dice_scores),
+                             ("iou", self.train_iou_scores, self.val_iou_scores)):
+            plt.figure(figsize=(8, 5))
+            plt.plot(self.epochs, tr, label=f"train {name}")
+            plt.plot(self.epochs, va, label=f"val {name}")
+            plt.legend()
+            plt.savefig(os.path.join(self.images_dir, f"{name}_plot.png"))
+            plt.close()
+
+    def train(self, resume_from=None):
+        start_epoch = 0
+        if resume_from:
+            start_epoch = self.load_checkpoint(resume_from) + 1
+            print(f"從 epoch {start_epoch} 恢復訓練")
+        if not resume_from or self.config["training"].get("reference_resume_semantics", False):
+            self.epochs, self.train_losses, self.val_losses = [], [], []
+            self.train_dice_scores, self.val_dice_scores = [], []
+            self.train_iou_scores, self.val_iou_scores = [], []
+        best_val_dice = 0.0
+        for epoch in range(start_epoch, self.num_epochs):
+            tr = self.train_epoch(epoch)
+            va = self.validate_epoch(self.val_loader)
+            self.epochs.append(epoch + 1)
+            self.train_losses.append(tr[0])
+            self.val_losses.append(va["loss"])
+            self.train_dice_scores.append(tr[2])
+            self.val_dice_scores.append(va["dice"])
+            self.train_iou_scores.append(tr[1])
+            self.val_iou_scores.append(va["iou"])
+            print(f"Epoch [{epoch + 1}/{self.num_epochs}]")
+            print(f"  Train Loss: {tr[0]:.4f}, Dice: {tr[2]:.4f}, IoU: {tr[1]:.4f}")
+            print(f"  Val Loss: {va['loss']:.4f}, Dice: {va['dice']:.4f}, IoU: {va['iou']:.4f}")
+            is_best = va["dice"] > best_val_dice
+            if is_best:
+                best_val_dice = va["dice"]
+            if (epoch + 1) % self.config["training"]["save_checkpoint_freq"] == 0 or is_best:
+                self.save_checkpoint(epoch, va, is_best)
+            self._write_history()
+        total = time.time() - self.start_time
+        print(f"Training completed in {total:.0f}s; best validation dice: {best_val_dice:.4f}")
+        return best_val_dice

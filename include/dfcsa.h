@@ -1,0 +1,286 @@
+/* libdfcsa -- MI355X (gfx950) kernels for the DFC-SA-Res U-Net training step.
+ *
+ * C ABI: plain pointers (device pointers unless stated), int sizes, a hipStream_t passed as
+ * void*.  Every entry point only enqueues work on that stream: it never allocates, never
+ * synchronises and never throws; it returns 0 on success, DFCSA_EINVAL for a shape/argument
+ * error, or -hipError_t for a launch error.  Scratch memory ("slabs") is owned by the caller
+ * (the PyTorch caching allocator on the Python side); sizes follow from the documented shapes.
+ *
+ * Layouts: activations are NHWC ("[M][C]" with M = B*H*W pixels), element type selected by
+ * `dtype` (DFCSA_DT_F32 = 0 or DFCSA_DT_BF16 = 1); all statistics, accumulators, parameters,
+ * gradients and optimizer state are fp32.  Channel counts of NHWC tensors are multiples of 8.
+ *
+ * The reference (YukiHataRin/DFC-SA-UNet) has no native boundary: every function below
+ * replaces PyTorch/ATen calls made by the reference's Python modules; the replaced call sites
+ * are cited per entry point (file:line in the reference checkout).
+ */
+#ifndef DFCSA_H_
+#define DFCSA_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DFCSA_DT_F32 0
+#define DFCSA_DT_BF16 1
+#define DFCSA_MAX_SEG 32
+#define DFCSA_EINVAL (-10000)
+
+/* ------------------------------------------------------------------------------------------
+ * Implicit-GEMM convolution (MFMA).  Replaces nn.Conv2d / nn.ConvTranspose2d forward and the
+ * data-gradient half of their backward, plus torch.cat of the block inputs:
+ *   models/unet_dfc_sa_res.py:58-59 (3x3), :66, :74, :81, :88 (1x1), :147-156 (ConvTranspose),
+ *   :102, :109, :182-200 (cat).
+ * C[m][n] = sum_k A[m][k] * weight[n][k] (+ bias[n]); A is gathered on the fly:
+ *   A[m][s*Cseg + c] = seg_ptr[s][b, oh*stride + seg_dh[s], ow*stride + seg_dw[s], c]
+ * over an output grid of Ho x Wo pixels (m = (b*Ho + oh)*Wo + ow), sources Hi x Wi.
+ * weight: [N][Kpad] of dtype, Kpad >= nseg*Cseg, multiple of 64 (bf16) / 32 (f32), zero-padded.
+ * mode PLAIN: columns [d*Nd, (d+1)*Nd) go to dest[d] ([M][Nd]).  mode SHUFFLE2 (ConvTranspose
+ * k2 s2): column n = (2i + j)*Nd + co goes to dest[0][b, 2oh+i, 2ow+j, co] of Hout x Wout.
+ * accumulate: dest += C.  stats (optional): per 128-row M tile t, stats[t][0][n] = sum of the
+ * fp32 accumulator (without bias) over valid rows, stats[t][1][n] = sum of squares.
+ * ---------------------------------------------------------------------------------------- */
+#define CONV_STORE_PLAIN 0
+#define CONV_STORE_SHUFFLE2 1
+typedef struct {
+  int dtype;
+  int M, N, Kpad, Cseg, nseg;
+  const void* seg_ptr[DFCSA_MAX_SEG];
+  int seg_dh[DFCSA_MAX_SEG];
+  int seg_dw[DFCSA_MAX_SEG];
+  int Ho, Wo, Hi, Wi, stride;
+  const void* weight;
+  const float* bias;
+  int mode, ndest;
+  void* dest[3];
+  int Nd, accumulate;
+  float* stats;
+  int Hout, Wout;
+} dfcsa_conv_desc;
+int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream);
+int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile (ntiles = ceil(M / mtile)) */
+
+/* ------------------------------------------------------------------------------------------
+ * Weight gradient (MFMA, reduction over pixels).  Replaces the weight half of
+ * convolution_backward for every conv of the block (unet_dfc_sa_res.py:58,66,74,81,88) and
+ * of ConvTranspose2d (:147-156).
+ * slab[s][i][j] = sum over pixels m in chunk s of G[m][i] * X[m][j], where G = concat of
+ * ng tensors [M][Cg] (i = src*Cg + c) and X is gathered like dfcsa_conv_desc's A (j = seg*Cseg+c).
+ * slab: [splits][NI][NJ] fp32 with NI = ng*Cg, NJ = nseg*Cseg; splits/mchunk from
+ * dfcsa_wgrad_plan.
+ * ---------------------------------------------------------------------------------------- */
+typedef struct {
+  int dtype;
+  int M;
+  int ng, Cg;
+  const void* g_ptr[3];
+  int nseg, Cseg;
+  const void* seg_ptr[DFCSA_MAX_SEG];
+  int seg_dh[DFCSA_MAX_SEG];
+  int seg_dw[DFCSA_MAX_SEG];
+  int Ho, Wo, Hi, Wi, stride;
+  float* slab;
+  int splits, mchunk;
+} dfcsa_wgrad_desc;
+int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk);
+int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
+/* grad += sum_s slab[s] mapped to the reference weight layout.
+ *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
+ *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.
+ *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij]. */
+int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
+                       int Ctot, int Creal, int ndst, float* const* dst, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Weight packing (fp32 reference layouts -> dtype GEMM operands).  Runs every forward
+ * (weights change every step).
+ * ---------------------------------------------------------------------------------------- */
+/* out[row0 + co][tap*Cpad + ci] = w[co][ci][tap] (ci < Cin), zero elsewhere in the row;
+ * out has row stride Kpad; w is [Cout][Cin][ntaps] fp32.  */
+int dfcsa_pack_conv_w(int dtype, const float* w, int Cout, int Cin, int ntaps, int Cpad,
+                      int Kpad, int row0, void* out, void* stream);
+/* transposed (dgrad) packing: out[ci][col0 + tap*Cout + co] = w[co][ci][tap] (row stride Kpad) */
+int dfcsa_pack_conv_w_t(int dtype, const float* w, int Cout, int Cin, int ntaps, int Kpad,
+                        int col0, void* out, void* stream);
+/* ConvTranspose2d weight [Cin][Cout][2][2]: fwd [4*Cout][Cin] (row ij*Cout+co), bwd [Cin][4*Cout],
+ * bias4[ij*Cout+co] = bias[co]. */
+int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, int Cin, int Cout, void* out_fwd,
+                       void* out_bwd, float* bias4, void* stream);
+/* zero-fill (used for padded weight rows) */
+int dfcsa_zero(void* p, int64_t bytes, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * BatchNorm2d (train: batch statistics, biased variance for normalising, unbiased for
+ * running_var, momentum 0.1, eps 1e-5; eval: running statistics).  Replaces
+ * native_batch_norm at unet_dfc_sa_res.py:60, :67, :75, :82.
+ * finalize: from the conv epilogue slab (sums of the accumulator without bias) and the conv
+ * bias, produce per-channel scale/shift (y_bn = y*scale + shift), mean, invstd; update the
+ * running statistics and num_batches_tracked in place (training only).  stats rows are
+ * ld floats long (stats[t][k][c] at (t*2 + k)*ld + c), so a slice of a wider GEMM works.
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_bn_finalize(const float* stats, int ntiles, int C, int ld, int count, const float* conv_bias,
+                      const float* gamma, const float* beta, float* running_mean, float* running_var,
+                      int64_t* num_batches_tracked, float momentum, float eps, int training,
+                      float* scale, float* shift, float* mean, float* invstd, void* stream);
+/* out = act(y*scale + shift): act 0 none, 1 relu, 2 sigmoid */
+int dfcsa_bn_act(int dtype, int M, int C, const void* y, const float* scale, const float* shift,
+                 int act, void* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * DFC block elementwise stages (forward).  unet_dfc_sa_res.py:97-114, :36-38.
+ * ---------------------------------------------------------------------------------------- */
+/* local = relu(bn1(y1)); attn = gamma * bilinear(o -> H x W) + act(bn2(y2)), act = relu when
+ * relu != 0 else identity (standalone LightSelfAttention).  y1 may be NULL (no local output).
+ * o: fp32 [B][P][P][C]; gamma: device scalar. */
+int dfcsa_block_local_attn(int dtype, int B, int H, int W, int C, const void* y1, const float* sc1,
+                           const float* sh1, const void* y2, const float* sc2, const float* sh2,
+                           const float* o, int P, const float* gamma, int relu, void* local, void* attn,
+                           void* stream);
+/* fused = g*local + (1-g)*attn, g = sigmoid(bn3(y3)) */
+int dfcsa_gate_fuse(int dtype, int M, int C, const void* y3, const float* sc3, const float* sh3,
+                    const void* local, const void* attn, void* fused, void* stream);
+/* out = relu(bn4(y4)) + res_scale * res */
+int dfcsa_block_out(int dtype, int M, int C, const void* y4, const float* sc4, const float* sh4,
+                    const void* res, const float* res_scale, void* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Backward elementwise + per-channel reductions.  Partial slabs: [ntiles][nsum][C] fp32 with
+ * ntiles = dfcsa_ew_ntiles(M, C); dz = gradient at the BatchNorm output, xh = normalised input.
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_ew_ntiles(int M, int C);
+/* block output: dz4 = dout*(y4*sc4+sh4 > 0); dres = res_scale*dout;
+ * sums: [sum dz4, sum dz4*xh4, sum dout*res] */
+int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, const void* y4, const float* sc4,
+                        const float* sh4, const float* mean4, const float* invstd4, const void* res,
+                        const float* res_scale, void* dz4, void* dres, float* partial, void* stream);
+/* dz = dact * (y*sc+sh > 0); sums [sum dz, sum dz*xh] */
+int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
+                      const float* sh, const float* mean, const float* invstd, void* dz,
+                      float* partial, void* stream);
+/* gate: g = sigmoid(y3*sc3+sh3); dz3 = dfused*(local-attn)*g*(1-g); dlocal += dfused*g;
+ * dattn += dfused*(1-g); sums [sum dz3, sum dz3*xh3] */
+int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,
+                   const float* sh3, const float* mean3, const float* invstd3, const void* local,
+                   const void* attn, void* dlocal, void* dattn, void* dz3, float* partial,
+                   void* stream);
+/* attention entry: dz2 = (dattn + adaptive_pool^T(dpooled)) * (y2*sc2+sh2 > 0) (mask only when
+ * relu != 0); dpooled fp32 [B][P][P][C]; sums [sum dz2, sum dz2*xh2] */
+int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled,
+                         int P, const void* y2, const float* sc2, const float* sh2, const float* mean2,
+                         const float* invstd2, int relu, void* dz2, float* partial, void* stream);
+/* from partial sums: coef[0][c] = mean dz, coef[1][c] = mean dz*xh; dgamma += sum dz*xh,
+ * dbeta += sum dz; if nsum == 3 and extra != null: *extra += sum over c of the third sum. */
+int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count,
+                          float* coef, float* dgamma, float* dbeta, float* extra, void* stream);
+/* dy = gamma*invstd*(dz - coef0 - xh*coef1); partial column sums of dy -> bias_partial
+ * [ntiles][C] (conv bias gradient) */
+int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
+                       const float* invstd, const float* gamma, const float* coef, void* dy,
+                       float* bias_partial, void* stream);
+/* out[c] += sum_t slab[t][c]  (ntiles x C); fp64 accumulation */
+int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream);
+/* per-channel partial sums of an NHWC tensor -> partial [ntiles][C] */
+int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * LightSelfAttention on the pooled map (unet_dfc_sa_res.py:20-39).  Pooled tensors are fp32
+ * [B][N][C], N = P*P (n = pi*P + pj); qkv = [B][N][2*Cq + C] (q | k | v).
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_lsa_pool_splits(int H, int P);
+/* partial[b][n][s][c] = sum over the s-th row slice of window n of act(y2*sc2+sh2) */
+int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                   const float* sh2, int P, int relu, float* partial, void* stream);
+/* pooled = partial sums / window area; qkv = pooled @ wT + b  (wT: [C][2Cq+C] fp32) */
+int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,
+                  const float* bias, float* pooled, float* qkv, void* stream);
+/* A = softmax_rows(q k^T) [B][N][N]; o[n][c] = sum_m A[n][m] v[m][c]  [B][N][C] */
+int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream);
+/* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
+int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, const void* dattn, int P, float* rows,
+                          void* stream);
+/* du[b][pi][pj][c] = sum_h wy(pi,h) rows[b][h][pj][c]; do = gamma*du; gpart[blk] = sum o*du */
+int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const float* o,
+                          const float* gamma, float* dO, float* gpart, int* ngpart, void* stream);
+/* attention core backward -> dqkv [B][N][2Cq+C]; dE scratch [B][N][N] */
+int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv, const float* A, const float* dO,
+                       float* dE, float* dqkv, void* stream);
+/* projection backward: dW[j][c] += sum_bn dqkv[bn][j]*pooled[bn][c] (w layout [2Cq+C][C]);
+ * db[j] += sum_bn dqkv[bn][j]; dpooled[bn][c] = sum_j dqkv[bn][j] * w[j][c] */
+int dfcsa_lsa_proj_bwd(int B, int N, int C, int Cq, const float* dqkv, const float* pooled,
+                       const float* w, float* dWq, float* dWk, float* dWv, float* dbq, float* dbk,
+                       float* dbv, float* dpooled, void* stream);
+/* out += sum of n floats (single workgroup, fp64) */
+int dfcsa_sum_to_scalar(const float* x, int n, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * U-Net plumbing: MaxPool2d(2,2) (unet_dfc_sa_res.py:132-141), input layout conversion,
+ * the bilinear shape fix (:180-199), final 1x1 head (:159, :203).
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_maxpool2_fwd(int dtype, int B, int H, int W, int C, const void* x, void* out, void* stream);
+/* dx += scatter of dout to the first maximum of each 2x2 window (PyTorch tie/NaN order) */
+int dfcsa_maxpool2_bwd(int dtype, int B, int H, int W, int C, const void* x, const void* dout, void* dx,
+                       void* stream);
+/* NCHW fp32 [B][Cin][H][W] -> NHWC dtype [B][H][W][Cpad] (zero channels Cin..Cpad-1) */
+int dfcsa_pack_input(int dtype, int B, int Cin, int H, int W, const float* x, int Cpad, void* out,
+                     void* stream);
+/* NHWC [B][Hi][Wi][C] -> [B][Ho][Wo][C], bilinear, align_corners=False */
+int dfcsa_resize_bilinear(int dtype, int B, int C, int Hi, int Wi, int Ho, int Wo, const void* x,
+                          void* out, void* stream);
+/* dx (fp32 accumulation buffer [B][Hi][Wi][C], must be zeroed) += resize^T(dout) */
+int dfcsa_resize_bilinear_bwd(int dtype, int B, int C, int Hi, int Wi, int Ho, int Wo, const void* dout,
+                              float* dx32, void* stream);
+/* fp32 buffer -> dtype tensor (out = x, or out += x when accumulate) */
+int dfcsa_cast_f32(int dtype, int64_t n, const float* x, void* out, int accumulate, void* stream);
+/* logits NCHW fp32 [B][Cout][HW] = x[M][C] @ w^T + b   (w fp32 [Cout][C]) */
+int dfcsa_head_fwd(int dtype, int B, int HW, int C, int Cout, const void* x, const float* w,
+                   const float* b, float* logits, void* stream);
+/* dx[M][C] = dlogit @ w; partial_w [ntiles][Cout][C], partial_b [ntiles][Cout] */
+int dfcsa_head_bwd(int dtype, int B, int HW, int C, int Cout, const void* x, const float* w,
+                   const float* dlogit, void* dx, float* partial_w, float* partial_b, int* ntiles,
+                   void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Loss and metrics: torch.sigmoid (utils/trainer.py:124) + calculate_metrics('bce_dice')
+ * (utils/metrics.py:211-264 -> BCEDiceLoss :52-78 -> BCELoss + dice_loss :6-24).
+ * stats (fp32[8]): [loss, bce_sum, sum p*t, sum p, sum t, sum b*t, sum b, finite(1/0)],
+ * b = (p > 0.5).
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_sigmoid(int64_t n, const float* x, float* y, void* stream);
+int dfcsa_sigmoid_bwd(int64_t n, const float* y, const float* dy, float* dx, void* stream);
+int dfcsa_bce_dice_partial_count(int64_t n);
+int dfcsa_bce_dice_fwd(int64_t n, const float* p, const float* t, float* partial, float wbce, float wdice,
+                       float* stats, void* stream);
+/* dp = dloss * (wbce*(p-t)/max(p(1-p),1e-12)/n + wdice*d(1-dice)/dp) */
+int dfcsa_bce_dice_bwd(int64_t n, const float* p, const float* t, const float* stats, float wbce,
+                       float wdice, const float* dloss, float* dp, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * clip_grad_norm_(max_norm) + SGD(momentum, weight_decay) over one flat fp32 parameter
+ * buffer (utils/trainer.py:149-151, train.py:73-78).  grad_scale multiplies the gradient
+ * first (1/world_size after an all-reduce sum).  If *skip_if_nonfinite is not finite the step
+ * is skipped on the device (the reference's NaN-loss `continue`, trainer.py:134-139).
+ * *mom_init == 0 -> momentum buffer = d (torch's first step), then set to 1.
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_sumsq_nparts(int64_t n);
+int dfcsa_sumsq_partial(int64_t n, const float* g, float* partial, void* stream);
+int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const float* partial, int nparts,
+                   float max_norm, float grad_scale, float lr, float momentum, float weight_decay,
+                   int* mom_init, const float* skip_if_nonfinite, float* norm_out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Profiling hook: when enabled for a kernel class, every launch of that class is bracketed by
+ * hipEvents on its own stream; dfcsa_prof_read returns the summed elapsed milliseconds and
+ * the launch count since the last reset (synchronises on the recorded events).
+ * ---------------------------------------------------------------------------------------- */
+#define DFCSA_PROF_CONV_GEMM 1
+#define DFCSA_PROF_WGRAD 2
+int dfcsa_prof_enable(int kernel_class, int enable);
+int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, double* flops);
+
+const char* dfcsa_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* DFCSA_H_ */

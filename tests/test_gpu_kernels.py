@@ -1,0 +1,211 @@
+"""Kernel-level numerics on the MI355X: each libdfcsa GEMM/kernel against a plain PyTorch
+fp32 CPU reference of the same op.  fp32 mode must match to ~1e-5 relative; bf16 mode to the
+bf16 input rounding (operands are rounded to bf16 in the reference too)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+dfcsa_ops = pytest.importorskip("dfcsa.ops")
+from dfcsa import ops  # noqa: E402
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def nhwc(x, dtype):
+    return x.permute(0, 2, 3, 1).contiguous().to("cuda", dtype)
+
+
+def nchw(y):
+    return y.permute(0, 3, 1, 2).float().cpu()
+
+
+def q(x, dtype):  # round to the compute dtype (reference sees the same operands)
+    return x.to(dtype).float()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (1, 64, 2, 64, 14, 14), (2, 16, 2, 136, 5, 11)])
+def test_conv3x3_multisource(dtype, tol, B, Cs, nsrc, C, H, W):
+    torch.manual_seed(0)
+    xs = [q(torch.randn(B, Cs, H, W), dtype) for _ in range(nsrc)]
+    w = q(torch.randn(C, nsrc * Cs, 3, 3) * 0.1, dtype)
+    b = torch.randn(C)
+    ref = F.conv2d(torch.cat(xs, 1), w, b, padding=1)
+    Kp = ops.rup(9 * nsrc * Cs, ops.KALIGN)
+    wp = ops.pack_conv_w(dtype, w.cuda(), nsrc * Cs, Kp)
+    y = torch.empty((B, H, W, C), dtype=dtype, device="cuda")
+    M = B * H * W
+    stats = torch.empty(ops.ntiles_gemm(M) * 2 * C, device="cuda")
+    xh = [nhwc(x, dtype) for x in xs]
+    segs = [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xh]
+    ops.conv_gemm(dtype, segs, Cs, (B, H, W), (H, W), wp, Kp, C, [y], C, bias=b.cuda(), stats=stats)
+    torch.cuda.synchronize()
+    assert rel(nchw(y), ref) < tol
+    st = stats.view(-1, 2, C).sum(0).cpu()
+    acc = ref - b.view(1, -1, 1, 1)
+    assert rel(st[0], acc.sum((0, 2, 3))) < max(tol, 1e-5) * 10
+    assert rel(st[1], (acc * acc).sum((0, 2, 3))) < max(tol, 1e-5) * 10
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+def test_conv1x1_three_dests_accumulate(dtype, tol):
+    torch.manual_seed(1)
+    B, H, W, Cin, C = 2, 6, 10, 24, 16
+    x = q(torch.randn(B, Cin, H, W), dtype)
+    w = q(torch.randn(3 * C, Cin, 1, 1) * 0.2, dtype)
+    ref = F.conv2d(x, w)
+    base = [q(torch.randn(B, C, H, W), dtype) for _ in range(3)]
+    Kp = ops.rup(Cin, ops.KALIGN)
+    wp = ops.pack_conv_w(dtype, w.cuda(), Cin, Kp)
+    dests = [nhwc(t, dtype) for t in base]
+    ops.conv_gemm(dtype, [(nhwc(x, dtype), 0, 0)], Cin, (B, H, W), (H, W), wp, Kp, 3 * C, dests, C,
+                  accumulate=True)
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert rel(nchw(dests[i]), ref[:, i * C:(i + 1) * C] + base[i]) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+def test_conv_transpose_fwd_bwd(dtype, tol):
+    from dfcsa.functions import ConvTranspose2x2
+    torch.manual_seed(2)
+    B, h, w, Cin, Cout = 2, 5, 7, 32, 16
+    mod = torch.nn.ConvTranspose2d(Cin, Cout, 2, 2)
+    with torch.no_grad():
+        mod.weight.copy_(q(mod.weight, dtype))
+    x = q(torch.randn(B, Cin, h, w), dtype)
+    xr = x.clone().requires_grad_(True)
+    ref = mod(xr)
+    g = q(torch.randn_like(ref), dtype)
+    ref.backward(g)
+    modg = torch.nn.ConvTranspose2d(Cin, Cout, 2, 2).cuda()
+    with torch.no_grad():
+        modg.weight.copy_(mod.weight)
+        modg.bias.copy_(mod.bias)
+    xh = nhwc(x, dtype).requires_grad_(True)
+    y = ConvTranspose2x2.apply(xh, modg, dtype, *modg.parameters())
+    y.backward(nhwc(g, dtype))
+    torch.cuda.synchronize()
+    assert rel(nchw(y), ref) < tol
+    assert rel(nchw(xh.grad), xr.grad) < tol
+    assert rel(modg.weight.grad, mod.weight.grad) < tol
+    assert rel(modg.bias.grad, mod.bias.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (3, 64, 2, 64, 14, 14), (2, 32, 1, 136, 20, 20)])
+def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W):
+    torch.manual_seed(3)
+    xs = [q(torch.randn(B, Cs, H, W), dtype) for _ in range(nsrc)]
+    x = torch.cat(xs, 1).requires_grad_(True)
+    w = torch.randn(C, nsrc * Cs, 3, 3, requires_grad=True)
+    g = q(torch.randn(B, C, H, W), dtype)
+    F.conv2d(x, w, padding=1).backward(g)
+    xh = [nhwc(t, dtype) for t in xs]
+    segs = [(t, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for t in xh]
+    gw = torch.zeros(C, nsrc * Cs, 3, 3, device="cuda")
+    ops.conv_wgrad_into(dtype, [nhwc(g, dtype)], C, segs, Cs, (B, H, W), (H, W), [gw], 9, nsrc * Cs, nsrc * Cs)
+    torch.cuda.synchronize()
+    assert rel(gw, w.grad) < tol
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+def test_dgrad_3x3_plus_1x1(dtype, tol):
+    """the fused input-gradient GEMM: 3x3 dgrad + two 1x1 dgrads into two destination sources"""
+    torch.manual_seed(4)
+    B, H, W, Cs, C = 2, 11, 9, 16, 24
+    x = torch.randn(B, 2 * Cs, H, W, requires_grad=True)
+    w1 = q(torch.randn(C, 2 * Cs, 3, 3) * 0.1, dtype)
+    w2 = q(torch.randn(C, 2 * Cs, 1, 1) * 0.1, dtype)
+    w3 = q(torch.randn(C, 2 * Cs, 1, 1) * 0.1, dtype)
+    g1, g2, g3 = (q(torch.randn(B, C, H, W), dtype) for _ in range(3))
+    (F.conv2d(x, w1, padding=1) * g1 + F.conv2d(x, w2) * g2 + F.conv2d(x, w3) * g3).sum().backward()
+    Kx = ops.rup(11 * C, ops.KALIGN)
+    Wdx = torch.zeros((2 * Cs, Kx), dtype=dtype, device="cuda")
+    ops.pack_conv_w_t(dtype, w1.cuda(), Kx, Wdx, 0)
+    ops.pack_conv_w_t(dtype, w2.cuda(), Kx, Wdx, 9 * C)
+    ops.pack_conv_w_t(dtype, w3.cuda(), Kx, Wdx, 10 * C)
+    d1, d2, d3 = (nhwc(t, dtype) for t in (g1, g2, g3))
+    segs = [(d1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(d2, 0, 0), (d3, 0, 0)]
+    dx = [torch.empty((B, H, W, Cs), dtype=dtype, device="cuda") for _ in range(2)]
+    ops.conv_gemm(dtype, segs, C, (B, H, W), (H, W), Wdx, Kx, 2 * Cs, dx, Cs)
+    torch.cuda.synchronize()
+    assert rel(torch.cat([nchw(dx[0]), nchw(dx[1])], 1), x.grad) < tol
+
+
+def test_maxpool_ties_and_odd_sizes():
+    from dfcsa.functions import MaxPool2x2
+    torch.manual_seed(5)
+    x = torch.randint(-2, 3, (2, 16, 9, 7)).float()  # many ties
+    xr = x.clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 2, 2)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    xh = nhwc(x, torch.float32).requires_grad_(True)
+    y = MaxPool2x2.apply(xh, torch.float32)
+    y.backward(nhwc(g, torch.float32))
+    assert torch.equal(nchw(y), ref)
+    assert torch.equal(nchw(xh.grad), xr.grad)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
+def test_resize_bilinear(dtype, tol):
+    from dfcsa.functions import ResizeBilinear
+    torch.manual_seed(6)
+    x = q(torch.randn(2, 8, 4, 5), dtype)
+    xr = x.clone().requires_grad_(True)
+    ref = F.interpolate(xr, size=(9, 11), mode="bilinear", align_corners=False)
+    g = q(torch.randn_like(ref), dtype)
+    ref.backward(g)
+    xh = nhwc(x, dtype).requires_grad_(True)
+    y = ResizeBilinear.apply(xh, (9, 11), dtype)
+    y.backward(nhwc(g, dtype))
+    assert rel(nchw(y), ref) < tol
+    assert rel(nchw(xh.grad), xr.grad) < tol
+
+
+def test_loss_and_metrics_kernel(golden):
+    from dfcsa.loss import bce_dice, metrics_from_stats
+    fx = golden("metrics_bce_dice.npz")
+    for c in sorted({k.split(".")[0] for k in fx}):
+        p = torch.tensor(fx[c + ".p"], device="cuda", requires_grad=True)
+        t = torch.tensor(fx[c + ".t"], device="cuda")
+        loss, stats = bce_dice(p, t, float(fx[c + ".wbce"]), float(fx[c + ".wdice"]))
+        loss.backward()
+        iou, dice = metrics_from_stats(stats)
+        assert abs(loss.item() - float(fx[c + ".loss"])) < 1e-5 * max(1.0, abs(float(fx[c + ".loss"])))
+        assert abs(iou - float(fx[c + ".iou"])) < 1e-9 and abs(dice - float(fx[c + ".dice"])) < 1e-9
+        ref = torch.tensor(fx[c + ".dp"])
+        assert rel(p.grad, ref) < 1e-5
+
+
+def test_clip_sgd_matches_torch():
+    from dfcsa.flat import FlatParams
+    from dfcsa.optim import FusedSGD
+    torch.manual_seed(7)
+    ref = torch.nn.Sequential(torch.nn.Linear(37, 50), torch.nn.Linear(50, 3))
+    mine = torch.nn.Sequential(torch.nn.Linear(37, 50), torch.nn.Linear(50, 3)).cuda()
+    mine.load_state_dict(ref.state_dict())
+    flat = FlatParams(mine)
+    opt_r = torch.optim.SGD(ref.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt_m = FusedSGD(mine.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    for step in range(3):
+        gs = [torch.randn_like(p) * (3.0 if step == 1 else 0.01) for p in ref.parameters()]
+        for p, g in zip(ref.parameters(), gs):
+            p.grad = g.clone()
+        nr = torch.nn.utils.clip_grad_norm_(ref.parameters(), max_norm=1.0)
+        opt_r.step()
+        opt_m.zero_grad()
+        for p, g in zip(mine.parameters(), gs):
+            p.grad.copy_(g)
+        opt_m.step(max_norm=1.0)
+        torch.cuda.synchronize()
+        assert abs(opt_m.last_norm.item() - nr.item()) < 1e-5 * nr.item()
+        for pr, pm in zip(ref.parameters(), mine.parameters()):
+            assert rel(pm, pr) < 1e-6
+    assert flat.valid()

@@ -1,0 +1,186 @@
+"""Block- and model-level parity on the MI355X against the golden fixtures produced by the
+reference (tests/golden/make_golden.py) and against the CPU oracle.
+
+fp32 compute mode: logits / loss / metrics to 1e-4 (north star), parameter gradients to 1e-3
+relative norm per tensor (BatchNorm-preceded conv biases have ~zero true gradient and are
+compared in absolute terms against the weight-gradient scale).
+bf16 compute mode: logits and loss within 1e-2 / 2e-2 relative (north star: 1e-2 bf16).
+"""
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+LP = {"bce_weight": 0.5, "dice_weight": 0.5}  # the DFC yamls' (ignored) keys
+
+
+def T(a, dev="cuda"):
+    return torch.from_numpy(np.asarray(a)).to(dev)
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(np.asarray(b) if not torch.is_tensor(b) else b).detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def sd_from(fx, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in fx.items() if k.startswith(prefix)}
+
+
+def check_grads(named, fx, prefix="grad.", tol=1e-3):
+    worst = []
+    for n, p in named:
+        ref = fx.get(prefix + n)
+        if ref is None:
+            continue
+        g = p.grad
+        assert g is not None, n
+        if n.endswith("conv_branch.0.bias") or n.endswith("attn_branch.0.bias") or n.endswith("gate.0.bias") \
+                or n.endswith("fusion_conv.0.bias") or n.endswith("key_conv.bias"):
+            # true gradient is 0 (a BatchNorm follows / softmax is shift-invariant over keys);
+            # both sides hold rounding noise
+            scale = max(np.abs(fx[prefix + n[:-4] + "weight"]).max(), 1e-6)
+            assert np.abs(g.double().cpu().numpy() - ref).max() < tol * scale, n
+            continue
+        r = rel(g, ref)
+        worst.append((r, n))
+        assert r < tol, (n, r)
+    return sorted(worst)[-3:]
+
+
+# ----------------------------------------------------------------------------- LSA
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "lsa_*.npz"))), ids=os.path.basename)
+def test_lsa_fp32(path):
+    from models.unet_dfc_sa_res import LightSelfAttention
+    fx = dict(np.load(path))
+    P = int(os.path.basename(path).split("_P")[1].split(".")[0])
+    C = fx["x"].shape[1]
+    m = LightSelfAttention(C, pool_size=P, ablation_on_qk_channels=8).cuda()
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd.")})
+    m.compute_dtype = torch.float32
+    x = T(fx["x"]).requires_grad_(True)
+    y = m(x)
+    y.backward(T(fx["g"]))
+    assert rel(y, fx["y"]) < 1e-5
+    assert rel(x.grad, fx["dx"]) < 1e-5
+    check_grads(m.named_parameters(), fx, tol=1e-4)
+
+
+# ----------------------------------------------------------------------------- block
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "block_*.npz"))), ids=os.path.basename)
+def test_block_fp32(path):
+    from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock
+    fx = dict(np.load(path))
+    name = os.path.basename(path)
+    cin, cout = int(name.split("_")[1].split("to")[0]), int(name.split("to")[1].split("_")[0])
+    P = int(name.split("_P")[1].split(".")[0])
+    blk = DynamicFusionConvAttnBlock(cin, cout, pool_size=P).cuda()
+    blk.load_state_dict(sd_from(fx, "sd0."))
+    blk.compute_dtype = torch.float32
+    blk.train()
+    x = T(fx["x"]).requires_grad_(True)
+    y = blk(x)
+    y.backward(T(fx["g"]))
+    assert rel(y, fx["y"]) < 1e-5
+    assert rel(x.grad, fx["dx"]) < 1e-4
+    check_grads(blk.named_parameters(), fx, tol=1e-3)
+    sd1 = sd_from(fx, "sd1.")
+    for k, v in blk.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            assert rel(v.float(), sd1[k].float()) < 1e-5, k
+
+
+# ----------------------------------------------------------------------------- model
+def make_model(precision, P=4):
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    base = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    m = UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=P, ablation_on_qk_channels=8, precision=precision)
+    m.load_state_dict(sd_from(base, "sd0."))
+    return m.cuda(), base
+
+
+def test_model_two_train_steps_fp32():
+    """Two full Trainer steps (fwd, sigmoid, bce_dice, backward, clip 1.0, SGD) == reference."""
+    from dfcsa.loss import metrics_from_stats, sigmoid
+    from dfcsa.optim import FusedSGD
+    from utils.metrics import calculate_metrics_device
+    model, fx = make_model("fp32")
+    model.train()
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    for step in (1, 2):
+        opt.zero_grad()
+        logits = model(T(fx[f"x{step}"]))
+        met = calculate_metrics_device(sigmoid(logits), T(fx[f"t{step}"]), "bce_dice", LP)
+        met["loss"].backward()
+        if step == 1:
+            grads_pre = None
+        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        torch.cuda.synchronize()
+        assert rel(logits, fx[f"logits{step}"]) < 1e-4
+        assert abs(met["loss"].item() - float(fx[f"loss{step}"])) < 1e-4 * abs(float(fx[f"loss{step}"]))
+        iou, dice = metrics_from_stats(met["stats"])
+        assert abs(iou - float(fx[f"iou{step}"])) < 1e-6 and abs(dice - float(fx[f"dice{step}"])) < 1e-6
+        assert abs(opt.last_norm.item() - float(fx[f"norm{step}"])) < 1e-3 * float(fx[f"norm{step}"])
+        if step == 1:
+            check_grads(model.named_parameters(), fx, prefix="step1.grad.", tol=2e-3)
+            sd = model.state_dict()
+            for k, v in fx.items():
+                if k.startswith("bn1."):
+                    assert rel(sd[k[4:]].float(), torch.from_numpy(np.asarray(v)).float()) < 1e-4, k
+    sd = model.state_dict()
+    for k, v in sd_from(fx, "sd2.").items():
+        assert rel(sd[k].float(), v.float()) < 1e-4, k
+
+
+@pytest.mark.parametrize("name,P", [("model_p8.npz", 8), ("model_odd36.npz", 4)])
+def test_model_grads_fp32(name, P):
+    from dfcsa.loss import sigmoid
+    from utils.metrics import calculate_metrics
+    model, base = make_model("fp32", P)
+    fx = dict(np.load(os.path.join(GOLDEN, name)))
+    x = T(fx["x"] if "x" in fx else base["x1"])
+    t = T(fx["t"] if "t" in fx else base["t1"])
+    model.train()
+    logits = model(x)
+    met = calculate_metrics(sigmoid(logits), t, "bce_dice", LP)
+    met["loss"].backward()
+    assert rel(logits, fx["logits"]) < 1e-4
+    assert abs(met["loss"].item() - float(fx["loss"])) < 1e-4 * abs(float(fx["loss"]))
+    check_grads(model.named_parameters(), fx, tol=2e-3)
+
+
+def test_model_eval_fp32():
+    model, base = make_model("fp32")
+    fx = dict(np.load(os.path.join(GOLDEN, "model_eval.npz")))
+    sd = model.state_dict()
+    sd.update(sd_from(fx, "buf."))
+    model.load_state_dict(sd)
+    model.eval()
+    with torch.no_grad():
+        y = model(T(fx["x"]))
+    assert rel(y, fx["logits"]) < 1e-4
+
+
+def test_model_bf16_vs_reference():
+    """bf16 compute (fp32 master weights/stats): logits and loss near the fp32 reference."""
+    from dfcsa.loss import sigmoid
+    from utils.metrics import calculate_metrics
+    model, fx = make_model("bf16")
+    model.train()
+    logits = model(T(fx["x1"]))
+    met = calculate_metrics(sigmoid(logits), T(fx["t1"]), "bce_dice", LP)
+    met["loss"].backward()
+    assert rel(logits, fx["logits1"]) < 2e-2
+    assert abs(met["loss"].item() - float(fx["loss1"])) < 1e-2 * abs(float(fx["loss1"]))
+    # gradients: direction agrees (bf16 activations through 9 BatchNorm'd blocks)
+    g = torch.cat([p.grad.flatten().double().cpu() for _, p in model.named_parameters()])
+    r = torch.cat([torch.from_numpy(fx["step1.grad." + n]).flatten().double() for n, _ in model.named_parameters()])
+    # fixture grads are post-clip; compare directions
+    cos = (g @ r / (g.norm() * r.norm())).item()
+    assert cos > 0.99, cos
