@@ -1,0 +1,203 @@
+"""Benchmark: DFC-SA-Res U-Net training throughput on MI355X (BASELINE.json metric).
+
+Workload (BASELINE.json configs[1], config_dfc-sa-res-block-p4.yaml overlaid): DFC-SA-Res,
+features [64, 128, 256, 512], pool_size 4, 3x224x224 -> 1x224x224, bf16 activations with fp32
+master weights/statistics, 16 images per GPU.  One step = the full Trainer step
+(utils/trainer.py:115-151): forward, sigmoid, BCE+Dice loss + IoU/Dice counts, backward,
+[bucketed RCCL all-reduce for N > 1], clip_grad_norm_(1.0) + SGD(0.01, 0.9, 1e-4).
+Synthetic data: the GLOBAL batch (16 x N images, N(0,1); masks Bernoulli(0.5)) is generated
+from fixed seeds and sharded by rank, resident in HBM before timing.
+
+Launch: `python bench.py` (N=1) or, for N > 1, `python -m torch.distributed.run --nproc-per-node N
+... bench.py --gpus N`.  Rank 0 prints ONE JSON line.  The line carries:
+  roofline      the dominant kernel class (implicit-GEMM conv or weight-gradient GEMM): its
+                algorithmic FLOPs (2*M*N*K per launch) / its summed launch time, timed with HIP
+                events on its own stream inside the timed region, vs the 2.5 PFLOP/s dense bf16
+                MFMA peak;
+  cpu_baseline  the CPU oracle (oracle/dfcsa_oracle.py, fp32 eager PyTorch = the reference
+                algorithm) timed on this host on a bounded sample (rank 0, N = 1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "dfc-sa-unet_amd")]
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip-level parameters)
+MFMA_F32_PEAK_TFLOPS = 157.3
+HBM_PEAK_GBS = 8000.0
+FWD_BWD_GFLOP_PER_IMG = 201.66   # SURVEY.md section 8d (torch.utils.flop_counter, P=4, 224^2)
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seconds_budget=25.0):
+    """Time the CPU oracle's full train step (fp32 eager PyTorch, same algorithm) on B=2 images
+    of the same workload; threads = this process's CPU share (<= 16)."""
+    import numpy as np  # noqa: F401
+    from oracle import dfcsa_oracle as O
+    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    torch.set_num_threads(threads)
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    torch.manual_seed(0)
+    ref = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4)
+    sd = {k: v.detach().clone() for k, v in ref.state_dict().items()}
+    g = torch.Generator().manual_seed(1234)
+    B = 2
+    x = torch.randn(B, 3, 224, 224, generator=g)
+    t = (torch.rand(B, 1, 224, 224, generator=g) > 0.5).float()
+    sd, bufs, _ = O.train_step(sd, {}, x, t, 4)   # warm-up step
+    n, t0 = 0, time.perf_counter()
+    while True:
+        sd, bufs, _ = O.train_step(sd, bufs, x, t, 4)
+        n += 1
+        el = time.perf_counter() - t0
+        if el > seconds_budget / 2 or n >= 3:
+            break
+    return {"value": round(n * B / el, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} timed train steps (after 1 warm-up) of B={B} 3x224x224 images, "
+                      f"oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch", type=int, default=16, help="images per GPU")
+    ap.add_argument("--img", type=int, default=224)
+    ap.add_argument("--pool", type=int, default=4)
+    ap.add_argument("--precision", default="bf16")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-kernel-timing", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    import dfcsa._lib as L
+    from dfcsa.ddp import GradBucketReducer, shard_rows
+    from dfcsa.loss import bce_dice, sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.model_factory import ModelFactory
+
+    cfg = {"model": {"name": "DFC-SA-Res-Block", "in_channels": 3, "out_channels": 1,
+                     "features": [64, 128, 256, 512], "pool_size": args.pool, "ablation_on_qk_channels": 8,
+                     "precision": args.precision},
+           "training": {"learning_rate": 0.01, "momentum": 0.9, "weight_decay": 1e-4}}
+    torch.manual_seed(0)
+    model = ModelFactory.get_model(cfg).to(dev).train()
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+
+    B, S = args.batch, args.img
+    gb = B * world
+    g = torch.Generator().manual_seed(1234)
+    xg = torch.randn(gb, 3, S, S, generator=g)
+    g2 = torch.Generator().manual_seed(1235)
+    tg = (torch.rand(gb, 1, S, S, generator=g2) > 0.5).float()
+    lo, hi = shard_rows(gb, rank, world)
+    x = xg[lo:hi].to(dev)
+    t = tg[lo:hi].to(dev)
+    del xg, tg
+
+    model(x[:1])  # materialise the flat parameter/gradient storage before the reducer/optimizer
+    reducer = GradBucketReducer(model) if world > 1 else None
+    scale = reducer.grad_scale if reducer else 1.0
+
+    def step():
+        opt.zero_grad()
+        p = sigmoid(model(x))
+        loss, stats = bce_dice(p, t, 1.0, 1.0)   # 'bce_dice' with the yaml's (ignored) weight keys
+        if reducer:
+            reducer.start()
+        loss.backward()
+        if reducer:
+            reducer.finish()
+        opt.step(max_norm=1.0, grad_scale=scale, skip_if_nonfinite=loss)
+        return stats
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        stats = step()
+    torch.cuda.synchronize()
+    log(f"[rank {rank}] warm-up done; loss {stats[0].item():.4f}")
+
+    timing = not args.no_kernel_timing
+    if timing:
+        L.LIB.dfcsa_prof_enable(1, 1)
+        L.LIB.dfcsa_prof_enable(2, 1)
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        stats = step()
+    torch.cuda.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        te = torch.tensor([el], device=dev, dtype=torch.float64)
+        dist.all_reduce(te, op=dist.ReduceOp.MAX)
+        el = te.item()
+    final_loss = stats[0].item()
+
+    roof = None
+    if timing:
+        import ctypes
+        cls = {}
+        for c, name in ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad)"), (2, "conv_wgrad (weight-gradient GEMM)")):
+            ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
+            L.LIB.dfcsa_prof_read(c, ctypes.addressof(ms), ctypes.addressof(n), ctypes.addressof(fl))
+            cls[c] = (name, ms.value, n.value, fl.value)
+            L.LIB.dfcsa_prof_enable(c, 0)
+        dom = max(cls.values(), key=lambda v: v[1])
+        name, ms, n, fl = dom
+        peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
+        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(ach / peak, 4), "traffic": None,
+                "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
+                "share_of_step": round(ms / (el * 1e3), 3),
+                "other_class": {c[0]: {"ms_per_step": round(c[1] / args.steps, 3),
+                                       "tflops": round(c[3] / (c[1] * 1e-3) / 1e12, 2) if c[1] > 0 else 0}
+                                for c in cls.values() if c is not dom}}
+
+    imgs = args.steps * B * world
+    value = imgs / el
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        log("[rank 0] timing the CPU oracle baseline ...")
+        cpu = cpu_baseline()
+    if rank == 0:
+        out = {"metric": "training images/sec (fwd+bwd) 3x224x224 DFC-SA-Res", "value": round(value, 2),
+               "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+               "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
+               "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
+               "config": {"workload": f"DFC-SA-Res P={args.pool} features 64..512 {S}x{S} train step",
+                          "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
+                          "parallelism": f"dp{world}", "final_loss": round(final_loss, 5),
+                          "model_tflops": round(value * FWD_BWD_GFLOP_PER_IMG / 1e3, 2)},
+               "roofline": roof, "cpu_baseline": cpu}
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -307,6 +307,7 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
   hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_CONV_GEMM, st, 2.0 * a.M * a.N * a.K);
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
 }
 

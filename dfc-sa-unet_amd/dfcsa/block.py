@@ -21,6 +21,7 @@ import torch.nn as nn
 
 from . import ops
 from ._lib import call
+from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 
 
@@ -343,5 +344,6 @@ class DFCBlockFunction(torch.autograd.Function):
         need_dx = any(ctx.needs_input_grad[4:4 + ctx.nsrc])
         dxs = block_backward(ctx.blk, ctx.saved, dout, need_dx, ctx.dtype)
         ctx.saved = None
+        notify_grads_ready(ctx.blk)
         grads = list(dxs) if dxs is not None else [None] * ctx.nsrc
         return (None, None, None, None, *grads, *([None] * ctx.nparams))

@@ -1,0 +1,98 @@
+"""Data parallelism for the DFC-SA-Res step: one process per GPU, gradients all-reduced over
+torch.distributed ('nccl' backend = RCCL on ROCm, xGMI between the MI355X GPUs of a node).
+
+The reference has no parallelism (single device, train.py:56-59); this is the build's own
+design:
+  * the minibatch is sharded over ranks; BatchNorm statistics and the batch Dice loss stay
+    per-replica (standard DDP semantics -- the multi-GPU step equals the mean of per-shard
+    reference gradients, which is what tests/golden/ddp_shards.npz pins);
+  * all gradients live in one flat fp32 buffer (dfcsa.flat), cut into contiguous buckets from
+    its END, because backward produces gradients from the last layer to the first;
+  * every module backward (DFC block, transposed conv, head) reports when its parameters'
+    gradients are final; a bucket whose modules are all final is all-reduced immediately with
+    async_op=True, so RCCL runs on its own stream underneath the remaining backward kernels;
+  * ``finish()`` makes the compute stream wait for every bucket (no host synchronisation);
+    the optimizer then applies 1/world_size inside the fused clip+SGD pass.
+"""
+import torch
+import torch.distributed as dist
+
+
+class GradBucketReducer:
+    def __init__(self, model, bucket_mb=32.0, group=None):
+        self.model = model
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.flat = model.flat_params()
+        units = model.grad_units()  # [(module, lo, hi)] in flat-buffer order
+        self.unit_of = {}
+        self.buckets = []           # [(lo, hi, n_units)]
+        cap = int(bucket_mb * (1 << 20) / 4)
+        cur, lo, hi = [], None, None
+        for mod, a, b in reversed(units):
+            if cur and (hi - a) > cap:
+                self.buckets.append([lo, hi, cur])
+                cur = []
+            if not cur:
+                hi = b
+            lo = a
+            cur.append(mod)
+        if cur:
+            self.buckets.append([lo, hi, cur])
+        for i, (_, _, mods) in enumerate(self.buckets):
+            for m in mods:
+                self.unit_of[id(m)] = i
+                m._dfcsa_reducer = self
+        self._pending = None
+        self._works = []
+
+    def start(self):
+        """Arm for one backward pass."""
+        self._pending = [len(b[2]) for b in self.buckets]
+        self._works = []
+        self._launched = [False] * len(self.buckets)
+
+    def unit_ready(self, module):
+        if self._pending is None:
+            return
+        i = self.unit_of.get(id(module))
+        if i is None:
+            return
+        self._pending[i] -= 1
+        # launch in bucket order only (every rank issues the same collective sequence)
+        j = len(self._works)
+        while j < len(self.buckets) and self._pending[j] == 0:
+            lo, hi, _ = self.buckets[j]
+            self._works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+            j += 1
+
+    def finish(self):
+        """Ensure every bucket has been reduced (launch stragglers), make the current stream wait."""
+        if self._pending is None:
+            return
+        for j in range(len(self._works), len(self.buckets)):
+            lo, hi, _ = self.buckets[j]
+            self._works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
+                                               async_op=True))
+        for w in self._works:
+            w.wait()
+        self._pending = None
+
+    @property
+    def grad_scale(self):
+        return 1.0 / self.world
+
+
+def notify_grads_ready(module):
+    r = getattr(module, "_dfcsa_reducer", None)
+    if r is not None:
+        r.unit_ready(module)
+
+
+def shard_rows(n, rank, world):
+    """Rows [lo, hi) of a global batch of n owned by `rank` (global batch split evenly)."""
+    if n % world:
+        raise ValueError(f"global batch {n} is not divisible by world size {world}")
+    per = n // world
+    return rank * per, (rank + 1) * per

@@ -11,6 +11,7 @@ import torch
 from . import ops
 from ._lib import call
 from .block import grad_of
+from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 
 
@@ -93,6 +94,7 @@ class ConvTranspose2x2(torch.autograd.Function):
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
             ops.conv_gemm(dtype, segs, Cout, (B, h, w), (2 * h, 2 * w), ctx.Wb, ctx.Kb, Cin, [dx], Cin, stride=2)
+        notify_grads_ready(mod)
         return (dx, None, None, *([None] * ctx.np))
 
 
@@ -144,4 +146,5 @@ class Head1x1(torch.autograd.Function):
              P(pb), None, stream())
         call("dfcsa_slab_colsum", P(pw), nt.value, Cout * C, P(grad_of(mod.weight)), stream())
         call("dfcsa_slab_colsum", P(pb), nt.value, Cout, P(grad_of(mod.bias)), stream())
+        notify_grads_ready(mod)
         return (dx if ctx.needs_input_grad[0] else None, None, None, *([None] * ctx.np))

@@ -146,6 +146,20 @@ class UNetDFCSA(nn.Module):
             self._flat = FlatParams(self)
         return self._flat
 
+    def grad_units(self):
+        """[(module, lo, hi)]: the modules whose backward finalises a contiguous range of the flat
+        gradient buffer, in buffer order (used by the data-parallel bucket reducer)."""
+        from dfcsa.flat import ALIGN
+        flat = self.flat_params()
+        index = {id(p): i for i, p in enumerate(flat.params)}
+        units = []
+        for mod in (self.down1, self.down2, self.down3, self.down4, self.bottleneck, self.up4, self.up_conv4,
+                    self.up3, self.up_conv3, self.up2, self.up_conv2, self.up1, self.up_conv1, self.final_conv):
+            ps = list(mod.parameters())
+            first, last = index[id(ps[0])], index[id(ps[-1])]
+            units.append((mod, flat.offsets[first], flat.offsets[last] + rup(ps[-1].numel(), ALIGN)))
+        return units
+
     # -------------------------------------------------------------- forward
     def forward(self, x):
         """x: [B, in_channels, H, W] float -> logits [B, out_channels, H, W] fp32 (no sigmoid)."""
