@@ -400,6 +400,24 @@ __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restri
   }
 }
 
+// dst[g][j] = sum over rows of group g of src[t][j]; grid (ceil(rowlen/256), G)
+__global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restrict__ src, int T, int rowlen,
+                                                          float* __restrict__ dst, int per) {
+  const int j = blockIdx.x * 256 + threadIdx.x, g = blockIdx.y;
+  if (j >= rowlen) return;
+  const int t0 = g * per, t1 = min(T, t0 + per);
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  int t = t0;
+  for (; t + 3 < t1; t += 4) {
+    s0 += src[(size_t)t * rowlen + j];
+    s1 += src[(size_t)(t + 1) * rowlen + j];
+    s2 += src[(size_t)(t + 2) * rowlen + j];
+    s3 += src[(size_t)(t + 3) * rowlen + j];
+  }
+  for (; t < t1; ++t) s0 += src[(size_t)t * rowlen + j];
+  dst[(size_t)g * rowlen + j] = (s0 + s1) + (s2 + s3);
+}
+
 __global__ void __launch_bounds__(256) sum_scalar_kernel(const float* x, int n, float* out) {
   __shared__ double r[256];
   double s = 0;
@@ -569,6 +587,15 @@ extern "C" int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* 
   EwArgs a = zargs(M, C);
   a.a0 = x; a.partial = partial;
   return launch_red<EW_CHANNEL_SUM>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_rows_reduce(const float* src, int T, int rowlen, float* dst, int G, void* stream) {
+  if (T <= 0 || rowlen <= 0 || G <= 0) return DFCSA_EINVAL;
+  const int per = (T + G - 1) / G;
+  hipLaunchKernelGGL(rows_reduce_kernel, dim3((rowlen + 255) / 256, G), dim3(256), 0, (hipStream_t)stream, src, T,
+                     rowlen, dst, per);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_sum_to_scalar(const float* x, int n, float* out, void* stream) {

@@ -110,6 +110,20 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
   }
 }
 
+// grid (N, B): pooled[b][n][c] = sum of the S partial slices / window area
+__global__ void __launch_bounds__(256) lsa_pooled_kernel(int H, int W, int C, int P, int S,
+                                                         const float* __restrict__ partial, float* __restrict__ pooled) {
+  const int n = blockIdx.x, b = blockIdx.y, N = P * P;
+  const int pi = n / P, pj = n - pi * P;
+  const float inv = 1.f / (float)((win_hi(pi, H, P) - win_lo(pi, H, P)) * (win_hi(pj, W, P) - win_lo(pj, W, P)));
+  const float* p = partial + (((size_t)b * N + n) * S) * C;
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += p[(size_t)k * C + c];
+    pooled[((size_t)b * N + n) * C + c] = s * inv;
+  }
+}
+
 // grid (ceil(J/256), ceil(N/16), B); J = 2Cq + C
 __global__ void __launch_bounds__(256) lsa_qkv_kernel(int H, int W, int C, int Cq, int P, int S,
                                                       const float* __restrict__ partial,
@@ -368,6 +382,14 @@ extern "C" int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void*
   else
     hipLaunchKernelGGL(lsa_pool_kernel<float>, grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2, P, S,
                        relu, partial);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_pooled(int B, int H, int W, int C, int P, const float* partial, float* pooled,
+                                void* stream) {
+  hipLaunchKernelGGL(lsa_pooled_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, W, C, P,
+                     pool_splits(H, P), partial, pooled);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -242,6 +242,118 @@ __global__ void __launch_bounds__(256) head_bwd_kernel(int B, int HW, int C, int
   }
 }
 
+// Fast head paths: cpp = C/8 lanes cooperate on one pixel (cpp a power of two <= 64), so one
+// wave-instruction loads 1 KB contiguous; weights live in registers.
+template <typename T, int NO>
+__global__ void __launch_bounds__(256) head_fwd_fast_kernel(int B, int HW, int C, const T* __restrict__ x,
+                                                            const float* __restrict__ w, const float* __restrict__ bias,
+                                                            float* __restrict__ out) {
+  const int cpp = C >> 3;
+  const int lane = threadIdx.x & 63, sub = lane & (cpp - 1);
+  const int ppw = 64 / cpp;                                 // pixels per wave
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, nwaves = gridDim.x * 4;
+  float wr[NO][8];
+#pragma unroll
+  for (int o = 0; o < NO; ++o)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) wr[o][q] = w[o * C + sub * 8 + q];
+  const int64_t M = (int64_t)B * HW;
+  for (int64_t m0 = (int64_t)wave * ppw; m0 < M; m0 += (int64_t)nwaves * ppw) {
+    const int64_t m = m0 + lane / cpp;
+    float v[8];
+    float s[NO];
+    const bool ok = m < M;
+    if (ok) load8<T>(x + m * C + sub * 8, v);
+#pragma unroll
+    for (int o = 0; o < NO; ++o) {
+      float a = 0.f;
+      if (ok)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a += v[q] * wr[o][q];
+      for (int k = 1; k < cpp; k <<= 1) a += __shfl_xor(a, k, 64);
+      s[o] = a;
+    }
+    if (ok && sub == 0) {
+      const int b = (int)(m / HW), hw = (int)(m % HW);
+#pragma unroll
+      for (int o = 0; o < NO; ++o) out[((size_t)b * NO + o) * HW + hw] = s[o] + (bias ? bias[o] : 0.f);
+    }
+  }
+}
+
+// dx = dl @ w; per-block partial dw[o][c] = sum g_o x_c and db[o] = sum g_o over the block's pixels
+template <typename T, int NO>
+__global__ void __launch_bounds__(256) head_bwd_fast_kernel(int B, int HW, int C, const T* __restrict__ x,
+                                                            const float* __restrict__ w, const float* __restrict__ dl,
+                                                            T* __restrict__ dx, float* __restrict__ pw,
+                                                            float* __restrict__ pb) {
+  const int cpp = C >> 3;
+  const int lane = threadIdx.x & 63, sub = lane & (cpp - 1);
+  const int ppw = 64 / cpp;
+  const int wave_in_blk = threadIdx.x >> 6;
+  const int wave = (blockIdx.x * 256 + threadIdx.x) >> 6, nwaves = gridDim.x * 4;
+  float wr[NO][8], aw[NO][8], ab[NO];
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+    ab[o] = 0.f;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { wr[o][q] = w[o * C + sub * 8 + q]; aw[o][q] = 0.f; }
+  }
+  const int64_t M = (int64_t)B * HW;
+  for (int64_t m0 = (int64_t)wave * ppw; m0 < M; m0 += (int64_t)nwaves * ppw) {
+    const int64_t m = m0 + lane / cpp;
+    if (m >= M) continue;
+    const int b = (int)(m / HW), hw = (int)(m % HW);
+    float g[NO], v[8], d[8];
+#pragma unroll
+    for (int o = 0; o < NO; ++o) g[o] = dl[((size_t)b * NO + o) * HW + hw];
+    load8<T>(x + m * C + sub * 8, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      float a = 0.f;
+#pragma unroll
+      for (int o = 0; o < NO; ++o) { a += g[o] * wr[o][q]; aw[o][q] += g[o] * v[q]; }
+      d[q] = a;
+    }
+#pragma unroll
+    for (int o = 0; o < NO; ++o) ab[o] += (sub == 0) ? g[o] : 0.f;
+    store8<T>(dx + m * C + sub * 8, d);
+  }
+  // reduce over the lanes that share `sub` (pixel groups) within the wave, then across waves
+#pragma unroll
+  for (int o = 0; o < NO; ++o) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+      for (int k = cpp; k < 64; k <<= 1) aw[o][q] += __shfl_xor(aw[o][q], k, 64);
+    for (int k = 1; k < 64; k <<= 1) ab[o] += __shfl_xor(ab[o], k, 64);
+  }
+  __shared__ float red[4][NO][512 + 1];
+  if (lane < cpp) {
+#pragma unroll
+    for (int o = 0; o < NO; ++o)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[wave_in_blk][o][sub * 8 + q] = aw[o][q];
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int o = 0; o < NO; ++o) red[wave_in_blk][o][512] = ab[o];
+  __syncthreads();
+  for (int e = threadIdx.x; e < NO * C; e += 256) {
+    const int o = e / C, c = e % C;
+    pw[(size_t)blockIdx.x * NO * C + e] = red[0][o][c] + red[1][o][c] + red[2][o][c] + red[3][o][c];
+  }
+  if (threadIdx.x < NO)
+    pb[(size_t)blockIdx.x * NO + threadIdx.x] =
+        red[0][threadIdx.x][512] + red[1][threadIdx.x][512] + red[2][threadIdx.x][512] + red[3][threadIdx.x][512];
+}
+
+constexpr int kHeadBwdBlocks = 1024;
+
+inline bool head_fast_ok(int C, int Cout) {
+  const int cpp = C / 8;
+  return C % 8 == 0 && cpp >= 1 && cpp <= 64 && (cpp & (cpp - 1)) == 0 && Cout >= 1 && Cout <= 4;
+}
+
 // ---------------------------------------------------------------- weight packing
 template <typename T>
 __global__ void pack_conv_w_kernel(const float* __restrict__ w, int Cout, int Cin, int ntaps, int Cpad, int Kpad,
@@ -266,6 +378,30 @@ __global__ void pack_conv_w_t_kernel(const float* __restrict__ w, int Cout, int 
     const int tap = (int)(r % ntaps);
     const int ci = (int)(r / ntaps);
     out[(size_t)ci * Kpad + col0 + tap * Cout + co] = ElemTraits<T>::from_f(w[((size_t)co * Cin + ci) * ntaps + tap]);
+  }
+}
+
+template <typename T>
+__global__ void pack_t3_kernel(int Cin, int Kpad, int wcin, const float* __restrict__ w0, int c0, int t0,
+                               const float* __restrict__ w1, int c1, int t1, const float* __restrict__ w2, int c2,
+                               int t2, int ident2, T* __restrict__ out) {
+  const int64_t total = (int64_t)Cin * Kpad;
+  const int e0 = t0 * c0, e1 = e0 + t1 * c1, e2 = e1 + t2 * c2;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ci = (int)(e / Kpad), k = (int)(e % Kpad);
+    float v = 0.f;
+    if (k < e0) {
+      const int tap = k / c0, co = k - tap * c0;
+      if (ci < wcin) v = w0[((size_t)co * wcin + ci) * t0 + tap];
+    } else if (k < e1) {
+      const int kk = k - e0, tap = kk / c1, co = kk - tap * c1;
+      if (ci < wcin) v = w1[((size_t)co * wcin + ci) * t1 + tap];
+    } else if (k < e2) {
+      const int kk = k - e1, tap = kk / c2, co = kk - tap * c2;
+      if (ident2) v = (ci == co ? 1.f : 0.f);
+      else if (ci < wcin) v = w2[((size_t)co * wcin + ci) * t2 + tap];
+    }
+    out[e] = ElemTraits<T>::from_f(v);
   }
 }
 
@@ -454,6 +590,23 @@ extern "C" int dfcsa_head_fwd(int dtype, int B, int HW, int C, int Cout, const v
   if (C % 8 || Cout < 1 || Cout > 8) return DFCSA_EINVAL;
   int64_t M = (int64_t)B * HW;
   hipStream_t st = (hipStream_t)stream;
+  if (head_fast_ok(C, Cout)) {
+    const int ppw = 64 / (C / 8);
+    int blocks = (int)std::min<int64_t>(4096, (M / ppw + 3) / 4 + 1);
+#define HF(NO)                                                                                             \
+  if (Cout == NO) {                                                                                        \
+    if (dtype == DFCSA_DT_BF16)                                                                            \
+      hipLaunchKernelGGL((head_fwd_fast_kernel<bf16_t, NO>), dim3(blocks), dim3(256), 0, st, B, HW, C,       \
+                         (const bf16_t*)x, w, b, logits);                                                  \
+    else                                                                                                   \
+      hipLaunchKernelGGL((head_fwd_fast_kernel<float, NO>), dim3(blocks), dim3(256), 0, st, B, HW, C,        \
+                         (const float*)x, w, b, logits);                                                   \
+  }
+    HF(1) HF(2) HF(3) HF(4)
+#undef HF
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
   if (dtype == DFCSA_DT_BF16)
     hipLaunchKernelGGL(head_fwd_kernel<bf16_t>, dim3(grid_for(M)), dim3(256), 0, st, B, HW, C, Cout,
                        (const bf16_t*)x, w, b, logits);
@@ -469,10 +622,26 @@ extern "C" int dfcsa_head_bwd(int dtype, int B, int HW, int C, int Cout, const v
                               void* stream) {
   if (C % 8 || Cout < 1 || Cout > 8) return DFCSA_EINVAL;
   int64_t M = (int64_t)B * HW;
-  int blocks = (int)((M + 255) / 256);
+  const bool fast = head_fast_ok(C, Cout);
+  int blocks = fast ? kHeadBwdBlocks : (int)((M + 255) / 256);
   if (ntiles) *ntiles = blocks;
   if (!partial_w) return 0;  // size query
   hipStream_t st = (hipStream_t)stream;
+  if (fast) {
+#define HB(NO)                                                                                             \
+  if (Cout == NO) {                                                                                        \
+    if (dtype == DFCSA_DT_BF16)                                                                            \
+      hipLaunchKernelGGL((head_bwd_fast_kernel<bf16_t, NO>), dim3(blocks), dim3(256), 0, st, B, HW, C,       \
+                         (const bf16_t*)x, w, dlogit, (bf16_t*)dx, partial_w, partial_b);                  \
+    else                                                                                                   \
+      hipLaunchKernelGGL((head_bwd_fast_kernel<float, NO>), dim3(blocks), dim3(256), 0, st, B, HW, C,        \
+                         (const float*)x, w, dlogit, (float*)dx, partial_w, partial_b);                    \
+  }
+    HB(1) HB(2) HB(3) HB(4)
+#undef HB
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
   size_t shm = (size_t)256 * Cout * sizeof(float);
   if (dtype == DFCSA_DT_BF16)
     hipLaunchKernelGGL(head_bwd_kernel<bf16_t>, dim3(blocks), dim3(256), shm, st, B, HW, C, Cout, (const bf16_t*)x,
@@ -510,6 +679,26 @@ extern "C" int dfcsa_pack_conv_w_t(int dtype, const float* w, int Cout, int Cin,
   else
     hipLaunchKernelGGL(pack_conv_w_t_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, Cout, Cin, ntaps, Kpad,
                        col0, (float*)out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_t3(int dtype, int Cin, int Kpad, int wcin, const float* w0, int cout0, int ntaps0, const float* w1,
+                             int cout1, int ntaps1, const float* w2, int cout2, int ntaps2, int identity2, void* out,
+                             void* stream) {
+  if (!w0) { cout0 = 0; ntaps0 = 1; }
+  if (!w1) { cout1 = 0; ntaps1 = 1; }
+  if (!w2 && !identity2) { cout2 = 0; ntaps2 = 1; }
+  if (identity2) ntaps2 = 1;
+  if (ntaps0 * cout0 + ntaps1 * cout1 + ntaps2 * cout2 > Kpad) return DFCSA_EINVAL;
+  int64_t n = (int64_t)Cin * Kpad;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(pack_t3_kernel<bf16_t>, dim3(grid_for(n)), dim3(256), 0, st, Cin, Kpad, wcin, w0, cout0, ntaps0, w1,
+                       cout1, ntaps1, w2, cout2, ntaps2, identity2, (bf16_t*)out);
+  else
+    hipLaunchKernelGGL(pack_t3_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, Cin, Kpad, wcin, w0, cout0, ntaps0, w1,
+                       cout1, ntaps1, w2, cout2, ntaps2, identity2, (float*)out);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -223,8 +223,15 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
   int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   int64_t total = (int64_t)NI * NJ;
   if (e >= total) return;
-  float s = 0.f;
-  for (int k = 0; k < splits; ++k) s += slab[(int64_t)k * total + e];
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
+  int k = 0;
+  for (; k + 7 < splits; k += 8) {  // 8 independent loads in flight (latency-bound otherwise)
+    const float* p = slab + (int64_t)k * total + e;
+    a0 += p[0]; a1 += p[total]; a2 += p[2 * total]; a3 += p[3 * total];
+    a4 += p[4 * total]; a5 += p[5 * total]; a6 += p[6 * total]; a7 += p[7 * total];
+  }
+  for (; k < splits; ++k) a0 += slab[(int64_t)k * total + e];
+  const float s = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
   int i = (int)(e / NJ), j = (int)(e % NJ);
   if (layout == 0) {
     int rows = NI / ndst;

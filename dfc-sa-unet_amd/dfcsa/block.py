@@ -160,8 +160,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
     ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                         [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     KpC = rup(C, ops.KALIGN)
-    W4t = torch.zeros((3 * C, KpC), dtype=dtype, device=dev)
-    ops.pack_conv_w_t(dtype, conv4.weight, KpC, W4t, 0)
+    W4t = ops.pack_t3(dtype, 3 * C, KpC, [conv4.weight])
     dfused = torch.empty_like(s.y4)
     dlocal = torch.empty_like(s.y4)
     dattn = torch.empty_like(s.y4)
@@ -179,8 +178,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
     del dz3
     ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                         [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
-    W3t = torch.zeros((2 * C, KpC), dtype=dtype, device=dev)
-    ops.pack_conv_w_t(dtype, conv3.weight, KpC, W3t, 0)
+    W3t = ops.pack_t3(dtype, 2 * C, KpC, [conv3.weight])
     ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
 
@@ -220,17 +218,17 @@ def block_backward(blk, s, dout, need_dx, dtype):
 
     # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM ----
     Kx = rup(11 * C, ops.KALIGN)
-    Wdx = torch.zeros((Cin_p, Kx), dtype=dtype, device=dev)
-    ops.pack_conv_w_t(dtype, conv1.weight, Kx, Wdx, 0)
-    ops.pack_conv_w_t(dtype, conv2.weight, Kx, Wdx, 9 * C)
-    if has_res:
-        ops.pack_conv_w_t(dtype, blk.residual_conv.weight, Kx, Wdx, 10 * C)
-    else:
-        Wdx[:, 10 * C:11 * C] = torch.eye(C, dtype=dtype, device=dev)  # identity residual
+    Wdx = ops.pack_t3(dtype, Cin_p, Kx, [conv1.weight, conv2.weight,
+                                         blk.residual_conv.weight if has_res else None],
+                      identity_last=not has_res)  # identity residual: an identity weight block
     segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dy2, 0, 0), (dres, 0, 0)]
     dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
     ops.conv_gemm(dtype, segs, C, grid, hw, Wdx, Kx, Cin_p, dxs, Cs)
     return dxs
+
+
+def _lsa_gemm_ok(C, J):
+    return C % 8 == 0 and J % 8 == 0 and C >= 64
 
 
 def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
@@ -246,15 +244,26 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
     S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
     call("dfcsa_lsa_pool", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), stream())
-    Wqkv = torch.empty((J, C), device=dev, dtype=f32)
-    WqkvT = torch.empty((C, J), device=dev, dtype=f32)
-    for w, off in ((lsa.query_conv.weight, 0), (lsa.key_conv.weight, Cq), (lsa.value_conv.weight, 2 * Cq)):
-        ops.pack_conv_w(f32, w, C, C, out=Wqkv, row0=off)
-        ops.pack_conv_w_t(f32, w, J, WqkvT, col0=off)
     bqkv = torch.cat([lsa.query_conv.bias.detach(), lsa.key_conv.bias.detach(), lsa.value_conv.bias.detach()])
     pooled = torch.empty((B, N, C), device=dev, dtype=f32)
     qkv = torch.empty((B, N, J), device=dev, dtype=f32)
-    call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
+    ws = ((lsa.query_conv.weight, 0), (lsa.key_conv.weight, Cq), (lsa.value_conv.weight, 2 * Cq))
+    if _lsa_gemm_ok(C, J):
+        # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
+        call("dfcsa_lsa_pooled", B, H, W, C, Pp, P(part), P(pooled), stream())
+        Kp = rup(C, ops.KALIGN)
+        Wp = torch.empty((J, Kp), device=dev, dtype=f32)
+        for w, off in ws:
+            ops.pack_conv_w(f32, w, C, Kp, out=Wp, row0=off)
+        ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), Wp, Kp, J, [qkv], J, bias=bqkv)
+        Wqkv = None
+    else:
+        Wqkv = torch.empty((J, C), device=dev, dtype=f32)
+        WqkvT = torch.empty((C, J), device=dev, dtype=f32)
+        for w, off in ws:
+            ops.pack_conv_w(f32, w, C, C, out=Wqkv, row0=off)
+            ops.pack_conv_w_t(f32, w, J, WqkvT, col0=off)
+        call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
     A = torch.empty((B, N, N), device=dev, dtype=f32)
     o = torch.empty((B, N, C), device=dev, dtype=f32)
     call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
@@ -282,10 +291,26 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype):
     dqkv = torch.empty((B, N, J), device=dev, dtype=f32)
     call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
     dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
-    call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
-         P(grad_of(lsa.query_conv.weight)), P(grad_of(lsa.key_conv.weight)), P(grad_of(lsa.value_conv.weight)),
-         P(grad_of(lsa.query_conv.bias)), P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)),
-         P(dpooled), stream())
+    qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
+    if _lsa_gemm_ok(C, J):
+        BN = B * N
+        # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums, dpooled = dqkv Wqkv
+        slab, splits, NI, NJ = ops.wgrad(f32, [dqkv], J, [(pooled, 0, 0)], C, (1, BN, 1), (BN, 1))
+        dW = torch.zeros((J, C), device=dev, dtype=f32)
+        ops.wgrad_reduce(slab, splits, NI, NJ, 0, 1, C, C, [dW])
+        db = torch.zeros(J, device=dev, dtype=f32)
+        ops.channel_sum_into(f32, dqkv, db)
+        for w, b, lo, hi in ((qw, lsa.query_conv.bias, 0, Cq), (kw, lsa.key_conv.bias, Cq, 2 * Cq),
+                             (vw, lsa.value_conv.bias, 2 * Cq, J)):
+            grad_of(w).add_(dW[lo:hi].view_as(w))
+            grad_of(b).add_(db[lo:hi])
+        Kj = rup(J, ops.KALIGN)
+        WT = ops.pack_t3(f32, C, Kj, [qw, kw, vw])
+        ops.conv_gemm(f32, [(dqkv, 0, 0)], J, (1, BN, 1), (BN, 1), WT, Kj, C, [dpooled], C)
+    else:
+        call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
+             P(grad_of(qw)), P(grad_of(kw)), P(grad_of(vw)), P(grad_of(lsa.query_conv.bias)),
+             P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)), P(dpooled), stream())
     return dpooled
 
 

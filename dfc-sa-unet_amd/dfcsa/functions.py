@@ -144,7 +144,7 @@ class Head1x1(torch.autograd.Function):
         dx = torch.empty_like(x)
         call("dfcsa_head_bwd", dt(dtype), B, H * W, C, Cout, P(x), P(mod.weight), P(g.contiguous()), P(dx), P(pw),
              P(pb), None, stream())
-        call("dfcsa_slab_colsum", P(pw), nt.value, Cout * C, P(grad_of(mod.weight)), stream())
-        call("dfcsa_slab_colsum", P(pb), nt.value, Cout, P(grad_of(mod.bias)), stream())
+        ops.colsum_into(pw, nt.value, Cout * C, grad_of(mod.weight))
+        ops.colsum_into(pb, nt.value, Cout, grad_of(mod.bias))
         notify_grads_ready(mod)
         return (dx if ctx.needs_input_grad[0] else None, None, None, *([None] * ctx.np))

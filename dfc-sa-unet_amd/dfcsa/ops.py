@@ -148,8 +148,23 @@ class BNState:
         self.scale, self.shift, self.mean, self.invstd = buf[0], buf[1], buf[2], buf[3]
 
 
+REDUCE_GROUPS = 256
+
+
+def rows_reduce(src, T, rowlen):
+    """First stage of a per-tile slab reduction: [T][rowlen] -> [G][rowlen] (G <= 256)."""
+    if T <= REDUCE_GROUPS // 4:
+        return src, T
+    G = REDUCE_GROUPS
+    dst = torch.empty(G * rowlen, device=src.device, dtype=torch.float32)
+    call("dfcsa_rows_reduce", P(src), T, rowlen, P(dst), G, stream())
+    return dst, G
+
+
 def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
     st = BNState(C, bn_mod.weight.device)
+    if training:
+        stats, ntiles = rows_reduce(stats, ntiles, 2 * ld)
     nbt = bn_mod.num_batches_tracked if training else None
     call("dfcsa_bn_finalize", P(stats) if training else None, ntiles, C, ld, count, P(conv_bias),
          P(bn_mod.weight), P(bn_mod.bias), P(bn_mod.running_mean), P(bn_mod.running_var), P(nbt),
@@ -160,6 +175,7 @@ def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
 
 def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
+    partial, ntiles = rows_reduce(partial, ntiles, nsum * C)
     call("dfcsa_bn_bwd_finalize", P(partial), ntiles, nsum, C, count, P(coef), P(dgamma), P(dbeta), P(extra),
          stream())
     return coef
@@ -173,8 +189,14 @@ def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
     call("dfcsa_bn_bwd_apply", dt(dtype), M, C, P(dz), P(y), P(bn.mean), P(bn.invstd), P(gamma), P(coef), P(dy),
          P(part), stream())
     if bias_grad is not None:
-        call("dfcsa_slab_colsum", P(part), nt, C, P(bias_grad), stream())
+        colsum_into(part, nt, C, bias_grad)
     return dy
+
+
+def colsum_into(slab, nt, C, out):
+    """out[c] += sum_t slab[t][c]"""
+    slab, nt = rows_reduce(slab, nt, C)
+    call("dfcsa_slab_colsum", P(slab), nt, C, P(out), stream())
 
 
 def channel_sum_into(dtype, x, out):
@@ -182,4 +204,22 @@ def channel_sum_into(dtype, x, out):
     nt = ntiles_ew(M, C)
     part = torch.empty(nt * C, device=x.device, dtype=torch.float32)
     call("dfcsa_channel_sum", dt(dtype), M, C, P(x), P(part), stream())
-    call("dfcsa_slab_colsum", P(part), nt, C, P(out), stream())
+    colsum_into(part, nt, C, out)
+
+
+def pack_t3(dtype, Cin, Kpad, segs, identity_last=False, out=None, device=None):
+    """Transposed packing of up to three weights side by side (full rows, zero tail):
+    segs = [w0, w1, w2] (None = absent); with identity_last the third segment is I (Cout=Cin)."""
+    ws = list(segs) + [None] * (3 - len(segs))
+    wcin = next(w.shape[1] for w in ws if w is not None)
+    args = []
+    for i, w in enumerate(ws):
+        if w is None:
+            cout = Cin if (i == 2 and identity_last) else 0
+            args += [None, cout, 1]
+        else:
+            args += [P(w), w.shape[0], (w.shape[2] * w.shape[3]) if w.dim() == 4 else 1]
+    if out is None:
+        out = torch.empty((Cin, Kpad), dtype=dtype, device=device or ws[0].device)
+    call("dfcsa_pack_t3", dt(dtype), Cin, Kpad, wcin, *args, int(identity_last), P(out), stream())
+    return out

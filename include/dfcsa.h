@@ -103,6 +103,14 @@ int dfcsa_pack_conv_w(int dtype, const float* w, int Cout, int Cin, int ntaps, i
 /* transposed (dgrad) packing: out[ci][col0 + tap*Cout + co] = w[co][ci][tap] (row stride Kpad) */
 int dfcsa_pack_conv_w_t(int dtype, const float* w, int Cout, int Cin, int ntaps, int Kpad,
                         int col0, void* out, void* stream);
+/* transposed packing of up to three weights side by side, full rows (zeros elsewhere):
+ * out[ci][off_s + tap*Cout_s + co] = w_s[co][ci][tap] for s = 0..2 (off_0 = 0, off_{s+1} = off_s +
+ * ntaps_s*Cout_s), rows ci < Cin, row stride Kpad; the weights have wcin input channels (rows
+ * ci >= wcin are zero).  w_s may be NULL (segment absent, Cout_s = 0) or, for s = 2 with
+ * identity2 != 0, the identity (out[ci][off_2 + co] = (ci == co)). */
+int dfcsa_pack_t3(int dtype, int Cin, int Kpad, int wcin, const float* w0, int cout0, int ntaps0, const float* w1,
+                  int cout1, int ntaps1, const float* w2, int cout2, int ntaps2, int identity2, void* out,
+                  void* stream);
 /* ConvTranspose2d weight [Cin][Cout][2][2]: fwd [4*Cout][Cin] (row ij*Cout+co), bwd [Cin][4*Cout],
  * bias4[ij*Cout+co] = bias[co]. */
 int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, int Cin, int Cout, void* out_fwd,
@@ -178,6 +186,10 @@ int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int
 int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
                        const float* invstd, const float* gamma, const float* coef, void* dy,
                        float* bias_partial, void* stream);
+/* Two-stage reduction helper for per-tile slabs: dst[g][j] = sum of rows t in group g of
+ * src[t][j] (T rows of rowlen floats, G groups of ceil(T/G) consecutive rows).  The finalize
+ * entry points then reduce G rows instead of T.  dst: [G][rowlen] fp32 (caller scratch). */
+int dfcsa_rows_reduce(const float* src, int T, int rowlen, float* dst, int G, void* stream);
 /* out[c] += sum_t slab[t][c]  (ntiles x C); fp64 accumulation */
 int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream);
 /* per-channel partial sums of an NHWC tensor -> partial [ntiles][C] */
@@ -191,6 +203,8 @@ int dfcsa_lsa_pool_splits(int H, int P);
 /* partial[b][n][s][c] = sum over the s-th row slice of window n of act(y2*sc2+sh2) */
 int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
                    const float* sh2, int P, int relu, float* partial, void* stream);
+/* pooled = partial sums / window area  ([B][N][C] fp32) */
+int dfcsa_lsa_pooled(int B, int H, int W, int C, int P, const float* partial, float* pooled, void* stream);
 /* pooled = partial sums / window area; qkv = pooled @ wT + b  (wT: [C][2Cq+C] fp32) */
 int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,
                   const float* bias, float* pooled, float* qkv, void* stream);

@@ -209,3 +209,26 @@ def test_clip_sgd_matches_torch():
         for pr, pm in zip(ref.parameters(), mine.parameters()):
             assert rel(pm, pr) < 1e-6
     assert flat.valid()
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("C,Cout", [(64, 1), (8, 1), (32, 3), (24, 1)])
+def test_head_fwd_bwd(dtype, tol, C, Cout):
+    from dfcsa.functions import Head1x1
+    torch.manual_seed(8)
+    B, H, W = 2, 13, 9
+    mod = torch.nn.Conv2d(C, Cout, 1)
+    x = q(torch.randn(B, C, H, W), dtype)
+    xr = x.clone().requires_grad_(True)
+    ref = mod(xr)
+    g = torch.randn_like(ref)
+    ref.backward(g)
+    modg = torch.nn.Conv2d(C, Cout, 1).cuda()
+    modg.load_state_dict(mod.state_dict())
+    xh = nhwc(x, dtype).requires_grad_(True)
+    y = Head1x1.apply(xh, modg, dtype, *modg.parameters())
+    y.backward(g.cuda())
+    assert rel(y, ref) < tol
+    assert rel(nchw(xh.grad), xr.grad) < tol
+    assert rel(modg.weight.grad, mod.weight.grad) < max(tol, 1e-5)
+    assert rel(modg.bias.grad, mod.bias.grad) < 1e-5
