@@ -292,8 +292,34 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
     }
   }
   // deterministic in-workgroup reduction over pixel lanes
-  __shared__ float red[256 * 8];
+  __shared__ float red[4 * 3 * 512];
   float* out = a.partial + (size_t)blockIdx.x * NS * a.C;
+  const bool pow2 = (cpp & (cpp - 1)) == 0;
+  if (pow2 && cpp <= 64) {
+    // lanes l and l ^ (k*cpp) hold the same channels: butterfly over the wave's pixel lanes,
+    // then the 4 per-wave partials go through LDS
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = acc[s][q];
+        for (int off = cpp; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
+        acc[s][q] = v;
+      }
+    if (lane < cpp)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[(wave * NS + s) * a.C + ck * 8 + q] = acc[s][q];
+    __syncthreads();
+    for (int e = tid; e < NS * a.C; e += 256) {
+      const int s = e / a.C, c = e - s * a.C;
+      out[e] = (red[(0 * NS + s) * a.C + c] + red[(1 * NS + s) * a.C + c]) +
+               (red[(2 * NS + s) * a.C + c] + red[(3 * NS + s) * a.C + c]);
+    }
+    return;
+  }
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     if (active) {
@@ -431,7 +457,13 @@ __global__ void __launch_bounds__(256) sum_scalar_kernel(const float* x, int n, 
   if (threadIdx.x == 0) *out += (float)r[0];
 }
 
-constexpr int kTilePx = 256;
+// pixels per reduction tile: ~16 chunk-iterations per thread (fewer, fuller tiles than a fixed size)
+inline int tile_px(int C) {
+  const int cpp = C / 8, pl = 256 / (cpp > 0 ? cpp : 1);
+  int t = 32768 / (C > 0 ? C : 1);
+  if (t < pl) t = pl;
+  return t;
+}
 
 template <int MODE>
 int launch_fwd(int dtype, const EwArgs& a, hipStream_t st) {
@@ -447,8 +479,8 @@ int launch_fwd(int dtype, const EwArgs& a, hipStream_t st) {
 template <int MODE>
 int launch_red(int dtype, EwArgs a, hipStream_t st) {
   if (a.C % 8 || a.C > 2048 || a.M <= 0) return DFCSA_EINVAL;
-  a.tile_px = kTilePx;
-  int blocks = (a.M + kTilePx - 1) / kTilePx;
+  a.tile_px = tile_px(a.C);
+  int blocks = (a.M + a.tile_px - 1) / a.tile_px;
   if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_red_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((ew_red_kernel<float, MODE>), dim3(blocks), dim3(256), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -465,7 +497,7 @@ EwArgs zargs(int M, int C) {
 
 }  // namespace
 
-extern "C" int dfcsa_ew_ntiles(int M, int C) { (void)C; return (M + kTilePx - 1) / kTilePx; }
+extern "C" int dfcsa_ew_ntiles(int M, int C) { return (M + tile_px(C) - 1) / tile_px(C); }
 
 extern "C" int dfcsa_bn_finalize(const float* stats, int ntiles, int C, int ld, int count, const float* conv_bias,
                                  const float* gamma, const float* beta, float* running_mean, float* running_var,
