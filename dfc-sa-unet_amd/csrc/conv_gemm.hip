@@ -59,6 +59,124 @@ __device__ __forceinline__ void mma(f32x4_t& acc, const Frag<float>& a, const Fr
   for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], acc, 0, 0, 0);
 }
 
+// Shared epilogue: BN partial statistics of the fp32 accumulator, bias, conversion, LDS-staged
+// coalesced 16-byte stores (plain / 3-way column split / ConvTranspose pixel shuffle), optional
+// accumulate into the destination.  smem must hold max(2*WM*BN floats, BM*(BN*sizeof(T)+16)) B.
+template <typename T, int BM, int BN, int WM, int WN>
+__device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t (&acc)[BM / WM / 16][BN / WN / 16],
+                                              char* smem, int m0, int n0, int m_tile, int tid, int lane, int wm,
+                                              int wn) {
+  constexpr int NT = WM * WN * 64;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  const int M = args.M, N = args.N;
+  // (1) BatchNorm partial statistics of the raw accumulator, per column, rows m < M only, one
+  //     slab row per 64-row sub-tile of M (so the layout does not depend on the tile shape).
+  constexpr int SUBW = WTM >= 64 ? WTM / 64 : 1;   // sub-tiles covered by one wave
+  constexpr int SUBS = BM / 64;                    // sub-tiles of the workgroup tile
+  float* red = (float*)smem;                       // [WM][SUBW][2][BN] after the main loop
+  if (args.stats) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s[SUBW], q[SUBW];
+#pragma unroll
+      for (int u = 0; u < SUBW; ++u) { s[u] = 0.f; q[u] = 0.f; }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          const float v = (m < M) ? acc[i][j][r] : 0.f;
+          constexpr int dummy = 0;
+          const int u = SUBW > 1 ? (i * 16) / 64 : dummy;
+          s[u] += v;
+          q[u] += v * v;
+        }
+#pragma unroll
+      for (int u = 0; u < SUBW; ++u) {
+        float a = s[u], b = q[u];
+        a += __shfl_xor(a, 16, 64); a += __shfl_xor(a, 32, 64);
+        b += __shfl_xor(b, 16, 64); b += __shfl_xor(b, 32, 64);
+        if (lane < 16) {
+          const int col = wn * WTN + j * 16 + lane;
+          red[((wm * SUBW + u) * 2 + 0) * BN + col] = a;
+          red[((wm * SUBW + u) * 2 + 1) * BN + col] = b;
+        }
+      }
+    }
+    __syncthreads();
+    for (int e = tid; e < SUBS * BN; e += NT) {
+      const int st = e / BN, c = e - st * BN;
+      const int n = n0 + c;
+      const int row0 = m0 + st * 64;
+      if (n < N && row0 < M) {
+        float sm = 0.f, q = 0.f;
+        if (WTM >= 64) {
+          const int w = (st * 64) / WTM, u = st - w * SUBW;
+          sm = red[((w * SUBW + u) * 2) * BN + c];
+          q = red[((w * SUBW + u) * 2 + 1) * BN + c];
+        } else {
+          for (int w = 0; w < WM; ++w)
+            if ((w * WTM) / 64 == st) { sm += red[(w * 2) * BN + c]; q += red[(w * 2 + 1) * BN + c]; }
+        }
+        const size_t t = (size_t)(m0 / 64) + st;
+        args.stats[t * 2 * N + n] = sm;
+        args.stats[t * 2 * N + N + n] = q;
+      }
+    }
+    __syncthreads();
+  }
+
+  // (2) bias, convert, stage the tile through LDS, coalesced 16-B stores.
+  T* otile = (T*)smem;
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    int col = wn * WTN + j * 16 + (lane & 15);
+    int n = n0 + col;
+    float bv = (args.bias && n < N) ? args.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        *(T*)((char*)otile + row * OSTR + col * sizeof(T)) = ElemTraits<T>::from_f(acc[i][j][r] + bv);
+      }
+  }
+  __syncthreads();
+  constexpr int OCH = BN / 8;                      // 8-element chunks per tile row
+  for (int e = tid; e < BM * OCH; e += NT) {
+    int row = e / OCH, cc = e % OCH;
+    int m = m0 + row, n = n0 + cc * 8;
+    if (m >= M || n >= N) continue;
+    float v[8];
+    const T* src = (const T*)((const char*)otile + row * OSTR + cc * 8 * sizeof(T));
+#pragma unroll
+    for (int q = 0; q < 8; ++q) v[q] = ElemTraits<T>::to_f(src[q]);
+    T* dst;
+    if (args.mode == CONV_STORE_SHUFFLE2) {
+      // ConvTranspose2d(k=2, s=2): column n = (i*2 + j) * Cout + co  ->  pixel (2oh+i, 2ow+j)
+      int ij = n / args.Nd, co = n - ij * args.Nd;
+      int b = dm_div(args.dm_hw, m);
+      int rem = m - b * args.dm_hw.d;
+      int oh = dm_div(args.dm_w, rem);
+      int ow = rem - oh * args.dm_w.d;
+      int y = 2 * oh + (ij >> 1), x = 2 * ow + (ij & 1);
+      dst = (T*)args.dest[0] + ((size_t)((b * args.Hout + y) * args.Wout + x) * args.Nd + co);
+    } else {
+      int d = n / args.Nd, col = n - d * args.Nd;
+      dst = (T*)args.dest[d] + ((size_t)m * args.Nd + col);
+    }
+    if (args.accumulate) {
+      float o[8];
+      load8<T>(dst, o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] += o[q];
+    }
+    store8<T>(dst, v);
+  }
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 __global__ void __launch_bounds__(WM* WN * 64)
 conv_gemm_kernel(const ConvGemmArgs args) {
@@ -183,90 +301,137 @@ conv_gemm_kernel(const ConvGemmArgs args) {
     __syncthreads();
   }
 
-  // ---------------- epilogue ----------------
-  // (1) BatchNorm partial statistics of the raw accumulator, per column, rows m < M only.
-  float* red = (float*)smem;  // [WM][2][BN] after the main loop
-  if (args.stats) {
+  conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wm, wn);
+}
+
+
+// --------------------------------------------------------------------------------------------
+// bf16 hot path: operands staged by LDS-DMA (global_load_lds_dwordx4).  Each wave-instruction
+// fills one 8-row x 128-B block of the K-stage image; the XOR swizzle is applied on the SOURCE
+// side (lane -> which 16-B chunk of its row it fetches), so the fragment reads are the same
+// conflict-free ds_read_b128 as the register-staged kernel.  Zero padding (image border, K tail,
+// N tail) fetches a 1-KB zero page instead of masking, so every LDS slot is written each stage.
+// Two LDS buffers; one vmcnt(0) + barrier per 64-deep K stage.
+// --------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) uint4 g_zero_page[64];
+
+typedef __attribute__((address_space(3))) void lds_void;
+typedef const __attribute__((address_space(1))) void glb_void;
+
+__device__ __forceinline__ void glds16(const void* src, char* lds_base) {
+  __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM* WN * 64)
+conv_gemm_glds_kernel(const ConvGemmArgs args) {
+  using T = bf16_t;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int A_IN = BM / (8 * NW), B_IN = BN / (8 * NW);
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  constexpr int SMEM = (2 * STAGE > BM * OSTR) ? 2 * STAGE : BM * OSTR;
+  static_assert(NW % 2 == 0 && A_IN >= 1 && B_IN >= 1, "glds tiling");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int n_tile = blockIdx.x, m_tile = blockIdx.y;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int M = args.M, N = args.N;
+  // 16-B chunk this lane fetches within its 128-B row (source-side swizzle)
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+  const int rsub = lane >> 3;
+
+  int a_pix[A_IN], a_oh[A_IN], a_ow[A_IN];
 #pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      float s = 0.f, q = 0.f;
+  for (int i = 0; i < A_IN; ++i) {
+    const int m = m0 + (i * NW + wave) * 8 + rsub;
+    if (m < M) {
+      const int b = dm_div(args.dm_hw, m);
+      const int rem = m - b * args.dm_hw.d;
+      const int oh = dm_div(args.dm_w, rem);
+      const int ow = rem - oh * args.dm_w.d;
+      a_oh[i] = oh * args.stride;
+      a_ow[i] = ow * args.stride;
+      a_pix[i] = (b * args.Hi + a_oh[i]) * args.Wi + a_ow[i];
+    } else {
+      a_oh[i] = -(1 << 20);  // forces the bounds test to fail
+      a_ow[i] = 0;
+      a_pix[i] = 0;
+    }
+  }
+  const T* b_row[B_IN];
+#pragma unroll
+  for (int i = 0; i < B_IN; ++i) {
+    const int n = n0 + (i * NW + wave) * 8 + rsub;
+    b_row[i] = n < N ? (const T*)args.Bw + (size_t)n * args.Kpad : nullptr;
+  }
+  const void* zero = (const void*)g_zero_page;
+
+  auto issue = [&](int kt, int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + BM * 128;
+    const int kbase = kt * 64 + cchunk * 8;
+    const int seg = dm_div(args.dm_cseg, kbase);
+    const int ch = kbase - seg * args.Cseg;
+    const bool kvalid = kbase < args.K;
+    const ConvSeg sg = args.seg[kvalid ? seg : 0];
+    const int soff = sg.dh * args.Wi + sg.dw;
+#pragma unroll
+    for (int i = 0; i < A_IN; ++i) {
+      const int ih = a_oh[i] + sg.dh, iw = a_ow[i] + sg.dw;
+      const bool ok = kvalid && ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi;
+      const void* src = ok ? (const void*)((const T*)sg.ptr + ((size_t)(a_pix[i] + soff) * args.Cseg + ch)) : zero;
+      glds16(src, A + (i * NW + wave) * 8 * 128);
+    }
+#pragma unroll
+    for (int i = 0; i < B_IN; ++i) {
+      const void* src = b_row[i] ? (const void*)(b_row[i] + kbase) : zero;
+      glds16(src, B + (i * NW + wave) * 8 * 128);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nk = args.Kpad / 64;
+  issue(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const char* A = smem + (kt & 1) * STAGE;
+    const char* B = A + BM * 128;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      Frag<T> fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) read_frag<T>(A, wm * WTM + i * 16 + (lane & 15), g, lane, fa[i]);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) read_frag<T>(B, wn * WTN + j * 16 + (lane & 15), g, lane, fb[j]);
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          int m = m0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-          float v = (m < M) ? acc[i][j][r] : 0.f;
-          s += v;
-          q += v * v;
-        }
-      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
-      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      if (lane < 16) {
-        int col = wn * WTN + j * 16 + lane;
-        red[(wm * 2 + 0) * BN + col] = s;
-        red[(wm * 2 + 1) * BN + col] = q;
-      }
+        for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
     }
-    __syncthreads();
-    for (int c = tid; c < BN; c += NT) {
-      int n = n0 + c;
-      if (n < N) {
-        float s = 0.f, q = 0.f;
-        for (int w = 0; w < WM; ++w) { s += red[(w * 2) * BN + c]; q += red[(w * 2 + 1) * BN + c]; }
-        args.stats[(size_t)m_tile * 2 * N + n] = s;
-        args.stats[(size_t)m_tile * 2 * N + N + n] = q;
-      }
-    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
+  conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wm, wn);
+}
 
-  // (2) bias, convert, stage the tile through LDS, coalesced 16-B stores.
-  T* otile = (T*)smem;
-#pragma unroll
-  for (int j = 0; j < FN; ++j) {
-    int col = wn * WTN + j * 16 + (lane & 15);
-    int n = n0 + col;
-    float bv = (args.bias && n < N) ? args.bias[n] : 0.f;
-#pragma unroll
-    for (int i = 0; i < FM; ++i)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        *(T*)((char*)otile + row * OSTR + col * sizeof(T)) = ElemTraits<T>::from_f(acc[i][j][r] + bv);
-      }
-  }
-  __syncthreads();
-  constexpr int OCH = BN / 8;                      // 8-element chunks per tile row
-  for (int e = tid; e < BM * OCH; e += NT) {
-    int row = e / OCH, cc = e % OCH;
-    int m = m0 + row, n = n0 + cc * 8;
-    if (m >= M || n >= N) continue;
-    float v[8];
-    const T* src = (const T*)((const char*)otile + row * OSTR + cc * 8 * sizeof(T));
-#pragma unroll
-    for (int q = 0; q < 8; ++q) v[q] = ElemTraits<T>::to_f(src[q]);
-    T* dst;
-    if (args.mode == CONV_STORE_SHUFFLE2) {
-      // ConvTranspose2d(k=2, s=2): column n = (i*2 + j) * Cout + co  ->  pixel (2oh+i, 2ow+j)
-      int ij = n / args.Nd, co = n - ij * args.Nd;
-      int b = dm_div(args.dm_hw, m);
-      int rem = m - b * args.dm_hw.d;
-      int oh = dm_div(args.dm_w, rem);
-      int ow = rem - oh * args.dm_w.d;
-      int y = 2 * oh + (ij >> 1), x = 2 * ow + (ij & 1);
-      dst = (T*)args.dest[0] + ((size_t)((b * args.Hout + y) * args.Wout + x) * args.Nd + co);
-    } else {
-      int d = n / args.Nd, col = n - d * args.Nd;
-      dst = (T*)args.dest[d] + ((size_t)m * args.Nd + col);
-    }
-    if (args.accumulate) {
-      float o[8];
-      load8<T>(dst, o);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] += o[q];
-    }
-    store8<T>(dst, v);
-  }
+template <int BM, int BN, int WM, int WN>
+int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
+  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -277,8 +442,34 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
   return 0;
 }
 
+int g_conv_cfg = 0;  // tuning override (dfcsa_set_tuning knob 1)
+
+// config ids: 1 reg 128x64, 2 reg 128x128, 3 dma 128x64, 4 dma 256x64, 5 dma 128x128, 6 dma 256x128
 template <typename T>
 int launch_t(const ConvGemmArgs& a, hipStream_t st) {
+  if constexpr (sizeof(T) == 2) {
+    switch (g_conv_cfg) {
+      case 1: return launch_cfg<T, 128, 64, 4, 1>(a, st);
+      case 2: return launch_cfg<T, 128, 128, 2, 2>(a, st);
+      case 3: return launch_glds<128, 64, 2, 1>(a, st);
+      case 4: return launch_glds<256, 64, 4, 1>(a, st);
+      case 5: return launch_glds<128, 128, 2, 2>(a, st);
+      case 6: return launch_glds<256, 128, 2, 2>(a, st);
+      default: break;
+    }
+    // measured on MI355X (tools/gemm_bench.py, the model's B=16 shapes): LDS-DMA 128x128 wins
+    // for N > 64 (600-675 TF on the 3x3 convs); for N <= 64 the LDS-DMA 256x64 tile wins on
+    // deep K (3x3) and the register-staged 128x64 on the memory-bound small-K 1x1s.
+    if (a.N <= 64) {
+      if (a.K >= 512 && (a.M + 255) / 256 >= 256) return launch_glds<256, 64, 4, 1>(a, st);
+      return launch_cfg<T, 128, 64, 4, 1>(a, st);
+    }
+    return launch_glds<128, 128, 2, 2>(a, st);
+  }
+  // fp32 (parity mode + the fp32 LightSelfAttention projections): small problems (M = B*P*P
+  // rows) get 64x64 tiles so that enough workgroups run
+  const int t128 = ((a.M + 127) / 128) * ((a.N + 127) / 128);
+  if (t128 < 128) return launch_cfg<T, 64, 64, 2, 2>(a, st);
   if (a.N <= 64) return launch_cfg<T, 128, 64, 4, 1>(a, st);
   return launch_cfg<T, 128, 128, 2, 2>(a, st);
 }
@@ -311,4 +502,9 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
 }
 
-extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 128; }
+extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }
+
+extern "C" int dfcsa_set_tuning(int knob, int value) {
+  if (knob == 1) { g_conv_cfg = value; return 0; }
+  return DFCSA_EINVAL;
+}

@@ -420,6 +420,85 @@ __global__ void pack_convT_kernel(const float* __restrict__ w, const float* __re
   }
 }
 
+// ---------------------------------------------------------------- one-launch pack plan
+__device__ __forceinline__ void store_as(void* out, int64_t i, int dtype, float v) {
+  if (dtype == DFCSA_DT_BF16) ((bf16_t*)out)[i] = f2bf(v);
+  else ((float*)out)[i] = v;
+}
+
+__global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* __restrict__ tab, int n,
+                                                        int64_t total) {
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    int lo = 0, hi = n - 1;  // last entry with start <= e
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (tab[mid].start <= e) lo = mid; else hi = mid - 1;
+    }
+    const dfcsa_pack_entry& t = tab[lo];
+    const int64_t i = e - t.start;
+    const int* a = t.a;
+    float v = 0.f;
+    switch (t.kind) {
+      case DFCSA_PACK_ROWS: {
+        const int Kpad = a[4], Cpad = a[3];
+        const int co = (int)(i / Kpad), k = (int)(i % Kpad);
+        const int tap = k / Cpad, ci = k - tap * Cpad;
+        if (tap < a[2] && ci < a[1]) v = t.w0[((size_t)co * a[1] + ci) * a[2] + tap];
+        store_as(t.out, (int64_t)(a[5] + co) * Kpad + k, t.dtype, v);
+        break;
+      }
+      case DFCSA_PACK_T3: {
+        const int Kpad = a[1], wcin = a[2], c0 = a[3], c1 = a[4], c2 = a[5], t0 = a[6];
+        const int ci = (int)(i / Kpad), k = (int)(i % Kpad);
+        const int e0 = t0 * c0, e1 = e0 + c1, e2 = e1 + c2;
+        if (k < e0) {
+          const int tap = k / c0, co = k - tap * c0;
+          if (ci < wcin) v = t.w0[((size_t)co * wcin + ci) * t0 + tap];
+        } else if (k < e1) {
+          if (ci < wcin) v = t.w1[(size_t)(k - e0) * wcin + ci];
+        } else if (k < e2) {
+          const int co = k - e1;
+          if (a[7]) v = (ci == co) ? 1.f : 0.f;
+          else if (ci < wcin) v = t.w2[(size_t)co * wcin + ci];
+        }
+        store_as(t.out, i, t.dtype, v);
+        break;
+      }
+      case DFCSA_PACK_CONVT_FWD: {
+        const int Cin = a[0], Cout = a[1], Kp = a[2];
+        const int r = (int)(i / Kp), ci = (int)(i % Kp);
+        const int ij = r / Cout, co = r - ij * Cout;
+        if (ci < Cin) v = t.w0[((size_t)ci * Cout + co) * 4 + ij];
+        store_as(t.out, i, t.dtype, v);
+        break;
+      }
+      case DFCSA_PACK_CONVT_BWD: {
+        const int Cin = a[0], Cout = a[1], Kp = a[2];
+        const int ci = (int)(i / Kp), k = (int)(i % Kp);
+        if (k < 4 * Cout && ci < Cin) {
+          const int ij = k / Cout, co = k - ij * Cout;
+          v = t.w0[((size_t)ci * Cout + co) * 4 + ij];
+        }
+        store_as(t.out, i, t.dtype, v);
+        break;
+      }
+      case DFCSA_PACK_CONCAT: {
+        if (i < a[0]) v = t.w0[i];
+        else if (i < a[0] + a[1]) v = t.w1 ? t.w1[i - a[0]] : 0.f;
+        else if (i < a[0] + a[1] + a[2]) v = t.w2 ? t.w2[i - a[0] - a[1]] : 0.f;
+        ((float*)t.out)[i] = v;
+        break;
+      }
+      case DFCSA_PACK_BIAS4: {
+        ((float*)t.out)[i] = t.w0[i % a[0]];
+        break;
+      }
+      default:
+        break;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- sigmoid / loss
 __global__ void sigmoid_kernel(int64_t n, const float* __restrict__ x, float* __restrict__ y) {
   for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
@@ -713,6 +792,14 @@ extern "C" int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, 
   else
     hipLaunchKernelGGL(pack_convT_kernel<float>, dim3(grid_for(n)), dim3(256), 0, st, w, bias, Cin, Cout,
                        (float*)out_fwd, (float*)out_bwd, bias4);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_pack_plan(const dfcsa_pack_entry* table_dev, int n, int64_t total, void* stream) {
+  if (!table_dev || n <= 0 || total <= 0) return DFCSA_EINVAL;
+  int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
+  hipLaunchKernelGGL(pack_plan_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, table_dev, n, total);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -13,7 +13,7 @@ from . import _lib
 from ._lib import call
 
 KALIGN = 64          # Kpad granularity (64 bf16 / 32 f32 per K stage -> 64 serves both)
-GEMM_MTILE = 128     # rows per conv_gemm stats tile
+GEMM_MTILE = 64      # rows per conv_gemm stats tile (dfcsa_conv_gemm_mtile)
 
 
 def stream():

@@ -38,7 +38,7 @@ extern "C" {
  * weight: [N][Kpad] of dtype, Kpad >= nseg*Cseg, multiple of 64 (bf16) / 32 (f32), zero-padded.
  * mode PLAIN: columns [d*Nd, (d+1)*Nd) go to dest[d] ([M][Nd]).  mode SHUFFLE2 (ConvTranspose
  * k2 s2): column n = (2i + j)*Nd + co goes to dest[0][b, 2oh+i, 2ow+j, co] of Hout x Wout.
- * accumulate: dest += C.  stats (optional): per 128-row M tile t, stats[t][0][n] = sum of the
+ * accumulate: dest += C.  stats (optional): per 64-row M tile t, stats[t][0][n] = sum of the
  * fp32 accumulator (without bias) over valid rows, stats[t][1][n] = sum of squares.
  * ---------------------------------------------------------------------------------------- */
 #define CONV_STORE_PLAIN 0
@@ -115,6 +115,37 @@ int dfcsa_pack_t3(int dtype, int Cin, int Kpad, int wcin, const float* w0, int c
  * bias4[ij*Cout+co] = bias[co]. */
 int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, int Cin, int Cout, void* out_fwd,
                        void* out_bwd, float* bias4, void* stream);
+/* One-launch weight packing for a whole model.  A device table of entries (built once; the
+ * parameter and packed-buffer pointers are stable) is processed in a single grid-stride launch
+ * over the concatenated element ranges [start, start + count) of all entries.
+ * kinds (a* = integer args):
+ *  PACK_ROWS  0: out[(a5 + co)*a4 + k] = w0[co][ci][tap] with k = tap*a3 + ci (ci < a1), else 0;
+ *                a0 = Cout, a1 = Cin, a2 = ntaps, a3 = Cpad, a4 = Kpad, a5 = row0; count Cout*Kpad
+ *  PACK_T3    1: dfcsa_pack_t3 semantics; a0 = Cin rows, a1 = Kpad, a2 = wcin, a3..a5 = Cout_0..2,
+ *                a6 = ntaps_0 (segments 1, 2 have one tap), a7 = identity2; count Cin*Kpad
+ *  CONVT_FWD  2: out[(ij*a1 + co)*a2 + ci] = w0[ci][co][ij] (ci < a0), zero to Kpad a2
+ *  CONVT_BWD  3: out[ci*a2 + ij*a1 + co] = w0[ci][co][ij], zero to Kpad a2
+ *  CONCAT     4: fp32 out[i] = w0[i] (i < a0), w1[i - a0] (< a0 + a1), w2[...] (< a0+a1+a2), else 0
+ *                up to a3 = count
+ *  BIAS4      5: fp32 out[ij*a0 + co] = w0[co]; count 4*a0
+ * dtype: element type of `out` for kinds 0-3. */
+#define DFCSA_PACK_ROWS 0
+#define DFCSA_PACK_T3 1
+#define DFCSA_PACK_CONVT_FWD 2
+#define DFCSA_PACK_CONVT_BWD 3
+#define DFCSA_PACK_CONCAT 4
+#define DFCSA_PACK_BIAS4 5
+typedef struct {
+  int64_t start, count;
+  int kind, dtype;
+  const float* w0;
+  const float* w1;
+  const float* w2;
+  void* out;
+  int a[8];
+} dfcsa_pack_entry;
+int dfcsa_pack_plan(const dfcsa_pack_entry* table_dev, int n, int64_t total, void* stream);
+
 /* zero-fill (used for padded weight rows) */
 int dfcsa_zero(void* p, int64_t bytes, void* stream);
 
@@ -291,6 +322,10 @@ int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const float* parti
 #define DFCSA_PROF_WGRAD 2
 int dfcsa_prof_enable(int kernel_class, int enable);
 int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, double* flops);
+
+/* Tuning knobs (benchmarking/autotuning only; 0 = automatic choice).
+ * knob 1: conv_gemm tile configuration (see conv_gemm.hip, kConvCfgs). */
+int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);
 

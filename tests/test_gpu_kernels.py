@@ -232,3 +232,32 @@ def test_head_fwd_bwd(dtype, tol, C, Cout):
     assert rel(nchw(xh.grad), xr.grad) < tol
     assert rel(modg.weight.grad, mod.weight.grad) < max(tol, 1e-5)
     assert rel(modg.bias.grad, mod.bias.grad) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,Cs,nsrc,C,k3", [(8, 128, 64, 1, 64, False),    # 256x64 LDS-DMA tile
+                                              (4, 128, 64, 1, 256, False),   # 256x128 tile
+                                              (4, 128, 16, 2, 128, True),    # 256x128, 3x3, 2 sources
+                                              (2, 96, 8, 1, 64, True)])      # Cseg 8 < K stage
+def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3):
+    dtype = torch.bfloat16
+    torch.manual_seed(9)
+    xs = [q(torch.randn(B, Cs, H, H), dtype) for _ in range(nsrc)]
+    ks = 3 if k3 else 1
+    w = q(torch.randn(C, nsrc * Cs, ks, ks) * 0.1, dtype)
+    b = torch.randn(C)
+    ref = F.conv2d(torch.cat(xs, 1), w, b, padding=ks // 2)
+    taps = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)] if k3 else [(0, 0)]
+    Kp = ops.rup(len(taps) * nsrc * Cs, ops.KALIGN)
+    wp = ops.pack_conv_w(dtype, w.cuda(), nsrc * Cs, Kp)
+    M = B * H * H
+    y = torch.empty((B, H, H, C), dtype=dtype, device="cuda")
+    stats = torch.empty(ops.ntiles_gemm(M) * 2 * C, device="cuda")
+    xh = [nhwc(x, dtype) for x in xs]
+    segs = [(x, dh, dw) for dh, dw in taps for x in xh]
+    ops.conv_gemm(dtype, segs, Cs, (B, H, H), (H, H), wp, Kp, C, [y], C, bias=b.cuda(), stats=stats)
+    torch.cuda.synchronize()
+    assert rel(nchw(y), ref) < 1e-2
+    st = stats.view(-1, 2, C).sum(0).cpu()
+    acc = ref - b.view(1, -1, 1, 1)
+    assert rel(st[0], acc.sum((0, 2, 3))) < 1e-4
+    assert rel(st[1], (acc * acc).sum((0, 2, 3))) < 1e-4
