@@ -410,8 +410,9 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   }
 }
 
+// out[c] += sum_t slab[t][c]; columns split over up to three destinations at n0, n0 + n1
 __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int C,
-                                                           float* out) {
+                                                           int n0, int n1, float* d0, float* d1, float* d2) {
   __shared__ double r[16][64];
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
@@ -422,7 +423,9 @@ __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restri
   __syncthreads();
   if (part == 0 && c < C) {
     for (int p = 1; p < 16; ++p) s += r[p][cl];
-    out[c] += (float)s;
+    if (c < n0) d0[c] += (float)s;
+    else if (c < n0 + n1) d1[c - n0] += (float)s;
+    else d2[c - n0 - n1] += (float)s;
   }
 }
 
@@ -610,7 +613,17 @@ extern "C" int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const
 extern "C" int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream) {
   if (C <= 0 || ntiles <= 0) return DFCSA_EINVAL;
   hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, ntiles,
-                     C, out);
+                     C, C, 0, out, nullptr, nullptr);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, int n1, float* d0, float* d1,
+                                  float* d2, void* stream) {
+  if (C <= 0 || ntiles <= 0 || n0 < 0 || n1 < 0 || n0 + n1 > C || !d0 || (n1 && !d1) || (n0 + n1 < C && !d2))
+    return DFCSA_EINVAL;
+  hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, ntiles,
+                     C, n0, n1, d0, d1, d2);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

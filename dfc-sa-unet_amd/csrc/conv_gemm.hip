@@ -506,5 +506,6 @@ extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }
 
 extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 1) { g_conv_cfg = value; return 0; }
+  if (knob == 2) { g_wgrad_target = value > 0 ? value : 512; return 0; }
   return DFCSA_EINVAL;
 }

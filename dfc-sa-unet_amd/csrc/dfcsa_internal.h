@@ -43,3 +43,5 @@ struct ProfScope {
   ProfScope(int cls, hipStream_t st, double flops);
   ~ProfScope();
 };
+
+extern int g_wgrad_target;

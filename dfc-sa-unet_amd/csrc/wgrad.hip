@@ -240,6 +240,11 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     if (cin >= Creal) return;
     float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
     dst[((int64_t)r * Creal + cin) * ntaps + tap] += s;
+  } else if (layout == 2) {
+    // 1x1 weights stacked by rows: [0, Ctot) -> d0, [Ctot, 2 Ctot) -> d1, [2 Ctot, NI) -> d2
+    const int d = i < Ctot ? 0 : (i < 2 * Ctot ? 1 : 2);
+    float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
+    dst[(int64_t)(i - d * Ctot) * NJ + j] += s;
   } else {
     // ConvTranspose2d weight [Cin][Cout][2][2]; i = ci, j = ij*Cout + co (Ctot = Cout)
     int ij = j / Ctot, co = j - ij * Ctot;
@@ -258,12 +263,16 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
+
 extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk) {
   if (M <= 0 || NI <= 0 || NJ <= 0 || !splits || !mchunk) return DFCSA_EINVAL;
   const int kms = dtype == DFCSA_DT_BF16 ? 64 : 32;
   const int BI = NI <= 64 ? 64 : 128;
   const int tiles = ((NI + BI - 1) / BI) * ((NJ + 127) / 128);
-  int s = 1024 / tiles;
+  // splits trade occupancy against split-K slab traffic (each split writes NI*NJ fp32 that the
+  // reduce reads back): ~2 workgroups per CU is enough to keep the MFMA pipes busy
+  int s = g_wgrad_target / tiles;
   if (s < 1) s = 1;
   int max_s = M / (4 * kms);  // keep >= 4 stages per chunk
   if (max_s < 1) max_s = 1;
@@ -305,7 +314,8 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
 
 extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                                   int Ctot, int Creal, int ndst, float* const* dst, void* stream) {
-  if (!slab || !dst || ndst < 1 || ndst > 3 || NI % ndst) return DFCSA_EINVAL;
+  if (!slab || !dst || ndst < 1 || ndst > 3) return DFCSA_EINVAL;
+  if (layout == 2 ? (ndst != 3 || Ctot <= 0 || 2 * Ctot > NI) : (NI % ndst != 0)) return DFCSA_EINVAL;
   int64_t total = (int64_t)NI * NJ;
   int blocks = (int)((total + 255) / 256);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, splits,

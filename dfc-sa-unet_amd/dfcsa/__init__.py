@@ -9,7 +9,21 @@ missing.  Public pieces:
   dfcsa.optim       fused clip_grad_norm_ + momentum SGD
   dfcsa.ddp         data parallelism over RCCL (torch.distributed 'nccl' backend)
 """
+import os
+
+from ._lib import LIB as _LIB
 from ._lib import version  # noqa: F401
+
+
+def set_tuning(knob, value):
+    """Benchmark-only kernel selection overrides (include/dfcsa.h, dfcsa_set_tuning)."""
+    if _LIB.dfcsa_set_tuning(int(knob), int(value)) != 0:
+        raise ValueError(f"unknown tuning knob {knob}")
+
+
+for _kv in filter(None, os.environ.get("DFCSA_TUNE", "").split(",")):   # e.g. DFCSA_TUNE=2=1024
+    _k, _v = _kv.split("=")
+    set_tuning(_k, _v)
 
 PRECISIONS = {"bf16": "bfloat16", "bfloat16": "bfloat16", "fp32": "float32", "float32": "float32"}
 

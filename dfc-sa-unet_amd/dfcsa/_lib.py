@@ -77,6 +77,12 @@ class WgradDesc(ctypes.Structure):
                 ("mchunk", ctypes.c_int)]
 
 
+class PackEntry(ctypes.Structure):
+    _fields_ = [("start", ctypes.c_int64), ("count", ctypes.c_int64), ("kind", ctypes.c_int), ("dtype", ctypes.c_int),
+                ("w0", ctypes.c_void_p), ("w1", ctypes.c_void_p), ("w2", ctypes.c_void_p), ("out", ctypes.c_void_p),
+                ("a", ctypes.c_int * 8)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(

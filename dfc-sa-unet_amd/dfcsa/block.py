@@ -23,6 +23,7 @@ from . import ops
 from ._lib import call
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
+from .packs import get_packset, param_key
 
 
 def grad_of(p):
@@ -61,21 +62,14 @@ def block_forward(blk, xs, pool_size, training, dtype):
     nt = ops.ntiles_gemm(M)
     s = _Saved()
 
-    # ---- weights -> GEMM operands (fp32 master -> dtype) ----
-    Kp1 = rup(9 * Cin_p, ops.KALIGN)
-    W1p = ops.pack_conv_w(dtype, conv1.weight, Cin_p, Kp1)
+    # ---- weights -> persistent GEMM operands (one pack-plan launch per forward) ----
     N2 = 2 * C if has_res else C
-    Kp2 = rup(Cin_p, ops.KALIGN)
-    W2p = torch.empty((N2, Kp2), dtype=dtype, device=dev)
-    ops.pack_conv_w(dtype, conv2.weight, Cin_p, Kp2, out=W2p, row0=0)
-    if has_res:
-        ops.pack_conv_w(dtype, blk.residual_conv.weight, Cin_p, Kp2, out=W2p, row0=C)
-        b2 = torch.cat([conv2.bias.detach(), torch.zeros(C, device=dev)])
-    else:
-        b2 = conv2.bias
+    Kp1, Kp2 = rup(9 * Cin_p, ops.KALIGN), rup(Cin_p, ops.KALIGN)
     Kp3, Kp4 = rup(2 * C, ops.KALIGN), rup(3 * C, ops.KALIGN)
-    W3p = ops.pack_conv_w(dtype, conv3.weight, 2 * C, Kp3)
-    W4p = ops.pack_conv_w(dtype, conv4.weight, 3 * C, Kp4)
+    pk = get_packset(blk, (dtype, nsrc, Cs, param_key(blk)),
+                     lambda ps: _build_block_packs(ps, blk, dtype, Cin_p, C, has_res))
+    W1p, W2p, W3p, W4p = pk["W1p"], pk["W2p"], pk["W3p"], pk["W4p"]
+    b2 = pk["b2"] if has_res else conv2.bias
 
     def stats(n):
         return torch.empty(nt * 2 * n, device=dev, dtype=torch.float32) if training else None
@@ -97,7 +91,7 @@ def block_forward(blk, xs, pool_size, training, dtype):
     Pp = pool_size
     Cq = lsa.query_conv.out_channels
     J, N = 2 * Cq + C, Pp * Pp
-    pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype)
+    pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
 
     local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
@@ -127,7 +121,46 @@ def block_forward(blk, xs, pool_size, training, dtype):
     s.y1, s.y2, s.res, s.local, s.attn, s.y3, s.fused, s.y4 = y1, y2, res, local, attn, y3, fused, y4
     s.bn = (bn1, bn2, bn3, bn4)
     s.pooled, s.qkv, s.A, s.o, s.Wqkv = pooled, qkv, A, o, Wqkv
+    s.pk = pk
     return out, s
+
+
+def _build_block_packs(ps, blk, dtype, Cin_p, C, has_res):
+    """Entries of one DFC block: forward operands, transposed dgrad operands, LSA projections."""
+    conv1, conv2, conv3, conv4 = blk.conv_branch[0], blk.attn_branch[0], blk.gate[0], blk.fusion_conv[0]
+    N2 = 2 * C if has_res else C
+    Kp2 = rup(Cin_p, ops.KALIGN)
+    ps.rows("W1p", dtype, conv1.weight, Cin_p, rup(9 * Cin_p, ops.KALIGN))
+    ps.rows("W2p", dtype, conv2.weight, Cin_p, Kp2, row0=0, rows=N2)
+    if has_res:
+        ps.rows("W2p", dtype, blk.residual_conv.weight, Cin_p, Kp2, row0=C)
+        ps.concat("b2", [conv2.bias], N2)
+    ps.rows("W3p", dtype, conv3.weight, 2 * C, rup(2 * C, ops.KALIGN))
+    ps.rows("W4p", dtype, conv4.weight, 3 * C, rup(3 * C, ops.KALIGN))
+    KpC = rup(C, ops.KALIGN)
+    ps.t3("W4t", dtype, 3 * C, KpC, [conv4.weight])
+    ps.t3("W3t", dtype, 2 * C, KpC, [conv3.weight])
+    ps.t3("Wdx", dtype, Cin_p, rup(11 * C, ops.KALIGN),
+          [conv1.weight, conv2.weight, blk.residual_conv.weight if has_res else None], identity_last=not has_res)
+    _build_lsa_packs(ps, blk.attn_branch[3])
+
+
+def _build_lsa_packs(ps, lsa):
+    f32 = torch.float32
+    C = lsa.value_conv.out_channels
+    Cq = lsa.query_conv.out_channels
+    J = 2 * Cq + C
+    qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
+    ps.concat("bqkv", [lsa.query_conv.bias, lsa.key_conv.bias, lsa.value_conv.bias], J)
+    if _lsa_gemm_ok(C, J):
+        Kp = rup(C, ops.KALIGN)
+        for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
+            ps.rows("Wp", f32, w, C, Kp, row0=off, rows=J)
+        ps.t3("WT", f32, C, rup(J, ops.KALIGN), [qw, kw, vw])
+    else:
+        for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
+            ps.rows("Wqkv", f32, w, C, C, row0=off, rows=J)
+        ps.t3("WqkvT", f32, C, J, [qw, kw, vw])
 
 
 def block_backward(blk, s, dout, need_dx, dtype):
@@ -160,7 +193,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
     ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                         [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     KpC = rup(C, ops.KALIGN)
-    W4t = ops.pack_t3(dtype, 3 * C, KpC, [conv4.weight])
+    W4t = s.pk["W4t"]
     dfused = torch.empty_like(s.y4)
     dlocal = torch.empty_like(s.y4)
     dattn = torch.empty_like(s.y4)
@@ -178,12 +211,12 @@ def block_backward(blk, s, dout, need_dx, dtype):
     del dz3
     ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                         [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
-    W3t = ops.pack_t3(dtype, 2 * C, KpC, [conv3.weight])
+    W3t = s.pk["W3t"]
     ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
 
     # ---- LightSelfAttention ----
-    dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype)
+    dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
 
     # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
     dz2 = torch.empty_like(s.y2)
@@ -218,9 +251,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
 
     # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM ----
     Kx = rup(11 * C, ops.KALIGN)
-    Wdx = ops.pack_t3(dtype, Cin_p, Kx, [conv1.weight, conv2.weight,
-                                         blk.residual_conv.weight if has_res else None],
-                      identity_last=not has_res)  # identity residual: an identity weight block
+    Wdx = s.pk["Wdx"]  # [W1^T | W2^T | Wres^T or I] side by side
     segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dy2, 0, 0), (dres, 0, 0)]
     dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
     ops.conv_gemm(dtype, segs, C, grid, hw, Wdx, Kx, Cin_p, dxs, Cs)
@@ -231,7 +262,7 @@ def _lsa_gemm_ok(C, J):
     return C % 8 == 0 and J % 8 == 0 and C >= 64
 
 
-def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
+def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk):
     """LightSelfAttention up to the pooled output o (unet_dfc_sa_res.py:24-34): pool of
     act(y*scale + shift) -> q/k/v 1x1 convs -> softmax(q k^T) -> o = v A^T (all fp32)."""
     B, H, W, C = y.shape
@@ -244,25 +275,18 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
     S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
     call("dfcsa_lsa_pool", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), stream())
-    bqkv = torch.cat([lsa.query_conv.bias.detach(), lsa.key_conv.bias.detach(), lsa.value_conv.bias.detach()])
+    bqkv = pk["bqkv"]
     pooled = torch.empty((B, N, C), device=dev, dtype=f32)
     qkv = torch.empty((B, N, J), device=dev, dtype=f32)
-    ws = ((lsa.query_conv.weight, 0), (lsa.key_conv.weight, Cq), (lsa.value_conv.weight, 2 * Cq))
     if _lsa_gemm_ok(C, J):
         # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
         call("dfcsa_lsa_pooled", B, H, W, C, Pp, P(part), P(pooled), stream())
         Kp = rup(C, ops.KALIGN)
-        Wp = torch.empty((J, Kp), device=dev, dtype=f32)
-        for w, off in ws:
-            ops.pack_conv_w(f32, w, C, Kp, out=Wp, row0=off)
+        Wp = pk["Wp"]
         ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), Wp, Kp, J, [qkv], J, bias=bqkv)
         Wqkv = None
     else:
-        Wqkv = torch.empty((J, C), device=dev, dtype=f32)
-        WqkvT = torch.empty((C, J), device=dev, dtype=f32)
-        for w, off in ws:
-            ops.pack_conv_w(f32, w, C, C, out=Wqkv, row0=off)
-            ops.pack_conv_w_t(f32, w, J, WqkvT, col0=off)
+        Wqkv, WqkvT = pk["Wqkv"], pk["WqkvT"]
         call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
     A = torch.empty((B, N, N), device=dev, dtype=f32)
     o = torch.empty((B, N, C), device=dev, dtype=f32)
@@ -270,7 +294,7 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype):
     return pooled, qkv, A, o, Wqkv
 
 
-def lsa_core_backward(lsa, saved, dattn, pool_size, dtype):
+def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
     """Backward of gamma * bilinear(o) (unet_dfc_sa_res.py:36-38) through the attention core;
     accumulates gamma/q/k/v parameter gradients and returns d(pooled) [B][N][C] fp32."""
     pooled, qkv, A, o, Wqkv = saved
@@ -294,18 +318,14 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype):
     qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
     if _lsa_gemm_ok(C, J):
         BN = B * N
-        # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums, dpooled = dqkv Wqkv
+        # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums, dpooled = dqkv Wqkv;
+        # the stacked q/k/v rows go straight into the three weight / bias gradients
         slab, splits, NI, NJ = ops.wgrad(f32, [dqkv], J, [(pooled, 0, 0)], C, (1, BN, 1), (BN, 1))
-        dW = torch.zeros((J, C), device=dev, dtype=f32)
-        ops.wgrad_reduce(slab, splits, NI, NJ, 0, 1, C, C, [dW])
-        db = torch.zeros(J, device=dev, dtype=f32)
-        ops.channel_sum_into(f32, dqkv, db)
-        for w, b, lo, hi in ((qw, lsa.query_conv.bias, 0, Cq), (kw, lsa.key_conv.bias, Cq, 2 * Cq),
-                             (vw, lsa.value_conv.bias, 2 * Cq, J)):
-            grad_of(w).add_(dW[lo:hi].view_as(w))
-            grad_of(b).add_(db[lo:hi])
+        ops.wgrad_reduce(slab, splits, NI, NJ, 2, 1, Cq, C, [grad_of(qw), grad_of(kw), grad_of(vw)])
+        call("dfcsa_slab_colsum3", P(dqkv), BN, J, Cq, Cq, P(grad_of(lsa.query_conv.bias)),
+             P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)), stream())
         Kj = rup(J, ops.KALIGN)
-        WT = ops.pack_t3(f32, C, Kj, [qw, kw, vw])
+        WT = pk["WT"]
         ops.conv_gemm(f32, [(dqkv, 0, 0)], J, (1, BN, 1), (BN, 1), WT, Kj, C, [dpooled], C)
     else:
         call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
@@ -323,12 +343,13 @@ class LSAFunction(torch.autograd.Function):
         dev = x.device
         one = torch.ones(C, device=dev)
         zero = torch.zeros(C, device=dev)
-        saved = lsa_core_forward(lsa, x, one, zero, False, pool_size, dtype)
+        pk = get_packset(lsa, ("lsa", param_key(lsa)), lambda ps: _build_lsa_packs(ps, lsa))
+        saved = lsa_core_forward(lsa, x, one, zero, False, pool_size, dtype, pk)
         out = torch.empty_like(x)
         call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, None, None, None, P(x), P(one), P(zero),
              P(saved[3]), pool_size, P(lsa.gamma), 0, None, P(out), stream())
         ctx.lsa, ctx.saved, ctx.ps, ctx.dtype, ctx.np = lsa, saved, pool_size, dtype, len(params)
-        ctx.x = x
+        ctx.x, ctx.pk = x, pk
         return out
 
     @staticmethod
@@ -337,7 +358,7 @@ class LSAFunction(torch.autograd.Function):
         x = ctx.x
         B, H, W, C = x.shape
         dev = x.device
-        dpooled = lsa_core_backward(ctx.lsa, ctx.saved, g, ctx.ps, ctx.dtype)
+        dpooled = lsa_core_backward(ctx.lsa, ctx.saved, g, ctx.ps, ctx.dtype, ctx.pk)
         one = torch.ones(C, device=dev)
         zero = torch.zeros(C, device=dev)
         dx = torch.empty_like(x)

@@ -13,6 +13,7 @@ from ._lib import call
 from .block import grad_of
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
+from .packs import get_packset, param_key
 
 
 class InputToNHWC(torch.autograd.Function):
@@ -60,17 +61,9 @@ class ConvTranspose2x2(torch.autograd.Function):
         Cout = mod.out_channels
         dev = x.device
         Kf = rup(Cin, ops.KALIGN)
-        Wf = torch.zeros((4 * Cout, Kf), dtype=dtype, device=dev)
         Kb = rup(4 * Cout, ops.KALIGN)
-        Wb = torch.zeros((Cin, Kb), dtype=dtype, device=dev)
-        b4 = torch.empty(4 * Cout, dtype=torch.float32, device=dev)
-        # pack writes rows of Cin (fwd) / 4*Cout (bwd) columns; the zero tails pad K
-        Wf_v = torch.empty((4 * Cout, Cin), dtype=dtype, device=dev)
-        Wb_v = torch.empty((Cin, 4 * Cout), dtype=dtype, device=dev)
-        call("dfcsa_pack_convT_w", dt(dtype), P(mod.weight), P(mod.bias), Cin, Cout, P(Wf_v), P(Wb_v), P(b4),
-             stream())
-        Wf[:, :Cin] = Wf_v
-        Wb[:, :4 * Cout] = Wb_v
+        pk = get_packset(mod, (dtype, param_key(mod)), lambda ps: ps.convT(dtype, mod.weight, mod.bias, Kf, Kb))
+        Wf, Wb, b4 = pk["Wf"], pk["Wb"], pk["b4"]
         out = torch.empty((B, 2 * h, 2 * w, Cout), dtype=dtype, device=dev)
         ops.conv_gemm(dtype, [(x, 0, 0)], Cin, (B, h, w), (h, w), Wf, Kf, 4 * Cout, [out], Cout, bias=b4,
                       mode=1, out_hw=(2 * h, 2 * w))

@@ -16,6 +16,7 @@ import torch
 import torch.nn as nn
 
 import dfcsa
+from dfcsa import packs
 from dfcsa.block import DFCBlockFunction, LSAFunction
 from dfcsa.flat import FlatParams
 from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPool2x2, ResizeBilinear
@@ -138,6 +139,7 @@ class UNetDFCSA(nn.Module):
     def _apply(self, fn, *args, **kwargs):
         out = super()._apply(fn, *args, **kwargs)
         self._flat = None  # parameters moved: re-flatten lazily on the next forward
+        self._dfcsa_plan = None
         return out
 
     def flat_params(self):
@@ -169,6 +171,9 @@ class UNetDFCSA(nn.Module):
         if torch.is_grad_enabled():
             flat.attach_grads()
         dt = self.compute_dtype
+        if getattr(self, "_plan_flat", None) is not flat:  # parameter storage changed: stale plan
+            self._dfcsa_plan, self._plan_flat = None, flat
+        planned = packs.sync_model_plan(self)  # one launch packs every conv operand of the model
         mp = lambda t: MaxPool2x2.apply(t, dt)  # noqa: E731
         h = _nchw_to_nhwc(x, dt)
         d1 = self.down1.forward_nhwc([h], dt)
@@ -182,7 +187,10 @@ class UNetDFCSA(nn.Module):
             if u.shape[1:3] != skip.shape[1:3]:
                 u = ResizeBilinear.apply(u, tuple(skip.shape[1:3]), dt)
             u = block.forward_nhwc([u, skip], dt)  # cat([up, skip]) order, never materialised
-        return Head1x1.apply(u, self.final_conv, dt, *self.final_conv.parameters())
+        logits = Head1x1.apply(u, self.final_conv, dt, *self.final_conv.parameters())
+        if not planned:
+            packs.rebuild_model_plan(self, x.device)
+        return logits
 
 
 class UNetDFCSARes(UNetDFCSA):

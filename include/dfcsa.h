@@ -88,7 +88,9 @@ int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
 /* grad += sum_s slab[s] mapped to the reference weight layout.
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
  *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.
- *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij]. */
+ *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij].
+ *  layout 2 (stacked 1x1 q/k/v): rows [0,Ctot) -> dst[0], [Ctot,2Ctot) -> dst[1], rest -> dst[2];
+ *     dst[d][row - base][j] with NJ columns (ndst must be 3). */
 int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                        int Ctot, int Creal, int ndst, float* const* dst, void* stream);
 
@@ -223,6 +225,9 @@ int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, c
 int dfcsa_rows_reduce(const float* src, int T, int rowlen, float* dst, int G, void* stream);
 /* out[c] += sum_t slab[t][c]  (ntiles x C); fp64 accumulation */
 int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream);
+/* as dfcsa_slab_colsum with columns [0,n0) -> d0, [n0,n0+n1) -> d1, [n0+n1,C) -> d2 */
+int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, int n1, float* d0, float* d1, float* d2,
+                       void* stream);
 /* per-channel partial sums of an NHWC tensor -> partial [ntiles][C] */
 int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, void* stream);
 
@@ -324,7 +329,8 @@ int dfcsa_prof_enable(int kernel_class, int enable);
 int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, double* flops);
 
 /* Tuning knobs (benchmarking/autotuning only; 0 = automatic choice).
- * knob 1: conv_gemm tile configuration (see conv_gemm.hip, kConvCfgs). */
+ * knob 1: conv_gemm tile configuration (see conv_gemm.hip, launch_t).
+ * knob 2: target workgroups per weight-gradient launch (split-K count = target / tiles). */
 int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);

@@ -261,3 +261,49 @@ def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3):
     acc = ref - b.view(1, -1, 1, 1)
     assert rel(st[0], acc.sum((0, 2, 3))) < 1e-4
     assert rel(st[1], (acc * acc).sum((0, 2, 3))) < 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_pack_plan_matches_single_packs(dtype):
+    """One dfcsa_pack_plan launch reproduces the per-weight pack kernels bit for bit."""
+    from dfcsa import _lib
+    from dfcsa.packs import PackSet
+    dev = "cuda"
+    g = torch.Generator(device="cpu").manual_seed(5)
+    r = lambda *s: torch.randn(*s, generator=g).to(dev)  # noqa: E731
+    C, Cin, Cq = 64, 40, 8
+    w3, w1, wr = r(C, Cin, 3, 3), r(C, Cin, 1, 1), r(C, Cin, 1, 1)
+    w4 = r(C, 3 * C, 1, 1)
+    wT, bT = r(96, 32, 2, 2), r(32)
+    b = r(C)
+    ps = PackSet(("t",), torch.device(dev))
+    ps.rows("W1p", dtype, w3, 48, ops.rup(9 * 48, 64))
+    ps.rows("W2p", dtype, w1, 48, 64, row0=0, rows=2 * C)
+    ps.rows("W2p", dtype, wr, 48, 64, row0=C)
+    ps.t3("Wdx", dtype, 48, ops.rup(11 * C, 64), [w3, w1, wr])
+    ps.t3("Wid", dtype, C, ops.rup(11 * C, 64), [r(C, C, 3, 3), r(C, C, 1, 1), None], identity_last=True)
+    ps.t3("W4t", dtype, 3 * C, 64, [w4])
+    ps.concat("b2", [b], 2 * C)
+    ps.convT(dtype, wT, bT, 128, 128)
+    ps.run()
+    torch.cuda.synchronize()
+    want = ops.pack_conv_w(dtype, w3, 48, ops.rup(9 * 48, 64))
+    assert torch.equal(ps["W1p"], want)
+    w2 = torch.empty((2 * C, 64), dtype=dtype, device=dev)
+    ops.pack_conv_w(dtype, w1, 48, 64, out=w2, row0=0)
+    ops.pack_conv_w(dtype, wr, 48, 64, out=w2, row0=C)
+    assert torch.equal(ps["W2p"], w2)
+    assert torch.equal(ps["Wdx"], ops.pack_t3(dtype, 48, ops.rup(11 * C, 64), [w3, w1, wr]))
+    assert torch.equal(ps["W4t"], ops.pack_t3(dtype, 3 * C, 64, [w4]))
+    wid = ps["Wid"].float()
+    assert torch.equal(wid[:, 10 * C:11 * C], torch.eye(C, device=dev))
+    assert torch.equal(ps["b2"][:C], b) and not ps["b2"][C:].any()
+    fv = torch.empty((4 * 32, 96), dtype=dtype, device=dev)
+    bv = torch.empty((96, 128), dtype=dtype, device=dev)
+    b4 = torch.empty(128, device=dev)
+    _lib.call("dfcsa_pack_convT_w", ops.dt(dtype), ops.P(wT), ops.P(bT), 96, 32, ops.P(fv), ops.P(bv), ops.P(b4),
+              ops.stream())
+    assert torch.equal(ps["Wf"][:, :96], fv) and not ps["Wf"][:, 96:].float().any()
+    assert torch.equal(ps["Wb"], bv)
+    assert torch.equal(ps["b4"], b4)
