@@ -29,6 +29,17 @@ class FusedSGD(torch.optim.Optimizer):
         self._partial = None
         self.last_norm = None
 
+    @classmethod
+    def from_torch_sgd(cls, opt):
+        """The fused equivalent of a ``torch.optim.SGD`` built as in the reference's train.py:73-78
+        (one group, no dampening/nesterov); None if the optimizer is something else."""
+        if type(opt) is not torch.optim.SGD or len(opt.param_groups) != 1:
+            return None
+        g = opt.param_groups[0]
+        if g.get("dampening", 0.0) or g.get("nesterov", False) or g.get("maximize", False) or any(opt.state.values()):
+            return None
+        return cls(g["params"], lr=g["lr"], momentum=g["momentum"], weight_decay=g["weight_decay"])
+
     # ------------------------------------------------------------------ helpers
     def _resolve(self):
         params = self.param_groups[0]["params"]

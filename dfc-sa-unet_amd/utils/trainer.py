@@ -11,7 +11,8 @@ On the MI355X path the step is device-resident (``train_step``): the NaN check s
 update on the device and the metrics stay on the device; the epoch loop reads them back once
 per batch for the running averages, as the reference's ``.item()`` calls do.  With a
 ``dfcsa.optim.FusedSGD`` optimizer, clipping + SGD is one fused pass; with any other
-torch optimizer the reference's clip_grad_norm_ + step() are called.
+torch optimizer the reference's clip_grad_norm_ + step() are called.  A plain
+``torch.optim.SGD`` (what the reference's train.py builds) is converted to FusedSGD.
 
 Differences kept deliberately small and listed: plots are written only when matplotlib is
 importable; best/worst validation samples are kept (tensors on the host) but image dumps
@@ -41,7 +42,9 @@ class Trainer:
         self.config = config
         self.device = device
         self.model = model.to(device)
-        self.optimizer = optimizer
+        # the reference's train.py builds torch.optim.SGD(model.parameters(), ...): run it as the
+        # fused device pass (same update; clip_grad_norm_ included)
+        self.optimizer = FusedSGD.from_torch_sgd(optimizer) or optimizer
         self.train_loader = train_loader
         self.val_loader = val_loader
         self.loss_type = config["training"].get("loss", {}).get("type", "dice")

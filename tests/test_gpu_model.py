@@ -188,3 +188,38 @@ def test_model_bf16_vs_reference():
     r = torch.cat([torch.from_numpy(fx["step1.grad." + n]).flatten().double() for n in names])
     cos = (g @ r / (g.norm() * r.norm())).item()  # fixture grads are post-clip: compare directions
     assert cos > 0.90, cos
+
+
+def test_trainer_reference_style_epoch(tmp_path):
+    """The reference's train.py wiring (torch.optim.SGD + Trainer over dict batches) runs the fused
+    device step and reproduces the reference's two steps; checkpoint save/load round-trips."""
+    from utils.trainer import Trainer
+    from dfcsa.optim import FusedSGD
+    model, fx = make_model("fp32")
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    cfg = {"training": {"num_epochs": 1, "save_checkpoint_freq": 1, "loss": {"type": "bce_dice", "params": LP}},
+           "logging": {"log_dir": str(tmp_path / "logs"), "images_dir": str(tmp_path / "img"),
+                       "save_best_worst_samples": 1}}
+    batches = [{"image": torch.from_numpy(np.asarray(fx[f"x{s}"])).float(),
+                "mask": torch.from_numpy(np.asarray(fx[f"t{s}"])).float(),
+                "filename": [f"a{s}", f"b{s}"]} for s in (1, 2)]
+    tr = Trainer(model, batches, batches[:1], opt, torch.device("cuda"), cfg)
+    assert isinstance(tr.optimizer, FusedSGD)
+    loss, iou, dice = tr.train_epoch(0)
+    torch.cuda.synchronize()
+    want = (float(fx["loss1"]) + float(fx["loss2"])) / 2
+    assert abs(loss - want) < 1e-4 * abs(want)
+    assert abs(dice - (float(fx["dice1"]) + float(fx["dice2"])) / 2) < 1e-6
+    sd = model.state_dict()
+    for k, v in sd_from(fx, "sd2.").items():
+        assert rel(sd[k].float(), v.float()) < 1e-4, k
+    va = tr.validate_epoch(batches[:1])
+    assert len(va["best_samples"]) == 1 and len(va["worst_samples"]) == 1
+    tr.save_checkpoint(0, va, is_best=True)
+    model2, _ = make_model("fp32")
+    opt2 = FusedSGD(model2.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    tr2 = Trainer(model2, batches, batches[:1], opt2, torch.device("cuda"), cfg)
+    ep = tr2.load_checkpoint(str(tmp_path / "logs" / "checkpoints" / "checkpoint_epoch_1.pth"))
+    assert ep == 0
+    for k, v in model.state_dict().items():
+        assert torch.equal(model2.state_dict()[k], v), k
