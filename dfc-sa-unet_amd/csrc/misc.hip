@@ -421,81 +421,79 @@ __global__ void pack_convT_kernel(const float* __restrict__ w, const float* __re
 }
 
 // ---------------------------------------------------------------- one-launch pack plan
+// One workgroup per task; an entry owns tasks [start, start + count).  Entries are few (~150),
+// tasks many, so the entry lookup is a binary search per workgroup.
+__device__ __forceinline__ float load_as(const void* p, int64_t i, int dtype) {
+  return dtype == DFCSA_DT_BF16 ? bf2f(((const bf16_t*)p)[i]) : ((const float*)p)[i];
+}
 __device__ __forceinline__ void store_as(void* out, int64_t i, int dtype, float v) {
   if (dtype == DFCSA_DT_BF16) ((bf16_t*)out)[i] = f2bf(v);
   else ((float*)out)[i] = v;
 }
 
-__global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* __restrict__ tab, int n,
-                                                        int64_t total) {
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    int lo = 0, hi = n - 1;  // last entry with start <= e
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (tab[mid].start <= e) lo = mid; else hi = mid - 1;
+__global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* __restrict__ tab, int n) {
+  __shared__ float tile[64][65];
+  const int64_t task = blockIdx.x;
+  int lo = 0, hi = n - 1;  // last entry with start <= task
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (tab[mid].start <= task) lo = mid; else hi = mid - 1;
+  }
+  const dfcsa_pack_entry& t = tab[lo];
+  const int64_t tl = task - t.start;
+  if (tl >= t.count) return;
+  const int* a = t.a;
+  const int tid = threadIdx.x;
+  switch (t.kind) {
+    case DFCSA_PACK_ROWS: {
+      // out[(row0 + co)*Kpad + tap*Cpad + ci] = w[co][ci][tap]; the source row is contiguous
+      const int Cout = a[0], Cin = a[1], ntaps = a[2], Cpad = a[3], Kpad = a[4], row0 = a[5], per = a[6];
+      const int nrow = Cin * ntaps;
+      for (int r = 0; r < per; ++r) {
+        const int co = (int)tl * per + r;
+        if (co >= Cout) break;
+        const float* src = t.w0 + (size_t)co * nrow;
+        const int64_t ob = (int64_t)(row0 + co) * Kpad;
+        for (int e = tid; e < nrow; e += 256) {
+          const int tap = e / Cin, ci = e - tap * Cin;
+          store_as(t.out, ob + tap * Cpad + ci, t.dtype, src[ci * ntaps + tap]);
+        }
+      }
+      break;
     }
-    const dfcsa_pack_entry& t = tab[lo];
-    const int64_t i = e - t.start;
-    const int* a = t.a;
-    float v = 0.f;
-    switch (t.kind) {
-      case DFCSA_PACK_ROWS: {
-        const int Kpad = a[4], Cpad = a[3];
-        const int co = (int)(i / Kpad), k = (int)(i % Kpad);
-        const int tap = k / Cpad, ci = k - tap * Cpad;
-        if (tap < a[2] && ci < a[1]) v = t.w0[((size_t)co * a[1] + ci) * a[2] + tap];
-        store_as(t.out, (int64_t)(a[5] + co) * Kpad + k, t.dtype, v);
-        break;
+    case DFCSA_PACK_TRANSPOSE: {
+      // dst[c*ldd + r] = src[r*lds + c] for r < R, c < C (elements of `dtype`), 64x64 tiles
+      const int R = a[0], C = a[1], lds = a[2], ldd = a[3], tc = a[4];
+      const int r0 = (int)(tl / tc) * 64, c0 = (int)(tl % tc) * 64;
+      const int lane = tid & 63, q = tid >> 6;
+      for (int i = 0; i < 16; ++i) {
+        const int rr = r0 + i * 4 + q, cc = c0 + lane;
+        if (rr < R && cc < C) tile[i * 4 + q][lane] = load_as(t.w0, (int64_t)rr * lds + cc, t.dtype);
       }
-      case DFCSA_PACK_T3: {
-        const int Kpad = a[1], wcin = a[2], c0 = a[3], c1 = a[4], c2 = a[5], t0 = a[6];
-        const int ci = (int)(i / Kpad), k = (int)(i % Kpad);
-        const int e0 = t0 * c0, e1 = e0 + c1, e2 = e1 + c2;
-        if (k < e0) {
-          const int tap = k / c0, co = k - tap * c0;
-          if (ci < wcin) v = t.w0[((size_t)co * wcin + ci) * t0 + tap];
-        } else if (k < e1) {
-          if (ci < wcin) v = t.w1[(size_t)(k - e0) * wcin + ci];
-        } else if (k < e2) {
-          const int co = k - e1;
-          if (a[7]) v = (ci == co) ? 1.f : 0.f;
-          else if (ci < wcin) v = t.w2[(size_t)co * wcin + ci];
-        }
-        store_as(t.out, i, t.dtype, v);
-        break;
+      __syncthreads();
+      for (int i = 0; i < 16; ++i) {
+        const int cc = c0 + i * 4 + q, rr = r0 + lane;
+        if (rr < R && cc < C) store_as(t.out, (int64_t)cc * ldd + rr, t.dtype, tile[lane][i * 4 + q]);
       }
-      case DFCSA_PACK_CONVT_FWD: {
-        const int Cin = a[0], Cout = a[1], Kp = a[2];
-        const int r = (int)(i / Kp), ci = (int)(i % Kp);
-        const int ij = r / Cout, co = r - ij * Cout;
-        if (ci < Cin) v = t.w0[((size_t)ci * Cout + co) * 4 + ij];
-        store_as(t.out, i, t.dtype, v);
-        break;
-      }
-      case DFCSA_PACK_CONVT_BWD: {
-        const int Cin = a[0], Cout = a[1], Kp = a[2];
-        const int ci = (int)(i / Kp), k = (int)(i % Kp);
-        if (k < 4 * Cout && ci < Cin) {
-          const int ij = k / Cout, co = k - ij * Cout;
-          v = t.w0[((size_t)ci * Cout + co) * 4 + ij];
-        }
-        store_as(t.out, i, t.dtype, v);
-        break;
-      }
-      case DFCSA_PACK_CONCAT: {
-        if (i < a[0]) v = t.w0[i];
-        else if (i < a[0] + a[1]) v = t.w1 ? t.w1[i - a[0]] : 0.f;
-        else if (i < a[0] + a[1] + a[2]) v = t.w2 ? t.w2[i - a[0] - a[1]] : 0.f;
+      break;
+    }
+    case DFCSA_PACK_CONCAT: {
+      const int n0 = a[0], n1 = a[1], n2 = a[2], total = a[3];
+      for (int i = tid; i < total; i += 256) {
+        float v = 0.f;
+        if (i < n0) v = t.w0[i];
+        else if (i < n0 + n1) v = t.w1[i - n0];
+        else if (i < n0 + n1 + n2) v = t.w2[i - n0 - n1];
         ((float*)t.out)[i] = v;
-        break;
       }
-      case DFCSA_PACK_BIAS4: {
-        ((float*)t.out)[i] = t.w0[i % a[0]];
-        break;
-      }
-      default:
-        break;
+      break;
     }
+    case DFCSA_PACK_BIAS4: {
+      for (int i = tid; i < 4 * a[0]; i += 256) ((float*)t.out)[i] = t.w0[i % a[0]];
+      break;
+    }
+    default:
+      break;
   }
 }
 
@@ -797,9 +795,8 @@ extern "C" int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, 
 }
 
 extern "C" int dfcsa_pack_plan(const dfcsa_pack_entry* table_dev, int n, int64_t total, void* stream) {
-  if (!table_dev || n <= 0 || total <= 0) return DFCSA_EINVAL;
-  int blocks = (int)std::min<int64_t>(8192, (total + 255) / 256);
-  hipLaunchKernelGGL(pack_plan_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, table_dev, n, total);
+  if (!table_dev || n <= 0 || total <= 0 || total > (1 << 30)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(pack_plan_kernel, dim3((unsigned)total), dim3(256), 0, (hipStream_t)stream, table_dev, n);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

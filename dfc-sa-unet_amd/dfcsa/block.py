@@ -126,22 +126,30 @@ def block_forward(blk, xs, pool_size, training, dtype):
 
 
 def _build_block_packs(ps, blk, dtype, Cin_p, C, has_res):
-    """Entries of one DFC block: forward operands, transposed dgrad operands, LSA projections."""
+    """Entries of one DFC block.  Phase A: forward operands from the fp32 weights; phase B:
+    the dgrad operands as transposes of those (W4t = W4p^T, W3t = W3p^T, and the fused block-input
+    dgrad operand Wdx = [W1p(tap)^T for 9 taps | W2p^T | Wres^T or I])."""
     conv1, conv2, conv3, conv4 = blk.conv_branch[0], blk.attn_branch[0], blk.gate[0], blk.fusion_conv[0]
     N2 = 2 * C if has_res else C
     Kp2 = rup(Cin_p, ops.KALIGN)
-    ps.rows("W1p", dtype, conv1.weight, Cin_p, rup(9 * Cin_p, ops.KALIGN))
-    ps.rows("W2p", dtype, conv2.weight, Cin_p, Kp2, row0=0, rows=N2)
+    W1p = ps.rows("W1p", dtype, conv1.weight, Cin_p, rup(9 * Cin_p, ops.KALIGN))
+    W2p = ps.rows("W2p", dtype, conv2.weight, Cin_p, Kp2, row0=0, rows=N2)
     if has_res:
         ps.rows("W2p", dtype, blk.residual_conv.weight, Cin_p, Kp2, row0=C)
         ps.concat("b2", [conv2.bias], N2)
-    ps.rows("W3p", dtype, conv3.weight, 2 * C, rup(2 * C, ops.KALIGN))
-    ps.rows("W4p", dtype, conv4.weight, 3 * C, rup(3 * C, ops.KALIGN))
+    W3p = ps.rows("W3p", dtype, conv3.weight, 2 * C, rup(2 * C, ops.KALIGN))
+    W4p = ps.rows("W4p", dtype, conv4.weight, 3 * C, rup(3 * C, ops.KALIGN))
     KpC = rup(C, ops.KALIGN)
-    ps.t3("W4t", dtype, 3 * C, KpC, [conv4.weight])
-    ps.t3("W3t", dtype, 2 * C, KpC, [conv3.weight])
-    ps.t3("Wdx", dtype, Cin_p, rup(11 * C, ops.KALIGN),
-          [conv1.weight, conv2.weight, blk.residual_conv.weight if has_res else None], identity_last=not has_res)
+    ps.transpose(W4p, 0, 0, C, 3 * C, "W4t", (3 * C, KpC))
+    ps.transpose(W3p, 0, 0, C, 2 * C, "W3t", (2 * C, KpC))
+    wdx = (Cin_p, rup(11 * C, ops.KALIGN))
+    for tap in range(9):
+        ps.transpose(W1p, 0, tap * Cin_p, C, Cin_p, "Wdx", wdx, dc0=tap * C)
+    ps.transpose(W2p, 0, 0, C, Cin_p, "Wdx", wdx, dc0=9 * C)
+    if has_res:
+        ps.transpose(W2p, C, 0, C, Cin_p, "Wdx", wdx, dc0=10 * C)
+    else:  # identity residual: constant identity block (written once)
+        ps.buffer("Wdx", wdx, dtype)[:, 10 * C:11 * C].copy_(torch.eye(C, dtype=dtype, device=ps.device))
     _build_lsa_packs(ps, blk.attn_branch[3])
 
 
@@ -155,12 +163,12 @@ def _build_lsa_packs(ps, lsa):
     if _lsa_gemm_ok(C, J):
         Kp = rup(C, ops.KALIGN)
         for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
-            ps.rows("Wp", f32, w, C, Kp, row0=off, rows=J)
-        ps.t3("WT", f32, C, rup(J, ops.KALIGN), [qw, kw, vw])
+            Wp = ps.rows("Wp", f32, w, C, Kp, row0=off, rows=J)
+        ps.transpose(Wp, 0, 0, J, C, "WT", (C, rup(J, ops.KALIGN)))
     else:
         for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
-            ps.rows("Wqkv", f32, w, C, C, row0=off, rows=J)
-        ps.t3("WqkvT", f32, C, J, [qw, kw, vw])
+            Wq = ps.rows("Wqkv", f32, w, C, C, row0=off, rows=J)
+        ps.transpose(Wq, 0, 0, J, C, "WqkvT", (C, J))
 
 
 def block_backward(blk, s, dout, need_dx, dtype):

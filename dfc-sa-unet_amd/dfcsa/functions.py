@@ -62,7 +62,7 @@ class ConvTranspose2x2(torch.autograd.Function):
         dev = x.device
         Kf = rup(Cin, ops.KALIGN)
         Kb = rup(4 * Cout, ops.KALIGN)
-        pk = get_packset(mod, (dtype, param_key(mod)), lambda ps: ps.convT(dtype, mod.weight, mod.bias, Kf, Kb))
+        pk = get_packset(mod, (dtype, param_key(mod)), lambda ps: _convT_packs(ps, mod, dtype, Kf, Kb))
         Wf, Wb, b4 = pk["Wf"], pk["Wb"], pk["b4"]
         out = torch.empty((B, 2 * h, 2 * w, Cout), dtype=dtype, device=dev)
         ops.conv_gemm(dtype, [(x, 0, 0)], Cin, (B, h, w), (h, w), Wf, Kf, 4 * Cout, [out], Cout, bias=b4,
@@ -89,6 +89,15 @@ class ConvTranspose2x2(torch.autograd.Function):
             ops.conv_gemm(dtype, segs, Cout, (B, h, w), (2 * h, 2 * w), ctx.Wb, ctx.Kb, Cin, [dx], Cin, stride=2)
         notify_grads_ready(mod)
         return (dx, None, None, *([None] * ctx.np))
+
+
+def _convT_packs(ps, mod, dtype, Kf, Kb):
+    """Wb[ci][ij*Cout + co] = W[ci][co][ij] (dgrad operand, phase A); Wf = Wb^T (forward operand,
+    rows ij*Cout + co, phase B); b4[ij*Cout + co] = bias[co]."""
+    Cin, Cout = mod.weight.shape[0], mod.weight.shape[1]
+    Wb = ps.rows("Wb", dtype, mod.weight, Cout, Kb)
+    ps.transpose(Wb, 0, 0, Cin, 4 * Cout, "Wf", (4 * Cout, Kf))
+    ps.bias4("b4", mod.bias)
 
 
 class ResizeBilinear(torch.autograd.Function):

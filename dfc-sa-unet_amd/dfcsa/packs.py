@@ -7,8 +7,10 @@ weights change once per step (optimizer), so the packed operands are rebuilt onc
 
 A ``PackSet`` owns the packed tensors of one module and the table entries that fill them
 (``dfcsa_pack_entry``, include/dfcsa.h).  The model gathers the PackSets of all its modules into
-one ``PackPlan`` whose device-resident table is processed by ONE ``dfcsa_pack_plan`` launch at
-the start of each forward (instead of ~100 small pack launches).  Modules used outside a model
+one ``PackPlan`` whose two device-resident tables are processed by two ``dfcsa_pack_plan``
+launches at the start of each forward (instead of ~100 small pack launches): phase A permutes
+the fp32 master weights into the forward operands (coalesced row reads), phase B transposes
+those into the dgrad operands with 64x64 LDS tiles.  Modules used outside a model
 (a standalone block) run their own PackSet.
 """
 import ctypes
@@ -35,83 +37,82 @@ def _table(entries, device):
 
 
 class PackSet:
+    """Packed operands of one module.  Phase-A entries read the fp32 master weights (ROWS,
+    CONCAT, BIAS4); phase-B entries transpose phase-A outputs (so they run in a second launch)."""
+
     def __init__(self, key, device):
         self.key = key
         self.device = device
         self.t = {}
-        self.entries = []
+        self.entries = ([], [])
         self.fresh = False
-        self._tab = None
+        self._tabs = None
         _EPOCH[0] += 1
 
     def __getitem__(self, name):
         return self.t[name]
 
-    def _new(self, name, shape, dtype):
-        out = torch.empty(shape, dtype=dtype, device=self.device)
-        self.t[name] = out
+    def buffer(self, name, shape, dtype):
+        """A zero-initialised persistent operand (padding stays zero: entries never write it)."""
+        out = self.t.get(name)
+        if out is None:
+            out = torch.zeros(shape, dtype=dtype, device=self.device)
+            self.t[name] = out
         return out
 
-    def _entry(self, kind, dtype, out, count, w0=None, w1=None, w2=None, a=()):
+    def _entry(self, phase, kind, dtype, out_ptr, count, w0=None, w1=None, w2=None, a=()):
         e = _lib.PackEntry()
         e.count, e.kind, e.dtype = count, kind, dt(dtype)
-        e.w0, e.w1, e.w2, e.out = P(w0), P(w1), P(w2), P(out)
+        e.w0, e.w1, e.w2, e.out = w0, w1, w2, out_ptr
         for i, v in enumerate(a):
             e.a[i] = int(v)
-        self.entries.append(e)
+        self.entries[phase].append(e)
 
     # ---- entry builders (semantics: include/dfcsa.h, DFCSA_PACK_*) ----
     def rows(self, name, dtype, w, Cpad, Kpad, row0=0, rows=None):
-        """forward operand: out[row0 + co][tap*Cpad + ci] = w[co][ci][tap]"""
-        out = self.t.get(name)
-        if out is None:
-            out = self._new(name, (rows or w.shape[0], Kpad), dtype)
+        """out[row0 + r][tap*Cpad + c] = w[r][c][tap] (conv weight [Cout][Cin][kh][kw]; for a
+        ConvTranspose weight [Cin][Cout][2][2] this is its dgrad operand)."""
+        out = self.buffer(name, (rows or w.shape[0], Kpad), dtype)
+        R, Cc = w.shape[0], w.shape[1]
         ntaps = w.shape[2] * w.shape[3] if w.dim() == 4 else 1
-        self._entry(0, dtype, out, w.shape[0] * Kpad, w0=w, a=(w.shape[0], w.shape[1], ntaps, Cpad, Kpad, row0))
+        if ntaps * Cpad > Kpad or Cc > Cpad or row0 + R > out.shape[0]:
+            raise ValueError("pack plan: rows entry does not fit its operand")
+        per = max(1, 4096 // (Cc * ntaps))
+        self._entry(0, 0, dtype, P(out), (R + per - 1) // per, w0=P(w),
+                    a=(R, Cc, ntaps, Cpad, Kpad, row0, per))
         return out
 
-    def t3(self, name, dtype, Cin, Kpad, ws, identity_last=False):
-        """transposed dgrad operand of up to three weights side by side (pack_t3 semantics)."""
-        ws = list(ws) + [None] * (3 - len(ws))
-        wcin = next(w.shape[1] for w in ws if w is not None)
-        t0 = (ws[0].shape[2] * ws[0].shape[3]) if ws[0].dim() == 4 else 1
-        for w in ws[1:]:
-            if w is not None and w.dim() == 4 and w.shape[2] * w.shape[3] != 1:
-                raise ValueError("pack plan: segments 1 and 2 must be 1x1 weights")
-        c = [w.shape[0] if w is not None else 0 for w in ws]
-        if identity_last:
-            c[2] = Cin
-        if t0 * c[0] + c[1] + c[2] > Kpad:
-            raise ValueError("pack plan: t3 segments exceed Kpad")
-        out = self._new(name, (Cin, Kpad), dtype)
-        self._entry(1, dtype, out, Cin * Kpad, w0=ws[0], w1=ws[1], w2=ws[2],
-                    a=(Cin, Kpad, wcin, c[0], c[1], c[2], t0, int(identity_last)))
-        return out
-
-    def convT(self, dtype, w, bias, Kf, Kb):
-        Cin, Cout = w.shape[0], w.shape[1]
-        wf = self._new("Wf", (4 * Cout, Kf), dtype)
-        self._entry(2, dtype, wf, 4 * Cout * Kf, w0=w, a=(Cin, Cout, Kf))
-        wb = self._new("Wb", (Cin, Kb), dtype)
-        self._entry(3, dtype, wb, Cin * Kb, w0=w, a=(Cin, Cout, Kb))
-        b4 = self._new("b4", (4 * Cout,), torch.float32)
-        self._entry(5, torch.float32, b4, 4 * Cout, w0=bias, a=(Cout,))
+    def transpose(self, src, r0, c0, R, C, name, shape, dr0=0, dc0=0):
+        """dst[dr0 + c][dc0 + r] = src[r0 + r][c0 + c] (same dtype; src is a phase-A operand)."""
+        dst = self.buffer(name, shape, src.dtype)
+        if r0 + R > src.shape[0] or c0 + C > src.shape[1] or dr0 + C > dst.shape[0] or dc0 + R > dst.shape[1]:
+            raise ValueError("pack plan: transpose out of range")
+        es = src.element_size()
+        tc = (C + 63) // 64
+        self._entry(1, 1, src.dtype, dst.data_ptr() + (dr0 * dst.shape[1] + dc0) * es, ((R + 63) // 64) * tc,
+                    w0=src.data_ptr() + (r0 * src.shape[1] + c0) * es, a=(R, C, src.shape[1], dst.shape[1], tc))
+        return dst
 
     def concat(self, name, parts, total):
-        """fp32 out = cat(parts) zero-padded to `total` (parts: up to three 1-D tensors or None)."""
+        """fp32 out = cat(parts) zero-padded to `total` (parts: up to three 1-D tensors)."""
         parts = list(parts) + [None] * (3 - len(parts))
         lens = [p.numel() if p is not None else 0 for p in parts]
-        out = self._new(name, (total,), torch.float32)
-        self._entry(4, torch.float32, out, total, w0=parts[0], w1=parts[1], w2=parts[2],
+        out = self.buffer(name, (total,), torch.float32)
+        self._entry(0, 4, torch.float32, P(out), 1, w0=P(parts[0]), w1=P(parts[1]), w2=P(parts[2]),
                     a=(lens[0], lens[1], lens[2], total))
+        return out
+
+    def bias4(self, name, b):
+        out = self.buffer(name, (4 * b.numel(),), torch.float32)
+        self._entry(0, 5, torch.float32, P(out), 1, w0=P(b), a=(b.numel(),))
         return out
 
     # ---- execution ----
     def run(self):
-        if self._tab is None:
-            self._tab = _table(self.entries, self.device)
-        raw, n, total = self._tab
-        call("dfcsa_pack_plan", P(raw), n, total, stream())
+        if self._tabs is None:
+            self._tabs = [_table(es, self.device) for es in self.entries if es]
+        for raw, n, total in self._tabs:
+            call("dfcsa_pack_plan", P(raw), n, total, stream())
 
 
 class PackPlan:
@@ -120,15 +121,17 @@ class PackPlan:
     def __init__(self, sets, device):
         self.sets = list(sets)
         self.epoch = _EPOCH[0]
-        entries = [e for s in self.sets for e in s.entries]
-        self.tab = _table(entries, device) if entries else None
+        self.tabs = []
+        for phase in (0, 1):
+            entries = [e for s in self.sets for e in s.entries[phase]]
+            if entries:
+                self.tabs.append(_table(entries, device))
 
     def valid(self):
         return self.epoch == _EPOCH[0]
 
     def run(self):
-        if self.tab is not None:
-            raw, n, total = self.tab
+        for raw, n, total in self.tabs:
             call("dfcsa_pack_plan", P(raw), n, total, stream())
         for s in self.sets:
             s.fresh = True

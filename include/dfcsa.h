@@ -118,23 +118,24 @@ int dfcsa_pack_t3(int dtype, int Cin, int Kpad, int wcin, const float* w0, int c
 int dfcsa_pack_convT_w(int dtype, const float* w, const float* bias, int Cin, int Cout, void* out_fwd,
                        void* out_bwd, float* bias4, void* stream);
 /* One-launch weight packing for a whole model.  A device table of entries (built once; the
- * parameter and packed-buffer pointers are stable) is processed in a single grid-stride launch
- * over the concatenated element ranges [start, start + count) of all entries.
+ * parameter and packed-buffer pointers are stable) is processed by one launch of `total`
+ * workgroups: entry e owns workgroup tasks [start, start + count) (entries sorted by start).
  * kinds (a* = integer args):
- *  PACK_ROWS  0: out[(a5 + co)*a4 + k] = w0[co][ci][tap] with k = tap*a3 + ci (ci < a1), else 0;
- *                a0 = Cout, a1 = Cin, a2 = ntaps, a3 = Cpad, a4 = Kpad, a5 = row0; count Cout*Kpad
- *  PACK_T3    1: dfcsa_pack_t3 semantics; a0 = Cin rows, a1 = Kpad, a2 = wcin, a3..a5 = Cout_0..2,
- *                a6 = ntaps_0 (segments 1, 2 have one tap), a7 = identity2; count Cin*Kpad
- *  CONVT_FWD  2: out[(ij*a1 + co)*a2 + ci] = w0[ci][co][ij] (ci < a0), zero to Kpad a2
- *  CONVT_BWD  3: out[ci*a2 + ij*a1 + co] = w0[ci][co][ij], zero to Kpad a2
- *  CONCAT     4: fp32 out[i] = w0[i] (i < a0), w1[i - a0] (< a0 + a1), w2[...] (< a0+a1+a2), else 0
- *                up to a3 = count
- *  BIAS4      5: fp32 out[ij*a0 + co] = w0[co]; count 4*a0
- * dtype: element type of `out` for kinds 0-3. */
+ *  PACK_ROWS      0: out[(a5 + co)*a4 + tap*a3 + ci] = w0[co][ci][tap] (fp32 source) for ci < a1;
+ *                    a0 = Cout, a1 = Cin, a2 = ntaps, a3 = Cpad, a4 = Kpad, a5 = row0,
+ *                    a6 = rows per task; count = ceil(Cout / a6).  Padding is not written.
+ *  PACK_TRANSPOSE 1: out[c*a3 + r] = w0[r*a2 + c] for r < a0, c < a1 (both of `dtype`), in
+ *                    64x64 tiles; a4 = ceil(a1 / 64); count = ceil(a0 / 64) * a4.  w0 / out point
+ *                    at the first element of the sub-matrices.
+ *  PACK_CONCAT    4: fp32 out[i] = w0[i] (i < a0), w1[i - a0] (< a0 + a1), w2[...] (< a0+a1+a2),
+ *                    else 0, up to a3; count 1
+ *  PACK_BIAS4     5: fp32 out[ij*a0 + co] = w0[co], ij < 4; count 1
+ * dtype: element type of `out` (ROWS) / of both operands (TRANSPOSE).  A transpose that reads
+ * a ROWS output must run in a later launch (the host splits the plan into two tables).
+ * Replaces the per-step weight casts/permutations ATen performs inside every conv call of
+ * models/unet_dfc_sa_res.py:58-88, :147-156. */
 #define DFCSA_PACK_ROWS 0
-#define DFCSA_PACK_T3 1
-#define DFCSA_PACK_CONVT_FWD 2
-#define DFCSA_PACK_CONVT_BWD 3
+#define DFCSA_PACK_TRANSPOSE 1
 #define DFCSA_PACK_CONCAT 4
 #define DFCSA_PACK_BIAS4 5
 typedef struct {

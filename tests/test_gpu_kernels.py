@@ -265,45 +265,64 @@ def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-def test_pack_plan_matches_single_packs(dtype):
-    """One dfcsa_pack_plan launch reproduces the per-weight pack kernels bit for bit."""
+@pytest.mark.parametrize("cin,C", [(40, 64), (64, 64), (8, 16)])
+def test_pack_plan_matches_single_packs(dtype, cin, C):
+    """The two-phase pack plan (row permutes, then 64x64 tile transposes) reproduces the
+    per-weight pack kernels bit for bit for a DFC block (with and without a residual conv), its
+    LightSelfAttention projections and a ConvTranspose2d."""
+    import torch.nn as nn
     from dfcsa import _lib
+    from dfcsa.block import _build_block_packs
+    from dfcsa.functions import _convT_packs
     from dfcsa.packs import PackSet
-    dev = "cuda"
-    g = torch.Generator(device="cpu").manual_seed(5)
-    r = lambda *s: torch.randn(*s, generator=g).to(dev)  # noqa: E731
-    C, Cin, Cq = 64, 40, 8
-    w3, w1, wr = r(C, Cin, 3, 3), r(C, Cin, 1, 1), r(C, Cin, 1, 1)
-    w4 = r(C, 3 * C, 1, 1)
-    wT, bT = r(96, 32, 2, 2), r(32)
-    b = r(C)
-    ps = PackSet(("t",), torch.device(dev))
-    ps.rows("W1p", dtype, w3, 48, ops.rup(9 * 48, 64))
-    ps.rows("W2p", dtype, w1, 48, 64, row0=0, rows=2 * C)
-    ps.rows("W2p", dtype, wr, 48, 64, row0=C)
-    ps.t3("Wdx", dtype, 48, ops.rup(11 * C, 64), [w3, w1, wr])
-    ps.t3("Wid", dtype, C, ops.rup(11 * C, 64), [r(C, C, 3, 3), r(C, C, 1, 1), None], identity_last=True)
-    ps.t3("W4t", dtype, 3 * C, 64, [w4])
-    ps.concat("b2", [b], 2 * C)
-    ps.convT(dtype, wT, bT, 128, 128)
+    from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock
+    torch.manual_seed(cin + C)
+    blk = DynamicFusionConvAttnBlock(cin, C, pool_size=4).cuda()
+    has_res = cin != C
+    ps = PackSet(("t",), torch.device("cuda"))
+    _build_block_packs(ps, blk, dtype, cin, C, has_res)
+    up = nn.ConvTranspose2d(96, 32, 2, 2).cuda()
+    ps2 = PackSet(("u",), torch.device("cuda"))
+    _convT_packs(ps2, up, dtype, 128, 128)
     ps.run()
+    ps2.run()
     torch.cuda.synchronize()
-    want = ops.pack_conv_w(dtype, w3, 48, ops.rup(9 * 48, 64))
-    assert torch.equal(ps["W1p"], want)
-    w2 = torch.empty((2 * C, 64), dtype=dtype, device=dev)
-    ops.pack_conv_w(dtype, w1, 48, 64, out=w2, row0=0)
-    ops.pack_conv_w(dtype, wr, 48, 64, out=w2, row0=C)
+    conv1, conv2, conv3, conv4 = blk.conv_branch[0], blk.attn_branch[0], blk.gate[0], blk.fusion_conv[0]
+    K = lambda n: ops.rup(n, 64)  # noqa: E731
+    assert torch.equal(ps["W1p"], ops.pack_conv_w(dtype, conv1.weight, cin, K(9 * cin)))
+    w2 = torch.zeros((2 * C if has_res else C, K(cin)), dtype=dtype, device="cuda")
+    ops.pack_conv_w(dtype, conv2.weight, cin, K(cin), out=w2, row0=0)
+    if has_res:
+        ops.pack_conv_w(dtype, blk.residual_conv.weight, cin, K(cin), out=w2, row0=C)
+        assert torch.equal(ps["b2"][:C], conv2.bias) and not ps["b2"][C:].any()
     assert torch.equal(ps["W2p"], w2)
-    assert torch.equal(ps["Wdx"], ops.pack_t3(dtype, 48, ops.rup(11 * C, 64), [w3, w1, wr]))
-    assert torch.equal(ps["W4t"], ops.pack_t3(dtype, 3 * C, 64, [w4]))
-    wid = ps["Wid"].float()
-    assert torch.equal(wid[:, 10 * C:11 * C], torch.eye(C, device=dev))
-    assert torch.equal(ps["b2"][:C], b) and not ps["b2"][C:].any()
-    fv = torch.empty((4 * 32, 96), dtype=dtype, device=dev)
-    bv = torch.empty((96, 128), dtype=dtype, device=dev)
-    b4 = torch.empty(128, device=dev)
-    _lib.call("dfcsa_pack_convT_w", ops.dt(dtype), ops.P(wT), ops.P(bT), 96, 32, ops.P(fv), ops.P(bv), ops.P(b4),
-              ops.stream())
-    assert torch.equal(ps["Wf"][:, :96], fv) and not ps["Wf"][:, 96:].float().any()
-    assert torch.equal(ps["Wb"], bv)
-    assert torch.equal(ps["b4"], b4)
+    assert torch.equal(ps["W3p"], ops.pack_conv_w(dtype, conv3.weight, 2 * C, K(2 * C)))
+    assert torch.equal(ps["W4p"], ops.pack_conv_w(dtype, conv4.weight, 3 * C, K(3 * C)))
+    assert torch.equal(ps["W4t"], ops.pack_t3(dtype, 3 * C, K(C), [conv4.weight]))
+    assert torch.equal(ps["W3t"], ops.pack_t3(dtype, 2 * C, K(C), [conv3.weight]))
+    want = ops.pack_t3(dtype, cin, K(11 * C), [conv1.weight, conv2.weight,
+                                                blk.residual_conv.weight if has_res else None],
+                       identity_last=not has_res)
+    assert torch.equal(ps["Wdx"], want)
+    lsa = blk.attn_branch[3]
+    qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
+    Cq = qw.shape[0]
+    J = 2 * Cq + C
+    assert torch.equal(ps["bqkv"], torch.cat([lsa.query_conv.bias, lsa.key_conv.bias, lsa.value_conv.bias]))
+    if "Wp" in ps.t:
+        wp = torch.zeros((J, K(C)), device="cuda")
+        for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
+            ops.pack_conv_w(torch.float32, w, C, K(C), out=wp, row0=off)
+        assert torch.equal(ps["Wp"], wp)
+        assert torch.equal(ps["WT"], ops.pack_t3(torch.float32, C, K(J), [qw, kw, vw]))
+    else:
+        assert torch.equal(ps["WqkvT"], ops.pack_t3(torch.float32, C, J, [qw, kw, vw]))
+    fv = torch.empty((4 * 32, 96), dtype=dtype, device="cuda")
+    bv = torch.empty((96, 128), dtype=dtype, device="cuda")
+    b4 = torch.empty(128, device="cuda")
+    _lib.call("dfcsa_pack_convT_w", ops.dt(dtype), ops.P(up.weight), ops.P(up.bias), 96, 32, ops.P(fv), ops.P(bv),
+              ops.P(b4), ops.stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ps2["Wf"][:, :96], fv) and not ps2["Wf"][:, 96:].float().any()
+    assert torch.equal(ps2["Wb"], bv)
+    assert torch.equal(ps2["b4"], b4)

@@ -1,0 +1,9 @@
+set -e
+mkdir -p gpurun_out
+timeout -k 10 400 python -m pytest tests -m gpu -x -q > gpurun_out/t.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof_r4 -o run -- python3 $R/bench.py --steps 10 --warmup 3 --no-cpu-baseline --no-kernel-timing --no-graph > $R/gpurun_out/prof_r4.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/pmc_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-graph > $R/gpurun_out/pmc_fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/pmc_write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-kernel-timing --no-graph > $R/gpurun_out/pmc_write.log 2>&1
+ls -R $R/gpurun_out | head -30

@@ -43,5 +43,16 @@ for k, ms, fl in rec:
     agg[k][0] += 1; agg[k][1] += ms; agg[k][2] += fl
 tot = sum(v[1] for v in agg.values())
 print(f"GEMM total {tot:.3f} ms/step over {len(rec)} calls")
+def roof_ms(k, n):
+    kind, _, M, N, K, nseg = k
+    if kind == "conv":
+        cin = K // nseg * (nseg // 9 if nseg >= 9 and nseg % 9 == 0 else nseg)
+        by = 2 * (M * cin + N * K + M * N)
+    else:
+        by = 2 * (M * N + M * K // max(1, (nseg // 9 if nseg % 9 == 0 else 1))) + 4 * N * K
+    return n * max(2.0 * M * N * K / 2.5e15, by / 6.3e12) * 1e3
+tr = 0.0
 for k, (n, ms, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-    print(f"{ms:7.3f} ms  {fl/ms/1e9:7.1f} TF  n={n}  {k}")
+    r = roof_ms(k, n); tr += r
+    print(f"{ms:7.3f} ms  {fl/ms/1e9:7.1f} TF  roof {r:6.3f} ms ({r/ms*100:5.1f}%)  n={n}  {k}")
+print(f"sum of per-call roofline times {tr:.3f} ms ({tr/tot*100:.1f}% of measured)")
