@@ -19,6 +19,9 @@
 // register-staged double-buffered LDS with an XOR swizzle that makes the ds_read_b128 fragment
 // reads conflict-free; mfma_f32_16x16x32_bf16 (bf16) or 8 x mfma_f32_16x16x4f32 (f32 parity
 // mode; exact f32 FMA chain).
+#include <cstdio>
+#include <cstdlib>
+
 #include "common.h"
 #include "dfcsa_internal.h"
 
@@ -442,7 +445,215 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
   return 0;
 }
 
-int g_conv_cfg = 0;  // tuning override (dfcsa_set_tuning knob 1)
+// --------------------------------------------------------------------------------------------
+// Memory-bound 1x1 GEMMs (K <= 256, large M): persistent streaming kernel.
+// A workgroup keeps its slice of the weights (N_wg = 4*NWC columns x KP) in REGISTERS (each wave
+// owns NWC columns and holds their MFMA B fragments for the whole K), and walks 64-row M tiles
+// grid-stride.  The next tile's A image is fetched by LDS-DMA while the current tile is
+// multiplied and written, so loads, MFMA and the epilogue of different tiles overlap inside one
+// workgroup, and the small LDS footprint lets several workgroups share a CU.  Waves split the
+// columns, so per-column BatchNorm partial sums of a 64-row tile need no cross-wave reduction.
+// --------------------------------------------------------------------------------------------
+template <int NWC, int KP>
+__global__ void __launch_bounds__(256)
+conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
+  using T = bf16_t;
+  constexpr int KS = KP / 64;               // 64-wide K stages (one 64x128B LDS image each)
+  constexpr int KG = KP / 32;               // 32-wide MFMA k groups
+  constexpr int FN = NWC / 16;              // column fragments per wave
+  constexpr int NWG = 4 * NWC;              // columns per workgroup
+  constexpr int IMG = 64 * 128;             // bytes of one stage image
+  constexpr int SLOT = KS * IMG;
+  constexpr int OSTR = NWG * 2 + 16;        // output staging row stride (bytes)
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + 64 * OSTR];
+  char* otile = smem + 2 * SLOT;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = args.M, N = args.N, K = args.K;
+  const int n0 = blockIdx.y * NWG;
+  const int rsub = lane >> 3;
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+
+  // B fragments of this wave's columns, whole K (zero beyond N / Kpad)
+  bf16x8_t bfr[FN][KG];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wave * NWC + j * 16 + (lane & 15);
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int k = g * 32 + 8 * (lane >> 4);
+      if (n < N && k < args.Kpad) bfr[j][g] = *(const bf16x8_t*)((const T*)args.Bw + (size_t)n * args.Kpad + k);
+      else bfr[j][g] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  float bias[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = n0 + wave * NWC + j * 16 + (lane & 15);
+    bias[j] = (args.bias && n < N) ? args.bias[n] : 0.f;
+  }
+  const void* zero = (const void*)g_zero_page;
+
+  // A image of tile t into slot s: instruction i covers stage i/2, rows ((i&1)*4 + wave)*8 + rsub
+  auto issue = [&](int t, int slot) {
+    char* base = smem + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int st = i >> 1, rb = (i & 1) * 4 + wave;
+      const int m = t * 64 + rb * 8 + rsub;
+      const int k = st * 64 + cchunk * 8;
+      const void* src = zero;
+      if (m < M && k < K) {
+        const int seg = dm_div(args.dm_cseg, k);
+        const int ch = k - seg * args.Cseg;
+        src = (const void*)((const T*)args.seg[seg].ptr + ((size_t)m * args.Cseg + ch));
+      }
+      glds16(src, base + st * IMG + rb * 8 * 128);
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t >= mtiles) return;
+  issue(t, 0);
+  int slot = 0;
+  for (; t < mtiles; t += gridDim.x, slot ^= 1) {
+    const int tn = t + gridDim.x;
+    if (tn < mtiles) {
+      issue(tn, slot ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    const char* img = smem + slot * SLOT;
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      Frag<T> fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) read_frag<T>(img + (g >> 1) * IMG, i * 16 + (lane & 15), g & 1, lane, fa[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
+    }
+    const int m0 = t * 64;
+    // BatchNorm partial sums of the raw accumulator over this 64-row tile (valid rows only)
+    if (args.stats) {
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        float s = 0.f, q = 0.f;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+            const float v = m < M ? acc[i][j][r] : 0.f;
+            s += v;
+            q += v * v;
+          }
+        s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+        q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+        const int n = n0 + wave * NWC + j * 16 + lane;
+        if (lane < 16 && n < N) {
+          args.stats[(size_t)t * 2 * N + n] = s;
+          args.stats[(size_t)t * 2 * N + N + n] = q;
+        }
+      }
+    }
+    // bias + convert into the staging tile (previous tile's stores have drained: barrier above)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wave * NWC + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = i * 16 + (lane >> 4) * 4 + r;
+          *(T*)(otile + row * OSTR + col * 2) = f2bf(acc[i][j][r] + bias[j]);
+        }
+    }
+    __syncthreads();
+    constexpr int OCH = NWG / 8;
+    for (int e = tid; e < 64 * OCH; e += 256) {
+      const int row = e / OCH, cc = e - row * OCH;
+      const int m = m0 + row, n = n0 + cc * 8;
+      if (m >= M || n >= N) continue;
+      const int d = n / args.Nd, col = n - d * args.Nd;
+      T* dst = (T*)args.dest[d] + ((size_t)m * args.Nd + col);
+      uint4 v = *(const uint4*)(otile + row * OSTR + cc * 16);
+      if (args.accumulate) {
+        float a[8], o[8];
+        load8<T>((const T*)&v, a);
+        load8<T>(dst, o);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) a[q] += o[q];
+        store8<T>(dst, a);
+      } else {
+        *(uint4*)dst = v;
+      }
+    }
+  }
+}
+
+int g_stream_wgs = 0;   // workgroups per CU of the streaming kernel (0 = occupancy limit)
+int g_debug = -1;
+
+template <int NWC, int KP>
+int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
+  static int occ = 0;
+  if (!occ) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<NWC, KP>, 256, 0) != hipSuccess ||
+        occ < 1)
+      occ = 1;
+  }
+  const int mtiles = (a.M + 63) / 64;
+  const int ny = (a.N + 4 * NWC - 1) / (4 * NWC);
+  const int per_cu = g_stream_wgs > 0 ? g_stream_wgs : occ;
+  int gx = (256 * per_cu + ny - 1) / ny;
+  if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
+  if (gx > mtiles) gx = mtiles;
+  hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+// the streaming kernel serves 1x1 (no shift, stride 1, plain store) bf16 GEMMs with K <= 256
+int try_stream(const ConvGemmArgs& a, hipStream_t st) {
+  if (g_debug < 0) g_debug = getenv("DFCSA_DEBUG") ? 1 : 0;
+  if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return 1;
+  // measured (tools/stream_bench.py, B=16 shapes): the streaming kernel wins for K = 64 with
+  // N >= 128 (2 and 3 destinations, accumulate) and for N >= 384; the tile kernels keep N = 64
+  // and K = 128..256 with N <= 256
+  if (!((a.Kpad == 64 && a.N >= 128) || (a.N >= 384 && a.Kpad <= 128))) return 1;
+  for (int i = 0; i < a.nseg; ++i)
+    if (a.seg[i].dh || a.seg[i].dw) return 1;
+  if (a.Ho != a.Hi || a.Wo != a.Wi) return 1;
+  // per-wave columns: register budget NWC/16 * KP/32 <= 16 fragments
+  const int kp = a.Kpad;
+  auto pick = [&](int nwc) {
+    switch (kp) {
+      case 64: return nwc == 16 ? launch_stream<16, 64>(a, st) : nwc == 32 ? launch_stream<32, 64>(a, st)
+                      : nwc == 48 ? launch_stream<48, 64>(a, st) : launch_stream<64, 64>(a, st);
+      case 128: return nwc == 16 ? launch_stream<16, 128>(a, st) : nwc == 32 ? launch_stream<32, 128>(a, st)
+                      : nwc == 48 ? launch_stream<48, 128>(a, st) : launch_stream<64, 128>(a, st);
+      case 192: return nwc == 16 ? launch_stream<16, 192>(a, st) : launch_stream<32, 192>(a, st);
+      default: return nwc == 16 ? launch_stream<16, 256>(a, st) : launch_stream<32, 256>(a, st);
+    }
+  };
+  const int maxf = 16 / (kp / 32);           // column fragments per wave that fit
+  int nwc = 16;
+  for (int c : {64, 48, 32, 16})
+    if (c / 16 <= maxf && (a.N % (4 * c) == 0 || (c == 16))) { nwc = c; break; }
+  if (kp >= 192 && nwc > 32) nwc = 32;
+  return pick(nwc);
+}
+
+int g_conv_cfg = 0;  // tuning override (dfcsa_set_tuning knob 1; 7 = no streaming 1x1 kernel)
 
 // config ids: 1 reg 128x64, 2 reg 128x128, 3 dma 128x64, 4 dma 256x64, 5 dma 128x128, 6 dma 256x128
 template <typename T>
@@ -460,6 +671,7 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // measured on MI355X (tools/gemm_bench.py, the model's B=16 shapes): LDS-DMA 128x128 wins
     // for N > 64 (600-675 TF on the 3x3 convs); for N <= 64 the LDS-DMA 256x64 tile wins on
     // deep K (3x3) and the register-staged 128x64 on the memory-bound small-K 1x1s.
+    if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (a.N <= 64) {
       if (a.K >= 512 && (a.M + 255) / 256 >= 256) return launch_glds<256, 64, 4, 1>(a, st);
       return launch_cfg<T, 128, 64, 4, 1>(a, st);
@@ -507,5 +719,7 @@ extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }
 extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 1) { g_conv_cfg = value; return 0; }
   if (knob == 2) { g_wgrad_target = value > 0 ? value : 512; return 0; }
+  if (knob == 3) { g_stream_wgs = value; return 0; }
+  if (knob == 4) { g_debug = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -331,7 +331,9 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
 
 /* Tuning knobs (benchmarking/autotuning only; 0 = automatic choice).
  * knob 1: conv_gemm tile configuration (see conv_gemm.hip, launch_t).
- * knob 2: target workgroups per weight-gradient launch (split-K count = target / tiles). */
+ * knob 2: target workgroups per weight-gradient launch (split-K count = target / tiles).
+ * knob 3: workgroups per CU of the persistent 1x1 streaming GEMM (0 = occupancy limit).
+ * knob 4: 1 = print kernel selection decisions to stderr. */
 int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);

@@ -326,3 +326,41 @@ def test_pack_plan_matches_single_packs(dtype, cin, C):
     assert torch.equal(ps2["Wf"][:, :96], fv) and not ps2["Wf"][:, 96:].float().any()
     assert torch.equal(ps2["Wb"], bv)
     assert torch.equal(ps2["b4"], b4)
+
+
+@pytest.mark.parametrize("Cs,nsrc,C,nd,acc,bias,stats", [
+    (64, 1, 64, 2, True, False, False),     # W3t dgrad: 1 source, 2 accumulated dests
+    (64, 1, 64, 3, False, False, False),    # W4t dgrad: 3 dests
+    (64, 3, 64, 1, False, True, True),      # fusion conv fwd: 3 sources (K = 192), stats
+    (8, 1, 64, 2, False, True, True),       # first block 1x1: K = 8 padded to 64
+    (128, 1, 256, 1, False, True, True),    # K = 128, N = 256
+    (128, 1, 96, 2, False, True, True),     # N = 192 -> 48 columns per wave
+    (256, 1, 256, 2, False, True, True),    # K = 256, N = 512
+])
+def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats):
+    """bf16 1x1 GEMMs with M >= 65536 take the persistent streaming kernel (ragged last tile)."""
+    torch.manual_seed(Cs + C + nd)
+    B, H, W = 3, 150, 147                      # M = 66150: 1034 tiles, last one partial
+    dtype = torch.bfloat16
+    xs = [q(torch.randn(B, Cs, H, W), dtype) for _ in range(nsrc)]
+    N = nd * C
+    w = q(torch.randn(N, nsrc * Cs, 1, 1) * 0.1, dtype)
+    b = torch.randn(N) if bias else None
+    ref = F.conv2d(torch.cat(xs, 1), w, b)
+    base = [q(torch.randn(B, C, H, W), dtype) for _ in range(nd)]
+    Kp = ops.rup(nsrc * Cs, ops.KALIGN)
+    wp = ops.pack_conv_w(dtype, w.cuda(), nsrc * Cs, Kp)
+    dests = [nhwc(t, dtype) if acc else torch.empty((B, H, W, C), dtype=dtype, device="cuda") for t in base]
+    M = B * H * W
+    st = torch.full((ops.ntiles_gemm(M) * 2 * N,), float("nan"), device="cuda") if stats else None
+    ops.conv_gemm(dtype, [(nhwc(x, dtype), 0, 0) for x in xs], Cs, (B, H, W), (H, W), wp, Kp, N, dests, C,
+                  bias=b.cuda() if bias else None, accumulate=acc, stats=st)
+    torch.cuda.synchronize()
+    for i in range(nd):
+        want = ref[:, i * C:(i + 1) * C] + (base[i] if acc else 0)
+        assert rel(nchw(dests[i]), want) < 1e-2
+    if stats:
+        s = st.view(-1, 2, N).sum(0).cpu()
+        a = ref - (b.view(1, -1, 1, 1) if bias else 0)
+        assert rel(s[0], a.sum((0, 2, 3))) < 1e-3
+        assert rel(s[1], (a * a).sum((0, 2, 3))) < 1e-3
