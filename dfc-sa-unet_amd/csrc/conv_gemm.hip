@@ -325,7 +325,7 @@ __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_base, 16, 0, 0);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NST>
 __global__ void __launch_bounds__(WM* WN * 64)
 conv_gemm_glds_kernel(const ConvGemmArgs args) {
   using T = bf16_t;
@@ -335,7 +335,8 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int OSTR = BN * (int)sizeof(T) + 16;
-  constexpr int SMEM = (2 * STAGE > BM * OSTR) ? 2 * STAGE : BM * OSTR;
+  constexpr int SMEM = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
+  constexpr int OPS = A_IN + B_IN;  // LDS-DMA instructions per wave per stage
   static_assert(NW % 2 == 0 && A_IN >= 1 && B_IN >= 1, "glds tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
@@ -348,22 +349,32 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
   const int rsub = lane >> 3;
 
-  int a_pix[A_IN], a_oh[A_IN], a_ow[A_IN];
+  // Segment table in LDS: the per-lane segment lookup of the gather must not be a vector-memory
+  // load (it would sit between the counted LDS-DMAs and force a full vmcnt drain).
+  __shared__ ConvSeg segtab[DFCSA_MAX_SEG];
+  if (tid < args.nseg) segtab[tid] = args.seg[tid];
+  // Per A row: element offset of its (shift 0,0) source pixel and 3-bit in-bounds masks for the
+  // row / column shifts -1, 0, +1 (every segment shift of the step is in that range).
+  int a_off[A_IN], a_mask[A_IN];
 #pragma unroll
   for (int i = 0; i < A_IN; ++i) {
     const int m = m0 + (i * NW + wave) * 8 + rsub;
+    a_off[i] = 0;
+    a_mask[i] = 0;
     if (m < M) {
       const int b = dm_div(args.dm_hw, m);
       const int rem = m - b * args.dm_hw.d;
       const int oh = dm_div(args.dm_w, rem);
       const int ow = rem - oh * args.dm_w.d;
-      a_oh[i] = oh * args.stride;
-      a_ow[i] = ow * args.stride;
-      a_pix[i] = (b * args.Hi + a_oh[i]) * args.Wi + a_ow[i];
-    } else {
-      a_oh[i] = -(1 << 20);  // forces the bounds test to fail
-      a_ow[i] = 0;
-      a_pix[i] = 0;
+      const int ih = oh * args.stride, iw = ow * args.stride;
+      a_off[i] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg;
+      int hm = 0, wmk = 0;
+#pragma unroll
+      for (int d = -1; d <= 1; ++d) {
+        hm |= (ih + d >= 0 && ih + d < args.Hi) << (d + 1);
+        wmk |= (iw + d >= 0 && iw + d < args.Wi) << (d + 1);
+      }
+      a_mask[i] = hm | (wmk << 3);
     }
   }
   const T* b_row[B_IN];
@@ -373,21 +384,23 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
     b_row[i] = n < N ? (const T*)args.Bw + (size_t)n * args.Kpad : nullptr;
   }
   const void* zero = (const void*)g_zero_page;
+  __syncthreads();
 
   auto issue = [&](int kt, int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + BM * 128;
     const int kbase = kt * 64 + cchunk * 8;
-    const int seg = dm_div(args.dm_cseg, kbase);
-    const int ch = kbase - seg * args.Cseg;
     const bool kvalid = kbase < args.K;
-    const ConvSeg sg = args.seg[kvalid ? seg : 0];
-    const int soff = sg.dh * args.Wi + sg.dw;
+    const int seg = kvalid ? dm_div(args.dm_cseg, kbase) : 0;
+    const int ch = kbase - seg * args.Cseg;
+    const ConvSeg sg = segtab[seg];
+    const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch;
+    const int sh = (sg.dh + 1) | ((sg.dw + 1 + 3) << 8);
+    const T* base = (const T*)sg.ptr;
 #pragma unroll
     for (int i = 0; i < A_IN; ++i) {
-      const int ih = a_oh[i] + sg.dh, iw = a_ow[i] + sg.dw;
-      const bool ok = kvalid && ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi;
-      const void* src = ok ? (const void*)((const T*)sg.ptr + ((size_t)(a_pix[i] + soff) * args.Cseg + ch)) : zero;
+      const bool ok = kvalid && ((a_mask[i] >> (sh & 255)) & (a_mask[i] >> (sh >> 8)) & 1);
+      const void* src = ok ? (const void*)(base + (unsigned)(a_off[i] + delta)) : zero;
       glds16(src, A + (i * NW + wave) * 8 * 128);
     }
 #pragma unroll
@@ -403,13 +416,27 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
 
+  // NST-deep ring: stages kt+1 .. kt+NST-2 stay in flight while stage kt is multiplied; the
+  // only vector-memory ops in the loop are the DMAs, so a counted vmcnt isolates stage kt.
   const int nk = args.Kpad / 64;
-  issue(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const char* A = smem + (kt & 1) * STAGE;
+    const int after = min(NST - 2, nk - 1 - kt);
+    if constexpr (NST >= 4) {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NST == 3) {
+      if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* A = smem + (kt % NST) * STAGE;
     const char* B = A + BM * 128;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -423,16 +450,15 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 #pragma unroll
         for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
   }
+  __syncthreads();
   conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wm, wn);
 }
 
-template <int BM, int BN, int WM, int WN>
+template <int BM, int BN, int WM, int WN, int NST = 2>
 int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
-  hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, st, a);
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -602,6 +628,7 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
 
 int g_stream_wgs = 0;   // workgroups per CU of the streaming kernel (0 = occupancy limit)
 int g_debug = -1;
+int g_stream_force = 0;  // knob 5: take the streaming kernel whenever it applies (tests)
 
 template <int NWC, int KP>
 int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
@@ -629,7 +656,7 @@ int try_stream(const ConvGemmArgs& a, hipStream_t st) {
   // measured (tools/stream_bench.py, B=16 shapes): the streaming kernel wins for K = 64 with
   // N >= 128 (2 and 3 destinations, accumulate) and for N >= 384; the tile kernels keep N = 64
   // and K = 128..256 with N <= 256
-  if (!((a.Kpad == 64 && a.N >= 128) || (a.N >= 384 && a.Kpad <= 128))) return 1;
+  if (!g_stream_force && !((a.Kpad == 64 && a.N >= 128) || (a.N >= 384 && a.Kpad <= 128))) return 1;
   for (int i = 0; i < a.nseg; ++i)
     if (a.seg[i].dh || a.seg[i].dw) return 1;
   if (a.Ho != a.Hi || a.Wo != a.Wi) return 1;
@@ -656,9 +683,16 @@ int try_stream(const ConvGemmArgs& a, hipStream_t st) {
 int g_conv_cfg = 0;  // tuning override (dfcsa_set_tuning knob 1; 7 = no streaming 1x1 kernel)
 
 // config ids: 1 reg 128x64, 2 reg 128x128, 3 dma 128x64, 4 dma 256x64, 5 dma 128x128, 6 dma 256x128
+bool shifts_small(const ConvGemmArgs& a) {  // LDS-DMA kernels: segment shifts in [-1, 1]
+  for (int i = 0; i < a.nseg; ++i)
+    if (a.seg[i].dh < -1 || a.seg[i].dh > 1 || a.seg[i].dw < -1 || a.seg[i].dw > 1) return false;
+  return true;
+}
+
 template <typename T>
 int launch_t(const ConvGemmArgs& a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
+    if (!shifts_small(a)) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
     switch (g_conv_cfg) {
       case 1: return launch_cfg<T, 128, 64, 4, 1>(a, st);
       case 2: return launch_cfg<T, 128, 128, 2, 2>(a, st);
@@ -666,17 +700,25 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
       case 4: return launch_glds<256, 64, 4, 1>(a, st);
       case 5: return launch_glds<128, 128, 2, 2>(a, st);
       case 6: return launch_glds<256, 128, 2, 2>(a, st);
+      case 8: return launch_glds<128, 128, 2, 2, 3>(a, st);
+      case 9: return launch_glds<128, 128, 2, 2, 4>(a, st);
+      case 10: return launch_glds<256, 128, 4, 2, 3>(a, st);
+      case 11: return launch_glds<256, 64, 4, 1, 3>(a, st);
+      case 12: return launch_glds<128, 64, 2, 1, 4>(a, st);
+      case 13: return launch_glds<256, 128, 4, 2, 2>(a, st);
+      case 14: return launch_glds<128, 128, 4, 2, 2>(a, st);
+      case 15: return launch_glds<128, 64, 4, 1, 2>(a, st);
+      case 16: return launch_glds<128, 128, 4, 2, 3>(a, st);
+      case 17: return launch_glds<256, 64, 8, 1, 2>(a, st);
+      case 18: return launch_glds<256, 128, 8, 2, 2>(a, st);
       default: break;
     }
-    // measured on MI355X (tools/gemm_bench.py, the model's B=16 shapes): LDS-DMA 128x128 wins
-    // for N > 64 (600-675 TF on the 3x3 convs); for N <= 64 the LDS-DMA 256x64 tile wins on
-    // deep K (3x3) and the register-staged 128x64 on the memory-bound small-K 1x1s.
-    if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
-    if (a.N <= 64) {
-      if (a.K >= 512 && (a.M + 255) / 256 >= 256) return launch_glds<256, 64, 4, 1>(a, st);
-      return launch_cfg<T, 128, 64, 4, 1>(a, st);
-    }
-    return launch_glds<128, 128, 2, 2>(a, st);
+    // measured on MI355X (tools/gemm_bench.py, the model's B=16 shapes): 8-wave LDS-DMA tiles
+    // (waves of 32x64) beat 4-wave 64x64 ones -- twice the waves per SIMD hide the LDS and
+    // DMA latency: 128x128/8 waves 690-730 TF on the 3x3 convs (vs ~600), 128x64/4 waves for
+    // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
+    if (a.N <= 64) return launch_glds<128, 64, 4, 1, 2>(a, st);
+    return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
   // fp32 (parity mode + the fp32 LightSelfAttention projections): small problems (M = B*P*P
   // rows) get 64x64 tiles so that enough workgroups run
@@ -721,5 +763,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 2) { g_wgrad_target = value > 0 ? value : 512; return 0; }
   if (knob == 3) { g_stream_wgs = value; return 0; }
   if (knob == 4) { g_debug = value; return 0; }
+  if (knob == 5) { g_stream_force = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -238,7 +238,10 @@ def test_head_fwd_bwd(dtype, tol, C, Cout):
                                               (4, 128, 64, 1, 256, False),   # 256x128 tile
                                               (4, 128, 16, 2, 128, True),    # 256x128, 3x3, 2 sources
                                               (2, 96, 8, 1, 64, True)])      # Cseg 8 < K stage
-def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3):
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
+def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3, cfg):
+    """Every bf16 tile configuration (tuning knob 1; 0 = automatic) on the same problems."""
+    import dfcsa
     dtype = torch.bfloat16
     torch.manual_seed(9)
     xs = [q(torch.randn(B, Cs, H, H), dtype) for _ in range(nsrc)]
@@ -254,8 +257,12 @@ def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3):
     stats = torch.empty(ops.ntiles_gemm(M) * 2 * C, device="cuda")
     xh = [nhwc(x, dtype) for x in xs]
     segs = [(x, dh, dw) for dh, dw in taps for x in xh]
-    ops.conv_gemm(dtype, segs, Cs, (B, H, H), (H, H), wp, Kp, C, [y], C, bias=b.cuda(), stats=stats)
-    torch.cuda.synchronize()
+    dfcsa.set_tuning(1, cfg)
+    try:
+        ops.conv_gemm(dtype, segs, Cs, (B, H, H), (H, H), wp, Kp, C, [y], C, bias=b.cuda(), stats=stats)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(1, 0)
     assert rel(nchw(y), ref) < 1e-2
     st = stats.view(-1, 2, C).sum(0).cpu()
     acc = ref - b.view(1, -1, 1, 1)
@@ -337,8 +344,11 @@ def test_pack_plan_matches_single_packs(dtype, cin, C):
     (128, 1, 96, 2, False, True, True),     # N = 192 -> 48 columns per wave
     (256, 1, 256, 2, False, True, True),    # K = 256, N = 512
 ])
-def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats):
-    """bf16 1x1 GEMMs with M >= 65536 take the persistent streaming kernel (ragged last tile)."""
+@pytest.mark.parametrize("force", [1, 0])
+def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats, force):
+    """bf16 1x1 GEMMs with M >= 65536: the persistent streaming kernel (forced for every template
+    variant) and the automatic choice, ragged last tile."""
+    import dfcsa
     torch.manual_seed(Cs + C + nd)
     B, H, W = 3, 150, 147                      # M = 66150: 1034 tiles, last one partial
     dtype = torch.bfloat16
@@ -353,9 +363,13 @@ def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats):
     dests = [nhwc(t, dtype) if acc else torch.empty((B, H, W, C), dtype=dtype, device="cuda") for t in base]
     M = B * H * W
     st = torch.full((ops.ntiles_gemm(M) * 2 * N,), float("nan"), device="cuda") if stats else None
-    ops.conv_gemm(dtype, [(nhwc(x, dtype), 0, 0) for x in xs], Cs, (B, H, W), (H, W), wp, Kp, N, dests, C,
-                  bias=b.cuda() if bias else None, accumulate=acc, stats=st)
-    torch.cuda.synchronize()
+    dfcsa.set_tuning(5, force)
+    try:
+        ops.conv_gemm(dtype, [(nhwc(x, dtype), 0, 0) for x in xs], Cs, (B, H, W), (H, W), wp, Kp, N, dests, C,
+                      bias=b.cuda() if bias else None, accumulate=acc, stats=st)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(5, 0)
     for i in range(nd):
         want = ref[:, i * C:(i + 1) * C] + (base[i] if acc else 0)
         assert rel(nchw(dests[i]), want) < 1e-2
