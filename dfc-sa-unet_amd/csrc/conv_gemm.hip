@@ -335,7 +335,8 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int OSTR = BN * (int)sizeof(T) + 16;
-  constexpr int SMEM = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
+  constexpr int SMEM_MAIN = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
+  constexpr int SMEM = SMEM_MAIN + DFCSA_MAX_SEG * (int)sizeof(ConvSeg);
   constexpr int OPS = A_IN + B_IN;  // LDS-DMA instructions per wave per stage
   static_assert(NW % 2 == 0 && A_IN >= 1 && B_IN >= 1, "glds tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -351,7 +352,9 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 
   // Segment table in LDS: the per-lane segment lookup of the gather must not be a vector-memory
   // load (it would sit between the counted LDS-DMAs and force a full vmcnt drain).
-  __shared__ ConvSeg segtab[DFCSA_MAX_SEG];
+  // (kept inside the one staging array: a second __shared__ object can make hipcc drain
+  // vmcnt before the first ds_read of every k-step)
+  ConvSeg* segtab = (ConvSeg*)(smem + SMEM_MAIN);
   if (tid < args.nseg) segtab[tid] = args.seg[tid];
   // Per A row: element offset of its (shift 0,0) source pixel and 3-bit in-bounds masks for the
   // row / column shifts -1, 0, +1 (every segment shift of the step is in that range).
@@ -717,6 +720,7 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // (waves of 32x64) beat 4-wave 64x64 ones -- twice the waves per SIMD hide the LDS and
     // DMA latency: 128x128/8 waves 690-730 TF on the 3x3 convs (vs ~600), 128x64/4 waves for
     // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
+    if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (a.N <= 64) return launch_glds<128, 64, 4, 1, 2>(a, st);
     return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
@@ -764,5 +768,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 3) { g_stream_wgs = value; return 0; }
   if (knob == 4) { g_debug = value; return 0; }
   if (knob == 5) { g_stream_force = value; return 0; }
+  if (knob == 6) { g_wgrad_waves = (value == 8 || value == 4) ? value : 0; return 0; }
+  if (knob == 7) { g_wgrad_noglds = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -45,3 +45,5 @@ struct ProfScope {
 };
 
 extern int g_wgrad_target;
+extern int g_wgrad_waves;
+extern int g_wgrad_noglds;

@@ -66,17 +66,18 @@ __device__ __forceinline__ void f32_frag(const char* img, int kb, int col0, int 
   for (int s = 0; s < 8; ++s) f[s] = t[(r + s) * BW + col];
 }
 
-template <typename T, int BI, int BJ>
-__global__ void __launch_bounds__(256) wgrad_kernel(const WgradArgs args) {
+template <typename T, int BI, int BJ, int NW>
+__global__ void __launch_bounds__(NW * 64) wgrad_kernel(const WgradArgs args) {
+  constexpr int NT = NW * 64;
   constexpr int EPC = ElemTraits<T>::kChunk;
   constexpr int KMS = (sizeof(T) == 2) ? 64 : 32;    // pixels per stage
   constexpr int NG = KMS / 32;
   constexpr int CPR_G = BI * (int)sizeof(T) / 16;    // 16-B chunks per G row
   constexpr int CPR_X = BJ * (int)sizeof(T) / 16;
-  constexpr int RPP_G = 256 / CPR_G, RPP_X = 256 / CPR_X;  // rows per pass
+  constexpr int RPP_G = NT / CPR_G, RPP_X = NT / CPR_X;    // rows per pass
   constexpr int NPG = KMS / RPP_G, NPX = KMS / RPP_X;       // passes per stage
   constexpr int GB = KMS * BI * (int)sizeof(T), XB = KMS * BJ * (int)sizeof(T);
-  constexpr int WTM = BI / 2, WTN = BJ / 2;
+  constexpr int WTM = BI / (NW / 2), WTN = BJ / 2;       // waves: NW/2 x 2
   constexpr int FM = WTM / 16, FN = WTN / 16;
 
   __shared__ __attribute__((aligned(16))) char smem[2 * (GB + XB)];
@@ -217,6 +218,149 @@ __global__ void __launch_bounds__(256) wgrad_kernel(const WgradArgs args) {
     }
 }
 
+
+// --------------------------------------------------------------------------------------------
+// bf16 weight gradient with LDS-DMA staging (global_load_lds_dwordx4): the [pixel][channel]
+// images are filled directly from global memory; the XOR block swizzle of the transposed reads
+// is applied on the source side (lane -> which logical 16-B chunk it fetches), so the images are
+// bit-identical to the register-staged kernel's.  Per-lane gather state (group pointer / segment,
+// swizzled channel) is fixed per DMA slot, only the pixel advances with the stage.
+// --------------------------------------------------------------------------------------------
+__device__ __attribute__((aligned(16))) uint4 g_wg_zero[64];
+
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void glb_void_t;
+
+template <int BI, int BJ, int NW>
+__global__ void __launch_bounds__(NW * 64) wgrad_glds_kernel(const WgradArgs args) {
+  using T = bf16_t;
+  constexpr int KMS = 64;
+  constexpr int GB = KMS * BI * 2, XB = KMS * BJ * 2, STAGE = GB + XB;
+  constexpr int CPR_G = BI / 8, CPR_X = BJ / 8;            // 16-B chunks per image row
+  constexpr int RPI_G = 64 / CPR_G, RPI_X = 64 / CPR_X;    // rows per DMA instruction
+  constexpr int NI_G = CPR_G / NW, NI_X = CPR_X / NW;      // DMA instructions per wave per stage
+  static_assert(NI_G >= 1 && NI_X >= 1, "wgrad glds tiling");
+  constexpr int WM = NW / 2;
+  constexpr int WTM = BI / WM, WTN = BJ / 2;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int SMEM_MAIN = 2 * STAGE;
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN + DFCSA_MAX_SEG * (int)sizeof(ConvSeg)];
+  ConvSeg* segtab = (ConvSeg*)(smem + SMEM_MAIN);
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI, split = blockIdx.z;
+  const int mbeg = split * args.mchunk;
+  const int mend = min(args.M, mbeg + args.mchunk);
+  if (tid < args.nseg) segtab[tid] = args.seg[tid];
+  __syncthreads();
+
+  // G slots: row within the stage and source pointer (channel fixed), or null
+  int g_row[NI_G];
+  const T* g_src[NI_G];
+#pragma unroll
+  for (int q = 0; q < NI_G; ++q) {
+    const int ins = q * NW + wave;
+    const int r = ins * RPI_G + lane / CPR_G, pc = lane % CPR_G;
+    const int lc = (blk_swz<BI>(r, pc >> 1) << 1) | (pc & 1);
+    const int i = i0 + lc * 8;
+    g_row[q] = r;
+    g_src[q] = nullptr;
+    if (i < args.NI) {
+      const int grp = dm_div(args.dm_cg, i);
+      g_src[q] = (const T*)args.g_ptr[grp] + (i - grp * args.Cg);
+    }
+  }
+  // X slots: row, segment (LDS table) and channel
+  int x_row[NI_X], x_seg[NI_X], x_ch[NI_X];
+#pragma unroll
+  for (int q = 0; q < NI_X; ++q) {
+    const int ins = q * NW + wave;
+    const int r = ins * RPI_X + lane / CPR_X, pc = lane % CPR_X;
+    const int lc = (blk_swz<BJ>(r, pc >> 1) << 1) | (pc & 1);
+    const int j = j0 + lc * 8;
+    x_row[q] = r;
+    x_seg[q] = -1;
+    x_ch[q] = 0;
+    if (j < args.NJ) {
+      const int sg = dm_div(args.dm_cseg, j);
+      x_seg[q] = sg;
+      x_ch[q] = j - sg * args.Cseg;
+    }
+  }
+  const void* zero = (const void*)g_wg_zero;
+
+  auto issue = [&](int kt, int buf) {
+    char* G = smem + buf * STAGE;
+    char* X = G + GB;
+    const int mb = mbeg + kt * KMS;
+#pragma unroll
+    for (int q = 0; q < NI_G; ++q) {
+      const int m = mb + g_row[q];
+      const void* src = (g_src[q] && m < mend) ? (const void*)(g_src[q] + (size_t)m * args.Cg) : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(G + (q * NW + wave) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NI_X; ++q) {
+      const int m = mb + x_row[q];
+      const void* src = zero;
+      if (x_seg[q] >= 0 && m < mend) {
+        const ConvSeg sg = segtab[x_seg[q]];
+        const int b = dm_div(args.dm_hw, m);
+        const int rem = m - b * args.dm_hw.d;
+        const int oh = dm_div(args.dm_w, rem);
+        const int ow = rem - oh * args.dm_w.d;
+        const int ih = oh * args.stride + sg.dh, iw = ow * args.stride + sg.dw;
+        if (ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi)
+          src = (const void*)((const T*)sg.ptr + ((size_t)((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + x_ch[q]));
+      }
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(X + (q * NW + wave) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend > mbeg) ? (mend - mbeg + KMS - 1) / KMS : 0;
+  if (nk > 0) issue(0, 0);
+  for (int kt = 0; kt < nk; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
+    const char* G = smem + (kt & 1) * STAGE;
+    const char* X = G + GB;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) fa[i] = tr_frag<BI>(G, 32 * g, wm * WTM + i * 16, lane);
+#pragma unroll
+      for (int j = 0; j < FN; ++j) fb[j] = tr_frag<BJ>(X, 32 * g, wn * WTN + j * 16, lane);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+
+  float* out = args.slab + (size_t)split * args.NI * args.NJ;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = j0 + wn * WTN + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = i0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        if (row < args.NI && col < args.NJ) out[(size_t)row * args.NJ + col] = acc[i][j][r];
+      }
+    }
+}
+
 __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI, int NJ,
                                     int layout, int ntaps, int Ctot, int Creal, int ndst,
                                     float* d0, float* d1, float* d2) {
@@ -256,13 +400,31 @@ template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   constexpr int BJ = 128;
   dim3 grid((a.NJ + BJ - 1) / BJ, (a.NI + BI - 1) / BI, splits);
-  hipLaunchKernelGGL((wgrad_kernel<T, BI, BJ>), grid, dim3(256), 0, st, a);
+  // 8 waves (32x64 wave tiles) hide more latency (5-10 % on the 3x3 shapes); the 64-row
+  // tiles of the L1 3x3 (NI = 64, NJ = 1152) measured faster with 4
+  const int waves = g_wgrad_waves ? g_wgrad_waves : ((a.NI <= 64 && a.NJ > 256) ? 4 : 8);
+  if constexpr (sizeof(T) == 2) {
+    if (!g_wgrad_noglds) {
+      if (waves == 8)
+        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 8>), grid, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 4>), grid, dim3(256), 0, st, a);
+      DFCSA_CHECK_LAUNCH();
+      return 0;
+    }
+  }
+  if (waves == 8)
+    hipLaunchKernelGGL((wgrad_kernel<T, BI, BJ, 8>), grid, dim3(512), 0, st, a);
+  else
+    hipLaunchKernelGGL((wgrad_kernel<T, BI, BJ, 4>), grid, dim3(256), 0, st, a);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
 
 }  // namespace
 
+int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6; 0 = automatic)
+int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
 int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
 
 extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk) {
@@ -274,6 +436,9 @@ extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, i
   // reduce reads back): ~2 workgroups per CU is enough to keep the MFMA pipes busy
   int s = g_wgrad_target / tiles;
   if (s < 1) s = 1;
+  // few tiles (deep layers): at least ~3 workgroups per CU, else the chip is underfilled
+  // (measured: 12544 x 512 x 9216 runs 276 us with 1 split, 180 us with 3)
+  if (s <= 2) s = (768 + tiles - 1) / tiles;
   int max_s = M / (4 * kms);  // keep >= 4 stages per chunk
   if (max_s < 1) max_s = 1;
   if (s > max_s) s = max_s;

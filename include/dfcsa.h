@@ -334,7 +334,9 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 2: target workgroups per weight-gradient launch (split-K count = target / tiles).
  * knob 3: workgroups per CU of the persistent 1x1 streaming GEMM (0 = occupancy limit).
  * knob 4: 1 = print kernel selection decisions to stderr.
- * knob 5: 1 = use the 1x1 streaming GEMM whenever it applies (coverage tests). */
+ * knob 5: 1 = use the 1x1 streaming GEMM whenever it applies (coverage tests).
+ * knob 6: waves per weight-gradient workgroup (4 or 8; 0 = automatic).
+ * knob 7: 1 = register-staged bf16 weight gradient instead of the LDS-DMA kernel. */
 int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);

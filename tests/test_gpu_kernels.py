@@ -99,7 +99,11 @@ def test_conv_transpose_fwd_bwd(dtype, tol):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (3, 64, 2, 64, 14, 14), (2, 32, 1, 136, 20, 20)])
-def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W):
+@pytest.mark.parametrize("variant", [(0, 0), (1, 4), (1, 8), (0, 4), (0, 8)])  # (knob 7 reg-staged, knob 6 waves)
+def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W, variant):
+    import dfcsa
+    if dtype == torch.float32 and variant[0] == 0 and variant[1]:
+        pytest.skip("fp32 always runs the register-staged kernel")
     torch.manual_seed(3)
     xs = [q(torch.randn(B, Cs, H, W), dtype) for _ in range(nsrc)]
     x = torch.cat(xs, 1).requires_grad_(True)
@@ -109,8 +113,14 @@ def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W):
     xh = [nhwc(t, dtype) for t in xs]
     segs = [(t, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for t in xh]
     gw = torch.zeros(C, nsrc * Cs, 3, 3, device="cuda")
-    ops.conv_wgrad_into(dtype, [nhwc(g, dtype)], C, segs, Cs, (B, H, W), (H, W), [gw], 9, nsrc * Cs, nsrc * Cs)
-    torch.cuda.synchronize()
+    dfcsa.set_tuning(7, variant[0])
+    dfcsa.set_tuning(6, variant[1])
+    try:
+        ops.conv_wgrad_into(dtype, [nhwc(g, dtype)], C, segs, Cs, (B, H, W), (H, W), [gw], 9, nsrc * Cs, nsrc * Cs)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(7, 0)
+        dfcsa.set_tuning(6, 0)
     assert rel(gw, w.grad) < tol
 
 
