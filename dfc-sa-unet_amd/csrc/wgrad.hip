@@ -400,9 +400,9 @@ template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   constexpr int BJ = 128;
   dim3 grid((a.NJ + BJ - 1) / BJ, (a.NI + BI - 1) / BI, splits);
-  // 8 waves (32x64 wave tiles) hide more latency (5-10 % on the 3x3 shapes); the 64-row
-  // tiles of the L1 3x3 (NI = 64, NJ = 1152) measured faster with 4
-  const int waves = g_wgrad_waves ? g_wgrad_waves : ((a.NI <= 64 && a.NJ > 256) ? 4 : 8);
+  // 8 waves (32x64 wave tiles) hide more latency: LDS-DMA + 8 waves measured best or equal on
+  // every shape of the step (tools/wgrad_bench.py; 5-15 % on the 3x3 layers)
+  const int waves = g_wgrad_waves ? g_wgrad_waves : 8;
   if constexpr (sizeof(T) == 2) {
     if (!g_wgrad_noglds) {
       if (waves == 8)
