@@ -47,3 +47,4 @@ struct ProfScope {
 extern int g_wgrad_target;
 extern int g_wgrad_waves;
 extern int g_wgrad_noglds;
+extern int g_wgrad_narrow;

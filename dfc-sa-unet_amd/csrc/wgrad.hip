@@ -26,7 +26,7 @@ typedef __attribute__((address_space(3))) v4s_t lds_v4s;
 // physical 32-byte block of logical block `blk` in pixel row `r` (bf16 images)
 template <int BW>
 __device__ __forceinline__ int blk_swz(int r, int blk) {
-  if constexpr (BW == 128) return blk ^ ((r & 3) | (((r >> 3) & 1) << 2));
+  if constexpr (BW >= 128) return blk ^ ((r & 3) | (((r >> 3) & 1) << 2));
   else return blk ^ (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
 }
 
@@ -231,8 +231,9 @@ __device__ __attribute__((aligned(16))) uint4 g_wg_zero[64];
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void glb_void_t;
 
-template <int BI, int BJ, int NW>
-__global__ void __launch_bounds__(NW * 64) wgrad_glds_kernel(const WgradArgs args) {
+template <int BI, int BJ, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArgs args) {
+  constexpr int NW = WM * WN;
   using T = bf16_t;
   constexpr int KMS = 64;
   constexpr int GB = KMS * BI * 2, XB = KMS * BJ * 2, STAGE = GB + XB;
@@ -240,15 +241,14 @@ __global__ void __launch_bounds__(NW * 64) wgrad_glds_kernel(const WgradArgs arg
   constexpr int RPI_G = 64 / CPR_G, RPI_X = 64 / CPR_X;    // rows per DMA instruction
   constexpr int NI_G = CPR_G / NW, NI_X = CPR_X / NW;      // DMA instructions per wave per stage
   static_assert(NI_G >= 1 && NI_X >= 1, "wgrad glds tiling");
-  constexpr int WM = NW / 2;
-  constexpr int WTM = BI / WM, WTN = BJ / 2;
+  constexpr int WTM = BI / WM, WTN = BJ / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int SMEM_MAIN = 2 * STAGE;
   __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN + DFCSA_MAX_SEG * (int)sizeof(ConvSeg)];
   ConvSeg* segtab = (ConvSeg*)(smem + SMEM_MAIN);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WN, wn = wave % WN;
   const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI, split = blockIdx.z;
   const int mbeg = split * args.mchunk;
   const int mend = min(args.M, mbeg + args.mchunk);
@@ -396,6 +396,10 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
   }
 }
 
+// 64-row (NI <= 64) bf16 tiles take 256 columns when NJ is wide (4 x 2 wave layout of 32x64
+// tiles instead of 16x64: half the LDS fragment reads per MFMA)
+bool wide_j(const WgradArgs& a) { return a.NI <= 64 && a.NJ >= 512 && !g_wgrad_narrow; }
+
 template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   constexpr int BJ = 128;
@@ -405,10 +409,14 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   const int waves = g_wgrad_waves ? g_wgrad_waves : 8;
   if constexpr (sizeof(T) == 2) {
     if (!g_wgrad_noglds) {
-      if (waves == 8)
-        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 8>), grid, dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 4>), grid, dim3(256), 0, st, a);
+      if (BI == 64 && wide_j(a)) {
+        dim3 g2((a.NJ + 255) / 256, (a.NI + BI - 1) / BI, splits);
+        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4>), g2, dim3(512), 0, st, a);
+      } else if (waves == 8) {
+        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, BI == 64 ? 2 : 4, BI == 64 ? 4 : 2>), grid, dim3(512), 0, st, a);
+      } else {
+        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2>), grid, dim3(256), 0, st, a);
+      }
       DFCSA_CHECK_LAUNCH();
       return 0;
     }
@@ -425,13 +433,15 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6; 0 = automatic)
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
+int g_wgrad_narrow = 1;    // 0 = allow the 64x256 wgrad tile (dfcsa_set_tuning knob 8; measured slower on the L1 3x3)
 int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
 
 extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk) {
   if (M <= 0 || NI <= 0 || NJ <= 0 || !splits || !mchunk) return DFCSA_EINVAL;
   const int kms = dtype == DFCSA_DT_BF16 ? 64 : 32;
   const int BI = NI <= 64 ? 64 : 128;
-  const int tiles = ((NI + BI - 1) / BI) * ((NJ + 127) / 128);
+  const int BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 && NJ >= 512 && !g_wgrad_narrow) ? 256 : 128;
+  const int tiles = ((NI + BI - 1) / BI) * ((NJ + BJ - 1) / BJ);
   // splits trade occupancy against split-K slab traffic (each split writes NI*NJ fp32 that the
   // reduce reads back): ~2 workgroups per CU is enough to keep the MFMA pipes busy
   int s = g_wgrad_target / tiles;

@@ -336,7 +336,8 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 4: 1 = print kernel selection decisions to stderr.
  * knob 5: 1 = use the 1x1 streaming GEMM whenever it applies (coverage tests).
  * knob 6: waves per weight-gradient workgroup (4 or 8; 0 = automatic).
- * knob 7: 1 = register-staged bf16 weight gradient instead of the LDS-DMA kernel. */
+ * knob 7: 1 = register-staged bf16 weight gradient instead of the LDS-DMA kernel.
+ * knob 8: 0 = allow the 64x256 weight-gradient tile for 64-row problems (default 1: off). */
 int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);

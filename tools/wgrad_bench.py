@@ -12,7 +12,7 @@ B = 16
 SHAPES = [(224, 64, 1, 64, 2, True), (112, 128, 1, 128, 2, True), (56, 256, 1, 256, 2, True),
           (28, 512, 1, 512, 2, True), (14, 1024, 1, 512, 1, True), (224, 64, 1, 64, 3, False),
           (224, 64, 2, 64, 1, False), (112, 128, 1, 64, 1, True)]
-variants = [(w, t) for w in (4, 8) for t in (512, 1024)]
+variants = [(8, 512, 0), (8, 512, 1), (8, 1024, 0)]
 NOGLDS = int(os.environ.get("NOGLDS", "0"))
 LIB.dfcsa_set_tuning(7, NOGLDS)
 for H, Cg, ng, Cs, nsrc, k3 in SHAPES:
@@ -23,9 +23,10 @@ for H, Cg, ng, Cs, nsrc, k3 in SHAPES:
     NI, NJ = ng * Cg, len(segs) * Cs
     fl = 2.0 * M * NI * NJ
     row = {"M": M, "NI": NI, "NJ": NJ}
-    for w, t in variants:
+    for w, t, nar in variants:
         LIB.dfcsa_set_tuning(6, w)
         LIB.dfcsa_set_tuning(2, t)
+        LIB.dfcsa_set_tuning(8, nar)
         def run():
             slab, sp, ni, nj = ops.wgrad(bf, gs, Cg, segs, Cs, (B, H, H), (H, H))
             return slab, sp
@@ -39,7 +40,7 @@ for H, Cg, ng, Cs, nsrc, k3 in SHAPES:
         e1.record()
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) * 200
-        row[f"w{w}t{t}"] = (round(us, 1), round(fl / us / 1e6, 1), sp)
+        row[f"w{w}t{t}n{nar}"] = (round(us, 1), round(fl / us / 1e6, 1), sp)
     print(json.dumps(row), flush=True)
 LIB.dfcsa_set_tuning(6, 4)
 LIB.dfcsa_set_tuning(2, 512)
