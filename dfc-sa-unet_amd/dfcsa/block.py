@@ -24,6 +24,7 @@ from ._lib import call
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
+from .streams import on_side
 
 
 def grad_of(p):
@@ -197,9 +198,10 @@ def block_backward(blk, s, dout, need_dx, dtype):
                                extra=grad_of(blk.res_scale))
     dy4 = ops.bn_bwd_apply(dtype, dz4, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
     del dz4
-    # fusion conv: dW4 and d[fused, local, attn]
-    ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                        [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
+    # fusion conv: dW4 (side stream) and d[fused, local, attn]
+    with on_side(dev, dy4, s.fused, s.local, s.attn):
+        ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                            [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
     dfused = torch.empty_like(s.y4)
@@ -217,8 +219,9 @@ def block_backward(blk, s, dout, need_dx, dtype):
     coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
     dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
     del dz3
-    ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                        [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
+    with on_side(dev, dy3):
+        ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                            [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
     W3t = s.pk["W3t"]
     ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
@@ -244,16 +247,17 @@ def block_backward(blk, s, dout, need_dx, dtype):
     dy1 = ops.bn_bwd_apply(dtype, dz1, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
     del dz1
 
-    # ---- weight gradients of the input-side convs ----
+    # ---- weight gradients of the input-side convs (side stream) ----
     xs = s.xs
-    ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9, Cin_p,
-                        Cin_real)
-    if has_res:
-        ops.conv_wgrad_into(dtype, [dy2, dres], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
-                            [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
-    else:
-        ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw, [grad_of(conv2.weight)], 1,
+    with on_side(dev, dy1, dy2, dres, *xs):
+        ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
                             Cin_p, Cin_real)
+        if has_res:
+            ops.conv_wgrad_into(dtype, [dy2, dres], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
+                                [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
+        else:
+            ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw, [grad_of(conv2.weight)], 1,
+                                Cin_p, Cin_real)
     if not need_dx:
         return None
 

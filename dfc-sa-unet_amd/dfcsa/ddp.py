@@ -17,6 +17,8 @@ design:
 import torch
 import torch.distributed as dist
 
+from . import streams
+
 
 class GradBucketReducer:
     def __init__(self, model, bucket_mb=32.0, group=None):
@@ -63,9 +65,19 @@ class GradBucketReducer:
         j = len(self._works)
         while j < len(self.buckets) and self._pending[j] == 0:
             lo, hi, _ = self.buckets[j]
-            self._works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                               async_op=True))
+            self._works.append(self._launch(lo, hi))
             j += 1
+
+    def _launch(self, lo, hi):
+        """all_reduce a bucket once both the compute stream (BN / attention grads) and the side
+        stream (weight-gradient GEMMs, dfcsa.streams) have produced it."""
+        main = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
+        if main is None:
+            return dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        side = streams.side_stream(self.flat.grad.device)
+        side.wait_stream(main)
+        with torch.cuda.stream(side):
+            return dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
     def finish(self):
         """Ensure every bucket has been reduced (launch stragglers), make the current stream wait."""
@@ -73,8 +85,9 @@ class GradBucketReducer:
             return
         for j in range(len(self._works), len(self.buckets)):
             lo, hi, _ = self.buckets[j]
-            self._works.append(dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group,
-                                               async_op=True))
+            self._works.append(self._launch(lo, hi))
+        if self.flat.grad.is_cuda:
+            streams.join()
         for w in self._works:
             w.wait()
         self._pending = None

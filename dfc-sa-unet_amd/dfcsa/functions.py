@@ -14,6 +14,7 @@ from .block import grad_of
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
+from .streams import on_side
 
 
 class InputToNHWC(torch.autograd.Function):
@@ -79,10 +80,11 @@ class ConvTranspose2x2(torch.autograd.Function):
         Cout = mod.out_channels
         g = g.contiguous()
         segs = [(g, i, j) for i in range(2) for j in range(2)]
-        # weight / bias gradients
-        ops.conv_wgrad_into(dtype, [x], Cin, segs, Cout, (B, h, w), (2 * h, 2 * w), [grad_of(mod.weight)],
-                            ntaps=4, Ctot=Cout, Creal=Cout, layout=1, stride=2)
-        ops.channel_sum_into(dtype, g, grad_of(mod.bias))
+        # weight / bias gradients (side stream)
+        with on_side(x.device, x, g):
+            ops.conv_wgrad_into(dtype, [x], Cin, segs, Cout, (B, h, w), (2 * h, 2 * w), [grad_of(mod.weight)],
+                                ntaps=4, Ctot=Cout, Creal=Cout, layout=1, stride=2)
+            ops.channel_sum_into(dtype, g, grad_of(mod.bias))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)

@@ -10,6 +10,7 @@ import ctypes
 
 import torch
 
+from . import streams
 from ._lib import LIB, call
 from .ops import P, stream
 
@@ -73,6 +74,7 @@ class FusedSGD(torch.optim.Optimizer):
         skip_if_nonfinite: device scalar; the update is skipped on the device if it is NaN/inf."""
         loss = closure() if closure is not None else None
         flat = self._resolve()
+        streams.join()  # weight gradients may still be in flight on the side stream
         g = self.param_groups[0]
         n = flat.numel
         if max_norm is not None:

@@ -1,0 +1,69 @@
+"""Optional side HIP stream for the weight-gradient work of the backward pass.
+
+In a block's backward the weight-gradient GEMMs (pixel reductions dW = dY^T X) depend only on
+the activation gradient dY and saved forward tensors; nothing on the data-gradient chain waits
+for them.  They are therefore issued on a second stream forked from the compute stream at the
+point dY exists, so the MFMA-bound wgrad kernels fill the CUs left idle by the latency- and
+HBM-bound elementwise / reduction kernels of the dgrad chain.  Tensors read on the side stream
+are ``record_stream``-ed (the caching allocator must not hand their memory to the compute
+stream before the side stream is done), and the compute stream joins the side stream when the
+autograd pass ends (``queue_callback``), so any consumer of ``param.grad`` -- the fused
+optimizer, ``clip_grad_norm_``, a DDP reducer -- sees complete gradients.  The fork/join is
+event-based and captures into HIP graphs.
+"""
+import contextlib
+
+import torch
+
+_SIDE = {}
+_JOIN_QUEUED = [False]
+import os
+
+# Off by default: measured 979 vs 1044 img/s (B=16 bench) -- the overlapped wgrad GEMMs contend
+# with the dgrad GEMMs for CUs/LDS/L2 more than they fill idle time.  DFCSA_SIDE_STREAM=1 enables.
+ENABLED = [os.environ.get("DFCSA_SIDE_STREAM", "0") == "1"]
+
+
+def side_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _SIDE[idx] = s
+    return s
+
+
+def _join():
+    _JOIN_QUEUED[0] = False
+    cur = torch.cuda.current_stream()
+    for s in _SIDE.values():
+        if s.device == cur.device:
+            cur.wait_stream(s)
+
+
+def join():
+    """Make the current stream wait for all side-stream work (idempotent, cheap)."""
+    _join()
+
+
+@contextlib.contextmanager
+def on_side(device, *tensors):
+    """Run the enclosed launches on the side stream, after everything issued so far on the
+    current stream; `tensors` (allocated elsewhere) are marked as used by the side stream."""
+    if not ENABLED[0]:
+        yield
+        return
+    main = torch.cuda.current_stream(device)
+    side = side_stream(device)
+    side.wait_stream(main)
+    if not _JOIN_QUEUED[0]:
+        try:
+            torch.autograd.Variable._execution_engine.queue_callback(_join)
+            _JOIN_QUEUED[0] = True
+        except RuntimeError:
+            pass  # not inside a backward pass: the caller joins explicitly
+    with torch.cuda.stream(side):
+        yield side
+    for t in tensors:
+        if t is not None:
+            t.record_stream(side)

@@ -99,7 +99,7 @@ def test_conv_transpose_fwd_bwd(dtype, tol):
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (3, 64, 2, 64, 14, 14), (2, 32, 1, 136, 20, 20)])
-@pytest.mark.parametrize("variant", [(0, 0), (1, 4), (1, 8), (0, 4), (0, 8)])  # (knob 7 reg-staged, knob 6 waves)
+@pytest.mark.parametrize("variant", [(0, 0, 1), (1, 4, 1), (1, 8, 1), (0, 4, 1), (0, 8, 0)])  # knobs 7, 6, 8
 def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W, variant):
     import dfcsa
     if dtype == torch.float32 and variant[0] == 0 and variant[1]:
@@ -115,12 +115,14 @@ def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W, variant):
     gw = torch.zeros(C, nsrc * Cs, 3, 3, device="cuda")
     dfcsa.set_tuning(7, variant[0])
     dfcsa.set_tuning(6, variant[1])
+    dfcsa.set_tuning(8, variant[2])
     try:
         ops.conv_wgrad_into(dtype, [nhwc(g, dtype)], C, segs, Cs, (B, H, W), (H, W), [gw], 9, nsrc * Cs, nsrc * Cs)
         torch.cuda.synchronize()
     finally:
         dfcsa.set_tuning(7, 0)
         dfcsa.set_tuning(6, 0)
+        dfcsa.set_tuning(8, 1)
     assert rel(gw, w.grad) < tol
 
 
