@@ -291,6 +291,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
       }
     }
   }
+  if (!a.partial) return;  // sums not wanted (e.g. the analytically-zero conv-bias gradient)
   // deterministic in-workgroup reduction over pixel lanes
   __shared__ float red[4 * 3 * 512];
   float* out = a.partial + (size_t)blockIdx.x * NS * a.C;

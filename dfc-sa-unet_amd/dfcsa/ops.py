@@ -6,6 +6,7 @@ all statistics / parameters / gradients are fp32.  Nothing here computes on the 
 there is no fallback: a CPU tensor is rejected.
 """
 import ctypes
+import os
 
 import torch
 
@@ -181,14 +182,24 @@ def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     return coef
 
 
+# The gradient of a conv bias that feeds a train-mode BatchNorm is exactly zero:
+#   sum_m dy_m = gamma*invstd*(sum_m dz_m - M*mean(dz) - mean(dz*xh)*sum_m xh_m) = 0  (sum xh = 0).
+# The reference's autograd evaluates it in floating point (rounding noise ~1e-7 of the weight
+# gradients); by default it is left at its exact value (no reduction pass).  Set
+# DFCSA_NUMERIC_BN_BIAS_GRAD=1 to accumulate the floating-point column sums instead.
+NUMERIC_BN_BIAS_GRAD = os.environ.get("DFCSA_NUMERIC_BN_BIAS_GRAD", "0") == "1"
+
+
 def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
     M, C = dz.numel() // dz.shape[-1], dz.shape[-1]
-    nt = ntiles_ew(M, C)
     dy = torch.empty_like(dz)
-    part = torch.empty(nt * C, device=dz.device, dtype=torch.float32)
+    part = None
+    if bias_grad is not None and NUMERIC_BN_BIAS_GRAD:
+        nt = ntiles_ew(M, C)
+        part = torch.empty(nt * C, device=dz.device, dtype=torch.float32)
     call("dfcsa_bn_bwd_apply", dt(dtype), M, C, P(dz), P(y), P(bn.mean), P(bn.invstd), P(gamma), P(coef), P(dy),
          P(part), stream())
-    if bias_grad is not None:
+    if part is not None:
         colsum_into(part, nt, C, bias_grad)
     return dy
 

@@ -216,7 +216,8 @@ int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* datt
 int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count,
                           float* coef, float* dgamma, float* dbeta, float* extra, void* stream);
 /* dy = gamma*invstd*(dz - coef0 - xh*coef1); partial column sums of dy -> bias_partial
- * [ntiles][C] (conv bias gradient) */
+ * [ntiles][C] (conv bias gradient; NULL = not computed: for a conv feeding a train-mode
+ * BatchNorm it is exactly zero, sum_m dy = gamma*invstd*(sum dz - M*coef0 - coef1*sum xh) = 0) */
 int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
                        const float* invstd, const float* gamma, const float* coef, void* dy,
                        float* bias_partial, void* stream);

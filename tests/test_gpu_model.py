@@ -73,9 +73,14 @@ def test_lsa_fp32(path):
 
 
 # ----------------------------------------------------------------------------- block
+@pytest.mark.parametrize("numeric_bias", [False, True])
 @pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "block_*.npz"))), ids=os.path.basename)
-def test_block_fp32(path):
+def test_block_fp32(path, numeric_bias, monkeypatch):
+    """Block fwd/bwd vs the reference; BN-preceded conv-bias gradients both as the exact zero
+    (default) and as the floating-point column sums the reference evaluates."""
+    from dfcsa import ops
     from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock
+    monkeypatch.setattr(ops, "NUMERIC_BN_BIAS_GRAD", numeric_bias)
     fx = dict(np.load(path))
     name = os.path.basename(path)
     cin, cout = int(name.split("_")[1].split("to")[0]), int(name.split("to")[1].split("_")[0])
