@@ -110,3 +110,14 @@ __device__ __forceinline__ float wave_max(float v) {
   } while (0)
 
 #define DFCSA_EINVAL (-10000)
+
+// XCD-aware workgroup order for 1-D grids padded to a multiple of 8: the hardware deals
+// workgroup ids round-robin over the 8 XCDs (id % 8); this maps them so that each XCD walks
+// one contiguous range of logical tiles (neighbouring tiles share halos / operand tiles in the
+// XCD's own L2).  Returns -1 for padding ids.
+__device__ __forceinline__ int xcd_remap(int lid, int total) {
+  const int per = (total + 7) >> 3;
+  const int L = (lid & 7) * per + (lid >> 3);
+  return L < total ? L : -1;
+}
+__host__ __device__ inline int xcd_pad(int total) { return (total + 7) & ~7; }

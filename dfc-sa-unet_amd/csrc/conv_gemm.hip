@@ -343,7 +343,10 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int n_tile = blockIdx.x, m_tile = blockIdx.y;
+  const int nN = (args.N + BN - 1) / BN;
+  const int L = xcd_remap(blockIdx.x, nN * ((args.M + BM - 1) / BM));
+  if (L < 0) return;
+  const int n_tile = L % nN, m_tile = L / nN;  // the N tiles of one M tile share an XCD
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int M = args.M, N = args.N;
   // 16-B chunk this lane fetches within its 128-B row (source-side swizzle)
@@ -460,7 +463,7 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
-  dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
+  dim3 grid(xcd_pad(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM)));
   hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
   return 0;

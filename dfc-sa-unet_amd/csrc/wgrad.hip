@@ -232,7 +232,7 @@ typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void glb_void_t;
 
 template <int BI, int BJ, int WM, int WN>
-__global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArgs args) {
+__global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArgs args, int nsplit) {
   constexpr int NW = WM * WN;
   using T = bf16_t;
   constexpr int KMS = 64;
@@ -249,7 +249,12 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  const int j0 = blockIdx.x * BJ, i0 = blockIdx.y * BI, split = blockIdx.z;
+  // XCD-aware order: all column/row tiles of one pixel split (and neighbouring splits) run on
+  // one XCD, so the 9 shifted taps of a 3x3 gather hit that XCD's L2 instead of HBM
+  const int nJ = (args.NJ + BJ - 1) / BJ, nI = (args.NI + BI - 1) / BI;
+  const int L = xcd_remap(blockIdx.x, nJ * nI * nsplit);
+  if (L < 0) return;
+  const int j0 = (L % nJ) * BJ, i0 = ((L / nJ) % nI) * BI, split = L / (nJ * nI);
   const int mbeg = split * args.mchunk;
   const int mend = min(args.M, mbeg + args.mchunk);
   if (tid < args.nseg) segtab[tid] = args.seg[tid];
@@ -409,13 +414,17 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   const int waves = g_wgrad_waves ? g_wgrad_waves : 8;
   if constexpr (sizeof(T) == 2) {
     if (!g_wgrad_noglds) {
+      // 1-D grid (x = padded tile count, y = splits count carrier): see the XCD remap in the kernel
       if (BI == 64 && wide_j(a)) {
-        dim3 g2((a.NJ + 255) / 256, (a.NI + BI - 1) / BI, splits);
-        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4>), g2, dim3(512), 0, st, a);
-      } else if (waves == 8) {
-        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, BI == 64 ? 2 : 4, BI == 64 ? 4 : 2>), grid, dim3(512), 0, st, a);
+        dim3 g2(xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits), splits);
+        g2.y = 1;
+        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4>), g2, dim3(512), 0, st, a, splits);
       } else {
-        hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2>), grid, dim3(256), 0, st, a);
+        dim3 g1(xcd_pad(grid.x * grid.y * splits));
+        if (waves == 8)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, BI == 64 ? 2 : 4, BI == 64 ? 4 : 2>), g1, dim3(512), 0, st, a, splits);
+        else
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2>), g1, dim3(256), 0, st, a, splits);
       }
       DFCSA_CHECK_LAUNCH();
       return 0;
