@@ -39,6 +39,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def pmc_traffic(cls):
+    """HBM bytes per launch of a kernel class from the committed rocprofv3 PMC passes
+    (profiles/rNN_pmc_traffic.json, written by tools/rocpd_export.py from separate FETCH_SIZE and
+    WRITE_SIZE passes over this benchmark, gfx950 correction: reads = 2 x FETCH_SIZE)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))[cls]
+        return round(d["hbm_bytes_per_launch"]), os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def cpu_baseline(seconds_budget=25.0):
     """Time the CPU oracle's full train step (fp32 eager PyTorch, same algorithm) on B=2 images
     of the same workload; threads = this process's CPU share (<= 16)."""
@@ -114,7 +129,7 @@ def main():
     t = tg[lo:hi].to(dev)
     del xg, tg
 
-    model(x[:1])  # materialise the flat parameter/gradient storage before the reducer/optimizer
+    model(x)  # materialise the flat parameter/gradient storage and packed operands first
     reducer = GradBucketReducer(model) if world > 1 else None
     scale = reducer.grad_scale if reducer else 1.0
 
@@ -192,10 +207,13 @@ def main():
             L.LIB.dfcsa_prof_enable(c, 0)
         dom = max(cls.values(), key=lambda v: v[1])
         name, ms, n, fl = dom
+        dom_key = "conv_gemm" if dom is cls[1] else "conv_wgrad"
         peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
         ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        traffic, tsrc = pmc_traffic(dom_key)
         roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
-                "frac": round(ach / peak, 4), "traffic": None,
+                "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
+                "traffic_source": tsrc,
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "ms_per_step": round(ms / args.steps, 3), "share_of_step": round(ms / (el * 1e3), 3),
                 "other_class": {c[0]: {"ms_per_step": round(c[1] / args.steps, 3),

@@ -2,7 +2,9 @@
 
   python tools/rocpd_export.py stats  <kernel-trace db> <out.csv>
       per-kernel Name,Calls,TotalDurationNs,AverageNs,Percentage (the --stats layout)
-  python tools/rocpd_export.py traffic <FETCH_SIZE db> <WRITE_SIZE db> <out.json> [pattern]
+  python tools/rocpd_export.py classes <kernel-trace db> <out.json>
+      launches / average duration of the bench's roofline kernel classes
+  python tools/rocpd_export.py traffic <FETCH_SIZE db> <WRITE_SIZE db> <out.json>
       HBM bytes per dispatch of the kernels whose name contains `pattern` (default conv_gemm),
       corrected as /opt/skills/guides/MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE and
       WRITE_SIZE are kilobytes; FETCH_SIZE counts half the bytes of 16-B/lane streaming reads
@@ -27,6 +29,21 @@ def stats(db, out):
             w.writerow([name, n, d, d / n, 100.0 * d / tot])
 
 
+def classes(db, out):
+    """Per kernel class (the bench roofline classes): launches, total and average duration."""
+    c = sqlite3.connect(db)
+    res = {}
+    for cls, pats in CLASSES.items():
+        n, tot = 0, 0
+        for name, cnt, d in c.execute("select name, count(*), sum(duration) from kernels group by name"):
+            if any(p in name for p in pats):
+                n += cnt
+                tot += d
+        res[cls] = {"launches": n, "total_ms": tot / 1e6, "avg_launch_ms": tot / 1e6 / max(n, 1)}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
 def _per_dispatch(db, counter):
     c = sqlite3.connect(db)
     out = {}
@@ -34,6 +51,10 @@ def _per_dispatch(db, counter):
                                     "where counter_name = ? group by dispatch_id", (counter,)):
         out[did] = (name, val * 1024.0)
     return out
+
+
+CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel", "conv1x1_stream_kernel"),
+           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<")}
 
 
 def traffic(fdb, wdb, out, pattern="conv_gemm"):
@@ -48,12 +69,13 @@ def traffic(fdb, wdb, out, pattern="conv_gemm"):
         k = per_kernel[name]
         k["launches_write"] += 1
         k["write_bytes"] += v
-    sel = {n: k for n, k in per_kernel.items() if pattern in n}
+    pats = CLASSES.get(pattern, (pattern,))
+    sel = {n: k for n, k in per_kernel.items() if any(p in n for p in pats)}
     nf = sum(k["launches_fetch"] for k in sel.values())
     nw = sum(k["launches_write"] for k in sel.values())
     rd = sum(k["read_bytes"] for k in sel.values())
     wr = sum(k["write_bytes"] for k in sel.values())
-    res = {"pattern": pattern, "launches": nf,
+    res = {"class": pattern, "kernels": list(pats), "launches": nf,
            "hbm_bytes_per_launch": (rd / max(nf, 1)) + (wr / max(nw, 1)),
            "read_bytes_per_launch": rd / max(nf, 1), "write_bytes_per_launch": wr / max(nw, 1),
            "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB",
@@ -61,12 +83,20 @@ def traffic(fdb, wdb, out, pattern="conv_gemm"):
                               "read_MB_per_launch": k["read_bytes"] / max(k["launches_fetch"], 1) / 1e6,
                               "write_MB_per_launch": k["write_bytes"] / max(k["launches_write"], 1) / 1e6}
                           for n, k in sorted(per_kernel.items(), key=lambda kv: -kv[1]["read_bytes"])}}
+    return res
+
+
+def traffic_all(fdb, wdb, out):
+    res = {c: traffic(fdb, wdb, None, c) for c in CLASSES}
     json.dump(res, open(out, "w"), indent=1)
-    print(json.dumps({k: v for k, v in res.items() if k != "per_kernel"}, indent=1))
+    for c, r in res.items():
+        print(c, r["launches"], round(r["hbm_bytes_per_launch"] / 1e6, 2), "MB/launch")
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "classes":
+        classes(sys.argv[2], sys.argv[3])
     else:
-        traffic(*sys.argv[2:])
+        traffic_all(*sys.argv[2:5])
