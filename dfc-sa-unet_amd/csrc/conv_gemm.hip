@@ -335,8 +335,7 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int OSTR = BN * (int)sizeof(T) + 16;
-  constexpr int SMEM_MAIN = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
-  constexpr int SMEM = SMEM_MAIN + DFCSA_MAX_SEG * (int)sizeof(ConvSeg);
+  constexpr int SMEM = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
   constexpr int OPS = A_IN + B_IN;  // LDS-DMA instructions per wave per stage
   static_assert(NW % 2 == 0 && A_IN >= 1 && B_IN >= 1, "glds tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
@@ -353,67 +352,64 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
   const int rsub = lane >> 3;
 
-  // Segment table in LDS: the per-lane segment lookup of the gather must not be a vector-memory
-  // load (it would sit between the counted LDS-DMAs and force a full vmcnt drain).
-  // (kept inside the one staging array: a second __shared__ object can make hipcc drain
-  // vmcnt before the first ds_read of every k-step)
-  ConvSeg* segtab = (ConvSeg*)(smem + SMEM_MAIN);
-  if (tid < args.nseg) segtab[tid] = args.seg[tid];
-  // Per A row: element offset of its (shift 0,0) source pixel and 3-bit in-bounds masks for the
-  // row / column shifts -1, 0, +1 (every segment shift of the step is in that range).
-  int a_off[A_IN], a_mask[A_IN];
+  // Address generation is kept scalar wherever it can be: Cseg % 64 == 0 (host-checked), so a
+  // 64-wide K stage lies inside ONE segment -> segment pointer, shift and channel base are
+  // wave-uniform (SGPR, loaded from the kernel arguments); per lane only the row offset, the
+  // chunk and a 9-bit "tap in bounds" mask (bit (dh+1)*3 + dw+1) remain.
+  const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave index as a scalar (M0 bases)
+  const int lane_ch = cchunk * 8;
+  int a_off[A_IN], a_tap[A_IN];
 #pragma unroll
   for (int i = 0; i < A_IN; ++i) {
     const int m = m0 + (i * NW + wave) * 8 + rsub;
-    a_off[i] = 0;
-    a_mask[i] = 0;
+    a_off[i] = lane_ch;
+    a_tap[i] = 0;
     if (m < M) {
       const int b = dm_div(args.dm_hw, m);
       const int rem = m - b * args.dm_hw.d;
       const int oh = dm_div(args.dm_w, rem);
       const int ow = rem - oh * args.dm_w.d;
       const int ih = oh * args.stride, iw = ow * args.stride;
-      a_off[i] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg;
-      int hm = 0, wmk = 0;
+      a_off[i] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch;
+      int t = 0;
 #pragma unroll
-      for (int d = -1; d <= 1; ++d) {
-        hm |= (ih + d >= 0 && ih + d < args.Hi) << (d + 1);
-        wmk |= (iw + d >= 0 && iw + d < args.Wi) << (d + 1);
-      }
-      a_mask[i] = hm | (wmk << 3);
+      for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+        for (int dw = -1; dw <= 1; ++dw)
+          t |= (ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+      a_tap[i] = t;
     }
   }
-  const T* b_row[B_IN];
+  // B rows: pointer at K = 0 for this lane's chunk (zero page + no advance for rows >= N)
+  const char* b_ptr[B_IN];
+  int b_step[B_IN];
 #pragma unroll
   for (int i = 0; i < B_IN; ++i) {
     const int n = n0 + (i * NW + wave) * 8 + rsub;
-    b_row[i] = n < N ? (const T*)args.Bw + (size_t)n * args.Kpad : nullptr;
+    const bool ok = n < N;
+    b_ptr[i] = ok ? (const char*)((const T*)args.Bw + (size_t)n * args.Kpad + lane_ch) : (const char*)g_zero_page;
+    b_step[i] = ok ? 128 : 0;
   }
   const void* zero = (const void*)g_zero_page;
-  __syncthreads();
 
   auto issue = [&](int kt, int buf) {
     char* A = smem + buf * STAGE;
     char* B = A + BM * 128;
-    const int kbase = kt * 64 + cchunk * 8;
-    const bool kvalid = kbase < args.K;
-    const int seg = kvalid ? dm_div(args.dm_cseg, kbase) : 0;
-    const int ch = kbase - seg * args.Cseg;
-    const ConvSeg sg = segtab[seg];
-    const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch;
-    const int sh = (sg.dh + 1) | ((sg.dw + 1 + 3) << 8);
+    const int k0 = kt * 64;                               // uniform
+    const int seg = dm_div(args.dm_cseg, k0);
+    const int ch0 = k0 - seg * args.Cseg;
+    const ConvSeg sg = args.seg[seg];                     // uniform index: scalar load
+    const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
+    const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
     const T* base = (const T*)sg.ptr;
 #pragma unroll
     for (int i = 0; i < A_IN; ++i) {
-      const bool ok = kvalid && ((a_mask[i] >> (sh & 255)) & (a_mask[i] >> (sh >> 8)) & 1);
+      const bool ok = __builtin_amdgcn_ubfe(a_tap[i], tb, 1) != 0;
       const void* src = ok ? (const void*)(base + (unsigned)(a_off[i] + delta)) : zero;
-      glds16(src, A + (i * NW + wave) * 8 * 128);
+      glds16(src, A + (i * NW + wv) * 8 * 128);
     }
 #pragma unroll
-    for (int i = 0; i < B_IN; ++i) {
-      const void* src = b_row[i] ? (const void*)(b_row[i] + kbase) : zero;
-      glds16(src, B + (i * NW + wave) * 8 * 128);
-    }
+    for (int i = 0; i < B_IN; ++i) glds16(b_ptr[i] + (size_t)kt * b_step[i], B + (i * NW + wv) * 8 * 128);
   };
 
   f32x4_t acc[FM][FN];
@@ -698,32 +694,40 @@ bool shifts_small(const ConvGemmArgs& a) {  // LDS-DMA kernels: segment shifts i
 template <typename T>
 int launch_t(const ConvGemmArgs& a, hipStream_t st) {
   if constexpr (sizeof(T) == 2) {
-    if (!shifts_small(a)) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
     switch (g_conv_cfg) {
       case 1: return launch_cfg<T, 128, 64, 4, 1>(a, st);
       case 2: return launch_cfg<T, 128, 128, 2, 2>(a, st);
-      case 3: return launch_glds<128, 64, 2, 1>(a, st);
-      case 4: return launch_glds<256, 64, 4, 1>(a, st);
-      case 5: return launch_glds<128, 128, 2, 2>(a, st);
-      case 6: return launch_glds<256, 128, 2, 2>(a, st);
-      case 8: return launch_glds<128, 128, 2, 2, 3>(a, st);
-      case 9: return launch_glds<128, 128, 2, 2, 4>(a, st);
-      case 10: return launch_glds<256, 128, 4, 2, 3>(a, st);
-      case 11: return launch_glds<256, 64, 4, 1, 3>(a, st);
-      case 12: return launch_glds<128, 64, 2, 1, 4>(a, st);
-      case 13: return launch_glds<256, 128, 4, 2, 2>(a, st);
-      case 14: return launch_glds<128, 128, 4, 2, 2>(a, st);
-      case 15: return launch_glds<128, 64, 4, 1, 2>(a, st);
-      case 16: return launch_glds<128, 128, 4, 2, 3>(a, st);
-      case 17: return launch_glds<256, 64, 8, 1, 2>(a, st);
-      case 18: return launch_glds<256, 128, 8, 2, 2>(a, st);
       default: break;
+    }
+    // LDS-DMA kernels need shifts in [-1, 1] and 64-aligned segments (scalar address
+    // generation); everything else (the 8-channel first layer) takes the register-staged tile
+    const bool glds_ok = shifts_small(a) && a.Cseg % 64 == 0;
+    if (glds_ok) {
+      switch (g_conv_cfg) {
+        case 3: return launch_glds<128, 64, 2, 1>(a, st);
+        case 4: return launch_glds<256, 64, 4, 1>(a, st);
+        case 5: return launch_glds<128, 128, 2, 2>(a, st);
+        case 6: return launch_glds<256, 128, 2, 2>(a, st);
+        case 8: return launch_glds<128, 128, 2, 2, 3>(a, st);
+        case 9: return launch_glds<128, 128, 2, 2, 4>(a, st);
+        case 10: return launch_glds<256, 128, 4, 2, 3>(a, st);
+        case 11: return launch_glds<256, 64, 4, 1, 3>(a, st);
+        case 12: return launch_glds<128, 64, 2, 1, 4>(a, st);
+        case 13: return launch_glds<256, 128, 4, 2, 2>(a, st);
+        case 14: return launch_glds<128, 128, 4, 2, 2>(a, st);
+        case 15: return launch_glds<128, 64, 4, 1, 2>(a, st);
+        case 16: return launch_glds<128, 128, 4, 2, 3>(a, st);
+        case 17: return launch_glds<256, 64, 8, 1, 2>(a, st);
+        case 18: return launch_glds<256, 128, 8, 2, 2>(a, st);
+        default: break;
+      }
     }
     // measured on MI355X (tools/gemm_bench.py, the model's B=16 shapes): 8-wave LDS-DMA tiles
     // (waves of 32x64) beat 4-wave 64x64 ones -- twice the waves per SIMD hide the LDS and
     // DMA latency: 128x128/8 waves 690-730 TF on the 3x3 convs (vs ~600), 128x64/4 waves for
     // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
     if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
+    if (!glds_ok) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
     if (a.N <= 64) return launch_glds<128, 64, 4, 1, 2>(a, st);
     return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
