@@ -778,5 +778,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 6) { g_wgrad_waves = (value == 8 || value == 4) ? value : 0; return 0; }
   if (knob == 7) { g_wgrad_noglds = value; return 0; }
   if (knob == 8) { g_wgrad_narrow = value; return 0; }
+  if (knob == 9) { g_fra_generic = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -48,3 +48,4 @@ extern int g_wgrad_target;
 extern int g_wgrad_waves;
 extern int g_wgrad_noglds;
 extern int g_wgrad_narrow;
+extern int g_fra_generic;

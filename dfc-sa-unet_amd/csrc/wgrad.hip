@@ -390,7 +390,9 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
     dst[((int64_t)r * Creal + cin) * ntaps + tap] += s;
   } else if (layout == 2) {
-    // 1x1 weights stacked by rows: [0, Ctot) -> d0, [Ctot, 2 Ctot) -> d1, [2 Ctot, NI) -> d2
+    // 1x1 weights stacked by rows: [0, Ctot) -> d0, [Ctot, 2 Ctot) -> d1, [2 Ctot, 2 Ctot + Creal)
+    // -> d2; later rows are GEMM padding
+    if (i >= 2 * Ctot + Creal) return;
     const int d = i < Ctot ? 0 : (i < 2 * Ctot ? 1 : 2);
     float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
     dst[(int64_t)(i - d * Ctot) * NJ + j] += s;

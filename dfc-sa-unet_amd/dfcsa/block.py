@@ -6,6 +6,9 @@ graph would touch is produced by one of our kernels, parameter gradients are acc
 straight into ``param.grad`` (fp32), and the block input gradient is one implicit GEMM that
 fuses the 3x3 dgrad with both 1x1 dgrads (attention entry + residual).
 
+FullResAttnDFCBlock (models/unet_dfc_sa_ablation_attention.py:29-92) runs the same flow with the
+pooled LSA replaced by full-resolution attention on a = relu(bn2 y2) (dfcsa/fra.py).
+
 Activation flow per block (NHWC, dtype T; M = B*H*W pixels; C = out channels):
   GEMM 3x3            x -> y1 (+bias, BN1 stats)
   GEMM 1x1 (N = 2C)   x -> [y2 (+bias, BN2 stats) | res]        (one launch)
@@ -19,7 +22,7 @@ Activation flow per block (NHWC, dtype T; M = B*H*W pixels; C = out channels):
 import torch
 import torch.nn as nn
 
-from . import ops
+from . import fra, ops
 from ._lib import call
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
@@ -88,16 +91,25 @@ def block_forward(blk, xs, pool_size, training, dtype):
     bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt, C, C, M, training)
     bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt, C, N2, M, training)
 
-    # ---- LightSelfAttention on the pooled map ----
-    Pp = pool_size
     Cq = lsa.query_conv.out_channels
-    J, N = 2 * Cq + C, Pp * Pp
-    pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
-
-    local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
-         P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
+    if getattr(lsa, "full_resolution", False):
+        # ---- FullResolutionAttention (unet_dfc_sa_ablation_attention.py:42-47, :71-75) on the
+        #      unpooled map a = relu(bn2 y2): flash-style kernels, no N x N tensor ----
+        Pp, J, N = 0, 2 * Cq + C, H * W
+        local = ops.bn_act(dtype, y1, bn1, 1)
+        a = ops.bn_act(dtype, y2, bn2, 1)
+        attn, s.fra = fra.core_forward(lsa, a, dtype, pk)
+        pooled = qkv = A = o = Wqkv = None
+    else:
+        # ---- LightSelfAttention on the pooled map ----
+        s.fra = None
+        Pp = pool_size
+        J, N = 2 * Cq + C, Pp * Pp
+        pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
+        local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+        attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+        call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
+             P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
 
     # ---- gate + fusion ----
     y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
@@ -151,7 +163,11 @@ def _build_block_packs(ps, blk, dtype, Cin_p, C, has_res):
         ps.transpose(W2p, C, 0, C, Cin_p, "Wdx", wdx, dc0=10 * C)
     else:  # identity residual: constant identity block (written once)
         ps.buffer("Wdx", wdx, dtype)[:, 10 * C:11 * C].copy_(torch.eye(C, dtype=dtype, device=ps.device))
-    _build_lsa_packs(ps, blk.attn_branch[3])
+    att = blk.attn_branch[3]
+    if getattr(att, "full_resolution", False):
+        fra.build_packs(ps, att, dtype)
+    else:
+        _build_lsa_packs(ps, att)
 
 
 def _build_lsa_packs(ps, lsa):
@@ -226,13 +242,20 @@ def block_backward(blk, s, dout, need_dx, dtype):
     ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
 
-    # ---- LightSelfAttention ----
-    dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
-
-    # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
     dz2 = torch.empty_like(s.y2)
-    call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale), P(bn2.shift),
-         P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part), stream())
+    if s.fra is not None:
+        # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
+        da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
+        s.fra = None
+        call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+             P(bn2.invstd), P(dz2), P(part), stream())
+        del da
+    else:
+        # ---- LightSelfAttention ----
+        dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
+        # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
+        call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
+             P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part), stream())
     del dattn
     coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
     dy2 = ops.bn_bwd_apply(dtype, dz2, s.y2, bn2, bn2m.weight, coef, grad_of(conv2.bias))

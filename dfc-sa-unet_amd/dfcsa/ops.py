@@ -174,6 +174,14 @@ def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
     return st
 
 
+def bn_act(dtype, y, bn, act):
+    """act(y * scale + shift): act 0 none, 1 relu, 2 sigmoid (NHWC, new tensor)."""
+    out = torch.empty_like(y)
+    C = y.shape[-1]
+    call("dfcsa_bn_act", dt(dtype), y.numel() // C, C, P(y), P(bn.scale), P(bn.shift), int(act), P(out), stream())
+    return out
+
+
 def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
     partial, ntiles = rows_reduce(partial, ntiles, nsum * C)

@@ -7,8 +7,9 @@ when no config is given or the model name is unknown).  Optional new keys (ignor
 reference, so unchanged yamls still run): ``model.precision`` / ``training.precision``
 ('bf16' default, 'fp32').
 
-Built on the MI355X path: 'DFC-SA-Res-Block' (UNetDFCSARes, the north-star model).  The other
-names the reference knows ('UNet', 'TransUNet', the ablation and ViT models) raise
+Built on the MI355X path: 'DFC-SA-Res-Block' (UNetDFCSARes, the north-star model), 'UNet'
+(config 1, model_factory.py:94-100) and 'UNet_FullResAttention' (config 5, :174-175).  The other
+names the reference knows (TransUNet, the other ablation models, the ViT) raise
 NotImplementedError naming what is missing.
 
 Pretrained weights are loaded with torch.load(weights_only=True) (a state_dict needs nothing
@@ -16,11 +17,14 @@ else); as in the reference a failure is reported and not raised.
 """
 import torch
 
+from models.unet import UNet
+from models.unet_dfc_sa_ablation_attention import UNet_FullResAttention
 from models.unet_dfc_sa_res import UNetDFCSARes
 
+_BUILT = ("DFC-SA-Res-Block", "UNet", "UNet_FullResAttention")
 _REFERENCE_ONLY = {
-    "UNet", "TransformerUNet", "TransUNet", "VisionTransformerSegmentation", "UNet_Baseline",
-    "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion", "UNet_FullResAttention",
+    "TransformerUNet", "TransUNet", "VisionTransformerSegmentation", "UNet_Baseline",
+    "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
     "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv",
 }
 
@@ -58,11 +62,16 @@ class ModelFactory:
         pool_size = m.get("pool_size", 8)
         qk = m.get("ablation_on_qk_channels", 8)
         precision = m.get("precision", config.get("training", {}).get("precision"))
+        if name == "UNet":  # features / pool_size are ignored, as in the reference (:94-100)
+            return UNet(n_channels=in_channels, n_classes=out_channels, bilinear=m.get("bilinear", False),
+                        precision=precision)
         if name == "DFC-SA-Res-Block":
             return UNetDFCSARes(in_channels=in_channels, out_channels=out_channels, features=features,
                                 pool_size=pool_size, ablation_on_qk_channels=qk, precision=precision)
+        if name == "UNet_FullResAttention":
+            return UNet_FullResAttention(in_channels, out_channels, features, precision=precision)
         if name in _REFERENCE_ONLY:
             raise NotImplementedError(
                 f"model {name!r} exists in the reference but is not built on the MI355X path yet "
-                f"(built: 'DFC-SA-Res-Block')")
+                f"(built: {', '.join(_BUILT)})")
         raise ValueError(f"不支援的模型類型: {name}")

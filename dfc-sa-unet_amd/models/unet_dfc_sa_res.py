@@ -68,7 +68,7 @@ class DynamicFusionConvAttnBlock(nn.Module):
         self.attn_branch = nn.Sequential(
             nn.Conv2d(in_channels, out_channels, kernel_size=1),
             nn.BatchNorm2d(out_channels), nn.ReLU(inplace=True),
-            LightSelfAttention(out_channels, pool_size=pool_size, ablation_on_qk_channels=ablation_on_qk_channels))
+            self._make_attention(out_channels, pool_size, ablation_on_qk_channels))
         self.gate = nn.Sequential(
             nn.Conv2d(out_channels * 2, out_channels, kernel_size=1),
             nn.BatchNorm2d(out_channels), nn.Sigmoid())
@@ -81,6 +81,10 @@ class DynamicFusionConvAttnBlock(nn.Module):
             self.residual_conv = nn.Identity()
         self.res_scale = nn.Parameter(torch.tensor(0.1))
         self.compute_dtype = torch.bfloat16
+
+    def _make_attention(self, channels, pool_size, ablation_on_qk_channels):
+        """The attention module of the branch (subclasses swap it; created in the reference's order)."""
+        return LightSelfAttention(channels, pool_size=pool_size, ablation_on_qk_channels=ablation_on_qk_channels)
 
     def forward_nhwc(self, xs, dtype):
         """xs: list of NHWC sources whose channel concat is the block input (skip concat
@@ -105,9 +109,7 @@ class UNetDFCSA(nn.Module):
         for c in f:
             if c % 8:
                 raise ValueError(f"feature widths must be multiples of 8 for the NHWC kernels, got {f}")
-        blk = lambda i, o: DynamicFusionConvAttnBlock(  # noqa: E731
-            i, o, kernel_size=3, stride=1, padding=1, pool_size=pool_size,
-            ablation_on_qk_channels=ablation_on_qk_channels)
+        blk = lambda i, o: self._make_block(i, o, pool_size, ablation_on_qk_channels)  # noqa: E731
         self.pool_size = pool_size
         self.in_channels = in_channels
         self.down1 = blk(in_channels, f[0])
@@ -130,6 +132,11 @@ class UNetDFCSA(nn.Module):
         self.final_conv = nn.Conv2d(f[0], out_channels, kernel_size=1)
         self.compute_dtype = dfcsa.resolve_dtype(precision)
         self._flat = None
+
+    def _make_block(self, in_channels, out_channels, pool_size, ablation_on_qk_channels):
+        """Block factory (AblationUNetBase's block_func, unet_dfc_sa_ablation_branches.py:105)."""
+        return DynamicFusionConvAttnBlock(in_channels, out_channels, kernel_size=3, stride=1, padding=1,
+                                          pool_size=pool_size, ablation_on_qk_channels=ablation_on_qk_channels)
 
     # -------------------------------------------------------------- precision / storage
     def set_precision(self, precision):

@@ -89,8 +89,9 @@ int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
  *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.
  *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij].
- *  layout 2 (stacked 1x1 q/k/v): rows [0,Ctot) -> dst[0], [Ctot,2Ctot) -> dst[1], rest -> dst[2];
- *     dst[d][row - base][j] with NJ columns (ndst must be 3). */
+ *  layout 2 (stacked 1x1 q/k/v): rows [0,Ctot) -> dst[0], [Ctot,2Ctot) -> dst[1],
+ *     [2Ctot, 2Ctot+Creal) -> dst[2], later rows (GEMM padding) dropped; dst[d][row - base][j]
+ *     with NJ columns (ndst must be 3). */
 int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                        int Ctot, int Creal, int ndst, float* const* dst, void* stream);
 
@@ -321,12 +322,49 @@ int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const float* parti
                    int* mom_init, const float* skip_if_nonfinite, float* norm_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Full-resolution self-attention (models/unet_dfc_sa_ablation_attention.py:15-26, the attention
+ * of FullResAttnDFCBlock / UNet_FullResAttention, config_ablation3_full_res_attn.yaml), flash-style:
+ * the N x N score matrix is never stored.  Per image (N = H*W tokens) qkv is NHWC [B][N][ldq] with
+ * q at columns [0,Cq), k at [Cq,2Cq), v at [2Cq,2Cq+C) (the 1x1 projections, done by
+ * dfcsa_conv_gemm); A = softmax_rows(q k^T) (no scale), O = A v.
+ * fwd: o = O [B][N][C], y = gamma*O + x [B][N][C] (dtype), lse [B*N] fp32 = log-sum-exp of each
+ *      score row (saved for the backward).
+ * bwd_prep: r[row] = sum_c dy*o (dgamma = sum r; delta = gamma*r).
+ * bwd: dqkv [B][N][ldq] = gradients of q, k, v for dy at y (padding columns zeroed); P is
+ *      recomputed from lse.
+ * path: 1 if the bf16 MFMA kernels serve this shape (fwd: C % 64 == 0, Cq in {8..128} powers of 2;
+ *      bwd: C in {64, 128}, Cq in {8, 16, 32}), 0 = the generic kernels (fp32, other shapes).
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_fra_path(int dtype, int C, int Cq, int ldq, int backward);
+int dfcsa_fra_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* x,
+                  const float* gamma, void* o, void* y, float* lse, void* stream);
+int dfcsa_fra_bwd_prep(int dtype, int rows, int C, const void* dy, const void* o, float* r, void* stream);
+int dfcsa_fra_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* dy,
+                  const float* gamma, const float* lse, const float* r, void* dqkv, void* stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Plain U-Net (models/unet.py, BASELINE config 1): MaxPool2d(2, ceil_mode=True) (:26) and the
+ * crop-to-match of Up.forward (:47-55), NHWC, C % 8 == 0.
+ * ---------------------------------------------------------------------------------------- */
+/* out [B][ceil(H/2)][ceil(W/2)][C] = max over the in-bounds pixels of each 2x2 window
+ * (first maximum in window order, NaN propagates, as ATen) */
+int dfcsa_maxpool2_ceil_fwd(int dtype, int B, int H, int W, int C, const void* x, void* out, void* stream);
+/* dx (every element written) = dout at the window's first maximum, 0 elsewhere */
+int dfcsa_maxpool2_ceil_bwd(int dtype, int B, int H, int W, int C, const void* x, const void* dout, void* dx,
+                            void* stream);
+/* dst [B][Hd][Wd][C]: dst[b][h][w][c] = src[b][h + oy][w + ox][c] inside src [B][Hs][Ws][C], else 0
+ * (a crop for oy, ox >= 0; its backward with -oy, -ox) */
+int dfcsa_window_copy(int dtype, int B, int C, int Hs, int Ws, const void* src, int Hd, int Wd, void* dst, int oy,
+                      int ox, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Profiling hook: when enabled for a kernel class, every launch of that class is bracketed by
  * hipEvents on its own stream; dfcsa_prof_read returns the summed elapsed milliseconds and
  * the launch count since the last reset (synchronises on the recorded events).
  * ---------------------------------------------------------------------------------------- */
 #define DFCSA_PROF_CONV_GEMM 1
 #define DFCSA_PROF_WGRAD 2
+#define DFCSA_PROF_ATTN 3
 int dfcsa_prof_enable(int kernel_class, int enable);
 int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, double* flops);
 
@@ -338,7 +376,8 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 5: 1 = use the 1x1 streaming GEMM whenever it applies (coverage tests).
  * knob 6: waves per weight-gradient workgroup (4 or 8; 0 = automatic).
  * knob 7: 1 = register-staged bf16 weight gradient instead of the LDS-DMA kernel.
- * knob 8: 0 = allow the 64x256 weight-gradient tile for 64-row problems (default 1: off). */
+ * knob 8: 0 = allow the 64x256 weight-gradient tile for 64-row problems (default 1: off).
+ * knob 9: 1 = generic (non-MFMA) full-resolution attention kernels (coverage tests). */
 int dfcsa_set_tuning(int knob, int value);
 
 const char* dfcsa_version(void);

@@ -19,6 +19,11 @@ Reference functions restated (file:line under the reference checkout):
   * calculate_metrics ('bce_dice')        utils/metrics.py:211-264          -> calculate_metrics
   * train step (zero_grad, fwd, sigmoid, loss, backward, clip_grad_norm_(1.0), SGD)
                                           utils/trainer.py:115-151, train.py:73-78 -> train_step
+  * FullResolutionAttention.forward       models/unet_dfc_sa_ablation_attention.py:15-26
+                                                                   -> full_resolution_attention
+  * FullResAttnDFCBlock / UNet_FullResAttention (AblationUNetBase.forward,
+    models/unet_dfc_sa_ablation_branches.py:129-164)          -> dfc_block / unet_dfc_sa_res(full_res=True)
+  * UNet.forward (DoubleConv, Down, Up, OutConv)  models/unet.py:6-101        -> unet
 """
 import math
 
@@ -70,13 +75,31 @@ def light_self_attention(a, sd, name, pool_size):
     return sd[name + ".gamma"] * o + a
 
 
-def dfc_block(x, sd, name, pool_size, training, bufs):
-    """models/unet_dfc_sa_res.py:95-116 (DynamicFusionConvAttnBlock.forward)."""
+def full_resolution_attention(a, sd, name):
+    """models/unet_dfc_sa_ablation_attention.py:15-26: attention over all H*W positions, q/k with
+    C//8 channels, softmax over keys without a 1/sqrt(d) scale, gamma-scaled residual."""
+    B, C, H, W = a.shape
+    N = H * W
+    q = conv(a, sd, name + ".query_conv").reshape(B, -1, N).permute(0, 2, 1)    # [B,N,C']
+    k = conv(a, sd, name + ".key_conv").reshape(B, -1, N)                       # [B,C',N]
+    att = torch.softmax(torch.bmm(q, k), dim=-1)                                # [B,N,N]
+    v = conv(a, sd, name + ".value_conv").reshape(B, -1, N)                     # [B,C,N]
+    o = torch.bmm(v, att.permute(0, 2, 1)).reshape(B, C, H, W)
+    return sd[name + ".gamma"] * o + a
+
+
+def dfc_block(x, sd, name, pool_size, training, bufs, full_res=False):
+    """models/unet_dfc_sa_res.py:95-116 (DynamicFusionConvAttnBlock.forward); with full_res the
+    attention branch is FullResolutionAttention (unet_dfc_sa_ablation_attention.py:71-92, otherwise
+    identical)."""
     local = F.relu(batch_norm(conv(x, sd, name + ".conv_branch.0", padding=1), sd,
                               name + ".conv_branch.1", training, bufs))
     a = F.relu(batch_norm(conv(x, sd, name + ".attn_branch.0"), sd, name + ".attn_branch.1",
                           training, bufs))
-    attn = light_self_attention(a, sd, name + ".attn_branch.3", pool_size)
+    if full_res:
+        attn = full_resolution_attention(a, sd, name + ".attn_branch.3")
+    else:
+        attn = light_self_attention(a, sd, name + ".attn_branch.3", pool_size)
     comb = torch.cat([local, attn], dim=1)
     g = torch.sigmoid(batch_norm(conv(comb, sd, name + ".gate.0"), sd, name + ".gate.1",
                                  training, bufs))
@@ -94,9 +117,11 @@ def conv_transpose2x2(x, sd, name):
     return F.conv_transpose2d(x, sd[name + ".weight"], sd[name + ".bias"], stride=2)
 
 
-def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None):
-    """models/unet_dfc_sa_res.py:161-204 (UNetDFCSA.forward; UNetDFCSARes adds nothing)."""
-    blk = lambda t, n: dfc_block(t, sd, n, pool_size, training, bufs)  # noqa: E731
+def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None, full_res=False):
+    """models/unet_dfc_sa_res.py:161-204 (UNetDFCSA.forward; UNetDFCSARes adds nothing).  With
+    full_res: UNet_FullResAttention (AblationUNetBase.forward, unet_dfc_sa_ablation_branches.py:
+    129-164, the same graph with FullResAttnDFCBlock blocks)."""
+    blk = lambda t, n: dfc_block(t, sd, n, pool_size, training, bufs, full_res)  # noqa: E731
     d1 = blk(x, "down1")
     d2 = blk(F.max_pool2d(d1, 2, 2), "down2")
     d3 = blk(F.max_pool2d(d2, 2, 2), "down3")
@@ -108,6 +133,29 @@ def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None):
             u = F.interpolate(u, size=skip.shape[2:], mode="bilinear", align_corners=False)
         u = blk(torch.cat([u, skip], dim=1), f"up_conv{lvl}")
     return conv(u, sd, "final_conv")
+
+
+def unet(x, sd, training=True, bufs=None):
+    """models/unet.py:69-101 with bilinear=False: DoubleConv (:6-18), Down = MaxPool2d(2,
+    ceil_mode=True) + DoubleConv (:21-30), Up = ConvTranspose2d(k2, s2) + crop + cat([skip, up]) +
+    DoubleConv (:33-58), OutConv 1x1 (:61-66)."""
+    def dconv(t, n):
+        for i in (0, 3):
+            t = F.relu(batch_norm(conv(t, sd, f"{n}.conv.{i}", padding=1), sd, f"{n}.conv.{i + 1}", training, bufs))
+        return t
+    xs = [dconv(x, "inc")]
+    for i in range(1, 5):
+        xs.append(dconv(F.max_pool2d(xs[-1], 2, ceil_mode=True), f"down{i}.mpconv.1"))
+    u = xs[4]
+    for i, skip in zip(range(1, 5), (xs[3], xs[2], xs[1], xs[0])):
+        u = F.conv_transpose2d(u, sd[f"up{i}.up.weight"], sd[f"up{i}.up.bias"], stride=2)
+        dy, dx = skip.shape[2] - u.shape[2], skip.shape[3] - u.shape[3]
+        if dy < 0 or dx < 0:
+            u = u[:, :, :skip.shape[2], :skip.shape[3]]
+        else:
+            skip = skip[:, :, dy // 2:dy // 2 + u.shape[2], dx // 2:dx // 2 + u.shape[3]]
+        u = dconv(torch.cat([skip, u], dim=1), f"up{i}.conv")
+    return conv(u, sd, "outc.conv")
 
 
 # ------------------------------------------------------------------------------------------
@@ -149,13 +197,16 @@ def param_names(sd):
                                   or k.endswith("num_batches_tracked"))]
 
 
-def forward_backward(sd, x, t, pool_size, loss_params=None):
+def forward_backward(sd, x, t, pool_size, loss_params=None, model="dfc"):
     """fwd -> sigmoid -> calculate_metrics -> backward.  Returns (logits, metrics, grads,
-    updated BN buffers)."""
+    updated BN buffers).  model: 'dfc' (UNetDFCSARes), 'fullres' (UNet_FullResAttention), 'unet'."""
     params = {k: (v.detach().clone().requires_grad_(True) if k in set(param_names(sd)) else v)
               for k, v in sd.items()}
     bufs = {}
-    logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs)
+    if model == "unet":
+        logits = unet(x, params, training=True, bufs=bufs)
+    else:
+        logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs, full_res=(model == "fullres"))
     met = calculate_metrics(torch.sigmoid(logits), t, "bce_dice", loss_params)
     met["loss"].backward()
     grads = {k: params[k].grad.detach().clone() for k in param_names(sd)}

@@ -10,6 +10,10 @@ Reference files imported (file-by-file, via importlib, because the reference's p
                                 UNetDFCSA :118-204, UNetDFCSARes :207-220
   * utils/metrics.py            dice_loss :6-24, BCEDiceLoss :52-78, calculate_metrics :211-264
   * models/unet.py              UNet :69-101 (config 1)
+  * models/unet_dfc_sa_ablation_attention.py   FullResolutionAttention :7-26, FullResAttnDFCBlock
+                                :29-92, UNet_FullResAttention :95-97 (config 5; imported under a stub
+                                package because it uses a package-relative import of
+                                unet_dfc_sa_ablation_branches.py)
 The train-step semantics follow utils/trainer.py:115-151 and train.py:73-78.
 
 Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz, ~a few MB)
@@ -37,6 +41,22 @@ ref_metrics = _load("ref_metrics", "utils/metrics.py")
 ref_unet = _load("ref_unet", "models/unet.py")
 
 
+def _load_models_pkg(relmod):
+    """Import reference models/<relmod>.py inside a stub package so its relative imports resolve
+    (the reference's own models/__init__.py imports a module that does not exist)."""
+    import types
+    if "refmodels" not in sys.modules:
+        pkg = types.ModuleType("refmodels")
+        pkg.__path__ = [os.path.join(REF, "models")]
+        sys.modules["refmodels"] = pkg
+    name = "refmodels." + relmod
+    spec = importlib.util.spec_from_file_location(name, os.path.join(REF, "models", relmod + ".py"))
+    mod = importlib.util.module_from_spec(spec)
+    sys.modules[name] = mod
+    spec.loader.exec_module(mod)
+    return mod
+
+
 def np32(t):
     return t.detach().cpu().numpy().astype(np.float32)
 
@@ -53,6 +73,26 @@ def sd_arrays(module, prefix="sd."):
 
 def grad_arrays(module, prefix="grad."):
     return {prefix + n: np32(p.grad) for n, p in module.named_parameters() if p.grad is not None}
+
+
+def fp64_noise(module32, module64, prefix="noise."):
+    """Per-tensor relative distance between the reference's fp32 gradients and the same reference
+    run in float64 on the same weights and inputs: the reference's own fp32 rounding floor.  The GPU
+    tests scale their gradient tolerance by it (deep nets with train-mode BatchNorm amplify fp32
+    summation-order differences into gradient noise of a few 1e-3 on some tensors)."""
+    g64 = dict(module64.named_parameters())
+    out = {}
+    for n, p in module32.named_parameters():
+        if p.grad is None:
+            continue
+        a, b = p.grad.double(), g64[n].grad
+        out[prefix + n] = np.float64(((a - b).norm() / (b.norm() + 1e-30)).item())
+    return out
+
+
+def fp64_twin(module):
+    import copy
+    return copy.deepcopy(module).double()
 
 
 # ----------------------------------------------------------------------------------------
@@ -265,22 +305,91 @@ def gen_ddp():
 # (6) Config 1 plumbing: plain UNet (widths hard-coded 64..1024) at 64x64, batch 2.
 # ----------------------------------------------------------------------------------------
 def gen_unet():
-    torch.manual_seed(6000)
-    m = ref_unet.UNet(3, 1, bilinear=False)
-    m.train()
-    x = torch.randn(2, 3, 20, 20)
-    t = (torch.rand(2, 1, 20, 20) > 0.5).float()
-    out = m(x)
-    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", {})
+    """20x20 (odd sizes: ceil-mode pooling 20->10->5->3->2 and both crop branches) and the
+    config-1 size 64x64, batch 2.  The 31 M parameters are not stored: the test builds the model
+    under the same seed (module tree and init order are the reference's) and checks per-tensor
+    init sums first; gradients are stored for the small tensors plus per-tensor norms."""
+    def run(seed, shape, name):
+        torch.manual_seed(seed)
+        m = ref_unet.UNet(3, 1, bilinear=False)
+        init = {"init_sum." + k: np.float64(v.double().sum()) for k, v in m.state_dict().items()
+                if v.is_floating_point()}
+        m.train()
+        m64 = fp64_twin(m)
+        x = torch.randn(*shape)
+        t = (torch.rand(shape[0], 1, shape[2], shape[3]) > 0.5).float()
+        out = m(x)
+        met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", {})
+        met["loss"].backward()
+        met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", {})
+        met64["loss"].backward()
+        n = sum(p.numel() for p in m.parameters())
+        keep = [k for k, p in m.named_parameters()
+                if p.numel() <= 4096 or k in ("inc.conv.0.weight", "outc.conv.weight")]
+        g64 = dict(m64.named_parameters())
+        small = {"grad." + k: np32(p.grad) for k, p in m.named_parameters() if k in keep}
+        small.update({"grad64." + k: np32(g64[k].grad) for k in keep})
+        norms = {"gnorm." + k: np.float64(p.grad.double().norm()) for k, p in m.named_parameters()}
+        bufs = {"buf." + k: v.numpy().copy() for k, v in m.state_dict().items() if "running" in k}
+        save(name, x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]), iou=np.float64(met["iou"]),
+             dice=np.float64(met["dice"]), nparams=np.int64(n), **init, **small, **norms, **bufs,
+             **fp64_noise(m, m64))
+    run(6000, (2, 3, 20, 20), "unet_small.npz")
+    run(6001, (2, 3, 64, 64), "unet_cfg1.npz")
+
+
+# ----------------------------------------------------------------------------------------
+# (7) Config 5: full-resolution attention (module, block, small model), gamma != 0.
+# ----------------------------------------------------------------------------------------
+def gen_fullres():
+    fra = _load_models_pkg("unet_dfc_sa_ablation_attention")
+    for (C, H) in [(16, 6), (32, 8), (64, 12)]:   # C = 16: q/k width 2 (padded GEMM width)
+        torch.manual_seed(7000 + C + H)
+        m = fra.FullResolutionAttention(C)
+        with torch.no_grad():
+            m.gamma.fill_(0.7)
+            m.query_conv.weight.mul_(3.0)   # sharper softmax than the default init
+            m.key_conv.weight.mul_(3.0)
+        x = torch.randn(2, C, H, H + 1, requires_grad=True)   # non-square map, N = H * (H + 1)
+        y = m(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        save(f"fra_C{C}_H{H}.npz", x=np32(x), g=np32(g), y=np32(y), dx=np32(x.grad), **sd_arrays(m),
+             **grad_arrays(m))
+    for (cin, cout, H) in [(8, 32, 10), (16, 16, 8)]:   # (16, 16): identity residual
+        torch.manual_seed(7100 + cin + cout + H)
+        blk = fra.FullResAttnDFCBlock(cin, cout)
+        with torch.no_grad():
+            blk.attn_branch[3].gamma.fill_(0.7)
+        sd0 = sd_arrays(blk, "sd0.")
+        blk.train()
+        x = torch.randn(2, cin, H, H, requires_grad=True)
+        y = blk(x)
+        g = torch.randn_like(y)
+        y.backward(g)
+        save(f"frablock_{cin}to{cout}_H{H}.npz", x=np32(x), g=np32(g), y=np32(y), dx=np32(x.grad), **sd0,
+             **sd_arrays(blk, "sd1."), **grad_arrays(blk))
+    torch.manual_seed(7200)
+    model = fra.UNet_FullResAttention(3, 1, [8, 16, 32, 64])
+    perturb_gammas(model)
+    sd0 = sd_arrays(model, "sd0.")
+    model.train()
+    m64 = fp64_twin(model)
+    gen = torch.Generator().manual_seed(7201)
+    x, t = batch(gen, (2, 3, 16, 16))
+    out = model(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
     met["loss"].backward()
-    n = sum(p.numel() for p in m.parameters())
-    save("unet_small.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
-         nparams=np.int64(n))
+    met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", LOSS_PARAMS)
+    met64["loss"].backward()
+    save("fullres_model.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+         iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), **sd0, **grad_arrays(model),
+         **fp64_noise(model, m64), **grad_arrays(m64, "grad64."))
 
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet"]
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres"]
     for w in which:
         globals()["gen_" + w]()
     print("torch", torch.__version__)

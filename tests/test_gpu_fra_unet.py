@@ -1,0 +1,309 @@
+"""MI355X parity of the config-5 path (full-resolution attention, csrc/fra.hip) and the config-1
+plain U-Net against the golden fixtures produced by the reference (tests/golden/make_golden.py)
+and against plain PyTorch fp32 references of the same ops.
+
+fp32 compute mode: module/block outputs 1e-5 .. 1e-4 relative, gradients 1e-3 (north star 1e-4
+on logits/loss); bf16 compute mode (MFMA kernels): outputs 1e-2, gradients 3e-2..5e-2 relative
+norm (bf16 operands with fp32 accumulation, statistics and softmax).
+"""
+import ctypes
+import glob
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+LP = {"bce_weight": 0.5, "dice_weight": 0.5}
+
+
+def T(a, dev="cuda"):
+    return torch.from_numpy(np.asarray(a)).to(dev)
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(np.asarray(b) if not torch.is_tensor(b) else b).detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def sd_from(fx, prefix):
+    return {k[len(prefix):]: torch.from_numpy(np.asarray(v)) for k, v in fx.items() if k.startswith(prefix)}
+
+
+ZERO_TRUE_GRAD = ("conv_branch.0.bias", "attn_branch.0.bias", "gate.0.bias", "fusion_conv.0.bias", "key_conv.bias",
+                  "conv.0.bias", "conv.3.bias")
+
+
+def check_grads(named, fx, prefix="grad.", tol=1e-3):
+    for n, p in named:
+        ref = fx.get(prefix + n)
+        if ref is None:
+            continue
+        assert p.grad is not None, n
+        if n.endswith(ZERO_TRUE_GRAD):
+            # true gradient is 0 (a train-mode BatchNorm follows / softmax is shift-invariant over keys)
+            wk = prefix + n[:-4] + "weight"
+            scale = max(np.abs(fx[wk]).max(), 1e-6) if wk in fx else 1e-3
+            assert np.abs(p.grad.double().cpu().numpy() - ref).max() < tol * scale, n
+            continue
+        ref64 = fx.get("grad64." + n)
+        if ref64 is not None:
+            # against the same reference run in float64: within max(tol, 2x the reference's own fp32
+            # error "noise.<name>" = |ref_fp32 - ref_fp64| / |ref_fp64|, make_golden.fp64_noise)
+            lim = max(tol, 2.0 * float(fx.get("noise." + n, 0.0)))
+            r = rel(p.grad, ref64)
+            assert r < lim, (n, r, lim)
+            continue
+        r = rel(p.grad, ref)
+        assert r < tol, (n, r)
+
+
+@pytest.fixture
+def generic_attention():
+    from dfcsa import set_tuning
+    set_tuning(9, 1)
+    yield
+    set_tuning(9, 0)
+
+
+# ----------------------------------------------------------------------------- attention module
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "fra_*.npz"))), ids=os.path.basename)
+def test_fra_module_fp32(path):
+    from models.unet_dfc_sa_ablation_attention import FullResolutionAttention
+    fx = dict(np.load(path))
+    C = fx["x"].shape[1]
+    m = FullResolutionAttention(C).cuda()
+    m.load_state_dict({k[3:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd.")})
+    m.compute_dtype = torch.float32
+    x = T(fx["x"]).requires_grad_(True)
+    y = m(x)
+    y.backward(T(fx["g"]))
+    assert rel(y, fx["y"]) < 1e-5
+    assert rel(x.grad, fx["dx"]) < 1e-4
+    check_grads(m.named_parameters(), fx, tol=1e-3)
+
+
+def _fra_torch(x, m):
+    """plain PyTorch fp32 FullResolutionAttention (reference :15-26) with m's parameters."""
+    B, C, H, W = x.shape
+    q = F.conv2d(x, m.query_conv.weight, m.query_conv.bias).reshape(B, -1, H * W).permute(0, 2, 1)
+    k = F.conv2d(x, m.key_conv.weight, m.key_conv.bias).reshape(B, -1, H * W)
+    a = torch.softmax(torch.bmm(q, k), dim=-1)
+    v = F.conv2d(x, m.value_conv.weight, m.value_conv.bias).reshape(B, C, H * W)
+    return m.gamma * torch.bmm(v, a.permute(0, 2, 1)).reshape(B, C, H, W) + x
+
+
+def _fra_case(C, H, W, dtype, seed=0):
+    from models.unet_dfc_sa_ablation_attention import FullResolutionAttention
+    torch.manual_seed(seed)
+    m = FullResolutionAttention(C).cuda()
+    with torch.no_grad():   # sharper-than-init softmax, score scale kept comparable across widths
+        m.gamma.fill_(0.7)
+        m.query_conv.weight.mul_(3.0 * (64 / C) ** 0.5)
+        m.key_conv.weight.mul_(3.0 * (64 / C) ** 0.5)
+    m.compute_dtype = dtype
+    x = torch.randn(2, C, H, W, device="cuda")
+    g = torch.randn(2, C, H, W, device="cuda")
+    xr = x.clone().requires_grad_(True)
+    yr = _fra_torch(xr, m)
+    gr = torch.autograd.grad(yr, [xr] + list(m.parameters()), g)
+    xk = x.clone().requires_grad_(True)
+    for p in m.parameters():
+        p.grad = None
+    y = m(xk)
+    y.backward(g)
+    return m, yr, gr, y, xk.grad
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 32, 32), (64, 30, 30), (128, 16, 16), (128, 12, 20), (256, 8, 8),
+                                   (512, 8, 8)])
+def test_fra_bf16_mfma_vs_torch_fp32(C, H, W):
+    """bf16 MFMA flash kernels (fwd for all widths; bwd MFMA for C <= 128) against plain PyTorch
+    fp32 on the same weights; N not a multiple of the 64/128 tiles exercises the masking."""
+    from dfcsa._lib import LIB
+    J = 2 * (C // 8) + C
+    assert LIB.dfcsa_fra_path(1, C, C // 8, J, 0) == 1
+    assert LIB.dfcsa_fra_path(1, C, C // 8, J, 1) == (1 if C <= 128 else 0)
+    m, yr, gr, y, dx = _fra_case(C, H, W, torch.bfloat16)
+    assert rel(y, yr) < 1e-2
+    assert rel(dx, gr[0]) < 3e-2
+    for (n, p), ref in zip(m.named_parameters(), gr[1:]):
+        if n == "key_conv.bias":   # true gradient 0 (softmax is invariant to a per-query shift)
+            continue
+        assert rel(p.grad, ref) < 5e-2, (n, rel(p.grad, ref))
+
+
+@pytest.mark.parametrize("C,H,W", [(64, 16, 16), (128, 10, 10)])
+def test_fra_generic_bf16_vs_torch_fp32(C, H, W, generic_attention):
+    from dfcsa._lib import LIB
+    assert LIB.dfcsa_fra_path(1, C, C // 8, 2 * (C // 8) + C, 0) == 0
+    m, yr, gr, y, dx = _fra_case(C, H, W, torch.bfloat16, seed=1)
+    assert rel(y, yr) < 1e-2
+    assert rel(dx, gr[0]) < 3e-2
+
+
+def test_fra_zero_gamma_gives_identity_and_no_qkv_grads():
+    """gamma initialises to 0 (reference :13): out == x exactly and the q/k/v gradients vanish."""
+    from models.unet_dfc_sa_ablation_attention import FullResolutionAttention
+    torch.manual_seed(3)
+    m = FullResolutionAttention(64).cuda()
+    m.compute_dtype = torch.float32
+    x = torch.randn(1, 64, 16, 16, device="cuda", requires_grad=True)
+    y = m(x)
+    assert torch.equal(y, x)
+    y.backward(torch.ones_like(y))
+    assert torch.all(m.value_conv.weight.grad == 0) and torch.all(m.query_conv.weight.grad == 0)
+    assert torch.equal(x.grad, torch.ones_like(x))
+
+
+# ----------------------------------------------------------------------------- block + model (config 5)
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "frablock_*.npz"))), ids=os.path.basename)
+def test_fra_block_fp32(path):
+    from models.unet_dfc_sa_ablation_attention import FullResAttnDFCBlock
+    fx = dict(np.load(path))
+    name = os.path.basename(path)
+    cin, cout = int(name.split("_")[1].split("to")[0]), int(name.split("to")[1].split("_")[0])
+    blk = FullResAttnDFCBlock(cin, cout).cuda()
+    blk.load_state_dict(sd_from(fx, "sd0."))
+    blk.compute_dtype = torch.float32
+    blk.train()
+    x = T(fx["x"]).requires_grad_(True)
+    y = blk(x)
+    y.backward(T(fx["g"]))
+    assert rel(y, fx["y"]) < 1e-5
+    assert rel(x.grad, fx["dx"]) < 1e-4
+    check_grads(blk.named_parameters(), fx, tol=1e-3)
+    sd1 = sd_from(fx, "sd1.")
+    for k, v in blk.state_dict().items():
+        if "running" in k or "num_batches" in k:
+            assert rel(v.float(), sd1[k].float()) < 1e-5, k
+
+
+def test_fullres_model_fp32_and_factory():
+    from dfcsa.loss import sigmoid
+    from models.model_factory import ModelFactory
+    from utils.metrics import calculate_metrics
+    fx = dict(np.load(os.path.join(GOLDEN, "fullres_model.npz")))
+    cfg = {"model": {"name": "UNet_FullResAttention", "features": [8, 16, 32, 64], "precision": "fp32"},
+           "training": {}}
+    model = ModelFactory.get_model(cfg)
+    model.load_state_dict(sd_from(fx, "sd0."))
+    model = model.cuda().train()
+    logits = model(T(fx["x"]))
+    met = calculate_metrics(sigmoid(logits), T(fx["t"]), "bce_dice", LP)
+    met["loss"].backward()
+    assert rel(logits, fx["logits"]) < 1e-4
+    assert abs(met["loss"].item() - float(fx["loss"])) < 1e-4 * abs(float(fx["loss"]))
+    assert abs(met["dice"] - float(fx["dice"])) < 1e-6
+    check_grads(model.named_parameters(), fx, tol=2e-3)
+
+
+def test_fullres_model_bf16_train_step():
+    """bf16 UNet_FullResAttention train step at 64x64 (N = 4096 tokens at level 1): finite loss,
+    logits near the fp32 path on the same weights."""
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.unet_dfc_sa_ablation_attention import UNet_FullResAttention
+    from utils.metrics import calculate_metrics_device
+    torch.manual_seed(11)
+    m32 = UNet_FullResAttention(3, 1, [64, 128, 256, 512], precision="fp32")
+    with torch.no_grad():
+        for n, p in m32.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    m16 = UNet_FullResAttention(3, 1, [64, 128, 256, 512], precision="bf16")
+    m16.load_state_dict(m32.state_dict())
+    m32, m16 = m32.cuda().train(), m16.cuda().train()
+    x = torch.randn(2, 3, 64, 64, device="cuda")
+    t = (torch.rand(2, 1, 64, 64, device="cuda") > 0.5).float()
+    l32 = m32(x)
+    l16 = m16(x)
+    assert rel(l16, l32) < 5e-2
+    opt = FusedSGD(m16.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad()
+    met = calculate_metrics_device(sigmoid(m16(x)), t, "bce_dice", {})
+    met["loss"].backward()
+    opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+    torch.cuda.synchronize()
+    assert np.isfinite(met["loss"].item()) and np.isfinite(opt.last_norm.item())
+
+
+# ----------------------------------------------------------------------------- plain U-Net (config 1)
+@pytest.mark.parametrize("name,seed,precision,tol", [("unet_small.npz", 6000, "fp32", 1e-4),
+                                                     ("unet_cfg1.npz", 6001, "fp32", 1e-4),
+                                                     ("unet_cfg1.npz", 6001, "bf16", 2e-2)])
+def test_unet_matches_reference(name, seed, precision, tol):
+    """Seeded reference initialisation + one forward/backward: logits, loss, Dice/IoU, gradient
+    norms of every tensor and the full gradients of the small ones (fixture), BN running stats."""
+    from dfcsa.loss import sigmoid
+    from models.unet import UNet
+    from utils.metrics import calculate_metrics
+    fx = dict(np.load(os.path.join(GOLDEN, name)))
+    torch.manual_seed(seed)
+    m = UNet(3, 1, precision=precision).cuda().train()
+    logits = m(T(fx["x"]))
+    met = calculate_metrics(sigmoid(logits), T(fx["t"]), "bce_dice", {})
+    met["loss"].backward()
+    assert rel(logits, fx["logits"]) < tol
+    assert abs(met["loss"].item() - float(fx["loss"])) < tol * abs(float(fx["loss"]))
+    if precision == "fp32":
+        assert abs(met["dice"] - float(fx["dice"])) < 1e-6
+        for n, p in m.named_parameters():
+            g = p.grad.double().norm().item()
+            ref = float(fx["gnorm." + n])
+            if n.endswith(("conv.0.bias", "conv.3.bias")):
+                continue
+            assert abs(g - ref) <= 2e-3 * ref + 1e-7, (n, g, ref)
+        check_grads(m.named_parameters(), fx, tol=2e-3)
+        for k, v in m.state_dict().items():
+            if "running" in k:
+                assert rel(v.float(), fx["buf." + k]) < 1e-5, k
+
+
+def test_unet_ceil_pool_and_crop_kernels():
+    """MaxPool2d(2, ceil_mode=True) and the crop copy against PyTorch on odd sizes, with the
+    backward (first-maximum scatter, zero padding)."""
+    from dfcsa.unet_ops import Crop, MaxPool2x2Ceil
+    torch.manual_seed(5)
+    for dtype in (torch.float32, torch.bfloat16):
+        x = torch.randn(2, 7, 9, 16, device="cuda").to(dtype)
+        x[0, 0, 0, :8] = x[0, 0, 1, :8]   # ties
+        xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
+        yr = F.max_pool2d(xr, 2, ceil_mode=True)
+        xk = x.clone().requires_grad_(True)
+        y = MaxPool2x2Ceil.apply(xk, dtype)
+        assert torch.equal(y.float().permute(0, 3, 1, 2), yr)
+        g = torch.randn_like(yr)
+        yr.backward(g)
+        y.backward(g.permute(0, 2, 3, 1).to(dtype))
+        assert torch.allclose(xk.grad.float().permute(0, 3, 1, 2), xr.grad, atol=1e-2 if dtype == torch.bfloat16 else 0)
+        c = Crop.apply(xk.detach(), 1, 2, 5, 6, dtype)
+        assert torch.equal(c, x[:, 1:6, 2:8, :])
+
+
+def test_factory_unet_config1_trains():
+    """config_unet.yaml overlaid by BASELINE configs[0] (64x64, batch 2) through the factory and the
+    Trainer's device step: loss decreases over a few SGD steps on a fixed batch."""
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.model_factory import ModelFactory
+    from utils.metrics import calculate_metrics_device
+    torch.manual_seed(0)
+    m = ModelFactory.get_model({"model": {"name": "UNet", "features": [16, 32, 64, 128]}, "training": {}})
+    m = m.cuda().train()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    x = torch.randn(2, 3, 64, 64, device="cuda")
+    t = (x[:, :1] > 0).float()
+    losses = []
+    for _ in range(8):
+        opt.zero_grad()
+        met = calculate_metrics_device(sigmoid(m(x)), t, "bce_dice", {})
+        met["loss"].backward()
+        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        losses.append(met["loss"].item())
+    assert losses[-1] < losses[0], losses

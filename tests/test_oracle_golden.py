@@ -132,3 +132,74 @@ def test_ddp_shard_means():
             acc = g if acc is None else {k: acc[k] + g[k] for k in acc}
         for k in acc:
             close(acc[k] / world, fx[f"w{world}.mean_grad.{k}"], rtol=1e-3, atol=1e-5)
+
+
+# ----------------------------------------------------------------------------- config 5 / config 1
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "fra_*.npz"))), ids=os.path.basename)
+def test_full_resolution_attention(path):
+    fx = dict(np.load(path))
+    sd = {k[3:]: T(v).requires_grad_(True) for k, v in fx.items() if k.startswith("sd.")}
+    x = T(fx["x"]).requires_grad_(True)
+    y = O.full_resolution_attention(x, {"m." + k: v for k, v in sd.items()}, "m")
+    close(y, fx["y"], rtol=1e-4, atol=1e-5)
+    y.backward(T(fx["g"]))
+    close(x.grad, fx["dx"], rtol=1e-4, atol=1e-4)
+    for k in sd:
+        close(sd[k].grad, fx["grad." + k], rtol=1e-3, atol=1e-4)
+
+
+@pytest.mark.parametrize("path", sorted(glob.glob(os.path.join(GOLDEN, "frablock_*.npz"))), ids=os.path.basename)
+def test_full_res_block(path):
+    fx = dict(np.load(path))
+    sd0 = {"b." + k: v for k, v in sd_from(fx, "sd0.").items()}
+    params = {k: (v.clone().requires_grad_(True) if v.is_floating_point() and "running" not in k else v)
+              for k, v in sd0.items()}
+    x = T(fx["x"]).requires_grad_(True)
+    bufs = {}
+    y = O.dfc_block(x, params, "b", 0, True, bufs, full_res=True)
+    close(y, fx["y"], rtol=1e-4, atol=1e-5)
+    y.backward(T(fx["g"]))
+    close(x.grad, fx["dx"], rtol=1e-4, atol=1e-4)
+    for k, v in fx.items():
+        if k.startswith("grad."):
+            close(params["b." + k[5:]].grad, v, rtol=1e-3, atol=1e-4)
+        if k.startswith("sd1.") and ("running" in k or "num_batches" in k):
+            close(bufs["b." + k[4:]], v, rtol=1e-5, atol=1e-6)
+
+
+def test_full_res_model():
+    fx = dict(np.load(os.path.join(GOLDEN, "fullres_model.npz")))
+    sd = sd_from(fx, "sd0.")
+    logits, met, grads, _ = O.forward_backward(sd, T(fx["x"]), T(fx["t"]), 0, {"bce_weight": 0.5}, model="fullres")
+    close(logits, fx["logits"], rtol=1e-4, atol=1e-5)
+    close(met["loss"], fx["loss"], rtol=1e-5)
+    assert abs(met["dice"] - fx["dice"]) < 1e-9
+    for k in O.param_names(sd):
+        close(grads[k], fx["grad." + k], rtol=1e-3, atol=1e-5)
+
+
+@pytest.mark.parametrize("name,seed", [("unet_small.npz", 6000), ("unet_cfg1.npz", 6001)])
+def test_unet_oracle_and_seeded_init(name, seed):
+    """The build's UNet module tree reproduces the reference's seeded initialisation (per-tensor
+    sums) and the oracle reproduces the reference's logits, loss, metrics and gradients."""
+    from models.unet import UNet
+    fx = dict(np.load(os.path.join(GOLDEN, name)))
+    torch.manual_seed(seed)
+    m = UNet(3, 1)
+    sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    assert sum(p.numel() for p in m.parameters()) == int(fx["nparams"]) == 31043521
+    for k, v in sd.items():
+        if v.is_floating_point():
+            assert abs(v.double().sum().item() - float(fx["init_sum." + k])) <= 1e-9 * max(1.0, abs(float(fx["init_sum." + k]))), k
+    logits, met, grads, bufs = O.forward_backward(sd, T(fx["x"]), T(fx["t"]), 0, {}, model="unet")
+    close(logits, fx["logits"], rtol=1e-4, atol=1e-5)
+    close(met["loss"], fx["loss"], rtol=1e-5)
+    assert abs(met["dice"] - fx["dice"]) < 1e-9 and abs(met["iou"] - fx["iou"]) < 1e-9
+    for k, g in grads.items():
+        ref = float(fx["gnorm." + k])
+        assert abs(g.double().norm().item() - ref) <= 1e-3 * ref + 1e-7, k
+        if "grad." + k in fx:
+            close(g, fx["grad." + k], rtol=1e-3, atol=1e-5 * max(1.0, ref))
+    for k, v in bufs.items():
+        if "running" in k:
+            close(v, fx["buf." + k], rtol=1e-5, atol=1e-6)
