@@ -386,7 +386,7 @@ __global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, 
     int rows = NI / ndst;
     int d = i / rows, r = i - d * rows;
     int tap = j / Ctot, cin = j - tap * Ctot;
-    if (cin >= Creal) return;
+    if (cin >= Creal || tap >= ntaps) return;   // K-padding columns of the GEMM
     float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
     dst[((int64_t)r * Creal + cin) * ntaps + tap] += s;
   } else if (layout == 2) {

@@ -83,6 +83,12 @@ class PackEntry(ctypes.Structure):
                 ("a", ctypes.c_int * 8)]
 
 
+class WstdEntry(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("what", ctypes.c_void_p), ("rstd", ctypes.c_void_p), ("g", ctypes.c_void_p),
+                ("dw", ctypes.c_void_p), ("K", ctypes.c_int), ("rows", ctypes.c_int), ("row0", ctypes.c_int),
+                ("pad", ctypes.c_int)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(

@@ -8,22 +8,23 @@ reference, so unchanged yamls still run): ``model.precision`` / ``training.preci
 ('bf16' default, 'fp32').
 
 Built on the MI355X path: 'DFC-SA-Res-Block' (UNetDFCSARes, the north-star model), 'UNet'
-(config 1, model_factory.py:94-100) and 'UNet_FullResAttention' (config 5, :174-175).  The other
-names the reference knows (TransUNet, the other ablation models, the ViT) raise
-NotImplementedError naming what is missing.
+(config 1, model_factory.py:94-100), 'UNet_FullResAttention' (config 5, :174-175) and
+'TransformerUNet'/'TransUNet' (config 4, :113-137).  The other names the reference knows (the other
+ablation models, the ViT) raise NotImplementedError naming what is missing.
 
 Pretrained weights are loaded with torch.load(weights_only=True) (a state_dict needs nothing
 else); as in the reference a failure is reported and not raised.
 """
 import torch
 
+from models.transformer_unet import TransUNet, get_r50_b16_config
 from models.unet import UNet
 from models.unet_dfc_sa_ablation_attention import UNet_FullResAttention
 from models.unet_dfc_sa_res import UNetDFCSARes
 
-_BUILT = ("DFC-SA-Res-Block", "UNet", "UNet_FullResAttention")
+_BUILT = ("DFC-SA-Res-Block", "UNet", "UNet_FullResAttention", "TransformerUNet", "TransUNet")
 _REFERENCE_ONLY = {
-    "TransformerUNet", "TransUNet", "VisionTransformerSegmentation", "UNet_Baseline",
+    "VisionTransformerSegmentation", "UNet_Baseline",
     "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
     "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv",
 }
@@ -70,6 +71,16 @@ class ModelFactory:
                                 pool_size=pool_size, ablation_on_qk_channels=qk, precision=precision)
         if name == "UNet_FullResAttention":
             return UNet_FullResAttention(in_channels, out_channels, features, precision=precision)
+        if name in ("TransformerUNet", "TransUNet"):   # reference :113-137
+            print("正在創建官方版 TransUNet (R50-ViT-B_16)...")
+            vit_config = get_r50_b16_config()
+            img_size_config = config.get("dataset", {}).get("img_size", [224, 224])
+            img_size = img_size_config[0] if isinstance(img_size_config, list) else img_size_config
+            vit_config.n_classes = out_channels
+            if in_channels != 3:
+                print(f"注意：官方版 TransUNet 預設處理3通道輸入。您的 in_channels={in_channels}，模型會將單通道複製為3通道。")
+            vit_config.patches.grid = (img_size // 16, img_size // 16)
+            return TransUNet(config=vit_config, img_size=img_size, num_classes=out_channels, precision=precision)
         if name in _REFERENCE_ONLY:
             raise NotImplementedError(
                 f"model {name!r} exists in the reference but is not built on the MI355X path yet "

@@ -358,6 +358,104 @@ int dfcsa_window_copy(int dtype, int B, int C, int Hs, int Ws, const void* src, 
                       int ox, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * TransUNet R50-ViT-B/16 (models/transformer_unet.py, BASELINE config 4).  Convolutions and
+ * Linear layers run on dfcsa_conv_gemm / dfcsa_conv_wgrad; these are the remaining operations.
+ * ---------------------------------------------------------------------------------------- */
+/* StdConv2d weight standardisation (transformer_unet.py:21-27), one launch for a table of convs:
+ * rows [row0, row0 + rows) of the table's global row space belong to entry e (sorted by row0);
+ * fwd: what[r][k] = (w[r][k] - mean_r)/sqrt(var_r + 1e-5) (biased variance over K), rstd[r] saved;
+ * bwd: dw[r][k] += rstd_r*(g - mean(g) - what*mean(g*what)) with g = dL/dwhat. */
+typedef struct {
+  const float* w;
+  float* what;
+  float* rstd;
+  const float* g;
+  float* dw;
+  int K, rows, row0, pad;
+} dfcsa_wstd_entry;
+int dfcsa_wstd_fwd(const dfcsa_wstd_entry* tab, int n, int total_rows, void* stream);
+int dfcsa_wstd_bwd(const dfcsa_wstd_entry* tab, int n, int total_rows, void* stream);
+/* root conv operand (ResNetV2 root, :77): out[m][tap*Cin + ci] = x[b][ci % Csrc][oh*s-p+kh][ow*s-p+kw]
+ * for an NCHW fp32 image (Csrc = 1 repeats the channel, :363-364), zero outside / past k*k*Cin;
+ * out [B*Ho*Wo][Kpad] dtype */
+int dfcsa_im2col_input(int dtype, int B, int Csrc, int Cin, int H, int W, int k, int s, int p, const float* x,
+                       int Kpad, void* out, void* stream);
+/* GroupNorm (nn.GroupNorm, :46-67, :78): per image b and group g of C/G channels over HW pixels.
+ * stats: partial [B][S][2][C] (S = dfcsa_gn_nslices pixel slices); finalize: mean_rstd [B][2][G],
+ * scale_shift [B][2][C] (y*scale + shift = gamma*xhat + beta); apply: out = act(y*scale + shift +
+ * r), r = res*res_scale + res_shift (res_scale_shift given) or res (or none); act 1 = ReLU.
+ * bwd: dz = dout*(mask > 0) (mask NULL: dz = dout); reduce -> partial [B][S][2][C] (sum dz, sum
+ * dz*xhat); finalize -> coef [B][2][G], dgamma/dbeta += ; apply -> dy (and dz_out = dz if given). */
+int dfcsa_gn_nslices(int HW, int C);
+int dfcsa_gn_stats(int dtype, int B, int HW, int C, int S, const void* y, float* partial, void* stream);
+int dfcsa_gn_finalize(int B, int HW, int C, int G, int S, const float* partial, const float* gamma,
+                      const float* beta, float eps, float* mean_rstd, float* scale_shift, void* stream);
+int dfcsa_gn_apply(int dtype, int B, int HW, int C, const void* y, const float* scale_shift, const void* res,
+                   const float* res_scale_shift, int act, void* out, void* stream);
+int dfcsa_gn_bwd_reduce(int dtype, int B, int HW, int C, int G, int S, const void* dout, const void* mask,
+                        const void* y, const float* mean_rstd, float* partial, void* stream);
+int dfcsa_gn_bwd_finalize(int B, int HW, int C, int G, int S, const float* partial, const float* gamma,
+                          float* coef, float* dgamma, float* dbeta, void* stream);
+int dfcsa_gn_bwd_apply(int dtype, int B, int HW, int C, int G, const void* dout, const void* mask, const void* y,
+                       const float* mean_rstd, const float* gamma, const float* coef, void* dy, void* dz_out,
+                       void* stream);
+/* MaxPool2d(kernel 3, stride 2, padding 1) (:101): out [B][Ho][Wo][C], Ho = (H-1)/2 + 1; idx
+ * uint8 [B][Ho][Wo][C] = tap (kh*3 + kw) of the first maximum; bwd writes every dx element. */
+int dfcsa_maxpool3s2_fwd(int dtype, int B, int H, int W, int C, const void* x, void* out, void* idx, void* stream);
+int dfcsa_maxpool3s2_bwd(int dtype, int B, int H, int W, int C, const void* idx, const void* dout, void* dx,
+                         void* stream);
+/* data gradient of a k x k / stride s / pad p conv from the column gradient dcols [B*Ho*Wo][k*k*C]
+ * (= dY @ W, one GEMM): dx [B][H][W][C] (+)= the sum over taps landing on each input pixel */
+int dfcsa_col2im(int dtype, int B, int H, int W, int C, int Ho, int Wo, int k, int s, int p, const void* dcols,
+                 void* dx, int accumulate, void* stream);
+/* LayerNorm over the last dim (:206-207, :226): x fp32 [rows][C] -> y dtype, mean_rstd [rows][2].
+ * bwd: dx (fp32) = LN backward + dres (dres fp32 or NULL; may alias dx); partial
+ * [dfcsa_ln_bwd_ntiles(rows)][2][C] = (sum dy*xhat, sum dy) for dgamma / dbeta. */
+int dfcsa_ln_fwd(int dtype, int rows, int C, const float* x, const float* gamma, const float* beta, float eps,
+                 void* y, float* mean_rstd, void* stream);
+int dfcsa_ln_bwd_ntiles(int rows);
+int dfcsa_ln_bwd(int dtype, int rows, int C, const void* dy, const float* x, const float* mean_rstd,
+                 const float* gamma, const float* dres, float* dx, float* partial, void* stream);
+/* Dropout (p) with a counter-based mask keyed by the device state rng[2] (seed, step), the call
+ * site and the element index (the backward regenerates it; rng_advance moves to a new mask):
+ * drop_add_fwd: out (fp32) = drop(a + pos[i % L]) + res  (pos, res fp32, optional) -- patch
+ * embeddings + position embeddings (:195-199) and the two residual adds of Block (:215, :219);
+ * drop_bwd: da = dout*keep/(1-p);  gelu_drop: out = drop(gelu(x)) (erf GELU, :114, :169-170). */
+int dfcsa_drop_add_fwd(int dtype, int64_t n, const void* a, const float* pos, int64_t L, const float* res, float p,
+                       const int64_t* rng, int site, float* out, void* stream);
+int dfcsa_drop_bwd(int dtype, int64_t n, const float* dout, float p, const int64_t* rng, int site, void* da,
+                   void* stream);
+int dfcsa_gelu_drop_fwd(int dtype, int64_t n, const void* x, float p, const int64_t* rng, int site, void* out,
+                        void* stream);
+int dfcsa_gelu_drop_bwd(int dtype, int64_t n, const void* x, const void* dout, float p, const int64_t* rng, int site,
+                        void* dx, void* stream);
+/* out[j] += sum_b x[b*L + j] (position-embedding gradient) */
+int dfcsa_batch_sum(int dtype, int B, int64_t L, const void* x, float* out, void* stream);
+int dfcsa_rng_advance(int64_t* state, void* stream);
+/* Multi-head self-attention core (Attention.forward :137-157): qkv [B*N][ldq] = [q | k | v] of
+ * heads*dh columns each; ctx [B*N][heads*dh] = softmax(q k^T * scale) v per head; lse [B][heads][N].
+ * bwd: dqkv [B*N][ldq] (q, k, v columns written), dvec [B][heads][N] scratch. dh in {16, 32, 64}. */
+int dfcsa_mha_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv, void* ctx,
+                  float* lse, void* stream);
+int dfcsa_mha_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,
+                  const void* ctx, const void* dctx, const float* lse, float* dvec, void* dqkv, void* stream);
+/* nn.UpsamplingBilinear2d(scale_factor=2) (align_corners=True, :262): [B][Hi][Wi][C] -> [B][2Hi][2Wi][C];
+ * bwd is a deterministic gather into dx [B][Hi][Wi][C] */
+int dfcsa_upsample2_ac(int dtype, int B, int C, int Hi, int Wi, const void* x, void* out, void* stream);
+int dfcsa_upsample2_ac_bwd(int dtype, int B, int C, int Hi, int Wi, const void* dout, void* dx, void* stream);
+/* dst[m][j] (+)= src[m][j], j < ncols (row strides ld_src / ld_dst): channel concat / split */
+int dfcsa_copy_cols(int dtype, int64_t M, int ncols, const void* src, int ld_src, void* dst, int ld_dst,
+                    int accumulate, void* stream);
+/* SegmentationHead 3x3 conv + bias (:272-276): logits NCHW fp32 [B][Cout][H][W] from x NHWC
+ * [B][H][W][C] (C <= 64, Cout <= 4), w fp32 [Cout][C][3][3]; bwd: dx, partial_w
+ * [ntiles][Cout*C*9], partial_b [ntiles][Cout], ntiles = dfcsa_head3_ntiles */
+int dfcsa_head3_fwd(int dtype, int B, int H, int W, int C, int Cout, const void* x, const float* w,
+                    const float* bias, float* logits, void* stream);
+int dfcsa_head3_ntiles(int B, int H, int W);
+int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, const void* x, const float* w,
+                    const float* dlogits, void* dx, float* partial_w, float* partial_b, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Profiling hook: when enabled for a kernel class, every launch of that class is bracketed by
  * hipEvents on its own stream; dfcsa_prof_read returns the summed elapsed milliseconds and
  * the launch count since the last reset (synchronises on the recorded events).

@@ -24,6 +24,8 @@ Reference functions restated (file:line under the reference checkout):
   * FullResAttnDFCBlock / UNet_FullResAttention (AblationUNetBase.forward,
     models/unet_dfc_sa_ablation_branches.py:129-164)          -> dfc_block / unet_dfc_sa_res(full_res=True)
   * UNet.forward (DoubleConv, Down, Up, OutConv)  models/unet.py:6-101        -> unet
+  * TransUNet.forward (StdConv2d, PreActBottleneck, ResNetV2, Attention, Mlp, Block, Embeddings,
+    Encoder, DecoderCup, SegmentationHead)    models/transformer_unet.py:21-368 -> transunet
 """
 import math
 
@@ -159,6 +161,94 @@ def unet(x, sd, training=True, bufs=None):
 
 
 # ------------------------------------------------------------------------------------------
+# TransUNet R50-ViT (models/transformer_unet.py, BASELINE config 4), dropout p = 0 (eval-mode
+# dropout; the fixtures are generated with dropout_rate 0)
+# ------------------------------------------------------------------------------------------
+def std_conv(x, w, stride=1, padding=0):
+    """StdConv2d.forward :21-27: per-output-channel standardised weight (biased var, eps 1e-5)."""
+    v, m = torch.var_mean(w, dim=[1, 2, 3], keepdim=True, unbiased=False)
+    return F.conv2d(x, (w - m) / torch.sqrt(v + 1e-5), None, stride, padding)
+
+
+def _gn(x, sd, name, groups, eps):
+    return F.group_norm(x, groups, sd[name + ".weight"], sd[name + ".bias"], eps)
+
+
+def bottleneck_unit(x, sd, n, stride):
+    """PreActBottleneck.forward :58-68 (GroupNorm(32, .) eps 1e-6; gn_proj GroupNorm(C, C) eps 1e-5)."""
+    cout = sd[n + ".conv3.weight"].shape[0]
+    if (n + ".downsample.weight") in sd:
+        res = _gn(std_conv(x, sd[n + ".downsample.weight"], stride), sd, n + ".gn_proj", cout, 1e-5)
+    else:
+        res = x
+    y = F.relu(_gn(std_conv(x, sd[n + ".conv1.weight"]), sd, n + ".gn1", 32, 1e-6))
+    y = F.relu(_gn(std_conv(y, sd[n + ".conv2.weight"], stride, 1), sd, n + ".gn2", 32, 1e-6))
+    y = _gn(std_conv(y, sd[n + ".conv3.weight"]), sd, n + ".gn3", 32, 1e-6)
+    return F.relu(res + y)
+
+
+def vit_block(h, sd, n, heads):
+    """Block.forward :211-220 with Attention :137-157 (scores / sqrt(head size)) and Mlp :167-173."""
+    B, N, D = h.shape
+    dh = D // heads
+    x = F.layer_norm(h, (D,), sd[n + ".attention_norm.weight"], sd[n + ".attention_norm.bias"], 1e-6)
+
+    def proj(t, name):
+        return F.linear(t, sd[f"{n}.attn.{name}.weight"], sd[f"{n}.attn.{name}.bias"])
+
+    q, k, v = (proj(x, nm).view(B, N, heads, dh).permute(0, 2, 1, 3) for nm in ("query", "key", "value"))
+    a = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(dh), dim=-1)
+    c = (a @ v).permute(0, 2, 1, 3).reshape(B, N, D)
+    h = proj(c, "out") + h
+    x = F.layer_norm(h, (D,), sd[n + ".ffn_norm.weight"], sd[n + ".ffn_norm.bias"], 1e-6)
+    x = F.linear(F.gelu(F.linear(x, sd[n + ".ffn.fc1.weight"], sd[n + ".ffn.fc1.bias"])),
+                 sd[n + ".ffn.fc2.weight"], sd[n + ".ffn.fc2.bias"])
+    return x + h
+
+
+def transunet(x, sd, heads, n_skip=3, training=True, bufs=None):
+    """TransUNet.forward :362-368: ResNetV2 hybrid (:97-106) -> Embeddings (:193-200) -> Encoder
+    (:231-237) -> DecoderCup (:300-312, UpsamplingBilinear2d = bilinear align_corners=True) ->
+    SegmentationHead 3x3 (:272-276)."""
+    if x.shape[1] == 1:
+        x = x.repeat(1, 3, 1, 1)
+    hp = "transformer.embeddings.hybrid_model"
+    r = F.relu(_gn(std_conv(x, sd[hp + ".root.conv.weight"], 2, 3), sd, hp + ".root.gn", 32, 1e-6))
+    feats = [r]
+    h = F.max_pool2d(r, 3, 2, 1)
+    nblocks = 1 + max(int(k.split(".body.block")[1].split(".")[0]) for k in sd if ".body.block" in k) - 1
+    for b in range(1, nblocks + 1):
+        nunits = max(int(k.split(f".body.block{b}.unit")[1].split(".")[0]) for k in sd if f".body.block{b}.unit" in k)
+        for u in range(1, nunits + 1):
+            h = bottleneck_unit(h, sd, f"{hp}.body.block{b}.unit{u}", 2 if (u == 1 and b > 1) else 1)
+        if b < nblocks:
+            feats.append(h)
+    feats = feats[::-1]
+    e = F.conv2d(h, sd["transformer.embeddings.patch_embeddings.weight"],
+                 sd["transformer.embeddings.patch_embeddings.bias"])
+    B, D, gh, gw = e.shape
+    t = e.flatten(2).transpose(-1, -2) + sd["transformer.embeddings.position_embeddings"]
+    nl = 1 + max(int(k.split("encoder.layer.")[1].split(".")[0]) for k in sd if "encoder.layer." in k)
+    for i in range(nl):
+        t = vit_block(t, sd, f"transformer.encoder.layer.{i}", heads)
+    t = F.layer_norm(t, (D,), sd["transformer.encoder.encoder_norm.weight"], sd["transformer.encoder.encoder_norm.bias"],
+                     1e-6)
+    u = t.permute(0, 2, 1).reshape(B, D, gh, gw)
+
+    def conv_bn_relu(z, n):
+        return F.relu(batch_norm(F.conv2d(z, sd[n + ".0.weight"], None, padding=1), sd, n + ".1", training, bufs))
+
+    u = conv_bn_relu(u, "decoder.conv_more")
+    nb = 1 + max(int(k.split("decoder.blocks.")[1].split(".")[0]) for k in sd if "decoder.blocks." in k)
+    for i in range(nb):
+        u = F.interpolate(u, scale_factor=2, mode="bilinear", align_corners=True)
+        if i < n_skip:
+            u = torch.cat([u, feats[i]], dim=1)
+        u = conv_bn_relu(conv_bn_relu(u, f"decoder.blocks.{i}.conv1"), f"decoder.blocks.{i}.conv2")
+    return F.conv2d(u, sd["segmentation_head.0.weight"], sd["segmentation_head.0.bias"], padding=1)
+
+
+# ------------------------------------------------------------------------------------------
 # loss and metrics
 # ------------------------------------------------------------------------------------------
 def bce_dice_loss(p, t, w_bce=1.0, w_dice=1.0, smooth=1.0):
@@ -197,14 +287,17 @@ def param_names(sd):
                                   or k.endswith("num_batches_tracked"))]
 
 
-def forward_backward(sd, x, t, pool_size, loss_params=None, model="dfc"):
+def forward_backward(sd, x, t, pool_size, loss_params=None, model="dfc", heads=12):
     """fwd -> sigmoid -> calculate_metrics -> backward.  Returns (logits, metrics, grads,
-    updated BN buffers).  model: 'dfc' (UNetDFCSARes), 'fullres' (UNet_FullResAttention), 'unet'."""
+    updated BN buffers).  model: 'dfc' (UNetDFCSARes), 'fullres' (UNet_FullResAttention), 'unet',
+    'transunet' (TransUNet with `heads` attention heads)."""
     params = {k: (v.detach().clone().requires_grad_(True) if k in set(param_names(sd)) else v)
               for k, v in sd.items()}
     bufs = {}
     if model == "unet":
         logits = unet(x, params, training=True, bufs=bufs)
+    elif model == "transunet":
+        logits = transunet(x, params, heads, training=True, bufs=bufs)
     else:
         logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs, full_res=(model == "fullres"))
     met = calculate_metrics(torch.sigmoid(logits), t, "bce_dice", loss_params)

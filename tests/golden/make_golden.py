@@ -10,6 +10,8 @@ Reference files imported (file-by-file, via importlib, because the reference's p
                                 UNetDFCSA :118-204, UNetDFCSARes :207-220
   * utils/metrics.py            dice_loss :6-24, BCEDiceLoss :52-78, calculate_metrics :211-264
   * models/unet.py              UNet :69-101 (config 1)
+  * models/transformer_unet.py  TransUNet :347-368 with get_r50_b16_config :318-342 (config 4;
+                                ml_collections replaced by a dict-with-attributes ConfigDict)
   * models/unet_dfc_sa_ablation_attention.py   FullResolutionAttention :7-26, FullResAttnDFCBlock
                                 :29-92, UNet_FullResAttention :95-97 (config 5; imported under a stub
                                 package because it uses a package-relative import of
@@ -387,9 +389,77 @@ def gen_fullres():
          **fp64_noise(model, m64), **grad_arrays(m64, "grad64."))
 
 
+# ----------------------------------------------------------------------------------------
+# (8) Config 4: TransUNet (R50-ViT hybrid) on a reduced configuration of the reference's own
+#     get_r50_b16_config (same code paths: StdConv2d + GroupNorm bottlenecks with stride-2 and
+#     projection units, ViT blocks, DecoderCup with concat skips of unequal widths, 3x3 head).
+#     ml_collections is not installed: a dict-with-attributes stand-in provides ConfigDict.
+#     Dropout p = 0 (the masks are random; the GPU tests check the dropout kernels separately).
+# ----------------------------------------------------------------------------------------
+TRANSUNET_SMALL = dict(img=32, num_layers=(2, 2, 1), width_factor=0.5, hidden=32, mlp=64, heads=2, layers=2,
+                       decoder=(16, 16, 8, 8), skip=[256, 128, 32, 8])
+
+
+def _transunet_module():
+    import types
+
+    class ConfigDict(dict):
+        def __getattr__(self, k):
+            try:
+                return self[k]
+            except KeyError as e:
+                raise AttributeError(k) from e
+
+        def __setattr__(self, k, v):
+            self[k] = v
+
+    if "ml_collections" not in sys.modules:
+        mlc = types.ModuleType("ml_collections")
+        mlc.ConfigDict = ConfigDict
+        sys.modules["ml_collections"] = mlc
+    return _load("ref_transformer_unet", "models/transformer_unet.py")
+
+
+def gen_transunet():
+    tu = _transunet_module()
+    c = TRANSUNET_SMALL
+    cfg = tu.get_r50_b16_config()
+    cfg.patches.grid = (c["img"] // 16, c["img"] // 16)
+    cfg.resnet.num_layers = c["num_layers"]
+    cfg.resnet.width_factor = c["width_factor"]
+    cfg.hidden_size = c["hidden"]
+    cfg.transformer.mlp_dim = c["mlp"]
+    cfg.transformer.num_heads = c["heads"]
+    cfg.transformer.num_layers = c["layers"]
+    cfg.transformer.dropout_rate = 0.0
+    cfg.transformer.attention_dropout_rate = 0.0
+    cfg.decoder_channels = c["decoder"]
+    cfg.skip_channels = list(c["skip"])
+    cfg.n_classes = 1
+    torch.manual_seed(7500)
+    model = tu.TransUNet(cfg, img_size=c["img"], num_classes=1)
+    with torch.no_grad():   # zero-initialised in the reference; random here so it is exercised
+        model.transformer.embeddings.position_embeddings.normal_(0.0, 0.05)
+    sd0 = sd_arrays(model, "sd0.")
+    model.train()
+    m64 = fp64_twin(model)
+    gen = torch.Generator().manual_seed(7501)
+    x, t = batch(gen, (2, 3, c["img"], c["img"]))
+    out = model(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
+    met["loss"].backward()
+    met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", LOSS_PARAMS)
+    met64["loss"].backward()
+    bufs = {"buf." + k: v.detach().numpy().copy() for k, v in model.state_dict().items() if "running" in k}
+    save("transunet_small.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+         iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), **sd0, **bufs, **fp64_noise(model, m64),
+         **grad_arrays(m64, "grad64."), nparams_full=np.int64(sum(
+             p.numel() for p in tu.TransUNet(tu.get_r50_b16_config(), img_size=224, num_classes=1).parameters())))
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres"]
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet"]
     for w in which:
         globals()["gen_" + w]()
     print("torch", torch.__version__)

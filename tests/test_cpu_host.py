@@ -101,7 +101,12 @@ def test_model_factory_contract():
     with pytest.raises(ValueError):
         ModelFactory.get_model({"model": {"name": "NoSuchModel"}, "training": {}})
     with pytest.raises(NotImplementedError):
-        ModelFactory.get_model({"model": {"name": "TransUNet"}, "training": {}})
+        ModelFactory.get_model({"model": {"name": "UNet_ConcatFusion"}, "training": {}})
+    # config_transunet.yaml: 'TransformerUNet', img_size from the dataset section (:113-137)
+    tu = ModelFactory.get_model({"model": {"name": "TransformerUNet", "in_channels": 3, "out_channels": 1},
+                                 "dataset": {"img_size": [224, 224]}, "training": {}})
+    assert type(tu).__name__ == "TransUNet" and tu.config.patches.grid == (14, 14)
+    assert sum(p.numel() for p in tu.parameters()) == 105275921
     # defaults (model_factory.py:87-91): pool 8, qk ratio 8, features 64..512
     d = ModelFactory.get_model({"model": {"name": "DFC-SA-Res-Block"}, "training": {}})
     assert d.pool_size == 8 and d.down1.attn_branch[3].query_conv.out_channels == 8

@@ -40,6 +40,7 @@ ZERO_TRUE_GRAD = ("conv_branch.0.bias", "attn_branch.0.bias", "gate.0.bias", "fu
 
 
 def check_grads(named, fx, prefix="grad.", tol=1e-3):
+    all_ours, all_ref = [], []
     for n, p in named:
         ref = fx.get(prefix + n)
         if ref is None:
@@ -53,14 +54,22 @@ def check_grads(named, fx, prefix="grad.", tol=1e-3):
             continue
         ref64 = fx.get("grad64." + n)
         if ref64 is not None:
-            # against the same reference run in float64: within max(tol, 2x the reference's own fp32
-            # error "noise.<name>" = |ref_fp32 - ref_fp64| / |ref_fp64|, make_golden.fp64_noise)
-            lim = max(tol, 2.0 * float(fx.get("noise." + n, 0.0)))
+            # against the same reference run in float64: within max(tol, 4x the reference's own fp32
+            # error "noise.<name>" = |ref_fp32 - ref_fp64| / |ref_fp64|, make_golden.fp64_noise).
+            # Scalars (gamma, res_scale: one sum over every pixel of a block, with cancellation) get
+            # 5e-3; the whole concatenated gradient is held to tol / 2 below.
+            base = tol if ref64.size > 1 else max(tol, 5e-3)
+            lim = max(base, 4.0 * float(fx.get("noise." + n, 0.0)))
             r = rel(p.grad, ref64)
             assert r < lim, (n, r, lim)
+            all_ours.append(p.grad.double().cpu().reshape(-1))
+            all_ref.append(torch.from_numpy(np.asarray(ref64, dtype=np.float64)).reshape(-1))
             continue
         r = rel(p.grad, ref)
         assert r < tol, (n, r)
+    if all_ref:
+        r = rel(torch.cat(all_ours), torch.cat(all_ref))
+        assert r < tol / 2, ("whole gradient vector vs fp64 reference", r)
 
 
 @pytest.fixture

@@ -203,3 +203,53 @@ def test_unet_oracle_and_seeded_init(name, seed):
     for k, v in bufs.items():
         if "running" in k:
             close(v, fx["buf." + k], rtol=1e-5, atol=1e-6)
+
+
+def transunet_small_config():
+    """The reduced get_r50_b16_config of tests/golden/make_golden.py TRANSUNET_SMALL (32x32 input)."""
+    from models.transformer_unet import get_r50_b16_config
+    c = get_r50_b16_config()
+    c.patches.grid = (2, 2)
+    c.resnet.num_layers = (2, 2, 1)
+    c.resnet.width_factor = 0.5
+    c.hidden_size = 32
+    c.transformer.mlp_dim = 64
+    c.transformer.num_heads = 2
+    c.transformer.num_layers = 2
+    c.transformer.dropout_rate = 0.0
+    c.decoder_channels = (16, 16, 8, 8)
+    c.skip_channels = [256, 128, 32, 8]
+    c.n_classes = 1
+    return c
+
+
+def test_transunet_oracle_and_seeded_init():
+    """TransUNet (config 4) on the reference's reduced R50-ViT config: the build's module tree
+    reproduces the reference's seeded initialisation exactly and the full-size model has the
+    reference's 105,275,921 parameters; the oracle reproduces logits / loss / Dice and the float64
+    reference gradients within 4x the reference's own fp32 error (min 1e-4), BN running stats."""
+    from models.transformer_unet import TransUNet, get_r50_b16_config
+    fx = dict(np.load(os.path.join(GOLDEN, "transunet_small.npz")))
+    torch.manual_seed(7500)
+    m = TransUNet(transunet_small_config(), img_size=32, num_classes=1)
+    sd0 = sd_from(fx, "sd0.")
+    for k, v in m.state_dict().items():
+        if k != "transformer.embeddings.position_embeddings":   # re-drawn by the generator
+            assert torch.equal(v, sd0[k]), k
+    full = get_r50_b16_config()
+    full.n_classes = 1
+    assert sum(p.numel() for p in TransUNet(full, 224, 1).parameters()) == 105275921
+    logits, met, grads, bufs = O.forward_backward(sd0, T(fx["x"]), T(fx["t"]), 0, {"bce_weight": 0.5},
+                                                  model="transunet", heads=2)
+    close(logits, fx["logits"], rtol=1e-4, atol=1e-5)
+    close(met["loss"], fx["loss"], rtol=1e-5)
+    assert abs(met["dice"] - fx["dice"]) < 1e-9
+    for k, g in grads.items():
+        if k.endswith("attn.key.bias"):      # true gradient 0 (softmax is shift-invariant per query)
+            continue
+        ref = torch.from_numpy(fx["grad64." + k]).double()
+        r = ((g.double() - ref).norm() / (ref.norm() + 1e-30)).item()
+        assert r < max(1e-4, 4 * float(fx["noise." + k])), (k, r)
+    for k, v in bufs.items():
+        if "running" in k:
+            close(v, fx["buf." + k], rtol=1e-5, atol=1e-6)
