@@ -1195,6 +1195,28 @@ __global__ void __launch_bounds__(256) head3_bwd_kernel(int B, int H, int W, int
   }
 }
 
+
+// ------------------------------------------------------------ wide column sums (bias gradients)
+// partial[t][c] = sum over rows [t*64, min(M, t*64 + 64)) of x[row][c]; any C % 8 == 0 (the Linear
+// layers of the ViT reach C = 3072, beyond the 2048-channel elementwise reductions)
+constexpr int COLSUM_ROWS = 64;
+
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_partial_kernel(int64_t M, int C, const T* __restrict__ x,
+                                                             float* __restrict__ partial) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; ++r) {
+    float v[8];
+    load8<T>(x + r * C + c0, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += v[q];
+  }
+  st8f(partial + (size_t)blockIdx.y * C + c0, acc);
+}
+
 // ------------------------------------------------------------ attention launch helpers
 template <typename T, int DH>
 int mha_launch(int B, int N, int heads, int ldq, float scale, const void* qkv, const void* ctx, const void* dctx,
@@ -1596,6 +1618,21 @@ extern "C" int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, 
   else
     hipLaunchKernelGGL(head3_bwd_kernel<float>, dim3(nt), dim3(256), 0, (hipStream_t)stream, B, H, W, C, Cout,
                        (const float*)x, w, dlogits, (float*)dx, partial_w, partial_b);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_colsum_ntiles(int64_t M) { return (int)((M + COLSUM_ROWS - 1) / COLSUM_ROWS); }
+
+extern "C" int dfcsa_colsum_partial(int dtype, int64_t M, int C, const void* x, float* partial, void* stream) {
+  if (M <= 0 || C <= 0 || C % 8) return DFCSA_EINVAL;
+  dim3 grid((C / 8 + 255) / 256, dfcsa_colsum_ntiles(M));
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(colsum_partial_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)x,
+                       partial);
+  else
+    hipLaunchKernelGGL(colsum_partial_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, M, C, (const float*)x,
+                       partial);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

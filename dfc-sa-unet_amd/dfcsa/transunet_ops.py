@@ -149,14 +149,18 @@ def _linear_packs(ps, w, dtype, name):
     ps.transpose(W, 0, 0, cout, cin, name + "t", (cin, rup(cout, KA)))
 
 
-def channel_sum3_into(dtype, x, n0, n1, d0, d1, d2):
-    """column sums of x [M][C] split into d0 [0, n0), d1 [n0, n0+n1), d2 [n0+n1, C)."""
+def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
+    """column sums of x [M][C] (any width) added to d0 [0, n0), d1 [n0, n0+n1), d2 [n0+n1, C)."""
     M, C = x.numel() // x.shape[-1], x.shape[-1]
-    nt = ops.ntiles_ew(M, C)
+    nt = LIB.dfcsa_colsum_ntiles(M)
     part = _f32((nt * C,), x.device)
-    call("dfcsa_channel_sum", dt(dtype), M, C, P(x), P(part), stream())
+    call("dfcsa_colsum_partial", dt(dtype), M, C, P(x), P(part), stream())
     part, nt = ops.rows_reduce(part, nt, C)
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
+
+
+def bias_grad_into(dtype, dy, bias):
+    channel_sum3_into(dtype, dy, dy.shape[-1], 0, grad_of(bias))
 
 
 def _ln_forward(dtype, h, ln, out_shape):
@@ -396,7 +400,7 @@ class PatchEmbed(torch.autograd.Function):
         call("dfcsa_drop_bwd", dt(dtype), de.numel(), P(dout.contiguous()), float(ctx.p), P(ctx.rng), SITE_EMBED,
              P(de), stream())
         call("dfcsa_batch_sum", dt(dtype), B, h * w * D, P(de), P(grad_of(pos)), stream())
-        ops.channel_sum_into(dtype, de, grad_of(conv.bias))
+        bias_grad_into(dtype, de, conv.bias)
         _wgrad_1x1(dtype, de, x, (B, h, w), (h, w), grad_of(conv.weight))
         dx = None
         if ctx.needs_input_grad[0]:
@@ -478,14 +482,14 @@ class ViTBlock(torch.autograd.Function):
         dm = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
         call("dfcsa_drop_bwd", dt(dtype), dm.numel(), P(dout), float(p), P(rng), site + 2, P(dm), stream())
         _wgrad_1x1(dtype, dm, g, grid, hw, grad_of(mlp.fc2.weight))
-        ops.channel_sum_into(dtype, dm, grad_of(mlp.fc2.bias))
+        bias_grad_into(dtype, dm, mlp.fc2.bias)
         dg = _gemm_1x1(dtype, dm, pk["W2t"], KD, F, torch.empty_like(f))
         del dm
         df = torch.empty_like(f)
         call("dfcsa_gelu_drop_bwd", dt(dtype), f.numel(), P(f), P(dg), float(p), P(rng), site + 1, P(df), stream())
         del dg
         _wgrad_1x1(dtype, df, y2, grid, hw, grad_of(mlp.fc1.weight))
-        ops.channel_sum_into(dtype, df, grad_of(mlp.fc1.bias))
+        bias_grad_into(dtype, df, mlp.fc1.bias)
         dy2 = _gemm_1x1(dtype, df, pk["W1t"], KF, D, torch.empty((B, gh, gw, D), dtype=dtype, device=dev))
         del df
         dh1 = _ln_backward(dtype, dy2, h1, mr2, blk.ffn_norm, dout)
@@ -493,7 +497,7 @@ class ViTBlock(torch.autograd.Function):
         da = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
         call("dfcsa_drop_bwd", dt(dtype), da.numel(), P(dh1), float(p_attn), P(rng), site, P(da), stream())
         _wgrad_1x1(dtype, da, cx, grid, hw, grad_of(att.out.weight))
-        ops.channel_sum_into(dtype, da, grad_of(att.out.bias))
+        bias_grad_into(dtype, da, att.out.bias)
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
         dqkv = torch.empty_like(qkv)

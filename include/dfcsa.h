@@ -446,6 +446,10 @@ int dfcsa_upsample2_ac_bwd(int dtype, int B, int C, int Hi, int Wi, const void* 
 /* dst[m][j] (+)= src[m][j], j < ncols (row strides ld_src / ld_dst): channel concat / split */
 int dfcsa_copy_cols(int dtype, int64_t M, int ncols, const void* src, int ld_src, void* dst, int ld_dst,
                     int accumulate, void* stream);
+/* column sums of x [M][C] per 64-row tile: partial [dfcsa_colsum_ntiles(M)][C] (Linear bias gradients,
+ * any C % 8 == 0) */
+int dfcsa_colsum_ntiles(int64_t M);
+int dfcsa_colsum_partial(int dtype, int64_t M, int C, const void* x, float* partial, void* stream);
 /* SegmentationHead 3x3 conv + bias (:272-276): logits NCHW fp32 [B][Cout][H][W] from x NHWC
  * [B][H][W][C] (C <= 64, Cout <= 4), w fp32 [Cout][C][3][3]; bwd: dx, partial_w
  * [ntiles][Cout*C*9], partial_b [ntiles][Cout], ntiles = dfcsa_head3_ntiles */

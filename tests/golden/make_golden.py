@@ -89,7 +89,25 @@ def fp64_noise(module32, module64, prefix="noise."):
             continue
         a, b = p.grad.double(), g64[n].grad
         out[prefix + n] = np.float64(((a - b).norm() / (b.norm() + 1e-30)).item())
+    a = torch.cat([p.grad.double().reshape(-1) for n, p in module32.named_parameters() if p.grad is not None])
+    b = torch.cat([g64[n].grad.reshape(-1) for n, p in module32.named_parameters() if p.grad is not None])
+    out[prefix + "all"] = np.float64(((a - b).norm() / (b.norm() + 1e-30)).item())
     return out
+
+
+def bf16_autocast_cosine(model, x, t, loss_params, m64):
+    """Gradient cosine between the reference run under CPU bf16 autocast and the float64 reference:
+    what bf16 arithmetic alone does to the gradient (the bar for the build's bf16 mode)."""
+    import copy
+    mb = copy.deepcopy(model)
+    mb.zero_grad()
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        out = mb(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out.float()), t, "bce_dice", loss_params)
+    met["loss"].backward()
+    g = torch.cat([p.grad.double().reshape(-1) for p in mb.parameters()])
+    r = torch.cat([p.grad.reshape(-1) for p in m64.parameters()])
+    return np.float64((g @ r / (g.norm() * r.norm())).item())
 
 
 def fp64_twin(module):
@@ -451,10 +469,20 @@ def gen_transunet():
     met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", LOSS_PARAMS)
     met64["loss"].backward()
     bufs = {"buf." + k: v.detach().numpy().copy() for k, v in model.state_dict().items() if "running" in k}
-    save("transunet_small.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+    m_ac = tu.TransUNet(cfg, img_size=c["img"], num_classes=1)
+    m_ac.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in sd0.items()})
+    m_ac.train()
+    cos_ac = bf16_autocast_cosine(m_ac, x, t, LOSS_PARAMS, m64)
+    save("transunet_small.npz", bf16_autocast_grad_cos=cos_ac, x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
          iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), **sd0, **bufs, **fp64_noise(model, m64),
          **grad_arrays(m64, "grad64."), nparams_full=np.int64(sum(
-             p.numel() for p in tu.TransUNet(tu.get_r50_b16_config(), img_size=224, num_classes=1).parameters())))
+             p.numel() for p in tu.TransUNet(_n_classes_1(tu.get_r50_b16_config()), img_size=224,
+                                             num_classes=1).parameters())))
+
+
+def _n_classes_1(cfg):
+    cfg.n_classes = 1
+    return cfg
 
 
 if __name__ == "__main__":
