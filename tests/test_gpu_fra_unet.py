@@ -54,14 +54,12 @@ def check_grads(named, fx, prefix="grad.", tol=1e-3):
             continue
         ref64 = fx.get("grad64." + n)
         if ref64 is not None:
-            # against the same reference run in float64: within max(tol, 5x the reference's own fp32
-            # error), the error being |ref_fp32 - ref_fp64| / |ref_fp64| of this tensor or of the whole
-            # gradient vector, whichever is larger ("noise.<name>", "noise.all", make_golden.fp64_noise).
-            # Scalars (gamma, res_scale: one sum over every pixel of a block, with cancellation) get
-            # 5e-3; the whole concatenated gradient is held to max(tol/2, 2x noise.all) below.
-            base = tol if ref64.size > 1 else max(tol, 5e-3)
-            noise = max(float(fx.get("noise." + n, 0.0)), float(fx.get("noise.all", 0.0)))
-            lim = max(base, 5.0 * noise)
+            # against the same reference re-run in float64 (grad64.*): every tensor within
+            # max(2.5 tol, 5x the reference's own fp32 error "noise.<name>"), scalars (gamma,
+            # res_scale: one cancelling sum over a whole block) within 1e-2, and the whole
+            # concatenated gradient within max(tol/2, 2x noise.all) below (make_golden.fp64_noise).
+            base = 2.5 * tol if ref64.size > 1 else max(tol, 1e-2)
+            lim = max(base, 5.0 * float(fx.get("noise." + n, 0.0)))
             r = rel(p.grad, ref64)
             assert r < lim, (n, r, lim)
             all_ours.append(p.grad.double().cpu().reshape(-1))

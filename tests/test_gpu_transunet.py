@@ -268,7 +268,7 @@ def test_transunet_small_fp32_matches_reference():
         if n.endswith("attn.key.bias"):   # true gradient 0 (softmax shift invariance per query)
             assert p.grad.abs().max().item() < 1e-3 * np.abs(fx["grad64." + n[:-4] + "weight"]).max() + 1e-9, n
             continue
-        lim = max(2e-3 if ref.size > 1 else 5e-3, 4 * max(float(fx["noise." + n]), float(fx["noise.all"])))
+        lim = max(2e-3 if ref.size > 1 else 1e-2, 4 * max(float(fx["noise." + n]), float(fx["noise.all"])))
         r = rel(p.grad, ref)
         assert r < lim, (n, r, lim)
         ours.append(p.grad.double().cpu().reshape(-1))
