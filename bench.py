@@ -82,6 +82,47 @@ def cpu_baseline(seconds_budget=25.0):
                       f"oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
 
 
+def val_dice_leg(cfg, dev, steps=120, batch=16, img=224, n_train=256, n_val=32):
+    """BASELINE.json metric's "val Dice": train the same model/config from the same seed on the
+    learnable synthetic task (utils.data_loader.SyntheticEllipses, seed 42 train / 43 val) for
+    `steps` Trainer steps, then validation Dice exactly as Trainer.validate_epoch reports it (eval-mode
+    BatchNorm, mean over batches of the batch-micro Dice, reference trainer.py:219,249)."""
+    from dfcsa.loss import metrics_from_stats, sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.model_factory import ModelFactory
+    from utils.data_loader import SyntheticEllipses
+    from utils.metrics import calculate_metrics_device
+
+    def stack(ds, n):
+        items = [ds[i] for i in range(n)]
+        return (torch.stack([it["image"] for it in items]).to(dev), torch.stack([it["mask"] for it in items]).to(dev))
+
+    t0 = time.perf_counter()
+    xtr, ttr = stack(SyntheticEllipses(n_train, (img, img), seed=42), n_train)
+    xva, tva = stack(SyntheticEllipses(n_val, (img, img), seed=43), n_val)
+    torch.manual_seed(0)
+    model = ModelFactory.get_model(cfg).to(dev).train()
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    g = torch.Generator().manual_seed(7)
+    for s in range(steps):
+        idx = torch.randint(0, n_train, (batch,), generator=g).to(dev)
+        opt.zero_grad()
+        met = calculate_metrics_device(sigmoid(model(xtr[idx])), ttr[idx], "bce_dice", {})
+        met["loss"].backward()
+        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+    train_loss = float(met["stats"][0].item())
+    model.eval()
+    dices = []
+    with torch.no_grad():
+        for i in range(0, n_val, batch):
+            st = calculate_metrics_device(sigmoid(model(xva[i:i + batch])), tva[i:i + batch], "bce_dice", {})["stats"]
+            dices.append(metrics_from_stats(st)[1])
+    return {"value": round(sum(dices) / len(dices), 4), "train_steps": steps, "batch": batch,
+            "final_train_loss": round(train_loss, 4), "train_images": n_train, "val_images": n_val,
+            "task": "SyntheticEllipses 1-4 ellipses/image, seed 42 train / 43 val (utils/data_loader.py)",
+            "seconds": round(time.perf_counter() - t0, 1)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -94,6 +135,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
+    ap.add_argument("--no-val-dice", action="store_true", help="skip the synthetic-task validation Dice leg")
+    ap.add_argument("--val-steps", type=int, default=120)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -220,6 +263,11 @@ def main():
                                        "tflops": round(c[3] / (c[1] * 1e-3) / 1e12, 2) if c[1] > 0 else 0}
                                 for c in cls.values() if c is not dom}}
 
+    vdice = None
+    if rank == 0 and world == 1 and not args.no_val_dice:
+        log("[rank 0] validation Dice leg (synthetic ellipses) ...")
+        vdice = val_dice_leg(cfg, dev, steps=args.val_steps, batch=B, img=S)
+
     imgs = args.steps * B * world
     value = imgs / el
     cpu = None
@@ -236,7 +284,7 @@ def main():
                           "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
                           "parallelism": f"dp{world}", "final_loss": round(final_loss, 5),
                           "model_tflops": round(value * FWD_BWD_GFLOP_PER_IMG / 1e3, 2)},
-               "roofline": roof, "cpu_baseline": cpu}
+               "roofline": roof, "cpu_baseline": cpu, "val_dice": vdice}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()
