@@ -82,7 +82,7 @@ def cpu_baseline(seconds_budget=25.0):
                       f"oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
 
 
-def val_dice_leg(cfg, dev, steps=120, batch=16, img=224, n_train=256, n_val=32):
+def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
     """BASELINE.json metric's "val Dice": train the same model/config from the same seed on the
     learnable synthetic task (utils.data_loader.SyntheticEllipses, seed 42 train / 43 val) for
     `steps` Trainer steps, then validation Dice exactly as Trainer.validate_epoch reports it (eval-mode
@@ -136,7 +136,7 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--no-val-dice", action="store_true", help="skip the synthetic-task validation Dice leg")
-    ap.add_argument("--val-steps", type=int, default=120)
+    ap.add_argument("--val-steps", type=int, default=600)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))

@@ -79,20 +79,32 @@ __device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, in
 }
 
 // ------------------------------- forward (no reductions) -------------------------------
+// Each lane keeps ONE 8-channel chunk for the whole grid-stride loop (the stride, a multiple of
+// 256 chunks, is a multiple of C/8 whenever C/8 divides 256 -- host-checked, `fixed`), so the
+// per-channel BatchNorm parameters are loaded once; indices are 32-bit (M*C/8 < 2^31).
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
   const int cpp = a.C >> 3;
-  const int64_t total = (int64_t)a.M * cpp;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int m = (int)(e / cpp);
-    const int c0 = (int)(e - (int64_t)m * cpp) * 8;
-    const size_t off = (size_t)m * a.C + c0;
-    float sc[8], sh[8], y[8], out[8];
-    if (a.a0) {
-      ld8f(a.sc + c0, sc);
-      ld8f(a.sh + c0, sh);
-      load8<T>((const T*)a.a0 + off, y);
+  const int total = a.M * cpp;
+  const int first = blockIdx.x * 256 + threadIdx.x;
+  const int stride = gridDim.x * 256;
+  const bool fixed = (256 % cpp) == 0;
+  float sc[8], sh[8], sc2[8], sh2[8];
+  int c0 = (first % cpp) * 8;
+  if (fixed) {
+    if (a.a0) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
+    if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
+  }
+  for (int e = first; e < total; e += stride) {
+    const int m = e / cpp;
+    if (!fixed) {
+      c0 = (e - m * cpp) * 8;
+      if (a.a0) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
+      if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
     }
+    const size_t off = (size_t)m * a.C + c0;
+    float y[8], out[8];
+    if (a.a0) load8<T>((const T*)a.a0 + off, y);
     if constexpr (MODE == EW_BN_ACT) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
@@ -107,10 +119,8 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
         for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f);
         store8<T>((T*)a.o0 + off, out);
       }
-      float y2[8], sc2[8], sh2[8];
+      float y2[8];
       load8<T>((const T*)a.a1 + off, y2);
-      ld8f(a.sc2 + c0, sc2);
-      ld8f(a.sh2 + c0, sh2);
       const int hw = a.H * a.W;
       const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
       int h0, h1, w0, w1;
@@ -176,9 +186,17 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   const int mbeg = blockIdx.x * a.tile_px;
   const int mend = min(a.M, mbeg + a.tile_px);
   float sc[8], sh[8], mu[8], is[8];
+  float gk[8], k0[8], k1[8];   // BN_BWD_APPLY: gamma*invstd, coef0, coef1 (loop-invariant per lane)
   if (active) {
     if (a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
     if (a.mean) { ld8f(a.mean + c0, mu); ld8f(a.invstd + c0, is); }
+    if constexpr (MODE == EW_BN_BWD_APPLY) {
+      ld8f(a.gamma + c0, gk);
+      ld8f(a.coef + c0, k0);
+      ld8f(a.coef + a.C + c0, k1);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) gk[q] *= is[q];
+    }
   }
   if (active) {
     for (int m = mbeg + lane_px; m < mend; m += pl) {
@@ -273,17 +291,14 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
         }
         store8<T>((T*)a.o0 + off, dz);
       } else if constexpr (MODE == EW_BN_BWD_APPLY) {
-        // a0 = dz, a1 = y; gamma, coef [2][C]; o0 = dy; sum dy (conv bias grad)
-        float dz[8], y[8], gm[8], k0[8], k1[8], dy[8];
+        // a0 = dz, a1 = y; gamma, coef [2][C] (hoisted); o0 = dy; sum dy (conv bias grad)
+        float dz[8], y[8], dy[8];
         load8<T>((const T*)a.a0 + off, dz);
         load8<T>((const T*)a.a1 + off, y);
-        ld8f(a.gamma + c0, gm);
-        ld8f(a.coef + c0, k0);
-        ld8f(a.coef + a.C + c0, k1);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float xh = (y[q] - mu[q]) * is[q];
-          float v = gm[q] * is[q] * (dz[q] - k0[q] - xh * k1[q]);
+          float v = gk[q] * (dz[q] - k0[q] - xh * k1[q]);
           dy[q] = v;
           acc[0][q] += v;
         }
@@ -471,7 +486,7 @@ inline int tile_px(int C) {
 
 template <int MODE>
 int launch_fwd(int dtype, const EwArgs& a, hipStream_t st) {
-  if (a.C % 8 || a.M <= 0) return DFCSA_EINVAL;
+  if (a.C % 8 || a.M <= 0 || (int64_t)a.M * (a.C / 8) >= (1ll << 31)) return DFCSA_EINVAL;
   int64_t chunks = (int64_t)a.M * (a.C / 8);
   int blocks = (int)std::min<int64_t>((chunks + 255) / 256, 256 * 16);
   if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_fwd_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);

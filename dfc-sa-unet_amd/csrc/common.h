@@ -103,6 +103,12 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// Workgroup barrier for LDS hand-offs only.  __syncthreads() is a workgroup fence + barrier and
+// the fence drains vmcnt (outstanding global loads / stores / LDS-DMA) before the barrier, which
+// serialises a DMA ring or a store stream; this waits for the wave's LDS operations only.  Global
+// data (incl. LDS-DMA images) must be waited for explicitly with s_waitcnt vmcnt before it.
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 #define DFCSA_CHECK_LAUNCH() \
   do {                       \
     hipError_t e_ = hipGetLastError(); \

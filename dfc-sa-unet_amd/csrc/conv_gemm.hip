@@ -317,6 +317,7 @@ conv_gemm_kernel(const ConvGemmArgs args) {
 // Two LDS buffers; one vmcnt(0) + barrier per 64-deep K stage.
 // --------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];
+__device__ __attribute__((aligned(16))) float g_store_sink[4 * 64];   // write-only target of masked stores
 
 typedef __attribute__((address_space(3))) void lds_void;
 typedef const __attribute__((address_space(1))) void glb_void;
@@ -436,7 +437,7 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
-    __syncthreads();
+    lds_barrier();   // the DMA ring stays in flight (a __syncthreads fence would drain it)
     if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
     const char* A = smem + (kt % NST) * STAGE;
     const char* B = A + BM * 128;
@@ -482,7 +483,7 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
 // workgroup, and the small LDS footprint lets several workgroups share a CU.  Waves split the
 // columns, so per-column BatchNorm partial sums of a 64-row tile need no cross-wave reduction.
 // --------------------------------------------------------------------------------------------
-template <int NWC, int KP>
+template <int NWC, int KP, bool ACC>
 __global__ void __launch_bounds__(256)
 conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   using T = bf16_t;
@@ -493,8 +494,10 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   constexpr int IMG = 64 * 128;             // bytes of one stage image
   constexpr int SLOT = KS * IMG;
   constexpr int OSTR = NWG * 2 + 16;        // output staging row stride (bytes)
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT + 64 * OSTR];
-  char* otile = smem + 2 * SLOT;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  // separate LDS object: the waitcnt pass then knows the output staging reads cannot alias the
+  // in-flight LDS-DMA images (one shared array makes it drain vmcnt before every staging read)
+  __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = args.M, N = args.N, K = args.K;
@@ -522,37 +525,76 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   }
   const void* zero = (const void*)g_zero_page;
 
-  // A image of tile t into slot s: instruction i covers stage i/2, rows ((i&1)*4 + wave)*8 + rsub
+  // A image of tile t into slot s: instruction i covers stage i/2, rows ((i&1)*4 + wave)*8 + rsub.
+  // The (segment, channel) of each of this lane's K chunks is tile-invariant: resolve the source
+  // pointers once (a per-lane index into the kernel-argument segment table is a vector load that
+  // the compiler follows with a full vmcnt drain -- not inside the streaming loop).
+  const T* a_src[2 * KS];
+#pragma unroll
+  for (int i = 0; i < 2 * KS; ++i) {
+    const int k = (i >> 1) * 64 + cchunk * 8;
+    a_src[i] = nullptr;
+    if (k < K) {
+      const int seg = dm_div(args.dm_cseg, k);
+      a_src[i] = (const T*)args.seg[seg].ptr + (k - seg * args.Cseg);
+    }
+  }
   auto issue = [&](int t, int slot) {
     char* base = smem + slot * SLOT;
 #pragma unroll
     for (int i = 0; i < 2 * KS; ++i) {
       const int st = i >> 1, rb = (i & 1) * 4 + wave;
       const int m = t * 64 + rb * 8 + rsub;
-      const int k = st * 64 + cchunk * 8;
-      const void* src = zero;
-      if (m < M && k < K) {
-        const int seg = dm_div(args.dm_cseg, k);
-        const int ch = k - seg * args.Cseg;
-        src = (const void*)((const T*)args.seg[seg].ptr + ((size_t)m * args.Cseg + ch));
-      }
+      const void* src = (m < M && a_src[i]) ? (const void*)(a_src[i] + (size_t)m * args.Cseg) : zero;
       glds16(src, base + st * IMG + rb * 8 * 128);
     }
   };
 
+  // vmcnt counts stores too and retires in order.  Every lane therefore issues a FIXED number of
+  // global stores per tile (FN stats stores when stats are on, NSTORE output stores; out-of-range
+  // ones go to a sink), so the wait for tile t's A image can leave the previous tile's stores in
+  // flight instead of draining them every iteration (accumulate mode, whose epilogue loads the
+  // destination, keeps the full drain).
+  constexpr int NSTORE = (64 * (NWG / 8)) / 256;
+  static_assert((64 * (NWG / 8)) % 256 == 0, "uniform store count per lane");
+  constexpr int OCH = NWG / 8;
+  // output chunk e = tid + it*256 of a tile: (row, column chunk) and the destination column base
+  // are tile-invariant (resolved once; no per-store kernel-argument loads)
+  T* o_base[NSTORE];
+  int o_row[NSTORE], o_ld[NSTORE];
+#pragma unroll
+  for (int it = 0; it < NSTORE; ++it) {
+    const int e = tid + it * 256;
+    const int row = e / OCH, cc = e - row * OCH, n = n0 + cc * 8;
+    o_row[it] = row;
+    o_base[it] = nullptr;
+    o_ld[it] = args.Nd;
+    if (n < N) {
+      const int d = n / args.Nd;
+      o_base[it] = (T*)args.dest[d] + (n - d * args.Nd);
+    }
+  }
+  constexpr bool lean = !ACC;
+  const bool with_stats = args.stats != nullptr;
   int t = blockIdx.x;
   if (t >= mtiles) return;
   issue(t, 0);
   int slot = 0;
+  bool first_iter = true;
   for (; t < mtiles; t += gridDim.x, slot ^= 1) {
     const int tn = t + gridDim.x;
     if (tn < mtiles) {
       issue(tn, slot ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+      if (ACC || first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+      else if (with_stats) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NSTORE + FN) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NSTORE) : "memory");
     } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (ACC || first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else if (with_stats) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE + FN) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
     }
-    __syncthreads();
+    first_iter = false;
+    lds_barrier();
     const char* img = smem + slot * SLOT;
     f32x4_t acc[4][FN];
 #pragma unroll
@@ -586,10 +628,13 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
           }
         s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-        const int n = n0 + wave * NWC + j * 16 + lane;
-        if (lane < 16 && n < N) {
-          args.stats[(size_t)t * 2 * N + n] = s;
-          args.stats[(size_t)t * 2 * N + N + n] = q;
+        const int n = n0 + wave * NWC + j * 16 + (lane & 15);
+        // one store instruction per fragment column, lanes 0-15: sum, 16-31: sum of squares; it is
+        // never skipped (lanes 0-31 are always active), columns >= N (only when N % NWG != 0) go
+        // to the sink -> a fixed store count per tile
+        if (lane < 32) {
+          float* dst = n < N ? args.stats + (size_t)t * 2 * N + (lane < 16 ? 0 : N) + n : g_store_sink + lane;
+          *dst = lane < 16 ? s : q;
         }
       }
     }
@@ -605,16 +650,21 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
           *(T*)(otile + row * OSTR + col * 2) = f2bf(acc[i][j][r] + bias[j]);
         }
     }
-    __syncthreads();
-    constexpr int OCH = NWG / 8;
-    for (int e = tid; e < 64 * OCH; e += 256) {
-      const int row = e / OCH, cc = e - row * OCH;
-      const int m = m0 + row, n = n0 + cc * 8;
-      if (m >= M || n >= N) continue;
-      const int d = n / args.Nd, col = n - d * args.Nd;
-      T* dst = (T*)args.dest[d] + ((size_t)m * args.Nd + col);
+    lds_barrier();
+#pragma unroll
+    for (int it = 0; it < NSTORE; ++it) {
+      const int e = tid + it * 256;
+      const int row = o_row[it], cc = e - row * OCH;
+      const int m = m0 + row;
       uint4 v = *(const uint4*)(otile + row * OSTR + cc * 16);
-      if (args.accumulate) {
+      const bool ok = m < M && o_base[it];
+      T* dst = ok ? o_base[it] + (size_t)m * o_ld[it] : (T*)(g_store_sink + 4 * (tid & 63));
+      if constexpr (lean) {   // branch-free: exactly one store instruction per iteration
+        *(uint4*)dst = v;
+        continue;
+      }
+      if (!ok) continue;
+      if constexpr (ACC) {
         float a[8], o[8];
         load8<T>((const T*)&v, a);
         load8<T>(dst, o);
@@ -636,7 +686,7 @@ template <int NWC, int KP>
 int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   static int occ = 0;
   if (!occ) {
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<NWC, KP>, 256, 0) != hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, conv1x1_stream_kernel<NWC, KP, false>, 256, 0) != hipSuccess ||
         occ < 1)
       occ = 1;
   }
@@ -646,7 +696,10 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   int gx = (256 * per_cu + ny - 1) / ny;
   if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
   if (gx > mtiles) gx = mtiles;
-  hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
+  if (a.accumulate)
+    hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
+  else
+    hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, false>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -655,10 +708,11 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
 int try_stream(const ConvGemmArgs& a, hipStream_t st) {
   if (g_debug < 0) g_debug = getenv("DFCSA_DEBUG") ? 1 : 0;
   if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return 1;
-  // measured (tools/stream_bench.py, B=16 shapes): the streaming kernel wins for K = 64 with
-  // N >= 128 (2 and 3 destinations, accumulate) and for N >= 384; the tile kernels keep N = 64
-  // and K = 128..256 with N <= 256
-  if (!g_stream_force && !((a.Kpad == 64 && a.N >= 128) || (a.N >= 384 && a.Kpad <= 128))) return 1;
+  // measured (tools/stream_bench.py, B=16 shapes): since the streaming loop keeps its stores in
+  // flight (fixed per-lane store counts, LDS-only barriers, hoisted argument-table reads) it is
+  // at least as fast as the tile kernels on every 1x1 shape it serves (L1 N=64 K=128: 52 vs 77 us,
+  // 3 destinations K=64: 96 vs 181 us), so it takes all of them
+  (void)g_stream_force;
   for (int i = 0; i < a.nseg; ++i)
     if (a.seg[i].dh || a.seg[i].dw) return 1;
   if (a.Ho != a.Hi || a.Wo != a.Wi) return 1;

@@ -9,11 +9,12 @@ from dfcsa._lib import LIB
 bf = torch.bfloat16
 B = 16
 # H, Cseg, nsrc, N, ndest, accumulate
-SHAPES = [(224, 64, 1, 128, 2, True), (224, 64, 1, 192, 3, False), (224, 64, 3, 64, 1, False),
+SHAPES = [(224, 64, 3, 64, 1, False), (224, 64, 2, 64, 1, False), (112, 128, 2, 128, 1, False),
+          (56, 256, 1, 512, 2, False), (56, 256, 2, 256, 1, False), (28, 512, 1, 1024, 2, False), (224, 64, 1, 128, 2, True), (224, 64, 1, 192, 3, False), (224, 64, 3, 64, 1, False),
           (224, 64, 2, 64, 1, False), (224, 64, 2, 128, 2, False), (224, 8, 1, 128, 2, False),
           (112, 128, 1, 256, 2, False), (112, 128, 3, 128, 1, False), (112, 128, 1, 384, 3, False),
           (112, 128, 2, 128, 1, False)]
-variants = [("tile", 7, 0)] + [(f"stream{w}", 0, w) for w in (0, 1, 2, 3, 4, 8, 100000)]
+variants = [("tile", 7, 0)] + [(f"stream{w}", 0, w) for w in (0, 2, 3)] + [("force0", -1, 0), ("force2", -1, 2)]
 for H, Cs, nsrc, N, nd, acc in SHAPES:
     M = B * H * H
     xs = [torch.randn(B, H, H, Cs, device="cuda").to(bf) for _ in range(nsrc)]
@@ -26,7 +27,8 @@ for H, Cs, nsrc, N, nd, acc in SHAPES:
     byts = 2 * M * (nsrc * Cs + N * (2 if acc else 1))
     row = {"M": M, "N": N, "K": nsrc * Cs, "acc": acc}
     for name, knob1, wgs in variants:
-        LIB.dfcsa_set_tuning(1, knob1)
+        LIB.dfcsa_set_tuning(1, max(knob1, 0))
+        LIB.dfcsa_set_tuning(5, 1 if knob1 < 0 else 0)
         LIB.dfcsa_set_tuning(3, wgs)
         run = lambda: ops.conv_gemm(bf, segs, Cs, (B, H, H), (H, H), w, Kp, N, dests, C, accumulate=acc,
                                     stats=None if acc else stats)
@@ -43,4 +45,5 @@ for H, Cs, nsrc, N, nd, acc in SHAPES:
         row[name] = (round(us, 1), round(byts / us / 1e3, 0))
     LIB.dfcsa_set_tuning(1, 0)
     LIB.dfcsa_set_tuning(3, 0)
+    LIB.dfcsa_set_tuning(5, 0)
     print(json.dumps(row), flush=True)
