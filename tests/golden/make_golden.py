@@ -396,7 +396,7 @@ def gen_fullres():
     model.train()
     m64 = fp64_twin(model)
     gen = torch.Generator().manual_seed(7201)
-    x, t = batch(gen, (2, 3, 16, 16))
+    x, t = batch(gen, (2, 3, 32, 32))   # 32x32: the 2x2 bottleneck gives BatchNorm 8 samples per channel
     out = model(x)
     met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
     met["loss"].backward()
