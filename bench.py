@@ -34,6 +34,16 @@ MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 FWD_BWD_GFLOP_PER_IMG = 201.66   # SURVEY.md section 8d (torch.utils.flop_counter, P=4, 224^2)
 
+# --model: the BASELINE configs.  Only 'dfc' is the headline line the driver records;
+# the others put the secondary configs' training step on the same clock.  GFLOP/img fwd+bwd
+# from SURVEY.md section 6 (torch.utils.flop_counter) where the survey measured it at that size.
+MODELS = {
+    "dfc": dict(name="DFC-SA-Res-Block", label="DFC-SA-Res", gflop={224: FWD_BWD_GFLOP_PER_IMG}),
+    "unet": dict(name="UNet", label="UNet (config 1)", gflop={64: 18.05}),
+    "transunet": dict(name="TransformerUNet", label="TransUNet R50-ViT-B/16 (config 4)", gflop={224: 174.94}),
+    "fullres": dict(name="UNet_FullResAttention", label="UNet_FullResAttention (config 5)", gflop={}),
+}
+
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
@@ -136,6 +146,8 @@ def main():
     ap.add_argument("--no-kernel-timing", action="store_true")
     ap.add_argument("--no-graph", action="store_true", help="eager launches instead of one HIP graph per step")
     ap.add_argument("--no-val-dice", action="store_true", help="skip the synthetic-task validation Dice leg")
+    ap.add_argument("--model", default="dfc", choices=sorted(MODELS),
+                    help="dfc = the BASELINE headline (config 2/3); unet / transunet / fullres = configs 1 / 4 / 5")
     ap.add_argument("--val-steps", type=int, default=600)
     args = ap.parse_args()
 
@@ -153,10 +165,13 @@ def main():
     from dfcsa.optim import FusedSGD
     from models.model_factory import ModelFactory
 
-    cfg = {"model": {"name": "DFC-SA-Res-Block", "in_channels": 3, "out_channels": 1,
+    spec = MODELS[args.model]
+    cfg = {"model": {"name": spec["name"], "in_channels": 3, "out_channels": 1,
                      "features": [64, 128, 256, 512], "pool_size": args.pool, "ablation_on_qk_channels": 8,
                      "precision": args.precision},
+           "dataset": {"img_size": [args.img, args.img]},
            "training": {"learning_rate": 0.01, "momentum": 0.9, "weight_decay": 1e-4}}
+    headline = args.model == "dfc"
     torch.manual_seed(0)
     model = ModelFactory.get_model(cfg).to(dev).train()
     opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
@@ -264,26 +279,28 @@ def main():
                                 for c in cls.values() if c is not dom}}
 
     vdice = None
-    if rank == 0 and world == 1 and not args.no_val_dice:
+    if rank == 0 and world == 1 and not args.no_val_dice and headline:
         log("[rank 0] validation Dice leg (synthetic ellipses) ...")
         vdice = val_dice_leg(cfg, dev, steps=args.val_steps, batch=B, img=S)
 
     imgs = args.steps * B * world
     value = imgs / el
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and headline:
         log("[rank 0] timing the CPU oracle baseline ...")
         cpu = cpu_baseline()
     if rank == 0:
-        out = {"metric": "training images/sec (fwd+bwd) 3x224x224 DFC-SA-Res", "value": round(value, 2),
+        gflop = spec["gflop"].get(S)
+        out = {"metric": f"training images/sec (fwd+bwd) 3x{S}x{S} {spec['label']}", "value": round(value, 2),
                "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
                "vs_baseline": None, "dtype": args.precision, "data": "synthetic",
                "launch": "eager" if graph is None else "hip_graph",
-               "config": {"workload": f"DFC-SA-Res P={args.pool} features 64..512 {S}x{S} train step",
+               "config": {"workload": (f"DFC-SA-Res P={args.pool} features 64..512 {S}x{S} train step" if headline
+                                       else f"{spec['label']} {S}x{S} train step"),
                           "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
                           "parallelism": f"dp{world}", "final_loss": round(final_loss, 5),
-                          "model_tflops": round(value * FWD_BWD_GFLOP_PER_IMG / 1e3, 2)},
+                          "model_tflops": round(value * gflop / 1e3, 2) if gflop else None},
                "roofline": roof, "cpu_baseline": cpu, "val_dice": vdice}
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -84,6 +84,11 @@ __device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, in
 // per-channel BatchNorm parameters are loaded once; indices are 32-bit (M*C/8 < 2^31).
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
+  const T* __restrict__ A0 = (const T*)a.a0;
+  const T* __restrict__ A1 = (const T*)a.a1;
+  const T* __restrict__ A2 = (const T*)a.a2;
+  T* __restrict__ O0 = (T*)a.o0;
+  T* __restrict__ O1 = (T*)a.o1;
   const int cpp = a.C >> 3;
   const int total = a.M * cpp;
   const int first = blockIdx.x * 256 + threadIdx.x;
@@ -95,6 +100,7 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
     if (a.a0) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
     if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
   }
+#pragma unroll 2
   for (int e = first; e < total; e += stride) {
     const int m = e / cpp;
     if (!fixed) {
@@ -104,23 +110,23 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
     }
     const size_t off = (size_t)m * a.C + c0;
     float y[8], out[8];
-    if (a.a0) load8<T>((const T*)a.a0 + off, y);
+    if (a.a0) load8<T>(A0 + off, y);
     if constexpr (MODE == EW_BN_ACT) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float v = y[q] * sc[q] + sh[q];
         out[q] = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 2 ? sigm(v) : v);
       }
-      store8<T>((T*)a.o0 + off, out);
+      store8<T>(O0 + off, out);
     } else if constexpr (MODE == EW_LOCAL_ATTN) {
       // a0 = y1 (sc, sh), a1 = y2 (sc2, sh2); tbl = o [B][P][P][C]; o0 = local, o1 = attn
       if (a.o0) {
 #pragma unroll
         for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f);
-        store8<T>((T*)a.o0 + off, out);
+        store8<T>(O0 + off, out);
       }
       float y2[8];
-      load8<T>((const T*)a.a1 + off, y2);
+      load8<T>(A1 + off, y2);
       const int hw = a.H * a.W;
       const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
       int h0, h1, w0, w1;
@@ -140,24 +146,24 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
         const float v = y2[q] * sc2[q] + sh2[q];
         out[q] = gm * up + (a.act ? fmaxf(v, 0.f) : v);
       }
-      store8<T>((T*)a.o1 + off, out);
+      store8<T>(O1 + off, out);
     } else if constexpr (MODE == EW_GATE_FUSE) {
       float l[8], at[8];
-      load8<T>((const T*)a.a1 + off, l);
-      load8<T>((const T*)a.a2 + off, at);
+      load8<T>(A1 + off, l);
+      load8<T>(A2 + off, at);
 #pragma unroll
       for (int q = 0; q < 8; ++q) {
         float g = sigm(y[q] * sc[q] + sh[q]);
         out[q] = g * l[q] + (1.f - g) * at[q];
       }
-      store8<T>((T*)a.o0 + off, out);
+      store8<T>(O0 + off, out);
     } else if constexpr (MODE == EW_BLOCK_OUT) {
       float r[8];
-      load8<T>((const T*)a.a1 + off, r);
+      load8<T>(A1 + off, r);
       const float rs = *a.scalar;
 #pragma unroll
       for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f) + rs * r[q];
-      store8<T>((T*)a.o0 + off, out);
+      store8<T>(O0 + off, out);
     }
   }
 }
@@ -183,6 +189,15 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
 #pragma unroll
     for (int q = 0; q < 8; ++q) acc[s][q] = 0.f;
 
+  // restrict-qualified views: the stores of one pixel cannot alias the loads of the next, so the
+  // unrolled loop issues several pixels' loads back to back (memory-level parallelism)
+  const T* __restrict__ A0 = (const T*)a.a0;
+  const T* __restrict__ A1 = (const T*)a.a1;
+  const T* __restrict__ A2 = (const T*)a.a2;
+  const T* __restrict__ A3 = (const T*)a.a3;
+  T* __restrict__ O0 = (T*)a.o0;
+  T* __restrict__ O1 = (T*)a.o1;
+  T* __restrict__ O2 = (T*)a.o2;
   const int mbeg = blockIdx.x * a.tile_px;
   const int mend = min(a.M, mbeg + a.tile_px);
   float sc[8], sh[8], mu[8], is[8];
@@ -199,19 +214,20 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
     }
   }
   if (active) {
+#pragma unroll 4
     for (int m = mbeg + lane_px; m < mend; m += pl) {
       const size_t off = (size_t)m * a.C + c0;
       if constexpr (MODE == EW_CHANNEL_SUM) {
         float x[8];
-        load8<T>((const T*)a.a0 + off, x);
+        load8<T>(A0 + off, x);
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[0][q] += x[q];
       } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
         // a0 = dout, a1 = y4, a2 = res; o0 = dz4, o1 = dres
         float d[8], y[8], r[8], dz[8], dr[8];
-        load8<T>((const T*)a.a0 + off, d);
-        load8<T>((const T*)a.a1 + off, y);
-        load8<T>((const T*)a.a2 + off, r);
+        load8<T>(A0 + off, d);
+        load8<T>(A1 + off, y);
+        load8<T>(A2 + off, r);
         const float rs = *a.scalar;
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
@@ -222,12 +238,12 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
           acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
           acc[2][q] += d[q] * r[q];
         }
-        store8<T>((T*)a.o0 + off, dz);
-        store8<T>((T*)a.o1 + off, dr);
+        store8<T>(O0 + off, dz);
+        store8<T>(O1 + off, dr);
       } else if constexpr (MODE == EW_BWD_RELU_BN) {
         float d[8], y[8], dz[8];
-        load8<T>((const T*)a.a0 + off, d);
-        load8<T>((const T*)a.a1 + off, y);
+        load8<T>(A0 + off, d);
+        load8<T>(A1 + off, y);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
@@ -235,16 +251,16 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
           acc[0][q] += z;
           acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
         }
-        store8<T>((T*)a.o0 + off, dz);
+        store8<T>(O0 + off, dz);
       } else if constexpr (MODE == EW_BWD_GATE) {
         // a0 = dfused, a1 = y3, a2 = local, a3 = attn; o0 = dlocal(+=), o1 = dattn(+=), o2 = dz3
         float df[8], y[8], l[8], at[8], dl[8], da[8], dz[8];
-        load8<T>((const T*)a.a0 + off, df);
-        load8<T>((const T*)a.a1 + off, y);
-        load8<T>((const T*)a.a2 + off, l);
-        load8<T>((const T*)a.a3 + off, at);
-        load8<T>((const T*)a.o0 + off, dl);
-        load8<T>((const T*)a.o1 + off, da);
+        load8<T>(A0 + off, df);
+        load8<T>(A1 + off, y);
+        load8<T>(A2 + off, l);
+        load8<T>(A3 + off, at);
+        load8<T>(O0 + off, dl);
+        load8<T>(O1 + off, da);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float g = sigm(y[q] * sc[q] + sh[q]);
@@ -256,14 +272,14 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
           acc[0][q] += z;
           acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
         }
-        store8<T>((T*)a.o0 + off, dl);
-        store8<T>((T*)a.o1 + off, da);
-        store8<T>((T*)a.o2 + off, dz);
+        store8<T>(O0 + off, dl);
+        store8<T>(O1 + off, da);
+        store8<T>(O2 + off, dz);
       } else if constexpr (MODE == EW_BWD_ATTN_ENTRY) {
         // a0 = dattn, a1 = y2, tbl = dpooled [B][P][P][C]; o0 = dz2
         float d[8], y[8], dz[8];
-        load8<T>((const T*)a.a0 + off, d);
-        load8<T>((const T*)a.a1 + off, y);
+        load8<T>(A0 + off, d);
+        load8<T>(A1 + off, y);
         const int hw = a.H * a.W;
         const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - h * a.W;
         const int P = a.P;
@@ -289,12 +305,12 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
           acc[0][q] += z;
           acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
         }
-        store8<T>((T*)a.o0 + off, dz);
+        store8<T>(O0 + off, dz);
       } else if constexpr (MODE == EW_BN_BWD_APPLY) {
         // a0 = dz, a1 = y; gamma, coef [2][C] (hoisted); o0 = dy; sum dy (conv bias grad)
         float dz[8], y[8], dy[8];
-        load8<T>((const T*)a.a0 + off, dz);
-        load8<T>((const T*)a.a1 + off, y);
+        load8<T>(A0 + off, dz);
+        load8<T>(A1 + off, y);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           float xh = (y[q] - mu[q]) * is[q];
@@ -302,7 +318,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
           dy[q] = v;
           acc[0][q] += v;
         }
-        store8<T>((T*)a.o0 + off, dy);
+        store8<T>(O0 + off, dy);
       }
     }
   }

@@ -583,6 +583,16 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   bool first_iter = true;
   for (; t < mtiles; t += gridDim.x, slot ^= 1) {
     const int tn = t + gridDim.x;
+    // accumulate mode: fetch this tile's destination values now, ahead of the next A image, so
+    // their latency overlaps the wait for this tile's A image instead of following the MFMAs
+    uint4 dpre[ACC ? NSTORE : 1];
+    if constexpr (ACC) {
+#pragma unroll
+      for (int it = 0; it < NSTORE; ++it) {
+        const int m = t * 64 + o_row[it];
+        dpre[it] = (m < M && o_base[it]) ? *(const uint4*)(o_base[it] + (size_t)m * o_ld[it]) : uint4{0, 0, 0, 0};
+      }
+    }
     if (tn < mtiles) {
       issue(tn, slot ^ 1);
       if (ACC || first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
@@ -667,7 +677,7 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
       if constexpr (ACC) {
         float a[8], o[8];
         load8<T>((const T*)&v, a);
-        load8<T>(dst, o);
+        load8<T>((const T*)&dpre[it], o);
 #pragma unroll
         for (int q = 0; q < 8; ++q) a[q] += o[q];
         store8<T>(dst, a);

@@ -366,21 +366,31 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     }
 }
 
-__global__ void wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI, int NJ,
-                                    int layout, int ntaps, int Ctot, int Creal, int ndst,
-                                    float* d0, float* d1, float* d2) {
-  int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  int64_t total = (int64_t)NI * NJ;
-  if (e >= total) return;
+// 64 output elements per workgroup, 4 split-ranges per element (threads sub*64 + el: each group
+// of 64 threads reads 64 consecutive elements of one split -> coalesced), 8 loads in flight per
+// thread; the 4 partial sums are combined in a fixed order through LDS (deterministic).
+__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI, int NJ,
+                                                           int layout, int ntaps, int Ctot, int Creal, int ndst,
+                                                           float* d0, float* d1, float* d2) {
+  __shared__ float part[4][64];
+  const int el = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + el;
+  const int64_t total = (int64_t)NI * NJ;
+  const int per = (splits + 3) >> 2, k0 = sub * per, k1 = min(splits, k0 + per);
   float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
-  int k = 0;
-  for (; k + 7 < splits; k += 8) {  // 8 independent loads in flight (latency-bound otherwise)
-    const float* p = slab + (int64_t)k * total + e;
-    a0 += p[0]; a1 += p[total]; a2 += p[2 * total]; a3 += p[3 * total];
-    a4 += p[4 * total]; a5 += p[5 * total]; a6 += p[6 * total]; a7 += p[7 * total];
+  if (e < total) {
+    int k = k0;
+    for (; k + 7 < k1; k += 8) {
+      const float* p = slab + (int64_t)k * total + e;
+      a0 += p[0]; a1 += p[total]; a2 += p[2 * total]; a3 += p[3 * total];
+      a4 += p[4 * total]; a5 += p[5 * total]; a6 += p[6 * total]; a7 += p[7 * total];
+    }
+    for (; k < k1; ++k) a0 += slab[(int64_t)k * total + e];
   }
-  for (; k < splits; ++k) a0 += slab[(int64_t)k * total + e];
-  const float s = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
+  part[sub][el] = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
+  __syncthreads();
+  if (sub != 0 || e >= total) return;
+  const float s = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
   int i = (int)(e / NJ), j = (int)(e % NJ);
   if (layout == 0) {
     int rows = NI / ndst;
@@ -503,7 +513,7 @@ extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ,
   if (!slab || !dst || ndst < 1 || ndst > 3) return DFCSA_EINVAL;
   if (layout == 2 ? (ndst != 3 || Ctot <= 0 || 2 * Ctot > NI) : (NI % ndst != 0)) return DFCSA_EINVAL;
   int64_t total = (int64_t)NI * NJ;
-  int blocks = (int)((total + 255) / 256);
+  int blocks = (int)((total + 63) / 64);
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, splits,
                      NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
                      ndst > 2 ? dst[2] : nullptr);
