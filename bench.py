@@ -268,7 +268,7 @@ def main():
         dom_key = "conv_gemm" if dom is cls[1] else "conv_wgrad"
         peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
         ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
-        traffic, tsrc = pmc_traffic(dom_key)
+        traffic, tsrc = pmc_traffic(dom_key) if headline else (None, None)   # PMC passes cover the headline
         roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc,
