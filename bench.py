@@ -173,7 +173,9 @@ def main():
            "training": {"learning_rate": 0.01, "momentum": 0.9, "weight_decay": 1e-4}}
     headline = args.model == "dfc"
     torch.manual_seed(0)
-    model = ModelFactory.get_model(cfg).to(dev).train()
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):   # the factory's messages: stdout carries ONE JSON line
+        model = ModelFactory.get_model(cfg).to(dev).train()
     opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
 
     B, S = args.batch, args.img
