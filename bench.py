@@ -254,20 +254,23 @@ def main():
     roof = None
     if not args.no_kernel_timing:
         import ctypes
-        L.LIB.dfcsa_prof_enable(1, 1)
-        L.LIB.dfcsa_prof_enable(2, 1)
+        classes = ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad)", "conv_gemm"),
+                   (2, "conv_wgrad (weight-gradient GEMM)", "conv_wgrad"),
+                   (3, "fra (full-resolution attention fwd/bwd, bf16 MFMA)", "fra"))
+        for c, _, _ in classes:
+            L.LIB.dfcsa_prof_enable(c, 1)
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         cls = {}
-        for c, name in ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad)"), (2, "conv_wgrad (weight-gradient GEMM)")):
+        for c, name, key in classes:
             ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
             L.LIB.dfcsa_prof_read(c, ctypes.addressof(ms), ctypes.addressof(n), ctypes.addressof(fl))
-            cls[c] = (name, ms.value, n.value, fl.value)
+            if n.value:
+                cls[c] = (name, ms.value, n.value, fl.value, key)
             L.LIB.dfcsa_prof_enable(c, 0)
         dom = max(cls.values(), key=lambda v: v[1])
-        name, ms, n, fl = dom
-        dom_key = "conv_gemm" if dom is cls[1] else "conv_wgrad"
+        name, ms, n, fl, dom_key = dom
         peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
         ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
         traffic, tsrc = pmc_traffic(dom_key) if headline else (None, None)   # PMC passes cover the headline
