@@ -460,6 +460,25 @@ int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, const void*
                     const float* dlogits, void* dx, float* partial_w, float* partial_b, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Sliding-window inference (reference inference.py:104-153 predict_large_image, :73-91
+ * calculate_segmentation_metrics).  Tiles are th x tw; the grid is ys[ny] x xs[nx] with tile
+ * t = iy*nx + ix (the reference's y-major loop order).
+ * ---------------------------------------------------------------------------------------- */
+/* img uint8 [H][W][C] -> out fp32 [T*variants][C][th][tw] for the T tiles with origins
+ * (ty[t], tx[t]): (v/255 - mean[c]) / std[c] (mean_std: HOST array of 2*C floats, :116-119).
+ * variants 3 appends the h-flipped and the v-flipped tile (TTA, :136-139). */
+int dfcsa_tiles_gather(const uint8_t* img, int H, int W, int C, const int* ty, const int* tx, int T, int th, int tw,
+                       int variants, const float* mean_std, float* out, void* stream);
+/* logits fp32 [ny*nx*variants][th][tw] -> canvas fp32 [H][W]: mean over the covering tiles of
+ * sigmoid (variants 3: (p + unflip(p_h) + unflip(p_v)) / 3), sums in tile order (:132-151). */
+int dfcsa_tiles_accumulate(const float* logits, const int* ys, int ny, const int* xs, int nx, int th, int tw,
+                           int variants, int H, int W, float* canvas, void* stream);
+/* counts[0..2] = TP, FP, FN of (prob > thr) against (gray(gt) > gt_thr); gt uint8 [n][gt_channels]
+ * (3 channels: OpenCV RGB2GRAY fixed point, :300-305).  counts: device, 4 x uint64, zeroed here. */
+int dfcsa_seg_counts(const float* prob, int64_t n, float thr, const uint8_t* gt, int gt_channels, int gt_thr,
+                     unsigned long long* counts, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Profiling hook: when enabled for a kernel class, every launch of that class is bracketed by
  * hipEvents on its own stream; dfcsa_prof_read returns the summed elapsed milliseconds and
  * the launch count since the last reset (synchronises on the recorded events).
