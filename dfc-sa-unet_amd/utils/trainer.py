@@ -16,9 +16,9 @@ torch optimizer the reference's clip_grad_norm_ + step() are called.  A plain
 
 Differences kept deliberately small and listed: plots are written only when matplotlib is
 importable; best/worst validation samples are kept (tensors on the host) but image dumps
-(cv2 in the reference) are not written; ``train(resume_from)`` restores histories and the
-start epoch (the reference resets them, trainer.py:334-349 -- pass
-``training.reference_resume_semantics: true`` to keep that behaviour).
+(cv2 in the reference) are not written; ``train(resume_from)`` restores the histories, the
+start epoch and the best validation Dice (the reference resets histories and best Dice,
+trainer.py:334-349 -- pass ``training.reference_resume_semantics: true`` to keep that behaviour).
 """
 import csv
 import os
@@ -165,6 +165,8 @@ class Trainer:
         for k in ("train_losses", "val_losses", "train_dice_scores", "val_dice_scores", "train_iou_scores",
                   "val_iou_scores", "best_val_loss"):
             setattr(self, k, ckpt[k])
+        # the reference does not store the epoch axis of the histories: rebuild it
+        self.epochs = list(range(ckpt["epoch"] + 2 - len(self.train_losses), ckpt["epoch"] + 2))
         return ckpt["epoch"]
 
     # ------------------------------------------------------------------ loop
@@ -196,11 +198,13 @@ class Trainer:
         if resume_from:
             start_epoch = self.load_checkpoint(resume_from) + 1
             print(f"從 epoch {start_epoch} 恢復訓練")
-        if not resume_from or self.config["training"].get("reference_resume_semantics", False):
+        reference_semantics = self.config["training"].get("reference_resume_semantics", False)
+        if not resume_from or reference_semantics:
             self.epochs, self.train_losses, self.val_losses = [], [], []
             self.train_dice_scores, self.val_dice_scores = [], []
             self.train_iou_scores, self.val_iou_scores = [], []
-        best_val_dice = 0.0
+        # the reference restarts the best-Dice tracking at 0 on resume (trainer.py:334-349)
+        best_val_dice = 0.0 if reference_semantics else max(self.val_dice_scores, default=0.0)
         for epoch in range(start_epoch, self.num_epochs):
             tr = self.train_epoch(epoch)
             va = self.validate_epoch(self.val_loader)

@@ -16,6 +16,9 @@ Reference files imported (file-by-file, via importlib, because the reference's p
                                 :29-92, UNet_FullResAttention :95-97 (config 5; imported under a stub
                                 package because it uses a package-relative import of
                                 unet_dfc_sa_ablation_branches.py)
+  * inference.py                calculate_segmentation_metrics :73-91, predict_large_image :104-153
+                                (those two functions only, taken from the source with ast: the module
+                                imports cv2 / matplotlib / torchvision, which are not installed)
 The train-step semantics follow utils/trainer.py:115-151 and train.py:73-78.
 
 Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz, ~a few MB)
@@ -485,9 +488,78 @@ def _n_classes_1(cfg):
     return cfg
 
 
+# ----------------------------------------------------------------------------------------
+# Sliding-window inference (inference.py:73-153).  The module itself imports cv2, matplotlib
+# and torchvision, none of which is installed here, so only the two functions under test are
+# taken from its source (ast) and run with the reference's own code.  torchvision's ToTensor /
+# Normalize, the only torchvision pieces they use, are restated below with torchvision's
+# arithmetic (uint8 -> float / 255; (x - mean) / std).  The "model" is a fixed 3x3 conv.
+# ----------------------------------------------------------------------------------------
+def _reference_inference_functions():
+    import ast
+    import types
+
+    from PIL import Image
+    from tqdm import tqdm
+
+    class Compose:
+        def __init__(self, ts):
+            self.ts = ts
+
+        def __call__(self, x):
+            for t in self.ts:
+                x = t(x)
+            return x
+
+    class ToTensor:
+        def __call__(self, pic):
+            a = torch.from_numpy(np.array(pic, dtype=np.uint8, copy=True))
+            return a.permute(2, 0, 1).contiguous().float().div(255)
+
+    class Normalize:
+        def __init__(self, mean, std):
+            self.mean, self.std = mean, std
+
+        def __call__(self, t):
+            m = torch.as_tensor(self.mean, dtype=t.dtype).view(-1, 1, 1)
+            s = torch.as_tensor(self.std, dtype=t.dtype).view(-1, 1, 1)
+            return t.sub(m).div(s)
+
+    transforms = types.SimpleNamespace(Compose=Compose, ToTensor=ToTensor, Normalize=Normalize)
+    src = open(os.path.join(REF, "inference.py"), encoding="utf-8").read()
+    tree = ast.parse(src)
+    keep = [n for n in tree.body if isinstance(n, ast.FunctionDef)
+            and n.name in ("calculate_segmentation_metrics", "predict_large_image")]
+    ns = {"np": np, "torch": torch, "Image": Image, "transforms": transforms, "tqdm": tqdm}
+    exec(compile(ast.Module(body=keep, type_ignores=[]), "reference/inference.py", "exec"), ns)
+    return ns["predict_large_image"], ns["calculate_segmentation_metrics"]
+
+
+def gen_inference():
+    predict_large_image, calc_counts = _reference_inference_functions()
+    torch.manual_seed(9000)
+    conv = torch.nn.Conv2d(3, 1, 3, padding=1)
+    with torch.no_grad():
+        conv.weight.mul_(3.0)
+    g = np.random.default_rng(9001)
+    cases = {"a": ((150, 230), 64, 20), "b": ((40, 50), 64, 20), "c": ((128, 128), 64, 0), "d": ((97, 301), 48, 10)}
+    out = {"conv.weight": np32(conv.weight), "conv.bias": np32(conv.bias)}
+    for name, ((h, w), tile, overlap) in cases.items():
+        img = g.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+        out[f"{name}.image"] = img
+        out[f"{name}.cfg"] = np.array([tile, overlap], dtype=np.int64)
+        for tta in (False, True):
+            out[f"{name}.canvas.tta{int(tta)}"] = predict_large_image(conv, img, tile, overlap, "cpu", use_tta=tta)
+        gt = g.integers(0, 2, size=(h, w), dtype=np.uint8) * 255
+        out[f"{name}.gt"] = gt
+        c = calc_counts((out[f"{name}.canvas.tta0"] > 0.5).astype(np.uint8), (gt > 128).astype(np.uint8))
+        out[f"{name}.counts"] = np.array([c["tp"], c["fp"], c["fn"], c["tn"]], dtype=np.int64)
+    save("inference.npz", **out)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet"]
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference"]
     for w in which:
         globals()["gen_" + w]()
     print("torch", torch.__version__)

@@ -228,3 +228,33 @@ def test_trainer_reference_style_epoch(tmp_path):
     assert ep == 0
     for k, v in model.state_dict().items():
         assert torch.equal(model2.state_dict()[k], v), k
+
+
+@pytest.mark.parametrize("reference_semantics", [False, True])
+def test_trainer_resume(tmp_path, reference_semantics):
+    """train(resume_from): start epoch = checkpoint epoch + 1 (trainer.py:337-340).  By default the
+    histories and best Dice continue from the checkpoint; training.reference_resume_semantics keeps
+    the reference's reset of both (trainer.py:341-349)."""
+    from dfcsa.optim import FusedSGD
+    from utils.trainer import Trainer
+    model, fx = make_model("fp32")
+    cfg = {"training": {"num_epochs": 2, "save_checkpoint_freq": 1, "loss": {"type": "bce_dice", "params": LP},
+                        "reference_resume_semantics": reference_semantics},
+           "logging": {"log_dir": str(tmp_path / "logs"), "images_dir": str(tmp_path / "img"),
+                       "save_best_worst_samples": 0}}
+    batches = [{"image": torch.from_numpy(np.asarray(fx[f"x{s}"])).float(),
+                "mask": torch.from_numpy(np.asarray(fx[f"t{s}"])).float()} for s in (1, 2)]
+    tr = Trainer(model, batches, batches[:1], FusedSGD(model.parameters(), lr=0.01, momentum=0.9),
+                 torch.device("cuda"), cfg)
+    tr.train()
+    assert tr.epochs == [1, 2] and len(tr.train_losses) == 2
+    cfg["training"]["num_epochs"] = 3
+    model2, _ = make_model("fp32")
+    tr2 = Trainer(model2, batches, batches[:1], FusedSGD(model2.parameters(), lr=0.01, momentum=0.9),
+                  torch.device("cuda"), cfg)
+    tr2.train(resume_from=str(tmp_path / "logs" / "checkpoints" / "checkpoint_epoch_2.pth"))
+    if reference_semantics:
+        assert tr2.epochs == [3] and len(tr2.train_losses) == 1
+    else:
+        assert tr2.epochs == [1, 2, 3] and tr2.train_losses[:2] == tr.train_losses
+        assert len(tr2.val_dice_scores) == 3

@@ -253,3 +253,47 @@ def test_transunet_oracle_and_seeded_init():
     for k, v in bufs.items():
         if "running" in k:
             close(v, fx["buf." + k], rtol=1e-5, atol=1e-6)
+
+
+# --------------------------------------------------------------------- sliding-window inference
+def test_inference_oracle_matches_reference_predict_large_image(golden):
+    """oracle/inference_oracle.py restates inference.py:73-153; the fixture is the reference's own
+    predict_large_image (tiles, TTA, overlap averaging) run with a fixed 3x3 conv as the model."""
+    from oracle import inference_oracle as IO
+    fx = golden("inference.npz")
+    conv = torch.nn.Conv2d(3, 1, 3, padding=1)
+    conv.weight.data = torch.from_numpy(fx["conv.weight"])
+    conv.bias.data = torch.from_numpy(fx["conv.bias"])
+
+    def predict(b):
+        with torch.no_grad():
+            return conv(torch.from_numpy(np.ascontiguousarray(b))).numpy()
+
+    for name in ("a", "b", "c", "d"):
+        img = fx[f"{name}.image"]
+        tile, overlap = (int(v) for v in fx[f"{name}.cfg"])
+        for tta in (0, 1):
+            got = IO.predict_large_image(predict, img, tile, overlap, use_tta=bool(tta))
+            want = fx[f"{name}.canvas.tta{tta}"]
+            assert got.shape == want.shape and got.dtype == np.float32
+            assert np.abs(got - want).max() < 2e-6, (name, tta)
+        pb = (fx[f"{name}.canvas.tta0"] > 0.5).astype(np.uint8)
+        c = IO.calculate_segmentation_metrics(pb, (fx[f"{name}.gt"] > 128).astype(np.uint8))
+        assert [c[k] for k in ("tp", "fp", "fn", "tn")] == fx[f"{name}.counts"].tolist()
+
+
+def test_inference_tile_grid_matches_oracle_loop():
+    """utils.inference.tile_grid (host logic) reproduces the reference loop's tile origins."""
+    from utils.inference import tile_grid
+    for (h, w, tile, ov) in [(150, 230, 64, 20), (40, 50, 64, 20), (128, 128, 64, 0), (1000, 777, 224, 50),
+                             (224, 224, 224, 50), (225, 223, 224, 50)]:
+        stride = tile - ov
+        want = []
+        for y in range(0, h, stride):
+            for x in range(0, w, stride):
+                ye, xe = min(y + tile, h), min(x + tile, w)
+                want.append((max(0, ye - tile), max(0, xe - tile), ye - max(0, ye - tile), xe - max(0, xe - tile)))
+        ys, xs, th, tw = tile_grid(h, w, tile, ov)
+        assert [(y, x, th, tw) for y in ys for x in xs] == want
+    with pytest.raises(ValueError):
+        tile_grid(10, 10, 50, 50)
