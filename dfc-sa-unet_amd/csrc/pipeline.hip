@@ -9,6 +9,16 @@
 //                     y-major loop order, so the fp32 sums are formed in the same order
 //   seg_counts        threshold + TP/FP/FN against a uint8 ground truth (:73-91, :289-314),
 //                     integer counts (exact); TN = n - TP - FP - FN on the host
+//
+// Paired training transforms (reference utils/data_loader.py:25-73, :119-135), bit-exact with the
+// Pillow calls the reference makes (Pillow 12.2.0; restated and pinned in oracle/augment_oracle.py):
+//   aug_resample      one pass of Image.resize(BILINEAR): Resample.c's separable 8-bit
+//                     convolution with 22-bit fixed-point coefficients (host-computed tables);
+//                     a batch of per-sample descriptors per launch (horizontal, then vertical)
+//   aug_finish        Image.rotate (BILINEAR image: Geometry.c's double-precision affine sampling,
+//                     contraction off; NEAREST mask: 16.16 fixed point) + FLIP_LEFT_RIGHT +
+//                     ToTensor + Normalize for the image, resize(NEAREST) + rotate + flip +
+//                     (/255 > 0.5) for the mask, straight into the NCHW fp32 batch
 // All work is bandwidth-bound byte/float streaming; no MFMA.
 #include <algorithm>
 #include <cmath>
@@ -126,7 +136,153 @@ __global__ void __launch_bounds__(256) seg_counts_kernel(const float* __restrict
   }
 }
 
+// ---------------------------------------------------------------- paired transforms
+// One thread per output element (all channels).  Horizontal pass (axis 1): line = output row
+// (source row row0 + line), taps step C bytes.  Vertical pass (axis 0): line = column, taps step
+// src_pitch bytes.  acc = 2^21 + sum(pixel * coeff), out = clamp(acc >> 22, 0, 255).
+__global__ void __launch_bounds__(256) aug_resample_kernel(const dfcsa_resample_desc* __restrict__ descs, int C) {
+  const dfcsa_resample_desc d = descs[blockIdx.y];
+  const int64_t total = (int64_t)d.n_out * d.n_lines;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    int o, line;
+    if (d.axis) {
+      line = (int)(e / d.n_out);
+      o = (int)(e - (int64_t)line * d.n_out);
+    } else {
+      o = (int)(e / d.n_lines);
+      line = (int)(e - (int64_t)o * d.n_lines);
+    }
+    const int first = d.bounds[2 * o], cnt = d.bounds[2 * o + 1];
+    const int32_t* k = d.kk + (int64_t)o * d.ksize;
+    const uint8_t* s;
+    int64_t step;
+    uint8_t* out;
+    if (d.axis) {
+      s = d.src + (int64_t)(d.row0 + line) * d.src_pitch + (int64_t)first * C;
+      step = C;
+      out = d.dst + (int64_t)line * d.dst_pitch + (int64_t)o * C;
+    } else {
+      s = d.src + (int64_t)first * d.src_pitch + (int64_t)line * C;
+      step = d.src_pitch;
+      out = d.dst + (int64_t)o * d.dst_pitch + (int64_t)line * C;
+    }
+    int acc[4] = {1 << 21, 1 << 21, 1 << 21, 1 << 21};
+    for (int t = 0; t < cnt; ++t) {
+      const int w = k[t];
+      for (int c = 0; c < C; ++c) acc[c] += (int)s[t * step + c] * w;
+    }
+    for (int c = 0; c < C; ++c) out[c] = (uint8_t)min(max(acc[c] >> 22, 0), 255);
+  }
+}
+
+// Geometry.c bilinear_filter (8-bit bands): sample at (xin, yin) of the [H][W][3] image.
+__device__ __forceinline__ bool bilinear_rgb(const uint8_t* img, int W, int H, double xin, double yin,
+                                             int (&v)[3]) {
+#pragma clang fp contract(off)
+  if (xin < 0.0 || xin >= W || yin < 0.0 || yin >= H) return false;
+  xin -= 0.5;
+  yin -= 0.5;
+  const double fx = floor(xin), fy = floor(yin);
+  const int x = (int)fx, y = (int)fy;
+  const double dx = xin - fx, dy = yin - fy;
+  const int x0 = min(max(x, 0), W - 1), x1 = min(max(x + 1, 0), W - 1);
+  const int ya = min(max(y, 0), H - 1);
+  const bool yb_ok = y + 1 >= 0 && y + 1 < H;
+  const uint8_t* ra = img + (int64_t)ya * W * 3;
+  const uint8_t* rb = img + (int64_t)(yb_ok ? y + 1 : ya) * W * 3;
+  for (int c = 0; c < 3; ++c) {
+    // BILINEAR(v, a, b, d) = a + (b - a) * d with integer (b - a), evaluated in double
+    const double v1 = (double)ra[x0 * 3 + c] + (double)((int)ra[x1 * 3 + c] - (int)ra[x0 * 3 + c]) * dx;
+    double v2 = v1;
+    if (yb_ok) v2 = (double)rb[x0 * 3 + c] + (double)((int)rb[x1 * 3 + c] - (int)rb[x0 * 3 + c]) * dx;
+    const double r = v1 + (v2 - v1) * dy;
+    v[c] = min(max((int)r, 0), 255);  // (UINT8) cast: truncation
+  }
+  return true;
+}
+
+__global__ void __launch_bounds__(256) aug_finish_kernel(const dfcsa_aug_desc* __restrict__ descs, int H, int W,
+                                                         NormArgs na, int normalize, float* __restrict__ images,
+                                                         float* __restrict__ masks) {
+#pragma clang fp contract(off)
+  const dfcsa_aug_desc d = descs[blockIdx.y];
+  const int64_t plane = (int64_t)H * W;
+  float* oi = images + (int64_t)blockIdx.y * 3 * plane;
+  float* om = masks + (int64_t)blockIdx.y * plane;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < plane; e += (int64_t)gridDim.x * blockDim.x) {
+    const int y = (int)(e / W), xo = (int)(e - (e / W) * W);
+    const int x = d.flip ? W - 1 - xo : xo;  // FLIP_LEFT_RIGHT after the rotation
+    int v[3] = {0, 0, 0};
+    int mx = -1, my = -1;                    // position in the resized mask (-1: fill)
+    if (d.rotate == 1) {
+      const double xi = x + 0.5, yi = y + 0.5;
+      const double xin = d.m[0] * xi + d.m[1] * yi + d.m[2];
+      const double yin = d.m[3] * xi + d.m[4] * yi + d.m[5];
+      bilinear_rgb(d.img, W, H, xin, yin, v);
+      const int64_t xx = (int64_t)d.fix[2] + (int64_t)y * d.fix[1] + (int64_t)x * d.fix[0];
+      const int64_t yy = (int64_t)d.fix[5] + (int64_t)y * d.fix[4] + (int64_t)x * d.fix[3];
+      const int xin_n = (int)(xx >> 16), yin_n = (int)(yy >> 16);
+      if (xin_n >= 0 && xin_n < W && yin_n >= 0 && yin_n < H) {
+        mx = xin_n;
+        my = yin_n;
+      }
+    } else {
+      int sx = x, sy = y;  // exact transposes: 0 none, 2 ROTATE_180, 3 ROTATE_90, 4 ROTATE_270
+      if (d.rotate == 2) {
+        sx = W - 1 - x;
+        sy = H - 1 - y;
+      } else if (d.rotate == 3) {
+        sx = W - 1 - y;
+        sy = x;
+      } else if (d.rotate == 4) {
+        sx = y;
+        sy = H - 1 - x;
+      }
+      const uint8_t* p = d.img + ((int64_t)sy * W + sx) * 3;
+      v[0] = p[0];
+      v[1] = p[1];
+      v[2] = p[2];
+      mx = sx;
+      my = sy;
+    }
+    uint8_t mv = 0;
+    if (mx >= 0) {
+      const int sxm = d.xtab[mx], sym = d.ytab[my];  // resize(NEAREST) tables (-1: fill 0)
+      if (sxm >= 0 && sym >= 0) mv = d.mask[(int64_t)sym * d.mask_w + sxm];
+    }
+    for (int c = 0; c < 3; ++c) {
+      float f = (float)v[c] / 255.0f;
+      if (normalize) f = (f - na.mean[c]) / na.stdv[c];
+      oi[c * plane + e] = f;
+    }
+    om[e] = ((float)mv / 255.0f > 0.5f) ? 1.0f : 0.0f;
+  }
+}
+
 }  // namespace
+
+extern "C" int dfcsa_aug_resample(const dfcsa_resample_desc* descs_dev, int n, int max_work, int C, void* stream) {
+  if (!descs_dev || n <= 0 || max_work <= 0 || C <= 0 || C > 4 || n > 65535) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(aug_resample_kernel, dim3(grid_for(max_work, 256, 2048), n), dim3(256), 0, (hipStream_t)stream,
+                     descs_dev, C);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_aug_finish(const dfcsa_aug_desc* descs_dev, int n, int H, int W, const float* mean_std,
+                                int normalize, float* images, float* masks, void* stream) {
+  if (!descs_dev || n <= 0 || n > 65535 || H <= 0 || W <= 0 || !images || !masks || (normalize && !mean_std))
+    return DFCSA_EINVAL;
+  NormArgs na;
+  for (int c = 0; c < 4; ++c) {
+    na.mean[c] = (normalize && c < 3) ? mean_std[c] : 0.f;
+    na.stdv[c] = (normalize && c < 3) ? mean_std[3 + c] : 1.f;
+  }
+  hipLaunchKernelGGL(aug_finish_kernel, dim3(grid_for((int64_t)H * W, 256, 2048), n), dim3(256), 0,
+                     (hipStream_t)stream, descs_dev, H, W, na, normalize, images, masks);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dfcsa_tiles_gather(const uint8_t* img, int H, int W, int C, const int* ty, const int* tx, int T, int th,
                                   int tw, int variants, const float* mean_std, float* out, void* stream) {

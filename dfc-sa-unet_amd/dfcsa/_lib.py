@@ -89,6 +89,19 @@ class WstdEntry(ctypes.Structure):
                 ("pad", ctypes.c_int)]
 
 
+class ResampleDesc(ctypes.Structure):
+    _fields_ = [("src", ctypes.c_void_p), ("dst", ctypes.c_void_p), ("bounds", ctypes.c_void_p),
+                ("kk", ctypes.c_void_p), ("n_out", ctypes.c_int), ("n_lines", ctypes.c_int), ("ksize", ctypes.c_int),
+                ("axis", ctypes.c_int), ("src_pitch", ctypes.c_int), ("dst_pitch", ctypes.c_int),
+                ("row0", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
+class AugDesc(ctypes.Structure):
+    _fields_ = [("img", ctypes.c_void_p), ("mask", ctypes.c_void_p), ("xtab", ctypes.c_void_p),
+                ("ytab", ctypes.c_void_p), ("m", ctypes.c_double * 6), ("fix", ctypes.c_int * 6),
+                ("rotate", ctypes.c_int), ("flip", ctypes.c_int), ("mask_w", ctypes.c_int), ("pad", ctypes.c_int)]
+
+
 def _load():
     if not os.path.exists(LIB_PATH):
         raise ImportError(

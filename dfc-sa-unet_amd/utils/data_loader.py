@@ -11,6 +11,11 @@ checkout; it is defined here by its use (README.md "Dataset Structure"): ``root/
 and ``root/mask/<name>`` share file names; items are ``{'image', 'mask', 'filename'}``.
 torchvision is not needed: ToTensor / Normalize are restated with numpy (same arithmetic).
 
+``dataset.gpu_augment: true`` (optional, new) moves the transforms to the GPU
+(``utils/augment.py``): the dataset then returns the decoded uint8 arrays plus the random draws
+(made in the reference's order), and ``DeviceBatches`` turns each batch into the device tensors
+the trainer consumes with three HIP launches, bit-exact with the Pillow path.
+
 ``SyntheticEllipses`` is the learnable synthetic task of SURVEY.md section 8d (1-4 random
 ellipses per image, mask-conditioned colour + N(0, 0.5) noise) used to measure validation Dice
 without a dataset.
@@ -100,7 +105,7 @@ class ExtNormalize(ExtTransform):
 class SegmentationDataset(Dataset):
     """root/original/<name> + root/mask/<name> (identical file names)."""
 
-    def __init__(self, root, transform=None, img_size=(224, 224)):
+    def __init__(self, root, transform=None, img_size=(224, 224), raw_augmentation=None):
         if Image is None:
             raise ImportError("PIL is required to read image files")
         self.root = root.replace("\\", "/")
@@ -112,6 +117,8 @@ class SegmentationDataset(Dataset):
                             and os.path.exists(os.path.join(self.mask_dir, n)))
         self.transform = transform
         self.img_size = tuple(img_size)
+        # raw mode (gpu_augment): None = off, else whether the random draws are made
+        self.raw_augmentation = raw_augmentation
 
     def __len__(self):
         return len(self.names)
@@ -120,6 +127,11 @@ class SegmentationDataset(Dataset):
         name = self.names[i]
         img = Image.open(os.path.join(self.img_dir, name)).convert("RGB")
         mask = Image.open(os.path.join(self.mask_dir, name)).convert("L")
+        if self.raw_augmentation is not None:
+            from utils.augment import draw_augmentation
+            angle, flip = draw_augmentation(self.raw_augmentation)
+            return {"image": np.asarray(img, dtype=np.uint8), "mask": np.asarray(mask, dtype=np.uint8),
+                    "angle": angle, "flip": flip, "filename": name}
         if self.transform is not None:
             img, mask = self.transform(img, mask)
         return {"image": img, "mask": mask, "filename": name}
@@ -156,6 +168,27 @@ class SyntheticEllipses(Dataset):
                 "mask": torch.from_numpy(mask[None].astype(np.float32)), "filename": f"synthetic_{self.seed}_{i}"}
 
 
+class DeviceBatches:
+    """Iterates a DataLoader of raw samples (lists) and yields device batches
+    {'image': [B,3,h,w] fp32, 'mask': [B,1,h,w] fp32, 'filename': [...]} built by the GPU
+    transforms."""
+
+    def __init__(self, loader, transform):
+        self.loader, self.transform = loader, transform
+
+    def __len__(self):
+        return len(self.loader)
+
+    def __iter__(self):
+        for samples in self.loader:
+            images, masks = self.transform(samples)
+            yield {"image": images, "mask": masks, "filename": [s["filename"] for s in samples]}
+
+
+def _collate_list(batch):
+    return batch
+
+
 # ------------------------------------------------------------------ factory
 class DataLoaderFactory:
     """Same config keys as the reference (data_loader.py:75-98): dataset.{train_dir, val_dir,
@@ -172,6 +205,7 @@ class DataLoaderFactory:
         self.img_size = tuple(ds.get("img_size", [224, 224]))
         self.use_augmentation = ds.get("augmentation", False)
         self.synthetic = ds.get("synthetic")
+        self.gpu_augment = bool(ds.get("gpu_augment", False))
         print(f"數據增強: {'啟用' if self.use_augmentation else '禁用'}")
 
     def get_transforms(self, is_train=True):
@@ -185,6 +219,13 @@ class DataLoaderFactory:
         if self.synthetic:
             n = int(self.synthetic) if is_train else max(1, int(self.synthetic) // 4)
             dataset = SyntheticEllipses(n, self.img_size, seed=42 if is_train else 43)
+        elif self.gpu_augment:
+            from utils.augment import PairedTransformGPU
+            dataset = SegmentationDataset(self.train_dir if is_train else self.val_dir, img_size=self.img_size,
+                                          raw_augmentation=bool(is_train and self.use_augmentation))
+            loader = DataLoader(dataset, batch_size=self.batch_size, shuffle=is_train,
+                                num_workers=self.num_workers, collate_fn=_collate_list)
+            return DeviceBatches(loader, PairedTransformGPU(self.img_size, device="cuda"))
         else:
             dataset = SegmentationDataset(self.train_dir if is_train else self.val_dir,
                                           transform=self.get_transforms(is_train), img_size=self.img_size)

@@ -479,6 +479,40 @@ int dfcsa_seg_counts(const float* prob, int64_t n, float thr, const uint8_t* gt,
                      unsigned long long* counts, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Paired image/mask transforms on the GPU (reference utils/data_loader.py:25-73, :119-135:
+ * ExtResize, ExtRandomRotation, ExtRandomHorizontalFlip, ExtToTensor, ExtNormalize), bit-exact with
+ * the Pillow calls the reference makes.  The random draws stay on the host, in the reference's
+ * order; decoding stays on the host.
+ * ---------------------------------------------------------------------------------------- */
+/* one pass of Image.resize(BILINEAR) for one sample: out[o] = clamp((2^21 + sum_t kk[o][t] *
+ * src[bounds[o][0] + t]) >> 22, 0, 255) along `axis` (1: along a row, 0: down a column) */
+typedef struct {
+  const uint8_t* src;     /* rows of src_pitch bytes; the horizontal pass reads rows row0.. */
+  uint8_t* dst;           /* rows of dst_pitch bytes */
+  const int* bounds;      /* [n_out][2]: first tap, tap count */
+  const int* kk;          /* [n_out][ksize] 22-bit fixed-point coefficients */
+  int n_out, n_lines, ksize, axis;
+  int src_pitch, dst_pitch, row0, pad;
+} dfcsa_resample_desc;
+/* descs_dev: n descriptors in device memory; max_work >= n_out * n_lines of every descriptor */
+int dfcsa_aug_resample(const dfcsa_resample_desc* descs_dev, int n, int max_work, int C, void* stream);
+/* rotation (rotate: 0 none, 1 affine, 2 ROTATE_180, 3 ROTATE_90, 4 ROTATE_270), flip, ToTensor,
+ * Normalize of the resized image img [H][W][3]; the mask is sampled from the source mask
+ * [.][mask_w] through the resize(NEAREST) tables xtab[W] / ytab[H] (-1: 0). */
+typedef struct {
+  const uint8_t* img;
+  const uint8_t* mask;
+  const int* xtab;
+  const int* ytab;
+  double m[6];            /* Image.rotate's inverse affine matrix (bilinear image sampling) */
+  int fix[6];             /* the same matrix in 16.16 fixed point, Geometry.c affine_fixed (mask) */
+  int rotate, flip, mask_w, pad;
+} dfcsa_aug_desc;
+/* images fp32 [n][3][H][W], masks fp32 [n][1][H][W]; mean_std: HOST array of 6 floats */
+int dfcsa_aug_finish(const dfcsa_aug_desc* descs_dev, int n, int H, int W, const float* mean_std, int normalize,
+                     float* images, float* masks, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Profiling hook: when enabled for a kernel class, every launch of that class is bracketed by
  * hipEvents on its own stream; dfcsa_prof_read returns the summed elapsed milliseconds and
  * the launch count since the last reset (synchronises on the recorded events).

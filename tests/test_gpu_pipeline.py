@@ -114,3 +114,69 @@ def test_predict_single_image():
     with torch.no_grad():
         want = torch.sigmoid(conv(x.cuda())).cpu().numpy()[0, 0]
     assert got.shape == (40, 56) and np.abs(got - want).max() < 1e-6
+
+
+# --------------------------------------------------------------------- paired transforms
+def _smooth_image(g, H, W):
+    """A natural-looking uint8 image (smooth gradients + noise) so interpolation weights matter."""
+    y, x = np.mgrid[0:H, 0:W].astype(np.float64)
+    base = np.stack([127 + 120 * np.sin(x / 7.0 + c) * np.cos(y / 11.0 - c) for c in range(3)], -1)
+    return np.clip(base + g.normal(0, 12, (H, W, 3)), 0, 255).astype(np.uint8)
+
+
+def test_paired_transform_gpu_bit_exact_with_pillow():
+    """The GPU batch transform equals the reference's Pillow chain (resize BILINEAR / NEAREST,
+    rotate BILINEAR / NEAREST, h-flip, ToTensor, Normalize, mask / 255 > 0.5) bit for bit, on a
+    batch of different source sizes (up- and down-scaling, identity), angles (incl. Pillow's exact
+    0 / 90 / 180 / 270 fast paths) and flips."""
+    from oracle import augment_oracle as A
+    from utils.augment import PairedTransformGPU
+    g = np.random.default_rng(21)
+    sizes = [(300, 400), (100, 150), (224, 224), (500, 223), (37, 1000), (224, 300), (7, 5), (640, 480), (224, 224)]
+    angles = [37.3, -81.25, None, 90.0, -90.0, 180.0, 0.0, -12.5, 44.999]
+    samples = []
+    for i, ((H, W), ang) in enumerate(zip(sizes, angles)):
+        img = _smooth_image(g, H, W)
+        mask = g.choice(np.array([0, 127, 128, 255], dtype=np.uint8), size=(H, W))
+        samples.append({"image": img, "mask": mask, "angle": ang, "flip": bool(i % 2)})
+    for size in ((224, 224), (160, 96)):
+        images, masks = PairedTransformGPU(size)(samples)
+        images, masks = images.cpu().numpy(), masks.cpu().numpy()
+        for i, s in enumerate(samples):
+            x, m = A.reference_transform(s["image"], s["mask"], size, s["angle"], s["flip"])
+            assert np.array_equal(images[i], x), (size, i, np.abs(images[i] - x).max())
+            assert np.array_equal(masks[i], m), (size, i)
+
+
+def test_dataset_gpu_augment_matches_pillow_loader(tmp_path):
+    """DataLoaderFactory with dataset.gpu_augment: same seeds -> the same batches as the reference's
+    Pillow transforms (same np.random draw order, same shuffling), as device tensors."""
+    from PIL import Image
+
+    from utils.data_loader import DataLoaderFactory
+    g = np.random.default_rng(22)
+    for split in ("train", "val"):
+        for sub in ("original", "mask"):
+            (tmp_path / split / sub).mkdir(parents=True)
+        for i, (H, W) in enumerate([(120, 160), (300, 260), (224, 224), (90, 90), (400, 333)]):
+            Image.fromarray(_smooth_image(g, H, W)).save(tmp_path / split / "original" / f"im{i}.png")
+            Image.fromarray((g.random((H, W)) > 0.6).astype(np.uint8) * 255, "L").save(
+                tmp_path / split / "mask" / f"im{i}.png")
+    cfg = {"dataset": {"train_dir": str(tmp_path / "train"), "val_dir": str(tmp_path / "val"), "img_size": [128, 96],
+                       "augmentation": True},
+           "training": {"batch_size": 2, "num_workers": 0}}
+    for loader_name in ("get_train_loader", "get_val_loader"):
+        cpu = getattr(DataLoaderFactory(cfg), loader_name)()
+        gpu = getattr(DataLoaderFactory(dict(cfg, dataset=dict(cfg["dataset"], gpu_augment=True))), loader_name)()
+        assert len(cpu) == len(gpu) == 3
+        for seed in (5, 6):
+            torch.manual_seed(seed)
+            np.random.seed(seed)
+            a = list(cpu)
+            torch.manual_seed(seed)
+            np.random.seed(seed)
+            b = list(gpu)
+            for ba, bb in zip(a, b):
+                assert list(ba["filename"]) == list(bb["filename"])
+                assert bb["image"].is_cuda and bb["mask"].is_cuda
+                assert torch.equal(ba["image"], bb["image"].cpu()) and torch.equal(ba["mask"], bb["mask"].cpu())

@@ -297,3 +297,57 @@ def test_inference_tile_grid_matches_oracle_loop():
         assert [(y, x, th, tw) for y in ys for x in xs] == want
     with pytest.raises(ValueError):
         tile_grid(10, 10, 50, 50)
+
+
+# --------------------------------------------------------------------- paired transforms
+def test_augment_restatement_matches_pillow():
+    """oracle/augment_oracle.py's restatement of Pillow's Resample.c / Geometry.c arithmetic (what the
+    dfcsa_aug_* kernels implement) is bit-exact with Pillow itself (the reference's library)."""
+    from PIL import Image
+
+    from oracle import augment_oracle as A
+    g = np.random.default_rng(0)
+    for (H, W, h, w) in [(300, 400, 224, 224), (100, 150, 224, 224), (224, 224, 224, 224), (500, 223, 224, 224),
+                         (37, 1000, 64, 32), (224, 300, 224, 224), (7, 5, 24, 20)]:
+        img = g.integers(0, 256, (H, W, 3), dtype=np.uint8)
+        ref = np.asarray(Image.fromarray(img).resize((w, h), Image.BILINEAR))
+        mine = A.resize_bilinear(img, w, h)
+        assert np.array_equal(ref, mine), (H, W, h, w)
+        m = (g.random((H, W)) > 0.5).astype(np.uint8) * 255
+        refm = np.array(Image.fromarray(m, "L").resize((w, h), Image.NEAREST))
+        assert np.array_equal(refm, m[A.scale_nearest_tables(H, h)][:, A.scale_nearest_tables(W, w)])
+        for ang in (37.3, -81.25, 12.0001, -0.5, 89.9):
+            M = A.rotate_matrix(ang, w, h)
+            assert np.array_equal(np.asarray(Image.fromarray(ref).rotate(ang, Image.BILINEAR)), A.rotate_bilinear(ref, M))
+            assert np.array_equal(np.array(Image.fromarray(refm, "L").rotate(ang, Image.NEAREST)), A.rotate_nearest(refm, M))
+
+
+def test_augment_host_tables_match_restatement():
+    """The product's host-side tables (utils/augment.py) equal the pinned restatement."""
+    from oracle import augment_oracle as A
+    from utils import augment as G
+    for (i, o) in [(400, 224), (150, 224), (224, 224), (1000, 32), (5, 20), (3, 1)]:
+        b0, k0 = A.resample_coeffs(i, o)
+        b1, k1 = G.resample_coeffs(i, o)
+        assert np.array_equal(b0, b1) and np.array_equal(k0, k1)
+        assert np.array_equal(A.scale_nearest_tables(i, o), G.nearest_table(i, o))
+    for ang in (37.3, -81.25, 0.5):
+        mode, m, fix = G.rotation(ang, 224, 200)
+        assert mode == 1 and m == A.rotate_matrix(ang, 224, 200)
+        assert tuple(fix) == A.rotate_fixed_coeffs(m)
+    assert G.rotation(None, 9, 9)[0] == 0 and G.rotation(-360.0, 9, 9)[0] == 0
+    assert G.rotation(180.0, 9, 7)[0] == 2 and G.rotation(90.0, 9, 9)[0] == 3 and G.rotation(-90.0, 9, 9)[0] == 4
+    assert G.rotation(90.0, 9, 7)[0] == 1  # non-square: Pillow takes the affine path
+
+
+def test_augmentation_draw_order_matches_reference():
+    """draw_augmentation makes the reference's np.random calls in its order (data_loader.py:41-53)."""
+    from utils.augment import draw_augmentation
+    np.random.seed(11)
+    got = [draw_augmentation(True) for _ in range(50)]
+    np.random.seed(11)
+    want = []
+    for _ in range(50):
+        angle = np.random.uniform(-90, 90) if np.random.random() < 0.5 else None
+        want.append((angle, bool(np.random.random() < 0.5)))
+    assert got == want and draw_augmentation(False) == (None, False)
