@@ -38,17 +38,26 @@ def test_ctypes_binding_loads_and_parses_header():
 
 def test_descriptor_layouts_match_c(tmp_path):
     from dfcsa import _lib
+    fields = [("dfcsa_conv_desc", _lib.ConvDesc, ("weight", "Wout")),
+              ("dfcsa_wgrad_desc", _lib.WgradDesc, ("slab", "mchunk")),
+              ("dfcsa_pack_entry", _lib.PackEntry, ("w0", "a")),
+              ("dfcsa_wstd_entry", _lib.WstdEntry, ("K", "pad")),
+              ("dfcsa_resample_desc", _lib.ResampleDesc, ("kk", "row0")),
+              ("dfcsa_aug_desc", _lib.AugDesc, ("m", "fix", "rotate", "mask_w"))]
+    exprs = []
+    want = []
+    for cname, py, names in fields:
+        exprs.append(f"sizeof({cname})")
+        want.append(ctypes.sizeof(py))
+        for n in names:
+            exprs.append(f"offsetof({cname}, {n})")
+            want.append(getattr(py, n).offset)
     src = tmp_path / "lay.c"
-    src.write_text('#include "dfcsa.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){printf("%zu %zu %zu %zu %zu %zu %zu %zu %zu\\n",'
-                   'sizeof(dfcsa_conv_desc), offsetof(dfcsa_conv_desc, weight), offsetof(dfcsa_conv_desc, Wout),'
-                   'sizeof(dfcsa_wgrad_desc), offsetof(dfcsa_wgrad_desc, slab), offsetof(dfcsa_wgrad_desc, mchunk),'
-                   'sizeof(dfcsa_pack_entry), offsetof(dfcsa_pack_entry, w0), offsetof(dfcsa_pack_entry, a));}\n')
+    src.write_text('#include "dfcsa.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(){'
+                   + "".join(f'printf("%zu\\n", (size_t){e});' for e in exprs) + "}\n")
     exe = tmp_path / "lay"
     subprocess.run(["gcc", "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
     got = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
-    want = [ctypes.sizeof(_lib.ConvDesc), _lib.ConvDesc.weight.offset, _lib.ConvDesc.Wout.offset,
-            ctypes.sizeof(_lib.WgradDesc), _lib.WgradDesc.slab.offset, _lib.WgradDesc.mchunk.offset,
-            ctypes.sizeof(_lib.PackEntry), _lib.PackEntry.w0.offset, _lib.PackEntry.a.offset]
     assert got == want
 
 
