@@ -792,7 +792,11 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
     if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (!glds_ok) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
-    if (a.N <= 64) return launch_glds<128, 64, 4, 1, 2>(a, st);
+    // N <= 64 with many rows: 256x64 / 8 waves (wave tile 32x64, twice the rows per B panel);
+    // fewer than one workgroup of 128x128 per CU (the 14^2 level, 28^2 with N <= 256): 128x64 doubles the
+    // workgroup count (gemm_bench: bottleneck dgrad 123 -> 108 us, bottleneck fwd 59 -> 52 us).
+    if (a.N <= 64) return a.M >= 65536 ? launch_glds<256, 64, 8, 1, 2>(a, st) : launch_glds<128, 64, 4, 1, 2>(a, st);
+    if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) return launch_glds<128, 64, 4, 1, 2>(a, st);
     return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
   // fp32 (parity mode + the fp32 LightSelfAttention projections): small problems (M = B*P*P

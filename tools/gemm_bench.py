@@ -14,7 +14,12 @@ SHAPES = [("L1 3x3 fwd up_conv1", 224, 64, 2, 9, 64), ("L1 3x3 dgrad up_conv1", 
           ("L1 1x1 entry+res", 224, 64, 2, 1, 128), ("L1 3x3 down1 (Cin 8)", 224, 8, 1, 9, 64),
           ("L2 3x3 fwd up_conv2", 112, 128, 2, 9, 128), ("L2 3x3 dgrad", 112, 128, 1, 11, 256),
           ("L3 3x3 fwd up_conv3", 56, 256, 2, 9, 256), ("L4 3x3 fwd up_conv4", 28, 512, 2, 9, 512),
-          ("BN 3x3 fwd bottleneck", 14, 512, 1, 9, 1024), ("L4 3x3 dgrad up_conv4", 28, 512, 1, 11, 1024)]
+          ("BN 3x3 fwd bottleneck", 14, 512, 1, 9, 1024), ("L4 3x3 dgrad up_conv4", 28, 512, 1, 11, 1024),
+          ("BN 3x3 dgrad bottleneck", 14, 1024, 1, 11, 512), ("L4 3x3 dgrad down4", 28, 512, 1, 11, 256),
+          ("L2 3x3 dgrad N64", 112, 128, 1, 11, 64)]
+if os.environ.get("GEMM_SHAPES"):
+    keep = os.environ["GEMM_SHAPES"].split(",")
+    SHAPES = [s for s in SHAPES if any(k in s[0] for k in keep)]
 cfgs = [int(c) for c in (sys.argv[1].split(",") if len(sys.argv) > 1 else "1,2,3,4,5,6".split(","))]
 res = []
 for name, H, Cs, nsrc, ntaps, N in SHAPES:
