@@ -34,6 +34,8 @@ enum {
   EW_BWD_ATTN_ENTRY,
   EW_BN_BWD_APPLY,
   EW_CHANNEL_SUM,
+  EW_SUM_OUT,       // ablation blocks: out = a0 (+ a1) + res_scale * a2
+  EW_BWD_SUM_OUT,   // its backward: dres = res_scale * dout, partial sums of dout * res
 };
 
 struct EwArgs {
@@ -97,7 +99,7 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
   float sc[8], sh[8], sc2[8], sh2[8];
   int c0 = (first % cpp) * 8;
   if (fixed) {
-    if (a.a0) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
+    if (a.a0 && a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
     if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
   }
 #pragma unroll 2
@@ -105,7 +107,7 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
     const int m = e / cpp;
     if (!fixed) {
       c0 = (e - m * cpp) * 8;
-      if (a.a0) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
+      if (a.a0 && a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
       if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
     }
     const size_t off = (size_t)m * a.C + c0;
@@ -164,6 +166,20 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f) + rs * r[q];
       store8<T>(O0 + off, out);
+    } else if constexpr (MODE == EW_SUM_OUT) {
+      // reference: fused = local + attn; out = fused + res_scale * res (fusion ablations)
+      float r[8];
+      load8<T>(A2 + off, r);
+      if (a.a1) {
+        float b[8];
+        load8<T>(A1 + off, b);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) y[q] += b[q];
+      }
+      const float rs = *a.scalar;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) out[q] = y[q] + rs * r[q];
+      store8<T>(O0 + off, out);
     }
   }
 }
@@ -173,6 +189,7 @@ template <int MODE> struct NSums { static constexpr int v = 2; };
 template <> struct NSums<EW_BWD_BLOCK_OUT> { static constexpr int v = 3; };
 template <> struct NSums<EW_BN_BWD_APPLY> { static constexpr int v = 1; };
 template <> struct NSums<EW_CHANNEL_SUM> { static constexpr int v = 1; };
+template <> struct NSums<EW_BWD_SUM_OUT> { static constexpr int v = 1; };
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
@@ -222,6 +239,18 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
         load8<T>(A0 + off, x);
 #pragma unroll
         for (int q = 0; q < 8; ++q) acc[0][q] += x[q];
+      } else if constexpr (MODE == EW_BWD_SUM_OUT) {
+        // a0 = dout, a2 = res; o1 = dres (optional)
+        float d[8], r[8], dr[8];
+        load8<T>(A0 + off, d);
+        load8<T>(A2 + off, r);
+        const float rs = *a.scalar;
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          dr[q] = rs * d[q];
+          acc[0][q] += d[q] * r[q];
+        }
+        if (O1) store8<T>(O1 + off, dr);
       } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
         // a0 = dout, a1 = y4, a2 = res; o0 = dz4, o1 = dres
         float d[8], y[8], r[8], dz[8], dr[8];
@@ -585,6 +614,29 @@ extern "C" int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, co
   a.a0 = dout; a.a1 = y4; a.a2 = res; a.sc = sc4; a.sh = sh4; a.mean = mean4; a.invstd = invstd4;
   a.scalar = res_scale; a.o0 = dz4; a.o1 = dres; a.partial = partial;
   return launch_red<EW_BWD_BLOCK_OUT>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_sum_out(int dtype, int M, int C, const void* a, const void* b, const void* res,
+                              const float* res_scale, void* out, void* stream) {
+  if (!a || !res || !res_scale || !out) return DFCSA_EINVAL;
+  EwArgs e = zargs(M, C);
+  e.a0 = a; e.a1 = b; e.a2 = res; e.scalar = res_scale; e.o0 = out;
+  return launch_fwd<EW_SUM_OUT>(dtype, e, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, const void* res, const float* res_scale,
+                                  void* dres, float* partial, void* stream) {
+  if (!dout || !res || !res_scale || !partial) return DFCSA_EINVAL;
+  EwArgs e = zargs(M, C);
+  e.a0 = dout; e.a2 = res; e.scalar = res_scale; e.o1 = dres; e.partial = partial;
+  return launch_red<EW_BWD_SUM_OUT>(dtype, e, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_sum_into(const float* x, int n, float* out, void* stream) {
+  if (!x || !out || n <= 0) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,

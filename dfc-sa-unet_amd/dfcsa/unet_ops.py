@@ -15,23 +15,32 @@ from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
 
 
-def _taps(xs):
+def _taps(xs, k=3):
+    if k == 1:
+        return [(x, 0, 0) for x in xs]
     return [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xs]
 
 
-def _conv3_packs(ps, conv, dtype, Cin_p, C):
-    """Wf [C][Kpad]: forward rows (k = tap*Cin_p + ci); Wt [Cin_p][Kpad(9C)]: dgrad rows,
+def _dgrad_taps(dy, k=3):
+    if k == 1:
+        return [(dy, 0, 0)]
+    return [(dy, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)]
+
+
+def _conv3_packs(ps, conv, dtype, Cin_p, C, k=3):
+    """Wf [C][Kpad]: forward rows (k = tap*Cin_p + ci); Wt [Cin_p][Kpad(ntaps*C)]: dgrad rows,
     Wt[ci][tap*C + co] = Wf[co][tap*Cin_p + ci]."""
-    Wf = ps.rows("Wf", dtype, conv.weight, Cin_p, rup(9 * Cin_p, ops.KALIGN))
-    shape = (Cin_p, rup(9 * C, ops.KALIGN))
-    for tap in range(9):
+    nt = k * k
+    Wf = ps.rows("Wf", dtype, conv.weight, Cin_p, rup(nt * Cin_p, ops.KALIGN))
+    shape = (Cin_p, rup(nt * C, ops.KALIGN))
+    for tap in range(nt):
         ps.transpose(Wf, 0, tap * Cin_p, C, Cin_p, "Wt", shape, dc0=tap * C)
 
 
 class ConvBNReLU(torch.autograd.Function):
     """forward: y = conv(cat(xs)) (+bias, BN partial sums in the GEMM epilogue) -> BN (train: batch
     statistics; eval: running) -> ReLU.  backward: ReLU/BN backward with the per-channel sums,
-    weight gradient GEMM, 3x3 dgrad GEMM split back over the sources."""
+    weight gradient GEMM, dgrad GEMM split back over the sources.  3x3/p1 or 1x1 convs."""
 
     @staticmethod
     def forward(ctx, conv, bn, dtype, nsrc, *args):
@@ -40,17 +49,19 @@ class ConvBNReLU(torch.autograd.Function):
         if any(tuple(x.shape) != (B, H, W, Cs) for x in xs):
             raise ValueError("ConvBNReLU sources must share one NHWC shape")
         Cin_p, C = nsrc * Cs, conv.out_channels
-        if conv.in_channels > Cin_p or C % 8 or conv.kernel_size != (3, 3) or conv.padding != (1, 1) \
-                or conv.stride != (1, 1):
-            raise ValueError(f"ConvBNReLU: 3x3/p1 conv {conv.in_channels}->{C} over {Cin_p} source channels")
+        k = conv.kernel_size[0]
+        if conv.in_channels > Cin_p or C % 8 or conv.kernel_size not in ((3, 3), (1, 1)) \
+                or conv.padding != ((1, 1) if k == 3 else (0, 0)) or conv.stride != (1, 1):
+            raise ValueError(f"ConvBNReLU: 3x3/p1 or 1x1 conv {conv.in_channels}->{C} over {Cin_p} source channels")
         M, dev = B * H * W, xs[0].device
         training = bn.training
-        pk = get_packset(conv, (dtype, nsrc, Cs, param_key(conv)), lambda ps: _conv3_packs(ps, conv, dtype, Cin_p, C))
+        pk = get_packset(conv, (dtype, nsrc, Cs, param_key(conv)),
+                         lambda ps: _conv3_packs(ps, conv, dtype, Cin_p, C, k))
         nt = ops.ntiles_gemm(M)
         st = torch.empty(nt * 2 * C, device=dev, dtype=torch.float32) if training else None
         y = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-        ops.conv_gemm(dtype, _taps(xs), Cs, (B, H, W), (H, W), pk["Wf"], rup(9 * Cin_p, ops.KALIGN), C, [y], C,
-                      bias=conv.bias, stats=st)
+        ops.conv_gemm(dtype, _taps(xs, k), Cs, (B, H, W), (H, W), pk["Wf"], rup(k * k * Cin_p, ops.KALIGN), C, [y],
+                      C, bias=conv.bias, stats=st)
         bnst = ops.bn_finalize(bn, conv.bias, st, nt, C, C, M, training)
         out = ops.bn_act(dtype, y, bnst, 1)
         ctx.conv, ctx.bn, ctx.dtype, ctx.nsrc, ctx.np = conv, bn, dtype, nsrc, len(args) - nsrc
@@ -73,14 +84,15 @@ class ConvBNReLU(torch.autograd.Function):
                               grad_of(conv.bias) if conv.bias is not None else None)
         del dz
         grid, hw = (B, H, W), (H, W)
-        ops.conv_wgrad_into(dtype, [dy], C, _taps(xs), Cs, grid, hw, [grad_of(conv.weight)], 9, ctx.nsrc * Cs,
+        k = conv.kernel_size[0]
+        ops.conv_wgrad_into(dtype, [dy], C, _taps(xs, k), Cs, grid, hw, [grad_of(conv.weight)], k * k, ctx.nsrc * Cs,
                             conv.in_channels)
         notify_grads_ready(conv)
         dxs = [None] * ctx.nsrc
         if any(ctx.needs_input_grad[4:4 + ctx.nsrc]):
-            segs = [(dy, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)]
             dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=y.device) for _ in range(ctx.nsrc)]
-            ops.conv_gemm(dtype, segs, C, grid, hw, ctx.pk["Wt"], rup(9 * C, ops.KALIGN), ctx.nsrc * Cs, dxs, Cs)
+            ops.conv_gemm(dtype, _dgrad_taps(dy, k), C, grid, hw, ctx.pk["Wt"], rup(k * k * C, ops.KALIGN),
+                          ctx.nsrc * Cs, dxs, Cs)
         ctx.xs = ctx.y = None
         return (None, None, None, None, *dxs, *([None] * ctx.np))
 

@@ -8,9 +8,11 @@ reference, so unchanged yamls still run): ``model.precision`` / ``training.preci
 ('bf16' default, 'fp32').
 
 Built on the MI355X path: 'DFC-SA-Res-Block' (UNetDFCSARes, the north-star model), 'UNet'
-(config 1, model_factory.py:94-100), 'UNet_FullResAttention' (config 5, :174-175) and
-'TransformerUNet'/'TransUNet' (config 4, :113-137).  The other names the reference knows (the other
-ablation models, the ViT) raise NotImplementedError naming what is missing.
+(config 1, model_factory.py:94-100), 'UNet_FullResAttention' (config 5, :174-175),
+'TransformerUNet'/'TransUNet' (config 4, :113-137) and the ablation zoo (:162-187: UNet_Baseline,
+UNet_AttentionOnly, UNet_AdditionFusion, UNet_ConcatFusion, UNet_EncoderOnlyDFC,
+UNet_DecoderOnlyDFC, UNet_BothStandardConv, with the reference's argument lists).  The plain ViT
+('VisionTransformerSegmentation') raises NotImplementedError.
 
 Pretrained weights are loaded with torch.load(weights_only=True) (a state_dict needs nothing
 else); as in the reference a failure is reported and not raised.
@@ -20,14 +22,18 @@ import torch
 from models.transformer_unet import TransUNet, get_r50_b16_config
 from models.unet import UNet
 from models.unet_dfc_sa_ablation_attention import UNet_FullResAttention
+from models.unet_dfc_sa_ablation_branches import UNet_AttentionOnly, UNet_Baseline
+from models.unet_dfc_sa_ablation_fusion import UNet_AdditionFusion, UNet_ConcatFusion
+from models.unet_dfc_sa_ablation_placement import UNet_BothStandardConv, UNet_DecoderOnlyDFC, UNet_EncoderOnlyDFC
 from models.unet_dfc_sa_res import UNetDFCSARes
 
-_BUILT = ("DFC-SA-Res-Block", "UNet", "UNet_FullResAttention", "TransformerUNet", "TransUNet")
-_REFERENCE_ONLY = {
-    "VisionTransformerSegmentation", "UNet_Baseline",
-    "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
-    "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv",
-}
+# reference :160-187 -- (class, takes pool_size)
+_ZOO = {"UNet_Baseline": (UNet_Baseline, False), "UNet_AttentionOnly": (UNet_AttentionOnly, True),
+        "UNet_AdditionFusion": (UNet_AdditionFusion, True), "UNet_ConcatFusion": (UNet_ConcatFusion, True),
+        "UNet_EncoderOnlyDFC": (UNet_EncoderOnlyDFC, True), "UNet_DecoderOnlyDFC": (UNet_DecoderOnlyDFC, True),
+        "UNet_BothStandardConv": (UNet_BothStandardConv, False)}
+_BUILT = ("DFC-SA-Res-Block", "UNet", "UNet_FullResAttention", "TransformerUNet", "TransUNet", *_ZOO)
+_REFERENCE_ONLY = {"VisionTransformerSegmentation"}
 
 
 class ModelFactory:
@@ -81,6 +87,11 @@ class ModelFactory:
                 print(f"注意：官方版 TransUNet 預設處理3通道輸入。您的 in_channels={in_channels}，模型會將單通道複製為3通道。")
             vit_config.patches.grid = (img_size // 16, img_size // 16)
             return TransUNet(config=vit_config, img_size=img_size, num_classes=out_channels, precision=precision)
+        if name in _ZOO:
+            cls, takes_pool = _ZOO[name]
+            if takes_pool:
+                return cls(in_channels, out_channels, features, pool_size, precision=precision)
+            return cls(in_channels, out_channels, features, precision=precision)
         if name in _REFERENCE_ONLY:
             raise NotImplementedError(
                 f"model {name!r} exists in the reference but is not built on the MI355X path yet "

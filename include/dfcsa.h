@@ -460,6 +460,18 @@ int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, const void*
                     const float* dlogits, void* dx, float* partial_w, float* partial_b, void* stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Ablation-zoo block outputs (reference unet_dfc_sa_ablation_branches.py:62-70, :93-101,
+ * unet_dfc_sa_ablation_fusion.py:35-49, :86-100): out = a (+ b) + res_scale * res; backward:
+ * dres = res_scale * dout (dres may be NULL), partial [ntiles][C] of dout * res (ntiles =
+ * dfcsa_ew_ntiles(M, C)); dfcsa_sum_into: *out += sum of x[0..n).
+ * ---------------------------------------------------------------------------------------- */
+int dfcsa_sum_out(int dtype, int M, int C, const void* a, const void* b, const void* res, const float* res_scale,
+                  void* out, void* stream);
+int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, const void* res, const float* res_scale, void* dres,
+                      float* partial, void* stream);
+int dfcsa_sum_into(const float* x, int n, float* out, void* stream);
+
+/* ------------------------------------------------------------------------------------------
  * Sliding-window inference (reference inference.py:104-153 predict_large_image, :73-91
  * calculate_segmentation_metrics).  Tiles are th x tw; the grid is ys[ny] x xs[nx] with tile
  * t = iy*nx + ix (the reference's y-major loop order).

@@ -16,6 +16,8 @@ Reference files imported (file-by-file, via importlib, because the reference's p
                                 :29-92, UNet_FullResAttention :95-97 (config 5; imported under a stub
                                 package because it uses a package-relative import of
                                 unet_dfc_sa_ablation_branches.py)
+  * models/unet_dfc_sa_ablation_branches.py / _fusion.py / _placement.py   the ablation zoo (seven
+                                models; imported under the stub package like the attention ablation)
   * inference.py                calculate_segmentation_metrics :73-91, predict_large_image :104-153
                                 (those two functions only, taken from the source with ast: the module
                                 imports cv2 / matplotlib / torchvision, which are not installed)
@@ -489,6 +491,56 @@ def _n_classes_1(cfg):
 
 
 # ----------------------------------------------------------------------------------------
+# (9) The ablation model zoo (unet_dfc_sa_ablation_branches.py, _fusion.py, _placement.py): every
+#     model at features 8..64, pool 4, 32x32 input, one train-mode forward + backward, fp32 and
+#     the float64 re-run (grad64.* / noise.*), like fullres_model.npz.
+# ----------------------------------------------------------------------------------------
+ZOO = ("UNet_Baseline", "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion", "UNet_EncoderOnlyDFC",
+       "UNet_DecoderOnlyDFC", "UNet_BothStandardConv")
+
+
+def _zoo_model(name):
+    mods = {"UNet_Baseline": "unet_dfc_sa_ablation_branches", "UNet_AttentionOnly": "unet_dfc_sa_ablation_branches",
+            "UNet_AdditionFusion": "unet_dfc_sa_ablation_fusion", "UNet_ConcatFusion": "unet_dfc_sa_ablation_fusion",
+            "UNet_EncoderOnlyDFC": "unet_dfc_sa_ablation_placement",
+            "UNet_DecoderOnlyDFC": "unet_dfc_sa_ablation_placement",
+            "UNet_BothStandardConv": "unet_dfc_sa_ablation_placement"}
+    cls = getattr(_load_models_pkg(mods[name]), name)
+    if name in ("UNet_Baseline", "UNet_BothStandardConv"):   # model_factory.py:162-187 argument lists
+        return cls(3, 1, [8, 16, 32, 64])
+    return cls(3, 1, [8, 16, 32, 64], 4)
+
+
+def gen_zoo():
+    for i, name in enumerate(ZOO):
+        torch.manual_seed(9100 + i)
+        model = _zoo_model(name)
+        perturb_gammas(model)
+        sd0 = sd_arrays(model, "sd0.")
+        model.train()
+        m64 = fp64_twin(model)
+        gen = torch.Generator().manual_seed(9200 + i)
+        x, t = batch(gen, (2, 3, 32, 32))
+        out = model(x)
+        met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
+        met["loss"].backward()
+        met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", LOSS_PARAMS)
+        met64["loss"].backward()
+        bufs = {"buf." + k: v.detach().numpy().copy() for k, v in model.state_dict().items() if "running" in k}
+        save(f"zoo_{name}.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+             iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), **sd0, **bufs, **grad_arrays(model),
+             **fp64_noise(model, m64), **grad_arrays(m64, "grad64."), nparams_full=np.int64(sum(p.numel() for p in _zoo_full(name).parameters())))
+
+
+def _zoo_full(name):
+    m = _zoo_model(name)
+    cls = type(m)
+    if name in ("UNet_Baseline", "UNet_BothStandardConv"):
+        return cls(3, 1, [64, 128, 256, 512])
+    return cls(3, 1, [64, 128, 256, 512], 8)
+
+
+# ----------------------------------------------------------------------------------------
 # Sliding-window inference (inference.py:73-153).  The module itself imports cv2, matplotlib
 # and torchvision, none of which is installed here, so only the two functions under test are
 # taken from its source (ast) and run with the reference's own code.  torchvision's ToTensor /
@@ -559,7 +611,7 @@ def gen_inference():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference"]
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference", "zoo"]
     for w in which:
         globals()["gen_" + w]()
     print("torch", torch.__version__)

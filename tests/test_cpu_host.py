@@ -110,7 +110,7 @@ def test_model_factory_contract():
     with pytest.raises(ValueError):
         ModelFactory.get_model({"model": {"name": "NoSuchModel"}, "training": {}})
     with pytest.raises(NotImplementedError):
-        ModelFactory.get_model({"model": {"name": "UNet_ConcatFusion"}, "training": {}})
+        ModelFactory.get_model({"model": {"name": "VisionTransformerSegmentation"}, "training": {}})
     # config_transunet.yaml: 'TransformerUNet', img_size from the dataset section (:113-137)
     tu = ModelFactory.get_model({"model": {"name": "TransformerUNet", "in_channels": 3, "out_channels": 1},
                                  "dataset": {"img_size": [224, 224]}, "training": {}})
@@ -119,6 +119,22 @@ def test_model_factory_contract():
     # defaults (model_factory.py:87-91): pool 8, qk ratio 8, features 64..512
     d = ModelFactory.get_model({"model": {"name": "DFC-SA-Res-Block"}, "training": {}})
     assert d.pool_size == 8 and d.down1.attn_branch[3].query_conv.out_channels == 8
+
+
+def test_ablation_zoo_state_dicts_match_reference(golden):
+    """Every ablation model (model_factory.py:160-187) builds with the reference's module tree:
+    state_dict keys and shapes of the fixture (features 8..64) and the full-size parameter count."""
+    from models.model_factory import ModelFactory
+    for name in ("UNet_Baseline", "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
+                 "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv"):
+        fx = golden(f"zoo_{name}.npz")
+        m = ModelFactory.get_model({"model": {"name": name, "features": [8, 16, 32, 64], "pool_size": 4},
+                                    "training": {}})
+        ref = {k[4:]: fx[k].shape for k in fx if k.startswith("sd0.")}
+        got = {k: tuple(v.shape) for k, v in m.state_dict().items()}
+        assert got == ref, name
+        full = ModelFactory.get_model({"model": {"name": name}, "training": {}})
+        assert sum(p.numel() for p in full.parameters()) == int(fx["nparams_full"]), name
 
 
 def test_pretrained_failure_is_reported_not_raised(tmp_path, capsys):
