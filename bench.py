@@ -42,6 +42,11 @@ MODELS = {
     "unet": dict(name="UNet", label="UNet (config 1)", gflop={64: 18.05}),
     "transunet": dict(name="TransformerUNet", label="TransUNet R50-ViT-B/16 (config 4)", gflop={224: 174.94}),
     "fullres": dict(name="UNet_FullResAttention", label="UNet_FullResAttention (config 5)", gflop={}),
+    # the ablation zoo (configs/config_ablation{1,2,4}_*.yaml): reported, not the headline
+    **{k: dict(name=n, label=n, gflop={}) for k, n in (
+        ("baseline", "UNet_Baseline"), ("attn_only", "UNet_AttentionOnly"), ("addition", "UNet_AdditionFusion"),
+        ("concat", "UNet_ConcatFusion"), ("encoder_only", "UNet_EncoderOnlyDFC"),
+        ("decoder_only", "UNet_DecoderOnlyDFC"), ("both_standard", "UNet_BothStandardConv"))},
 }
 
 
