@@ -178,6 +178,7 @@ __global__ void __launch_bounds__(256) gn_stats_kernel(int HW, int C, int S, con
   for (int q = 0; q < 8; ++q) acc[0][q] = acc[1][q] = 0.f;
   if (active) {
     const T* yb = y + (size_t)b * HW * C + ck * 8;
+#pragma unroll 4
     for (int p = p0 + lane_px; p < p1; p += pl) {
       float v[8];
       load8<T>(yb + (size_t)p * C, v);
@@ -280,6 +281,7 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_kernel(int HW, int C, int G
   }
   if (active) {
     const size_t base = (size_t)b * HW * C + ck * 8;
+#pragma unroll 4
     for (int p = p0 + lane_px; p < p1; p += pl) {
       const size_t off = base + (size_t)p * C;
       float d[8], v[8];
@@ -1208,7 +1210,18 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(int64_t M, int C, c
   if (c0 >= C) return;
   const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t r = r0; r < r1; ++r) {
+  int64_t r = r0;
+  // 8 rows' loads in flight per thread; the adds keep the sequential row order (same result)
+  for (; r + 7 < r1; r += 8) {
+    float v[8][8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) load8<T>(x + (r + u) * C + c0, v[u]);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += v[u][q];
+  }
+  for (; r < r1; ++r) {
     float v[8];
     load8<T>(x + r * C + c0, v);
 #pragma unroll
