@@ -259,34 +259,52 @@ def main():
     roof = None
     if not args.no_kernel_timing:
         import ctypes
-        classes = ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad)", "conv_gemm"),
-                   (2, "conv_wgrad (weight-gradient GEMM)", "conv_wgrad"),
-                   (3, "fra (full-resolution attention fwd/bwd, bf16 MFMA)", "fra"))
-        for c, _, _ in classes:
+        # kernel classes (bound, unit of the "flops" slot): the tile GEMMs are MFMA-bound; the 1x1
+        # streaming GEMMs are HBM-bound and report algorithmic bytes
+        classes = ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad, LDS-DMA tiles)", "conv_gemm", "mfma"),
+                   (2, "conv_wgrad (weight-gradient GEMM)", "conv_wgrad", "mfma"),
+                   (3, "fra (full-resolution attention fwd/bwd, bf16 MFMA)", "fra", "mfma"),
+                   (4, "conv1x1_stream (1x1 conv GEMMs, K <= 256, HBM-streaming)", "conv1x1_stream", "hbm"))
+        for c, _, _, _ in classes:
             L.LIB.dfcsa_prof_enable(c, 1)
         for _ in range(args.steps):
             step()
         torch.cuda.synchronize()
         cls = {}
-        for c, name, key in classes:
+        for c, name, key, bound in classes:
             ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
             L.LIB.dfcsa_prof_read(c, ctypes.addressof(ms), ctypes.addressof(n), ctypes.addressof(fl))
             if n.value:
-                cls[c] = (name, ms.value, n.value, fl.value, key)
+                cls[c] = (name, ms.value, n.value, fl.value, key, bound)
             L.LIB.dfcsa_prof_enable(c, 0)
+
+        def rate(v):
+            """(achieved, peak, unit) of a class: TFLOP/s against the dense MFMA peak, or GB/s
+            against HBM."""
+            _, ms_, _, units, _, bound_ = v
+            if bound_ == "hbm":
+                return (units / (ms_ * 1e-3) / 1e9 if ms_ > 0 else 0.0), HBM_PEAK_GBS, "GB/s"
+            pk = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
+            return (units / (ms_ * 1e-3) / 1e12 if ms_ > 0 else 0.0), pk, "TFLOP/s"
+
         dom = max(cls.values(), key=lambda v: v[1])
-        name, ms, n, fl, dom_key = dom
-        peak = MFMA_BF16_PEAK_TFLOPS if args.precision == "bf16" else MFMA_F32_PEAK_TFLOPS
-        ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
+        name, ms, n, fl, dom_key, bound = dom
+        ach, peak, unit = rate(dom)
         traffic, tsrc = pmc_traffic(dom_key) if headline else (None, None)   # PMC passes cover the headline
-        roof = {"bound": "mfma", "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": "TFLOP/s",
+        roof = {"bound": bound, "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": unit,
                 "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc,
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "ms_per_step": round(ms / args.steps, 3), "share_of_step": round(ms / (el * 1e3), 3),
-                "other_class": {c[0]: {"ms_per_step": round(c[1] / args.steps, 3),
-                                       "tflops": round(c[3] / (c[1] * 1e-3) / 1e12, 2) if c[1] > 0 else 0}
-                                for c in cls.values() if c is not dom}}
+                "other_class": {}}
+        for v in cls.values():
+            if v is dom:
+                continue
+            a_, p_, u_ = rate(v)
+            tr_, _ = pmc_traffic(v[4]) if headline else (None, None)
+            roof["other_class"][v[0]] = {"bound": v[5], "ms_per_step": round(v[1] / args.steps, 3),
+                                         "achieved": round(a_, 2), "unit": u_, "frac": round(a_ / p_, 4),
+                                         "avg_launch_ms": round(v[1] / max(v[2], 1), 4), "traffic": tr_}
 
     vdice = None
     if rank == 0 and world == 1 and not args.no_val_dice and headline:

@@ -715,17 +715,21 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
 }
 
 // the streaming kernel serves 1x1 (no shift, stride 1, plain store) bf16 GEMMs with K <= 256
+bool stream_applies(const ConvGemmArgs& a) {
+  if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return false;
+  for (int i = 0; i < a.nseg; ++i)
+    if (a.seg[i].dh || a.seg[i].dw) return false;
+  return a.Ho == a.Hi && a.Wo == a.Wi;
+}
+
 int try_stream(const ConvGemmArgs& a, hipStream_t st) {
   if (g_debug < 0) g_debug = getenv("DFCSA_DEBUG") ? 1 : 0;
-  if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return 1;
   // measured (tools/stream_bench.py, B=16 shapes): since the streaming loop keeps its stores in
   // flight (fixed per-lane store counts, LDS-only barriers, hoisted argument-table reads) it is
   // at least as fast as the tile kernels on every 1x1 shape it serves (L1 N=64 K=128: 52 vs 77 us,
   // 3 destinations K=64: 96 vs 181 us), so it takes all of them
   (void)g_stream_force;
-  for (int i = 0; i < a.nseg; ++i)
-    if (a.seg[i].dh || a.seg[i].dw) return 1;
-  if (a.Ho != a.Hi || a.Wo != a.Wi) return 1;
+  if (!stream_applies(a)) return 1;
   // per-wave columns: register budget NWC/16 * KP/32 <= 16 fragments
   const int kp = a.Kpad;
   auto pick = [&](int nwc) {
@@ -831,7 +835,13 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
   hipStream_t st = (hipStream_t)stream;
-  ProfScope prof(DFCSA_PROF_CONV_GEMM, st, 2.0 * a.M * a.N * a.K);
+  // profiling classes: the 1x1 streaming GEMMs are HBM-bound (their unit is bytes: A and the
+  // weight panel read once, the output written once, read too when accumulating); the tile
+  // kernels are MFMA-bound (2*M*N*K flop)
+  const bool streamed = d->dtype == DFCSA_DT_BF16 && g_conv_cfg != 7 && g_conv_cfg < 1 && stream_applies(a);
+  const double sbytes = 2.0 * ((double)a.M * a.Kpad + (double)a.N * a.Kpad + (double)a.M * a.N * (a.accumulate ? 2 : 1));
+  ProfScope prof(streamed ? DFCSA_PROF_CONV_STREAM : DFCSA_PROF_CONV_GEMM, st,
+                 streamed ? sbytes : 2.0 * a.M * a.N * a.K);
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
 }
 

@@ -532,6 +532,7 @@ int dfcsa_aug_finish(const dfcsa_aug_desc* descs_dev, int n, int H, int W, const
 #define DFCSA_PROF_CONV_GEMM 1
 #define DFCSA_PROF_WGRAD 2
 #define DFCSA_PROF_ATTN 3
+#define DFCSA_PROF_CONV_STREAM 4   /* 1x1 streaming GEMMs; the "flops" slot carries algorithmic bytes */
 int dfcsa_prof_enable(int kernel_class, int enable);
 int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, double* flops);
 

@@ -53,8 +53,9 @@ def _per_dispatch(db, counter):
     return out
 
 
-CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel", "conv1x1_stream_kernel"),
-           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<")}
+CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<"),
+           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<"),
+           "conv1x1_stream": ("conv1x1_stream_kernel",)}
 
 
 def traffic(fdb, wdb, out, pattern="conv_gemm"):
@@ -82,7 +83,7 @@ def traffic(fdb, wdb, out, pattern="conv_gemm"):
            "per_kernel": {n: {"launches": k["launches_fetch"],
                               "read_MB_per_launch": k["read_bytes"] / max(k["launches_fetch"], 1) / 1e6,
                               "write_MB_per_launch": k["write_bytes"] / max(k["launches_write"], 1) / 1e6}
-                          for n, k in sorted(per_kernel.items(), key=lambda kv: -kv[1]["read_bytes"])}}
+                          for n, k in sorted(sel.items(), key=lambda kv: -kv[1]["read_bytes"])}}
     return res
 
 
