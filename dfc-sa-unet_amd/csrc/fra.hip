@@ -826,7 +826,8 @@ bool mfma_fwd_ok(int dtype, int C, int Cq, int ldq) {
          (Cq == 8 || Cq == 16 || Cq == 32 || Cq == 64 || Cq == 128);
 }
 bool mfma_bwd_ok(int dtype, int C, int Cq, int ldq) {
-  return dtype == DFCSA_DT_BF16 && (C == 64 || C == 128) && ldq % 8 == 0 && (Cq == 8 || Cq == 16 || Cq == 32);
+  return dtype == DFCSA_DT_BF16 && (C == 64 || C == 128 || C == 256) && ldq % 8 == 0 &&
+         (Cq == 8 || Cq == 16 || Cq == 32);
 }
 
 template <int CQ, int DV>
@@ -862,7 +863,8 @@ template <int CQ>
 void launch_bwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* dy, const float* gamma,
                    const float* lse, const float* rr, void* dqkv, hipStream_t st) {
   if (C == 64) launch_bwd<CQ, 64>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
-  else launch_bwd<CQ, 128>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
+  else if (C == 128) launch_bwd<CQ, 128>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
+  else launch_bwd<CQ, 256>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
 }
 
 }  // namespace

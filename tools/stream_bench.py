@@ -14,6 +14,10 @@ SHAPES = [(224, 64, 3, 64, 1, False), (224, 64, 2, 64, 1, False), (112, 128, 2, 
           (224, 64, 2, 64, 1, False), (224, 64, 2, 128, 2, False), (224, 8, 1, 128, 2, False),
           (112, 128, 1, 256, 2, False), (112, 128, 3, 128, 1, False), (112, 128, 1, 384, 3, False),
           (112, 128, 2, 128, 1, False)]
+if os.environ.get("STREAM_H"):
+    SHAPES = [s for s in SHAPES if s[0] == int(os.environ["STREAM_H"])]
+if os.environ.get("STREAM_NOSTATS"):
+    SHAPES = [s[:5] + (s[5],) for s in SHAPES]
 variants = [("tile", 7, 0)] + [(f"stream{w}", 0, w) for w in (0, 2, 3)] + [("force0", -1, 0), ("force2", -1, 2)]
 for H, Cs, nsrc, N, nd, acc in SHAPES:
     M = B * H * H
@@ -31,7 +35,7 @@ for H, Cs, nsrc, N, nd, acc in SHAPES:
         LIB.dfcsa_set_tuning(5, 1 if knob1 < 0 else 0)
         LIB.dfcsa_set_tuning(3, wgs)
         run = lambda: ops.conv_gemm(bf, segs, Cs, (B, H, H), (H, H), w, Kp, N, dests, C, accumulate=acc,
-                                    stats=None if acc else stats)
+                                    stats=None if (acc or os.environ.get("STREAM_NOSTATS")) else stats)
         for _ in range(3):
             run()
         torch.cuda.synchronize()
