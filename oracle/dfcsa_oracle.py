@@ -26,6 +26,9 @@ Reference functions restated (file:line under the reference checkout):
   * UNet.forward (DoubleConv, Down, Up, OutConv)  models/unet.py:6-101        -> unet
   * TransUNet.forward (StdConv2d, PreActBottleneck, ResNetV2, Attention, Mlp, Block, Embeddings,
     Encoder, DecoderCup, SegmentationHead)    models/transformer_unet.py:21-368 -> transunet
+  * the ablation zoo: LocalOnlyBlock / AttentionOnlyBlock (unet_dfc_sa_ablation_branches.py:62-101),
+    AdditionFusionBlock / ConcatFusionBlock (unet_dfc_sa_ablation_fusion.py:35-100), placement models
+    (unet_dfc_sa_ablation_placement.py:85-284)          -> *_block, unet_dfc_sa_res(zoo=name)
 """
 import math
 
@@ -115,15 +118,73 @@ def dfc_block(x, sd, name, pool_size, training, bufs, full_res=False):
     return out + sd[name + ".res_scale"] * res
 
 
+def _residual(x, sd, name):
+    if (name + ".residual_conv.weight") in sd:
+        return conv(x, sd, name + ".residual_conv", bias=False)
+    return x
+
+
+def _local_branch(x, sd, name, training, bufs):
+    return F.relu(batch_norm(conv(x, sd, name + ".conv_branch.0", padding=1), sd, name + ".conv_branch.1",
+                             training, bufs))
+
+
+def _attn_branch(x, sd, name, pool_size, training, bufs):
+    a = F.relu(batch_norm(conv(x, sd, name + ".attn_branch.0"), sd, name + ".attn_branch.1", training, bufs))
+    return light_self_attention(a, sd, name + ".attn_branch.3", pool_size)
+
+
+def local_only_block(x, sd, name, pool_size, training, bufs):
+    """models/unet_dfc_sa_ablation_branches.py:93-101 (LocalOnlyBlock.forward)."""
+    return _local_branch(x, sd, name, training, bufs) + sd[name + ".res_scale"] * _residual(x, sd, name)
+
+
+def attention_only_block(x, sd, name, pool_size, training, bufs):
+    """models/unet_dfc_sa_ablation_branches.py:62-70 (AttentionOnlyBlock.forward)."""
+    return _attn_branch(x, sd, name, pool_size, training, bufs) + sd[name + ".res_scale"] * _residual(x, sd, name)
+
+
+def addition_fusion_block(x, sd, name, pool_size, training, bufs):
+    """models/unet_dfc_sa_ablation_fusion.py:35-49 (AdditionFusionBlock.forward)."""
+    fused = _local_branch(x, sd, name, training, bufs) + _attn_branch(x, sd, name, pool_size, training, bufs)
+    return fused + sd[name + ".res_scale"] * _residual(x, sd, name)
+
+
+def concat_fusion_block(x, sd, name, pool_size, training, bufs):
+    """models/unet_dfc_sa_ablation_fusion.py:86-100 (ConcatFusionBlock.forward)."""
+    comb = torch.cat([_local_branch(x, sd, name, training, bufs),
+                      _attn_branch(x, sd, name, pool_size, training, bufs)], dim=1)
+    fused = F.relu(batch_norm(conv(comb, sd, name + ".fusion_conv.0"), sd, name + ".fusion_conv.1", training, bufs))
+    return fused + sd[name + ".res_scale"] * _residual(x, sd, name)
+
+
+def _zoo_blocks(model):
+    """(encoder/bottleneck block, decoder block) of the ablation models (model_factory.py:160-187;
+    placement: unet_dfc_sa_ablation_placement.py:85-284)."""
+    dfc = lambda x, sd, n, p, tr, b: dfc_block(x, sd, n, p, tr, b)  # noqa: E731
+    return {"UNet_Baseline": (local_only_block, local_only_block),
+            "UNet_AttentionOnly": (attention_only_block, attention_only_block),
+            "UNet_AdditionFusion": (addition_fusion_block, addition_fusion_block),
+            "UNet_ConcatFusion": (concat_fusion_block, concat_fusion_block),
+            "UNet_EncoderOnlyDFC": (dfc, local_only_block),
+            "UNet_DecoderOnlyDFC": (local_only_block, dfc),
+            "UNet_BothStandardConv": (local_only_block, local_only_block)}[model]
+
+
 def conv_transpose2x2(x, sd, name):
     return F.conv_transpose2d(x, sd[name + ".weight"], sd[name + ".bias"], stride=2)
 
 
-def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None, full_res=False):
+def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None, full_res=False, zoo=None):
     """models/unet_dfc_sa_res.py:161-204 (UNetDFCSA.forward; UNetDFCSARes adds nothing).  With
     full_res: UNet_FullResAttention (AblationUNetBase.forward, unet_dfc_sa_ablation_branches.py:
-    129-164, the same graph with FullResAttnDFCBlock blocks)."""
-    blk = lambda t, n: dfc_block(t, sd, n, pool_size, training, bufs, full_res)  # noqa: E731
+    129-164, the same graph with FullResAttnDFCBlock blocks).  With zoo = an ablation model name:
+    the same graph with that model's blocks (encoder + bottleneck, decoder)."""
+    if zoo:
+        enc, dec = _zoo_blocks(zoo)
+        blk = lambda t, n: (enc if not n.startswith("up_conv") else dec)(t, sd, n, pool_size, training, bufs)  # noqa
+    else:
+        blk = lambda t, n: dfc_block(t, sd, n, pool_size, training, bufs, full_res)  # noqa: E731
     d1 = blk(x, "down1")
     d2 = blk(F.max_pool2d(d1, 2, 2), "down2")
     d3 = blk(F.max_pool2d(d2, 2, 2), "down3")
@@ -290,7 +351,8 @@ def param_names(sd):
 def forward_backward(sd, x, t, pool_size, loss_params=None, model="dfc", heads=12):
     """fwd -> sigmoid -> calculate_metrics -> backward.  Returns (logits, metrics, grads,
     updated BN buffers).  model: 'dfc' (UNetDFCSARes), 'fullres' (UNet_FullResAttention), 'unet',
-    'transunet' (TransUNet with `heads` attention heads)."""
+    'transunet' (TransUNet with `heads` attention heads), or an ablation-zoo model name
+    ('UNet_Baseline', ...)."""
     params = {k: (v.detach().clone().requires_grad_(True) if k in set(param_names(sd)) else v)
               for k, v in sd.items()}
     bufs = {}
@@ -298,6 +360,8 @@ def forward_backward(sd, x, t, pool_size, loss_params=None, model="dfc", heads=1
         logits = unet(x, params, training=True, bufs=bufs)
     elif model == "transunet":
         logits = transunet(x, params, heads, training=True, bufs=bufs)
+    elif model.startswith("UNet_"):
+        logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs, zoo=model)
     else:
         logits = unet_dfc_sa_res(x, params, pool_size, training=True, bufs=bufs, full_res=(model == "fullres"))
     met = calculate_metrics(torch.sigmoid(logits), t, "bce_dice", loss_params)

@@ -351,3 +351,22 @@ def test_augmentation_draw_order_matches_reference():
         angle = np.random.uniform(-90, 90) if np.random.random() < 0.5 else None
         want.append((angle, bool(np.random.random() < 0.5)))
     assert got == want and draw_augmentation(False) == (None, False)
+
+
+@pytest.mark.parametrize("name", ["UNet_Baseline", "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
+                                  "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv"])
+def test_zoo_oracle_matches_reference(golden, name):
+    """oracle.unet_dfc_sa_res(zoo=name) restates the seven ablation models: logits, loss and every
+    gradient of the reference's own run (tests/golden/zoo_*.npz)."""
+    fx = golden(f"zoo_{name}.npz")
+    sd = {k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd0.")}
+    x, t = torch.from_numpy(fx["x"]), torch.from_numpy(fx["t"])
+    logits, met, grads, _ = O.forward_backward(sd, x, t, 4, {"bce_weight": 0.5, "dice_weight": 0.5}, model=name)
+    assert ((logits - torch.from_numpy(fx["logits"])).norm() / torch.from_numpy(fx["logits"]).norm()).item() < 1e-5
+    assert abs(met["loss"].item() - float(fx["loss"])) < 1e-5 * abs(float(fx["loss"]))
+    for n, g in grads.items():
+        ref = fx.get("grad." + n)
+        if ref is None:
+            continue
+        ref = torch.from_numpy(ref)
+        assert ((g - ref).norm() / (ref.norm() + 1e-12)).item() < 1e-4 or (g - ref).abs().max().item() < 1e-7, n
