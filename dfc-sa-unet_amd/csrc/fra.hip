@@ -827,7 +827,7 @@ bool mfma_fwd_ok(int dtype, int C, int Cq, int ldq) {
 }
 bool mfma_bwd_ok(int dtype, int C, int Cq, int ldq) {
   return dtype == DFCSA_DT_BF16 && (C == 64 || C == 128 || C == 256) && ldq % 8 == 0 &&
-         (Cq == 8 || Cq == 16 || Cq == 32);
+         (Cq == 8 || Cq == 16 || Cq == 32 || (Cq == 64 && C == 64));
 }
 
 template <int CQ, int DV>
@@ -930,7 +930,8 @@ extern "C" int dfcsa_fra_bwd(int dtype, int B, int N, int C, int Cq, int ldq, co
     switch (Cq) {
       case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
       case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
-      default: launch_bwd_cq<32>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
+      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
+      default: launch_bwd<64, 64>(B, N, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;   // ViT heads
     }
   } else {
     dim3 grid((N + 3) / 4, B);

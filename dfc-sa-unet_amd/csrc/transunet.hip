@@ -1230,6 +1230,37 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(int64_t M, int C, c
   st8f(partial + (size_t)blockIdx.y * C + c0, acc);
 }
 
+// ------------------------------------------------------------ head-major relayout (bf16)
+// Token-major [B*N][ld] (ld = nparts * heads * dh; part p of head h at columns p*D + h*dh) <->
+// head-major [heads*B][N][nparts*dh] (the layout of the flash-attention kernels of fra.hip, one
+// "image" per (head, batch)).  Part 0 is multiplied by scale0 (the 1/sqrt(dh) of the scores folded
+// into q; a power of two for dh = 4^k, so exact).  One thread per 8-element chunk.
+__global__ void __launch_bounds__(256) heads_relayout_kernel(int unpack, int B, int N, int heads, int dh, int nparts,
+                                                             float scale0, const bf16_t* __restrict__ src,
+                                                             bf16_t* __restrict__ dst) {
+  const int D = heads * dh, ld = nparts * D, cpr = ld / 8;   // 8-element chunks per token row
+  const int64_t total = (int64_t)B * N * cpr;
+  for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t m = e / cpr;
+    const int col = (int)(e - m * cpr) * 8;
+    const int p = col / D, rem = col - p * D, h = rem / dh, j = rem - h * dh;
+    const int b = (int)(m / N), n = (int)(m - (int64_t)b * N);
+    const int64_t tok = m * ld + col;
+    const int64_t hm = ((int64_t)(h * B + b) * N + n) * (nparts * dh) + p * dh + j;
+    const bf16_t* s8 = src + (unpack ? hm : tok);
+    bf16_t* d8 = dst + (unpack ? tok : hm);
+    if (p == 0 && scale0 != 1.0f) {
+      float v[8];
+      load8<bf16_t>(s8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= scale0;
+      store8<bf16_t>(d8, v);
+    } else {
+      *(uint4*)d8 = *(const uint4*)s8;
+    }
+  }
+}
+
 // ------------------------------------------------------------ attention launch helpers
 template <typename T, int DH>
 int mha_launch(int B, int N, int heads, int ldq, float scale, const void* qkv, const void* ctx, const void* dctx,
@@ -1530,6 +1561,16 @@ extern "C" int dfcsa_batch_sum(int dtype, int B, int64_t L, const void* x, float
 extern "C" int dfcsa_rng_advance(int64_t* state, void* stream) {
   if (!state) return DFCSA_EINVAL;
   hipLaunchKernelGGL(rng_advance_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, state);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_heads_relayout(int unpack, int B, int N, int heads, int dh, int nparts, float scale0,
+                                    const void* src, void* dst, void* stream) {
+  if (B <= 0 || N <= 0 || heads <= 0 || dh <= 0 || dh % 8 || nparts <= 0 || !src || !dst) return DFCSA_EINVAL;
+  const int64_t chunks = (int64_t)B * N * nparts * heads * dh / 8;
+  hipLaunchKernelGGL(heads_relayout_kernel, dim3(grid_for(chunks)), dim3(256), 0, (hipStream_t)stream, unpack, B, N,
+                     heads, dh, nparts, scale0, (const bf16_t*)src, (bf16_t*)dst);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -20,6 +20,7 @@ are mapped through the standardisation by one table launch at the end of the bac
 root stem is the last node autograd runs).  The ViT residual stream is fp32 in every precision.
 """
 import math
+import os
 
 import torch
 
@@ -422,6 +423,53 @@ def _vit_packs(ps, blk, dtype, D, F):
     _linear_packs(ps, mlp.fc2.weight, dtype, "W2")
 
 
+FLASH_MHA = os.environ.get("DFCSA_MHA_FLASH", "1") != "0"
+
+
+def _flash_mha(dtype, dh):
+    """bf16 heads of width 64 run on the MFMA flash-attention kernels (fwd and bwd)."""
+    return (FLASH_MHA and dtype == torch.bfloat16 and dh == 64
+            and LIB.dfcsa_fra_path(_lib.DT_BF16, dh, dh, 3 * dh, 0) == 1
+            and LIB.dfcsa_fra_path(_lib.DT_BF16, dh, dh, 3 * dh, 1) == 1)
+
+
+def mha_flash_forward(dtype, qkv, B, N, heads, dh):
+    """Attention core (transformer_unet.py:146-154) of token-major qkv [B*N][3*heads*dh] on the bf16
+    MFMA flash kernels of fra.hip: a head-major copy of q|k|v with q pre-scaled by 1/sqrt(dh),
+    gamma = 1 and x = 0 (so their output is softmax(q k^T) v).  Returns (ctx [B*N][heads*dh], saved)."""
+    dev = qkv.device
+    Bh, scale = heads * B, 1.0 / math.sqrt(dh)
+    qkv_h = torch.empty((Bh, N, 3 * dh), dtype=dtype, device=dev)
+    call("dfcsa_heads_relayout", 0, B, N, heads, dh, 3, float(scale), P(qkv), P(qkv_h), stream())
+    o_h = torch.empty((Bh, N, dh), dtype=dtype, device=dev)
+    y_h = torch.empty_like(o_h)
+    one = torch.ones(1, device=dev)
+    lse = _f32((Bh * N,), dev)
+    call("dfcsa_fra_fwd", dt(dtype), Bh, N, dh, dh, 3 * dh, P(qkv_h), P(torch.zeros_like(o_h)), P(one), P(o_h),
+         P(y_h), P(lse), stream())
+    del y_h
+    cx = torch.empty((B * N, heads * dh), dtype=dtype, device=dev)
+    call("dfcsa_heads_relayout", 1, B, N, heads, dh, 1, 1.0, P(o_h), P(cx), stream())
+    return cx, (qkv_h, o_h, one, lse)
+
+
+def mha_flash_backward(dtype, saved, dcx, B, N, heads, dh):
+    """d(qkv) [B*N][3*heads*dh] from d(ctx) (the dQ and dK/dV flash kernels; dq rescaled)."""
+    qkv_h, o_h, one, lse = saved
+    dev = o_h.device
+    Bh, scale = heads * B, 1.0 / math.sqrt(dh)
+    dcx_h = torch.empty_like(o_h)
+    call("dfcsa_heads_relayout", 0, B, N, heads, dh, 1, 1.0, P(dcx.contiguous()), P(dcx_h), stream())
+    rvec = _f32((Bh * N,), dev)
+    call("dfcsa_fra_bwd_prep", dt(dtype), Bh * N, dh, P(dcx_h), P(o_h), P(rvec), stream())
+    dqkv_h = torch.empty_like(qkv_h)
+    call("dfcsa_fra_bwd", dt(dtype), Bh, N, dh, dh, 3 * dh, P(qkv_h), P(dcx_h), P(one), P(lse), P(rvec), P(dqkv_h),
+         stream())
+    dqkv = torch.empty((B * N, 3 * heads * dh), dtype=dtype, device=dev)
+    call("dfcsa_heads_relayout", 1, B, N, heads, dh, 3, float(scale), P(dqkv_h), P(dqkv), stream())
+    return dqkv
+
+
 class ViTBlock(torch.autograd.Function):
     """Block.forward (:211-220) with Attention (:137-157) and Mlp (:167-173):
       y1 = LN1(h); qkv = y1 [Wq|Wk|Wv]^T + b (one GEMM); ctx = MHA(qkv); h1 = drop(ctx Wo^T + bo) + h
@@ -442,10 +490,16 @@ class ViTBlock(torch.autograd.Function):
         y1, mr1 = _ln_forward(dtype, h, blk.attention_norm, (B, gh, gw, D))
         qkv = _gemm_1x1(dtype, y1, pk["Wqkv"], KD, 3 * D, torch.empty((B, gh, gw, 3 * D), dtype=dtype, device=dev),
                         bias=pk["bqkv"])
-        cx = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
-        lse = _f32((B * heads * N,), dev)
         scale = 1.0 / math.sqrt(dh)
-        call("dfcsa_mha_fwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(lse), stream())
+        flash = None
+        if _flash_mha(dtype, dh):
+            cx, flash = mha_flash_forward(dtype, qkv, B, N, heads, dh)
+            cx = cx.view(B, gh, gw, D)
+            lse = None
+        else:
+            cx = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
+            lse = _f32((B * heads * N,), dev)
+            call("dfcsa_mha_fwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(lse), stream())
         a = _gemm_1x1(dtype, cx, pk["Wo"], KD, D, torch.empty((B, gh, gw, D), dtype=dtype, device=dev),
                       bias=att.out.bias)
         h1 = _f32((B, gh, gw, D), dev)
@@ -465,6 +519,7 @@ class ViTBlock(torch.autograd.Function):
         ctx.blk, ctx.dtype, ctx.pk, ctx.np = blk, dtype, pk, len(params)
         ctx.cfg = (p, p_attn, rng, site, heads, dh, scale, F)
         ctx.t = (h, y1, mr1, qkv, cx, lse, h1, y2, mr2, f, g)
+        ctx.flash = flash
         return out
 
     @staticmethod
@@ -500,10 +555,14 @@ class ViTBlock(torch.autograd.Function):
         bias_grad_into(dtype, da, att.out.bias)
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
-        dqkv = torch.empty_like(qkv)
-        dvec = _f32((B * heads * N,), dev)
-        call("dfcsa_mha_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(dcx), P(lse), P(dvec),
-             P(dqkv), stream())
+        if ctx.flash is not None:
+            dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh).view_as(qkv)
+            ctx.flash = None
+        else:
+            dqkv = torch.empty_like(qkv)
+            dvec = _f32((B * heads * N,), dev)
+            call("dfcsa_mha_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(dcx), P(lse), P(dvec),
+                 P(dqkv), stream())
         del dcx
         ops.conv_wgrad_into(dtype, [dqkv], 3 * D, [(y1, 0, 0)], D, grid, hw,
                             [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],

@@ -435,6 +435,12 @@ int dfcsa_rng_advance(int64_t* state, void* stream);
 /* Multi-head self-attention core (Attention.forward :137-157): qkv [B*N][ldq] = [q | k | v] of
  * heads*dh columns each; ctx [B*N][heads*dh] = softmax(q k^T * scale) v per head; lse [B][heads][N].
  * bwd: dqkv [B*N][ldq] (q, k, v columns written), dvec [B][heads][N] scratch. dh in {16, 32, 64}. */
+/* bf16 relayout between token-major [B*N][nparts*heads*dh] (part p, head h at columns
+ * p*heads*dh + h*dh) and head-major [heads*B][N][nparts*dh]; unpack = 0: token -> head-major.
+ * Part 0 is multiplied by scale0.  Lets the bf16 MFMA flash-attention kernels (dfcsa_fra_*,
+ * gamma = 1, x = 0) run the ViT's multi-head attention with q pre-scaled by 1/sqrt(dh). */
+int dfcsa_heads_relayout(int unpack, int B, int N, int heads, int dh, int nparts, float scale0, const void* src,
+                         void* dst, void* stream);
 int dfcsa_mha_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv, void* ctx,
                   float* lse, void* stream);
 int dfcsa_mha_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,

@@ -121,6 +121,27 @@ def test_mha_fwd_bwd(B, N, heads, dh, dtype, tol):
         assert rel(dqkv[..., i * D:(i + 1) * D], dqr[..., i * D:(i + 1) * D]) < 3 * tol, i
 
 
+@pytest.mark.parametrize("B,N,heads", [(2, 196, 12), (1, 130, 2), (3, 4, 2)])
+def test_mha_flash_bf16(B, N, heads):
+    """bf16 ViT attention on the MFMA flash kernels (head-major relayout, q pre-scaled): against the
+    plain PyTorch fp32 attention of the same bf16 inputs, bf16 tolerances."""
+    from dfcsa.transunet_ops import mha_flash_backward, mha_flash_forward
+    torch.manual_seed(N + heads + B)
+    dh = 64
+    D = heads * dh
+    qkv = (torch.randn(B, N, 3 * D, device="cuda") * 1.5).to(torch.bfloat16)
+    qr = qkv.float().clone().requires_grad_(True)
+    yr = _mha_torch(qr, B, N, heads, dh)
+    g = torch.randn_like(yr)
+    dqr = torch.autograd.grad(yr, qr, g)[0]
+    cx, saved = mha_flash_forward(torch.bfloat16, qkv.view(B * N, 3 * D), B, N, heads, dh)
+    assert rel(cx.view(B, N, D), yr) < 1e-2
+    dqkv = mha_flash_backward(torch.bfloat16, saved, g.to(torch.bfloat16).view(B * N, D), B, N, heads, dh)
+    dqkv = dqkv.view(B, N, 3 * D)
+    for i in range(3):
+        assert rel(dqkv[..., i * D:(i + 1) * D], dqr[..., i * D:(i + 1) * D]) < 3e-2, i
+
+
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("H,W", [(112, 112), (7, 9), (2, 3)])
 def test_maxpool3s2(H, W, dtype):
