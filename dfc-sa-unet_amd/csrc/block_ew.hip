@@ -508,17 +508,32 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restric
   dst[(size_t)g * rowlen + j] = (s0 + s1) + (s2 + s3);
 }
 
-__global__ void __launch_bounds__(256) sum_scalar_kernel(const float* x, int n, float* out) {
-  __shared__ double r[256];
-  double s = 0;
-  for (int i = threadIdx.x; i < n; i += 256) s += x[i];
-  r[threadIdx.x] = s;
+// one workgroup, fixed summation order; 4 independent loads in flight per thread for the long
+// (per-pixel) vectors of the attention gammas (NT = 1024 there, 256 for per-channel vectors)
+template <int NT>
+__global__ void __launch_bounds__(NT) sum_scalar_kernel(const float* x, int n, float* out) {
+  __shared__ double r[NT];
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int i = threadIdx.x;
+  for (; i + 3 * NT < n; i += 4 * NT) {
+    s0 += x[i];
+    s1 += x[i + NT];
+    s2 += x[i + 2 * NT];
+    s3 += x[i + 3 * NT];
+  }
+  for (; i < n; i += NT) s0 += x[i];
+  r[threadIdx.x] = (s0 + s1) + (s2 + s3);
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
+  for (int o = NT / 2; o > 0; o >>= 1) {
     if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
     __syncthreads();
   }
   if (threadIdx.x == 0) *out += (float)r[0];
+}
+
+void launch_sum_scalar(const float* x, int n, float* out, hipStream_t st) {
+  if (n > 4096) hipLaunchKernelGGL(sum_scalar_kernel<1024>, dim3(1), dim3(1024), 0, st, x, n, out);
+  else hipLaunchKernelGGL(sum_scalar_kernel<256>, dim3(1), dim3(256), 0, st, x, n, out);
 }
 
 // pixels per reduction tile: ~16 chunk-iterations per thread (fewer, fuller tiles than a fixed size)
@@ -634,7 +649,7 @@ extern "C" int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, cons
 
 extern "C" int dfcsa_sum_into(const float* x, int n, float* out, void* stream) {
   if (!x || !out || n <= 0) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  launch_sum_scalar(x, n, out, (hipStream_t)stream);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -679,7 +694,7 @@ extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum,
                      count, coef, dgamma, dbeta, third);
   DFCSA_CHECK_LAUNCH();
   if (third) {
-    hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, st, third, C, extra);
+    launch_sum_scalar(third, C, extra, st);
     DFCSA_CHECK_LAUNCH();
   }
   return 0;
@@ -729,7 +744,7 @@ extern "C" int dfcsa_rows_reduce(const float* src, int T, int rowlen, float* dst
 
 extern "C" int dfcsa_sum_to_scalar(const float* x, int n, float* out, void* stream) {
   if (n <= 0) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(sum_scalar_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, x, n, out);
+  launch_sum_scalar(x, n, out, (hipStream_t)stream);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

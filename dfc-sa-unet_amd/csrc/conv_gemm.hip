@@ -857,5 +857,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 7) { g_wgrad_noglds = value; return 0; }
   if (knob == 8) { g_wgrad_narrow = value; return 0; }
   if (knob == 9) { g_fra_generic = value; return 0; }
+  if (knob == 10) { g_fra_occ = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -49,3 +49,4 @@ extern int g_wgrad_waves;
 extern int g_wgrad_noglds;
 extern int g_wgrad_narrow;
 extern int g_fra_generic;
+extern int g_fra_occ;

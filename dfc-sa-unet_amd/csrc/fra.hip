@@ -29,6 +29,7 @@
 #include "dfcsa_internal.h"
 
 int g_fra_generic = 0;  // tuning knob 9: force the generic kernels (coverage tests)
+int g_fra_occ = 15;     // tuning knob 10: waves-per-SIMD budgets of the narrow MFMA kernels
 
 namespace {
 
@@ -378,8 +379,9 @@ __device__ __forceinline__ void zero_pad_cols(char* smem, int tile_bytes, int ro
 // ---------------------------------------------------------------------------- forward
 // Workgroup: 4 waves x QB 16-query blocks; value columns [c0, c0 + DV) of grid.y; KT = 64 keys
 // per LDS tile (double-buffered, register-staged).  grid (ceil(N / (64 QB)), C/DV, B).
-template <int CQ, int DV, int QB>
-__global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
+template <int CQ, int DV, int QB, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
                                                     const bf16_t* __restrict__ x, const float* __restrict__ gamma,
                                                     bf16_t* __restrict__ o, bf16_t* __restrict__ y,
                                                     float* __restrict__ lse) {
@@ -402,15 +404,18 @@ __global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const
     const int q = qw0 + 16 * qb + li;
     qk_load_global<CQ>(qf[qb], base + (size_t)q * ldq, q < N, g);
   }
-  f32x4_t acc[QB][NCB];
-  float m[QB], l[QB];
+  // acc[qb][NCB] is the softmax denominator: a block of all-ones value columns, so the MFMA forms
+  // the row sum of the (bf16) P it multiplies, already reduced over the query's 4 lane groups
+  f32x4_t acc[QB][NCB + 1];
+  float m[QB];
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
     m[qb] = -INFINITY;
-    l[qb] = 0.f;
 #pragma unroll
-    for (int cb = 0; cb < NCB; ++cb) acc[qb][cb] = zero4();
+    for (int cb = 0; cb <= NCB; ++cb) acc[qb][cb] = zero4();
   }
+  const short one = (short)0x3f80;  // bf16 1.0
+  const bf16x8_t ones = {one, one, one, one, one, one, one, one};
 
   Stage<KT, CQ / 8> sk;
   Stage<KT, DV / 8> sv;
@@ -468,25 +473,18 @@ __global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const
       for (int qb = 0; qb < QB; ++qb) {
         const float mn = fmaxf(m[qb], mx[qb]);
         const float alpha = (m[qb] == -INFINITY) ? 0.f : exp2_((m[qb] - mn) * kL2E);
-        l[qb] *= alpha;
 #pragma unroll
-        for (int cb = 0; cb < NCB; ++cb) acc[qb][cb] *= alpha;
+        for (int cb = 0; cb <= NCB; ++cb) acc[qb][cb] *= alpha;
         m[qb] = mn;
       }
     }
 #pragma unroll
     for (int qb = 0; qb < QB; ++qb) {
       const float nm = -m[qb] * kL2E;
-      float ls = 0.f;
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float p = exp2_(fmaf(st[ks][qb][r], kL2E, nm));
-          st[ks][qb][r] = p;
-          ls += p;
-        }
-      l[qb] += ls;
+        for (int r = 0; r < 4; ++r) st[ks][qb][r] = exp2_(fmaf(st[ks][qb][r], kL2E, nm));
     }
     // O^T[c][q] += V^T[c][key] P^T[key][q], 32 keys per MFMA
 #pragma unroll
@@ -500,6 +498,8 @@ __global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const
 #pragma unroll
         for (int qb = 0; qb < QB; ++qb) acc[qb][cb] = mfma32(vf, pb[qb], acc[qb][cb]);
       }
+#pragma unroll
+      for (int qb = 0; qb < QB; ++qb) acc[qb][NCB] = mfma32(ones, pb[qb], acc[qb][NCB]);
     }
     if (t + 1 < ntiles) {
       char* nk = smem + ((t + 1) & 1) * (KB + VB);
@@ -512,9 +512,7 @@ __global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const
   const float gm = *gamma;
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
-    float lt = l[qb];
-    lt += __shfl_xor(lt, 16, 64);
-    lt += __shfl_xor(lt, 32, 64);
+    const float lt = acc[qb][NCB][0];
     const int q = qw0 + 16 * qb + li;
     if (q >= N) continue;
     const float inv = 1.f / lt;
@@ -538,10 +536,13 @@ __global__ void __launch_bounds__(256) fra_fwd_mfma(int N, int C, int ldq, const
 // ---------------------------------------------------------------------------- backward, dK/dV
 // Workgroup: 4 waves x 32 keys (two 16-key blocks per wave, K and V rows held in registers);
 // sweeps all queries in LDS tiles of QT = 64 (Q rows, dy rows, lse, r).  grid (ceil(N/128), 1, B).
-//   S[q][k] = Q K^T, dPy[q][k] = dy V^T, P = exp(S - lse_q), dS = gamma P (dPy - r_q)
-//   dV^T[c][k] += dy^T[c][q] P[q][k] (x gamma at the end),  dK^T[d][k] += Q^T[d][q] dS[q][k]
-template <int CQ, int C>
-__global__ void __launch_bounds__(256) fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
+//   S[q][k] = Q K^T, dPy'[q][k] = dy V^T - r_q (the MFMA chain starts from -r_q), P = exp(S - lse_q),
+//   dS/gamma = P dPy';  dV^T[c][k] += dy^T[c][q] P[q][k], dK^T[d][k] += Q^T[d][q] (dS/gamma)[q][k],
+//   both scaled by gamma at the end.  Query rows past N stage Q = dy = 0 and lse = r = 0, so their
+//   P = 1 and dPy' = 0 contribute exactly nothing: no per-score masking.
+template <int CQ, int C, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                         const float* __restrict__ lse, const float* __restrict__ rr,
                                                         bf16_t* __restrict__ dqkv) {
@@ -590,8 +591,8 @@ __global__ void __launch_bounds__(256) fra_bwd_dkv_mfma(int N, int ldq, const bf
     float* ls = (float*)(img + QBy + DBy);
     if (tid < QT) {
       const int q = qt0 + tid;
-      ls[tid] = q < N ? lseb[q] : 0.f;
-      ls[QT + tid] = q < N ? rrb[q] : 0.f;
+      ls[tid] = q < N ? lseb[q] * kL2E : 0.f;
+      ls[QT + tid] = q < N ? -rrb[q] : 0.f;
     }
   };
   const int ntiles = (N + QT - 1) / QT;
@@ -620,30 +621,29 @@ __global__ void __launch_bounds__(256) fra_bwd_dkv_mfma(int N, int ldq, const bf
       bf16x8_t da[NDC];
 #pragma unroll
       for (int dc = 0; dc < NDC; ++dc) da[dc] = lds_row8<C>(Di, qs * 16 + li, 32 * dc + 8 * g);
+      const float4 R4 = *(const float4*)(Ls + QT + qs * 16 + 4 * g);  // -r of rows 16 qs + 4g + r
+      const f32x4_t nr = {R4.x, R4.y, R4.z, R4.w};
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
         sp[qs][kb] = qk_mfma<CQ>(qa, kf[kb], zero4());
-        f32x4_t a = zero4();
+        f32x4_t a = nr;
 #pragma unroll
         for (int dc = 0; dc < NDC; ++dc) a = mfma32(da[dc], vf[kb][dc], a);
         dp[qs][kb] = a;
       }
     }
-    // P and dS (rows = queries 16 qs + 4g + r)
+    // P and dS / gamma (rows = queries 16 qs + 4g + r)
 #pragma unroll
     for (int qs = 0; qs < 4; ++qs) {
-      const float4 L4 = *(const float4*)(Ls + qs * 16 + 4 * g);
-      const float4 R4 = *(const float4*)(Ls + QT + qs * 16 + 4 * g);
-      const float Lr[4] = {L4.x * kL2E, L4.y * kL2E, L4.z * kL2E, L4.w * kL2E};
-      const float Rr[4] = {R4.x, R4.y, R4.z, R4.w};
+      const float4 L4 = *(const float4*)(Ls + qs * 16 + 4 * g);  // lse * log2(e)
+      const float Lr[4] = {L4.x, L4.y, L4.z, L4.w};
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const bool ok = qt0 + qs * 16 + 4 * g + r < N;
 #pragma unroll
         for (int kb = 0; kb < 2; ++kb) {
-          const float p = ok ? exp2_(fmaf(sp[qs][kb][r], kL2E, -Lr[r])) : 0.f;
+          const float p = exp2_(fmaf(sp[qs][kb][r], kL2E, -Lr[r]));
           sp[qs][kb][r] = p;
-          dp[qs][kb][r] = gm * p * (dp[qs][kb][r] - Rr[r]);
+          dp[qs][kb][r] *= p;
         }
       }
     }
@@ -689,9 +689,10 @@ __global__ void __launch_bounds__(256) fra_bwd_dkv_mfma(int N, int ldq, const bf
 #pragma unroll
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
-      if (d < CQ)
-        *(uint2*)(out + CQ + d) = make_uint2(pack2bf(dka[kb][db][0], dka[kb][db][1]),
-                                             pack2bf(dka[kb][db][2], dka[kb][db][3]));
+      if (d < CQ) {
+        const f32x4_t v = dka[kb][db] * gm;
+        *(uint2*)(out + CQ + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
     }
   }
 }
@@ -699,9 +700,12 @@ __global__ void __launch_bounds__(256) fra_bwd_dkv_mfma(int N, int ldq, const bf
 // ---------------------------------------------------------------------------- backward, dQ
 // Workgroup: 4 waves x 32 queries (Q and dy rows in registers); sweeps all keys in LDS tiles of
 // KT = 64 (K rows, V rows).  grid (ceil(N/128), 1, B).
-//   S^T = K Q^T, dPy^T = V dy^T, dS^T = gamma P^T (dPy^T - r_q), dQ^T[d][q] += K^T[d][k] dS^T[k][q]
-template <int CQ, int C>
-__global__ void __launch_bounds__(256) fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
+//   S^T = K Q^T, dPy'^T = V dy^T - r_q (the MFMA chain starts from -r_q), dS^T / gamma = P^T dPy'^T,
+//   dQ^T[d][q] += K^T[d][k] (dS / gamma)^T[k][q], scaled by gamma at the end.  Keys past N are
+//   masked on the last tile only (tile-uniform branch).
+template <int CQ, int C, int WPE>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
+fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
                                                        const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                        const float* __restrict__ lse, const float* __restrict__ rr,
                                                        bf16_t* __restrict__ dqkv) {
@@ -720,7 +724,8 @@ __global__ void __launch_bounds__(256) fra_bwd_dq_mfma(int N, int ldq, const bf1
   zero_pad_cols<CQ, KC>(smem, TB, KT, tid);
   QKFrag<CQ> qf[2];
   bf16x8_t df[2][NDC];
-  float Lq[2], Rq[2];
+  float Lq[2];
+  f32x4_t nR[2];
 #pragma unroll
   for (int qb = 0; qb < 2; ++qb) {
     const int q = qw0 + 16 * qb + li;
@@ -730,7 +735,8 @@ __global__ void __launch_bounds__(256) fra_bwd_dq_mfma(int N, int ldq, const bf1
     for (int dc = 0; dc < NDC; ++dc)
       df[qb][dc] = ok ? *(const bf16x8_t*)(dyb + (size_t)q * C + 32 * dc + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     Lq[qb] = ok ? -lse[(size_t)b * N + q] * kL2E : 0.f;
-    Rq[qb] = ok ? rr[(size_t)b * N + q] : 0.f;
+    const float nr = ok ? -rr[(size_t)b * N + q] : 0.f;
+    nR[qb] = f32x4_t{nr, nr, nr, nr};
   }
   f32x4_t dqa[2][NDB];
 #pragma unroll
@@ -767,17 +773,22 @@ __global__ void __launch_bounds__(256) fra_bwd_dq_mfma(int N, int ldq, const bf1
 #pragma unroll
       for (int qb = 0; qb < 2; ++qb) {
         const f32x4_t s = qk_mfma<CQ>(ka, qf[qb], zero4());
-        f32x4_t d = zero4();
+        f32x4_t d = nR[qb];
 #pragma unroll
         for (int dc = 0; dc < NDC; ++dc) d = mfma32(va[dc], df[qb][dc], d);
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const bool ok = kt0 + ks * 16 + 4 * g + r < N;
-          const float p = exp2_(fmaf(s[r], kL2E, Lq[qb]));
-          d[r] = ok ? gm * p * (d[r] - Rq[qb]) : 0.f;
-        }
+        for (int r = 0; r < 4; ++r) d[r] *= exp2_(fmaf(s[r], kL2E, Lq[qb]));
         ds[ks][qb] = d;
       }
+    }
+    if (kt0 + KT > N) {
+#pragma unroll
+      for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (kt0 + ks * 16 + 4 * g + r >= N)
+#pragma unroll
+            for (int qb = 0; qb < 2; ++qb) ds[ks][qb][r] = 0.f;
     }
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -806,14 +817,20 @@ __global__ void __launch_bounds__(256) fra_bwd_dq_mfma(int N, int ldq, const bf1
 #pragma unroll
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
-      if (d < CQ)
-        *(uint2*)(out + d) = make_uint2(pack2bf(dqa[qb][db][0], dqa[qb][db][1]),
-                                        pack2bf(dqa[qb][db][2], dqa[qb][db][3]));
+      if (d < CQ) {
+        const f32x4_t v = dqa[qb][db] * gm;
+        *(uint2*)(out + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      }
     }
   }
 }
 
 // ---------------------------------------------------------------------------- dispatch
+// Waves-per-SIMD budgets of the C = 64 / 128 MFMA kernels (tuning knob 10): bit 0 forward (3 / 2
+// waves), bit 1 dK/dV (3 / 2), bit 2 dQ (4 / 3), bit 3 forward at 4 waves for C = 64; 0 leaves the
+// compiler's default budget (kept for A/B measurements).  Default 15: all on.
+int fra_occ_tuned() { return g_fra_occ; }
+
 int fwd_dv(int C) {
   if (C == 64 || C == 128 || C == 256) return C;
   if (C % 256 == 0) return 256;
@@ -830,13 +847,28 @@ bool mfma_bwd_ok(int dtype, int C, int Cq, int ldq) {
          (Cq == 8 || Cq == 16 || Cq == 32 || (Cq == 64 && C == 64));
 }
 
+template <int CQ, int DV, int QB, int WPE>
+void launch_fwd_w(dim3 grid, int N, int C, int ldq, const void* qkv, const void* x, const float* gamma, void* o,
+                  void* y, float* lse, hipStream_t st) {
+  hipLaunchKernelGGL((fra_fwd_mfma<CQ, DV, QB, WPE>), grid, dim3(256), 0, st, N, C, ldq, (const bf16_t*)qkv,
+                     (const bf16_t*)x, gamma, (bf16_t*)o, (bf16_t*)y, lse);
+}
+
 template <int CQ, int DV>
 void launch_fwd(int B, int N, int C, int ldq, const void* qkv, const void* x, const float* gamma, void* o, void* y,
                 float* lse, hipStream_t st) {
   constexpr int QB = DV <= 128 ? 2 : 1;
   dim3 grid((N + 64 * QB - 1) / (64 * QB), C / DV, B);
-  hipLaunchKernelGGL((fra_fwd_mfma<CQ, DV, QB>), grid, dim3(256), 0, st, N, C, ldq, (const bf16_t*)qkv,
-                     (const bf16_t*)x, gamma, (bf16_t*)o, (bf16_t*)y, lse);
+  // waves-per-SIMD budgets (knob 10): without one the compiler sizes these kernels for 1-2 waves
+  const int occ = fra_occ_tuned();
+  if constexpr (DV == 64 && CQ <= 16) {
+    if (occ & 8) return launch_fwd_w<CQ, DV, QB, 4>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 3>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+  }
+  if constexpr (DV == 128 && CQ <= 16) {
+    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 2>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+  }
+  launch_fwd_w<CQ, DV, QB, 1>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
 }
 
 template <int CQ>
@@ -853,10 +885,21 @@ template <int CQ, int C>
 void launch_bwd(int B, int N, int ldq, const void* qkv, const void* dy, const float* gamma, const float* lse,
                 const float* rr, void* dqkv, hipStream_t st) {
   dim3 grid((N + 127) / 128, 1, B);
-  hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
-                     (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
-  hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
-                     (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+  const int occ = fra_occ_tuned();
+  constexpr bool narrow = CQ <= 16 && (C == 64 || C == 128);
+  constexpr int WKV = C == 64 ? 3 : 2, WQ = C == 64 ? 4 : 3;
+  if (narrow && (occ & 2))
+    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, narrow ? WKV : 1>), grid, dim3(256), 0, st, N, ldq,
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+  else
+    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+  if (narrow && (occ & 4))
+    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq,
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+  else
+    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
 }
 
 template <int CQ>
