@@ -407,7 +407,19 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(
   const int c = blockIdx.x * 64 + cl;
   double s = 0.0, q = 0.0;
   if (training && c < C) {
-    for (int t = part; t < ntiles; t += 16) {
+    // 8 tiles' loads in flight per step; the additions keep the sequential tile order
+    int t = part;
+    for (; t + 7 * 16 < ntiles; t += 8 * 16) {
+      float vs[8], vq[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        vs[j] = stats[(size_t)(t + 16 * j) * 2 * ld + c];
+        vq[j] = stats[(size_t)(t + 16 * j) * 2 * ld + ld + c];
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) { s += (double)vs[j]; q += (double)vq[j]; }
+    }
+    for (; t < ntiles; t += 16) {
       s += (double)stats[(size_t)t * 2 * ld + c];
       q += (double)stats[(size_t)t * 2 * ld + ld + c];
     }
@@ -452,7 +464,24 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   const int c = blockIdx.x * 64 + cl;
   double s0 = 0, s1 = 0, s2 = 0;
   if (c < C) {
-    for (int t = part; t < ntiles; t += 16) {
+    int t = part;
+    for (; t + 7 * 16 < ntiles; t += 8 * 16) {  // 8 tiles' loads in flight, sequential order kept
+      float v0[8], v1[8], v2[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const float* p = partial + (size_t)(t + 16 * j) * nsum * C + c;
+        v0[j] = p[0];
+        v1[j] = p[C];
+        v2[j] = nsum > 2 ? p[2 * C] : 0.f;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s0 += v0[j];
+        s1 += v1[j];
+        if (nsum > 2) s2 += v2[j];
+      }
+    }
+    for (; t < ntiles; t += 16) {
       const float* p = partial + (size_t)t * nsum * C + c;
       s0 += p[0];
       s1 += p[C];
@@ -478,8 +507,17 @@ __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restri
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double s = 0;
-  if (c < C)
-    for (int t = part; t < ntiles; t += 16) s += slab[(size_t)t * C + c];
+  if (c < C) {
+    int t = part;
+    for (; t + 7 * 16 < ntiles; t += 8 * 16) {  // 8 loads in flight, sequential order kept
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = slab[(size_t)(t + 16 * j) * C + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) s += v[j];
+    }
+    for (; t < ntiles; t += 16) s += slab[(size_t)t * C + c];
+  }
   r[part][cl] = s;
   __syncthreads();
   if (part == 0 && c < C) {
@@ -498,6 +536,13 @@ __global__ void __launch_bounds__(256) rows_reduce_kernel(const float* __restric
   const int t0 = g * per, t1 = min(T, t0 + per);
   float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
   int t = t0;
+  for (; t + 7 < t1; t += 8) {  // 8 rows in flight; same accumulation order as the 4-row step
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = src[(size_t)(t + k) * rowlen + j];
+    s0 += v[0]; s1 += v[1]; s2 += v[2]; s3 += v[3];
+    s0 += v[4]; s1 += v[5]; s2 += v[6]; s3 += v[7];
+  }
   for (; t + 3 < t1; t += 4) {
     s0 += src[(size_t)t * rowlen + j];
     s1 += src[(size_t)(t + 1) * rowlen + j];
