@@ -25,6 +25,8 @@
 //    max grows by more than 2^8).
 //  * generic (fp32 or bf16 storage, any C/Cq): one wave per row, fp32 VALU, exact online
 //    softmax; the fp32 parity path and the path for narrow or unaligned shapes.
+#include <algorithm>
+
 #include "common.h"
 #include "dfcsa_internal.h"
 
@@ -914,7 +916,38 @@ void launch_bwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* dy
 
 extern "C" int dfcsa_fra_path(int dtype, int C, int Cq, int ldq, int backward) {
   if (g_fra_generic) return 0;
-  return backward ? (mfma_bwd_ok(dtype, C, Cq, ldq) ? 1 : 0) : (mfma_fwd_ok(dtype, C, Cq, ldq) ? 1 : 0);
+  if (!backward) return mfma_fwd_ok(dtype, C, Cq, ldq) ? 1 : 0;
+  if (mfma_bwd_ok(dtype, C, Cq, ldq)) return 1;
+  // wide bf16 layers (C > 256: the 64^2 / 32^2 levels, where N is small) materialise the score
+  // matrices: library GEMMs for S, dP, dV, dK, dQ around dfcsa_fra_bwd_probs
+  return (dtype == DFCSA_DT_BF16 && C > 256) ? 2 : 0;
+}
+
+// Materialised-score backward, elementwise step (rows = B*N queries, N keys per row, fp32):
+//   S  <- gamma * P,  P = exp(S - lse_row)
+//   dP <- gamma * P * (dP - r_row)            (= dS; dV = S^T dy, dK = dS^T Q, dQ = dS K)
+__global__ void __launch_bounds__(256) fra_bwd_probs_kernel(int64_t total, int N, float* __restrict__ S,
+                                                            float* __restrict__ dP, const float* __restrict__ lse,
+                                                            const float* __restrict__ rr,
+                                                            const float* __restrict__ gamma) {
+  const float gm = *gamma;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int64_t row = e / N;
+    const float p = gm * __expf(S[e] - lse[row]);
+    S[e] = p;
+    dP[e] = p * (dP[e] - rr[row]);
+  }
+}
+
+extern "C" int dfcsa_fra_bwd_probs(int B, int N, float* S, float* dP, const float* lse, const float* r,
+                                   const float* gamma, void* stream) {
+  if (B <= 0 || N <= 0 || !S || !dP || !lse || !r || !gamma) return DFCSA_EINVAL;
+  const int64_t total = (int64_t)B * N * N;
+  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
+  hipLaunchKernelGGL(fra_bwd_probs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, total, N, S, dP, lse,
+                     r, gamma);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_fra_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* x,
