@@ -615,47 +615,47 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     const char* Di = Qi + QBy;
     const float* Ls = (const float*)(Di + DBy);
 
-    f32x4_t sp[4][2], dp[4][2];
-#pragma unroll
-    for (int qs = 0; qs < 4; ++qs) {
-      QKFrag<CQ> qa;
-      qk_load_lds<CQ, KC>(qa, Qi, qs * 16 + li, g);
-      bf16x8_t da[NDC];
-#pragma unroll
-      for (int dc = 0; dc < NDC; ++dc) da[dc] = lds_row8<C>(Di, qs * 16 + li, 32 * dc + 8 * g);
-      const float4 R4 = *(const float4*)(Ls + QT + qs * 16 + 4 * g);  // -r of rows 16 qs + 4g + r
-      const f32x4_t nr = {R4.x, R4.y, R4.z, R4.w};
-#pragma unroll
-      for (int kb = 0; kb < 2; ++kb) {
-        sp[qs][kb] = qk_mfma<CQ>(qa, kf[kb], zero4());
-        f32x4_t a = nr;
-#pragma unroll
-        for (int dc = 0; dc < NDC; ++dc) a = mfma32(da[dc], vf[kb][dc], a);
-        dp[qs][kb] = a;
-      }
-    }
-    // P and dS / gamma (rows = queries 16 qs + 4g + r)
-#pragma unroll
-    for (int qs = 0; qs < 4; ++qs) {
-      const float4 L4 = *(const float4*)(Ls + qs * 16 + 4 * g);  // lse * log2(e)
-      const float Lr[4] = {L4.x, L4.y, L4.z, L4.w};
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-#pragma unroll
-        for (int kb = 0; kb < 2; ++kb) {
-          const float p = exp2_(fmaf(sp[qs][kb][r], kL2E, -Lr[r]));
-          sp[qs][kb][r] = p;
-          dp[qs][kb][r] *= p;
-        }
-      }
-    }
+    // two halves of 32 queries: scores of one half are consumed by the dV/dK MFMAs before the next
+    // half is formed (half the live score registers)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
+      f32x4_t sp[2][2], dp[2][2];
+#pragma unroll
+      for (int hs = 0; hs < 2; ++hs) {
+        const int qs = 2 * h + hs;
+        QKFrag<CQ> qa;
+        qk_load_lds<CQ, KC>(qa, Qi, qs * 16 + li, g);
+        bf16x8_t da[NDC];
+#pragma unroll
+        for (int dc = 0; dc < NDC; ++dc) da[dc] = lds_row8<C>(Di, qs * 16 + li, 32 * dc + 8 * g);
+        const float4 R4 = *(const float4*)(Ls + QT + qs * 16 + 4 * g);  // -r of rows 16 qs + 4g + r
+        const f32x4_t nr = {R4.x, R4.y, R4.z, R4.w};
+#pragma unroll
+        for (int kb = 0; kb < 2; ++kb) {
+          sp[hs][kb] = qk_mfma<CQ>(qa, kf[kb], zero4());
+          f32x4_t a = nr;
+#pragma unroll
+          for (int dc = 0; dc < NDC; ++dc) a = mfma32(da[dc], vf[kb][dc], a);
+          dp[hs][kb] = a;
+        }
+        // P and dS / gamma (rows = queries 16 qs + 4g + r)
+        const float4 L4 = *(const float4*)(Ls + qs * 16 + 4 * g);  // lse * log2(e)
+        const float Lr[4] = {L4.x, L4.y, L4.z, L4.w};
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+          for (int kb = 0; kb < 2; ++kb) {
+            const float p = exp2_(fmaf(sp[hs][kb][r], kL2E, -Lr[r]));
+            sp[hs][kb][r] = p;
+            dp[hs][kb][r] *= p;
+          }
+        }
+      }
       bf16x8_t pb[2], sb[2];
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb) {
-        pb[kb] = pack_b(sp[2 * h][kb], sp[2 * h + 1][kb]);
-        sb[kb] = pack_b(dp[2 * h][kb], dp[2 * h + 1][kb]);
+        pb[kb] = pack_b(sp[0][kb], sp[1][kb]);
+        sb[kb] = pack_b(dp[0][kb], dp[1][kb]);
       }
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
