@@ -230,9 +230,14 @@ def main():
             step()
         torch.cuda.current_stream().wait_stream(side)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            gstats = step()
-        torch.cuda.synchronize()
+        try:
+            with torch.cuda.graph(graph):
+                gstats = step()
+            torch.cuda.synchronize()
+        except RuntimeError as e:  # e.g. a collective the runtime cannot capture: time eager steps
+            log(f"[rank {rank}] HIP graph capture failed ({e}); timing eager steps")
+            graph = None
+            torch.cuda.synchronize()
 
     def run_step():
         if graph is None:
