@@ -21,6 +21,8 @@
 #include "common.h"
 #include "dfcsa_internal.h"
 
+int g_ew_tile_elems = 16384;  // tuning knob 11: elements (pixels x channels) per reduction tile
+
 namespace {
 
 enum {
@@ -584,7 +586,7 @@ void launch_sum_scalar(const float* x, int n, float* out, hipStream_t st) {
 // pixels per reduction tile: ~16 chunk-iterations per thread (fewer, fuller tiles than a fixed size)
 inline int tile_px(int C) {
   const int cpp = C / 8, pl = 256 / (cpp > 0 ? cpp : 1);
-  int t = 32768 / (C > 0 ? C : 1);
+  int t = g_ew_tile_elems / (C > 0 ? C : 1);
   if (t < pl) t = pl;
   return t;
 }

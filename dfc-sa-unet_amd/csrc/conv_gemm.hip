@@ -858,5 +858,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 8) { g_wgrad_narrow = value; return 0; }
   if (knob == 9) { g_fra_generic = value; return 0; }
   if (knob == 10) { g_fra_occ = value; return 0; }
+  if (knob == 11) { g_ew_tile_elems = value >= 4096 ? value : 16384; return 0; }
   return DFCSA_EINVAL;
 }

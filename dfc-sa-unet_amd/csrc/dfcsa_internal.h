@@ -50,3 +50,4 @@ extern int g_wgrad_noglds;
 extern int g_wgrad_narrow;
 extern int g_fra_generic;
 extern int g_fra_occ;
+extern int g_ew_tile_elems;

@@ -23,7 +23,9 @@ def bench(fn, n=20):
     return e0.elapsed_time(e1) / n * 1e3
 
 
-for (B, H, C) in [(16, 224, 64), (16, 112, 128), (16, 56, 256), (16, 28, 512)]:
+TILES = [int(v) for v in os.environ.get("EW_TILES", "32768").split(",")]
+for tile, (B, H, C) in [(tl, s) for s in [(16, 224, 64), (16, 112, 128), (16, 56, 256), (16, 28, 512)] for tl in TILES]:
+    LIB.dfcsa_set_tuning(11, tile)
     M = B * H * H
     t = lambda: torch.randn(B, H, H, C, device="cuda").to(bf)
     a, b, c, d, e, f, h = t(), t(), t(), t(), t(), t(), t()
@@ -45,5 +47,6 @@ for (B, H, C) in [(16, 224, 64), (16, 112, 128), (16, 56, 256), (16, 28, 512)]:
     rows["gate_fuse 3R1W"] = (bench(lambda: call("dfcsa_gate_fuse", 1, M, C, P(a), P(sc), P(sh), P(b), P(c), P(d), stream())), 4 * E)
     rows["block_out 2R1W"] = (bench(lambda: call("dfcsa_block_out", 1, M, C, P(a), P(sc), P(sh), P(b), P(g), P(c), stream())), 3 * E)
     rows["copy 1R1W (torch)"] = (bench(lambda: c.copy_(a)), 2 * E)
-    print(json.dumps({"shape": [B, H, H, C], **{k: [round(us, 1), round(by / us / 1e3)] for k, (us, by) in rows.items()}}),
+    print(json.dumps({"shape": [B, H, H, C], "tile_elems": tile, **{k: [round(us, 1), round(by / us / 1e3)] for k, (us, by) in rows.items()}}),
           flush=True)
+LIB.dfcsa_set_tuning(11, 16384)
