@@ -70,7 +70,7 @@ def test_host_side_planning_functions():
     assert L.dfcsa_wgrad_plan(3136, 1024, 4608, 0, ctypes.addressof(s), ctypes.addressof(mc)) == 0
     assert mc.value % 32 == 0 and s.value >= 1
     assert L.dfcsa_wgrad_plan(0, 1, 1, 1, ctypes.addressof(s), ctypes.addressof(mc)) != 0
-    assert L.dfcsa_ew_ntiles(802816, 64) == 1568
+    assert L.dfcsa_ew_ntiles(802816, 64) == 3136   # 16384-element tiles: 256 pixels of 64 channels
     assert L.dfcsa_lsa_pool_splits(224, 4) >= 1 and L.dfcsa_lsa_pool_splits(14, 32) == 1
     assert 1 <= L.dfcsa_sumsq_nparts(29052083) <= 1024
     assert L.dfcsa_bce_dice_partial_count(16 * 224 * 224) == 512
