@@ -52,6 +52,37 @@ class MaxPool2x2(torch.autograd.Function):
         return dx, None
 
 
+class MaxPoolFork(torch.autograd.Function):
+    """d -> (maxpool2x2(d), d): an encoder output feeds both the next level (reference
+    models/unet_dfc_sa_res.py:165-172, pool1..pool4) and the decoder skip (:179-201).  Its backward
+    forms dd = dskip + maxpool_bwd(dpooled) in one pass: the pooling-gradient kernel accumulates
+    into the skip gradient (a fresh tensor from the decoder block's dgrad GEMM) instead of a
+    zero-filled buffer that autograd would then add to the skip gradient."""
+
+    @staticmethod
+    def forward(ctx, x, dtype):
+        B, H, W, C = x.shape
+        out = torch.empty((B, H // 2, W // 2, C), dtype=dtype, device=x.device)
+        call("dfcsa_maxpool2_fwd", dt(dtype), B, H, W, C, P(x), P(out), stream())
+        ctx.save_for_backward(x)
+        ctx.dtype = dtype
+        return out, x.view_as(x)
+
+    @staticmethod
+    def backward(ctx, g_pool, g_skip):
+        (x,) = ctx.saved_tensors
+        B, H, W, C = x.shape
+        if g_skip is None:
+            dx = torch.zeros_like(x)
+        elif g_skip.is_contiguous() and g_skip.dtype == x.dtype and g_skip.shape == x.shape:
+            dx = g_skip
+        else:
+            dx = g_skip.to(x.dtype).contiguous().clone()
+        if g_pool is not None:
+            call("dfcsa_maxpool2_bwd", dt(ctx.dtype), B, H, W, C, P(x), P(g_pool.contiguous()), P(dx), stream())
+        return dx, None
+
+
 class ConvTranspose2x2(torch.autograd.Function):
     """out[b, 2h+i, 2w+j, co] = sum_ci x[b,h,w,ci] W[ci,co,i,j] + bias[co]: one GEMM with N = 4*Cout
     and a pixel-shuffle epilogue; dgrad = stride-2 gather GEMM; wgrad = pixel reduction."""

@@ -19,7 +19,7 @@ import dfcsa
 from dfcsa import packs
 from dfcsa.block import DFCBlockFunction, LSAFunction
 from dfcsa.flat import FlatParams
-from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPool2x2, ResizeBilinear
+from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPoolFork, ResizeBilinear
 from dfcsa.ops import rup
 
 
@@ -181,13 +181,13 @@ class UNetDFCSA(nn.Module):
         if getattr(self, "_plan_flat", None) is not flat:  # parameter storage changed: stale plan
             self._dfcsa_plan, self._plan_flat = None, flat
         planned = packs.sync_model_plan(self)  # one launch packs every conv operand of the model
-        mp = lambda t: MaxPool2x2.apply(t, dt)  # noqa: E731
+        fork = lambda t: MaxPoolFork.apply(t, dt)  # noqa: E731  (pooled, skip alias)
         h = _nchw_to_nhwc(x, dt)
-        d1 = self.down1.forward_nhwc([h], dt)
-        d2 = self.down2.forward_nhwc([mp(d1)], dt)
-        d3 = self.down3.forward_nhwc([mp(d2)], dt)
-        d4 = self.down4.forward_nhwc([mp(d3)], dt)
-        u = self.bottleneck.forward_nhwc([mp(d4)], dt)
+        p1, d1 = fork(self.down1.forward_nhwc([h], dt))
+        p2, d2 = fork(self.down2.forward_nhwc([p1], dt))
+        p3, d3 = fork(self.down3.forward_nhwc([p2], dt))
+        p4, d4 = fork(self.down4.forward_nhwc([p3], dt))
+        u = self.bottleneck.forward_nhwc([p4], dt)
         for up, block, skip in ((self.up4, self.up_conv4, d4), (self.up3, self.up_conv3, d3),
                                 (self.up2, self.up_conv2, d2), (self.up1, self.up_conv1, d1)):
             u = ConvTranspose2x2.apply(u, up, dt, *up.parameters())
