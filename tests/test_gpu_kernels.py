@@ -165,6 +165,28 @@ def test_maxpool_ties_and_odd_sizes():
     assert torch.equal(nchw(xh.grad), xr.grad)
 
 
+def test_maxpool_fork_accumulates_into_skip_gradient():
+    """MaxPoolFork (encoder output -> pooled + skip): dx = maxpool_bwd(d pooled) + d skip, formed
+    in place in the skip gradient; also with the skip unused (no skip gradient)."""
+    from dfcsa.functions import MaxPoolFork
+    torch.manual_seed(7)
+    x = torch.randint(-2, 3, (2, 16, 10, 8)).float()  # ties
+    xr = x.clone().requires_grad_(True)
+    ref = F.max_pool2d(xr, 2, 2)
+    g1, g2 = torch.randn_like(ref), torch.randn_like(x)
+    (ref * g1).sum().backward()
+    want = xr.grad + g2
+    xh = nhwc(x, torch.float32).requires_grad_(True)
+    pooled, skip = MaxPoolFork.apply(xh, torch.float32)
+    assert torch.equal(nchw(pooled), ref) and torch.equal(nchw(skip), x)
+    ((pooled * nhwc(g1, torch.float32)).sum() + (skip * nhwc(g2, torch.float32)).sum()).backward()
+    assert torch.equal(nchw(xh.grad), want)
+    xh2 = nhwc(x, torch.float32).requires_grad_(True)
+    pooled2, _ = MaxPoolFork.apply(xh2, torch.float32)
+    (pooled2 * nhwc(g1, torch.float32)).sum().backward()
+    assert torch.equal(nchw(xh2.grad), xr.grad)
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-6), (torch.bfloat16, 1e-2)])
 def test_resize_bilinear(dtype, tol):
     from dfcsa.functions import ResizeBilinear
