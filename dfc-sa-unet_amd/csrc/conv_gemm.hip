@@ -787,6 +787,7 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
         case 16: return launch_glds<128, 128, 4, 2, 3>(a, st);
         case 17: return launch_glds<256, 64, 8, 1, 2>(a, st);
         case 18: return launch_glds<256, 128, 8, 2, 2>(a, st);
+        case 19: return launch_glds<64, 64, 2, 2, 2>(a, st);
         default: break;
       }
     }
@@ -800,7 +801,14 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // fewer than one workgroup of 128x128 per CU (the 14^2 level, 28^2 with N <= 256): 128x64 doubles the
     // workgroup count (gemm_bench: bottleneck dgrad 123 -> 108 us, bottleneck fwd 59 -> 52 us).
     if (a.N <= 64) return a.M >= 65536 ? launch_glds<256, 64, 8, 1, 2>(a, st) : launch_glds<128, 64, 4, 1, 2>(a, st);
-    if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) return launch_glds<128, 64, 4, 1, 2>(a, st);
+    if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) {
+      // still under one 128x64 workgroup per CU with a short K (the ViT GEMMs of TransUNet:
+      // M = 8 x 196 rows, K = 768 / 3072): 64x64 tiles (4 waves of 32x32) double the workgroups
+      // again (config 4: 499 -> 511 img/s).  Long-K GEMMs (the 14^2 3x3 dgrads) keep 128x64.
+      if (a.K <= 3072 && ((a.M + 127) / 128) * ((a.N + 63) / 64) < 256)
+        return launch_glds<64, 64, 2, 2, 2>(a, st);
+      return launch_glds<128, 64, 4, 1, 2>(a, st);
+    }
     return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
   // fp32 (parity mode + the fp32 LightSelfAttention projections): small problems (M = B*P*P

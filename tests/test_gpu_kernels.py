@@ -272,7 +272,7 @@ def test_head_fwd_bwd(dtype, tol, C, Cout):
                                               (4, 128, 64, 1, 256, False),   # 256x128 tile
                                               (4, 128, 16, 2, 128, True),    # 256x128, 3x3, 2 sources
                                               (2, 96, 8, 1, 64, True)])      # Cseg 8 < K stage
-@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18])
+@pytest.mark.parametrize("cfg", [0, 1, 2, 3, 4, 5, 6, 8, 9, 10, 11, 12, 13, 14, 15, 16, 17, 18, 19])
 def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3, cfg):
     """Every bf16 tile configuration (tuning knob 1; 0 = automatic) on the same problems."""
     import dfcsa
