@@ -124,7 +124,7 @@ def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
         opt.zero_grad()
         met = calculate_metrics_device(sigmoid(model(xtr[idx])), ttr[idx], "bce_dice", {})
         met["loss"].backward()
-        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
     train_loss = float(met["stats"][0].item())
     model.eval()
     dices = []
@@ -205,9 +205,8 @@ def main():
         if reducer:
             reducer.start()
         loss.backward()
-        if reducer:
-            reducer.finish()
-        opt.step(max_norm=1.0, grad_scale=scale, skip_if_nonfinite=loss)
+        skip = reducer.finish(loss) if reducer else loss   # NaN on any rank -> every rank skips
+        opt.step(max_norm=1.0, grad_scale=scale, skip_if_nan=skip)
         return stats
 
     def barrier():

@@ -37,6 +37,16 @@ def grad_of(p):
     return p.grad
 
 
+def raise_eval_backward():
+    """The backward kernels implement train-mode BatchNorm (batch statistics: dz is centred by
+    mean(dz) and mean(dz*xh), the pre-BN conv bias gets its exact-zero gradient).  An eval-mode
+    forward (running statistics) would need the per-channel affine backward instead, so it is
+    refused rather than answered with wrong gradients."""
+    raise NotImplementedError("backward through an eval-mode (running-statistics) BatchNorm forward is not "
+                              "implemented by the dfcsa kernels; run the forward in train mode or under "
+                              "torch.no_grad()")
+
+
 def _conv3x3_segments(xs):
     return [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xs]
 
@@ -418,10 +428,13 @@ class DFCBlockFunction(torch.autograd.Function):
         training = blk.training
         out, saved = block_forward(blk, xs, pool_size, training, dtype)
         ctx.blk, ctx.saved, ctx.dtype, ctx.nsrc, ctx.nparams = blk, saved, dtype, nsrc, len(args) - nsrc
+        ctx.training = training
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        if not ctx.training:
+            raise_eval_backward()
         need_dx = any(ctx.needs_input_grad[4:4 + ctx.nsrc])
         dxs = block_backward(ctx.blk, ctx.saved, dout, need_dx, ctx.dtype)
         ctx.saved = None

@@ -11,8 +11,16 @@ design:
   * every module backward (DFC block, transposed conv, head) reports when its parameters'
     gradients are final; a bucket whose modules are all final is all-reduced immediately with
     async_op=True, so RCCL runs on its own stream underneath the remaining backward kernels;
-  * ``finish()`` makes the compute stream wait for every bucket (no host synchronisation);
-    the optimizer then applies 1/world_size inside the fused clip+SGD pass.
+  * ``finish(loss)`` makes the compute stream wait for every bucket (no host synchronisation);
+    the optimizer then applies 1/world_size inside the fused clip+SGD pass.  With ``loss`` it
+    also all-reduces (MAX) a NaN indicator of every rank's loss and returns the device scalar the
+    optimizer's NaN skip reads, so a NaN loss on ANY rank skips the update on EVERY rank (the
+    reference's NaN ``continue``, utils/trainer.py:134-139, made consistent across replicas; a
+    rank-local decision would let the other ranks apply the NaN gradients they received);
+  * BatchNorm running statistics are per replica between syncs (each rank normalises its own
+    shard, as torch DDP does).  ``broadcast_buffers()`` copies rank 0's running statistics to
+    every rank (torch DDP's broadcast_buffers); call it before validation or checkpointing so all
+    ranks evaluate and save the same model.
 """
 import torch
 import torch.distributed as dist
@@ -79,18 +87,41 @@ class GradBucketReducer:
         with torch.cuda.stream(side):
             return dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
-    def finish(self):
-        """Ensure every bucket has been reduced (launch stragglers), make the current stream wait."""
+    def finish(self, loss=None):
+        """Ensure every bucket has been reduced (launch stragglers), make the current stream wait.
+        With ``loss``: returns a device scalar that is NaN iff some rank's loss is NaN (else 0),
+        for ``FusedSGD.step(skip_if_nan=...)``."""
         if self._pending is None:
-            return
+            return None
         for j in range(len(self._works), len(self.buckets)):
             lo, hi, _ = self.buckets[j]
             self._works.append(self._launch(lo, hi))
+        flag = None
+        if loss is not None:
+            flag = torch.isnan(loss.detach().reshape(1)).float()
+            self._works.append(dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
         if self.flat.grad.is_cuda:
             streams.join()
         for w in self._works:
             w.wait()
         self._pending = None
+        if flag is None:
+            return None
+        return torch.where(flag > 0, torch.full_like(flag, float("nan")), torch.zeros_like(flag))
+
+    @torch.no_grad()
+    def broadcast_buffers(self, src=0):
+        """Copy rank ``src``'s floating-point buffers (BatchNorm running_mean / running_var) to every
+        rank in one collective."""
+        bufs = [b for b in self.model.buffers() if b.is_floating_point()]
+        if not bufs:
+            return
+        flat = torch.cat([b.reshape(-1) for b in bufs])
+        dist.broadcast(flat, src=src, group=self.group)
+        o = 0
+        for b in bufs:
+            b.copy_(flat[o:o + b.numel()].view_as(b))
+            o += b.numel()
 
     @property
     def grad_scale(self):

@@ -28,6 +28,7 @@ class FusedSGD(torch.optim.Optimizer):
         self._mom = None
         self._mom_init = None
         self._partial = None
+        self._pending_mom = None   # momentum buffers loaded before the flat storage existed
         self.last_norm = None
 
     @classmethod
@@ -49,15 +50,27 @@ class FusedSGD(torch.optim.Optimizer):
                 any(a is not b for a, b in zip(flat.params, params)):
             raise RuntimeError("FusedSGD needs the parameters of a dfcsa model after its first forward "
                                "(they live in one flat buffer); got foreign parameters")
+        frozen = [i for i, p in enumerate(params) if not p.requires_grad]
+        if frozen:
+            # torch's SGD skips parameters without a gradient; the fused pass updates the whole
+            # flat buffer, so frozen parameters would drift under weight decay / momentum
+            raise NotImplementedError(f"FusedSGD: {len(frozen)} parameter(s) have requires_grad=False; "
+                                      "freeze nothing or use torch.optim.SGD")
         if flat is not self._flat:
             self._flat = flat
             self._mom = torch.zeros_like(flat.data)
             self._mom_init = torch.zeros(1, dtype=torch.int32, device=flat.device)
-            self._partial = torch.empty(LIB.dfcsa_sumsq_nparts(flat.numel), dtype=torch.float32,
+            self._partial = torch.empty(LIB.dfcsa_sumsq_nparts(flat.numel), dtype=torch.float64,
                                         device=flat.device)
             self.last_norm = torch.zeros(1, dtype=torch.float32, device=flat.device)
+            pending, self._pending_mom = self._pending_mom, None
             for p, off in zip(flat.params, flat.offsets):
-                self.state[p]["momentum_buffer"] = self._mom[off:off + p.numel()].view_as(p)
+                view = self._mom[off:off + p.numel()].view_as(p)
+                if pending is not None:
+                    view.copy_(pending[id(p)])
+                self.state[p]["momentum_buffer"] = view
+            if pending is not None:
+                self._mom_init.fill_(1)   # resumed: the next step continues the loaded momentum
         return flat
 
     def zero_grad(self, set_to_none=True):
@@ -68,10 +81,11 @@ class FusedSGD(torch.optim.Optimizer):
             super().zero_grad(set_to_none)
 
     @torch.no_grad()
-    def step(self, closure=None, max_norm=None, grad_scale=1.0, skip_if_nonfinite=None):
+    def step(self, closure=None, max_norm=None, grad_scale=1.0, skip_if_nan=None):
         """max_norm: clip the global L2 norm first (None = no clipping).
         grad_scale: multiply gradients first (1/world_size after an all-reduce sum).
-        skip_if_nonfinite: device scalar; the update is skipped on the device if it is NaN/inf."""
+        skip_if_nan: device scalar; the update is skipped on the device if it is NaN (the
+        reference's NaN-loss skip, utils/trainer.py:134-139; an inf loss still steps)."""
         loss = closure() if closure is not None else None
         flat = self._resolve()
         streams.join()  # weight gradients may still be in flight on the side stream
@@ -84,18 +98,20 @@ class FusedSGD(torch.optim.Optimizer):
             nparts, mn = 0, float("inf")
         call("dfcsa_clip_sgd", ctypes.c_int64(n), P(flat.data), P(flat.grad), P(self._mom), P(self._partial),
              nparts, mn, float(grad_scale), float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-             P(self._mom_init), P(skip_if_nonfinite), P(self.last_norm), stream())
+             P(self._mom_init), P(skip_if_nan), P(self.last_norm), stream())
         return loss
 
     def load_state_dict(self, state_dict):
+        """torch.optim.SGD state (e.g. a reference checkpoint's optimizer_state_dict): the loaded
+        momentum buffers are copied into the flat momentum storage -- now if it exists, otherwise
+        when the model's first forward has created it (the next step() resolves it)."""
         super().load_state_dict(state_dict)
-        flat = getattr(self.param_groups[0]["params"][0], "_dfcsa_flat", None)
-        if flat is None:
-            return
-        bufs = [self.state[p].get("momentum_buffer") for p in flat.params]
-        if all(b is not None for b in bufs):
-            self._flat = None
+        params = self.param_groups[0]["params"]
+        bufs = [self.state[p].get("momentum_buffer") if p in self.state else None for p in params]
+        if not all(b is not None for b in bufs):
+            return   # no momentum yet (checkpoint taken before the first step): start fresh
+        flat = getattr(params[0], "_dfcsa_flat", None)
+        self._pending_mom = {id(p): b.detach().clone() for p, b in zip(params, bufs)}
+        self._flat = None
+        if flat is not None and flat.valid():
             self._resolve()
-            for p, b in zip(flat.params, bufs):
-                self.state[p]["momentum_buffer"].copy_(b)
-            self._mom_init.fill_(1)

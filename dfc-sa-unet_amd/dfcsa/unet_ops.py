@@ -9,7 +9,7 @@ import torch
 
 from . import ops
 from ._lib import call
-from .block import grad_of
+from .block import grad_of, raise_eval_backward
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
@@ -66,10 +66,13 @@ class ConvBNReLU(torch.autograd.Function):
         out = ops.bn_act(dtype, y, bnst, 1)
         ctx.conv, ctx.bn, ctx.dtype, ctx.nsrc, ctx.np = conv, bn, dtype, nsrc, len(args) - nsrc
         ctx.xs, ctx.y, ctx.bnst, ctx.pk = xs, y, bnst, pk
+        ctx.training = training
         return out
 
     @staticmethod
     def backward(ctx, dout):
+        if not ctx.training:
+            raise_eval_backward()
         conv, bn, dtype, xs, y, bnst = ctx.conv, ctx.bn, ctx.dtype, ctx.xs, ctx.y, ctx.bnst
         B, H, W, C = y.shape
         Cs = xs[0].shape[-1]

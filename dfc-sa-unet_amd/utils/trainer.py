@@ -15,8 +15,9 @@ torch optimizer the reference's clip_grad_norm_ + step() are called.  A plain
 ``torch.optim.SGD`` (what the reference's train.py builds) is converted to FusedSGD.
 
 Differences kept deliberately small and listed: plots are written only when matplotlib is
-importable; best/worst validation samples are kept (tensors on the host) but image dumps
-(cv2 in the reference) are not written; ``train(resume_from)`` restores the histories, the
+importable; best/worst validation samples are kept (tensors on the host, stored in the
+checkpoint's ``metrics`` like the reference's) but image dumps (cv2 in the reference) are not
+written; ``train(resume_from)`` restores the histories, the
 start epoch and the best validation Dice (the reference resets histories and best Dice,
 trainer.py:334-349 -- pass ``training.reference_resume_semantics: true`` to keep that behaviour).
 """
@@ -81,9 +82,9 @@ class Trainer:
         loss = met["loss"]
         loss.backward()
         if isinstance(self.optimizer, FusedSGD):
-            self.optimizer.step(max_norm=self.max_norm, skip_if_nonfinite=loss)
+            self.optimizer.step(max_norm=self.max_norm, skip_if_nan=loss)
         else:
-            if torch.isfinite(loss):  # host sync; reference behaviour with a foreign optimizer
+            if not torch.isnan(loss):  # host sync; reference behaviour with a foreign optimizer
                 torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm)
                 self.optimizer.step()
         return met
@@ -151,7 +152,7 @@ class Trainer:
                 "train_dice_scores": self.train_dice_scores, "val_dice_scores": self.val_dice_scores,
                 "train_iou_scores": self.train_iou_scores, "val_iou_scores": self.val_iou_scores,
                 "best_val_loss": self.best_val_loss,
-                "metrics": {k: v for k, v in metrics.items() if k not in ("best_samples", "worst_samples")}}
+                "metrics": metrics}   # incl. best/worst samples (host tensors), as trainer.py:276-288
         path = os.path.join(self.checkpoint_dir, f"checkpoint_epoch_{epoch + 1}.pth").replace("\\", "/")
         torch.save(ckpt, path)
         if is_best:

@@ -311,15 +311,17 @@ int dfcsa_bce_dice_bwd(int64_t n, const float* p, const float* t, const float* s
 /* ------------------------------------------------------------------------------------------
  * clip_grad_norm_(max_norm) + SGD(momentum, weight_decay) over one flat fp32 parameter
  * buffer (utils/trainer.py:149-151, train.py:73-78).  grad_scale multiplies the gradient
- * first (1/world_size after an all-reduce sum).  If *skip_if_nonfinite is not finite the step
- * is skipped on the device (the reference's NaN-loss `continue`, trainer.py:134-139).
+ * first (1/world_size after an all-reduce sum).  If *skip_if_nan is NaN the step is skipped on
+ * the device (the reference's NaN-loss `continue`, trainer.py:134-139; an inf loss still steps).
+ * A NaN total norm gives a NaN clip coefficient (torch's clip_grad_norm_).  partial: nparts fp64
+ * per-block sums of squares.
  * *mom_init == 0 -> momentum buffer = d (torch's first step), then set to 1.
  * ---------------------------------------------------------------------------------------- */
 int dfcsa_sumsq_nparts(int64_t n);
-int dfcsa_sumsq_partial(int64_t n, const float* g, float* partial, void* stream);
-int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const float* partial, int nparts,
+int dfcsa_sumsq_partial(int64_t n, const float* g, double* partial, void* stream);
+int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const double* partial, int nparts,
                    float max_norm, float grad_scale, float lr, float momentum, float weight_decay,
-                   int* mom_init, const float* skip_if_nonfinite, float* norm_out, void* stream);
+                   int* mom_init, const float* skip_if_nan, float* norm_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Full-resolution self-attention (models/unet_dfc_sa_ablation_attention.py:15-26, the attention

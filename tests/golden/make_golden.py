@@ -609,9 +609,164 @@ def gen_inference():
     save("inference.npz", **out)
 
 
+# ----------------------------------------------------------------------------------------
+# (11) bf16 calibration: what PyTorch's own bf16 autocast does to the reference's logits, loss and
+#      metrics on the small model (sd0 of model_small.npz) over the fixture batch and 5 seeded
+#      batches.  The GPU tests hold the build's bf16 mode to max(1e-2, this error) per batch.
+# ----------------------------------------------------------------------------------------
+def _autocast_errors(model, x, t):
+    import copy
+    with torch.no_grad():
+        o32 = copy.deepcopy(model)(x)
+        m64 = fp64_twin(model)
+        o64 = m64(x.double())
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            ob = copy.deepcopy(model)(x)
+    ob = ob.float()
+    a = ref_metrics.calculate_metrics(torch.sigmoid(o32), t, "bce_dice", {})
+    b = ref_metrics.calculate_metrics(torch.sigmoid(ob), t, "bce_dice", {})
+    rel = lambda u, v: np.float64(((u.double() - v.double()).norm() / v.double().norm()).item())  # noqa: E731
+    return o32, a, {"ac_logits_rel": rel(ob, o32), "ac_logits_rel64": rel(ob, o64),
+                    "ac_loss_rel": np.float64(abs(b["loss"].item() - a["loss"].item()) / abs(a["loss"].item())),
+                    "ac_iou": np.float64(b["iou"]), "ac_dice": np.float64(b["dice"])}
+
+
+def gen_bf16calib():
+    fx = dict(np.load(os.path.join(OUT, "model_small.npz")))
+    model = base_model(4)
+    model.train()
+    out = {}
+    batches = [("x1", torch.from_numpy(fx["x1"]), torch.from_numpy(fx["t1"]))]
+    for s in range(5):
+        gen = torch.Generator().manual_seed(11000 + s)
+        batches.append((f"s{s}",) + batch(gen, (2, 3, 32, 32)))
+    for tag, x, t in batches:
+        o32, met, e = _autocast_errors(model, x, t)
+        out.update({f"{tag}.x": np32(x), f"{tag}.t": np32(t), f"{tag}.logits": np32(o32),
+                    f"{tag}.loss": np32(met["loss"]), f"{tag}.iou": np.float64(met["iou"]),
+                    f"{tag}.dice": np.float64(met["dice"])})
+        out.update({f"{tag}.{k}": v for k, v in e.items()})
+        print(tag, {k: float(v) for k, v in e.items()})
+    save("bf16_calib.npz", tags=np.array([b[0] for b in batches]), **out)
+
+
+# ----------------------------------------------------------------------------------------
+# (12) Config-2 geometry: DFC-SA-Res features 64..512, P = 4, 224 x 224, batch 2, gammas 0.5,
+#      one reference train step (fwd, sigmoid, bce_dice, backward, clip 1.0, SGD).  The 29 M
+#      parameters are not stored: the test builds the model under the same seed (same module tree
+#      and creation order) and checks the per-tensor init sums first.  Stored: logits, loss, IoU,
+#      Dice, pre-clip per-tensor gradient norms (+ float64 run and the fp32-vs-fp64 noise), the full
+#      gradients of the small tensors, the total norm, the BN running stats after the step, the
+#      per-tensor norms of the SGD update, and the autocast bf16 calibration at this geometry.
+# ----------------------------------------------------------------------------------------
+def gen_cfg2():
+    torch.manual_seed(12000)
+    m = ref_res.UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4, ablation_on_qk_channels=8)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    init = {"init_sum." + k: np.float64(v.double().sum()) for k, v in m.state_dict().items() if v.is_floating_point()}
+    m.train()
+    gen = torch.Generator().manual_seed(12001)
+    x, t = batch(gen, (2, 3, 224, 224))
+    _, _, calib = _autocast_errors(m, x, t)
+    print("cfg2 autocast", {k: float(v) for k, v in calib.items()})
+    m64 = fp64_twin(m)
+    w0 = {n: p.detach().clone() for n, p in m.named_parameters()}
+    opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad()
+    out = m(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", LOSS_PARAMS)
+    met["loss"].backward()
+    met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", LOSS_PARAMS)
+    met64["loss"].backward()
+    gnorm = {"gnorm." + n: np.float64(p.grad.double().norm()) for n, p in m.named_parameters()}
+    g64 = dict(m64.named_parameters())
+    gnorm64 = {"gnorm64." + n: np.float64(g64[n].grad.norm()) for n, _ in m.named_parameters()}
+    small = {"grad." + n: np32(p.grad) for n, p in m.named_parameters() if p.numel() <= 4096}
+    small.update({"grad64." + n: np32(g64[n].grad) for n, p in m.named_parameters() if p.numel() <= 4096})
+    noise = fp64_noise(m, m64)
+    norm = torch.nn.utils.clip_grad_norm_(m.parameters(), max_norm=1.0)
+    opt.step()
+    upd = {"dnorm." + n: np.float64((p.detach().double() - w0[n].double()).norm()) for n, p in m.named_parameters()}
+    bufs = {"buf." + k: v.numpy().copy() for k, v in m.state_dict().items() if "running" in k}
+    save("cfg2_step.npz", x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]),
+         iou=np.float64(met["iou"]), dice=np.float64(met["dice"]), norm=np32(norm),
+         nparams=np.int64(sum(p.numel() for p in m.parameters())), **init, **gnorm, **gnorm64, **small, **noise,
+         **upd, **bufs, **{"calib." + k: v for k, v in calib.items()})
+
+
+# ----------------------------------------------------------------------------------------
+# (13) Checkpoint interop: the reference Trainer (utils/trainer.py) trains the small model for one
+#      epoch of two batches, validates, and writes its checkpoint with its own save_checkpoint
+#      (:267-298; metrics with best/worst samples).  A second reference Trainer loads it with its own
+#      load_checkpoint (:300-324) and trains one more epoch on a third batch: the expected loss and
+#      parameters after resuming (SGD momentum restored from the checkpoint).
+#      utils/visualization.py needs cv2 (absent): the Trainer's plotting imports are stubbed (no
+#      plotting is called by train_epoch / validate_epoch / save_checkpoint / load_checkpoint).
+# ----------------------------------------------------------------------------------------
+def _reference_trainer():
+    import types
+    if "utils" not in sys.modules or not hasattr(sys.modules["utils"], "_refstub"):
+        pkg = types.ModuleType("utils")
+        pkg.__path__ = [os.path.join(REF, "utils")]
+        pkg._refstub = True
+        sys.modules["utils"] = pkg
+        sys.modules["utils.metrics"] = ref_metrics
+        vis = types.ModuleType("utils.visualization")
+        for f in ("save_loss_plot", "save_metrics_plot", "save_prediction_samples"):
+            setattr(vis, f, lambda *a, **k: None)
+        sys.modules["utils.visualization"] = vis
+    return _load("ref_trainer", "utils/trainer.py")
+
+
+def gen_ckpt():
+    import shutil
+    import tempfile
+    tr_mod = _reference_trainer()
+    fx = dict(np.load(os.path.join(OUT, "model_small.npz")))
+    gen = torch.Generator().manual_seed(13000)
+    x3, t3 = batch(gen, (2, 3, 32, 32))
+    batches = [{"image": torch.from_numpy(fx[f"x{s}"]), "mask": torch.from_numpy(fx[f"t{s}"]),
+                "filename": [f"a{s}.png", f"b{s}.png"]} for s in (1, 2)]
+    b3 = [{"image": x3, "mask": t3, "filename": ["a3.png", "b3.png"]}]
+    tmp = tempfile.mkdtemp()
+    cfg = {"training": {"num_epochs": 1, "save_checkpoint_freq": 1,
+                        "loss": {"type": "bce_dice", "params": LOSS_PARAMS}},
+           "logging": {"log_dir": os.path.join(tmp, "logs"), "images_dir": os.path.join(tmp, "img"),
+                       "save_best_worst_samples": 1}}
+    model = base_model(4)
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    tr = tr_mod.Trainer(model, batches, batches[:1], opt, torch.device("cpu"), cfg)
+    loss, iou, dice = tr.train_epoch(0)
+    tr.train_losses.append(loss)
+    tr.train_dice_scores.append(dice)
+    tr.train_iou_scores.append(iou)
+    val = tr.validate_epoch(batches[:1])
+    tr.val_losses.append(val["loss"])
+    tr.val_dice_scores.append(val["dice"])
+    tr.val_iou_scores.append(val["iou"])
+    tr.epochs.append(1)
+    tr.save_checkpoint(0, val, is_best=True)
+    src = os.path.join(tmp, "logs", "checkpoints", "checkpoint_epoch_1.pth")
+    shutil.copy(src, os.path.join(OUT, "ref_checkpoint_epoch_1.pth"))
+    # resume with the reference's own loader, one more epoch on batch 3
+    model2 = ref_res.UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, ablation_on_qk_channels=8)
+    opt2 = torch.optim.SGD(model2.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    tr2 = tr_mod.Trainer(model2, b3, b3, opt2, torch.device("cpu"), cfg)
+    ep = tr2.load_checkpoint(src)
+    loss3, iou3, dice3 = tr2.train_epoch(ep + 1)
+    save("ref_checkpoint_resume.npz", epoch=np.int64(ep), x3=np32(x3), t3=np32(t3), loss3=np.float64(loss3),
+         iou3=np.float64(iou3), dice3=np.float64(dice3), train_loss1=np.float64(loss), val_dice1=np.float64(val["dice"]),
+         **sd_arrays(model2, "sd3."))
+    shutil.rmtree(tmp)
+
+
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference", "zoo"]
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference", "zoo",
+                             "bf16calib", "cfg2", "ckpt"]
     for w in which:
         globals()["gen_" + w]()
     print("torch", torch.__version__)

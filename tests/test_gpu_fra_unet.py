@@ -255,7 +255,7 @@ def test_fullres_model_bf16_train_step():
     opt.zero_grad()
     met = calculate_metrics_device(sigmoid(m16(x)), t, "bce_dice", {})
     met["loss"].backward()
-    opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+    opt.step(max_norm=1.0, skip_if_nan=met["loss"])
     torch.cuda.synchronize()
     assert np.isfinite(met["loss"].item()) and np.isfinite(opt.last_norm.item())
 
@@ -331,6 +331,6 @@ def test_factory_unet_config1_trains():
         opt.zero_grad()
         met = calculate_metrics_device(sigmoid(m(x)), t, "bce_dice", {})
         met["loss"].backward()
-        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
         losses.append(met["loss"].item())
     assert losses[-1] < losses[0], losses

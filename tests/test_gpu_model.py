@@ -4,7 +4,8 @@ reference (tests/golden/make_golden.py) and against the CPU oracle.
 fp32 compute mode: logits / loss / metrics to 1e-4 (north star), parameter gradients to 1e-3
 relative norm per tensor (BatchNorm-preceded conv biases have ~zero true gradient and are
 compared in absolute terms against the weight-gradient scale).
-bf16 compute mode: logits and loss within 1e-2 / 2e-2 relative (north star: 1e-2 bf16).
+bf16 compute mode: loss within 1e-2, logits within max(1e-2, the reference's own bf16-autocast
+error on the same batch, tests/golden/bf16_calib.npz) -- see tests/test_gpu_parity2.py.
 """
 import glob
 import os
@@ -125,7 +126,7 @@ def test_model_two_train_steps_fp32():
         met["loss"].backward()
         if step == 1:
             grads_pre = None
-        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
         torch.cuda.synchronize()
         assert rel(logits, fx[f"logits{step}"]) < 1e-4
         assert abs(met["loss"].item() - float(fx[f"loss{step}"])) < 1e-4 * abs(float(fx[f"loss{step}"]))
@@ -181,7 +182,8 @@ def test_model_bf16_vs_reference():
     logits = model(T(fx["x1"]))
     met = calculate_metrics(sigmoid(logits), T(fx["t1"]), "bce_dice", LP)
     met["loss"].backward()
-    assert rel(logits, fx["logits1"]) < 2e-2
+    calib = dict(np.load(os.path.join(GOLDEN, "bf16_calib.npz")))
+    assert rel(logits, fx["logits1"]) <= max(1e-2, float(calib["x1.ac_logits_rel"]))
     assert abs(met["loss"].item() - float(fx["loss1"])) < 1e-2 * abs(float(fx["loss1"]))
     # Gradients: bf16 activations through 9 BatchNorm'd blocks at random init are intrinsically
     # noisy.  Calibration (same weights and batch): PyTorch's own bf16 autocast of the reference

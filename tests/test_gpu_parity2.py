@@ -1,0 +1,408 @@
+"""Round-2 parity on the MI355X: the bf16 bar, the config-2 geometry, reference checkpoint interop,
+the data-parallel step's HIP backward + grad_scale path, and the graph-captured RCCL reducer.
+
+bf16 bar (north star: 1e-2 bf16).  PyTorch's own bf16 autocast of the REFERENCE misses 1e-2 on
+logits on this network: tests/golden/bf16_calib.npz holds its error on the small model over the
+fixture batch and 5 seeded batches (1.20e-2 .. 1.33e-2), cfg2_step.npz at the config-2 geometry
+(1.81e-2).  The bar is therefore max(1e-2, the reference's own autocast error on the same batch),
+per batch; loss, IoU and Dice are held to the plain 1e-2; thresholded predictions must agree
+exactly on every pixel whose fp32 logit is farther than EPS from the 0.5-probability boundary.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+LP = {"bce_weight": 0.5, "dice_weight": 0.5}
+ZERO = ("conv_branch.0.bias", "attn_branch.0.bias", "gate.0.bias", "fusion_conv.0.bias", "key_conv.bias")
+EPS = 0.05   # |logit| margin of the thresholded-metric rule (SURVEY.md section 7, bf16 parity)
+
+
+def T(a, dev="cuda"):
+    return torch.from_numpy(np.asarray(a)).to(dev)
+
+
+def rel(a, b):
+    a = torch.as_tensor(a).detach().double().cpu()
+    b = torch.as_tensor(np.asarray(b) if not torch.is_tensor(b) else b).detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def load(name):
+    return dict(np.load(os.path.join(GOLDEN, name)))
+
+
+def small_model(precision):
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    fx = load("model_small.npz")
+    m = UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, ablation_on_qk_channels=8, precision=precision)
+    m.load_state_dict({k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd0.")})
+    return m.cuda().train()
+
+
+def bf16_bar_check(logits, loss, stats, ref_logits, ref_loss, ref_iou, ref_dice, ac_rel, t):
+    """The bf16 bar of the module docstring.  Returns (logits rel, bar)."""
+    from dfcsa.loss import metrics_from_stats
+    r = rel(logits, ref_logits)
+    bar = max(1e-2, float(ac_rel))
+    assert r <= bar, (r, bar)
+    assert abs(loss - float(ref_loss)) <= 1e-2 * abs(float(ref_loss))
+    iou, dice = metrics_from_stats(stats)
+    assert abs(iou - float(ref_iou)) <= 1e-2 * max(abs(float(ref_iou)), 1e-2), (iou, ref_iou)
+    assert abs(dice - float(ref_dice)) <= 1e-2 * max(abs(float(ref_dice)), 1e-2), (dice, ref_dice)
+    lr = torch.as_tensor(np.asarray(ref_logits))
+    confident = lr.abs() > EPS
+    ours = logits.detach().float().cpu() > 0
+    assert torch.equal(ours[confident], (lr > 0)[confident]), "thresholded prediction flipped on a confident pixel"
+    return r, bar
+
+
+# ----------------------------------------------------------------------------- bf16 bar
+@pytest.mark.parametrize("tag", ["x1", "s0", "s1", "s2", "s3", "s4"])
+def test_bf16_small_model_within_reference_autocast(tag):
+    from dfcsa.loss import sigmoid
+    from utils.metrics import calculate_metrics_device
+    fx = load("bf16_calib.npz")
+    model = small_model("bf16")
+    with torch.no_grad():
+        logits = model(T(fx[f"{tag}.x"]))
+        met = calculate_metrics_device(sigmoid(logits), T(fx[f"{tag}.t"]), "bce_dice", {})
+    r, bar = bf16_bar_check(logits, met["loss"].item(), met["stats"], fx[f"{tag}.logits"], fx[f"{tag}.loss"],
+                            fx[f"{tag}.iou"], fx[f"{tag}.dice"], fx[f"{tag}.ac_logits_rel"], fx[f"{tag}.t"])
+    print(f"{tag}: bf16 logits rel {r:.4e}, reference autocast {float(fx[tag + '.ac_logits_rel']):.4e}")
+
+
+def test_bf16_small_model_no_worse_than_autocast_on_average():
+    """Over the 6 calibration batches our bf16 mode is, on average, at least as close to the fp32
+    reference as the reference's own bf16 autocast."""
+    fx = load("bf16_calib.npz")
+    model = small_model("bf16")
+    ratios = []
+    for tag in [str(t) for t in fx["tags"]]:
+        with torch.no_grad():
+            logits = model(T(fx[f"{tag}.x"]))
+        ratios.append(rel(logits, fx[f"{tag}.logits"]) / float(fx[f"{tag}.ac_logits_rel"]))
+    assert np.mean(ratios) <= 1.0, ratios
+
+
+# ----------------------------------------------------------------------------- config-2 geometry
+def cfg2_model(precision):
+    """The fixture's model: torch.manual_seed(12000), DFC-SA-Res 64..512, P=4, gammas 0.5 (same
+    module tree / creation order as the reference, so the seeded init is the reference's)."""
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    fx = load("cfg2_step.npz")
+    torch.manual_seed(12000)
+    m = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4, ablation_on_qk_channels=8, precision=precision)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    for k, v in m.state_dict().items():
+        if v.is_floating_point():
+            assert abs(v.double().sum().item() - float(fx["init_sum." + k])) <= 1e-6 * max(1.0, abs(float(fx["init_sum." + k]))), k
+    return m, fx
+
+
+def scalar_or(base, n, p_numel, fx):
+    """Tolerance of one gradient tensor at the config-2 geometry.  Scalars (res_scale, gamma) are a
+    single sum over a whole block of cancelling terms: for down4.res_scale the terms' condition
+    number sum|d*r| / |sum d*r| is 2.7e3 (measured on the reference), and the reference's OWN fp32
+    gradient at the block output is 0.37 % off its float64 re-run (ours: 0.51 %), so the worst-case
+    fp32 error of such a scalar is ~10x; they are held to 5e-2 against float64 instead of 5x the
+    reference's one-sample fp32 error."""
+    lim = max(base, 5.0 * float(fx["noise." + n]))
+    return max(lim, 5e-2) if p_numel == 1 else lim
+
+
+def test_cfg2_geometry_fp32_train_step():
+    """Config-2 geometry (64..512, 224^2, P=4, B=2), fp32 compute mode, one full Trainer step:
+    against the reference's own run (cfg2_step.npz) -- logits/loss 1e-4, IoU/Dice, pre-clip
+    per-tensor gradient norms and the small tensors' full gradients against the reference re-run
+    in float64, BN running stats, per-tensor SGD update norms -- and against the CPU oracle run
+    here on the box (full per-tensor gradients, parameters after clip + SGD)."""
+    from dfcsa.loss import metrics_from_stats, sigmoid
+    from dfcsa.optim import FusedSGD
+    from oracle import dfcsa_oracle as O
+    from utils.metrics import calculate_metrics_device
+    m, fx = cfg2_model("fp32")
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    x, t = T(fx["x"]), T(fx["t"])
+    opt.zero_grad()
+    logits = m(x)
+    met = calculate_metrics_device(sigmoid(logits), t, "bce_dice", LP)
+    met["loss"].backward()
+    torch.cuda.synchronize()
+    assert rel(logits, fx["logits"]) < 1e-4
+    assert abs(met["loss"].item() - float(fx["loss"])) < 1e-4 * abs(float(fx["loss"]))
+    iou, dice = metrics_from_stats(met["stats"])
+    assert abs(iou - float(fx["iou"])) < 1e-4 and abs(dice - float(fx["dice"])) < 1e-4
+    pre = {n: p.grad.detach().clone() for n, p in m.named_parameters()}
+    for n, g in pre.items():
+        if n.endswith(ZERO):
+            continue
+        lim = scalar_or(5e-3, n, g.numel(), fx)
+        ref_norm = float(fx["gnorm64." + n])
+        assert abs(g.double().norm().item() - ref_norm) <= lim * ref_norm, (n, g.norm().item(), ref_norm)
+        if "grad64." + n in fx:
+            assert rel(g, fx["grad64." + n]) < lim, n
+    opt.step(max_norm=1.0, skip_if_nan=met["loss"])
+    torch.cuda.synchronize()
+    assert abs(opt.last_norm.item() - float(fx["norm"])) < 1e-3 * float(fx["norm"])
+    sd = m.state_dict()
+    for k, v in sd.items():
+        if "running" in k:
+            assert rel(v.float(), fx["buf." + k]) < 1e-4, k
+    for n, p in m.named_parameters():
+        if n.endswith(ZERO):
+            continue
+        d = (p.detach().double().cpu() - sd0[n].double()).norm().item()
+        assert abs(d - float(fx["dnorm." + n])) <= scalar_or(5e-3, n, p.numel(), fx) * float(fx["dnorm." + n]), n
+
+    # the CPU oracle on this host: full gradient tensors and parameters after clip + SGD
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    sd1, _, ref = O.train_step(sd0, {}, x.cpu(), t.cpu(), 4, LP)
+    clipped = {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
+    for n in O.param_names(sd0):
+        if n.endswith(ZERO):
+            continue
+        lim = max(scalar_or(5e-3, n, clipped[n].numel(), fx), 10.0 * float(fx["noise." + n]))
+        assert rel(clipped[n], ref["grads"][n]) < lim, n
+        assert rel(sd[n].cpu() - sd0[n], sd1[n] - sd0[n]) < lim, n   # the SGD update itself
+
+
+def test_cfg2_geometry_bf16_within_reference_autocast():
+    """Config-2 geometry in the benchmark dtype (bf16): logits within max(1e-2, the reference's
+    autocast error at this geometry), loss/IoU/Dice 1e-2, confident pixels agree."""
+    from dfcsa.loss import sigmoid
+    from utils.metrics import calculate_metrics_device
+    m, fx = cfg2_model("bf16")
+    m = m.cuda().train()
+    with torch.no_grad():
+        logits = m(T(fx["x"]))
+        met = calculate_metrics_device(sigmoid(logits), T(fx["t"]), "bce_dice", LP)
+    r, bar = bf16_bar_check(logits, met["loss"].item(), met["stats"], fx["logits"], fx["loss"], fx["iou"], fx["dice"],
+                            fx["calib.ac_logits_rel"], fx["t"])
+    print(f"cfg2 bf16 logits rel {r:.4e} (bar {bar:.4e})")
+
+
+# ----------------------------------------------------------------------------- checkpoint interop
+def test_reference_checkpoint_resume(tmp_path):
+    """A checkpoint written by the reference's own Trainer.save_checkpoint (tests/golden/
+    ref_checkpoint_epoch_1.pth, utils/trainer.py:267-298) loads with weights_only=True into our
+    Trainer (model, torch.optim.SGD converted to the fused pass, histories), and one more epoch
+    reproduces the reference's resumed epoch (its own load_checkpoint + train_epoch): loss and
+    every parameter -- which requires the SGD momentum to be restored from the checkpoint.  Our own
+    checkpoint of that state keeps the reference's metrics layout (best/worst samples)."""
+    from utils.trainer import Trainer
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    fx = load("ref_checkpoint_resume.npz")
+    model = UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, precision="fp32")
+    opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    cfg = {"training": {"num_epochs": 2, "save_checkpoint_freq": 1, "loss": {"type": "bce_dice", "params": LP}},
+           "logging": {"log_dir": str(tmp_path / "logs"), "images_dir": str(tmp_path / "img"),
+                       "save_best_worst_samples": 1}}
+    b3 = [{"image": torch.from_numpy(fx["x3"]), "mask": torch.from_numpy(fx["t3"]), "filename": ["a3", "b3"]}]
+    tr = Trainer(model, b3, b3, opt, torch.device("cuda"), cfg)
+    ep = tr.load_checkpoint(os.path.join(GOLDEN, "ref_checkpoint_epoch_1.pth"))
+    assert ep == int(fx["epoch"])
+    assert abs(tr.train_losses[0] - float(fx["train_loss1"])) < 1e-12
+    assert abs(tr.val_dice_scores[0] - float(fx["val_dice1"])) < 1e-12
+    loss, iou, dice = tr.train_epoch(ep + 1)
+    torch.cuda.synchronize()
+    assert abs(loss - float(fx["loss3"])) < 1e-4 * abs(float(fx["loss3"]))
+    assert abs(dice - float(fx["dice3"])) < 1e-6 and abs(iou - float(fx["iou3"])) < 1e-6
+    sd = model.state_dict()
+    for k, v in fx.items():
+        if k.startswith("sd3.") and "num_batches" not in k:
+            assert rel(sd[k[4:]].float(), torch.from_numpy(np.asarray(v)).float()) < 1e-4, k
+    va = tr.validate_epoch(b3)
+    tr.save_checkpoint(ep + 1, va, is_best=False)
+    ck = torch.load(str(tmp_path / "logs" / "checkpoints" / f"checkpoint_epoch_{ep + 2}.pth"), weights_only=True)
+    assert set(ck) == {"epoch", "model_state_dict", "optimizer_state_dict", "train_losses", "val_losses",
+                       "train_dice_scores", "val_dice_scores", "train_iou_scores", "val_iou_scores", "best_val_loss",
+                       "metrics"}
+    assert set(ck["metrics"]) == {"loss", "iou", "dice", "best_samples", "worst_samples"}
+    assert len(ck["metrics"]["best_samples"]) == 1 and "image" in ck["metrics"]["best_samples"][0]
+
+
+def test_fused_sgd_resume_matches_torch_sgd():
+    """FusedSGD.load_state_dict before the first forward keeps the loaded momentum (the
+    step after resuming equals torch.optim.SGD loaded from the same state)."""
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from utils.metrics import calculate_metrics_device
+    fx = load("model_small.npz")
+    ck = torch.load(os.path.join(GOLDEN, "ref_checkpoint_epoch_1.pth"), weights_only=True)
+    model = small_model("fp32")
+    model.load_state_dict(ck["model_state_dict"])
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.load_state_dict(ck["optimizer_state_dict"])   # before the first forward: no flat storage yet
+    x, t = T(fx["x2"]), T(fx["t2"])
+    opt.zero_grad()
+    met = calculate_metrics_device(sigmoid(model(x)), t, "bce_dice", LP)
+    met["loss"].backward()
+    g = {n: p.grad.detach().clone() for n, p in model.named_parameters()}
+    w = {n: p.detach().clone() for n, p in model.named_parameters()}
+    opt.step(max_norm=1.0, skip_if_nan=met["loss"])
+    # the same step with torch's clip_grad_norm_ + SGD from the same state
+    ps = [torch.nn.Parameter(w[n].clone()) for n, _ in model.named_parameters()]
+    for p, n in zip(ps, g):
+        p.grad = g[n].clone()
+    topt = torch.optim.SGD(ps, lr=0.01, momentum=0.9, weight_decay=1e-4)
+    topt.load_state_dict(ck["optimizer_state_dict"])
+    torch.nn.utils.clip_grad_norm_(ps, max_norm=1.0)
+    topt.step()
+    for (n, p), q in zip(model.named_parameters(), ps):
+        assert rel(p, q) < 1e-6, n
+
+
+def test_clip_sgd_nan_semantics():
+    """a NaN loss skips the update (reference trainer.py:134-139); an inf loss does not;
+    a NaN gradient norm gives NaN gradients/weights like torch's clip_grad_norm_ (coef = NaN)."""
+    from dfcsa.optim import FusedSGD
+    model = small_model("fp32")
+    model(T(load("model_small.npz")["x1"]))    # materialise the flat storage
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad()
+    for p in model.parameters():
+        p.grad.fill_(0.01)
+    w0 = [p.detach().clone() for p in model.parameters()]
+    opt.step(max_norm=1.0, skip_if_nan=torch.tensor([float("nan")], device="cuda"))
+    assert all(torch.equal(p, q) for p, q in zip(model.parameters(), w0))
+    opt.step(max_norm=1.0, skip_if_nan=torch.tensor([float("inf")], device="cuda"))
+    assert not all(torch.equal(p, q) for p, q in zip(model.parameters(), w0))
+    opt.zero_grad()
+    next(iter(model.parameters())).grad.view(-1)[0] = float("nan")
+    opt.step(max_norm=1.0)
+    assert torch.isnan(opt.last_norm).all()
+    assert all(torch.isnan(p).all() for p in model.parameters())
+
+
+def test_eval_mode_backward_is_refused():
+    """the backward kernels are train-mode BatchNorm; a backward through an eval-mode
+    forward raises instead of returning wrong gradients."""
+    from dfcsa.loss import sigmoid
+    model = small_model("fp32").eval()
+    x = T(load("model_small.npz")["x1"]).requires_grad_(True)
+    out = sigmoid(model(x)).sum()
+    with pytest.raises(NotImplementedError):
+        out.backward()
+
+
+# ----------------------------------------------------------------------------- data parallel
+def test_ddp_step_hip_backward_with_grad_scale():
+    """The DP step without a second GPU: the HIP backward of each half of ddp_shards.npz accumulates
+    into the flat gradient buffer (what the all-reduce SUM of 2 ranks produces), then the fused
+    clip + SGD applies grad_scale = 1/2.  Gradients vs the reference's mean of per-shard gradients;
+    parameters after the step vs the reference SGD step taken with those mean gradients."""
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from oracle import dfcsa_oracle as O
+    from utils.metrics import calculate_metrics_device
+    dd = load("ddp_shards.npz")
+    model = small_model("fp32")
+    sd0 = {k: v.detach().cpu().clone() for k, v in model.state_dict().items()}
+    x, t = T(dd["x"]), T(dd["t"])
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad()
+    for r in range(2):
+        met = calculate_metrics_device(sigmoid(model(x[4 * r:4 * r + 4])), t[4 * r:4 * r + 4], "bce_dice", LP)
+        met["loss"].backward()
+    torch.cuda.synchronize()
+    mean = {}
+    for n, p in model.named_parameters():
+        ref = dd[f"w2.mean_grad.{n}"]
+        mean[n] = torch.from_numpy(ref)
+        if n.endswith(ZERO):
+            continue
+        assert rel(p.grad * 0.5, ref) < 2e-3, n
+    opt.step(max_norm=1.0, grad_scale=0.5, skip_if_nan=met["loss"])
+    torch.cuda.synchronize()
+    sd1, _, norm, _ = O.clip_and_sgd(sd0, mean, {})
+    assert abs(opt.last_norm.item() - norm.item()) < 1e-3 * norm.item()
+    for n, p in model.named_parameters():
+        if n.endswith(ZERO):
+            continue
+        assert rel(p.detach().cpu() - sd0[n], sd1[n] - sd0[n]) < 3e-3, n   # the SGD update
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def test_rccl_bucket_reducer_graph_replay_equals_eager():
+    """bench.py's multi-GPU step rehearsed in-process on one GPU: an RCCL (backend 'nccl') group of
+    world size 1, the bucket reducer forced to several buckets, the NaN-agreement flag, and the
+    whole step captured in one HIP graph; 2 graph replays after 1 eager step equal 3 eager steps."""
+    import torch.distributed as dist
+    from dfcsa.ddp import GradBucketReducer
+    from dfcsa.loss import bce_dice, sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(_free_port())
+    dev = torch.device("cuda:0")
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    try:
+        def build():
+            torch.manual_seed(0)
+            m = UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, precision="fp32").to(dev).train()
+            with torch.no_grad():
+                for n, p in m.named_parameters():
+                    if n.endswith("gamma"):
+                        p.fill_(0.5)
+            return m
+
+        g = torch.Generator().manual_seed(1)
+        x = torch.randn(4, 3, 64, 64, generator=g).to(dev)
+        t = (torch.rand(4, 1, 64, 64, generator=g) > 0.5).float().to(dev)
+
+        def make_step(model):
+            opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+            model(x)
+            red = GradBucketReducer(model, bucket_mb=0.05)
+
+            def step():
+                opt.zero_grad()
+                loss, stats = bce_dice(sigmoid(model(x)), t, 1.0, 1.0)
+                red.start()
+                loss.backward()
+                skip = red.finish(loss)
+                opt.step(max_norm=1.0, grad_scale=red.grad_scale, skip_if_nan=skip)
+                return stats
+            return step, len(red.buckets)
+
+        m_eager = build()
+        step_e, nb = make_step(m_eager)
+        assert nb >= 4
+        for _ in range(3):
+            step_e()
+        torch.cuda.synchronize()
+        m_graph = build()
+        step_g, _ = make_step(m_graph)
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(side):
+            step_g()
+        torch.cuda.current_stream().wait_stream(side)
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):
+            step_g()
+        graph.replay()
+        graph.replay()
+        torch.cuda.synchronize()
+        for (n, a), (_, b) in zip(m_eager.named_parameters(), m_graph.named_parameters()):
+            assert rel(b, a) < 1e-6, n
+    finally:
+        dist.destroy_process_group()

@@ -348,7 +348,7 @@ def test_transunet_full_factory_bf16_train_steps():
         opt.zero_grad()
         met = calculate_metrics_device(sigmoid(m(x)), t, "bce_dice", {})
         met["loss"].backward()
-        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
         losses.append(met["loss"].item())
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses

@@ -70,6 +70,6 @@ def test_zoo_model_bf16_train_steps(name):
         opt.zero_grad()
         met = calculate_metrics_device(sigmoid(m16(x)), t, "bce_dice", LP)
         met["loss"].backward()
-        opt.step(max_norm=1.0, skip_if_nonfinite=met["loss"])
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
         losses.append(met["loss"].item())
     assert all(np.isfinite(losses)) and losses[-1] < losses[0], losses

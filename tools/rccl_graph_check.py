@@ -51,7 +51,7 @@ def main():
             red.start()
             loss.backward()
             red.finish()
-            opt.step(max_norm=1.0, grad_scale=red.grad_scale, skip_if_nonfinite=loss)
+            opt.step(max_norm=1.0, grad_scale=red.grad_scale, skip_if_nan=loss)
             return stats
         return step, len(red.buckets)
 
