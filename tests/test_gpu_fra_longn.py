@@ -1,0 +1,104 @@
+"""Full-resolution attention at the lengths config 5 really runs (512 x 512 input):
+level 1: N = 262,144 tokens, C = 64 (d_qk = 8); level 2: N = 65,536, C = 128 (d_qk = 16).
+
+Reference op: models/unet_dfc_sa_ablation_attention.py:15-26 -- A = softmax_rows(q k^T) (no scale),
+O = A v, y = gamma O + x.  The kernels are called through the C ABI (dfcsa_fra_fwd / _bwd_prep /
+_bwd) on bf16 q|k|v and checked against plain PyTorch fp32 on the SAME bf16 values, computed on
+the GPU in query chunks (the N x N matrix is never held whole):
+  * forward: O and the row log-sum-exp lse on 256 sampled query rows (first / last rows included);
+  * backward: dQ on those rows, dK and dV on 256 sampled keys (needs every query's P column:
+    accumulated over all query chunks with the reference lse).
+Bar: rel <= 1e-2 (north star, bf16) for O, dQ, dK, dV; |lse - lse_ref| <= 1e-2 absolute (lse is
+a log: an absolute error e is a relative error e of every probability of the row).
+Two score scales: typical (score std ~1.4) and sharp (std ~6), which stresses the online-softmax
+rescaling across the 4096 key tiles of a row.
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+CHUNK = 2048
+
+
+def rel(a, b):
+    a, b = a.double(), b.double()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _reference(q, k, v, dy, gamma, rows, keys):
+    """fp32 torch, chunked over queries.  Returns O[rows], lse[rows], dQ[rows], dK[keys], dV[keys]."""
+    N, C = v.shape
+    dKs = torch.zeros(len(keys), q.shape[1], device=q.device, dtype=torch.float64)
+    dVs = torch.zeros(len(keys), C, device=q.device, dtype=torch.float64)
+    vk = v[keys]
+    for c0 in range(0, N, CHUNK):
+        qc = q[c0:c0 + CHUNK]
+        S = qc @ k.t()
+        lse = torch.logsumexp(S, dim=1)
+        S.sub_(lse[:, None]).exp_()                     # P, in place
+        O = S @ v
+        r = (dy[c0:c0 + CHUNK] * O).sum(1)                # rowsum(dy * O)
+        Pk = S[:, keys]                                  # [chunk][keys]
+        dPk = dy[c0:c0 + CHUNK] @ vk.t()                 # dy_i . v_j
+        dSk = gamma * Pk * (dPk - r[:, None])
+        dKs += (dSk.t() @ qc).double()
+        dVs += (gamma * Pk.t() @ dy[c0:c0 + CHUNK]).double()
+        del S, O, Pk, dPk, dSk
+    # the sampled query rows: O, lse and dQ
+    S = q[rows] @ k.t()
+    lse_r = torch.logsumexp(S, dim=1)
+    P = (S - lse_r[:, None]).exp_()
+    O_r = P @ v
+    r_r = (dy[rows] * O_r).sum(1)
+    dS = gamma * P * (dy[rows] @ v.t() - r_r[:, None])
+    dQ_r = dS @ k
+    return O_r, lse_r, dQ_r, dKs.float(), dVs.float()
+
+
+@pytest.mark.parametrize("N,C,scale", [(262144, 64, 0.7), (262144, 64, 1.5), (65536, 128, 0.5), (65536, 128, 1.1)],
+                         ids=["L1_N262144_C64", "L1_N262144_C64_sharp", "L2_N65536_C128", "L2_N65536_C128_sharp"])
+def test_fra_long_n_fwd_bwd_vs_torch_fp32(N, C, scale):
+    from dfcsa._lib import DT_BF16, LIB, call
+    from dfcsa.ops import P, stream
+    Cq = C // 8
+    J = 2 * Cq + C
+    assert LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 0) == 1 and LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 1) == 1
+    dev = torch.device("cuda")
+    g = torch.Generator(device=dev).manual_seed(N + C)
+    qkv = torch.empty(1, N, J, device=dev, dtype=torch.bfloat16)
+    qkv[..., :2 * Cq] = (scale * torch.randn(1, N, 2 * Cq, device=dev, generator=g)).bfloat16()
+    qkv[..., 2 * Cq:] = torch.randn(1, N, C, device=dev, generator=g).bfloat16()
+    x = torch.randn(1, N, C, device=dev, generator=g).bfloat16()
+    dy = torch.randn(1, N, C, device=dev, generator=g).bfloat16()
+    gamma = torch.tensor([0.7], device=dev)
+    o = torch.empty(1, N, C, device=dev, dtype=torch.bfloat16)
+    y = torch.empty_like(o)
+    lse = torch.empty(N, device=dev, dtype=torch.float32)
+    call("dfcsa_fra_fwd", DT_BF16, 1, N, C, Cq, J, P(qkv), P(x), P(gamma), P(o), P(y), P(lse), stream())
+    r = torch.empty(N, device=dev, dtype=torch.float32)
+    call("dfcsa_fra_bwd_prep", DT_BF16, N, C, P(dy), P(o), P(r), stream())
+    dqkv = torch.empty_like(qkv)
+    call("dfcsa_fra_bwd", DT_BF16, 1, N, C, Cq, J, P(qkv), P(dy), P(gamma), P(lse), P(r), P(dqkv), stream())
+    torch.cuda.synchronize()
+
+    q = qkv[0, :, :Cq].float()
+    k = qkv[0, :, Cq:2 * Cq].float()
+    v = qkv[0, :, 2 * Cq:].float()
+    d = dy[0].float()
+    sel = torch.randperm(N, generator=torch.Generator().manual_seed(7))[:254].to(dev)
+    rows = torch.cat([torch.tensor([0, N - 1], device=dev), sel])
+    keys = torch.cat([torch.tensor([0, N - 1], device=dev), torch.randperm(N, generator=torch.Generator().manual_seed(8))[:254].to(dev)])
+    O_r, lse_r, dQ_r, dK_s, dV_s = _reference(q, k, v, d, 0.7, rows, keys)
+
+    errs = {"O": rel(o[0, rows].float(), O_r), "lse_abs": (lse[rows] - lse_r).abs().max().item(),
+            "dQ": rel(dqkv[0, rows, :Cq].float(), dQ_r), "dK": rel(dqkv[0, keys, Cq:2 * Cq].float(), dK_s),
+            "dV": rel(dqkv[0, keys, 2 * Cq:].float(), dV_s)}
+    print(f"N={N} C={C} scale={scale}: " + ", ".join(f"{k} {v:.3e}" for k, v in errs.items()))
+    assert rel(o[0, rows].float(), O_r) <= 1e-2
+    assert (lse[rows] - lse_r).abs().max().item() <= 1e-2
+    assert rel(y[0, rows].float(), 0.7 * O_r + x[0, rows].float()) <= 1e-2
+    assert torch.isfinite(dqkv).all()
+    assert rel(dqkv[0, rows, :Cq].float(), dQ_r) <= 1e-2
+    assert rel(dqkv[0, keys, Cq:2 * Cq].float(), dK_s) <= 1e-2
+    assert rel(dqkv[0, keys, 2 * Cq:].float(), dV_s) <= 1e-2
