@@ -15,12 +15,20 @@ Launch: `python bench.py` (N=1) or, for N > 1, `python -m torch.distributed.run 
                 events on its own stream inside the timed region, vs the 2.5 PFLOP/s dense bf16
                 MFMA peak;
   cpu_baseline  the CPU oracle (oracle/dfcsa_oracle.py, fp32 eager PyTorch = the reference
-                algorithm) timed on this host on a bounded sample (rank 0, N = 1 only).
+                algorithm) timed on this host on the same B=16 workload (rank 0, N = 1 only);
+  step_roofline whole-step fractions: mfma_frac = model FLOP/s / dense bf16
+                peak, hbm_frac = the step's rocprofv3-counted HBM bytes/s / 8 TB/s (profiles/
+                rNN_pmc_step.json), roofline_frac = img/s / the per-layer roofline ceiling (6.1 k);
+  trainer_faithful  the same model/optimizer driven by utils.trainer.Trainer.train_epoch over host
+                batches (H2D copy + the reference's per-step .item() syncs, eager launches), beside
+                the device-resident HIP-graph rate that is `value`.
 """
 import argparse
 import json
 import os
+import subprocess
 import sys
+import tempfile
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -33,6 +41,8 @@ MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip-
 MFMA_F32_PEAK_TFLOPS = 157.3
 HBM_PEAK_GBS = 8000.0
 FWD_BWD_GFLOP_PER_IMG = 201.66   # SURVEY.md section 8d (torch.utils.flop_counter, P=4, 224^2)
+ALG_GB_PER_IMG = 1.07            # minimum bf16 bytes per image
+ROOFLINE_CEILING_IMG_S = 6100.0  # per-layer max(F/P, B/BW) ceiling per GPU
 
 # --model: the BASELINE configs.  Only 'dfc' is the headline line the driver records;
 # the others put the secondary configs' training step on the same clock.  GFLOP/img fwd+bwd
@@ -69,32 +79,84 @@ def pmc_traffic(cls):
         return None, None
 
 
-def cpu_baseline(seconds_budget=25.0):
-    """Time the CPU oracle's full train step (fp32 eager PyTorch, same algorithm) on B=2 images
-    of the same workload; threads = this process's CPU share (<= 16)."""
-    import numpy as np  # noqa: F401
+def cpu_model_name():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    return None
+
+
+def cpu_baseline(batch=16, timed_steps=2):
+    """Time the CPU oracle's full train step (fp32 eager PyTorch, the reference algorithm) on the
+    headline workload: B=16 images of 3x224x224, P=4, features 64..512, 1 warm-up + `timed_steps`
+    steps.  Threads: this process's CPU affinity, capped by OMP_NUM_THREADS when the launcher sets
+    it (the GPU box gives one GPU's job a 16-core share of a larger machine)."""
     from oracle import dfcsa_oracle as O
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
+    aff = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    threads = max(1, min(aff, omp) if omp > 0 else aff)
     torch.set_num_threads(threads)
     from models.unet_dfc_sa_res import UNetDFCSARes
     torch.manual_seed(0)
     ref = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4)
     sd = {k: v.detach().clone() for k, v in ref.state_dict().items()}
     g = torch.Generator().manual_seed(1234)
-    B = 2
-    x = torch.randn(B, 3, 224, 224, generator=g)
-    t = (torch.rand(B, 1, 224, 224, generator=g) > 0.5).float()
+    x = torch.randn(batch, 3, 224, 224, generator=g)
+    t = (torch.rand(batch, 1, 224, 224, generator=g) > 0.5).float()
     sd, bufs, _ = O.train_step(sd, {}, x, t, 4)   # warm-up step
-    n, t0 = 0, time.perf_counter()
-    while True:
+    t0 = time.perf_counter()
+    for _ in range(timed_steps):
         sd, bufs, _ = O.train_step(sd, bufs, x, t, 4)
-        n += 1
+    el = time.perf_counter() - t0
+    return {"value": round(timed_steps * batch / el, 4), "unit": "images/s", "cores": threads, "kind": "port",
+            "cpu_model": cpu_model_name(), "affinity_cpus": aff,
+            "sample": f"{timed_steps} timed train steps (after 1 warm-up) of B={batch} 3x224x224 images, P=4, "
+                      f"features 64..512: oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
+
+
+def trainer_faithful_leg(model, opt, x, t, steps):
+    """The reference's step loop as a user runs it: utils.trainer.Trainer.train_epoch over host
+    (pinned) batches -- H2D copy per batch, the device step, and the reference's per-step host
+    syncs (loss .item(), IoU/Dice as Python floats, trainer.py:142,154-156) -- eager launches."""
+    import contextlib
+    import io
+
+    from utils.trainer import Trainer
+    xb, tb = x.cpu().pin_memory(), t.cpu().pin_memory()
+    loader = [{"image": xb, "mask": tb} for _ in range(steps)]
+    with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as tmp:
+        cfg = {"training": {"num_epochs": 1, "loss": {"type": "bce_dice", "params": {}}},
+               "logging": {"log_dir": os.path.join(tmp, "l"), "images_dir": os.path.join(tmp, "i")}}
+        tr = Trainer(model, loader[:1], loader[:1], opt, x.device, cfg)
+        tr.train_epoch(0)                      # warm-up
+        torch.cuda.synchronize()
+        tr.train_loader = loader
+        t0 = time.perf_counter()
+        tr.train_epoch(0)
+        torch.cuda.synchronize()
         el = time.perf_counter() - t0
-        if el > seconds_budget / 2 or n >= 3:
-            break
-    return {"value": round(n * B / el, 4), "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} timed train steps (after 1 warm-up) of B={B} 3x224x224 images, "
-                      f"oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
+    return {"value": round(steps * x.shape[0] / el, 2), "unit": "images/s", "steps": steps,
+            "ms_per_step": round(el / steps * 1e3, 3),
+            "how": "utils.trainer.Trainer.train_epoch over pinned host batches: H2D copy + per-step "
+                   ".item() syncs as the reference (trainer.py:115-163), eager launches, no HIP graph"}
+
+
+def step_pmc_bytes():
+    """HBM bytes per step from the newest committed whole-step PMC pass (profiles/rNN_pmc_step.json,
+    FETCH_SIZE and WRITE_SIZE summed over every kernel of a step, gfx950 read correction)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_step.json")))
+    if not files:
+        return None, None
+    try:
+        d = json.load(open(files[-1]))
+        return float(d["hbm_bytes_per_step"]), os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
 
 
 def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
@@ -154,6 +216,7 @@ def main():
     ap.add_argument("--model", default="dfc", choices=sorted(MODELS),
                     help="dfc = the BASELINE headline (config 2/3); unet / transunet / fullres = configs 1 / 4 / 5")
     ap.add_argument("--val-steps", type=int, default=600)
+    ap.add_argument("--no-trainer-faithful", action="store_true", help="skip the Trainer.train_epoch rate")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -310,6 +373,11 @@ def main():
                                          "achieved": round(a_, 2), "unit": u_, "frac": round(a_ / p_, 4),
                                          "avg_launch_ms": round(v[1] / max(v[2], 1), 4), "traffic": tr_}
 
+    faithful = None
+    if world == 1 and not args.no_trainer_faithful and headline:
+        log(f"[rank {rank}] Trainer-faithful leg (Trainer.train_epoch, host batches, .item() syncs) ...")
+        faithful = trainer_faithful_leg(model, opt, x, t, args.steps)
+
     vdice = None
     if rank == 0 and world == 1 and not args.no_val_dice and headline:
         log("[rank 0] validation Dice leg (synthetic ellipses) ...")
@@ -323,6 +391,16 @@ def main():
         cpu = cpu_baseline()
     if rank == 0:
         gflop = spec["gflop"].get(S)
+        step_roof = None
+        if headline and gflop:
+            per_gpu = value / world
+            pmc, psrc = step_pmc_bytes()
+            step_roof = {"mfma_frac": round(per_gpu * gflop * 1e9 / (MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+                         "hbm_frac": round(per_gpu * pmc / B / (HBM_PEAK_GBS * 1e9), 4) if pmc else None,
+                         "hbm_frac_algorithmic": round(per_gpu * ALG_GB_PER_IMG / HBM_PEAK_GBS, 4),
+                         "roofline_frac": round(per_gpu / ROOFLINE_CEILING_IMG_S, 4),
+                         "ceiling_img_s_per_gpu": ROOFLINE_CEILING_IMG_S,
+                         "hbm_bytes_per_step": pmc, "hbm_source": psrc}
         out = {"metric": f"training images/sec (fwd+bwd) 3x{S}x{S} {spec['label']}", "value": round(value, 2),
                "unit": "images/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
                "ms_per_step": round(el / args.steps * 1e3, 3), "higher_is_better": True, "scaling": "weak",
@@ -333,7 +411,8 @@ def main():
                           "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
                           "parallelism": f"dp{world}", "final_loss": round(final_loss, 5),
                           "model_tflops": round(value * gflop / 1e3, 2) if gflop else None},
-               "roofline": roof, "cpu_baseline": cpu, "val_dice": vdice}
+               "roofline": roof, "step_roofline": step_roof, "trainer_faithful": faithful,
+               "cpu_baseline": cpu, "val_dice": vdice}
         print(json.dumps(out), flush=True)
     if world > 1:
         dist.barrier()

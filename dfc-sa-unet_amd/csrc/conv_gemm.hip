@@ -867,5 +867,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 9) { g_fra_generic = value; return 0; }
   if (knob == 10) { g_fra_occ = value; return 0; }
   if (knob == 11) { g_ew_tile_elems = value >= 4096 ? value : 16384; return 0; }
+  if (knob == 12) { g_wgrad_fuse_all = value; return 0; }
+  if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
   return DFCSA_EINVAL;
 }

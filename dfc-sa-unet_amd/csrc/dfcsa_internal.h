@@ -32,6 +32,12 @@ struct WgradArgs {
   DivMod dm_hw, dm_w, dm_cseg, dm_cg;
   float* slab;
   int mchunk;
+  // fused split-K reduction (fuse = 1): destination mapping of dfcsa_wgrad_reduce, split count,
+  // ticket counters of this launch's output tiles (zero on entry, re-zeroed by each tile's last
+  // arriving workgroup)
+  int fuse, nsplit, layout, ntaps, Ctot, Creal, ndst;
+  float* dst[3];
+  unsigned* cnt;
 };
 
 // profiling hook (prof.cpp)
@@ -48,6 +54,8 @@ extern int g_wgrad_target;
 extern int g_wgrad_waves;
 extern int g_wgrad_noglds;
 extern int g_wgrad_narrow;
+extern int g_wgrad_fuse_all;
+extern int g_wgrad_fuse_max;
 extern int g_fra_generic;
 extern int g_fra_occ;
 extern int g_ew_tile_elems;

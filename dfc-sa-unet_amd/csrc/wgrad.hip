@@ -8,8 +8,13 @@
 // [pixel][channel] images and the MFMA fragments (8 consecutive pixels per lane) are read with
 // the gfx950 hardware-transposing ds_read_b64_tr_b16 (bf16).  An XOR swizzle of the 16-column
 // blocks keeps those transposed reads bank-conflict-free.  The pixel axis is split into chunks
-// (split-K) with fp32 partial slabs reduced by dfcsa_wgrad_reduce in a fixed order
-// (deterministic, no float atomics), which also permutes into the reference weight layout.
+// (split-K).  With a destination (ndst > 0) and a modest split count the partials are reduced
+// INSIDE the launch: each workgroup publishes its fp32 partial tile with write-through stores,
+// takes a ticket on its output tile, and the last arriving workgroup sums the tile's partials in
+// split order and adds them into the weight gradient in the reference layout (deterministic, no
+// float atomics, no second launch, the partials read back from the on-die caches).  High split
+// counts (the shallow, HBM-bound layers) keep the separate fixed-order reduction
+// (dfcsa_wgrad_reduce).
 //
 // Replaces the weight half of ATen convolution_backward for the convolutions at reference
 // models/unet_dfc_sa_res.py:58, 66, 74, 81, 88 and ConvTranspose2d at :147-156.
@@ -30,8 +35,128 @@ __device__ __forceinline__ int blk_swz(int r, int blk) {
   else return blk ^ (((r >> 1) & 1) | (((r >> 3) & 1) << 1));
 }
 
-template <typename T, int BI>
-struct WgTile;
+// ---------------------------------------------------------------------------------------------
+// Fused split-K epilogue
+// ---------------------------------------------------------------------------------------------
+constexpr int kCntRing = 1 << 18;       // ticket counters (one per output tile of a launch)
+__device__ unsigned g_wg_cnt[kCntRing];
+
+// dW element (i, j) of the GEMM -> the reference weight layout (dfcsa_wgrad_reduce's mapping)
+__device__ __forceinline__ void wgrad_dst_add(const WgradArgs& a, int i, int j, float v) {
+  if (i >= a.NI || j >= a.NJ) return;
+  if (a.layout == 0) {
+    const int rows = a.NI / a.ndst;
+    const int d = i / rows, r = i - d * rows;
+    const int tap = j / a.Ctot, cin = j - tap * a.Ctot;
+    if (cin >= a.Creal || tap >= a.ntaps) return;
+    float* dst = d == 0 ? a.dst[0] : (d == 1 ? a.dst[1] : a.dst[2]);
+    dst[((int64_t)r * a.Creal + cin) * a.ntaps + tap] += v;
+  } else if (a.layout == 2) {
+    if (i >= 2 * a.Ctot + a.Creal) return;
+    const int d = i < a.Ctot ? 0 : (i < 2 * a.Ctot ? 1 : 2);
+    a.dst[d][(int64_t)(i - d * a.Ctot) * a.NJ + j] += v;
+  } else {
+    const int ij = j / a.Ctot, co = j - ij * a.Ctot;
+    a.dst[0][((int64_t)i * a.Ctot + co) * 4 + ij] += v;
+  }
+}
+
+// write-through (sc1) 16-B store: the bytes leave the XCD's L2 at once, so another XCD's
+// workgroup reading them with sc1 loads after the ticket sees them (no L2 write-back fence).
+// The s_nop covers the store-data hazard of >8-byte VMEM stores (the next VALU may not rewrite
+// the data VGPRs for one wait state), which the compiler does not insert after inline asm.
+__device__ __forceinline__ void st_sc1_x4(float* p, f32x4_t v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+// four sc1 16-B loads in flight, one wait
+__device__ __forceinline__ void ld_sc1_x4x4(const float* p0, const float* p1, const float* p2, const float* p3,
+                                            f32x4_t& v0, f32x4_t& v1, f32x4_t& v2, f32x4_t& v3) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc1\n\t"
+      "global_load_dwordx4 %1, %5, off sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc1\n\t"
+      "global_load_dwordx4 %3, %7, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2), "=&v"(v3)
+      : "v"(p0), "v"(p1), "v"(p2), "v"(p3)
+      : "memory");
+}
+
+// The accumulator fragments of one wave: acc[i][j] holds rows rbase + i*16 + (lane>>4)*4 + r,
+// column cbase + j*16 + (lane&15).  fuse == 0: plain [split][NI][NJ] partial slab.  Otherwise
+// nsplit == 1 adds straight into dst; else partial tile -> ticket -> last arriver reduces.
+// Partial tile layout (per output tile, per split): [wave][fragment][lane][4] -- every wave store
+// is 1 KiB contiguous and the reducing lane reads exactly the elements it holds itself.
+template <int FM, int FN, int NW>
+__device__ __forceinline__ void wgrad_epilogue(const WgradArgs& a, f32x4_t (&acc)[FM][FN], int tile, int split,
+                                               int rbase, int cbase, int lane, int wave, int tid, int* last_s) {
+  constexpr int NF = FM * FN;
+  if (!a.fuse) {
+    float* out = a.slab + (size_t)split * a.NI * a.NJ;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int col = cbase + j * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int row = rbase + i * 16 + (lane >> 4) * 4 + r;
+          if (row < a.NI && col < a.NJ) out[(size_t)row * a.NJ + col] = acc[i][j][r];
+        }
+      }
+    return;
+  }
+#ifndef DFCSA_NO_WGRAD_FUSE
+  if (a.nsplit > 1) {
+    constexpr int TILEF = NW * NF * 256;  // floats of one partial tile
+    float* tbase = a.slab + (size_t)tile * a.nsplit * TILEF + (size_t)(wave * NF) * 256 + lane * 4;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) st_sc1_x4(tbase + (size_t)split * TILEF + f * 256, acc[f / FN][f % FN]);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) {
+      const unsigned old = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *last_s = (old == (unsigned)(a.nsplit - 1));
+      if (*last_s) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // for the next launch
+      }
+    }
+    __syncthreads();
+    if (!*last_s) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // sum the partials in split order 0..nsplit-1 (own one from registers: the same bits)
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
+      const float* fb = tbase + f * 256;
+      for (int p0 = 0; p0 < a.nsplit; p0 += 4) {
+        f32x4_t v[4];
+        const float* ptr[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ptr[q] = fb + (size_t)min(p0 + q, a.nsplit - 1) * TILEF;
+        ld_sc1_x4x4(ptr[0], ptr[1], ptr[2], ptr[3], v[0], v[1], v[2], v[3]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int p = p0 + q;
+          if (p == split) sum += acc[f / FN][f % FN];
+          else if (p < a.nsplit) sum += v[q];
+        }
+      }
+      acc[f / FN][f % FN] = sum;
+    }
+  }
+#endif
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = cbase + j * 16 + (lane & 15);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) wgrad_dst_add(a, rbase + i * 16 + (lane >> 4) * 4 + r, col, acc[i][j][r]);
+    }
+}
+
 
 // bf16: rows of BW channels = BW*2 bytes; chunk (8 channels) ch of row r
 template <int BW>
@@ -204,18 +329,8 @@ __global__ void __launch_bounds__(NW * 64) wgrad_kernel(const WgradArgs args) {
     __syncthreads();
   }
 
-  float* out = args.slab + (size_t)split * args.NI * args.NJ;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      int col = j0 + wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        int row = i0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        if (row < args.NI && col < args.NJ) out[(size_t)row * args.NJ + col] = acc[i][j][r];
-      }
-    }
+  wgrad_epilogue<FM, FN, NW>(args, acc, blockIdx.y * gridDim.x + blockIdx.x, split, i0 + wm * WTM, j0 + wn * WTN,
+                             lane, wave, tid, (int*)smem);   // smem is free after the main loop's last barrier
 }
 
 
@@ -352,45 +467,16 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     }
   }
 
-  float* out = args.slab + (size_t)split * args.NI * args.NJ;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int j = 0; j < FN; ++j) {
-      const int col = j0 + wn * WTN + j * 16 + (lane & 15);
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int row = i0 + wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-        if (row < args.NI && col < args.NJ) out[(size_t)row * args.NJ + col] = acc[i][j][r];
-      }
-    }
+  wgrad_epilogue<FM, FN, NW>(args, acc, L % (nJ * nI), split, i0 + wm * WTM, j0 + wn * WTN, lane, wave, tid,
+                             (int*)smem);
 }
 
-// 64 output elements per workgroup, 4 split-ranges per element (threads sub*64 + el: each group
-// of 64 threads reads 64 consecutive elements of one split -> coalesced), 8 loads in flight per
-// thread; the 4 partial sums are combined in a fixed order through LDS (deterministic).
-__global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI, int NJ,
-                                                           int layout, int ntaps, int Ctot, int Creal, int ndst,
-                                                           float* d0, float* d1, float* d2) {
-  __shared__ float part[4][64];
-  const int el = threadIdx.x & 63, sub = threadIdx.x >> 6;
-  const int64_t e = (int64_t)blockIdx.x * 64 + el;
-  const int64_t total = (int64_t)NI * NJ;
-  const int per = (splits + 3) >> 2, k0 = sub * per, k1 = min(splits, k0 + per);
-  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
-  if (e < total) {
-    int k = k0;
-    for (; k + 7 < k1; k += 8) {
-      const float* p = slab + (int64_t)k * total + e;
-      a0 += p[0]; a1 += p[total]; a2 += p[2 * total]; a3 += p[3 * total];
-      a4 += p[4 * total]; a5 += p[5 * total]; a6 += p[6 * total]; a7 += p[7 * total];
-    }
-    for (; k < k1; ++k) a0 += slab[(int64_t)k * total + e];
-  }
-  part[sub][el] = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
-  __syncthreads();
-  if (sub != 0 || e >= total) return;
-  const float s = (part[0][el] + part[1][el]) + (part[2][el] + part[3][el]);
+// 64 output elements per workgroup, SUB split-ranges per element (threads sub*64 + el: each group
+// of 64 threads reads 64 consecutive elements of one split -> coalesced; SUB grows with the split
+// count so that high-split launches get enough threads), 8 loads in flight per thread; the SUB
+// partial sums are combined in a fixed order through LDS (deterministic).
+__device__ __forceinline__ void reduce_dst_add(int64_t e, int NI, int NJ, int layout, int ntaps, int Ctot, int Creal,
+                                               int ndst, float* d0, float* d1, float* d2, float s) {
   int i = (int)(e / NJ), j = (int)(e % NJ);
   if (layout == 0) {
     int rows = NI / ndst;
@@ -411,6 +497,52 @@ __global__ void __launch_bounds__(256) wgrad_reduce_kernel(const float* __restri
     int ij = j / Ctot, co = j - ij * Ctot;
     d0[((int64_t)i * Ctot + co) * 4 + ij] += s;
   }
+}
+
+template <int SUB>
+__global__ void __launch_bounds__(64 * SUB) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI,
+                                                                int NJ, int layout, int ntaps, int Ctot, int Creal,
+                                                                int ndst, float* d0, float* d1, float* d2) {
+  __shared__ float part[SUB][64];
+  const int el = threadIdx.x & 63, sub = threadIdx.x >> 6;
+  const int64_t e = (int64_t)blockIdx.x * 64 + el;
+  const int64_t total = (int64_t)NI * NJ;
+  const int per = (splits + SUB - 1) / SUB, k0 = sub * per, k1 = min(splits, k0 + per);
+  float a0 = 0.f, a1 = 0.f, a2 = 0.f, a3 = 0.f, a4 = 0.f, a5 = 0.f, a6 = 0.f, a7 = 0.f;
+  if (e < total) {
+    int k = k0;
+    for (; k + 7 < k1; k += 8) {
+      const float* p = slab + (int64_t)k * total + e;
+      a0 += p[0]; a1 += p[total]; a2 += p[2 * total]; a3 += p[3 * total];
+      a4 += p[4 * total]; a5 += p[5 * total]; a6 += p[6 * total]; a7 += p[7 * total];
+    }
+    for (; k < k1; ++k) a0 += slab[(int64_t)k * total + e];
+  }
+  part[sub][el] = ((a0 + a1) + (a2 + a3)) + ((a4 + a5) + (a6 + a7));
+  __syncthreads();
+  if (sub != 0 || e >= total) return;
+  float s = part[0][el];
+#pragma unroll
+  for (int q = 1; q < SUB; ++q) s += part[q][el];
+  reduce_dst_add(e, NI, NJ, layout, ntaps, Ctot, Creal, ndst, d0, d1, d2, s);
+}
+
+int launch_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps, int Ctot, int Creal, int ndst,
+                  float* d0, float* d1, float* d2, hipStream_t st) {
+  const int64_t total = (int64_t)NI * NJ;
+  const int blocks = (int)((total + 63) / 64);
+  // >= ~16 splits per thread keeps the loads in flight; more sub-ranges when the blocks are few
+  if (splits >= 128 && blocks < 1024)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(1024), 0, st, slab, splits, NI, NJ, layout, ntaps,
+                       Ctot, Creal, ndst, d0, d1, d2);
+  else if (splits >= 32 && blocks < 2048)
+    hipLaunchKernelGGL(wgrad_reduce_kernel<8>, dim3(blocks), dim3(512), 0, st, slab, splits, NI, NJ, layout, ntaps,
+                       Ctot, Creal, ndst, d0, d1, d2);
+  else
+    hipLaunchKernelGGL(wgrad_reduce_kernel<4>, dim3(blocks), dim3(256), 0, st, slab, splits, NI, NJ, layout, ntaps,
+                       Ctot, Creal, ndst, d0, d1, d2);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 // 64-row (NI <= 64) bf16 tiles take 256 columns when NJ is wide (4 x 2 wave layout of 32x64
@@ -456,12 +588,26 @@ int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
 int g_wgrad_narrow = 1;    // 0 = allow the 64x256 wgrad tile (dfcsa_set_tuning knob 8; measured slower on the L1 3x3)
 int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
+int g_wgrad_fuse_all = 0;  // knob 12: 1 = reduce in-kernel at any split count, -1 = never (separate launch)
+// knob 13: most splits reduced in-kernel.  Default 0 = never: measured on the headline step
+// (tools/wgrad_shapes.py, bench A/B) the last arriver's serialized read of the partials costs more
+// than the separate fixed-order reduction launch (W4 H14: 114 vs 72 us; step 1172 vs 1198 img/s at
+// <= 4 splits, 1149 at <= 16), so the fused path stays selectable, tested, and off.
+int g_wgrad_fuse_max = 0;
 
-extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk) {
+// output tile of the wgrad kernel a launch uses (launch_wgrad's choice)
+void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
+  *BI = NI <= 64 ? 64 : 128;
+  *BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 && NJ >= 512 && !g_wgrad_narrow) ? 256 : 128;
+}
+
+extern "C" int dfcsa_wgrad_fuse_max(void) { return g_wgrad_fuse_max; }
+
+extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk, int64_t* slab_floats) {
   if (M <= 0 || NI <= 0 || NJ <= 0 || !splits || !mchunk) return DFCSA_EINVAL;
   const int kms = dtype == DFCSA_DT_BF16 ? 64 : 32;
-  const int BI = NI <= 64 ? 64 : 128;
-  const int BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 && NJ >= 512 && !g_wgrad_narrow) ? 256 : 128;
+  int BI, BJ;
+  wgrad_tile(NI, NJ, dtype, &BI, &BJ);
   const int tiles = ((NI + BI - 1) / BI) * ((NJ + BJ - 1) / BJ);
   // splits trade occupancy against split-K slab traffic (each split writes NI*NJ fp32 that the
   // reduce reads back): ~2 workgroups per CU is enough to keep the MFMA pipes busy
@@ -483,6 +629,11 @@ extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, i
   s = (M + mc - 1) / mc;
   *splits = s;
   *mchunk = mc;
+  if (slab_floats) {
+    const int64_t plain = (int64_t)s * NI * NJ;
+    const int64_t tiled = (int64_t)tiles * s * BI * BJ;
+    *slab_floats = plain > tiled ? plain : tiled;
+  }
   return 0;
 }
 
@@ -491,6 +642,7 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   if (d->Cg % 8 || d->Cseg % 8 || d->mchunk <= 0 || d->splits <= 0) return DFCSA_EINVAL;
   const int kms = d->dtype == DFCSA_DT_BF16 ? 64 : 32;
   if (d->mchunk % kms) return DFCSA_EINVAL;
+  if (d->ndst < 0 || d->ndst > 3) return DFCSA_EINVAL;
   WgradArgs a;
   a.M = d->M; a.ng = d->ng; a.Cg = d->Cg; a.NI = d->ng * d->Cg;
   for (int i = 0; i < 3; ++i) a.g_ptr[i] = i < d->ng ? d->g_ptr[i] : nullptr;
@@ -500,23 +652,51 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   a.dm_hw = make_divmod(d->Ho * d->Wo); a.dm_w = make_divmod(d->Wo);
   a.dm_cseg = make_divmod(d->Cseg); a.dm_cg = make_divmod(d->Cg);
   a.slab = d->slab; a.mchunk = d->mchunk;
+  a.nsplit = d->splits;
+  a.layout = d->layout; a.ntaps = d->ntaps; a.Ctot = d->Ctot; a.Creal = d->Creal; a.ndst = d->ndst;
+  for (int i = 0; i < 3; ++i) a.dst[i] = i < d->ndst ? d->dst[i] : nullptr;
+  if (d->ndst > 0) {
+    if (d->layout == 2 ? (d->ndst != 3 || d->Ctot <= 0 || 2 * d->Ctot > a.NI) : (a.NI % d->ndst != 0)) return DFCSA_EINVAL;
+    if (d->Ctot <= 0) return DFCSA_EINVAL;
+  }
+  // one split: the kernel adds its tile straight into dst (no slab, no second launch)
+  a.fuse = d->ndst > 0 && (d->splits == 1 ||
+                           (g_wgrad_fuse_all >= 0 && (d->splits <= g_wgrad_fuse_max || g_wgrad_fuse_all > 0)));
+  if (!a.fuse && !d->slab) return DFCSA_EINVAL;
+  a.cnt = nullptr;
+  if (a.fuse && d->splits > 1) {
+    // ticket counters: a ring region per launch, so launches in flight on other streams never
+    // share one (each tile's last arriver re-zeroes its counter)
+    static unsigned* ring = nullptr;
+    static int next = 0;
+    if (!ring && hipGetSymbolAddress((void**)&ring, HIP_SYMBOL(g_wg_cnt)) != hipSuccess) return DFCSA_EINVAL;
+    int BI, BJ;
+    wgrad_tile(a.NI, a.NJ, d->dtype, &BI, &BJ);
+    const int tiles = ((a.NI + BI - 1) / BI) * ((a.NJ + BJ - 1) / BJ);
+    if (tiles > kCntRing) return DFCSA_EINVAL;
+    if (next + tiles > kCntRing) next = 0;
+    a.cnt = ring + next;
+    next += tiles;
+  }
   hipStream_t st = (hipStream_t)stream;
   double flops = 2.0 * a.M * a.NI * a.NJ;
-  ProfScope prof(DFCSA_PROF_WGRAD, st, flops);
+  ProfScope prof(DFCSA_PROF_WGRAD, st, flops);   // the class covers the reduction launch too
+  int rc;
   if (d->dtype == DFCSA_DT_BF16)
-    return a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st) : launch_wgrad<bf16_t, 128>(a, d->splits, st);
-  return a.NI <= 64 ? launch_wgrad<float, 64>(a, d->splits, st) : launch_wgrad<float, 128>(a, d->splits, st);
+    rc = a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st) : launch_wgrad<bf16_t, 128>(a, d->splits, st);
+  else
+    rc = a.NI <= 64 ? launch_wgrad<float, 64>(a, d->splits, st) : launch_wgrad<float, 128>(a, d->splits, st);
+  if (rc) return rc;
+  if (d->ndst > 0 && !a.fuse)
+    return launch_reduce(d->slab, d->splits, a.NI, a.NJ, d->layout, d->ntaps, d->Ctot, d->Creal, d->ndst, a.dst[0],
+                         a.dst[1], a.dst[2], st);
+  return 0;
 }
 
 extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                                   int Ctot, int Creal, int ndst, float* const* dst, void* stream) {
   if (!slab || !dst || ndst < 1 || ndst > 3) return DFCSA_EINVAL;
   if (layout == 2 ? (ndst != 3 || Ctot <= 0 || 2 * Ctot > NI) : (NI % ndst != 0)) return DFCSA_EINVAL;
-  int64_t total = (int64_t)NI * NJ;
-  int blocks = (int)((total + 63) / 64);
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, slab, splits,
-                     NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
-                     ndst > 2 ? dst[2] : nullptr);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
+  return launch_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
+                       ndst > 2 ? dst[2] : nullptr, (hipStream_t)stream);
 }

@@ -74,7 +74,8 @@ class WgradDesc(ctypes.Structure):
                 ("seg_dw", ctypes.c_int * MAX_SEG),
                 ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("Hi", ctypes.c_int), ("Wi", ctypes.c_int),
                 ("stride", ctypes.c_int), ("slab", ctypes.c_void_p), ("splits", ctypes.c_int),
-                ("mchunk", ctypes.c_int)]
+                ("mchunk", ctypes.c_int), ("layout", ctypes.c_int), ("ntaps", ctypes.c_int), ("Ctot", ctypes.c_int),
+                ("Creal", ctypes.c_int), ("ndst", ctypes.c_int), ("dst", ctypes.c_void_p * 3)]
 
 
 class PackEntry(ctypes.Structure):

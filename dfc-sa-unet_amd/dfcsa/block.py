@@ -365,8 +365,8 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
         BN = B * N
         # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums, dpooled = dqkv Wqkv;
         # the stacked q/k/v rows go straight into the three weight / bias gradients
-        slab, splits, NI, NJ = ops.wgrad(f32, [dqkv], J, [(pooled, 0, 0)], C, (1, BN, 1), (BN, 1))
-        ops.wgrad_reduce(slab, splits, NI, NJ, 2, 1, Cq, C, [grad_of(qw), grad_of(kw), grad_of(vw)])
+        ops.conv_wgrad_into(f32, [dqkv], J, [(pooled, 0, 0)], C, (1, BN, 1), (BN, 1),
+                            [grad_of(qw), grad_of(kw), grad_of(vw)], 1, Cq, C, layout=2)
         call("dfcsa_slab_colsum3", P(dqkv), BN, J, Cq, Cq, P(grad_of(lsa.query_conv.bias)),
              P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)), stream())
         Kj = rup(J, ops.KALIGN)

@@ -80,10 +80,9 @@ def core_backward(mod, saved, dy, dtype, pk):
     else:
         call("dfcsa_fra_bwd", T, B, N, C, Cq, Jp, P(qkv), P(dy), P(mod.gamma), P(lse), P(r), P(dqkv), stream())
     grid, hw = (B, H, W), (H, W)
-    slab, splits, NI, NJ = ops.wgrad(dtype, [dqkv], Jp, [(a, 0, 0)], C, grid, hw)
-    ops.wgrad_reduce(slab, splits, NI, NJ, 2, 1, Cq, C, [_grad_of(mod.query_conv.weight),
-                                                         _grad_of(mod.key_conv.weight),
-                                                         _grad_of(mod.value_conv.weight)])
+    ops.conv_wgrad_into(dtype, [dqkv], Jp, [(a, 0, 0)], C, grid, hw,
+                        [_grad_of(mod.query_conv.weight), _grad_of(mod.key_conv.weight),
+                         _grad_of(mod.value_conv.weight)], 1, Cq, C, layout=2)
     nt = ops.ntiles_ew(M, Jp)
     part = torch.empty(nt * Jp, device=dev, dtype=f32)
     call("dfcsa_channel_sum", T, M, Jp, P(dqkv), P(part), stream())

@@ -80,14 +80,13 @@ def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=N
     call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
 
 
-def wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride=1):
-    """Returns (slab, splits) with slab [splits][ng*Cg][nseg*Cseg] fp32."""
+def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride):
     B, Ho, Wo = grid
     M = B * Ho * Wo
     NI, NJ = len(gs) * Cg, len(segs) * Cseg
-    splits, mchunk = ctypes.c_int(), ctypes.c_int()
-    call("dfcsa_wgrad_plan", M, NI, NJ, dt(dtype), ctypes.addressof(splits), ctypes.addressof(mchunk))
-    slab = torch.empty(splits.value * NI * NJ, device=gs[0].device, dtype=torch.float32)
+    splits, mchunk, floats = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    call("dfcsa_wgrad_plan", M, NI, NJ, dt(dtype), ctypes.addressof(splits), ctypes.addressof(mchunk),
+         ctypes.addressof(floats))
     d = _lib.WgradDesc()
     d.dtype = dt(dtype)
     d.M, d.ng, d.Cg = M, len(gs), Cg
@@ -101,10 +100,19 @@ def wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride=1):
     d.Ho, d.Wo = Ho, Wo
     d.Hi, d.Wi = in_hw
     d.stride = stride
-    d.slab = P(slab)
     d.splits, d.mchunk = splits.value, mchunk.value
+    return d, floats.value, NI, NJ
+
+
+def wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride=1):
+    """Split-K partials only: returns (slab, splits, NI, NJ) with slab [splits][NI][NJ] fp32 (the
+    caller reduces with wgrad_reduce)."""
+    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
+    slab = torch.empty(floats, device=gs[0].device, dtype=torch.float32)
+    d.slab = P(slab)
+    d.ndst = 0
     call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
-    return slab, splits.value, NI, NJ
+    return slab, d.splits, NI, NJ
 
 
 def wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts):
@@ -114,8 +122,15 @@ def wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts):
 
 
 def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, Creal, layout=0, stride=1):
-    slab, splits, NI, NJ = wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
-    wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, grads)
+    """grads[d] += the weight gradient in the reference layout, in one dfcsa_conv_wgrad call (the
+    split-K reduction runs inside the kernel, or as its second launch at high split counts)."""
+    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
+    slab = torch.empty(floats, device=gs[0].device, dtype=torch.float32) if d.splits > 1 else None
+    d.slab = P(slab)
+    d.layout, d.ntaps, d.Ctot, d.Creal, d.ndst = layout, ntaps, Ctot, Creal, len(grads)
+    for i, t in enumerate(grads):
+        d.dst[i] = P(t)
+    call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
 
 
 # --------------------------------------------------------------------------- packing

@@ -65,10 +65,17 @@ int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile (ntiles = ceil(M / mtil
  * Weight gradient (MFMA, reduction over pixels).  Replaces the weight half of
  * convolution_backward for every conv of the block (unet_dfc_sa_res.py:58,66,74,81,88) and
  * of ConvTranspose2d (:147-156).
- * slab[s][i][j] = sum over pixels m in chunk s of G[m][i] * X[m][j], where G = concat of
- * ng tensors [M][Cg] (i = src*Cg + c) and X is gathered like dfcsa_conv_desc's A (j = seg*Cseg+c).
- * slab: [splits][NI][NJ] fp32 with NI = ng*Cg, NJ = nseg*Cseg; splits/mchunk from
- * dfcsa_wgrad_plan.
+ * partial[s][i][j] = sum over pixels m in chunk s of G[m][i] * X[m][j], where G = concat of
+ * ng tensors [M][Cg] (i = src*Cg + c) and X is gathered like dfcsa_conv_desc's A (j = seg*Cseg+c),
+ * NI = ng*Cg, NJ = nseg*Cseg; splits/mchunk/slab size from dfcsa_wgrad_plan.
+ * ndst == 0: slab = [splits][NI][NJ] fp32, reduced by the caller (dfcsa_wgrad_reduce).
+ * ndst > 0: the launch also reduces the partials and adds them to dst[] in `layout` (the mapping
+ *   of dfcsa_wgrad_reduce), by a fixed-order reduction launch after the wgrad kernel; or, with
+ *   splits <= dfcsa_wgrad_fuse_max() (0 by default, tuning knob 13), inside the wgrad kernel:
+ *   every workgroup publishes its fp32 partial tile (write-through stores), takes a ticket on its
+ *   output tile, and the LAST arriving workgroup of the tile sums the partials in split order
+ *   0..splits-1 and adds the sum to dst (deterministic, no float atomics, no second launch).
+ *   slab must hold *slab_floats floats either way.
  * ---------------------------------------------------------------------------------------- */
 typedef struct {
   int dtype;
@@ -82,10 +89,13 @@ typedef struct {
   int Ho, Wo, Hi, Wi, stride;
   float* slab;
   int splits, mchunk;
+  int layout, ntaps, Ctot, Creal, ndst;
+  float* dst[3];
 } dfcsa_wgrad_desc;
-int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk);
+int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk, int64_t* slab_floats);
+int dfcsa_wgrad_fuse_max(void);
 int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
-/* grad += sum_s slab[s] mapped to the reference weight layout.
+/* grad += sum_s slab[s] (slab [splits][NI][NJ]) mapped to the reference weight layout.
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
  *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.
  *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij].

@@ -39,7 +39,7 @@ def test_ctypes_binding_loads_and_parses_header():
 def test_descriptor_layouts_match_c(tmp_path):
     from dfcsa import _lib
     fields = [("dfcsa_conv_desc", _lib.ConvDesc, ("weight", "Wout")),
-              ("dfcsa_wgrad_desc", _lib.WgradDesc, ("slab", "mchunk")),
+              ("dfcsa_wgrad_desc", _lib.WgradDesc, ("slab", "mchunk", "ndst", "dst")),
               ("dfcsa_pack_entry", _lib.PackEntry, ("w0", "a")),
               ("dfcsa_wstd_entry", _lib.WstdEntry, ("K", "pad")),
               ("dfcsa_resample_desc", _lib.ResampleDesc, ("kk", "row0")),
@@ -64,12 +64,19 @@ def test_descriptor_layouts_match_c(tmp_path):
 def test_host_side_planning_functions():
     """Pure host entry points (no device work) can run without a GPU."""
     from dfcsa._lib import LIB as L
-    s, mc = ctypes.c_int(), ctypes.c_int()
-    assert L.dfcsa_wgrad_plan(802816, 64, 1152, 1, ctypes.addressof(s), ctypes.addressof(mc)) == 0
+    s, mc, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    A = ctypes.addressof
+    assert L.dfcsa_wgrad_plan(802816, 64, 1152, 1, A(s), A(mc), A(fl)) == 0
     assert mc.value % 64 == 0 and s.value * mc.value >= 802816 and (s.value - 1) * mc.value < 802816
-    assert L.dfcsa_wgrad_plan(3136, 1024, 4608, 0, ctypes.addressof(s), ctypes.addressof(mc)) == 0
+    assert fl.value >= s.value * 64 * 1152
+    assert L.dfcsa_wgrad_plan(3136, 1024, 4608, 0, A(s), A(mc), A(fl)) == 0
     assert mc.value % 32 == 0 and s.value >= 1
-    assert L.dfcsa_wgrad_plan(0, 1, 1, 1, ctypes.addressof(s), ctypes.addressof(mc)) != 0
+    # a deep bf16 layer: few splits; the slab also covers the tile-ordered partials of the
+    # in-kernel reduction (off by default: dfcsa_wgrad_fuse_max() == 0, tuning knob 13)
+    assert L.dfcsa_wgrad_plan(3136, 1024, 4608, 1, A(s), A(mc), A(fl)) == 0
+    assert 1 < s.value <= 16 and fl.value >= s.value * 1024 * 4608
+    assert L.dfcsa_wgrad_fuse_max() == 0
+    assert L.dfcsa_wgrad_plan(0, 1, 1, 1, A(s), A(mc), A(fl)) != 0
     assert L.dfcsa_ew_ntiles(802816, 64) == 3136   # 16384-element tiles: 256 pixels of 64 channels
     assert L.dfcsa_lsa_pool_splits(224, 4) >= 1 and L.dfcsa_lsa_pool_splits(14, 32) == 1
     assert 1 <= L.dfcsa_sumsq_nparts(29052083) <= 1024

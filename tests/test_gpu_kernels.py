@@ -97,6 +97,47 @@ def test_conv_transpose_fwd_bwd(dtype, tol):
     assert rel(modg.bias.grad, mod.bias.grad) < tol
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,Cs,C,H,fuse_all", [(2, 512, 256, 14, 0), (4, 256, 512, 16, 0), (16, 64, 64, 56, 1),
+                                               (1, 64, 64, 8, 0)])
+def test_wgrad_fused_split_reduction(dtype, B, Cs, C, H, fuse_all):
+    """The split-K reduction inside the wgrad kernel (last-arriving workgroup per output tile sums
+    the partials in split order): against torch fp32, bitwise reproducible run to run, and it
+    ACCUMULATES into the gradient.  Shapes: deep layers (2-16 splits), a high-split shallow layer
+    forced through the fused path (tuning knob 12), and a single-split case (direct store)."""
+    import ctypes
+
+    import dfcsa
+    from dfcsa._lib import LIB
+    torch.manual_seed(5)
+    tol = 2e-6 if dtype == torch.float32 else 1e-2
+    x = q(torch.randn(B, Cs, H, H), dtype)
+    g = q(torch.randn(B, C, H, H), dtype)
+    w = torch.zeros(C, Cs, 3, 3, requires_grad=True)
+    F.conv2d(x.requires_grad_(False), w, padding=1).backward(g)
+    ref = w.grad + 0.25
+    xh, gh = nhwc(x, dtype), nhwc(g, dtype)
+    segs = [(xh, kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+    sp, mc, fl = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
+    LIB.dfcsa_wgrad_plan(B * H * H, C, 9 * Cs, ops.dt(dtype), ctypes.addressof(sp), ctypes.addressof(mc),
+                         ctypes.addressof(fl))
+    outs = []
+    dfcsa.set_tuning(12, fuse_all)
+    dfcsa.set_tuning(13, 16)      # exercise the in-kernel reduction up to 16 splits
+    assert fuse_all or sp.value <= LIB.dfcsa_wgrad_fuse_max()
+    try:
+        for _ in range(2):
+            gw = torch.full((C, Cs, 3, 3), 0.25, device="cuda")
+            ops.conv_wgrad_into(dtype, [gh], C, segs, Cs, (B, H, H), (H, H), [gw], 9, Cs, Cs)
+            outs.append(gw)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(12, 0)
+        dfcsa.set_tuning(13, 0)
+    assert rel(outs[0], ref) < tol, (sp.value, rel(outs[0], ref))
+    assert torch.equal(outs[0], outs[1]), "fused split-K reduction is not bitwise reproducible"
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (3, 64, 2, 64, 14, 14), (2, 32, 1, 136, 20, 20)])
 @pytest.mark.parametrize("variant", [(0, 0, 1), (1, 4, 1), (1, 8, 1), (0, 4, 1), (0, 8, 0)])  # knobs 7, 6, 8

@@ -333,76 +333,20 @@ def test_ddp_step_hip_backward_with_grad_scale():
         assert rel(p.detach().cpu() - sd0[n], sd1[n] - sd0[n]) < 3e-3, n   # the SGD update
 
 
-def _free_port():
-    s = socket.socket()
-    s.bind(("127.0.0.1", 0))
-    port = s.getsockname()[1]
-    s.close()
-    return port
-
-
 def test_rccl_bucket_reducer_graph_replay_equals_eager():
-    """bench.py's multi-GPU step rehearsed in-process on one GPU: an RCCL (backend 'nccl') group of
-    world size 1, the bucket reducer forced to several buckets, the NaN-agreement flag, and the
-    whole step captured in one HIP graph; 2 graph replays after 1 eager step equal 3 eager steps."""
-    import torch.distributed as dist
-    from dfcsa.ddp import GradBucketReducer
-    from dfcsa.loss import bce_dice, sigmoid
-    from dfcsa.optim import FusedSGD
-    from models.unet_dfc_sa_res import UNetDFCSARes
-    os.environ["MASTER_ADDR"] = "127.0.0.1"
-    os.environ["MASTER_PORT"] = str(_free_port())
-    dev = torch.device("cuda:0")
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
-    try:
-        def build():
-            torch.manual_seed(0)
-            m = UNetDFCSARes(3, 1, [8, 16, 32, 64], pool_size=4, precision="fp32").to(dev).train()
-            with torch.no_grad():
-                for n, p in m.named_parameters():
-                    if n.endswith("gamma"):
-                        p.fill_(0.5)
-            return m
-
-        g = torch.Generator().manual_seed(1)
-        x = torch.randn(4, 3, 64, 64, generator=g).to(dev)
-        t = (torch.rand(4, 1, 64, 64, generator=g) > 0.5).float().to(dev)
-
-        def make_step(model):
-            opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
-            model(x)
-            red = GradBucketReducer(model, bucket_mb=0.05)
-
-            def step():
-                opt.zero_grad()
-                loss, stats = bce_dice(sigmoid(model(x)), t, 1.0, 1.0)
-                red.start()
-                loss.backward()
-                skip = red.finish(loss)
-                opt.step(max_norm=1.0, grad_scale=red.grad_scale, skip_if_nan=skip)
-                return stats
-            return step, len(red.buckets)
-
-        m_eager = build()
-        step_e, nb = make_step(m_eager)
-        assert nb >= 4
-        for _ in range(3):
-            step_e()
-        torch.cuda.synchronize()
-        m_graph = build()
-        step_g, _ = make_step(m_graph)
-        side = torch.cuda.Stream()
-        side.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(side):
-            step_g()
-        torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):
-            step_g()
-        graph.replay()
-        graph.replay()
-        torch.cuda.synchronize()
-        for (n, a), (_, b) in zip(m_eager.named_parameters(), m_graph.named_parameters()):
-            assert rel(b, a) < 1e-6, n
-    finally:
-        dist.destroy_process_group()
+    """bench.py's multi-GPU step rehearsed on one GPU (tools/rccl_graph_check.py, in a child process so
+    the RCCL communicator lives and dies with it): an RCCL (backend 'nccl') group of world size 1,
+    the bucket reducer forced to several buckets, the NaN-agreement flag, and the whole step
+    captured in one HIP graph; 2 graph replays after 1 eager step equal 3 eager steps."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    env.pop("MASTER_PORT", None)
+    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_graph_check.py")], capture_output=True,
+                       text=True, timeout=240, env=env)
+    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and line, (r.returncode, r.stdout[-2000:], r.stderr[-2000:])
+    res = json.loads(line[-1])
+    assert res["ok"], res

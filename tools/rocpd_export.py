@@ -4,6 +4,12 @@
       per-kernel Name,Calls,TotalDurationNs,AverageNs,Percentage (the --stats layout)
   python tools/rocpd_export.py classes <kernel-trace db> <out.json>
       launches / average duration of the bench's roofline kernel classes
+  python tools/rocpd_export.py step <FETCH_SIZE db> <WRITE_SIZE db> <out.json>
+      HBM bytes of ONE whole training step (the dispatches after the second-to-last clip_sgd
+      launch up to the last one) in total and per kernel group (bench.py's step_roofline.hbm_frac)
+  python tools/rocpd_export.py sq <SQ/GRBM counter db> <out.json>
+      per kernel group: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_MFMA, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE,
+      GRBM_GUI_ACTIVE and the MFMA-busy fraction = MFMA busy cycles / (GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
   python tools/rocpd_export.py traffic <FETCH_SIZE db> <WRITE_SIZE db> <out.json>
       HBM bytes per dispatch of the kernels whose name contains `pattern` (default conv_gemm),
       corrected as /opt/skills/guides/MI355X_MICROARCH.md prescribes for gfx950: FETCH_SIZE and
@@ -94,10 +100,98 @@ def traffic_all(fdb, wdb, out):
         print(c, r["launches"], round(r["hbm_bytes_per_launch"] / 1e6, 2), "MB/launch")
 
 
+GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<")),
+          ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_reduce_kernel")),
+          ("conv1x1_stream", ("conv1x1_stream_kernel",)),
+          ("ew_red (BN/gate/attention backward elementwise + partial sums)", ("ew_red_kernel",)),
+          ("ew_fwd (BN apply, gate fusion, block output)", ("ew_fwd_kernel",)),
+          ("bn_and_slab_finalizers", ("rows_reduce_kernel", "bn_finalize_kernel", "bn_bwd_finalize_kernel",
+                                      "slab_colsum", "sum_scalar_kernel")),
+          ("lsa (pooled attention)", ("lsa_",)),
+          ("maxpool", ("maxpool2",)),
+          ("optimizer", ("sumsq_kernel", "clip_sgd_kernel", "set_flag_kernel")),
+          ("pack_plan", ("pack_plan_kernel",)),
+          ("loss/head/input", ("bce_dice", "sigmoid", "head_", "pack_input")))
+
+
+def group_of(name):
+    for g, pats in GROUPS:
+        if any(p in name for p in pats):
+            return g
+    return "other"
+
+
+def _dispatch_rows(db, counter):
+    c = sqlite3.connect(db)
+    return list(c.execute("select dispatch_id, kernel_name, sum(value) from counters_collection where counter_name = ? "
+                          "group by dispatch_id order by dispatch_id", (counter,)))
+
+
+def _last_step(rows):
+    ends = [i for i, (_, n, _) in enumerate(rows) if "clip_sgd_kernel" in n]
+    if len(ends) < 2:
+        raise SystemExit("need >= 2 clip_sgd dispatches (2 steps) in the counter pass")
+    return rows[ends[-2] + 1: ends[-1] + 1]
+
+
+def step(fdb, wdb, out):
+    rd = _last_step(_dispatch_rows(fdb, "FETCH_SIZE"))
+    wr = _last_step(_dispatch_rows(wdb, "WRITE_SIZE"))
+    groups = defaultdict(lambda: {"launches": 0, "read_bytes": 0.0, "write_bytes": 0.0})
+    for _, n, v in rd:
+        g = groups[group_of(n)]
+        g["launches"] += 1
+        g["read_bytes"] += 2.0 * v * 1024.0
+    for _, n, v in wr:
+        groups[group_of(n)]["write_bytes"] += v * 1024.0
+    tot_r = sum(g["read_bytes"] for g in groups.values())
+    tot_w = sum(g["write_bytes"] for g in groups.values())
+    res = {"hbm_bytes_per_step": tot_r + tot_w, "read_bytes_per_step": tot_r, "write_bytes_per_step": tot_w,
+           "launches_per_step": len(rd),
+           "correction": "read = 2 x FETCH_SIZE KiB (gfx950 half-count), write = WRITE_SIZE KiB; one step = the "
+                         "dispatches after the second-to-last clip_sgd launch through the last one",
+           "groups": {k: {"launches": v["launches"], "read_MB": round(v["read_bytes"] / 1e6, 2),
+                          "write_MB": round(v["write_bytes"] / 1e6, 2)}
+                      for k, v in sorted(groups.items(), key=lambda kv: -(kv[1]["read_bytes"] + kv[1]["write_bytes"]))}}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps({k: v for k, v in res.items() if k != "groups"}))
+
+
+def sq(db, out):
+    c = sqlite3.connect(db)
+    per = defaultdict(lambda: defaultdict(float))
+    launches = defaultdict(set)
+    for did, name, cn, v in c.execute("select dispatch_id, kernel_name, counter_name, sum(value) from counters_collection "
+                                      "group by dispatch_id, counter_name"):
+        g = group_of(name)
+        per[g][cn] += v
+        launches[g].add(did)
+    res = {}
+    for g, d in per.items():
+        r = {k: v for k, v in d.items()}
+        r["launches"] = len(launches[g])
+        if d.get("GRBM_GUI_ACTIVE") and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+            r["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
+        if d.get("SQ_LDS_IDX_ACTIVE"):
+            r["lds_bank_conflict_frac"] = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_LDS_IDX_ACTIVE"]
+        res[g] = r
+    res["_definition"] = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs), "
+                          "summed over the group's dispatches; lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / "
+                          "SQ_LDS_IDX_ACTIVE")
+    json.dump(res, open(out, "w"), indent=1)
+    for g, r in res.items():
+        if g[0] != "_":
+            print(g, r.get("launches"), round(r.get("mfma_busy_frac", float("nan")), 4))
+
+
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "classes":
         classes(sys.argv[2], sys.argv[3])
+    elif sys.argv[1] == "step":
+        step(sys.argv[2], sys.argv[3], sys.argv[4])
+    elif sys.argv[1] == "sq":
+        sq(sys.argv[2], sys.argv[3])
     else:
         traffic_all(*sys.argv[2:5])
