@@ -126,6 +126,7 @@ def trainer_faithful_leg(model, opt, x, t, steps):
     import io
 
     from utils.trainer import Trainer
+    os.environ.setdefault("TQDM_DISABLE", "1")   # the epoch progress bar would flood stderr
     xb, tb = x.cpu().pin_memory(), t.cpu().pin_memory()
     loader = [{"image": xb, "mask": tb} for _ in range(steps)]
     with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as tmp:
