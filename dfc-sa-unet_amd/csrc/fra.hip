@@ -544,10 +544,10 @@ fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
 //   P = 1 and dPy' = 0 contribute exactly nothing: no per-score masking.
 template <int CQ, int C, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
+fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                         const float* __restrict__ lse, const float* __restrict__ rr,
-                                                        bf16_t* __restrict__ dqkv) {
+                                                        bf16_t* __restrict__ dqkv, float* __restrict__ part) {
   constexpr int QT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
   constexpr int QBy = QT * KC * 2, DBy = QT * C * 2, LBy = QT * 4 * 2;
@@ -556,10 +556,10 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int b = blockIdx.z;
+  const int b = blockIdx.z, ch = blockIdx.y, c0 = ch * C;   // value-column chunk (wide layers)
   const int kw0 = (blockIdx.x * 4 + wave) * 32;
   const bf16_t* base = qkv + (size_t)b * N * ldq;
-  const bf16_t* dyb = dy + (size_t)b * N * C;
+  const bf16_t* dyb = dy + (size_t)b * N * ldd + c0;
   const float* lseb = lse + (size_t)b * N;
   const float* rrb = rr + (size_t)b * N;
 
@@ -574,7 +574,7 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     qk_load_global<CQ>(kf[kb], base + (size_t)key * ldq + CQ, ok, g);
 #pragma unroll
     for (int dc = 0; dc < NDC; ++dc)
-      vf[kb][dc] = ok ? *(const bf16x8_t*)(base + (size_t)key * ldq + 2 * CQ + 32 * dc + 8 * g)
+      vf[kb][dc] = ok ? *(const bf16x8_t*)(base + (size_t)key * ldq + 2 * CQ + c0 + 32 * dc + 8 * g)
                       : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
   }
   f32x4_t dva[2][NCB], dka[2][NDB];
@@ -594,12 +594,12 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     if (tid < QT) {
       const int q = qt0 + tid;
       ls[tid] = q < N ? lseb[q] * kL2E : 0.f;
-      ls[QT + tid] = q < N ? -rrb[q] : 0.f;
+      ls[QT + tid] = (q < N && ch == 0) ? -rrb[q] : 0.f;  // -r enters dP once, in chunk 0
     }
   };
   const int ntiles = (N + QT - 1) / QT;
   sq.load(base, ldq, 0, N, tid);
-  sd.load(dyb, C, 0, N, tid);
+  sd.load(dyb, ldd, 0, N, tid);
   sq.template store<KC>(smem, tid);
   sd.template store<C>(smem + QBy, tid);
   stage_scalars(smem, 0);
@@ -609,7 +609,7 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     const int qt0 = t * QT;
     if (t + 1 < ntiles) {
       sq.load(base, ldq, qt0 + QT, N, tid);
-      sd.load(dyb, C, qt0 + QT, N, tid);
+      sd.load(dyb, ldd, qt0 + QT, N, tid);
     }
     const char* Qi = smem + (t & 1) * TB;
     const char* Di = Qi + QBy;
@@ -686,14 +686,19 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
       const f32x4_t v = dva[kb][cb] * gm;
-      *(uint2*)(out + 2 * CQ + cb * 16 + 4 * g) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+      *(uint2*)(out + 2 * CQ + c0 + cb * 16 + 4 * g) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
     }
 #pragma unroll
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
       if (d < CQ) {
-        const f32x4_t v = dka[kb][db] * gm;
-        *(uint2*)(out + CQ + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        if (part) {  // wide layers: this chunk's share of dK (fp32, unscaled), summed by fra_wide_finish
+          float* pp = part + (((size_t)ch * gridDim.z + b) * N + key) * CQ + d;
+          *(float4*)pp = make_float4(dka[kb][db][0], dka[kb][db][1], dka[kb][db][2], dka[kb][db][3]);
+        } else {
+          const f32x4_t v = dka[kb][db] * gm;
+          *(uint2*)(out + CQ + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
       }
     }
   }
@@ -707,10 +712,10 @@ fra_bwd_dkv_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
 //   masked on the last tile only (tile-uniform branch).
 template <int CQ, int C, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
-fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
+fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                        const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                        const float* __restrict__ lse, const float* __restrict__ rr,
-                                                       bf16_t* __restrict__ dqkv) {
+                                                       bf16_t* __restrict__ dqkv, float* __restrict__ part) {
   constexpr int KT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
   constexpr int KBy = KT * KC * 2, VBy = KT * C * 2, TB = KBy + VBy;
@@ -718,10 +723,10 @@ fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
   __shared__ __attribute__((aligned(16))) char smem[2 * TB];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
-  const int b = blockIdx.z;
+  const int b = blockIdx.z, ch = blockIdx.y, c0 = ch * C;   // value-column chunk (wide layers)
   const int qw0 = (blockIdx.x * 4 + wave) * 32;
   const bf16_t* base = qkv + (size_t)b * N * ldq;
-  const bf16_t* dyb = dy + (size_t)b * N * C;
+  const bf16_t* dyb = dy + (size_t)b * N * ldd + c0;
 
   zero_pad_cols<CQ, KC>(smem, TB, KT, tid);
   QKFrag<CQ> qf[2];
@@ -735,9 +740,9 @@ fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     qk_load_global<CQ>(qf[qb], base + (size_t)q * ldq, ok, g);
 #pragma unroll
     for (int dc = 0; dc < NDC; ++dc)
-      df[qb][dc] = ok ? *(const bf16x8_t*)(dyb + (size_t)q * C + 32 * dc + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+      df[qb][dc] = ok ? *(const bf16x8_t*)(dyb + (size_t)q * ldd + 32 * dc + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     Lq[qb] = ok ? -lse[(size_t)b * N + q] * kL2E : 0.f;
-    const float nr = ok ? -rr[(size_t)b * N + q] : 0.f;
+    const float nr = (ok && ch == 0) ? -rr[(size_t)b * N + q] : 0.f;  // -r enters dP once, in chunk 0
     nR[qb] = f32x4_t{nr, nr, nr, nr};
   }
   f32x4_t dqa[2][NDB];
@@ -751,7 +756,7 @@ fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
   Stage<KT, C / 8> sv;
   const int ntiles = (N + KT - 1) / KT;
   sk.load(base + CQ, ldq, 0, N, tid);
-  sv.load(base + 2 * CQ, ldq, 0, N, tid);
+  sv.load(base + 2 * CQ + c0, ldq, 0, N, tid);
   sk.template store<KC>(smem, tid);
   sv.template store<C>(smem + KBy, tid);
   __syncthreads();
@@ -760,7 +765,7 @@ fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     const int kt0 = t * KT;
     if (t + 1 < ntiles) {
       sk.load(base + CQ, ldq, kt0 + KT, N, tid);
-      sv.load(base + 2 * CQ, ldq, kt0 + KT, N, tid);
+      sv.load(base + 2 * CQ + c0, ldq, kt0 + KT, N, tid);
     }
     const char* Ki = smem + (t & 1) * TB;
     const char* Vi = Ki + KBy;
@@ -820,8 +825,13 @@ fra_bwd_dq_mfma(int N, int ldq, const bf16_t* __restrict__ qkv,
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
       if (d < CQ) {
-        const f32x4_t v = dqa[qb][db] * gm;
-        *(uint2*)(out + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        if (part) {  // wide layers: this chunk's share of dQ (fp32, unscaled)
+          float* pp = part + (((size_t)ch * gridDim.z + b) * N + q) * CQ + d;
+          *(float4*)pp = make_float4(dqa[qb][db][0], dqa[qb][db][1], dqa[qb][db][2], dqa[qb][db][3]);
+        } else {
+          const f32x4_t v = dqa[qb][db] * gm;
+          *(uint2*)(out + d) = make_uint2(pack2bf(v[0], v[1]), pack2bf(v[2], v[3]));
+        }
       }
     }
   }
@@ -883,33 +893,73 @@ void launch_fwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* x,
   }
 }
 
+// C = the value-column width one workgroup owns; Ctot = C except on wide layers, where grid.y runs
+// over the Ctot / C chunks and dQ / dK leave as per-chunk fp32 partials (part: dK shares, then dQ
+// shares) for fra_wide_finish.
 template <int CQ, int C>
-void launch_bwd(int B, int N, int ldq, const void* qkv, const void* dy, const float* gamma, const float* lse,
-                const float* rr, void* dqkv, hipStream_t st) {
-  dim3 grid((N + 127) / 128, 1, B);
+void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy, const float* gamma,
+                const float* lse, const float* rr, void* dqkv, float* part, hipStream_t st) {
+  dim3 grid((N + 127) / 128, Ctot / C, B);
+  float* pk = part;
+  float* pq = part ? part + (size_t)(Ctot / C) * B * N * CQ : nullptr;
   const int occ = fra_occ_tuned();
   constexpr bool narrow = CQ <= 16 && (C == 64 || C == 128);
   constexpr int WKV = C == 64 ? 3 : 2, WQ = C == 64 ? 4 : 3;
   if (narrow && (occ & 2))
-    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, narrow ? WKV : 1>), grid, dim3(256), 0, st, N, ldq,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, narrow ? WKV : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk);
   else
-    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+    hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk);
   if (narrow && (occ & 4))
-    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq);
   else
-    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv);
+    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq);
 }
 
 template <int CQ>
 void launch_bwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* dy, const float* gamma,
                    const float* lse, const float* rr, void* dqkv, hipStream_t st) {
-  if (C == 64) launch_bwd<CQ, 64>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
-  else if (C == 128) launch_bwd<CQ, 128>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
-  else launch_bwd<CQ, 256>(B, N, ldq, qkv, dy, gamma, lse, rr, dqkv, st);
+  if (C == 64) launch_bwd<CQ, 64>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
+  else if (C == 128) launch_bwd<CQ, 128>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
+  else launch_bwd<CQ, 256>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
+}
+
+// Wide layers (C > 256: the 64^2 / 32^2 levels of config 5): value columns in chunks of kWideChunk.
+// dP = dy V^T is a sum over value columns and dS = gamma P (dP - r) is linear in dP, so each chunk's
+// kernels compute dS_chunk = gamma P dP_chunk (-r added by chunk 0 only) and dQ = sum_chunks dS_chunk K,
+// dK = sum_chunks dS_chunk^T Q exactly; dV columns belong to one chunk and are written directly.
+// The score tile is recomputed per chunk (d_qk = C/8 << kWideChunk, a small share of the MFMAs).
+constexpr int kWideChunk = 128;
+
+bool wide_bwd_ok(int dtype, int C, int Cq, int ldq) {
+  return dtype == DFCSA_DT_BF16 && C > 256 && C % kWideChunk == 0 && C <= 4096 && ldq % 8 == 0 &&
+         (Cq == 8 || Cq == 16 || Cq == 32 || Cq == 64 || Cq == 128);
+}
+
+// dqkv[row][0, CQ) = gamma * sum_chunks dQ share, dqkv[row][CQ, 2CQ) = gamma * sum_chunks dK share;
+// one thread per (row, 4 columns), chunk order fixed (deterministic)
+__global__ void __launch_bounds__(256) fra_wide_finish(int64_t rows, int CQ, int nch, int ldq,
+                                                       const float* __restrict__ part,
+                                                       const float* __restrict__ gamma, bf16_t* __restrict__ dqkv) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int q4 = CQ / 4;
+  if (e >= 2 * rows * q4) return;
+  const int which = (int)(e / (rows * q4));  // 0 = dK, 1 = dQ
+  const int64_t rem = e - (int64_t)which * rows * q4;
+  const int64_t row = rem / q4;
+  const int d = (int)(rem - row * q4) * 4;
+  const float* p = part + ((size_t)which * nch * rows + row) * CQ + d;
+  float4 s = *(const float4*)p;
+  for (int c = 1; c < nch; ++c) {
+    const float4 v = *(const float4*)(p + (size_t)c * rows * CQ);
+    s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+  }
+  const float gm = *gamma;
+  bf16_t* out = dqkv + row * ldq + (which == 0 ? CQ : 0) + d;
+  *(uint2*)out = make_uint2(pack2bf(gm * s.x, gm * s.y), pack2bf(gm * s.z, gm * s.w));
 }
 
 }  // namespace
@@ -918,34 +968,35 @@ extern "C" int dfcsa_fra_path(int dtype, int C, int Cq, int ldq, int backward) {
   if (g_fra_generic) return 0;
   if (!backward) return mfma_fwd_ok(dtype, C, Cq, ldq) ? 1 : 0;
   if (mfma_bwd_ok(dtype, C, Cq, ldq)) return 1;
-  // wide bf16 layers (C > 256: the 64^2 / 32^2 levels, where N is small) materialise the score
-  // matrices: library GEMMs for S, dP, dV, dK, dQ around dfcsa_fra_bwd_probs
-  return (dtype == DFCSA_DT_BF16 && C > 256) ? 2 : 0;
+  return wide_bwd_ok(dtype, C, Cq, ldq) ? 2 : 0;  // value-chunked MFMA kernels + dfcsa_fra_bwd_wide
 }
 
-// Materialised-score backward, elementwise step (rows = B*N queries, N keys per row, fp32):
-//   S  <- gamma * P,  P = exp(S - lse_row)
-//   dP <- gamma * P * (dP - r_row)            (= dS; dV = S^T dy, dK = dS^T Q, dQ = dS K)
-__global__ void __launch_bounds__(256) fra_bwd_probs_kernel(int64_t total, int N, float* __restrict__ S,
-                                                            float* __restrict__ dP, const float* __restrict__ lse,
-                                                            const float* __restrict__ rr,
-                                                            const float* __restrict__ gamma) {
-  const float gm = *gamma;
-  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
-    const int64_t row = e / N;
-    const float p = gm * __expf(S[e] - lse[row]);
-    S[e] = p;
-    dP[e] = p * (dP[e] - rr[row]);
+extern "C" int dfcsa_fra_bwd_wide_bytes(int B, int N, int C, int Cq, int64_t* bytes) {
+  if (B <= 0 || N <= 0 || C <= 0 || Cq <= 0 || !bytes) return DFCSA_EINVAL;
+  *bytes = (int64_t)2 * (C / kWideChunk) * B * N * Cq * (int64_t)sizeof(float);
+  return 0;
+}
+
+extern "C" int dfcsa_fra_bwd_wide(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* dy,
+                                  const float* gamma, const float* lse, const float* r, void* dqkv, float* work,
+                                  void* stream) {
+  if (B <= 0 || N <= 0 || !work || !wide_bwd_ok(dtype, C, Cq, ldq) || g_fra_generic) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_ATTN, st, 4.0 * B * (double)N * N * (Cq + C));
+  if (ldq != 2 * Cq + C) {
+    hipError_t e = hipMemsetAsync(dqkv, 0, (size_t)B * N * ldq * 2, st);
+    if (e != hipSuccess) return -(int)e;
   }
-}
-
-extern "C" int dfcsa_fra_bwd_probs(int B, int N, float* S, float* dP, const float* lse, const float* r,
-                                   const float* gamma, void* stream) {
-  if (B <= 0 || N <= 0 || !S || !dP || !lse || !r || !gamma) return DFCSA_EINVAL;
-  const int64_t total = (int64_t)B * N * N;
-  const int blocks = (int)std::min<int64_t>((total + 255) / 256, 256 * 32);
-  hipLaunchKernelGGL(fra_bwd_probs_kernel, dim3(blocks), dim3(256), 0, (hipStream_t)stream, total, N, S, dP, lse,
-                     r, gamma);
+  switch (Cq) {
+    case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, work, st); break;
+    case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, work, st); break;
+    case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, work, st); break;
+    case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, work, st); break;
+    default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, work, st); break;
+  }
+  const int64_t rows = (int64_t)B * N, threads = 2 * rows * (Cq / 4);
+  hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, rows, Cq,
+                     C / kWideChunk, ldq, work, gamma, (bf16_t*)dqkv);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1007,7 +1058,7 @@ extern "C" int dfcsa_fra_bwd(int dtype, int B, int N, int C, int Cq, int ldq, co
       case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
       case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
       case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;
-      default: launch_bwd<64, 64>(B, N, ldq, qkv, dy, gamma, lse, r, dqkv, st); break;   // ViT heads
+      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dy, gamma, lse, r, dqkv, nullptr, st); break;   // ViT heads
     }
   } else {
     dim3 grid((N + 3) / 4, B);

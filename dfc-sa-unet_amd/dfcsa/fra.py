@@ -6,11 +6,14 @@ forward (a = the NHWC attention input, C channels, Cq = C // 8):
     O, lse = flash(q, k, v)                        dfcsa_fra_fwd; y = gamma * O + a in its epilogue
 backward (dy at y):
     r = rowsum(dy * O)                             dfcsa_fra_bwd_prep; dgamma = sum r
-    dqkv = flash_bwd(q, k, v, dy, lse, r)          dfcsa_fra_bwd (P recomputed from lse)
+    dqkv = flash_bwd(q, k, v, dy, lse, r)          dfcsa_fra_bwd (P recomputed from lse); C > 256:
+                                                   dfcsa_fra_bwd_wide (value-column chunks of 128)
     dW = dqkv^T a, db = colsum(dqkv)               weight-gradient GEMM + channel sums
     da = dy + dqkv @ Wqkv                          dgrad GEMM accumulated onto dy
 Jp = 2 Cq + C rounded up to a multiple of 8 (zero weight rows; only the tiny test widths pad).
 """
+import ctypes
+
 import torch
 
 from . import _lib, ops
@@ -75,8 +78,12 @@ def core_backward(mod, saved, dy, dtype, pk):
     call("dfcsa_fra_bwd_prep", T, M, C, P(dy), P(o), P(r), stream())
     call("dfcsa_sum_to_scalar", P(r), M, P(_grad_of(mod.gamma)), stream())
     dqkv = torch.empty_like(qkv)
-    if _lib.LIB.dfcsa_fra_path(T, C, Cq, Jp, 1) == 2 and B * N * N * 8 <= WIDE_SCORE_BYTES:
-        _materialised_backward(B, N, C, Cq, Jp, qkv, dy, mod.gamma, lse, r, dqkv)
+    if _lib.LIB.dfcsa_fra_path(T, C, Cq, Jp, 1) == 2:
+        nb = ctypes.c_int64()
+        call("dfcsa_fra_bwd_wide_bytes", B, N, C, Cq, ctypes.byref(nb))
+        work = torch.empty(nb.value // 4, device=dev, dtype=f32)
+        call("dfcsa_fra_bwd_wide", T, B, N, C, Cq, Jp, P(qkv), P(dy), P(mod.gamma), P(lse), P(r), P(dqkv),
+             P(work), stream())
     else:
         call("dfcsa_fra_bwd", T, B, N, C, Cq, Jp, P(qkv), P(dy), P(mod.gamma), P(lse), P(r), P(dqkv), stream())
     grid, hw = (B, H, W), (H, W)
@@ -95,31 +102,6 @@ def core_backward(mod, saved, dy, dtype, pk):
         call("dfcsa_cast_f32", _lib.DT_F32, C, P(tail), P(dbv), 1, stream())
     ops.conv_gemm(dtype, [(dqkv, 0, 0)], Jp, grid, hw, pk["WqkvT"], rup(Jp, ops.KALIGN), C, [dy], C, accumulate=True)
     return dy
-
-
-# Wide layers (C > 256 at 64^2 / 32^2: N = 4096 / 1024) have few queries and many value channels:
-# the flash kernels' register tiles do not fit C, so the two score matrices are materialised
-# ([B][N][N] fp32 each, 134 MB at B = 2, N = 4096) and the five contractions run as library GEMMs
-# (fp32, hipBLASLt) around one elementwise kernel -- instead of the per-key generic kernels.
-WIDE_SCORE_BYTES = 8 << 30
-
-
-def _materialised_backward(B, N, C, Cq, Jp, qkv, dy, gamma, lse, r, dqkv):
-    f32 = torch.float32
-    qkv3 = qkv.reshape(B, N, Jp)
-    q = qkv3[..., :Cq].to(f32)
-    k = qkv3[..., Cq:2 * Cq].to(f32)
-    v = qkv3[..., 2 * Cq:2 * Cq + C].to(f32)
-    g = dy.reshape(B, N, C).to(f32)
-    S = torch.bmm(q, k.transpose(1, 2))     # S[q][k]
-    dP = torch.bmm(g, v.transpose(1, 2))    # dP[q][k] = dy_q . v_k
-    call("dfcsa_fra_bwd_probs", B, N, P(S), P(dP), P(lse), P(r), P(gamma), stream())
-    d3 = dqkv.reshape(B, N, Jp)
-    d3[..., :Cq].copy_(torch.bmm(dP, k))                                  # dQ = dS K
-    d3[..., Cq:2 * Cq].copy_(torch.bmm(dP.transpose(1, 2), q))            # dK = dS^T Q
-    d3[..., 2 * Cq:2 * Cq + C].copy_(torch.bmm(S.transpose(1, 2), g))     # dV = (gamma P)^T dy
-    if Jp > 2 * Cq + C:
-        d3[..., 2 * Cq + C:].zero_()
 
 
 class FRAFunction(torch.autograd.Function):

@@ -345,11 +345,12 @@ int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const double* part
  * bwd: dqkv [B][N][ldq] = gradients of q, k, v for dy at y (padding columns zeroed); P is
  *      recomputed from lse.
  * path: 1 if the bf16 MFMA kernels serve this shape (fwd: C % 64 == 0, Cq in {8..128} powers of 2;
- *      bwd: C in {64, 128, 256}, Cq in {8, 16, 32}), 2 (bwd only: bf16, C > 256) = materialised
- *      scores: the caller forms S = Q K^T and dP = dy V^T [B][N][N] fp32 with library GEMMs,
- *      calls dfcsa_fra_bwd_probs, then dV = S^T dy, dK = dS^T Q, dQ = dS K; 0 = the generic
- *      kernels (fp32, other shapes; dfcsa_fra_bwd also serves path-2 shapes this way).
- * bwd_probs: in place, S <- gamma * exp(S - lse_row), dP <- S * (dP - r_row) (= dS).
+ *      bwd: C in {64, 128, 256}, Cq in {8, 16, 32}), 2 (bwd only: bf16, C > 256, C % 128 == 0 --
+ *      the 64^2 / 32^2 levels) = dfcsa_fra_bwd_wide, 0 = the generic kernels (fp32, other shapes).
+ * bwd_wide: the same MFMA kernels over value-column chunks of 128 (dP = dy V^T is a sum over value
+ *      columns and dS is linear in dP, so dQ / dK are exact sums of per-chunk shares, kept as fp32
+ *      partials in `work` and summed in fixed chunk order; dV columns are written per chunk).
+ *      work: dfcsa_fra_bwd_wide_bytes(B, N, C, Cq) bytes of device memory.
  * ---------------------------------------------------------------------------------------- */
 int dfcsa_fra_path(int dtype, int C, int Cq, int ldq, int backward);
 int dfcsa_fra_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* x,
@@ -357,8 +358,9 @@ int dfcsa_fra_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* q
 int dfcsa_fra_bwd_prep(int dtype, int rows, int C, const void* dy, const void* o, float* r, void* stream);
 int dfcsa_fra_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* dy,
                   const float* gamma, const float* lse, const float* r, void* dqkv, void* stream);
-int dfcsa_fra_bwd_probs(int B, int N, float* S, float* dP, const float* lse, const float* r, const float* gamma,
-                        void* stream);
+int dfcsa_fra_bwd_wide_bytes(int B, int N, int C, int Cq, int64_t* bytes);
+int dfcsa_fra_bwd_wide(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const void* dy,
+                       const float* gamma, const float* lse, const float* r, void* dqkv, float* work, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Plain U-Net (models/unet.py, BASELINE config 1): MaxPool2d(2, ceil_mode=True) (:26) and the

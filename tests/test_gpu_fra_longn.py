@@ -12,7 +12,11 @@ Bar: rel <= 1e-2 (north star, bf16) for O, dQ, dK, dV; |lse - lse_ref| <= 1e-2 a
 a log: an absolute error e is a relative error e of every probability of the row).
 Two score scales: typical (score std ~1.4) and sharp (std ~6), which stresses the online-softmax
 rescaling across the 4096 key tiles of a row.
+The two wide levels of config 5 (64^2: N = 4096, C = 512, d_qk = 64; 32^2: N = 1024, C = 1024,
+d_qk = 128) run dfcsa_fra_bwd_wide (value-column chunks; dQ/dK as summed per-chunk shares).
 """
+import ctypes
+
 import pytest
 import torch
 
@@ -56,14 +60,18 @@ def _reference(q, k, v, dy, gamma, rows, keys):
     return O_r, lse_r, dQ_r, dKs.float(), dVs.float()
 
 
-@pytest.mark.parametrize("N,C,scale", [(262144, 64, 0.7), (262144, 64, 1.5), (65536, 128, 0.5), (65536, 128, 1.1)],
-                         ids=["L1_N262144_C64", "L1_N262144_C64_sharp", "L2_N65536_C128", "L2_N65536_C128_sharp"])
+@pytest.mark.parametrize("N,C,scale", [(262144, 64, 0.7), (262144, 64, 1.5), (65536, 128, 0.5), (65536, 128, 1.1),
+                                       (4096, 512, 0.3), (4096, 512, 0.6), (1024, 1024, 0.2), (1024, 1024, 0.45)],
+                         ids=["L1_N262144_C64", "L1_N262144_C64_sharp", "L2_N65536_C128", "L2_N65536_C128_sharp",
+                              "L5_N4096_C512", "L5_N4096_C512_sharp", "L6_N1024_C1024", "L6_N1024_C1024_sharp"])
 def test_fra_long_n_fwd_bwd_vs_torch_fp32(N, C, scale):
     from dfcsa._lib import DT_BF16, LIB, call
     from dfcsa.ops import P, stream
     Cq = C // 8
     J = 2 * Cq + C
-    assert LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 0) == 1 and LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 1) == 1
+    wide = C > 256
+    assert LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 0) == 1
+    assert LIB.dfcsa_fra_path(DT_BF16, C, Cq, J, 1) == (2 if wide else 1)
     dev = torch.device("cuda")
     g = torch.Generator(device=dev).manual_seed(N + C)
     qkv = torch.empty(1, N, J, device=dev, dtype=torch.bfloat16)
@@ -79,7 +87,14 @@ def test_fra_long_n_fwd_bwd_vs_torch_fp32(N, C, scale):
     r = torch.empty(N, device=dev, dtype=torch.float32)
     call("dfcsa_fra_bwd_prep", DT_BF16, N, C, P(dy), P(o), P(r), stream())
     dqkv = torch.empty_like(qkv)
-    call("dfcsa_fra_bwd", DT_BF16, 1, N, C, Cq, J, P(qkv), P(dy), P(gamma), P(lse), P(r), P(dqkv), stream())
+    if wide:   # value-column chunked kernels (64^2 / 32^2 levels of config 5)
+        nb = ctypes.c_int64()
+        call("dfcsa_fra_bwd_wide_bytes", 1, N, C, Cq, ctypes.byref(nb))
+        work = torch.full((nb.value // 4,), float("nan"), device=dev)   # every partial must be written
+        call("dfcsa_fra_bwd_wide", DT_BF16, 1, N, C, Cq, J, P(qkv), P(dy), P(gamma), P(lse), P(r), P(dqkv),
+             P(work), stream())
+    else:
+        call("dfcsa_fra_bwd", DT_BF16, 1, N, C, Cq, J, P(qkv), P(dy), P(gamma), P(lse), P(r), P(dqkv), stream())
     torch.cuda.synchronize()
 
     q = qkv[0, :, :Cq].float()

@@ -144,11 +144,12 @@ def _fra_case(C, H, W, dtype, seed=0):
 
 
 @pytest.mark.parametrize("C,H,W", [(64, 32, 32), (64, 30, 30), (128, 16, 16), (128, 12, 20), (256, 8, 8),
-                                   (256, 12, 13), (512, 8, 8), (512, 13, 11), (1024, 6, 6)])
+                                   (256, 12, 13), (512, 8, 8), (512, 13, 11), (1024, 6, 6),
+                                   (1024, 11, 9), (512, 24, 23)])
 def test_fra_bf16_mfma_vs_torch_fp32(C, H, W):
-    """bf16 MFMA flash kernels (fwd for all widths; bwd MFMA for C <= 256, materialised scores with
-    library GEMMs around dfcsa_fra_bwd_probs above) against plain PyTorch fp32 on the same
-    weights; N not a multiple of the 64/128 tiles exercises the masking."""
+    """bf16 MFMA flash kernels (fwd for all widths; bwd MFMA for C <= 256, the value-chunked
+    dfcsa_fra_bwd_wide above) against plain PyTorch fp32 on the same weights; N not a multiple
+    of the 64/128 tiles exercises the masking."""
     from dfcsa._lib import LIB
     J = 2 * (C // 8) + C
     assert LIB.dfcsa_fra_path(1, C, C // 8, J, 0) == 1
