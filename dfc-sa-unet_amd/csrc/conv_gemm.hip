@@ -869,5 +869,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 11) { g_ew_tile_elems = value >= 4096 ? value : 16384; return 0; }
   if (knob == 12) { g_wgrad_fuse_all = value; return 0; }
   if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
+  if (knob == 14) { g_wgrad_nst = (value >= 2 && value <= 4) ? value : 2; return 0; }
   return DFCSA_EINVAL;
 }

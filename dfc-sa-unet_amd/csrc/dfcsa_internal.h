@@ -56,6 +56,7 @@ extern int g_wgrad_noglds;
 extern int g_wgrad_narrow;
 extern int g_wgrad_fuse_all;
 extern int g_wgrad_fuse_max;
+extern int g_wgrad_nst;
 extern int g_fra_generic;
 extern int g_fra_occ;
 extern int g_ew_tile_elems;

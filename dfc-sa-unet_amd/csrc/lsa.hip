@@ -199,63 +199,116 @@ __global__ void __launch_bounds__(256) lsa_attn_kernel(int N, int C, int Cq, con
   }
 }
 
-// grid (H, B): rows[b][h][pj][c] = sum_w wx(pj, w) * dattn[b][h][w][c]
+// Source positions of the bilinear upsample increase with the destination index, so the
+// destinations that read source cell p along an axis (in -> out) form one range [lo, hi): lo a
+// little before the first contributor, hi past the last (i0 > p beyond it).  The ranges are
+// over-estimates; positions inside them with a zero weight are skipped, so only the summation
+// split (fixed) depends on them.
+__device__ __forceinline__ void contrib_range(int p, int in, int out, int& lo, int& hi) {
+  lo = (int)(((float)(p - 1) + 0.5f) * (float)out / (float)in - 0.5f) - 2;
+  if (lo < 0) lo = 0;
+  hi = (int)(((float)p + 1.5f) * (float)out / (float)in - 0.5f) + 3;
+  if (hi > out) hi = out;
+}
+
+// grid (H, B): rows[b][h][pj][c] = sum_w wx(pj, w) * dattn[b][h][w][c].  Work items (pj, 8
+// channels) x NSL slices of the w range, so all 256 threads stream the row (P * C / 8 items alone
+// leave most of the workgroup idle at C = 64); slices are combined in a fixed order through LDS.
 template <typename T>
 __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int C, const T* __restrict__ d, int P,
                                                               float* __restrict__ rows) {
+  __shared__ float red[256 * 8];
   const int h = blockIdx.x, b = blockIdx.y;
-  const int cpp = C >> 3;
+  const int cpp = C >> 3, items = P * cpp;
+  const int nsl = items >= 256 ? 1 : 256 / items;
   const T* row = d + ((size_t)b * H + h) * W * C;
-  for (int item = threadIdx.x; item < P * cpp; item += 256) {
-    const int pj = item / cpp, c0 = (item - pj * cpp) * 8;
+  for (int base = 0; base < items; base += 256) {
+    const int e = base + threadIdx.x % (nsl == 1 ? 256 : items), sl = nsl == 1 ? 0 : threadIdx.x / items;
+    const bool on = e < items && sl < nsl;
     float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    // source position of w is increasing in w: start a little before the first contributor
-    int w = (int)(((float)(pj - 1) + 0.5f) * (float)W / (float)P - 0.5f) - 2;
-    if (w < 0) w = 0;
-    for (; w < W; ++w) {
-      int i0, i1;
-      float l0, l1;
-      bilin_axis(w, P, W, i0, i1, l0, l1);
-      if (i0 > pj) break;
-      const float wt = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
-      if (wt == 0.f) continue;
-      float v[8];
-      load8<T>(row + (size_t)w * C + c0, v);
+    int pj = 0, c0 = 0;
+    if (on) {
+      pj = e / cpp;
+      c0 = (e - pj * cpp) * 8;
+      int lo, hi;
+      contrib_range(pj, P, W, lo, hi);
+      for (int w = lo + sl; w < hi; w += nsl) {
+        int i0, i1;
+        float l0, l1;
+        bilin_axis(w, P, W, i0, i1, l0, l1);
+        const float wt = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
+        if (wt == 0.f) continue;
+        float v[8];
+        load8<T>(row + (size_t)w * C + c0, v);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) acc[q] += wt * v[q];
+        for (int q = 0; q < 8; ++q) acc[q] += wt * v[q];
+      }
     }
-    float* out = rows + (((size_t)b * H + h) * P + pj) * C + c0;
+    if (nsl == 1) {
+      if (on) {
+        float* out = rows + (((size_t)b * H + h) * P + pj) * C + c0;
 #pragma unroll
-    for (int q = 0; q < 8; ++q) out[q] = acc[q];
+        for (int q = 0; q < 8; ++q) out[q] = acc[q];
+      }
+      continue;
+    }
+    if (on)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[(sl * items + e) * 8 + q] = acc[q];
+    __syncthreads();
+    for (int k = threadIdx.x; k < items * 8; k += 256) {
+      const int it = k >> 3, q = k & 7;
+      float v = 0.f;
+      for (int s2 = 0; s2 < nsl; ++s2) v += red[(s2 * items + it) * 8 + q];
+      const int pj2 = it / cpp, cc = (it - pj2 * cpp) * 8 + q;
+      rows[(((size_t)b * H + h) * P + pj2) * C + cc] = v;
+    }
+    __syncthreads();
   }
 }
 
-// grid (N, B): du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du
+// grid (N, B): du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du.
+// Channels x NSL slices of the h range (all 256 threads busy at C = 64), combined in LDS.
 __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
                                                               const float* __restrict__ o, const float* gamma,
                                                               float* __restrict__ dO, float* __restrict__ gpart) {
-  __shared__ float red[8];
+  __shared__ float red[256 + 8];
   const int n = blockIdx.x, b = blockIdx.y, N = P * P;
   const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
-  int hlo = (int)(((float)(pi - 1) + 0.5f) * (float)H / (float)P - 0.5f) - 2;
-  if (hlo < 0) hlo = 0;
+  const int nsl = C >= 256 ? 1 : 256 / C;
+  const int cw = nsl == 1 ? 256 : C;
+  const int sl = threadIdx.x / cw, cl = threadIdx.x - sl * cw;
+  int lo, hi;
+  contrib_range(pi, P, H, lo, hi);
   float gsum = 0.f;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int cb = 0; cb < C; cb += cw) {
+    const int c = cb + cl;
     float s = 0.f;
-    for (int h = hlo; h < H; ++h) {
-      int i0, i1;
-      float l0, l1;
-      bilin_axis(h, P, H, i0, i1, l0, l1);
-      if (i0 > pi) break;
-      const float wt = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
-      if (wt != 0.f) s += wt * rows[(((size_t)b * H + h) * P + pj) * C + c];
+    if (c < C && sl < nsl) {
+      for (int h = lo + sl; h < hi; h += nsl) {
+        int i0, i1;
+        float l0, l1;
+        bilin_axis(h, P, H, i0, i1, l0, l1);
+        const float wt = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
+        if (wt != 0.f) s += wt * rows[(((size_t)b * H + h) * P + pj) * C + c];
+      }
     }
-    const size_t idx = ((size_t)b * N + n) * C + c;
-    gsum += o[idx] * s;
-    dO[idx] = gm * s;
+    if (nsl > 1) {
+      if (sl < nsl) red[threadIdx.x] = s;
+      __syncthreads();
+      s = 0.f;
+      if (sl == 0)
+        for (int s2 = 0; s2 < nsl; ++s2) s += red[s2 * cw + cl];
+      __syncthreads();
+    }
+    if (sl == 0 && c < C) {
+      const size_t idx = ((size_t)b * N + n) * C + c;
+      gsum += o[idx] * s;
+      dO[idx] = gm * s;
+    }
   }
-  gsum = block_reduce_sum(gsum, red);
+  gsum = block_reduce_sum(gsum, red + 256);
   if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
 }
 

@@ -346,7 +346,7 @@ __device__ __attribute__((aligned(16))) uint4 g_wg_zero[64];
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void glb_void_t;
 
-template <int BI, int BJ, int WM, int WN>
+template <int BI, int BJ, int WM, int WN, int NST>
 __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArgs args, int nsplit) {
   constexpr int NW = WM * WN;
   using T = bf16_t;
@@ -358,7 +358,8 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
   static_assert(NI_G >= 1 && NI_X >= 1, "wgrad glds tiling");
   constexpr int WTM = BI / WM, WTN = BJ / WN;
   constexpr int FM = WTM / 16, FN = WTN / 16;
-  constexpr int SMEM_MAIN = 2 * STAGE;
+  constexpr int SMEM_MAIN = NST * STAGE;
+  constexpr int OPS = NI_G + NI_X;   // DMA instructions per wave per stage (issued unconditionally)
   __shared__ __attribute__((aligned(16))) char smem[SMEM_MAIN + DFCSA_MAX_SEG * (int)sizeof(ConvSeg)];
   ConvSeg* segtab = (ConvSeg*)(smem + SMEM_MAIN);
 
@@ -445,12 +446,26 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
 
   const int nk = (mend > mbeg) ? (mend - mbeg + KMS - 1) / KMS : 0;
-  if (nk > 0) issue(0, 0);
+  // NST-deep ring: stages kt+1 .. kt+NST-2 stay in flight while stage kt is multiplied; the DMAs
+  // are the only vector-memory ops in the loop, so a counted vmcnt isolates stage kt
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int after = min(NST - 2, nk - 1 - kt);
+    if constexpr (NST >= 4) {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NST == 3) {
+      if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
     __syncthreads();
-    if (kt + 1 < nk) issue(kt + 1, (kt + 1) & 1);
-    const char* G = smem + (kt & 1) * STAGE;
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* G = smem + (kt % NST) * STAGE;
     const char* X = G + GB;
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -562,13 +577,18 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
       if (BI == 64 && wide_j(a)) {
         dim3 g2(xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits), splits);
         g2.y = 1;
-        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4>), g2, dim3(512), 0, st, a, splits);
+        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4, 2>), g2, dim3(512), 0, st, a, splits);
       } else {
         dim3 g1(xcd_pad(grid.x * grid.y * splits));
-        if (waves == 8)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, BI == 64 ? 2 : 4, BI == 64 ? 4 : 2>), g1, dim3(512), 0, st, a, splits);
+        constexpr int WM8 = BI == 64 ? 2 : 4, WN8 = BI == 64 ? 4 : 2;
+        if (waves == 8 && g_wgrad_nst >= 4)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4>), g1, dim3(512), 0, st, a, splits);
+        else if (waves == 8 && g_wgrad_nst == 3)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3>), g1, dim3(512), 0, st, a, splits);
+        else if (waves == 8)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2>), g1, dim3(512), 0, st, a, splits);
         else
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2>), g1, dim3(256), 0, st, a, splits);
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2, 2>), g1, dim3(256), 0, st, a, splits);
       }
       DFCSA_CHECK_LAUNCH();
       return 0;
@@ -588,6 +608,7 @@ int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
 int g_wgrad_narrow = 1;    // 0 = allow the 64x256 wgrad tile (dfcsa_set_tuning knob 8; measured slower on the L1 3x3)
 int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
+int g_wgrad_nst = 2;       // knob 14: LDS-DMA ring depth of the bf16 wgrad kernel (2, 3, 4)
 int g_wgrad_fuse_all = 0;  // knob 12: 1 = reduce in-kernel at any split count, -1 = never (separate launch)
 // knob 13: most splits reduced in-kernel.  Default 0 = never: measured on the headline step
 // (tools/wgrad_shapes.py, bench A/B) the last arriver's serialized read of the partials costs more

@@ -1,8 +1,8 @@
 """Per-launch timing of every weight-gradient GEMM of the headline step (DFC-SA-Res 64..512,
 B=16, 224^2, bf16), each timed as 10 calls captured in one HIP graph (pure device time): the
 complete gradient update (ops.conv_wgrad_into: wgrad kernel + split-K reduction into the weight
-gradient) with the in-kernel reduction threshold at its default, at 16 splits, and disabled.
-One JSON line per shape + totals.  Usage: python tools/wgrad_shapes.py"""
+gradient) under each tuning mode of MODES (WGRAD_MODES=a,b selects), with each mode's result
+checked against the first mode's (relative max difference).  One JSON line per shape + totals.  Usage: python tools/wgrad_shapes.py"""
 import json
 import os
 import sys
@@ -18,7 +18,12 @@ B = 16
 bf = torch.bfloat16
 BLOCKS = [(8, 64, 224, 1), (64, 128, 112, 1), (128, 256, 56, 1), (256, 512, 28, 1), (512, 1024, 14, 1),
           (512, 512, 28, 2), (256, 256, 56, 2), (128, 128, 112, 2), (64, 64, 224, 2)]
-MODES = {"default": (0, 0), "fuse16": (0, 16), "unfused": (-1, 0)}   # knobs 12, 13
+# mode -> {tuning knob: value} (knobs 12/13: in-kernel split reduction, 14: LDS ring depth,
+# 2: workgroups per launch target); every knob is reset to its default after each shape
+MODES = {"default": {}, "fuse16": {13: 16}, "unfused": {12: -1},
+         "nst3": {14: 3}, "nst4": {14: 4}, "nst3_t256": {14: 3, 2: 256}, "nst4_t256": {14: 4, 2: 256},
+         "nst3_t1024": {14: 3, 2: 1024}, "t1024": {2: 1024}}
+DEFAULTS = {2: 512, 12: 0, 13: 0, 14: 2}
 if os.environ.get("WGRAD_MODES"):
     MODES = {k: v for k, v in MODES.items() if k in os.environ["WGRAD_MODES"].split(",")}
 
@@ -68,14 +73,22 @@ def main():
                 for _ in gs]
         Ctot = Cin if ntaps == 9 else NJ
         row = {"shape": name, "M": M, "NI": NI, "NJ": NJ, "gflop": round(2.0 * M * NI * NJ / 1e9, 2)}
-        for mode, (k12, k13) in MODES.items():
-            dfcsa.set_tuning(12, k12)
-            dfcsa.set_tuning(13, k13)
+        ref = None
+        for mode, knobs in MODES.items():
+            for k, v in knobs.items():
+                dfcsa.set_tuning(k, v)
             us = graph_time(lambda: ops.conv_wgrad_into(bf, gs, c, segs, cs, (B, H, H), (H, H), dsts, ntaps, Ctot, Ctot))
+            for d in dsts:
+                d.zero_()
+            ops.conv_wgrad_into(bf, gs, c, segs, cs, (B, H, H), (H, H), dsts, ntaps, Ctot, Ctot)
+            out = torch.cat([d.flatten() for d in dsts])
+            if ref is None:
+                ref = out.clone()
             row[mode] = round(us, 1)
+            row[mode + "_maxdiff"] = float((out - ref).abs().max() / (ref.abs().max() + 1e-30))
             tot[mode] += us
-        dfcsa.set_tuning(12, 0)
-        dfcsa.set_tuning(13, 0)
+            for k in knobs:
+                dfcsa.set_tuning(k, DEFAULTS[k])
         print(json.dumps(row), flush=True)
     print(json.dumps({k: round(v, 1) for k, v in tot.items()}))
 
