@@ -400,42 +400,176 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   }
 }
 
-__global__ void __launch_bounds__(1024) bn_finalize_kernel(
-    const float* __restrict__ stats, int ntiles, int C, int ld, int count, const float* bias, const float* gamma,
-    const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps, int training,
-    float* scale, float* shift, float* mean, float* invstd) {
-  __shared__ double rs[16][64], rq[16][64];
+// ---------------------------------------------------------------------------------------------
+// Column sums of per-tile partial rows, fused with the per-channel finalisation that consumes them
+// (BatchNorm statistics, BatchNorm-backward coefficients, bias gradients): one launch instead of a
+// row-reduction launch + a finalize launch.  grid (ceil(C/64), R), 1024 threads = 16 parts x 64
+// channels; workgroup (x, g) sums rows [g*per, min(T, (g+1)*per)) of channel block x in double,
+// 8 rows' loads in flight per thread.  R > 1: each group hands its NS double sums over through
+// write-through (sc1) stores into a scratch ring, then takes an agent-scope ticket; the
+// last-arriving group of block x reads all R hand-offs (sc1 loads) and combines them in a fixed
+// order (deterministic), then finalises.  The partial rows are only read.
+// ---------------------------------------------------------------------------------------------
+constexpr int kRedRing = 1 << 16;          // ticket counters
+constexpr int kRedScr = 1 << 20;           // hand-off doubles (8 MiB)
+__device__ unsigned g_red_cnt[kRedRing];
+__device__ double g_red_scr[kRedScr];
+
+__device__ __forceinline__ void st_sc1_d(double* p, double v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// three sc1 8-byte loads in flight, one wait
+__device__ __forceinline__ void ld_sc1_d3(const double* p0, const double* p1, const double* p2, double& v0,
+                                          double& v1, double& v2) {
+  asm volatile(
+      "global_load_dwordx2 %0, %3, off sc1\n\t"
+      "global_load_dwordx2 %1, %4, off sc1\n\t"
+      "global_load_dwordx2 %2, %5, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+      : "v"(p0), "v"(p1), "v"(p2)
+      : "memory");
+}
+// twelve sc1 8-byte loads in flight, one wait
+__device__ __forceinline__ void ld_sc1_d12(const double* const (&p)[12], double (&v)[12]) {
+  asm volatile(
+      "global_load_dwordx2 %0, %12, off sc1\n\t"
+      "global_load_dwordx2 %1, %13, off sc1\n\t"
+      "global_load_dwordx2 %2, %14, off sc1\n\t"
+      "global_load_dwordx2 %3, %15, off sc1\n\t"
+      "global_load_dwordx2 %4, %16, off sc1\n\t"
+      "global_load_dwordx2 %5, %17, off sc1\n\t"
+      "global_load_dwordx2 %6, %18, off sc1\n\t"
+      "global_load_dwordx2 %7, %19, off sc1\n\t"
+      "global_load_dwordx2 %8, %20, off sc1\n\t"
+      "global_load_dwordx2 %9, %21, off sc1\n\t"
+      "global_load_dwordx2 %10, %22, off sc1\n\t"
+      "global_load_dwordx2 %11, %23, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+        "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7]), "v"(p[8]),
+        "v"(p[9]), "v"(p[10]), "v"(p[11])
+      : "memory");
+}
+
+// true (workgroup-uniform) if this workgroup finalises channel block x; part-0 threads then hold
+// the column totals in tot[].  Column c of sum k of row t: src[t * rowlen + k * kstride + c].
+template <int NS>
+__device__ bool colred_block(const float* src, int T, int rowlen, int kstride, int C, int per, unsigned* cnt,
+                             double* scr, double (&tot)[NS], double (*sh)[16][64], int* flag) {
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  double s = 0.0, q = 0.0;
-  if (training && c < C) {
-    // 8 tiles' loads in flight per step; the additions keep the sequential tile order
-    int t = part;
-    for (; t + 7 * 16 < ntiles; t += 8 * 16) {
-      float vs[8], vq[8];
+  const int R = gridDim.y, g = blockIdx.y;
+  const int t0 = g * per, t1 = min(T, t0 + per);
+  double s[NS];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        vs[j] = stats[(size_t)(t + 16 * j) * 2 * ld + c];
-        vq[j] = stats[(size_t)(t + 16 * j) * 2 * ld + ld + c];
-      }
+  for (int k = 0; k < NS; ++k) s[k] = 0.0;
+  if (c < C) {
+    int t = t0 + part;
+    for (; t + 7 * 16 < t1; t += 8 * 16) {  // 8 rows in flight, sequential order kept
+      float v[8][NS];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) { s += (double)vs[j]; q += (double)vq[j]; }
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) v[j][k] = src[(size_t)(t + 16 * j) * rowlen + k * kstride + c];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int k = 0; k < NS; ++k) s[k] += (double)v[j][k];
     }
-    for (; t < ntiles; t += 16) {
-      s += (double)stats[(size_t)t * 2 * ld + c];
-      q += (double)stats[(size_t)t * 2 * ld + ld + c];
+    for (; t < t1; t += 16)
+#pragma unroll
+      for (int k = 0; k < NS; ++k) s[k] += (double)src[(size_t)t * rowlen + k * kstride + c];
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sh[k][part][cl] = s[k];
+  __syncthreads();
+  if (part == 0)
+#pragma unroll
+    for (int k = 0; k < NS; ++k)
+      for (int p = 1; p < 16; ++p) s[k] += sh[k][p][cl];
+  if (R == 1) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) tot[k] = s[k];
+    return true;
+  }
+  if (part == 0) {   // scr[((x * R + g) * NS + k) * 64 + channel]
+    double* slot = scr + ((size_t)(blockIdx.x * R + g) * NS) * 64 + cl;
+#pragma unroll
+    for (int k = 0; k < NS; ++k) st_sc1_d(slot + k * 64, s[k]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = old == (unsigned)(R - 1);
+    if (*flag) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     }
   }
-  rs[part][cl] = s;
-  rq[part][cl] = q;
   __syncthreads();
+  if (!*flag) return false;
+  // part p combines groups p, p + 16, ... in order; the parts are then combined in order
+  double gs[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) gs[k] = 0.0;
+  if (R <= 16) {   // one group per part
+    if (part < R) {
+      const double* slot = scr + ((size_t)(blockIdx.x * R + part) * NS) * 64 + cl;
+      double w[3];
+      ld_sc1_d3(slot, slot + (NS > 1 ? 64 : 0), slot + (NS > 2 ? 128 : 0), w[0], w[1], w[2]);
+#pragma unroll
+      for (int k = 0; k < NS; ++k) gs[k] = w[k];
+    }
+  } else {  // groups part + 16 j (j < 4, R <= 64), every sum: one round of loads
+    const double* p[12];
+    const double* own = scr + ((size_t)(blockIdx.x * R + g) * NS) * 64 + cl;   // valid dummy
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const int gg = part + 16 * j;
+        p[j * 3 + k] = (gg < R && k < NS) ? scr + ((size_t)(blockIdx.x * R + gg) * NS + k) * 64 + cl : own;
+      }
+    double w[12];
+    ld_sc1_d12(p, w);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int k = 0; k < NS; ++k)
+        if (part + 16 * j < R) gs[k] += w[j * 3 + k];
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sh[k][part][cl] = gs[k];
+  __syncthreads();
+  if (part == 0)
+#pragma unroll
+    for (int k = 0; k < NS; ++k) {
+      double v = 0.0;
+      for (int p = 0; p < 16; ++p) v += sh[k][p][cl];
+      tot[k] = v;
+    }
+  return true;
+}
+
+__global__ void __launch_bounds__(1024) bn_finalize_kernel(
+    const float* __restrict__ stats, int ntiles, int per, unsigned* cnt, double* scr, int C, int ld, int count, const float* bias,
+    const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps,
+    int training, float* scale, float* shift, float* mean, float* invstd) {
+  __shared__ double sh[2][16][64];
+  __shared__ int flag;
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double tot[2] = {0.0, 0.0};
+  if (training && !colred_block<2>(stats, ntiles, 2 * ld, ld, C, per, cnt, scr, tot, sh, &flag)) return;
   if (part == 0 && c < C) {
     float mu, var, istd;
     if (training) {
-      for (int p = 1; p < 16; ++p) { s += rs[p][cl]; q += rq[p][cl]; }
       const double n = (double)count;
-      const double ma = s / n;
-      double v = q / n - ma * ma;
+      const double ma = tot[0] / n;
+      double v = tot[1] / n - ma * ma;
       if (v < 0.0) v = 0.0;
       const double b = bias ? (double)bias[c] : 0.0;
       mu = (float)(ma + b);
@@ -458,72 +592,75 @@ __global__ void __launch_bounds__(1024) bn_finalize_kernel(
   if (training && nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;
 }
 
-__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ partial, int ntiles,
-                                                               int nsum, int C, int count, float* coef,
-                                                               float* dgamma, float* dbeta, float* third) {
-  __shared__ double r0[16][64], r1[16][64], r2[16][64];
+// coef[0][c] = sum0 / count, coef[1][c] = sum1 / count; dgamma += sum1, dbeta += sum0; with a
+// third sum (res_scale gradient) its channel total goes to third[c] and, once every channel block
+// has finished (second ticket), the last one adds sum_c third[c] to *extra in channel order.
+template <int NS>
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ partial, int ntiles, int per,
+                                                               unsigned* cnt, double* scr, int C, int count, float* coef,
+                                                               float* dgamma, float* dbeta, float* third,
+                                                               float* extra) {
+  __shared__ double sh[NS][16][64];
+  __shared__ int flag;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  double s0 = 0, s1 = 0, s2 = 0;
-  if (c < C) {
-    int t = part;
-    for (; t + 7 * 16 < ntiles; t += 8 * 16) {  // 8 tiles' loads in flight, sequential order kept
-      float v0[8], v1[8], v2[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        const float* p = partial + (size_t)(t + 16 * j) * nsum * C + c;
-        v0[j] = p[0];
-        v1[j] = p[C];
-        v2[j] = nsum > 2 ? p[2 * C] : 0.f;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        s0 += v0[j];
-        s1 += v1[j];
-        if (nsum > 2) s2 += v2[j];
-      }
-    }
-    for (; t < ntiles; t += 16) {
-      const float* p = partial + (size_t)t * nsum * C + c;
-      s0 += p[0];
-      s1 += p[C];
-      if (nsum > 2) s2 += p[2 * C];
+  double tot[NS];
+  if (!colred_block<NS>(partial, ntiles, NS * C, C, C, per, cnt, scr, tot, sh, &flag)) return;
+  if (part == 0 && c < C) {
+    coef[c] = (float)(tot[0] / count);
+    coef[C + c] = (float)(tot[1] / count);
+    if (dgamma) dgamma[c] += (float)tot[1];
+    if (dbeta) dbeta[c] += (float)tot[0];
+    if constexpr (NS > 2) {
+      if (third) st_sc1_dw(third + c, (float)tot[2]);
     }
   }
-  r0[part][cl] = s0; r1[part][cl] = s1; r2[part][cl] = s2;
-  __syncthreads();
-  if (part == 0 && c < C) {
-    for (int p = 1; p < 16; ++p) { s0 += r0[p][cl]; s1 += r1[p][cl]; s2 += r2[p][cl]; }
-    coef[c] = (float)(s0 / count);
-    coef[C + c] = (float)(s1 / count);
-    if (dgamma) dgamma[c] += (float)s1;
-    if (dbeta) dbeta[c] += (float)s0;
-    if (third) third[c] = (float)s2;
+  if constexpr (NS > 2) {
+    if (!extra) return;
+    unsigned* cnt2 = cnt + gridDim.x;
+    if (gridDim.x > 1) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (threadIdx.x == 0) {
+        const unsigned old = __hip_atomic_fetch_add(cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        flag = old == gridDim.x - 1;
+        if (flag) {
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          __hip_atomic_store(cnt2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      __syncthreads();
+      if (!flag) return;
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+    // sum_c third[c], channel order: thread i adds channels i, i + 1024 (C <= 2048), then a tree
+    double v = 0.0;
+    for (int cc = threadIdx.x; cc < C; cc += 1024) v += (double)ld_sc1_f(third + cc);
+    double* r = &sh[0][0][0];  // 1024 doubles (NS = 3: 3 x 16 x 64)
+    r[threadIdx.x] = v;
+    __syncthreads();
+    for (int o = 512; o > 0; o >>= 1) {
+      if (threadIdx.x < o) r[threadIdx.x] += r[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *extra += (float)r[0];
   }
 }
 
 // out[c] += sum_t slab[t][c]; columns split over up to three destinations at n0, n0 + n1
-__global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int C,
-                                                           int n0, int n1, float* d0, float* d1, float* d2) {
-  __shared__ double r[16][64];
+__global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int per,
+                                                           unsigned* cnt, double* scr, int C, int n0, int n1, float* d0,
+                                                           float* d1, float* d2) {
+  __shared__ double sh[1][16][64];
+  __shared__ int flag;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
-  double s = 0;
-  if (c < C) {
-    int t = part;
-    for (; t + 7 * 16 < ntiles; t += 8 * 16) {  // 8 loads in flight, sequential order kept
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = slab[(size_t)(t + 16 * j) * C + c];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) s += v[j];
-    }
-    for (; t < ntiles; t += 16) s += slab[(size_t)t * C + c];
-  }
-  r[part][cl] = s;
-  __syncthreads();
+  double tot[1];
+  if (!colred_block<1>(slab, ntiles, C, 0, C, per, cnt, scr, tot, sh, &flag)) return;
   if (part == 0 && c < C) {
-    for (int p = 1; p < 16; ++p) s += r[p][cl];
+    const double s = tot[0];
     if (c < n0) d0[c] += (float)s;
     else if (c < n0 + n1) d1[c - n0] += (float)s;
     else d2[c - n0 - n1] += (float)s;
@@ -623,16 +760,70 @@ EwArgs zargs(int M, int C) {
 
 }  // namespace
 
+// row groups of a fused column reduction (colred_block): ~128 rows per group (one round of 8
+// loads per thread), at most 64 groups; tickets: nblk (+ extra) counters from a ring (each last
+// arriver re-zeroes its counter); hand-off scratch: nblk * R * ns * 64 doubles from a ring
+struct RedPlan {
+  int R = 1, per = 1;
+  unsigned* cnt = nullptr;
+  double* scr = nullptr;
+};
+static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
+  int R = (T + 127) / 128;
+  if (R > 64) R = 64;
+  const int64_t rmax = (int64_t)(kRedScr / 4) / ((int64_t)(nblk > 0 ? nblk : 1) * (ns > 0 ? ns : 1) * 64);
+  if (R > rmax) R = (int)rmax;
+  if (R < 1) R = 1;
+  int per = (T + R - 1) / R;
+  while (R > 1 && T - (R - 1) * per < 1) {   // no empty group
+    --R;
+    per = (T + R - 1) / R;
+  }
+  p->R = R;
+  p->per = per;
+  p->cnt = nullptr;
+  const int need = nblk + extra;
+  if (R > 1 || extra) {
+    static unsigned* ring = nullptr;
+    static int next = 0;
+    if (!ring && hipGetSymbolAddress((void**)&ring, HIP_SYMBOL(g_red_cnt)) != hipSuccess) return DFCSA_EINVAL;
+    if (need > kRedRing) return DFCSA_EINVAL;
+    if (next + need > kRedRing) next = 0;
+    p->cnt = ring + next;
+    next += need;
+  }
+  if (R > 1) {
+    static double* scr = nullptr;
+    static int64_t snext = 0;
+    if (!scr && hipGetSymbolAddress((void**)&scr, HIP_SYMBOL(g_red_scr)) != hipSuccess) return DFCSA_EINVAL;
+    const int64_t words = (int64_t)nblk * R * ns * 64;
+    if (words > kRedScr) return DFCSA_EINVAL;
+    if (snext + words > kRedScr) snext = 0;
+    p->scr = scr + snext;
+    snext += words;
+  }
+  return 0;
+}
+
+// tickets for other translation units' last-arriver hand-offs (same ring as the reductions here)
+unsigned* dfcsa_ticket_alloc(int n) {
+  RedPlan rp;
+  return red_plan(1, 0, 0, n, &rp) ? nullptr : rp.cnt;
+}
+
 extern "C" int dfcsa_ew_ntiles(int M, int C) { return (M + tile_px(C) - 1) / tile_px(C); }
 
 extern "C" int dfcsa_bn_finalize(const float* stats, int ntiles, int C, int ld, int count, const float* conv_bias,
                                  const float* gamma, const float* beta, float* running_mean, float* running_var,
                                  int64_t* nbt, float momentum, float eps, int training, float* scale,
                                  float* shift, float* mean, float* invstd, void* stream) {
-  if (C <= 0 || (training && (!stats || count <= 0))) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, stats, ntiles,
-                     C, ld, count, conv_bias, gamma, beta, running_mean, running_var, nbt, momentum, eps, training,
-                     scale, shift, mean, invstd);
+  if (C <= 0 || (training && (!stats || count <= 0 || ntiles <= 0))) return DFCSA_EINVAL;
+  const int nblk = (C + 63) / 64;
+  RedPlan rp;
+  if (training && red_plan(ntiles, nblk, 2, 0, &rp)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(nblk, rp.R), dim3(1024), 0, (hipStream_t)stream, stats, ntiles,
+                     rp.per, rp.cnt, rp.scr, C, ld, count, conv_bias, gamma, beta, running_mean, running_var, nbt, momentum,
+                     eps, training, scale, shift, mean, invstd);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -732,18 +923,21 @@ extern "C" int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const
 
 extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count, float* coef,
                                      float* dgamma, float* dbeta, float* extra, void* stream) {
-  if (nsum < 2 || nsum > 3 || C <= 0) return DFCSA_EINVAL;
+  if (nsum < 2 || nsum > 3 || C <= 0 || C > 2048 || ntiles <= 0) return DFCSA_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  // the third per-channel sum (res_scale gradient) is reduced to a scalar afterwards; it is
-  // staged in the tail of `coef` ([3][C]) when requested
+  const int nblk = (C + 63) / 64;
+  // the third per-channel sum (res_scale gradient) is staged in the tail of `coef` ([3][C]) and
+  // reduced to the scalar *extra by the last channel block
   float* third = (nsum == 3 && extra) ? coef + 2 * C : nullptr;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3((C + 63) / 64), dim3(1024), 0, st, partial, ntiles, nsum, C,
-                     count, coef, dgamma, dbeta, third);
+  RedPlan rp;
+  if (red_plan(ntiles, nblk, nsum, third ? 1 : 0, &rp)) return DFCSA_EINVAL;
+  if (nsum == 3)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
+                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, third, third ? extra : nullptr);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
+                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, nullptr, nullptr);
   DFCSA_CHECK_LAUNCH();
-  if (third) {
-    launch_sum_scalar(third, C, extra, st);
-    DFCSA_CHECK_LAUNCH();
-  }
   return 0;
 }
 
@@ -757,19 +951,18 @@ extern "C" int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const
 }
 
 extern "C" int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream) {
-  if (C <= 0 || ntiles <= 0) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, ntiles,
-                     C, C, 0, out, nullptr, nullptr);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
+  return dfcsa_slab_colsum3(slab, ntiles, C, C, 0, out, nullptr, nullptr, stream);
 }
 
 extern "C" int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, int n1, float* d0, float* d1,
                                   float* d2, void* stream) {
   if (C <= 0 || ntiles <= 0 || n0 < 0 || n1 < 0 || n0 + n1 > C || !d0 || (n1 && !d1) || (n0 + n1 < C && !d2))
     return DFCSA_EINVAL;
-  hipLaunchKernelGGL(slab_colsum_kernel, dim3((C + 63) / 64), dim3(1024), 0, (hipStream_t)stream, slab, ntiles,
-                     C, n0, n1, d0, d1, d2);
+  const int nblk = (C + 63) / 64;
+  RedPlan rp;
+  if (red_plan(ntiles, nblk, 1, 0, &rp)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(slab_colsum_kernel, dim3(nblk, rp.R), dim3(1024), 0, (hipStream_t)stream, slab, ntiles, rp.per,
+                     rp.cnt, rp.scr, C, n0, n1, d0, d1, d2);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -109,6 +109,34 @@ __device__ __forceinline__ float wave_max(float v) {
 // data (incl. LDS-DMA images) must be waited for explicitly with s_waitcnt vmcnt before it.
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// Cross-workgroup hand-off helpers (last-arriver reductions): write-through (sc1) stores leave
+// the XCD's L2 at once, sc1 loads do not hit a stale L2 line of another XCD; the writer waits for
+// its stores (s_waitcnt vmcnt(0)) before taking an agent-scope ticket.
+__device__ __forceinline__ void st_sc1_dw(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ float ld_sc1_f(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return v;
+}
+// true in the workgroup that arrives last of `n` sharing *cnt (which it re-zeroes for the next
+// launch); every thread calls it (contains barriers)
+__device__ __forceinline__ bool wg_last_of(unsigned* cnt, unsigned n, int* flag_smem) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned old = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag_smem = old == n - 1;
+    if (*flag_smem) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      __hip_atomic_store(cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  __syncthreads();
+  return *flag_smem != 0;
+}
+
 #define DFCSA_CHECK_LAUNCH() \
   do {                       \
     hipError_t e_ = hipGetLastError(); \

@@ -57,6 +57,8 @@ extern int g_wgrad_narrow;
 extern int g_wgrad_fuse_all;
 extern int g_wgrad_fuse_max;
 extern int g_wgrad_nst;
+// n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
+unsigned* dfcsa_ticket_alloc(int n);
 extern int g_fra_generic;
 extern int g_fra_occ;
 extern int g_ew_tile_elems;

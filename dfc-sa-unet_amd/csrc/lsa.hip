@@ -232,16 +232,29 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
       c0 = (e - pj * cpp) * 8;
       int lo, hi;
       contrib_range(pj, P, W, lo, hi);
-      for (int w = lo + sl; w < hi; w += nsl) {
-        int i0, i1;
-        float l0, l1;
-        bilin_axis(w, P, W, i0, i1, l0, l1);
-        const float wt = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
-        if (wt == 0.f) continue;
-        float v[8];
-        load8<T>(row + (size_t)w * C + c0, v);
+      // 4 source columns per step: independent loads in flight (zero weights load nothing)
+      for (int w0 = lo + sl; w0 < hi; w0 += 4 * nsl) {
+        float wt[4], v[4][8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[q] += wt * v[q];
+        for (int u = 0; u < 4; ++u) {
+          const int w = w0 + u * nsl;
+          wt[u] = 0.f;
+          if (w < hi) {
+            int i0, i1;
+            float l0, l1;
+            bilin_axis(w, P, W, i0, i1, l0, l1);
+            wt[u] = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
+          }
+          if (wt[u] != 0.f) load8<T>(row + (size_t)w * C + c0, v[u]);
+          else
+#pragma unroll
+            for (int q = 0; q < 8; ++q) v[u][q] = 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (wt[u] != 0.f)
+#pragma unroll
+            for (int q = 0; q < 8; ++q) acc[q] += wt[u] * v[u][q];
       }
     }
     if (nsl == 1) {
@@ -271,8 +284,11 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
 // Channels x NSL slices of the h range (all 256 threads busy at C = 64), combined in LDS.
 __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
                                                               const float* __restrict__ o, const float* gamma,
-                                                              float* __restrict__ dO, float* __restrict__ gpart) {
+                                                              float* __restrict__ dO, float* __restrict__ gpart,
+                                                              unsigned* cnt, float* gamma_grad) {
   __shared__ float red[256 + 8];
+  __shared__ double rd[256];
+  __shared__ int flag;
   const int n = blockIdx.x, b = blockIdx.y, N = P * P;
   const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
@@ -286,12 +302,23 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
     const int c = cb + cl;
     float s = 0.f;
     if (c < C && sl < nsl) {
-      for (int h = lo + sl; h < hi; h += nsl) {
-        int i0, i1;
-        float l0, l1;
-        bilin_axis(h, P, H, i0, i1, l0, l1);
-        const float wt = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
-        if (wt != 0.f) s += wt * rows[(((size_t)b * H + h) * P + pj) * C + c];
+      for (int h0 = lo + sl; h0 < hi; h0 += 4 * nsl) {  // 4 independent loads in flight
+        float wt[4], v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          const int h = h0 + u * nsl;
+          wt[u] = 0.f;
+          if (h < hi) {
+            int i0, i1;
+            float l0, l1;
+            bilin_axis(h, P, H, i0, i1, l0, l1);
+            wt[u] = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
+          }
+          v[u] = wt[u] != 0.f ? rows[(((size_t)b * H + h) * P + pj) * C + c] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (wt[u] != 0.f) s += wt[u] * v[u];
       }
     }
     if (nsl > 1) {
@@ -309,7 +336,23 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
     }
   }
   gsum = block_reduce_sum(gsum, red + 256);
-  if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
+  if (!gamma_grad) {
+    if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
+    return;
+  }
+  // fused dgamma: the last workgroup sums gpart in index order (per thread), then a fixed tree
+  if (threadIdx.x == 0) st_sc1_dw(gpart + (size_t)b * N + n, gsum);
+  if (!wg_last_of(cnt, gridDim.x * gridDim.y, &flag)) return;
+  double v = 0.0;
+  const int total = gridDim.x * gridDim.y;
+  for (int i = threadIdx.x; i < total; i += 256) v += (double)ld_sc1_f(gpart + i);
+  rd[threadIdx.x] = v;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (threadIdx.x < k) rd[threadIdx.x] += rd[threadIdx.x + k];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *gamma_grad += (float)rd[0];
 }
 
 // grid (N, B): query row n -> dE[b][n][:], dq[b][n][:]
@@ -481,9 +524,12 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
 }
 
 extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const float* o,
-                                     const float* gamma, float* dO, float* gpart, int* ngpart, void* stream) {
+                                     const float* gamma, float* dO, float* gpart, int* ngpart, float* gamma_grad,
+                                     void* stream) {
+  unsigned* cnt = nullptr;
+  if (gamma_grad && !(cnt = dfcsa_ticket_alloc(1))) return DFCSA_EINVAL;
   hipLaunchKernelGGL(lsa_up_bwd_cols_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, P, rows, o,
-                     gamma, dO, gpart);
+                     gamma, dO, gpart, cnt, gamma_grad);
   DFCSA_CHECK_LAUNCH();
   if (ngpart) *ngpart = B * P * P;
   return 0;

@@ -86,8 +86,7 @@ class SumOut(torch.autograd.Function):
         part = torch.empty(nte * C, device=dout.device, dtype=torch.float32)
         dres = torch.empty_like(res) if ctx.needs_input_grad[4] else None
         call("dfcsa_bwd_sum_out", dt(ctx.dtype), M, C, P(dout), P(res), P(ctx.rs), P(dres), P(part), stream())
-        part, nt = ops.rows_reduce(part, nte, C)
-        call("dfcsa_sum_into", P(part), nt * C, P(grad_of(ctx.rs)), stream())
+        call("dfcsa_sum_into", P(part), nte * C, P(grad_of(ctx.rs)), stream())
         ctx.res = None
         return None, None, dout, (dout if ctx.has_b else None), dres
 

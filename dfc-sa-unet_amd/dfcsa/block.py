@@ -354,8 +354,8 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
     call("dfcsa_lsa_up_bwd_rows", dt(dtype), B, H, W, C, P(dattn), Pp, P(rows), stream())
     dO = torch.empty((B, N, C), device=dev, dtype=f32)
     gpart = torch.empty(B * N, device=dev, dtype=f32)
-    call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None, stream())
-    call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
+    call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
+         P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
     dE = torch.empty((B, N, N), device=dev, dtype=f32)
     dqkv = torch.empty((B, N, J), device=dev, dtype=f32)
     call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())

@@ -93,7 +93,6 @@ def core_backward(mod, saved, dy, dtype, pk):
     nt = ops.ntiles_ew(M, Jp)
     part = torch.empty(nt * Jp, device=dev, dtype=f32)
     call("dfcsa_channel_sum", T, M, Jp, P(dqkv), P(part), stream())
-    part, nt = ops.rows_reduce(part, nt, Jp)
     dbv = _grad_of(mod.value_conv.bias)
     tail = dbv if Jp == J else torch.zeros(Jp - 2 * Cq, device=dev, dtype=f32)
     call("dfcsa_slab_colsum3", P(part), nt, Jp, Cq, Cq, P(_grad_of(mod.query_conv.bias)),

@@ -179,8 +179,6 @@ def rows_reduce(src, T, rowlen):
 
 def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
     st = BNState(C, bn_mod.weight.device)
-    if training:
-        stats, ntiles = rows_reduce(stats, ntiles, 2 * ld)
     nbt = bn_mod.num_batches_tracked if training else None
     call("dfcsa_bn_finalize", P(stats) if training else None, ntiles, C, ld, count, P(conv_bias),
          P(bn_mod.weight), P(bn_mod.bias), P(bn_mod.running_mean), P(bn_mod.running_var), P(nbt),
@@ -199,7 +197,6 @@ def bn_act(dtype, y, bn, act):
 
 def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
-    partial, ntiles = rows_reduce(partial, ntiles, nsum * C)
     call("dfcsa_bn_bwd_finalize", P(partial), ntiles, nsum, C, count, P(coef), P(dgamma), P(dbeta), P(extra),
          stream())
     return coef
@@ -229,7 +226,6 @@ def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
 
 def colsum_into(slab, nt, C, out):
     """out[c] += sum_t slab[t][c]"""
-    slab, nt = rows_reduce(slab, nt, C)
     call("dfcsa_slab_colsum", P(slab), nt, C, P(out), stream())
 
 

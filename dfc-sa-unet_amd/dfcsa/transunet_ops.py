@@ -156,7 +156,6 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
     nt = LIB.dfcsa_colsum_ntiles(M)
     part = _f32((nt * C,), x.device)
     call("dfcsa_colsum_partial", dt(dtype), M, C, P(x), P(part), stream())
-    part, nt = ops.rows_reduce(part, nt, C)
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
 
 
@@ -179,7 +178,6 @@ def _ln_backward(dtype, dy, h, mr, ln, dres):
     part = _f32((nt * 2 * C,), h.device)
     dx = torch.empty_like(h)
     call("dfcsa_ln_bwd", dt(dtype), M, C, P(dy), P(h), P(mr), P(ln.weight), P(dres), P(dx), P(part), stream())
-    part, nt = ops.rows_reduce(part, nt, 2 * C)
     call("dfcsa_slab_colsum3", P(part), nt, 2 * C, C, C, P(grad_of(ln.weight)), P(grad_of(ln.bias)), None, stream())
     return dx
 

@@ -262,9 +262,12 @@ int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, floa
 /* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
 int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, const void* dattn, int P, float* rows,
                           void* stream);
-/* du[b][pi][pj][c] = sum_h wy(pi,h) rows[b][h][pj][c]; do = gamma*du; gpart[blk] = sum o*du */
+/* du[b][pi][pj][c] = sum_h wy(pi,h) rows[b][h][pj][c]; do = gamma*du; gpart[b*P*P + n] = sum_c o*du;
+ * gamma_grad != NULL: *gamma_grad += sum of gpart (fixed order, by the last workgroup: no extra
+ * launch); ngpart != NULL receives the gpart count B*P*P */
 int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const float* o,
-                          const float* gamma, float* dO, float* gpart, int* ngpart, void* stream);
+                          const float* gamma, float* dO, float* gpart, int* ngpart, float* gamma_grad,
+                          void* stream);
 /* attention core backward -> dqkv [B][N][2Cq+C]; dE scratch [B][N][N] */
 int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv, const float* A, const float* dO,
                        float* dE, float* dqkv, void* stream);
