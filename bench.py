@@ -218,6 +218,8 @@ def main():
                     help="dfc = the BASELINE headline (config 2/3); unet / transunet / fullres = configs 1 / 4 / 5")
     ap.add_argument("--val-steps", type=int, default=600)
     ap.add_argument("--no-trainer-faithful", action="store_true", help="skip the Trainer.train_epoch rate")
+    ap.add_argument("--sync-bn", action="store_true",
+                    help="opt-in SyncBatchNorm over the ranks (default: per-replica BN, standard DDP)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -258,6 +260,9 @@ def main():
     t = tg[lo:hi].to(dev)
     del xg, tg
 
+    if world > 1 and args.sync_bn:
+        from dfcsa import ops as dfops
+        dfops.set_sync_bn()
     model(x)  # materialise the flat parameter/gradient storage and packed operands first
     reducer = GradBucketReducer(model) if world > 1 else None
     scale = reducer.grad_scale if reducer else 1.0
@@ -410,7 +415,7 @@ def main():
                "config": {"workload": (f"DFC-SA-Res P={args.pool} features 64..512 {S}x{S} train step" if headline
                                        else f"{spec['label']} {S}x{S} train step"),
                           "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
-                          "parallelism": f"dp{world}", "final_loss": round(final_loss, 5),
+                          "parallelism": f"dp{world}", "sync_bn": bool(world > 1 and args.sync_bn), "final_loss": round(final_loss, 5),
                           "model_tflops": round(value * gflop / 1e3, 2) if gflop else None},
                "roofline": roof, "step_roofline": step_roof, "trainer_faithful": faithful,
                "cpu_baseline": cpu, "val_dice": vdice}

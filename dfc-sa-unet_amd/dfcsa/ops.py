@@ -177,8 +177,53 @@ def rows_reduce(src, T, rowlen):
     return dst, G
 
 
+# ---------------------------------------------------------------------------- SyncBN (opt-in)
+# BatchNorm stays per-replica by default (standard DDP).  set_sync_bn(group)
+# switches every BatchNorm of the MI355X path to SyncBatchNorm semantics over `group`: the forward
+# statistics (sum x, sum x^2) and the backward sums (sum dz, sum dz*xhat) are all-reduced, so mean,
+# variance, running statistics and the input gradient use the global batch; the BN weight/bias (and
+# res_scale) gradients stay local sums, as in torch.nn.SyncBatchNorm (DDP then averages them).
+# Shards must be equal-sized (the global count is world * local count).  One all-reduce of 2*C
+# floats per BatchNorm forward and nsum*C per backward, on the current stream (graph-capturable
+# with RCCL).
+_SYNC_BN = None
+
+
+def set_sync_bn(group=None, enabled=True):
+    """Enable (group = a torch.distributed process group, None = WORLD) or disable SyncBN."""
+    global _SYNC_BN
+    if not enabled:
+        _SYNC_BN = None
+        return
+    import torch.distributed as dist
+    g = group if group is not None else dist.group.WORLD
+    _SYNC_BN = (g, dist.get_world_size(g))
+
+
+def sync_bn_enabled():
+    return _SYNC_BN is not None
+
+
+def _allreduce_(t):
+    import torch.distributed as dist
+    g = _SYNC_BN[0]
+    if dist.get_backend(g) == "gloo":   # host-staged (CPU rehearsals / tests; synchronises)
+        h = t.cpu()
+        dist.all_reduce(h, op=dist.ReduceOp.SUM, group=g)
+        t.copy_(h)
+    else:                                # RCCL on the current stream
+        dist.all_reduce(t, op=dist.ReduceOp.SUM, group=g)
+
+
 def bn_finalize(bn_mod, conv_bias, stats, ntiles, C, ld, count, training):
     st = BNState(C, bn_mod.weight.device)
+    if training and _SYNC_BN is not None:
+        # global column sums [2][ld] (fp64 inside the kernel, one fp32 total per column), summed
+        # over the ranks, then finalised as a single row with the global count
+        tot = torch.zeros(2 * ld, device=stats.device, dtype=torch.float32)
+        call("dfcsa_slab_colsum", P(stats), ntiles, 2 * ld, P(tot), stream())
+        _allreduce_(tot)
+        stats, ntiles, count = tot, 1, count * _SYNC_BN[1]
     nbt = bn_mod.num_batches_tracked if training else None
     call("dfcsa_bn_finalize", P(stats) if training else None, ntiles, C, ld, count, P(conv_bias),
          P(bn_mod.weight), P(bn_mod.bias), P(bn_mod.running_mean), P(bn_mod.running_var), P(nbt),
@@ -197,6 +242,17 @@ def bn_act(dtype, y, bn, act):
 
 def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
+    if _SYNC_BN is not None:
+        # local sums -> the parameter gradients (dgamma, dbeta, res_scale); global sums -> coef
+        tot = torch.zeros(nsum * C, device=partial.device, dtype=torch.float32)
+        call("dfcsa_slab_colsum", P(partial), ntiles, nsum * C, P(tot), stream())
+        scratch = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
+        call("dfcsa_bn_bwd_finalize", P(tot), 1, nsum, C, count, P(scratch), P(dgamma), P(dbeta), P(extra),
+             stream())
+        _allreduce_(tot)
+        call("dfcsa_bn_bwd_finalize", P(tot), 1, nsum, C, count * _SYNC_BN[1], P(coef), None, None, None,
+             stream())
+        return coef
     call("dfcsa_bn_bwd_finalize", P(partial), ntiles, nsum, C, count, P(coef), P(dgamma), P(dbeta), P(extra),
          stream())
     return coef
