@@ -466,6 +466,234 @@ int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
   return 0;
 }
 
+// --------------------------------------------------------------------------------------------
+// 256x256 ping-pong kernel (deep 3x3 convs and dgrads with N % 256 == 0): ONE workgroup per CU,
+// 8 waves as 2 (M) x 4 (N), each wave owning a 128x64 output (acc[8][4] of 16x16 fragments).
+// The two wave rows (groups G0 = waves 0-3, G1 = waves 4-7; one wave of each per SIMD) run one
+// barrier apart: while one group issues its fragment reads and LDS-DMA for a phase, the other
+// runs that phase's 16 MFMAs at raised priority, so each SIMD's matrix pipe alternates between
+// its two waves instead of draining at a shared barrier.
+//
+// A K-tile (64 deep) is staged as four 16-KB half-tiles, A0 A1 B0 B1: A half h holds, for both
+// wave rows, the 64 output rows of M-quadrant h (tile rows wr*128 + h*64 + r); B half h the 32
+// columns of N-quadrant h of every wave column (tile columns wc*64 + h*32 + c).  Four phases per
+// K-tile compute the quadrants (0,0) (0,1) (1,1) (1,0) and read A0+B0, B1, A1 and nothing; each
+// phase also prefetches one half-tile into a slot whose previous contents both groups have
+// finished reading: B1 and A1 of K-tile t+1 in phases 1-2, A0 and B0 of K-tile t+2 in phases 3-4
+// (A0/B0 of this buffer were read in phase 1), so every half is issued 5-6 phases before it is
+// read.  Each half = 2 DMA instructions per wave; the counted vmcnt of each phase retires the
+// half read in the next phase, and precedes a barrier that both groups pass before that read
+// (G0 reads after its second barrier of the phase, G1 one barrier later).
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ void raw_barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  asm volatile("s_barrier" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int DEPTH, bool RF, bool BAL>
+__global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs args) {
+  using T = bf16_t;
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
+  constexpr int HALF = 128 * 128, BUF = 4 * HALF;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  constexpr int SMEM = (2 * BUF > BM * OSTR) ? 2 * BUF : BM * OSTR;
+  constexpr int LEAD = DEPTH == 1 ? 4 : 6;   // issue slot of half-tile s = s - LEAD
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nN = args.N / BN;
+  const int L = xcd_remap(blockIdx.x, nN * ((args.M + BM - 1) / BM));
+  if (L < 0) return;  // whole workgroup: no barrier is left unmatched
+  const int n_tile = L % nN, m_tile = L / nN;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int M = args.M;
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+  const int rsub = lane >> 3;
+  const int lane_ch = cchunk * 8;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+
+  // the 4 A rows and 4 B rows this lane fetches: index q = half*2 + instruction
+  int a_off[4], a_tap[4], b_off[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int h = q >> 1, j = q & 1;
+    const int hr = (j * 8 + wave) * 8 + rsub;            // row of the half-tile image
+    const int m = m0 + (hr >> 6) * 128 + h * 64 + (hr & 63);
+    a_off[q] = lane_ch;
+    a_tap[q] = 0;
+    if (m < M) {
+      const int b = dm_div(args.dm_hw, m);
+      const int rem = m - b * args.dm_hw.d;
+      const int oh = dm_div(args.dm_w, rem);
+      const int ow = rem - oh * args.dm_w.d;
+      const int ih = oh * args.stride, iw = ow * args.stride;
+      a_off[q] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch;
+      int t = 0;
+#pragma unroll
+      for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+        for (int dw = -1; dw <= 1; ++dw)
+          t |= (ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+      a_tap[q] = t;
+    }
+    const int n = n0 + (hr >> 5) * 64 + h * 32 + (hr & 31);
+    b_off[q] = n * args.Kpad + lane_ch;
+  }
+  const void* zero = (const void*)g_zero_page;
+  const T* Bw = (const T*)args.Bw;
+  const int nk = args.Kpad / 64;
+  const int slast = 4 * nk - 1;
+
+  // half-tile s = 4 * K-tile + {0: A0, 1: B0, 2: B1, 3: A1} into buffer (K-tile & 1)
+  auto issue = [&](int sq) {
+    if (sq > slast) return;
+    const int kt = sq >> 2, i = sq & 3;
+    char* bufp = smem + (kt & 1) * BUF;
+    if (i == 0 || i == 3) {
+      const int h = i == 0 ? 0 : 1;
+      char* dst = bufp + h * HALF;
+      const int k0 = kt * 64;
+      const int seg = dm_div(args.dm_cseg, k0);
+      const int ch0 = k0 - seg * args.Cseg;
+      const ConvSeg sg = args.seg[seg];
+      const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
+      const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
+      const T* base = (const T*)sg.ptr;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bool ok = __builtin_amdgcn_ubfe(a_tap[h * 2 + j], tb, 1) != 0;
+        const void* src = ok ? (const void*)(base + (unsigned)(a_off[h * 2 + j] + delta)) : zero;
+        glds16(src, dst + (j * 8 + wv) * 1024);
+      }
+    } else {
+      const int h = i == 1 ? 0 : 1;
+      char* dst = bufp + (2 + h) * HALF;
+#pragma unroll
+      for (int j = 0; j < 2; ++j) glds16(Bw + (unsigned)(b_off[h * 2 + j] + kt * 64), dst + (j * 8 + wv) * 1024);
+    }
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+  Frag<T> fa[4][2], fb0[2][2], fb1[2][2];
+
+  auto read_a = [&](const char* img) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) read_frag<T>(img, wr * 64 + i * 16 + (lane & 15), g, lane, fa[i][g]);
+  };
+  auto read_b = [&](const char* img, Frag<T> (&fb)[2][2]) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int g = 0; g < 2; ++g) read_frag<T>(img, wc * 32 + j * 16 + (lane & 15), g, lane, fb[j][g]);
+  };
+  auto quad = [&](int ms, int ns, const Frag<T> (&fb)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) mma(acc[ms * 4 + i][ns * 2 + j], fa[i][g], fb[j][g]);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  // The wait of slot q (= 4 * K-tile + phase) must retire every half read in slot q + 1:
+  // A0 (q+1) and -- unless pre-read in phase 4 -- B0 (q+2) before phase 1; B1 (q+2) before
+  // phase 2; A1 (q+2) before phase 3; with BAL the next B0 (q+3) before phase 4.
+  auto vwait = [&](int q) {
+    const int p = q & 3;
+    const int need = p == 2 ? (BAL ? q + 3 : q + 1) : (p == 3 ? (BAL ? q + 1 : q + 2) : q + 2);
+    const int r = min(q + LEAD, slast) - min(need, slast);
+    if (r >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (r == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (r == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (r == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  };
+
+  for (int sq = 0; sq < LEAD; ++sq) issue(sq);
+  {
+    const int r = min(LEAD - 1, slast) - (BAL ? 1 : 1);   // halves 0 and 1 needed first
+    if (r >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    else if (r == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else if (r == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else if (r == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  raw_barrier();
+  if (BAL) read_b(smem + 2 * HALF, fb0);   // B0 of K-tile 0 (later ones: pre-read in phase 4)
+  if (wr == 1) raw_barrier();   // G1 runs one barrier behind G0
+
+  // one K-tile; fbp holds (BAL) or receives its B0, fbq receives B1 (and with BAL the next B0)
+  auto ktile = [&](int kt, Frag<T> (&fbp)[2][2], Frag<T> (&fbq)[2][2]) {
+    const char* buf = smem + (kt & 1) * BUF;
+    const char* nbuf = smem + ((kt + 1) & 1) * BUF;
+    const int q = 4 * kt;
+    // phase 1: quadrant (0,0) [A0 + B0]
+    if (!RF) issue(q + LEAD);
+    read_a(buf);
+    if (!BAL) read_b(buf + 2 * HALF, fbp);
+    if (RF) issue(q + LEAD);
+    vwait(q);
+    raw_barrier();
+    quad(0, 0, fbp);
+    raw_barrier();
+    // phase 2: quadrant (0,1) [A0 + B1]
+    if (!RF) issue(q + 1 + LEAD);
+    read_b(buf + 3 * HALF, fbq);
+    if (RF) issue(q + 1 + LEAD);
+    vwait(q + 1);
+    raw_barrier();
+    quad(0, 1, fbq);
+    raw_barrier();
+    // phase 3: quadrant (1,1) [A1 + B1]
+    if (!RF) issue(q + 2 + LEAD);
+    read_a(buf + HALF);
+    if (RF) issue(q + 2 + LEAD);
+    vwait(q + 2);
+    raw_barrier();
+    quad(1, 1, fbq);
+    raw_barrier();
+    // phase 4: quadrant (1,0) [A1 + B0]
+    if (!RF) issue(q + 3 + LEAD);
+    if (BAL && kt + 1 < nk) read_b(nbuf + 2 * HALF, fbq);
+    if (RF) issue(q + 3 + LEAD);
+    vwait(q + 3);
+    raw_barrier();
+    quad(1, 0, fbp);
+    raw_barrier();
+  };
+  if (BAL) {
+    for (int kt = 0; kt < nk; kt += 2) {
+      ktile(kt, fb0, fb1);
+      if (kt + 1 < nk) ktile(kt + 1, fb1, fb0);
+    }
+  } else {
+    for (int kt = 0; kt < nk; ++kt) ktile(kt, fb0, fb1);
+  }
+  if (wr == 0) raw_barrier();   // re-align the groups before the epilogue reuses the LDS
+  __syncthreads();
+  conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wr, wc);
+}
+
+template <int DEPTH, bool RF, bool BAL>
+int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
+  dim3 grid(xcd_pad((a.N / 256) * ((a.M + 255) / 256)));
+  hipLaunchKernelGGL((conv_gemm_pp_kernel<DEPTH, RF, BAL>), grid, dim3(512), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
@@ -788,6 +1016,12 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
         case 17: return launch_glds<256, 64, 8, 1, 2>(a, st);
         case 18: return launch_glds<256, 128, 8, 2, 2>(a, st);
         case 19: return launch_glds<64, 64, 2, 2, 2>(a, st);
+        case 20: if (a.N % 256 == 0) return launch_pp<1, true, false>(a, st); break;
+        case 21: if (a.N % 256 == 0) return launch_pp<1, true, true>(a, st); break;
+        case 22: if (a.N % 256 == 0) return launch_pp<2, true, false>(a, st); break;
+        case 23: if (a.N % 256 == 0) return launch_pp<2, false, true>(a, st); break;
+        case 24: if (a.N % 256 == 0) return launch_pp<1, false, false>(a, st); break;
+        case 25: if (a.N % 256 == 0) return launch_pp<2, true, true>(a, st); break;
         default: break;
       }
     }
@@ -801,6 +1035,12 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // fewer than one workgroup of 128x128 per CU (the 14^2 level, 28^2 with N <= 256): 128x64 doubles the
     // workgroup count (gemm_bench: bottleneck dgrad 123 -> 108 us, bottleneck fwd 59 -> 52 us).
     if (a.N <= 64) return a.M >= 65536 ? launch_glds<256, 64, 8, 1, 2>(a, st) : launch_glds<128, 64, 4, 1, 2>(a, st);
+    // 256x256 ping-pong tiles (one workgroup per CU: half the L2->LDS bytes per flop of two
+    // 128x128 workgroups) wherever they still give >= 150 workgroups and a long K: measured
+    // (tools/pp_check.py) 1.06-1.23x the 128x128 tile on the 3x3 fwd/dgrad of the 112^2-28^2
+    // levels, slower below ~150 workgroups (one partial wave of tiles)
+    if (a.N % 256 == 0 && a.K >= 1152 && ((a.M + 255) / 256) * (a.N / 256) >= 150)
+      return launch_pp<2, true, false>(a, st);
     if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) {
       // still under one 128x64 workgroup per CU with a short K (the ViT GEMMs of TransUNet:
       // M = 8 x 196 rows, K = 768 / 3072): 64x64 tiles (4 waves of 32x32) double the workgroups
