@@ -407,10 +407,15 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
     for (int i = 0; i < A_IN; ++i) {
       const bool ok = __builtin_amdgcn_ubfe(a_tap[i], tb, 1) != 0;
       const void* src = ok ? (const void*)(base + (unsigned)(a_off[i] + delta)) : zero;
+      if (args.dbg & 1) src = (const char*)zero + lane_ch * 2;
       glds16(src, A + (i * NW + wv) * 8 * 128);
     }
 #pragma unroll
-    for (int i = 0; i < B_IN; ++i) glds16(b_ptr[i] + (size_t)kt * b_step[i], B + (i * NW + wv) * 8 * 128);
+    for (int i = 0; i < B_IN; ++i) {
+      const void* src = b_ptr[i] + (size_t)kt * b_step[i];
+      if (args.dbg & 2) src = (const char*)zero + lane_ch * 2;
+      glds16(src, B + (i * NW + wv) * 8 * 128);
+    }
   };
 
   f32x4_t acc[FM][FN];
@@ -565,13 +570,18 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
       for (int j = 0; j < 2; ++j) {
         const bool ok = __builtin_amdgcn_ubfe(a_tap[h * 2 + j], tb, 1) != 0;
         const void* src = ok ? (const void*)(base + (unsigned)(a_off[h * 2 + j] + delta)) : zero;
+        if (args.dbg & 1) src = (const char*)zero + lane_ch * 2;
         glds16(src, dst + (j * 8 + wv) * 1024);
       }
     } else {
       const int h = i == 1 ? 0 : 1;
       char* dst = bufp + (2 + h) * HALF;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) glds16(Bw + (unsigned)(b_off[h * 2 + j] + kt * 64), dst + (j * 8 + wv) * 1024);
+      for (int j = 0; j < 2; ++j) {
+        const void* src = Bw + (unsigned)(b_off[h * 2 + j] + kt * 64);
+        if (args.dbg & 2) src = (const char*)zero + lane_ch * 2;
+        glds16(src, dst + (j * 8 + wv) * 1024);
+      }
     }
   };
 
@@ -978,6 +988,7 @@ int try_stream(const ConvGemmArgs& a, hipStream_t st) {
   return pick(nwc);
 }
 
+int g_conv_dbg = 0;  // knob 15: timing experiments (ConvGemmArgs::dbg)
 int g_conv_cfg = 0;  // tuning override (dfcsa_set_tuning knob 1; 7 = no streaming 1x1 kernel)
 
 // config ids: 1 reg 128x64, 2 reg 128x128, 3 dma 128x64, 4 dma 256x64, 5 dma 128x128, 6 dma 256x128
@@ -1082,6 +1093,7 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   for (int i = 0; i < 3; ++i) a.dest[i] = i < d->ndest ? d->dest[i] : nullptr;
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
+  a.dbg = g_conv_dbg;
   hipStream_t st = (hipStream_t)stream;
   // profiling classes: the 1x1 streaming GEMMs are HBM-bound (their unit is bytes: A and the
   // weight panel read once, the output written once, read too when accumulating); the tile
@@ -1109,6 +1121,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 11) { g_ew_tile_elems = value >= 4096 ? value : 16384; return 0; }
   if (knob == 12) { g_wgrad_fuse_all = value; return 0; }
   if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
+  if (knob == 15) { g_conv_dbg = value; return 0; }
   if (knob == 14) { g_wgrad_nst = (value >= 2 && value <= 4) ? value : 2; return 0; }
   return DFCSA_EINVAL;
 }

@@ -21,6 +21,7 @@ struct ConvGemmArgs {
   int Nd, accumulate;
   float* stats;
   int Hout, Wout;
+  int dbg;   // timing experiments only (knob 15): 1 = A operand from the zero page, 2 = B
 };
 
 struct WgradArgs {

@@ -27,7 +27,7 @@ from ._lib import call
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
-from .streams import on_side
+from .streams import join_branch, on_branch, on_side
 
 
 def grad_of(p):
@@ -88,21 +88,30 @@ def block_forward(blk, xs, pool_size, training, dtype):
     def stats(n):
         return torch.empty(nt * 2 * n, device=dev, dtype=torch.float32) if training else None
 
-    # ---- local branch conv + attention entry / residual ----
-    y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    st1 = stats(C)
-    ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
-                  bias=conv1.bias, stats=st1)
+    # ---- attention entry / residual 1x1 conv, then the local branch 3x3 conv ----
+    Cq = lsa.query_conv.out_channels
+    fullres = getattr(lsa, "full_resolution", False)
     y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
     st2 = stats(N2)
     ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
                   [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
+    # the pooled attention chain (bn2 statistics -> pool -> q/k/v -> softmax core) runs on the
+    # branch stream beside the 3x3 conv (streams.on_branch)
+    branch = not fullres and ops._SYNC_BN is None
+    with on_branch(dev, branch, y2, st2):
+        bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt, C, N2, M, training)
+        if not fullres:
+            Pp = pool_size
+            lsa_saved = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
+    y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+    st1 = stats(C)
+    ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
+                  bias=conv1.bias, stats=st1)
     bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt, C, C, M, training)
-    bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt, C, N2, M, training)
+    join_branch(dev, branch, bn2, None if fullres else lsa_saved)
 
-    Cq = lsa.query_conv.out_channels
-    if getattr(lsa, "full_resolution", False):
+    if fullres:
         # ---- FullResolutionAttention (unet_dfc_sa_ablation_attention.py:42-47, :71-75) on the
         #      unpooled map a = relu(bn2 y2): flash-style kernels, no N x N tensor ----
         Pp, J, N = 0, 2 * Cq + C, H * W
@@ -113,9 +122,8 @@ def block_forward(blk, xs, pool_size, training, dtype):
     else:
         # ---- LightSelfAttention on the pooled map ----
         s.fra = None
-        Pp = pool_size
         J, N = 2 * Cq + C, Pp * Pp
-        pooled, qkv, A, o, Wqkv = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
+        pooled, qkv, A, o, Wqkv = lsa_saved
         local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
         attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
         call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
@@ -252,24 +260,29 @@ def block_backward(blk, s, dout, need_dx, dtype):
     ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
 
-    dz2 = torch.empty_like(s.y2)
-    if s.fra is not None:
-        # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
-        da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
-        s.fra = None
-        call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-             P(bn2.invstd), P(dz2), P(part), stream())
-        del da
-    else:
-        # ---- LightSelfAttention ----
-        dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
-        # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
-        call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
-             P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part), stream())
+    # the attention chain (LightSelfAttention backward -> attention entry -> bn2 backward) runs
+    # on the branch stream beside the local branch's bn1 backward (streams.on_branch)
+    branch = s.fra is None and ops._SYNC_BN is None
+    with on_branch(dev, branch, dattn):
+        dz2 = torch.empty_like(s.y2)
+        part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+        if s.fra is not None:
+            # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
+            da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
+            s.fra = None
+            call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+                 P(bn2.invstd), P(dz2), P(part2), stream())
+            del da
+        else:
+            # ---- LightSelfAttention ----
+            dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
+            # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
+            call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
+                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part2), stream())
+        coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+        dy2 = ops.bn_bwd_apply(dtype, dz2, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
+        del dz2, part2, coef2
     del dattn
-    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
-    dy2 = ops.bn_bwd_apply(dtype, dz2, s.y2, bn2, bn2m.weight, coef, grad_of(conv2.bias))
-    del dz2
 
     # ---- local branch: relu(bn1 y1) ----
     dz1 = torch.empty_like(s.y1)
@@ -279,6 +292,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
     coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
     dy1 = ops.bn_bwd_apply(dtype, dz1, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
     del dz1
+    join_branch(dev, branch, dy2)
 
     # ---- weight gradients of the input-side convs (side stream) ----
     xs = s.xs

@@ -67,3 +67,66 @@ def on_side(device, *tensors):
     for t in tensors:
         if t is not None:
             t.record_stream(side)
+
+
+# ---------------------------------------------------------------------------------------------
+# Branch stream: concurrency INSIDE a block.  The LightSelfAttention chain of a DFC-SA block
+# (pooled statistics, q/k/v projections on B*P*P rows, the N = P*P softmax core and their
+# backward) is a string of latency-bound launches that use a few dozen workgroups each, and it
+# is independent of the local 3x3 branch in both directions (forward: after the 1x1 attention
+# entry conv, until the local/attention merge; backward: after the gate backward, until the
+# input-gradient GEMM).  It is forked onto this stream so that it runs beside the local branch's
+# GEMM / elementwise kernels instead of between them.  DFCSA_BRANCH_STREAM=0 disables it.
+BRANCH_ENABLED = [os.environ.get("DFCSA_BRANCH_STREAM", "1") == "1"]
+_BRANCH = {}
+
+
+def branch_stream(device):
+    idx = device.index if device.index is not None else torch.cuda.current_device()
+    s = _BRANCH.get(idx)
+    if s is None:
+        s = torch.cuda.Stream(device=idx)
+        _BRANCH[idx] = s
+    return s
+
+
+def _record(obj, stream):
+    if obj is None:
+        return
+    if isinstance(obj, torch.Tensor):
+        obj.record_stream(stream)
+    elif isinstance(obj, (tuple, list)):
+        for o in obj:
+            _record(o, stream)
+    else:  # a plain record object (e.g. ops.BNState, __slots__ of tensors)
+        names = list(getattr(obj, "__slots__", ())) + list(getattr(obj, "__dict__", {}).keys())
+        for n in names:
+            o = getattr(obj, n, None)
+            if isinstance(o, (torch.Tensor, tuple, list)):
+                _record(o, stream)
+
+
+@contextlib.contextmanager
+def on_branch(device, enabled, *inputs):
+    """Run the enclosed launches on the branch stream, after everything issued so far on the
+    current stream.  `inputs` (allocated on the current stream, read on the branch) are
+    record_stream-ed.  The caller joins with join_branch(device, enabled, *outputs)."""
+    if not (enabled and BRANCH_ENABLED[0]):
+        yield None
+        return
+    main = torch.cuda.current_stream(device)
+    br = branch_stream(device)
+    br.wait_stream(main)
+    with torch.cuda.stream(br):
+        yield br
+    _record(inputs, br)
+
+
+def join_branch(device, enabled, *outputs):
+    """The current stream waits for the branch; `outputs` (allocated on the branch, used on the
+    current stream from here on) are record_stream-ed."""
+    if not (enabled and BRANCH_ENABLED[0]):
+        return
+    main = torch.cuda.current_stream(device)
+    main.wait_stream(branch_stream(device))
+    _record(outputs, main)
