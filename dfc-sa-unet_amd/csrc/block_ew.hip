@@ -38,6 +38,8 @@ enum {
   EW_CHANNEL_SUM,
   EW_SUM_OUT,       // ablation blocks: out = a0 (+ a1) + res_scale * a2
   EW_BWD_SUM_OUT,   // its backward: dres = res_scale * dout, partial sums of dout * res
+  EW_BN_BWD_APPLY_RELU,   // BN_BWD_APPLY with dz = relu'(bn(y)) * dact recomputed (no dz tensor)
+  EW_BN_BWD_APPLY_ENTRY,  // BN_BWD_APPLY with the attention-entry dz recomputed (no dz tensor)
 };
 
 struct EwArgs {
@@ -82,6 +84,26 @@ __device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, in
   l0 = 1.f - l1;
 }
 
+// Raw 16-B (bf16) / 32-B (fp32) chunk of 8 elements: loads are issued as raw vectors and
+// unpacked only when consumed, so a batch of U pixels costs 4 (bf16) VGPRs per input per pixel.
+template <typename T> struct Raw;
+template <> struct Raw<bf16_t> { uint4 v; };
+template <> struct Raw<float> { float4 v0, v1; };
+__device__ __forceinline__ Raw<bf16_t> ldraw(const bf16_t* p) { Raw<bf16_t> r; r.v = *(const uint4*)p; return r; }
+__device__ __forceinline__ Raw<float> ldraw(const float* p) {
+  Raw<float> r; r.v0 = *(const float4*)p; r.v1 = *(const float4*)(p + 4); return r;
+}
+__device__ __forceinline__ void unraw(const Raw<bf16_t>& r, float (&v)[8]) {
+  const uint4 u = r.v;
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void unraw(const Raw<float>& r, float (&v)[8]) {
+  v[0] = r.v0.x; v[1] = r.v0.y; v[2] = r.v0.z; v[3] = r.v0.w; v[4] = r.v1.x; v[5] = r.v1.y; v[6] = r.v1.z; v[7] = r.v1.w;
+}
+
 // ------------------------------- forward (no reductions) -------------------------------
 // Each lane keeps ONE 8-channel chunk for the whole grid-stride loop (the stride, a multiple of
 // 256 chunks, is a multiple of C/8 whenever C/8 divides 256 -- host-checked, `fixed`), so the
@@ -103,6 +125,108 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
   if (fixed) {
     if (a.a0 && a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
     if constexpr (MODE == EW_LOCAL_ATTN) { ld8f(a.sc2 + c0, sc2); ld8f(a.sh2 + c0, sh2); }
+  }
+  if (fixed) {
+    // batched: the loads of U chunks are issued before any of their stores (see ew_red_kernel)
+    constexpr int U = sizeof(T) == 2 ? 4 : 2;
+    constexpr int NIN = MODE == EW_GATE_FUSE || MODE == EW_SUM_OUT ? 3 : (MODE == EW_BN_ACT ? 1 : 2);
+    const float scal = (a.scalar && (MODE == EW_LOCAL_ATTN || MODE == EW_BLOCK_OUT || MODE == EW_SUM_OUT))
+                           ? *a.scalar : 0.f;
+    const bool has0 = a.a0 != nullptr, has1 = a.a1 != nullptr, st0 = a.o0 != nullptr;
+    const int elast = total - cpp + (first % cpp);   // last chunk of this lane's channel chunk
+    for (int eb = first; eb < total; eb += U * stride) {
+      Raw<T> in[U][NIN];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        // unconditional loads (see ew_red_kernel): chunks past the end re-load a valid pixel of
+        // this lane's channel chunk (stride is a multiple of cpp), their results are unused
+        const int e = min(eb + u * stride, elast);
+        {
+          const size_t off = (size_t)(e / cpp) * a.C + c0;
+          if (has0) in[u][0] = ldraw(A0 + off);
+          if constexpr (MODE == EW_LOCAL_ATTN || MODE == EW_BLOCK_OUT || MODE == EW_GATE_FUSE) in[u][1] = ldraw(A1 + off);
+          if constexpr (MODE == EW_GATE_FUSE) in[u][2] = ldraw(A2 + off);
+          if constexpr (MODE == EW_SUM_OUT) {
+            if (has1) in[u][1] = ldraw(A1 + off);
+            in[u][2] = ldraw(A2 + off);
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep every load of the batch ahead of its compute
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = eb + u * stride;
+        if (e >= total) break;
+        const int m = e / cpp;
+        const size_t off = (size_t)m * a.C + c0;
+        float y[8], out[8];
+        if (has0) unraw(in[u][0], y);
+        if constexpr (MODE == EW_BN_ACT) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float v = y[q] * sc[q] + sh[q];
+            out[q] = a.act == 1 ? fmaxf(v, 0.f) : (a.act == 2 ? sigm(v) : v);
+          }
+          store8<T>(O0 + off, out);
+        } else if constexpr (MODE == EW_LOCAL_ATTN) {
+          if (st0) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f);
+            store8<T>(O0 + off, out);
+          }
+          float y2[8];
+          unraw(in[u][1], y2);
+          const int hw = a.H * a.W;
+          const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
+          int h0, h1, w0, w1;
+          float lh0, lh1, lw0, lw1;
+          bilin_axis(h, a.P, a.H, h0, h1, lh0, lh1);
+          bilin_axis(w, a.P, a.W, w0, w1, lw0, lw1);
+          const float* ob = a.tbl + (size_t)b * a.P * a.P * a.C + c0;
+          float o00[8], o01[8], o10[8], o11[8];
+          ld8f(ob + (size_t)(h0 * a.P + w0) * a.C, o00);
+          ld8f(ob + (size_t)(h0 * a.P + w1) * a.C, o01);
+          ld8f(ob + (size_t)(h1 * a.P + w0) * a.C, o10);
+          ld8f(ob + (size_t)(h1 * a.P + w1) * a.C, o11);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float upv = lh0 * (lw0 * o00[q] + lw1 * o01[q]) + lh1 * (lw0 * o10[q] + lw1 * o11[q]);
+            const float v = y2[q] * sc2[q] + sh2[q];
+            out[q] = scal * upv + (a.act ? fmaxf(v, 0.f) : v);
+          }
+          store8<T>(O1 + off, out);
+        } else if constexpr (MODE == EW_GATE_FUSE) {
+          float l[8], at[8];
+          unraw(in[u][1], l);
+          unraw(in[u][2], at);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float g = sigm(y[q] * sc[q] + sh[q]);
+            out[q] = g * l[q] + (1.f - g) * at[q];
+          }
+          store8<T>(O0 + off, out);
+        } else if constexpr (MODE == EW_BLOCK_OUT) {
+          float r[8];
+          unraw(in[u][1], r);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) out[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f) + scal * r[q];
+          store8<T>(O0 + off, out);
+        } else if constexpr (MODE == EW_SUM_OUT) {
+          float r[8];
+          unraw(in[u][2], r);
+          if (has1) {
+            float bb[8];
+            unraw(in[u][1], bb);
+#pragma unroll
+            for (int q = 0; q < 8; ++q) y[q] += bb[q];
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) out[q] = y[q] + scal * r[q];
+          store8<T>(O0 + off, out);
+        }
+      }
+    }
+    return;
   }
 #pragma unroll 2
   for (int e = first; e < total; e += stride) {
@@ -190,8 +314,34 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
 template <int MODE> struct NSums { static constexpr int v = 2; };
 template <> struct NSums<EW_BWD_BLOCK_OUT> { static constexpr int v = 3; };
 template <> struct NSums<EW_BN_BWD_APPLY> { static constexpr int v = 1; };
+template <> struct NSums<EW_BN_BWD_APPLY_RELU> { static constexpr int v = 1; };
+template <> struct NSums<EW_BN_BWD_APPLY_ENTRY> { static constexpr int v = 1; };
 template <> struct NSums<EW_CHANNEL_SUM> { static constexpr int v = 1; };
 template <> struct NSums<EW_BWD_SUM_OUT> { static constexpr int v = 1; };
+
+// Attention-entry gradient of pixel m (channels c0..c0+7): the adaptive-avg-pool backward of
+// dpooled ([B][P][P][C] fp32), i.e. the sum over the pooling windows containing (h, w) of
+// dpooled / window size (windows rows [floor(i*H/P), ceil((i+1)*H/P)) as torch's adaptive pool).
+__device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, float (&add)[8]) {
+  const int hw = a.H * a.W;
+  const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - h * a.W;
+  const int P = a.P;
+  const int pi0 = (h * P) / a.H, pi1 = ((h + 1) * P + a.H - 1) / a.H - 1;
+  const int pj0 = (w * P) / a.W, pj1 = ((w + 1) * P + a.W - 1) / a.W - 1;
+#pragma unroll
+  for (int q = 0; q < 8; ++q) add[q] = 0.f;
+  for (int pi = pi0; pi <= pi1; ++pi) {
+    const int hs = (pi * a.H) / P, he = ((pi + 1) * a.H + P - 1) / P;
+    for (int pj = pj0; pj <= pj1; ++pj) {
+      const int ws = (pj * a.W) / P, we = ((pj + 1) * a.W + P - 1) / P;
+      const float inv = 1.f / (float)((he - hs) * (we - ws));
+      float v[8];
+      ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) add[q] += v[q] * inv;
+    }
+  }
+}
 
 template <typename T, int MODE>
 __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
@@ -224,7 +374,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   if (active) {
     if (a.sc) { ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); }
     if (a.mean) { ld8f(a.mean + c0, mu); ld8f(a.invstd + c0, is); }
-    if constexpr (MODE == EW_BN_BWD_APPLY) {
+    if constexpr (MODE == EW_BN_BWD_APPLY || MODE == EW_BN_BWD_APPLY_RELU || MODE == EW_BN_BWD_APPLY_ENTRY) {
       ld8f(a.gamma + c0, gk);
       ld8f(a.coef + c0, k0);
       ld8f(a.coef + a.C + c0, k1);
@@ -232,124 +382,152 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
       for (int q = 0; q < 8; ++q) gk[q] *= is[q];
     }
   }
+  // Batched loop: all loads of U pixels are issued before any of their stores, so U pixels'
+  // memory requests are in flight at once whatever alias analysis concludes (the compiler
+  // otherwise orders every load after the previous pixel's stores: one round trip per pixel).
+  constexpr int U = sizeof(T) == 2 ? 4 : 2;
+  constexpr int NIN = MODE == EW_BWD_GATE ? 6 : (MODE == EW_BWD_BLOCK_OUT ? 3 : (MODE == EW_CHANNEL_SUM ? 1 : 2));
+  const float scal = (a.scalar && (MODE == EW_BWD_BLOCK_OUT || MODE == EW_BWD_SUM_OUT)) ? *a.scalar : 0.f;
+  const bool st0 = O0 != nullptr, st1 = O1 != nullptr;
   if (active) {
-#pragma unroll 4
-    for (int m = mbeg + lane_px; m < mend; m += pl) {
-      const size_t off = (size_t)m * a.C + c0;
-      if constexpr (MODE == EW_CHANNEL_SUM) {
-        float x[8];
-        load8<T>(A0 + off, x);
+    for (int mb = mbeg + lane_px; mb < mend; mb += U * pl) {
+      Raw<T> in[U][NIN];
+      float add[U][8];
 #pragma unroll
-        for (int q = 0; q < 8; ++q) acc[0][q] += x[q];
-      } else if constexpr (MODE == EW_BWD_SUM_OUT) {
-        // a0 = dout, a2 = res; o1 = dres (optional)
-        float d[8], r[8], dr[8];
-        load8<T>(A0 + off, d);
-        load8<T>(A2 + off, r);
-        const float rs = *a.scalar;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          dr[q] = rs * d[q];
-          acc[0][q] += d[q] * r[q];
-        }
-        if (O1) store8<T>(O1 + off, dr);
-      } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
-        // a0 = dout, a1 = y4, a2 = res; o0 = dz4, o1 = dres
-        float d[8], y[8], r[8], dz[8], dr[8];
-        load8<T>(A0 + off, d);
-        load8<T>(A1 + off, y);
-        load8<T>(A2 + off, r);
-        const float rs = *a.scalar;
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
-          dz[q] = z;
-          dr[q] = rs * d[q];
-          acc[0][q] += z;
-          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
-          acc[2][q] += d[q] * r[q];
-        }
-        store8<T>(O0 + off, dz);
-        store8<T>(O1 + off, dr);
-      } else if constexpr (MODE == EW_BWD_RELU_BN) {
-        float d[8], y[8], dz[8];
-        load8<T>(A0 + off, d);
-        load8<T>(A1 + off, y);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
-          dz[q] = z;
-          acc[0][q] += z;
-          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
-        }
-        store8<T>(O0 + off, dz);
-      } else if constexpr (MODE == EW_BWD_GATE) {
-        // a0 = dfused, a1 = y3, a2 = local, a3 = attn; o0 = dlocal(+=), o1 = dattn(+=), o2 = dz3
-        float df[8], y[8], l[8], at[8], dl[8], da[8], dz[8];
-        load8<T>(A0 + off, df);
-        load8<T>(A1 + off, y);
-        load8<T>(A2 + off, l);
-        load8<T>(A3 + off, at);
-        load8<T>(O0 + off, dl);
-        load8<T>(O1 + off, da);
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float g = sigm(y[q] * sc[q] + sh[q]);
-          float dg = df[q] * (l[q] - at[q]);
-          float z = dg * g * (1.f - g);
-          dz[q] = z;
-          dl[q] += df[q] * g;
-          da[q] += df[q] * (1.f - g);
-          acc[0][q] += z;
-          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
-        }
-        store8<T>(O0 + off, dl);
-        store8<T>(O1 + off, da);
-        store8<T>(O2 + off, dz);
-      } else if constexpr (MODE == EW_BWD_ATTN_ENTRY) {
-        // a0 = dattn, a1 = y2, tbl = dpooled [B][P][P][C]; o0 = dz2
-        float d[8], y[8], dz[8];
-        load8<T>(A0 + off, d);
-        load8<T>(A1 + off, y);
-        const int hw = a.H * a.W;
-        const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - h * a.W;
-        const int P = a.P;
-        // adaptive-avg-pool windows containing (h, w): rows [floor(i*H/P), ceil((i+1)*H/P))
-        const int pi0 = (h * P) / a.H, pi1 = ((h + 1) * P + a.H - 1) / a.H - 1;
-        const int pj0 = (w * P) / a.W, pj1 = ((w + 1) * P + a.W - 1) / a.W - 1;
-        float add[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-        for (int pi = pi0; pi <= pi1; ++pi) {
-          const int hs = (pi * a.H) / P, he = ((pi + 1) * a.H + P - 1) / P;
-          for (int pj = pj0; pj <= pj1; ++pj) {
-            const int ws = (pj * a.W) / P, we = ((pj + 1) * a.W + P - 1) / P;
-            const float inv = 1.f / (float)((he - hs) * (we - ws));
-            float v[8];
-            ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
-#pragma unroll
-            for (int q = 0; q < 8; ++q) add[q] += v[q] * inv;
+      for (int u = 0; u < U; ++u) {
+        // no branch in the load phase (a conditional load makes the compiler merge registers
+        // behind a wait): pixels past the tile re-load the last pixel, their results are unused
+        const int m = min(mb + u * pl, mend - 1);
+        {
+          const size_t off = (size_t)m * a.C + c0;
+          if constexpr (MODE == EW_CHANNEL_SUM) {
+            in[u][0] = ldraw(A0 + off);
+          } else if constexpr (MODE == EW_BWD_SUM_OUT) {
+            in[u][0] = ldraw(A0 + off); in[u][1] = ldraw(A2 + off);
+          } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
+            in[u][0] = ldraw(A0 + off); in[u][1] = ldraw(A1 + off); in[u][2] = ldraw(A2 + off);
+          } else if constexpr (MODE == EW_BWD_GATE) {
+            in[u][0] = ldraw(A0 + off); in[u][1] = ldraw(A1 + off); in[u][2] = ldraw(A2 + off);
+            in[u][3] = ldraw(A3 + off); in[u][4] = ldraw((const T*)O0 + off); in[u][5] = ldraw((const T*)O1 + off);
+          } else {
+            in[u][0] = ldraw(A0 + off); in[u][1] = ldraw(A1 + off);
           }
+          if constexpr (MODE == EW_BWD_ATTN_ENTRY || MODE == EW_BN_BWD_APPLY_ENTRY) pool_bwd_add(a, m, c0, add[u]);
         }
+      }
+      __builtin_amdgcn_sched_barrier(0);   // keep every load of the batch ahead of its compute
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float z = (!a.act || y[q] * sc[q] + sh[q] > 0.f) ? (d[q] + add[q]) : 0.f;
-          dz[q] = z;
-          acc[0][q] += z;
-          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
-        }
-        store8<T>(O0 + off, dz);
-      } else if constexpr (MODE == EW_BN_BWD_APPLY) {
-        // a0 = dz, a1 = y; gamma, coef [2][C] (hoisted); o0 = dy; sum dy (conv bias grad)
-        float dz[8], y[8], dy[8];
-        load8<T>(A0 + off, dz);
-        load8<T>(A1 + off, y);
+      for (int u = 0; u < U; ++u) {
+        const int m = mb + u * pl;
+        if (m >= mend) break;
+        const size_t off = (size_t)m * a.C + c0;
+        if constexpr (MODE == EW_CHANNEL_SUM) {
+          float x[8];
+          unraw(in[u][0], x);
 #pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          float xh = (y[q] - mu[q]) * is[q];
-          float v = gk[q] * (dz[q] - k0[q] - xh * k1[q]);
-          dy[q] = v;
-          acc[0][q] += v;
+          for (int q = 0; q < 8; ++q) acc[0][q] += x[q];
+        } else if constexpr (MODE == EW_BWD_SUM_OUT) {
+          // a0 = dout, a2 = res; o1 = dres (optional)
+          float d[8], r[8], dr[8];
+          unraw(in[u][0], d);
+          unraw(in[u][1], r);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            dr[q] = scal * d[q];
+            acc[0][q] += d[q] * r[q];
+          }
+          if (st1) store8<T>(O1 + off, dr);
+        } else if constexpr (MODE == EW_BWD_BLOCK_OUT) {
+          // a0 = dout, a1 = y4, a2 = res; o0 = dz4 (optional), o1 = dres
+          float d[8], y[8], r[8], dz[8], dr[8];
+          unraw(in[u][0], d);
+          unraw(in[u][1], y);
+          unraw(in[u][2], r);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
+            dz[q] = z;
+            dr[q] = scal * d[q];
+            acc[0][q] += z;
+            acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+            acc[2][q] += d[q] * r[q];
+          }
+          if (st0) store8<T>(O0 + off, dz);   // without dz4 the apply recomputes it
+          store8<T>(O1 + off, dr);
+        } else if constexpr (MODE == EW_BWD_RELU_BN) {
+          float d[8], y[8], dz[8];
+          unraw(in[u][0], d);
+          unraw(in[u][1], y);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
+            dz[q] = z;
+            acc[0][q] += z;
+            acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+          }
+          if (st0) store8<T>(O0 + off, dz);
+        } else if constexpr (MODE == EW_BWD_GATE) {
+          // a0 = dfused, a1 = y3, a2 = local, a3 = attn; o0 = dlocal(+=), o1 = dattn(+=), o2 = dz3
+          float df[8], y[8], l[8], at[8], dl[8], da[8], dz[8];
+          unraw(in[u][0], df);
+          unraw(in[u][1], y);
+          unraw(in[u][2], l);
+          unraw(in[u][3], at);
+          unraw(in[u][4], dl);
+          unraw(in[u][5], da);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float g = sigm(y[q] * sc[q] + sh[q]);
+            float dg = df[q] * (l[q] - at[q]);
+            float z = dg * g * (1.f - g);
+            dz[q] = z;
+            dl[q] += df[q] * g;
+            da[q] += df[q] * (1.f - g);
+            acc[0][q] += z;
+            acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+          }
+          store8<T>(O0 + off, dl);
+          store8<T>(O1 + off, da);
+          store8<T>(O2 + off, dz);
+        } else if constexpr (MODE == EW_BWD_ATTN_ENTRY) {
+          // a0 = dattn, a1 = y2, tbl = dpooled [B][P][P][C]; o0 = dz2 (optional)
+          float d[8], y[8], dz[8];
+          unraw(in[u][0], d);
+          unraw(in[u][1], y);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float z = (!a.act || y[q] * sc[q] + sh[q] > 0.f) ? (d[q] + add[u][q]) : 0.f;
+            dz[q] = z;
+            acc[0][q] += z;
+            acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+          }
+          if (st0) store8<T>(O0 + off, dz);
+        } else if constexpr (MODE == EW_BN_BWD_APPLY || MODE == EW_BN_BWD_APPLY_RELU ||
+                             MODE == EW_BN_BWD_APPLY_ENTRY) {
+          // a0 = dz (APPLY) / the activation's output gradient (APPLY_RELU: dz = relu'(bn y) * a0;
+          // APPLY_ENTRY: dz = act'(bn y) * (a0 + pool backward of tbl)), a1 = y; gamma, coef [2][C]
+          // (hoisted); o0 = dy; sum dy (conv bias grad).  Recomputing dz costs a few VALU per
+          // element and saves the dz tensor's write + read.
+          float dz[8], y[8], dy[8];
+          unraw(in[u][0], dz);
+          unraw(in[u][1], y);
+          if constexpr (MODE == EW_BN_BWD_APPLY_RELU) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q) dz[q] = (y[q] * sc[q] + sh[q] > 0.f) ? dz[q] : 0.f;
+          } else if constexpr (MODE == EW_BN_BWD_APPLY_ENTRY) {
+#pragma unroll
+            for (int q = 0; q < 8; ++q)
+              dz[q] = (!a.act || y[q] * sc[q] + sh[q] > 0.f) ? (dz[q] + add[u][q]) : 0.f;
+          }
+#pragma unroll
+          for (int q = 0; q < 8; ++q) {
+            float xh = (y[q] - mu[q]) * is[q];
+            float v = gk[q] * (dz[q] - k0[q] - xh * k1[q]);
+            dy[q] = v;
+            acc[0][q] += v;
+          }
+          store8<T>(O0 + off, dy);
         }
-        store8<T>(O0 + off, dy);
       }
     }
   }
@@ -732,7 +910,8 @@ template <int MODE>
 int launch_fwd(int dtype, const EwArgs& a, hipStream_t st) {
   if (a.C % 8 || a.M <= 0 || (int64_t)a.M * (a.C / 8) >= (1ll << 31)) return DFCSA_EINVAL;
   int64_t chunks = (int64_t)a.M * (a.C / 8);
-  int blocks = (int)std::min<int64_t>((chunks + 255) / 256, 256 * 16);
+  // one batch (4 chunks) per thread where the grid allows (the kernel's batched loop)
+  int blocks = (int)std::min<int64_t>((chunks + 1023) / 1024, 65535);
   if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_fwd_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((ew_fwd_kernel<float, MODE>), dim3(blocks), dim3(256), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -948,6 +1127,30 @@ extern "C" int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const
   a.a0 = dz; a.a1 = y; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.coef = coef; a.o0 = dy;
   a.partial = bias_partial;
   return launch_red<EW_BN_BWD_APPLY>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bn_bwd_apply_relu(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
+                                       const float* sh, const float* mean, const float* invstd, const float* gamma,
+                                       const float* coef, void* dy, float* bias_partial, void* stream) {
+  if (!dact || !y || !sc || !sh || !mean || !invstd || !gamma || !coef || !dy) return DFCSA_EINVAL;
+  EwArgs a = zargs(M, C);
+  a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.coef = coef;
+  a.o0 = dy; a.partial = bias_partial;
+  return launch_red<EW_BN_BWD_APPLY_RELU>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, const void* dattn,
+                                        const float* dpooled, int P, const void* y, const float* sc,
+                                        const float* sh, const float* mean, const float* invstd, int relu,
+                                        const float* gamma, const float* coef, void* dy, float* bias_partial,
+                                        void* stream) {
+  if (!dattn || !dpooled || P <= 0 || !y || !sc || !sh || !mean || !invstd || !gamma || !coef || !dy)
+    return DFCSA_EINVAL;
+  EwArgs a = zargs(B * H * W, C);
+  a.B = B; a.H = H; a.W = W; a.P = P;
+  a.a0 = dattn; a.a1 = y; a.tbl = dpooled; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.act = relu;
+  a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial;
+  return launch_red<EW_BN_BWD_APPLY_ENTRY>(dtype, a, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* stream) {

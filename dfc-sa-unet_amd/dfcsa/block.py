@@ -223,15 +223,14 @@ def block_backward(blk, s, dout, need_dx, dtype):
     dout = dout.contiguous()
 
     # ---- block output: relu(bn4 y4) + res_scale * res ----
-    dz4 = torch.empty_like(s.y4)
+    # (dz4 = relu'(bn4 y4) * dout is not materialised: the apply recomputes it)
     dres = torch.empty_like(s.y4)
     part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
     call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean), P(bn4.invstd),
-         P(s.res), P(blk.res_scale), P(dz4), P(dres), P(part), stream())
+         P(s.res), P(blk.res_scale), None, P(dres), P(part), stream())
     coef = ops.bn_bwd_finalize(part, nte, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
                                extra=grad_of(blk.res_scale))
-    dy4 = ops.bn_bwd_apply(dtype, dz4, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
-    del dz4
+    dy4 = ops.bn_bwd_apply_relu(dtype, dout, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
     # fusion conv: dW4 (side stream) and d[fused, local, attn]
     with on_side(dev, dy4, s.fused, s.local, s.attn):
         ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
@@ -264,34 +263,36 @@ def block_backward(blk, s, dout, need_dx, dtype):
     # on the branch stream beside the local branch's bn1 backward (streams.on_branch)
     branch = s.fra is None and ops._SYNC_BN is None
     with on_branch(dev, branch, dattn):
-        dz2 = torch.empty_like(s.y2)
+        # (dz2 is not materialised: the apply recomputes it from the same inputs)
         part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
         if s.fra is not None:
             # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
             da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
             s.fra = None
             call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-                 P(bn2.invstd), P(dz2), P(part2), stream())
+                 P(bn2.invstd), None, P(part2), stream())
+            coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+            dy2 = ops.bn_bwd_apply_relu(dtype, da, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
             del da
         else:
             # ---- LightSelfAttention ----
             dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
             # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
             call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
-                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, P(dz2), P(part2), stream())
-        coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
-        dy2 = ops.bn_bwd_apply(dtype, dz2, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
-        del dz2, part2, coef2
+                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, None, P(part2), stream())
+            coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+            dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
+                                         grad_of(conv2.bias))
+            del dpooled
+        del part2, coef2
     del dattn
 
-    # ---- local branch: relu(bn1 y1) ----
-    dz1 = torch.empty_like(s.y1)
+    # ---- local branch: relu(bn1 y1) (dz1 recomputed by the apply, not materialised) ----
     call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
-         P(dz1), P(part), stream())
-    del dlocal
+         None, P(part), stream())
     coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
-    dy1 = ops.bn_bwd_apply(dtype, dz1, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
-    del dz1
+    dy1 = ops.bn_bwd_apply_relu(dtype, dlocal, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
+    del dlocal
     join_branch(dev, branch, dy2)
 
     # ---- weight gradients of the input-side convs (side stream) ----

@@ -280,6 +280,39 @@ def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
     return dy
 
 
+def bn_bwd_apply_relu(dtype, dact, y, bn, gamma, coef, bias_grad):
+    """bn_bwd_apply with dz = relu'(bn y) * dact recomputed in the kernel (the producing
+    dfcsa_bwd_relu_bn / dfcsa_bwd_block_out call then passes dz = None): no dz tensor."""
+    M, C = dact.numel() // dact.shape[-1], dact.shape[-1]
+    dy = torch.empty_like(dact)
+    part = None
+    if bias_grad is not None and NUMERIC_BN_BIAS_GRAD:
+        nt = ntiles_ew(M, C)
+        part = torch.empty(nt * C, device=dact.device, dtype=torch.float32)
+    call("dfcsa_bn_bwd_apply_relu", dt(dtype), M, C, P(dact), P(y), P(bn.scale), P(bn.shift), P(bn.mean),
+         P(bn.invstd), P(gamma), P(coef), P(dy), P(part), stream())
+    if part is not None:
+        colsum_into(part, nt, C, bias_grad)
+    return dy
+
+
+def bn_bwd_apply_entry(dtype, dattn, dpooled, P_, y, bn, relu, gamma, coef, bias_grad):
+    """bn_bwd_apply for the attention entry with dz = act'(bn y) * (dattn + pool backward of
+    dpooled) recomputed in the kernel (dfcsa_bwd_attn_entry then passes dz = None)."""
+    B, H, W, C = dattn.shape
+    M = B * H * W
+    dy = torch.empty_like(dattn)
+    part = None
+    if bias_grad is not None and NUMERIC_BN_BIAS_GRAD:
+        nt = ntiles_ew(M, C)
+        part = torch.empty(nt * C, device=dattn.device, dtype=torch.float32)
+    call("dfcsa_bn_bwd_apply_entry", dt(dtype), B, H, W, C, P(dattn), P(dpooled), P_, P(y), P(bn.scale),
+         P(bn.shift), P(bn.mean), P(bn.invstd), int(relu), P(gamma), P(coef), P(dy), P(part), stream())
+    if part is not None:
+        colsum_into(part, nt, C, bias_grad)
+    return dy
+
+
 def colsum_into(slab, nt, C, out):
     """out[c] += sum_t slab[t][c]"""
     call("dfcsa_slab_colsum", P(slab), nt, C, P(out), stream())

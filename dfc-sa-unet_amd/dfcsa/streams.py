@@ -19,8 +19,9 @@ _SIDE = {}
 _JOIN_QUEUED = [False]
 import os
 
-# Off by default: measured 979 vs 1044 img/s (B=16 bench) -- the overlapped wgrad GEMMs contend
-# with the dgrad GEMMs for CUs/LDS/L2 more than they fill idle time.  DFCSA_SIDE_STREAM=1 enables.
+# Off by default: the overlapped wgrad GEMMs contend with the dgrad chain for CUs/LDS/L2 about as
+# much as they fill idle time (round 1: 979 vs 1044 img/s; round 2 with the branch stream, same-box
+# A/B: 1245 on vs 1251 off).  DFCSA_SIDE_STREAM=1 enables.
 ENABLED = [os.environ.get("DFCSA_SIDE_STREAM", "0") == "1"]
 
 

@@ -232,6 +232,20 @@ int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int
 int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
                        const float* invstd, const float* gamma, const float* coef, void* dy,
                        float* bias_partial, void* stream);
+/* dfcsa_bn_bwd_apply with dz recomputed from the activation's output gradient instead of read
+ * from a dz tensor (the producing stage -- dfcsa_bwd_relu_bn / dfcsa_bwd_block_out with dz = NULL
+ * -- then only emits its partial sums): dz = (y*sc + sh > 0) ? dact : 0.  Replaces the BN/ReLU
+ * backward of reference models/unet_dfc_sa_res.py:57-62, :65-69, :80-84 (autograd). */
+int dfcsa_bn_bwd_apply_relu(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
+                            const float* sh, const float* mean, const float* invstd, const float* gamma,
+                            const float* coef, void* dy, float* bias_partial, void* stream);
+/* the same for the attention entry a = relu(bn2 y2) (reference :65-69 + the adaptive-avg-pool of
+ * :24 and the residual of :38): dz = act'(bn y) * (dattn + pool_backward(dpooled)); pairs with
+ * dfcsa_bwd_attn_entry(dz2 = NULL). */
+int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled, int P,
+                             const void* y, const float* sc, const float* sh, const float* mean,
+                             const float* invstd, int relu, const float* gamma, const float* coef, void* dy,
+                             float* bias_partial, void* stream);
 /* Two-stage reduction helper for per-tile slabs: dst[g][j] = sum of rows t in group g of
  * src[t][j] (T rows of rowlen floats, G groups of ceil(T/G) consecutive rows).  The finalize
  * entry points then reduce G rows instead of T.  dst: [G][rowlen] fp32 (caller scratch). */
