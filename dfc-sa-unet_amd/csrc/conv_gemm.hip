@@ -24,6 +24,7 @@
 
 #include "common.h"
 #include "dfcsa_internal.h"
+#include "small_gemm.h"
 
 namespace {
 
@@ -704,6 +705,26 @@ int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
   return 0;
 }
 
+// fp32 GEMMs with few rows (the LightSelfAttention q/k/v projections and their dgrad, M = B*P*P):
+// split-reduction 16x64 tiles (small_gemm.h), plain 1x1 store with bias and column split
+__global__ void __launch_bounds__(256) small_conv_f32_kernel(const ConvGemmArgs args) {
+  __shared__ float lds[4 * 16 * 64];
+  const float* A = (const float*)args.seg[0].ptr;
+  const float* Bw = (const float*)args.Bw;
+  small_gemm_tile<false>(A, args.Cseg, Bw, args.Kpad, args.M, args.N, args.K, blockIdx.x * 16, blockIdx.y * 64, lds,
+                         [&](int m, int n, float v) {
+                           if (args.bias) v += args.bias[n];
+                           const int d = n / args.Nd, col = n - d * args.Nd;
+                           ((float*)args.dest[d])[(size_t)m * args.Nd + col] = v;
+                         });
+}
+
+bool small_conv_applies(const ConvGemmArgs& a) {
+  return a.M <= 4096 && a.nseg == 1 && a.seg[0].dh == 0 && a.seg[0].dw == 0 && a.stride == 1 &&
+         a.mode == CONV_STORE_PLAIN && !a.stats && !a.accumulate && a.Ho == a.Hi && a.Wo == a.Wi &&
+         a.Cseg % 4 == 0 && a.K % 4 == 0;
+}
+
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
@@ -1062,8 +1083,13 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     }
     return launch_glds<128, 128, 4, 2, 2>(a, st);
   }
-  // fp32 (parity mode + the fp32 LightSelfAttention projections): small problems (M = B*P*P
-  // rows) get 64x64 tiles so that enough workgroups run
+  // fp32 (parity mode + the fp32 LightSelfAttention projections): few rows (M = B*P*P) -> the
+  // split-reduction small-M kernel; other small problems get 64x64 tiles
+  if (g_conv_cfg != 26 && small_conv_applies(a)) {
+    hipLaunchKernelGGL(small_conv_f32_kernel, dim3((a.M + 15) / 16, (a.N + 63) / 64), dim3(256), 0, st, a);
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
   const int t128 = ((a.M + 127) / 128) * ((a.N + 127) / 128);
   if (t128 < 128) return launch_cfg<T, 64, 64, 2, 2>(a, st);
   if (a.N <= 64) return launch_cfg<T, 128, 64, 4, 1>(a, st);
@@ -1122,6 +1148,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 12) { g_wgrad_fuse_all = value; return 0; }
   if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
   if (knob == 15) { g_conv_dbg = value; return 0; }
+  if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 14) { g_wgrad_nst = (value >= 2 && value <= 4) ? value : 2; return 0; }
   return DFCSA_EINVAL;
 }

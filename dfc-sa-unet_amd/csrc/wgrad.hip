@@ -20,6 +20,7 @@
 // models/unet_dfc_sa_res.py:58, 66, 74, 81, 88 and ConvTranspose2d at :147-156.
 #include "common.h"
 #include "dfcsa_internal.h"
+#include "small_gemm.h"
 
 namespace {
 
@@ -514,6 +515,18 @@ __device__ __forceinline__ void reduce_dst_add(int64_t e, int NI, int NJ, int la
   }
 }
 
+// fp32 weight gradient over few pixel rows (the LightSelfAttention projections, M = B*P*P): the
+// whole reduction in one launch (split over the 4 waves of a 16x64 tile, small_gemm.h), added
+// straight into the destination layout -- no split-K slab, no reduce launch
+__global__ void __launch_bounds__(256) small_wgrad_f32_kernel(const WgradArgs a) {
+  __shared__ float lds[4 * 16 * 64];
+  small_gemm_tile<true>((const float*)a.g_ptr[0], a.NI, (const float*)a.seg[0].ptr, a.Cseg, a.NI, a.NJ, a.M,
+                        blockIdx.x * 16, blockIdx.y * 64, lds, [&](int i, int j, float v) {
+                          reduce_dst_add((int64_t)i * a.NJ + j, a.NI, a.NJ, a.layout, a.ntaps, a.Ctot, a.Creal,
+                                         a.ndst, a.dst[0], a.dst[1], a.dst[2], v);
+                        });
+}
+
 template <int SUB>
 __global__ void __launch_bounds__(64 * SUB) wgrad_reduce_kernel(const float* __restrict__ slab, int splits, int NI,
                                                                 int NJ, int layout, int ntaps, int Ctot, int Creal,
@@ -615,6 +628,7 @@ int g_wgrad_fuse_all = 0;  // knob 12: 1 = reduce in-kernel at any split count, 
 // than the separate fixed-order reduction launch (W4 H14: 114 vs 72 us; step 1172 vs 1198 img/s at
 // <= 4 splits, 1149 at <= 16), so the fused path stays selectable, tested, and off.
 int g_wgrad_fuse_max = 0;
+int g_wgrad_noglds_f32small = 0;  // knob 16: 1 = fp32 small-M wgrads take the generic tiles
 
 // output tile of the wgrad kernel a launch uses (launch_wgrad's choice)
 void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
@@ -702,6 +716,12 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   double flops = 2.0 * a.M * a.NI * a.NJ;
   ProfScope prof(DFCSA_PROF_WGRAD, st, flops);   // the class covers the reduction launch too
+  if (d->dtype != DFCSA_DT_BF16 && a.M <= 4096 && a.ng == 1 && a.nseg == 1 && !a.seg[0].dh && !a.seg[0].dw &&
+      a.stride == 1 && d->ndst > 0 && a.Ho == a.Hi && a.Wo == a.Wi && !g_wgrad_noglds_f32small) {
+    hipLaunchKernelGGL(small_wgrad_f32_kernel, dim3((a.NI + 15) / 16, (a.NJ + 63) / 64), dim3(256), 0, st, a);
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
   int rc;
   if (d->dtype == DFCSA_DT_BF16)
     rc = a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st) : launch_wgrad<bf16_t, 128>(a, d->splits, st);
