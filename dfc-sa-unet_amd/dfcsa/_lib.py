@@ -119,6 +119,11 @@ def _load():
 
 LIB, PROTOS = _load()
 
+# DFCSA_TUNE="knob=value,..." applies dfcsa_set_tuning knobs at load time (A/B experiments)
+for _kv in filter(None, os.environ.get("DFCSA_TUNE", "").split(",")):
+    _k, _v = _kv.split("=")
+    LIB.dfcsa_set_tuning(int(_k), int(_v))
+
 
 def call(name, *args):
     """Invoke an entry point; raise DfcsaError on a non-zero status."""
