@@ -573,6 +573,18 @@ int launch_reduce(const float* slab, int splits, int NI, int NJ, int layout, int
   return 0;
 }
 
+// big output tiles (knob 17) for the deep layers: one 512-thread workgroup per CU stages
+// (BI + BJ) x 64 pixels per K stage for BI*BJ*64 MACs, so a 256x256 tile needs half the
+// L2->LDS bytes per flop of a 128x128 one (the per-CU L2 fetch rate, ~70 GB/s, not the MFMA,
+// bounds the 128x128 tile at ~0.46 of peak).  1: 256x256 (NI >= 256), 2: 256x128 (NI >= 256),
+// 3: 128x256 (NI >= 128, NJ >= 256)
+__host__ __device__ inline int wgrad_big_mode(int NI, int NJ, int big) {
+  if (big == 1 && NI >= 256 && NJ >= 256) return 1;
+  if (big == 2 && NI >= 256) return 2;
+  if (big == 3 && NI >= 128 && NJ >= 256) return 3;
+  return 0;
+}
+
 // 64-row (NI <= 64) bf16 tiles take 256 columns when NJ is wide (4 x 2 wave layout of 32x64
 // tiles instead of 16x64: half the LDS fragment reads per MFMA)
 bool wide_j(const WgradArgs& a) { return a.NI <= 64 && a.NJ >= 512 && !g_wgrad_narrow; }
@@ -586,6 +598,15 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   const int waves = g_wgrad_waves ? g_wgrad_waves : 8;
   if constexpr (sizeof(T) == 2) {
     if (!g_wgrad_noglds) {
+      if (const int bm = wgrad_big_mode(a.NI, a.NJ, g_wgrad_big)) {
+        const int bi = bm == 3 ? 128 : 256, bj = bm == 2 ? 128 : 256;
+        dim3 gb(xcd_pad(((a.NJ + bj - 1) / bj) * ((a.NI + bi - 1) / bi) * splits));
+        if (bm == 1) hipLaunchKernelGGL((wgrad_glds_kernel<256, 256, 2, 4, 2>), gb, dim3(512), 0, st, a, splits);
+        else if (bm == 2) hipLaunchKernelGGL((wgrad_glds_kernel<256, 128, 4, 2, 2>), gb, dim3(512), 0, st, a, splits);
+        else hipLaunchKernelGGL((wgrad_glds_kernel<128, 256, 2, 4, 2>), gb, dim3(512), 0, st, a, splits);
+        DFCSA_CHECK_LAUNCH();
+        return 0;
+      }
       // 1-D grid (x = padded tile count, y = splits count carrier): see the XCD remap in the kernel
       if (BI == 64 && wide_j(a)) {
         dim3 g2(xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits), splits);
@@ -631,7 +652,15 @@ int g_wgrad_fuse_max = 0;
 int g_wgrad_noglds_f32small = 0;  // knob 16: 1 = fp32 small-M wgrads take the generic tiles
 
 // output tile of the wgrad kernel a launch uses (launch_wgrad's choice)
+int g_wgrad_big = 0;        // knob 17: big wgrad tiles (wgrad_big_mode)
 void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
+  if (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds) {
+    if (const int bm = wgrad_big_mode(NI, NJ, g_wgrad_big)) {
+      *BI = bm == 3 ? 128 : 256;
+      *BJ = bm == 2 ? 128 : 256;
+      return;
+    }
+  }
   *BI = NI <= 64 ? 64 : 128;
   *BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 && NJ >= 512 && !g_wgrad_narrow) ? 256 : 128;
 }

@@ -167,6 +167,38 @@ def test_wgrad_3x3(dtype, tol, B, Cs, nsrc, C, H, W, variant):
     assert rel(gw, w.grad) < tol
 
 
+@pytest.mark.parametrize("mode", [1, 2, 3])
+@pytest.mark.parametrize("B,Cs,C,H,W,fuse", [(2, 256, 256, 14, 14, 0), (2, 128, 512, 12, 10, 16), (3, 64, 264, 9, 11, 0),
+                                             (1, 64, 128, 8, 8, 16)])
+def test_wgrad_big_tiles(mode, B, Cs, C, H, W, fuse):
+    """bf16 weight gradient on the big output tiles (tuning knob 17: 256x256, 256x128, 128x256; one
+    512-thread workgroup per CU) against torch fp32 on bf16-exact operands: full and ragged tiles
+    (C = 264), the slab reduction and the in-kernel split reduction (knob 13), bitwise repeatable."""
+    import dfcsa
+    torch.manual_seed(6)
+    dtype = torch.bfloat16
+    x = q(torch.randn(B, Cs, H, W), dtype)
+    g = q(torch.randn(B, C, H, W), dtype)
+    w = torch.zeros(C, Cs, 3, 3, requires_grad=True)
+    F.conv2d(x, w, padding=1).backward(g)
+    xh, gh = nhwc(x, dtype), nhwc(g, dtype)
+    segs = [(xh, kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+    outs = []
+    dfcsa.set_tuning(17, mode)
+    dfcsa.set_tuning(13, fuse)
+    try:
+        for _ in range(2):
+            gw = torch.zeros(C, Cs, 3, 3, device="cuda")
+            ops.conv_wgrad_into(dtype, [gh], C, segs, Cs, (B, H, W), (H, W), [gw], 9, Cs, Cs)
+            outs.append(gw)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(17, 0)
+        dfcsa.set_tuning(13, 0)
+    assert rel(outs[0], w.grad) < 1e-5, rel(outs[0], w.grad)
+    assert torch.equal(outs[0], outs[1])
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 def test_dgrad_3x3_plus_1x1(dtype, tol):
     """the fused input-gradient GEMM: 3x3 dgrad + two 1x1 dgrads into two destination sources"""

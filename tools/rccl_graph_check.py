@@ -17,16 +17,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dfc-sa-unet_amd")]
 
 
 def main():
-    os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-    if "MASTER_PORT" not in os.environ:
-        import socket
-        sk = socket.socket()
-        sk.bind(("127.0.0.1", 0))
-        os.environ["MASTER_PORT"] = str(sk.getsockname()[1])
-        sk.close()
     dev = torch.device("cuda:0")
     torch.cuda.set_device(dev)
-    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    # world size 1: an in-process store (no TCP rendezvous, no port to race for)
+    dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
     from dfcsa.ddp import GradBucketReducer
     from dfcsa.loss import bce_dice, sigmoid
     from dfcsa.optim import FusedSGD
