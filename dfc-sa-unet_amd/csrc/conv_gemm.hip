@@ -21,6 +21,7 @@
 // mode; exact f32 FMA chain).
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 
 #include "common.h"
 #include "dfcsa_internal.h"
@@ -947,6 +948,205 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   }
 }
 
+// --------------------------------------------------------------------------------------------
+// Fusion-conv input gradient with the gate backward in its epilogue (dfcsa_dgrad_gate):
+//   [dfused | dlocal | dattn] = dy4 . W4t, each bf16-rounded as the unfused GEMM stores them;
+//   g = sigmoid(bn3 y3); dlocal += dfused*g; dattn += dfused*(1-g); dz3 = dfused*(local-attn)*g*(1-g)
+// plus the BN3-backward sums (sum dz3, sum dz3*xhat3), one partial row per workgroup.  Workgroup
+// column block cb owns channels cb*64 .. +63 of all three column blocks (192 GEMM columns =
+// weight rows part*C + cb*64 + ch), so dfused stays on chip: the GEMM's 3 writes + the gate
+// pass's 6 reads and 3 writes become 3 reads + 3 writes.  Streaming structure of
+// conv1x1_stream_kernel (weights in registers, 64-row tiles walked grid-stride, next A image by
+// LDS-DMA behind the current tile); the gate inputs of a tile are fetched ahead of its wait.
+// Reference: models/unet_dfc_sa_res.py:102-110 (gate, fused, fusion_conv) backward.
+// --------------------------------------------------------------------------------------------
+struct GateEpi {
+  const bf16_t* y3;
+  const bf16_t* local;
+  const bf16_t* attn;
+  const float* sc;
+  const float* sh;
+  const float* mean;
+  const float* invstd;
+  bf16_t* dlocal;
+  bf16_t* dattn;
+  bf16_t* dz3;
+  float* part;
+};
+
+__device__ __forceinline__ float gate_sigm(float x) { return 1.f / (1.f + __expf(-x)); }  // = block_ew sigm
+
+template <int KP>
+__global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles) {
+  using T = bf16_t;
+  constexpr int NWC = 48, FN = 3, NWG = 192;
+  constexpr int KS = KP / 64, KG = KP / 32;
+  constexpr int IMG = 64 * 128, SLOT = KS * IMG;
+  constexpr int OSTR = NWG * 2 + 16;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
+  __shared__ float red[4][2][64];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = args.M, C = args.Nd, K = args.K;
+  const int cb = blockIdx.y;
+  const int rsub = lane >> 3;
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+
+  // B fragments: local column lc = wave*48 + j*16 (+ lane&15) -> weight row (lc/64)*C + cb*64 + lc%64
+  bf16x8_t bfr[FN][KG];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int lc = wave * NWC + j * 16;
+    const int n = (lc >> 6) * C + cb * 64 + (lc & 63) + (lane & 15);
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      const int k = g * 32 + 8 * (lane >> 4);
+      if (k < args.Kpad) bfr[j][g] = *(const bf16x8_t*)((const T*)args.Bw + (size_t)n * args.Kpad + k);
+      else bfr[j][g] = bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
+    }
+  }
+  const void* zero = (const void*)g_zero_page;
+  const T* a_src[2 * KS];
+#pragma unroll
+  for (int i = 0; i < 2 * KS; ++i) {
+    const int k = (i >> 1) * 64 + cchunk * 8;
+    a_src[i] = k < K ? (const T*)args.seg[0].ptr + k : nullptr;
+  }
+  auto issue = [&](int t, int slot) {
+    char* base = smem + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int st = i >> 1, rb = (i & 1) * 4 + wave;
+      const int m = t * 64 + rb * 8 + rsub;
+      const void* src = (m < M && a_src[i]) ? (const void*)(a_src[i] + (size_t)m * K) : zero;
+      glds16(src, base + st * IMG + rb * 8 * 128);
+    }
+  };
+
+  // epilogue items: channel chunk ck (8 channels), rows rr and rr + 32 of each tile
+  const int ck = tid & 7, rr = tid >> 3;
+  const int c0 = cb * 64 + ck * 8;
+  float sc[8], sh[8], mu[8], is[8];
+  load8<float>(e.sc + c0, sc);
+  load8<float>(e.sh + c0, sh);
+  load8<float>(e.mean + c0, mu);
+  load8<float>(e.invstd + c0, is);
+  float s0[8], s1[8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) { s0[q] = 0.f; s1[q] = 0.f; }
+
+  int t = blockIdx.x;
+  if (t < mtiles) issue(t, 0);
+  int slot = 0;
+  for (; t < mtiles; t += gridDim.x, slot ^= 1) {
+    const int tn = t + gridDim.x;
+    uint4 pin[2][3];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int m = min(t * 64 + rr + 32 * h, M - 1);
+      const size_t off = (size_t)m * C + c0;
+      pin[h][0] = *(const uint4*)(e.y3 + off);
+      pin[h][1] = *(const uint4*)(e.local + off);
+      pin[h][2] = *(const uint4*)(e.attn + off);
+    }
+    if (tn < mtiles) {
+      issue(tn, slot ^ 1);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    const char* img = smem + slot * SLOT;
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      Frag<T> fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) read_frag<T>(img + (g >> 1) * IMG, i * 16 + (lane & 15), g & 1, lane, fa[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wave * NWC + j * 16 + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *(T*)(otile + (i * 16 + (lane >> 4) * 4 + r) * OSTR + col * 2) = f2bf(acc[i][j][r]);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = rr + 32 * h, m = t * 64 + row;
+      if (m >= M) continue;
+      float df[8], dl[8], da[8], y[8], l[8], at[8], dz[8];
+      load8<T>((const T*)(otile + row * OSTR + ck * 16), df);
+      load8<T>((const T*)(otile + row * OSTR + 128 + ck * 16), dl);
+      load8<T>((const T*)(otile + row * OSTR + 256 + ck * 16), da);
+      load8<T>((const T*)&pin[h][0], y);
+      load8<T>((const T*)&pin[h][1], l);
+      load8<T>((const T*)&pin[h][2], at);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float g = gate_sigm(y[q] * sc[q] + sh[q]);
+        const float dg = df[q] * (l[q] - at[q]);
+        const float z = dg * g * (1.f - g);
+        dz[q] = z;
+        dl[q] += df[q] * g;
+        da[q] += df[q] * (1.f - g);
+        s0[q] += z;
+        s1[q] += z * ((y[q] - mu[q]) * is[q]);
+      }
+      const size_t off = (size_t)m * C + c0;
+      store8<T>(e.dlocal + off, dl);
+      store8<T>(e.dattn + off, da);
+      store8<T>(e.dz3 + off, dz);
+    }
+  }
+  // per-workgroup sums: the 8 row lanes of a wave (butterfly), then the 4 waves in order
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    float a0 = s0[q], a1 = s1[q];
+    for (int o = 8; o < 64; o <<= 1) { a0 += __shfl_xor(a0, o, 64); a1 += __shfl_xor(a1, o, 64); }
+    s0[q] = a0;
+    s1[q] = a1;
+  }
+  if (lane < 8)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { red[wave][0][lane * 8 + q] = s0[q]; red[wave][1][lane * 8 + q] = s1[q]; }
+  __syncthreads();
+  if (tid < 128) {
+    const int s = tid >> 6, c = tid & 63;
+    e.part[(size_t)blockIdx.x * 2 * C + s * C + cb * 64 + c] =
+        (red[0][s][c] + red[1][s][c]) + (red[2][s][c] + red[3][s][c]);
+  }
+}
+
+template <int KP>
+int gate_occ() {
+  static int occ = 0;
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP>, 256, 0) != hipSuccess || occ < 1))
+    occ = 1;
+  return occ;
+}
+
+// workgroups of one dfcsa_dgrad_gate launch (= partial rows): every CU's resident slots, at most one per tile
+int dgrad_gate_grid(int M, int C) {
+  const int kp = (C + 63) / 64 * 64;
+  const int occ = kp == 64 ? gate_occ<64>() : kp == 128 ? gate_occ<128>() : kp == 192 ? gate_occ<192>() : gate_occ<256>();
+  const int mtiles = (M + 63) / 64;
+  int gx = 256 * occ;
+  return gx > mtiles ? mtiles : gx;
+}
+
 int g_stream_wgs = 0;   // workgroups per CU of the streaming kernel (0 = occupancy limit)
 int g_debug = -1;
 int g_stream_force = 0;  // knob 5: take the streaming kernel whenever it applies (tests)
@@ -1129,6 +1329,40 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   ProfScope prof(streamed ? DFCSA_PROF_CONV_STREAM : DFCSA_PROF_CONV_GEMM, st,
                  streamed ? sbytes : 2.0 * a.M * a.N * a.K);
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
+}
+
+extern "C" int dfcsa_dgrad_gate_parts(int M, int C) {
+  if (M <= 0 || C <= 0) return DFCSA_EINVAL;
+  return dgrad_gate_grid(M, C);
+}
+
+extern "C" int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, const void* y3,
+                                const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
+                                const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
+                                float* partial, void* stream) {
+  if (M <= 0 || C <= 0 || C % 64 || C > 256 || Kpad != (C + 63) / 64 * 64) return DFCSA_EINVAL;
+  if (!dy4 || !w4t || !y3 || !sc3 || !sh3 || !mean3 || !invstd3 || !local || !attn || !dlocal || !dattn || !dz3 ||
+      !partial)
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M; a.N = 3 * C; a.K = C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 1; a.Nd = C;
+  a.seg[0].ptr = dy4;
+  a.Bw = w4t;
+  GateEpi e;
+  e.y3 = (const bf16_t*)y3; e.local = (const bf16_t*)local; e.attn = (const bf16_t*)attn;
+  e.sc = sc3; e.sh = sh3; e.mean = mean3; e.invstd = invstd3;
+  e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.dz3 = (bf16_t*)dz3; e.part = partial;
+  const int mtiles = (M + 63) / 64;
+  dim3 grid(dgrad_gate_grid(M, C), C / 64);
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + 3.0 * C * Kpad + 6.0 * (double)M * C));
+  if (Kpad == 64) hipLaunchKernelGGL(dgrad_gate_kernel<64>, grid, dim3(256), 0, st, a, e, mtiles);
+  else if (Kpad == 128) hipLaunchKernelGGL(dgrad_gate_kernel<128>, grid, dim3(256), 0, st, a, e, mtiles);
+  else if (Kpad == 192) hipLaunchKernelGGL(dgrad_gate_kernel<192>, grid, dim3(256), 0, st, a, e, mtiles);
+  else hipLaunchKernelGGL(dgrad_gate_kernel<256>, grid, dim3(256), 0, st, a, e, mtiles);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

@@ -19,15 +19,21 @@ Activation flow per block (NHWC, dtype T; M = B*H*W pixels; C = out channels):
   GEMM 1x1            [fused, local, attn] -> y4 (+bias, BN4 stats)
   EW                  out = relu(bn4 y4) + res_scale * res
 """
+import os
+
 import torch
 import torch.nn as nn
 
-from . import fra, ops
+from . import _lib, fra, ops
 from ._lib import call
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
 from .streams import join_branch, on_branch, on_side
+
+# bf16 blocks with C % 64 == 0, C <= 256: the fusion conv's input-gradient GEMM carries the gate
+# backward in its epilogue (dfcsa_dgrad_gate); DFCSA_DGRAD_GATE=0 selects the GEMM + dfcsa_bwd_gate pair
+FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
 
 
 def grad_of(p):
@@ -237,19 +243,28 @@ def block_backward(blk, s, dout, need_dx, dtype):
                             [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
-    dfused = torch.empty_like(s.y4)
     dlocal = torch.empty_like(s.y4)
     dattn = torch.empty_like(s.y4)
-    ops.conv_gemm(dtype, [(dy4, 0, 0)], C, grid, hw, W4t, KpC, 3 * C, [dfused, dlocal, dattn], C)
-    del dy4
-
-    # ---- gate: s = sigmoid(bn3 y3); fused = s*local + (1-s)*attn ----
     dz3 = torch.empty_like(s.y3)
-    part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
-    call("dfcsa_bwd_gate", T, M, C, P(dfused), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean), P(bn3.invstd),
-         P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
-    del dfused
-    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
+    # ---- gate: s = sigmoid(bn3 y3); fused = s*local + (1-s)*attn ----
+    if dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]:
+        # the gate backward runs in the epilogue of the fusion conv's input-gradient GEMM
+        # (dfused never stored; dfcsa_dgrad_gate)
+        npart = _lib.LIB.dfcsa_dgrad_gate_parts(M, C)
+        part = torch.empty(npart * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_dgrad_gate", M, C, P(dy4), P(W4t), KpC, P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+        del dy4
+    else:
+        npart = nte
+        dfused = torch.empty_like(s.y4)
+        ops.conv_gemm(dtype, [(dy4, 0, 0)], C, grid, hw, W4t, KpC, 3 * C, [dfused, dlocal, dattn], C)
+        del dy4
+        part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_bwd_gate", T, M, C, P(dfused), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+        del dfused
+    coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
     dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
     del dz3
     with on_side(dev, dy3):
@@ -288,6 +303,7 @@ def block_backward(blk, s, dout, need_dx, dtype):
     del dattn
 
     # ---- local branch: relu(bn1 y1) (dz1 recomputed by the apply, not materialised) ----
+    part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
     call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
          None, P(part), stream())
     coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))

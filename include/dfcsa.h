@@ -217,6 +217,18 @@ int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, 
                    const float* sh3, const float* mean3, const float* invstd3, const void* local,
                    const void* attn, void* dlocal, void* dattn, void* dz3, float* partial,
                    void* stream);
+/* fusion-conv input gradient with the gate backward in the epilogue (bf16, C % 64 == 0,
+ * C <= 256): [dfused | dlocal | dattn] = dy4 . W4t (W4t = dfcsa_conv_gemm's [3C][Kpad] dgrad
+ * operand of the fusion conv), each rounded to bf16 as the unfused GEMM stores them, then
+ * dfcsa_bwd_gate's arithmetic on them: dlocal/dattn written (not accumulated), dz3 written,
+ * dfused never stored.  Sums [sum dz3, sum dz3*xh3] per workgroup row: partial
+ * [dfcsa_dgrad_gate_parts(M, C)][2][C].  Replaces the dgrad GEMM + dfcsa_bwd_gate pair
+ * (reference models/unet_dfc_sa_res.py:102-110 backward). */
+int dfcsa_dgrad_gate_parts(int M, int C);
+int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, const void* y3,
+                     const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
+                     const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
+                     float* partial, void* stream);
 /* attention entry: dz2 = (dattn + adaptive_pool^T(dpooled)) * (y2*sc2+sh2 > 0) (mask only when
  * relu != 0); dpooled fp32 [B][P][P][C]; sums [sum dz2, sum dz2*xh2] */
 int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled,

@@ -485,3 +485,43 @@ def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats, force):
         a = ref - (b.view(1, -1, 1, 1) if bias else 0)
         assert rel(s[0], a.sum((0, 2, 3))) < 1e-3
         assert rel(s[1], (a * a).sum((0, 2, 3))) < 1e-3
+
+
+@pytest.mark.parametrize("M,C", [(65536 + 37, 64), (4 * 28 * 28, 128), (2 * 56 * 56 + 5, 256), (300, 64),
+                                 (16 * 224 * 224, 64), (16 * 112 * 112, 128), (16 * 56 * 56, 256)])
+def test_dgrad_gate_fused_equals_gemm_plus_gate(M, C):
+    """dfcsa_dgrad_gate (fusion-conv input gradient with the gate backward in its epilogue) against
+    the unfused pair it replaces (dfcsa_conv_gemm -> [dfused, dlocal, dattn], then
+    dfcsa_bwd_gate): dlocal, dattn and dz3 bit-identical (same MFMA order, same bf16 roundings),
+    the BN3-backward sums equal to fp32 summation-order noise; ragged M (M % 64 != 0)."""
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P, stream
+    torch.manual_seed(11)
+    bf = torch.bfloat16
+    dev = "cuda"
+    Kp = ops.rup(C, ops.KALIGN)
+    dy4 = torch.randn(M, C, device=dev).to(bf)
+    w4t = (torch.randn(3 * C, Kp, device=dev) * 0.1).to(bf)
+    y3, loc, att = (torch.randn(M, C, device=dev).to(bf) for _ in range(3))
+    sc, sh, mu = (torch.randn(C, device=dev) for _ in range(3))
+    istd = torch.rand(C, device=dev) + 0.5
+    # unfused reference path
+    dfu, dl0, da0, dz0 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(4))
+    ops.conv_gemm(bf, [(dy4.view(1, M, 1, C), 0, 0)], C, (1, M, 1), (M, 1), w4t, Kp, 3 * C,
+                  [dfu.view(1, M, 1, C), dl0.view(1, M, 1, C), da0.view(1, M, 1, C)], C)
+    nte = ops.ntiles_ew(M, C)
+    part0 = torch.empty(nte * 2 * C, device=dev)
+    call("dfcsa_bwd_gate", ops.dt(bf), M, C, P(dfu), P(y3), P(sc), P(sh), P(mu), P(istd), P(loc), P(att), P(dl0),
+         P(da0), P(dz0), P(part0), stream())
+    # fused
+    npart = LIB.dfcsa_dgrad_gate_parts(M, C)
+    assert 1 <= npart <= (M + 63) // 64
+    dl1, da1, dz1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
+    part1 = torch.empty(npart * 2 * C, device=dev)
+    call("dfcsa_dgrad_gate", M, C, P(dy4), P(w4t), Kp, P(y3), P(sc), P(sh), P(mu), P(istd), P(loc), P(att), P(dl1),
+         P(da1), P(dz1), P(part1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dl1, dl0) and torch.equal(da1, da0) and torch.equal(dz1, dz0)
+    s0 = part0.view(nte, 2, C).double().sum(0)
+    s1 = part1.view(npart, 2, C).double().sum(0)
+    assert rel(s1, s0) < 1e-5
