@@ -976,10 +976,17 @@ struct GateEpi {
 
 __device__ __forceinline__ float gate_sigm(float x) { return 1.f / (1.f + __expf(-x)); }  // = block_ew sigm
 
-template <int KP>
+// EPI_GATE: the gate backward above (192 columns: dfused | dlocal | dattn of channel block cb).
+// EPI_ACC_RELU_BN (dfcsa_dgrad_acc_relu_bn): the gate conv's input gradient dy3 . W3t ADDED into
+// [dlocal | dattn] (128 columns per workgroup; the same bf16 rounding as the accumulate-mode GEMM)
+// and, on the final dlocal, the BN1-backward sums of dz1 = dlocal * (y1*sc1 + sh1 > 0) (the sums
+// of dfcsa_bwd_relu_bn, whose read of dlocal and y1 it replaces by one read of y1).
+enum { EPI_GATE = 0, EPI_ACC_RELU_BN = 1 };
+
+template <int KP, int EPI>
 __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles) {
   using T = bf16_t;
-  constexpr int NWC = 48, FN = 3, NWG = 192;
+  constexpr int NWC = EPI == EPI_GATE ? 48 : 32, FN = NWC / 16, NWG = 4 * NWC;
   constexpr int KS = KP / 64, KG = KP / 32;
   constexpr int IMG = 64 * 128, SLOT = KS * IMG;
   constexpr int OSTR = NWG * 2 + 16;
@@ -1046,9 +1053,14 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
     for (int h = 0; h < 2; ++h) {
       const int m = min(t * 64 + rr + 32 * h, M - 1);
       const size_t off = (size_t)m * C + c0;
-      pin[h][0] = *(const uint4*)(e.y3 + off);
-      pin[h][1] = *(const uint4*)(e.local + off);
-      pin[h][2] = *(const uint4*)(e.attn + off);
+      pin[h][0] = *(const uint4*)(e.y3 + off);   // y3 (gate) / y1 (acc)
+      if constexpr (EPI == EPI_GATE) {
+        pin[h][1] = *(const uint4*)(e.local + off);
+        pin[h][2] = *(const uint4*)(e.attn + off);
+      } else {   // the destination values the GEMM adds to
+        pin[h][1] = *(const uint4*)(e.dlocal + off);
+        pin[h][2] = *(const uint4*)(e.dattn + off);
+      }
     }
     if (tn < mtiles) {
       issue(tn, slot ^ 1);
@@ -1087,6 +1099,26 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
     for (int h = 0; h < 2; ++h) {
       const int row = rr + 32 * h, m = t * 64 + row;
       if (m >= M) continue;
+      const size_t off = (size_t)m * C + c0;
+      if constexpr (EPI == EPI_ACC_RELU_BN) {
+        float gl[8], ga[8], ol[8], oa[8], y[8];
+        load8<T>((const T*)(otile + row * OSTR + ck * 16), gl);
+        load8<T>((const T*)(otile + row * OSTR + 128 + ck * 16), ga);
+        load8<T>((const T*)&pin[h][0], y);
+        load8<T>((const T*)&pin[h][1], ol);
+        load8<T>((const T*)&pin[h][2], oa);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          gl[q] = bf2f(f2bf(gl[q] + ol[q]));   // the value stored (and read back by the unfused pass)
+          ga[q] += oa[q];
+          const float z = (y[q] * sc[q] + sh[q] > 0.f) ? gl[q] : 0.f;
+          s0[q] += z;
+          s1[q] += z * ((y[q] - mu[q]) * is[q]);
+        }
+        store8<T>(e.dlocal + off, gl);
+        store8<T>(e.dattn + off, ga);
+        continue;
+      }
       float df[8], dl[8], da[8], y[8], l[8], at[8], dz[8];
       load8<T>((const T*)(otile + row * OSTR + ck * 16), df);
       load8<T>((const T*)(otile + row * OSTR + 128 + ck * 16), dl);
@@ -1105,7 +1137,6 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
         s0[q] += z;
         s1[q] += z * ((y[q] - mu[q]) * is[q]);
       }
-      const size_t off = (size_t)m * C + c0;
       store8<T>(e.dlocal + off, dl);
       store8<T>(e.dattn + off, da);
       store8<T>(e.dz3 + off, dz);
@@ -1130,18 +1161,22 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
   }
 }
 
-template <int KP>
+template <int KP, int EPI>
 int gate_occ() {
   static int occ = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP>, 256, 0) != hipSuccess || occ < 1))
+  if (!occ &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP, EPI>, 256, 0) != hipSuccess || occ < 1))
     occ = 1;
   return occ;
 }
 
-// workgroups of one dfcsa_dgrad_gate launch (= partial rows): every CU's resident slots, at most one per tile
+// workgroups of one dfcsa_dgrad_gate / _acc_relu_bn launch (= partial rows): every CU's resident
+// slots, at most one per tile
+template <int EPI>
 int dgrad_gate_grid(int M, int C) {
   const int kp = (C + 63) / 64 * 64;
-  const int occ = kp == 64 ? gate_occ<64>() : kp == 128 ? gate_occ<128>() : kp == 192 ? gate_occ<192>() : gate_occ<256>();
+  const int occ = kp == 64 ? gate_occ<64, EPI>() : kp == 128 ? gate_occ<128, EPI>()
+                  : kp == 192 ? gate_occ<192, EPI>() : gate_occ<256, EPI>();
   const int mtiles = (M + 63) / 64;
   int gx = 256 * occ;
   return gx > mtiles ? mtiles : gx;
@@ -1331,9 +1366,30 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
 }
 
+namespace {
+
+hipStream_t st_of(void* s) { return (hipStream_t)s; }
+
+template <int EPI>
+int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, hipStream_t st) {
+  const int M = a.M, C = a.Nd, Kpad = a.Kpad;
+  const int mtiles = (M + 63) / 64;
+  dim3 grid(dgrad_gate_grid<EPI>(M, C), C / 64);
+  const double moved = EPI == EPI_GATE ? 6.0 : 7.0;   // [M][C] tensors read + written besides A
+  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + (double)a.N * Kpad + moved * (double)M * C));
+  if (Kpad == 64) hipLaunchKernelGGL((dgrad_gate_kernel<64, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
+  else if (Kpad == 128) hipLaunchKernelGGL((dgrad_gate_kernel<128, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
+  else if (Kpad == 192) hipLaunchKernelGGL((dgrad_gate_kernel<192, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
+  else hipLaunchKernelGGL((dgrad_gate_kernel<256, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+}  // namespace
+
 extern "C" int dfcsa_dgrad_gate_parts(int M, int C) {
   if (M <= 0 || C <= 0) return DFCSA_EINVAL;
-  return dgrad_gate_grid(M, C);
+  return dgrad_gate_grid<EPI_GATE>(M, C);
 }
 
 extern "C" int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, const void* y3,
@@ -1353,16 +1409,30 @@ extern "C" int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, 
   e.y3 = (const bf16_t*)y3; e.local = (const bf16_t*)local; e.attn = (const bf16_t*)attn;
   e.sc = sc3; e.sh = sh3; e.mean = mean3; e.invstd = invstd3;
   e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.dz3 = (bf16_t*)dz3; e.part = partial;
-  const int mtiles = (M + 63) / 64;
-  dim3 grid(dgrad_gate_grid(M, C), C / 64);
-  hipStream_t st = (hipStream_t)stream;
-  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + 3.0 * C * Kpad + 6.0 * (double)M * C));
-  if (Kpad == 64) hipLaunchKernelGGL(dgrad_gate_kernel<64>, grid, dim3(256), 0, st, a, e, mtiles);
-  else if (Kpad == 128) hipLaunchKernelGGL(dgrad_gate_kernel<128>, grid, dim3(256), 0, st, a, e, mtiles);
-  else if (Kpad == 192) hipLaunchKernelGGL(dgrad_gate_kernel<192>, grid, dim3(256), 0, st, a, e, mtiles);
-  else hipLaunchKernelGGL(dgrad_gate_kernel<256>, grid, dim3(256), 0, st, a, e, mtiles);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
+  return launch_gate_epi<EPI_GATE>(a, e, st_of(stream));
+}
+
+extern "C" int dfcsa_dgrad_acc_relu_bn_parts(int M, int C) {
+  if (M <= 0 || C <= 0) return DFCSA_EINVAL;
+  return dgrad_gate_grid<EPI_ACC_RELU_BN>(M, C);
+}
+
+extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void* w3t, int Kpad, const void* y1,
+                                       const float* sc1, const float* sh1, const float* mean1, const float* invstd1,
+                                       void* dlocal, void* dattn, float* partial, void* stream) {
+  if (M <= 0 || C <= 0 || C % 64 || C > 256 || Kpad != (C + 63) / 64 * 64) return DFCSA_EINVAL;
+  if (!dy3 || !w3t || !y1 || !sc1 || !sh1 || !mean1 || !invstd1 || !dlocal || !dattn || !partial) return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M; a.N = 2 * C; a.K = C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 1; a.Nd = C;
+  a.seg[0].ptr = dy3;
+  a.Bw = w3t;
+  GateEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.y3 = (const bf16_t*)y1;
+  e.sc = sc1; e.sh = sh1; e.mean = mean1; e.invstd = invstd1;
+  e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.part = partial;
+  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, st_of(stream));
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

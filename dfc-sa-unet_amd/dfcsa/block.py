@@ -271,7 +271,15 @@ def block_backward(blk, s, dout, need_dx, dtype):
         ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                             [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
     W3t = s.pk["W3t"]
-    ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
+    fused_bn1 = dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]
+    if fused_bn1:
+        # accumulate GEMM with the local branch's BN1-backward sums in its epilogue
+        npart1 = _lib.LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
+        part1 = torch.empty(npart1 * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_dgrad_acc_relu_bn", M, C, P(dy3), P(W3t), KpC, P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
+             P(bn1.invstd), P(dlocal), P(dattn), P(part1), stream())
+    else:
+        ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
 
     # the attention chain (LightSelfAttention backward -> attention entry -> bn2 backward) runs
@@ -303,10 +311,13 @@ def block_backward(blk, s, dout, need_dx, dtype):
     del dattn
 
     # ---- local branch: relu(bn1 y1) (dz1 recomputed by the apply, not materialised) ----
-    part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
-    call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
-         None, P(part), stream())
-    coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
+    if fused_bn1:
+        part, npart = part1, npart1
+    else:
+        part, npart = torch.empty(nte * 2 * C, device=dev, dtype=f32), nte
+        call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
+             P(bn1.invstd), None, P(part), stream())
+    coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
     dy1 = ops.bn_bwd_apply_relu(dtype, dlocal, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
     del dlocal
     join_branch(dev, branch, dy2)

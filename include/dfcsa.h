@@ -229,6 +229,16 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
                      const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
                      const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
                      float* partial, void* stream);
+/* gate-conv input gradient added into [dlocal | dattn] (bf16, C % 64 == 0, C <= 256): dlocal +=
+ * (dy3 . W3t)[:, :C], dattn += (dy3 . W3t)[:, C:] (W3t = the [2C][Kpad] dgrad operand of the gate
+ * conv; same bf16 roundings as dfcsa_conv_gemm's accumulate mode), and on the final dlocal the
+ * sums of dfcsa_bwd_relu_bn (dz1 = dlocal*(y1*sc1+sh1 > 0): [sum dz1, sum dz1*xh1]) per
+ * workgroup row: partial [dfcsa_dgrad_acc_relu_bn_parts(M, C)][2][C].  Replaces the accumulate
+ * GEMM + dfcsa_bwd_relu_bn pair (reference models/unet_dfc_sa_res.py:57-62, :73-77 backward). */
+int dfcsa_dgrad_acc_relu_bn_parts(int M, int C);
+int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void* w3t, int Kpad, const void* y1,
+                            const float* sc1, const float* sh1, const float* mean1, const float* invstd1,
+                            void* dlocal, void* dattn, float* partial, void* stream);
 /* attention entry: dz2 = (dattn + adaptive_pool^T(dpooled)) * (y2*sc2+sh2 > 0) (mask only when
  * relu != 0); dpooled fp32 [B][P][P][C]; sums [sum dz2, sum dz2*xh2] */
 int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled,

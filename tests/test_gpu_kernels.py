@@ -525,3 +525,40 @@ def test_dgrad_gate_fused_equals_gemm_plus_gate(M, C):
     s0 = part0.view(nte, 2, C).double().sum(0)
     s1 = part1.view(npart, 2, C).double().sum(0)
     assert rel(s1, s0) < 1e-5
+
+
+@pytest.mark.parametrize("M,C", [(65536 + 37, 64), (16 * 112 * 112, 128), (2 * 56 * 56 + 5, 256), (300, 64),
+                                 (16 * 224 * 224, 64)])
+def test_dgrad_acc_relu_bn_fused_equals_gemm_plus_sums(M, C):
+    """dfcsa_dgrad_acc_relu_bn (gate-conv input gradient added into [dlocal, dattn] with the BN1
+    relu-backward sums in its epilogue) against the unfused pair it replaces (accumulate-mode
+    dfcsa_conv_gemm, then dfcsa_bwd_relu_bn's sums): dlocal and dattn bit-identical, the sums equal
+    to fp32 summation-order noise; ragged M."""
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P, stream
+    torch.manual_seed(12)
+    bf = torch.bfloat16
+    dev = "cuda"
+    Kp = ops.rup(C, ops.KALIGN)
+    dy3 = torch.randn(M, C, device=dev).to(bf)
+    w3t = (torch.randn(2 * C, Kp, device=dev) * 0.1).to(bf)
+    y1, dl_in, da_in = (torch.randn(M, C, device=dev).to(bf) for _ in range(3))
+    sc, sh, mu = (torch.randn(C, device=dev) for _ in range(3))
+    istd = torch.rand(C, device=dev) + 0.5
+    dl0, da0 = dl_in.clone(), da_in.clone()
+    ops.conv_gemm(bf, [(dy3.view(1, M, 1, C), 0, 0)], C, (1, M, 1), (M, 1), w3t, Kp, 2 * C,
+                  [dl0.view(1, M, 1, C), da0.view(1, M, 1, C)], C, accumulate=True)
+    nte = ops.ntiles_ew(M, C)
+    part0 = torch.empty(nte * 2 * C, device=dev)
+    call("dfcsa_bwd_relu_bn", ops.dt(bf), M, C, P(dl0), P(y1), P(sc), P(sh), P(mu), P(istd), None, P(part0), stream())
+    npart = LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
+    assert 1 <= npart <= (M + 63) // 64
+    dl1, da1 = dl_in.clone(), da_in.clone()
+    part1 = torch.empty(npart * 2 * C, device=dev)
+    call("dfcsa_dgrad_acc_relu_bn", M, C, P(dy3), P(w3t), Kp, P(y1), P(sc), P(sh), P(mu), P(istd), P(dl1), P(da1),
+         P(part1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(dl1, dl0) and torch.equal(da1, da0)
+    s0 = part0.view(nte, 2, C).double().sum(0)
+    s1 = part1.view(npart, 2, C).double().sum(0)
+    assert rel(s1, s0) < 1e-5
