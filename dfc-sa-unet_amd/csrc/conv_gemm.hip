@@ -1305,8 +1305,9 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // 256x256 ping-pong tiles (one workgroup per CU: half the L2->LDS bytes per flop of two
     // 128x128 workgroups) wherever they still give >= 150 workgroups and a long K: measured
     // (tools/pp_check.py) 1.06-1.23x the 128x128 tile on the 3x3 fwd/dgrad of the 112^2-28^2
-    // levels, slower below ~150 workgroups (one partial wave of tiles)
-    if (a.N % 256 == 0 && a.K >= 1152 && ((a.M + 255) / 256) * (a.N / 256) >= 150)
+    // levels, slower below ~150 workgroups (one partial wave of tiles) and at K < 2048 (round 2:
+    // the 112^2 decoder dgrad, K = 1408: 204 vs 175 us for the 128x128 tile; K = 1152: equal)
+    if (a.N % 256 == 0 && a.K >= 2048 && ((a.M + 255) / 256) * (a.N / 256) >= 150)
       return launch_pp<2, true, false>(a, st);
     if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) {
       // still under one 128x64 workgroup per CU with a short K (the ViT GEMMs of TransUNet:

@@ -16,7 +16,8 @@ SHAPES = [("L1 3x3 fwd up_conv1", 224, 64, 2, 9, 64), ("L1 3x3 dgrad up_conv1", 
           ("L3 3x3 fwd up_conv3", 56, 256, 2, 9, 256), ("L4 3x3 fwd up_conv4", 28, 512, 2, 9, 512),
           ("BN 3x3 fwd bottleneck", 14, 512, 1, 9, 1024), ("L4 3x3 dgrad up_conv4", 28, 512, 1, 11, 1024),
           ("BN 3x3 dgrad bottleneck", 14, 1024, 1, 11, 512), ("L4 3x3 dgrad down4", 28, 512, 1, 11, 256),
-          ("L2 3x3 dgrad N64", 112, 128, 1, 11, 64)]
+          ("L2 3x3 dgrad N64", 112, 128, 1, 11, 64), ("L3 3x3 dgrad up_conv3", 56, 256, 1, 11, 512),
+          ("L3 3x3 dgrad down3", 56, 256, 1, 11, 128), ("L3 3x3 fwd down3", 56, 128, 1, 9, 256)]
 if os.environ.get("GEMM_SHAPES"):
     keep = os.environ["GEMM_SHAPES"].split(",")
     SHAPES = [s for s in SHAPES if any(k in s[0] for k in keep)]
