@@ -1455,6 +1455,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 15) { g_conv_dbg = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
+  if (knob == 18) { g_wgrad_wide_small = value; return 0; }
   if (knob == 14) { g_wgrad_nst = (value >= 2 && value <= 4) ? value : 2; return 0; }
   return DFCSA_EINVAL;
 }

@@ -587,7 +587,11 @@ __host__ __device__ inline int wgrad_big_mode(int NI, int NJ, int big) {
 
 // 64-row (NI <= 64) bf16 tiles take 256 columns when NJ is wide (4 x 2 wave layout of 32x64
 // tiles instead of 16x64: half the LDS fragment reads per MFMA)
-bool wide_j(const WgradArgs& a) { return a.NI <= 64 && a.NJ >= 512 && !g_wgrad_narrow; }
+// knob 18: also for 128 < NJ <= 256 (the 1x1 wgrads over three 64-channel sources at 224^2: one
+// column tile, so G is read once instead of twice)
+bool wide_j(const WgradArgs& a) {
+  return a.NI <= 64 && ((a.NJ >= 512 && !g_wgrad_narrow) || (g_wgrad_wide_small && a.NJ > 128 && a.NJ <= 256));
+}
 
 template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
@@ -653,6 +657,7 @@ int g_wgrad_noglds_f32small = 0;  // knob 16: 1 = fp32 small-M wgrads take the g
 
 // output tile of the wgrad kernel a launch uses (launch_wgrad's choice)
 int g_wgrad_big = 0;        // knob 17: big wgrad tiles (wgrad_big_mode)
+int g_wgrad_wide_small = 0; // knob 18: 64x256 tile for NI <= 64, 128 < NJ <= 256 (wide_j)
 void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
   if (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds) {
     if (const int bm = wgrad_big_mode(NI, NJ, g_wgrad_big)) {
@@ -662,7 +667,8 @@ void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
     }
   }
   *BI = NI <= 64 ? 64 : 128;
-  *BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 && NJ >= 512 && !g_wgrad_narrow) ? 256 : 128;
+  *BJ = (dtype == DFCSA_DT_BF16 && !g_wgrad_noglds && NI <= 64 &&
+         ((NJ >= 512 && !g_wgrad_narrow) || (g_wgrad_wide_small && NJ > 128 && NJ <= 256))) ? 256 : 128;
 }
 
 extern "C" int dfcsa_wgrad_fuse_max(void) { return g_wgrad_fuse_max; }

@@ -562,3 +562,27 @@ def test_dgrad_acc_relu_bn_fused_equals_gemm_plus_sums(M, C):
     s0 = part0.view(nte, 2, C).double().sum(0)
     s1 = part1.view(npart, 2, C).double().sum(0)
     assert rel(s1, s0) < 1e-5
+
+
+@pytest.mark.parametrize("wide", [0, 1])
+@pytest.mark.parametrize("B,H,W,nsrc,NI", [(2, 20, 18, 3, 64), (1, 9, 7, 2, 40), (4, 16, 16, 3, 16)])
+def test_wgrad_1x1_multisource_wide_tile(wide, B, H, W, nsrc, NI):
+    """1x1 weight gradient over 2-3 concatenated 64-channel sources (the fusion / gate convs) with
+    the 64x256 tile of tuning knob 18 (one column tile: the output gradient read once) and without,
+    against torch fp32 on bf16-exact operands."""
+    import dfcsa
+    torch.manual_seed(8)
+    bf = torch.bfloat16
+    xs = [q(torch.randn(B, 64, H, W), bf) for _ in range(nsrc)]
+    g = q(torch.randn(B, NI, H, W), bf)
+    w = torch.zeros(NI, 64 * nsrc, 1, 1, requires_grad=True)
+    F.conv2d(torch.cat(xs, 1), w).backward(g)
+    segs = [(nhwc(x, bf), 0, 0) for x in xs]
+    gw = torch.zeros(NI, 64 * nsrc, device="cuda")
+    dfcsa.set_tuning(18, wide)
+    try:
+        ops.conv_wgrad_into(bf, [nhwc(g, bf)], NI, segs, 64, (B, H, W), (H, W), [gw], 1, 64 * nsrc, 64 * nsrc)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(18, 0)
+    assert rel(gw.view(NI, -1, 1, 1), w.grad) < 1e-5

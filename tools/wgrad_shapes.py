@@ -24,8 +24,8 @@ MODES = {"default": {}, "fuse16": {13: 16}, "unfused": {12: -1},
          "nst3": {14: 3}, "nst4": {14: 4}, "nst3_t256": {14: 3, 2: 256}, "nst4_t256": {14: 4, 2: 256},
          "nst3_t1024": {14: 3, 2: 1024}, "t1024": {2: 1024},
          "big1": {17: 1}, "big1_t256": {17: 1, 2: 256}, "big1_t1024": {17: 1, 2: 1024}, "big2": {17: 2},
-         "big2_t256": {17: 2, 2: 256}, "big3": {17: 3}, "big3_t256": {17: 3, 2: 256}, "big1_f16": {17: 1, 13: 16}}
-DEFAULTS = {2: 512, 12: 0, 13: 0, 14: 2, 17: 0}
+         "big2_t256": {17: 2, 2: 256}, "big3": {17: 3}, "big3_t256": {17: 3, 2: 256}, "big1_f16": {17: 1, 13: 16}, "wide192": {18: 1}}
+DEFAULTS = {2: 512, 12: 0, 13: 0, 14: 2, 17: 0, 18: 0}
 if os.environ.get("WGRAD_MODES"):
     MODES = {k: v for k, v in MODES.items() if k in os.environ["WGRAD_MODES"].split(",")}
 
