@@ -19,6 +19,7 @@
 // register-staged double-buffered LDS with an XOR swizzle that makes the ds_read_b128 fragment
 // reads conflict-free; mfma_f32_16x16x32_bf16 (bf16) or 8 x mfma_f32_16x16x4f32 (f32 parity
 // mode; exact f32 FMA chain).
+#include <algorithm>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -1182,6 +1183,154 @@ int dgrad_gate_grid(int M, int C) {
   return gx > mtiles ? mtiles : gx;
 }
 
+// --------------------------------------------------------------------------------------------
+// Fusion conv forward with the gate fusion in its A-operand prologue (dfcsa_gate_fusion_fwd,
+// C = 64): the A image of a 64-row tile is DMA'd as [y3 | local | attn] (three 64-channel K
+// stages); after it lands, each lane turns its two (row, 8-channel) chunks of the y3 stage into
+//   fused = g*local + (1-g)*attn,  g = sigmoid(y3*sc3 + sh3)        (dfcsa_gate_fuse's arithmetic)
+// in place in LDS (and stores them: the fusion conv's weight gradient reads `fused`), then the
+// tile is multiplied as by conv1x1_stream_kernel: y4 = [fused|local|attn] . W4^T + b4 with the
+// BN4 partial statistics per 64-row tile.  The separate gate-fusion pass (3 reads + 1 write) and
+// the GEMM's re-read of `fused` become one pass.  Reference models/unet_dfc_sa_res.py:102-110.
+// --------------------------------------------------------------------------------------------
+__global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const float* __restrict__ sc3,
+                                                              const float* __restrict__ sh3, bf16_t* __restrict__ fused,
+                                                              int mtiles) {
+  using T = bf16_t;
+  constexpr int C = 64, KP = 192, KS = 3, KG = 6, NWC = 16, FN = 1, NWG = 64;
+  constexpr int IMG = 64 * 128, SLOT = KS * IMG;
+  constexpr int OSTR = NWG * 2 + 16;
+  constexpr int NSTORE = (64 * (NWG / 8)) / 256, OCH = NWG / 8;
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int M = args.M;
+  const int rsub = lane >> 3;
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+  bf16x8_t bfr[FN][KG];
+  {
+    const int n = wave * NWC + (lane & 15);
+#pragma unroll
+    for (int g = 0; g < KG; ++g)
+      bfr[0][g] = *(const bf16x8_t*)((const T*)args.Bw + (size_t)n * args.Kpad + g * 32 + 8 * (lane >> 4));
+  }
+  const float bias = args.bias ? args.bias[wave * NWC + (lane & 15)] : 0.f;
+  const void* zero = (const void*)g_zero_page;
+  const T* a_src[KS];
+#pragma unroll
+  for (int i = 0; i < KS; ++i) a_src[i] = (const T*)args.seg[i].ptr + cchunk * 8;
+  auto issue = [&](int t, int slot) {
+    char* base = smem + slot * SLOT;
+#pragma unroll
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int st = i >> 1, rb = (i & 1) * 4 + wave;
+      const int m = t * 64 + rb * 8 + rsub;
+      const void* src = m < M ? (const void*)(a_src[st] + (size_t)m * C) : zero;
+      glds16(src, base + st * IMG + rb * 8 * 128);
+    }
+  };
+  // prologue items: logical chunk pc of rows pr and pr + 32
+  const int pc = tid & 7, pr = tid >> 3;
+  float sc[8], sh[8];
+  load8<float>(sc3 + pc * 8, sc);
+  load8<float>(sh3 + pc * 8, sh);
+  T* o_base[NSTORE];
+  int o_row[NSTORE];
+#pragma unroll
+  for (int it = 0; it < NSTORE; ++it) {
+    const int e = tid + it * 256;
+    o_row[it] = e / OCH;
+    o_base[it] = (T*)args.dest[0] + (e - o_row[it] * OCH) * 8;
+  }
+  int t = blockIdx.x;
+  if (t >= mtiles) return;
+  issue(t, 0);
+  int slot = 0;
+  bool first_iter = true;
+  for (; t < mtiles; t += gridDim.x, slot ^= 1) {
+    const int tn = t + gridDim.x;
+    // outstanding, in issue order: DMA(t), the previous tile's 2 fused + FN stats + NSTORE
+    // output stores, DMA(tn): the counted wait retires DMA(t) and leaves the rest in flight
+    if (tn < mtiles) {
+      issue(tn, slot ^ 1);
+      if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + 2 + FN + NSTORE) : "memory");
+    } else {
+      if (first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + FN + NSTORE) : "memory");
+    }
+    first_iter = false;
+    lds_barrier();
+    char* img = smem + slot * SLOT;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int row = pr + 32 * h, m = t * 64 + row;
+      const int off = row * 128 + swz(row, pc) * 16;
+      float y[8], l[8], at[8], f[8];
+      load8<T>((const T*)(img + off), y);
+      load8<T>((const T*)(img + IMG + off), l);
+      load8<T>((const T*)(img + 2 * IMG + off), at);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float g = gate_sigm(y[q] * sc[q] + sh[q]);
+        f[q] = g * l[q] + (1.f - g) * at[q];
+      }
+      store8<T>((T*)(img + off), f);
+      // one store per item whatever m (rows past M go to the sink): a fixed count per tile
+      T* dst = m < M ? fused + (size_t)m * C + pc * 8 : (T*)(g_store_sink + 4 * (tid & 63));
+      store8<T>(dst, f);
+    }
+    lds_barrier();
+    f32x4_t acc[4][FN];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) acc[i][0] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int g = 0; g < KG; ++g) {
+      Frag<T> fa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) read_frag<T>(img + (g >> 1) * IMG, i * 16 + (lane & 15), g & 1, lane, fa[i]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[0][g], acc[i][0], 0, 0, 0);
+    }
+    const int m0 = t * 64;
+    {
+      float s = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
+          const float v = m < M ? acc[i][0][r] : 0.f;
+          s += v;
+          q += v * v;
+        }
+      s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      const int n = wave * NWC + (lane & 15);
+      if (lane < 32) args.stats[(size_t)t * 2 * C + (lane < 16 ? 0 : C) + n] = lane < 16 ? s : q;
+    }
+    {
+      const int col = wave * NWC + (lane & 15);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          *(T*)(otile + (i * 16 + (lane >> 4) * 4 + r) * OSTR + col * 2) = f2bf(acc[i][0][r] + bias);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int it = 0; it < NSTORE; ++it) {
+      const int e = tid + it * 256;
+      const int row = o_row[it], cc = e - row * OCH;
+      const int m = m0 + row;
+      const uint4 v = *(const uint4*)(otile + row * OSTR + cc * 16);
+      T* dst = m < M ? o_base[it] + (size_t)m * C : (T*)(g_store_sink + 4 * (tid & 63));
+      *(uint4*)dst = v;
+    }
+  }
+}
+
 int g_stream_wgs = 0;   // workgroups per CU of the streaming kernel (0 = occupancy limit)
 int g_debug = -1;
 int g_stream_force = 0;  // knob 5: take the streaming kernel whenever it applies (tests)
@@ -1434,6 +1583,28 @@ extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void
   e.sc = sc1; e.sh = sh1; e.mean = mean1; e.invstd = invstd1;
   e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.part = partial;
   return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, st_of(stream));
+}
+
+extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
+                                     const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
+                                     void* fused, void* y4, float* stats4, void* stream) {
+  if (M <= 0 || C != 64 || Kpad != 192 || !y3 || !sc3 || !sh3 || !local || !attn || !w4 || !fused || !y4 || !stats4)
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M; a.N = C; a.K = 3 * C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 3; a.Nd = C; a.ndest = 1;
+  a.seg[0].ptr = y3; a.seg[1].ptr = local; a.seg[2].ptr = attn;
+  a.Bw = w4; a.bias = b4; a.dest[0] = y4; a.stats = stats4;
+  static int occ = 0;
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel, 256, 0) != hipSuccess || occ < 1))
+    occ = 1;
+  const int mtiles = (M + 63) / 64;
+  const int gx = std::min(256 * occ, mtiles);
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + (double)C * Kpad + 2.0 * (double)M * C));
+  hipLaunchKernelGGL(gate_fusion_fwd_kernel, dim3(gx), dim3(256), 0, st, a, sc3, sh3, (bf16_t*)fused, mtiles);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

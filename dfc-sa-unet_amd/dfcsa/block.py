@@ -32,7 +32,10 @@ from .packs import get_packset, param_key
 from .streams import join_branch, on_branch, on_side
 
 # bf16 blocks with C % 64 == 0, C <= 256: the fusion conv's input-gradient GEMM carries the gate
-# backward in its epilogue (dfcsa_dgrad_gate); DFCSA_DGRAD_GATE=0 selects the GEMM + dfcsa_bwd_gate pair
+# backward in its epilogue (dfcsa_dgrad_gate), the gate conv's accumulating one the BN1-backward
+# sums (dfcsa_dgrad_acc_relu_bn); C == 64 (train mode): the fusion conv's forward GEMM computes the
+# gate fusion in its A-operand prologue (dfcsa_gate_fusion_fwd).  DFCSA_DGRAD_GATE=0 selects the
+# separate GEMM + elementwise launches everywhere
 FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
 
 
@@ -142,12 +145,17 @@ def block_forward(blk, xs, pool_size, training, dtype):
                   bias=conv3.bias, stats=st3)
     bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt, C, C, M, training)
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
-         stream())
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st4 = stats(C)
-    ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C, [y4],
-                  C, bias=conv4.bias, stats=st4)
+    if dtype == torch.bfloat16 and C == 64 and Kp4 == 192 and training and FUSED_DGRAD_GATE[0]:
+        # the gate fusion runs in the fusion conv's A-operand prologue (dfcsa_gate_fusion_fwd)
+        call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4,
+             P(conv4.bias), P(fused), P(y4), P(st4), stream())
+    else:
+        call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
+             stream())
+        ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C, [y4],
+                      C, bias=conv4.bias, stats=st4)
     bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt, C, C, M, training)
     out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     call("dfcsa_block_out", dt(dtype), M, C, P(y4), P(bn4.scale), P(bn4.shift), P(res), P(blk.res_scale), P(out),

@@ -229,6 +229,14 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
                      const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
                      const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
                      float* partial, void* stream);
+/* fusion conv forward with the gate fusion in its A-operand prologue (bf16, C == 64, Kpad == 192):
+ * fused = g*local + (1-g)*attn, g = sigmoid(y3*sc3+sh3) (dfcsa_gate_fuse's arithmetic), stored;
+ * y4 = [fused | local | attn] . w4^T + b4 (w4 = the fusion conv's [64][192] forward operand) with
+ * the BatchNorm partial statistics of dfcsa_conv_gemm (stats4 [ceil(M/64)][2][64]).  Replaces the
+ * dfcsa_gate_fuse + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:102-110). */
+int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
+                          const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
+                          float* stats4, void* stream);
 /* gate-conv input gradient added into [dlocal | dattn] (bf16, C % 64 == 0, C <= 256): dlocal +=
  * (dy3 . W3t)[:, :C], dattn += (dy3 . W3t)[:, C:] (W3t = the [2C][Kpad] dgrad operand of the gate
  * conv; same bf16 roundings as dfcsa_conv_gemm's accumulate mode), and on the final dlocal the

@@ -586,3 +586,35 @@ def test_wgrad_1x1_multisource_wide_tile(wide, B, H, W, nsrc, NI):
     finally:
         dfcsa.set_tuning(18, 0)
     assert rel(gw.view(NI, -1, 1, 1), w.grad) < 1e-5
+
+
+@pytest.mark.parametrize("M", [16 * 224 * 224, 65536 + 37, 300])
+def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M):
+    """dfcsa_gate_fusion_fwd (fusion conv forward with the gate fusion in its A-operand prologue,
+    C = 64) against the pair it replaces (dfcsa_gate_fuse, then the [fused, local, attn] GEMM with
+    BN statistics): fused, y4 and the statistics slab; ragged M."""
+    from dfcsa._lib import call
+    from dfcsa.ops import P, stream
+    torch.manual_seed(13)
+    bf = torch.bfloat16
+    dev = "cuda"
+    C, Kp = 64, 192
+    y3, loc, att = (torch.randn(M, C, device=dev).to(bf) for _ in range(3))
+    sc, sh = torch.randn(C, device=dev), torch.randn(C, device=dev)
+    w4 = (torch.randn(C, Kp, device=dev) * 0.1).to(bf)
+    b4 = torch.randn(C, device=dev)
+    nt = ops.ntiles_gemm(M)
+    f0, y0 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(2))
+    st0 = torch.empty(nt * 2 * C, device=dev)
+    call("dfcsa_gate_fuse", ops.dt(bf), M, C, P(y3), P(sc), P(sh), P(loc), P(att), P(f0), stream())
+    v = lambda t: t.view(1, M, 1, C)
+    ops.conv_gemm(bf, [(v(f0), 0, 0), (v(loc), 0, 0), (v(att), 0, 0)], C, (1, M, 1), (M, 1), w4, Kp, C, [v(y0)], C,
+                  bias=b4, stats=st0)
+    f1, y1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(2))
+    st1 = torch.empty(nt * 2 * C, device=dev)
+    call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(sc), P(sh), P(loc), P(att), P(w4), Kp, P(b4), P(f1), P(y1), P(st1),
+         stream())
+    torch.cuda.synchronize()
+    assert rel(f1, f0) < 1e-6 and (f1.float() - f0.float()).abs().max().item() <= 2 ** -7 * f0.float().abs().max().item()
+    assert rel(y1, y0) < 2e-3
+    assert rel(st1, st0) < 1e-4
