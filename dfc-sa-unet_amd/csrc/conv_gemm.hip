@@ -977,6 +977,17 @@ struct GateEpi {
 
 __device__ __forceinline__ float gate_sigm(float x) { return 1.f / (1.f + __expf(-x)); }  // = block_ew sigm
 
+// F.interpolate(bilinear, align_corners=False) source taps along one axis (= block_ew bilin_axis)
+__device__ __forceinline__ void bilin_axis_c(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
+  float scale = (float)in / (float)out;
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
+
 // EPI_GATE: the gate backward above (192 columns: dfused | dlocal | dattn of channel block cb).
 // EPI_ACC_RELU_BN (dfcsa_dgrad_acc_relu_bn): the gate conv's input gradient dy3 . W3t ADDED into
 // [dlocal | dattn] (128 columns per workgroup; the same bf16 rounding as the accumulate-mode GEMM)
@@ -1193,11 +1204,29 @@ int dgrad_gate_grid(int M, int C) {
 // BN4 partial statistics per 64-row tile.  The separate gate-fusion pass (3 reads + 1 write) and
 // the GEMM's re-read of `fused` become one pass.  Reference models/unet_dfc_sa_res.py:102-110.
 // --------------------------------------------------------------------------------------------
-__global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const float* __restrict__ sc3,
-                                                              const float* __restrict__ sh3, bf16_t* __restrict__ fused,
-                                                              int mtiles) {
+// PRO_GATE_FUSION (above).  PRO_LOCAL_ATTN (dfcsa_local_attn_gate_fwd): the gate conv, A = [y1 | y2]
+// DMA'd; the prologue forms local = relu(bn1 y1) and attn = gamma * bilinear(o) + relu(bn2 y2)
+// (dfcsa_block_local_attn's arithmetic) in place and stores both; then y3 = [local|attn] . W3^T + b3
+// with BN3 statistics.  The o taps of a lane's two pixels are loaded ahead of the tile's wait.
+enum { PRO_GATE_FUSION = 0, PRO_LOCAL_ATTN = 1 };
+
+struct FwdPro {
+  const float* sc0;   // gate fusion: bn3; local/attn: bn1
+  const float* sh0;
+  const float* sc1;   // local/attn: bn2
+  const float* sh1;
+  const float* o;     // [B][P][P][64] fp32 LightSelfAttention output
+  const float* gamma;
+  int P, H, W;
+  bf16_t* out0;       // fused / local
+  bf16_t* out1;       // - / attn
+};
+
+template <int PRO>
+__global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
   using T = bf16_t;
-  constexpr int C = 64, KP = 192, KS = 3, KG = 6, NWC = 16, FN = 1, NWG = 64;
+  constexpr int C = 64, KS = PRO == PRO_GATE_FUSION ? 3 : 2, KG = 2 * KS, NWC = 16, FN = 1, NWG = 64;
+  constexpr int NOUT = PRO == PRO_GATE_FUSION ? 1 : 2;   // prologue stores per item
   constexpr int IMG = 64 * 128, SLOT = KS * IMG;
   constexpr int OSTR = NWG * 2 + 16;
   constexpr int NSTORE = (64 * (NWG / 8)) / 256, OCH = NWG / 8;
@@ -1232,9 +1261,15 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   };
   // prologue items: logical chunk pc of rows pr and pr + 32
   const int pc = tid & 7, pr = tid >> 3;
-  float sc[8], sh[8];
-  load8<float>(sc3 + pc * 8, sc);
-  load8<float>(sh3 + pc * 8, sh);
+  float sc[8], sh[8], sc2[8], sh2[8];
+  load8<float>(pr_.sc0 + pc * 8, sc);
+  load8<float>(pr_.sh0 + pc * 8, sh);
+  float gam = 0.f;
+  if constexpr (PRO == PRO_LOCAL_ATTN) {
+    load8<float>(pr_.sc1 + pc * 8, sc2);
+    load8<float>(pr_.sh1 + pc * 8, sh2);
+    gam = *pr_.gamma;
+  }
   T* o_base[NSTORE];
   int o_row[NSTORE];
 #pragma unroll
@@ -1250,15 +1285,44 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   bool first_iter = true;
   for (; t < mtiles; t += gridDim.x, slot ^= 1) {
     const int tn = t + gridDim.x;
-    // outstanding, in issue order: DMA(t), the previous tile's 2 fused + FN stats + NSTORE
-    // output stores, DMA(tn): the counted wait retires DMA(t) and leaves the rest in flight
-    if (tn < mtiles) {
-      issue(tn, slot ^ 1);
-      if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + 2 + FN + NSTORE) : "memory");
+    // LightSelfAttention taps of this tile's two pixels, loaded before the next tile's DMA
+    float ov[2][4][8], lw[2][4];
+    if constexpr (PRO == PRO_LOCAL_ATTN) {
+      const int hw = pr_.H * pr_.W;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int m = min(t * 64 + pr + 32 * h, M - 1);
+        const int b = m / hw, rem = m - b * hw, hh = rem / pr_.W, ww = rem - hh * pr_.W;
+        int h0, h1, w0, w1;
+        float lh0, lh1, lw0, lw1;
+        bilin_axis_c(hh, pr_.P, pr_.H, h0, h1, lh0, lh1);
+        bilin_axis_c(ww, pr_.P, pr_.W, w0, w1, lw0, lw1);
+        const float* ob = pr_.o + (size_t)b * pr_.P * pr_.P * C + pc * 8;
+        load8<float>(ob + (size_t)(h0 * pr_.P + w0) * C, ov[h][0]);
+        load8<float>(ob + (size_t)(h0 * pr_.P + w1) * C, ov[h][1]);
+        load8<float>(ob + (size_t)(h1 * pr_.P + w0) * C, ov[h][2]);
+        load8<float>(ob + (size_t)(h1 * pr_.P + w1) * C, ov[h][3]);
+        lw[h][0] = lh0; lw[h][1] = lh1; lw[h][2] = lw0; lw[h][3] = lw1;
+      }
+    }
+    // outstanding, in issue order: DMA(t), [o taps], the previous tile's prologue + FN stats +
+    // NSTORE output stores, DMA(tn): the counted wait retires everything before DMA(tn)
+    if constexpr (PRO == PRO_GATE_FUSION) {   // no loads besides the DMAs: leave the stores in flight
+      if (tn < mtiles) {
+        issue(tn, slot ^ 1);
+        if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + 2 * NOUT + FN + NSTORE) : "memory");
+      } else {
+        if (first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NOUT + FN + NSTORE) : "memory");
+      }
     } else {
-      if (first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 + FN + NSTORE) : "memory");
+      if (tn < mtiles) {
+        issue(tn, slot ^ 1);
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
     }
     first_iter = false;
     lds_barrier();
@@ -1267,19 +1331,36 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     for (int h = 0; h < 2; ++h) {
       const int row = pr + 32 * h, m = t * 64 + row;
       const int off = row * 128 + swz(row, pc) * 16;
-      float y[8], l[8], at[8], f[8];
+      float y[8], l[8], f[8];
       load8<T>((const T*)(img + off), y);
       load8<T>((const T*)(img + IMG + off), l);
-      load8<T>((const T*)(img + 2 * IMG + off), at);
+      T* sink = (T*)(g_store_sink + 4 * (tid & 63));
+      if constexpr (PRO == PRO_GATE_FUSION) {
+        float at[8];
+        load8<T>((const T*)(img + 2 * IMG + off), at);
 #pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const float g = gate_sigm(y[q] * sc[q] + sh[q]);
-        f[q] = g * l[q] + (1.f - g) * at[q];
+        for (int q = 0; q < 8; ++q) {
+          const float g = gate_sigm(y[q] * sc[q] + sh[q]);
+          f[q] = g * l[q] + (1.f - g) * at[q];
+        }
+        store8<T>((T*)(img + off), f);
+        // one store per item whatever m (rows past M go to the sink): a fixed count per tile
+        store8<T>(m < M ? pr_.out0 + (size_t)m * C + pc * 8 : sink, f);
+      } else {
+        float a2[8];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          f[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f);
+          const float upv = lw[h][0] * (lw[h][2] * ov[h][0][q] + lw[h][3] * ov[h][1][q]) +
+                            lw[h][1] * (lw[h][2] * ov[h][2][q] + lw[h][3] * ov[h][3][q]);
+          const float v = l[q] * sc2[q] + sh2[q];
+          a2[q] = gam * upv + fmaxf(v, 0.f);
+        }
+        store8<T>((T*)(img + off), f);
+        store8<T>((T*)(img + IMG + off), a2);
+        store8<T>(m < M ? pr_.out0 + (size_t)m * C + pc * 8 : sink, f);
+        store8<T>(m < M ? pr_.out1 + (size_t)m * C + pc * 8 : sink, a2);
       }
-      store8<T>((T*)(img + off), f);
-      // one store per item whatever m (rows past M go to the sink): a fixed count per tile
-      T* dst = m < M ? fused + (size_t)m * C + pc * 8 : (T*)(g_store_sink + 4 * (tid & 63));
-      store8<T>(dst, f);
     }
     lds_barrier();
     f32x4_t acc[4][FN];
@@ -1585,6 +1666,23 @@ extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void
   return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, st_of(stream));
 }
 
+namespace {
+template <int PRO>
+int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
+  static int occ = 0;
+  if (!occ &&
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO>, 256, 0) != hipSuccess || occ < 1))
+    occ = 1;
+  const int mtiles = (a.M + 63) / 64;
+  const int gx = std::min(256 * occ, mtiles);
+  const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
+  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + 64.0 * a.Kpad + moved * a.M * 64.0));
+  hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+}  // namespace
+
 extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
                                      const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
                                      void* fused, void* y4, float* stats4, void* stream) {
@@ -1595,16 +1693,32 @@ extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* 
   a.M = M; a.N = C; a.K = 3 * C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 3; a.Nd = C; a.ndest = 1;
   a.seg[0].ptr = y3; a.seg[1].ptr = local; a.seg[2].ptr = attn;
   a.Bw = w4; a.bias = b4; a.dest[0] = y4; a.stats = stats4;
-  static int occ = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel, 256, 0) != hipSuccess || occ < 1))
-    occ = 1;
-  const int mtiles = (M + 63) / 64;
-  const int gx = std::min(256 * occ, mtiles);
-  hipStream_t st = (hipStream_t)stream;
-  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + (double)C * Kpad + 2.0 * (double)M * C));
-  hipLaunchKernelGGL(gate_fusion_fwd_kernel, dim3(gx), dim3(256), 0, st, a, sc3, sh3, (bf16_t*)fused, mtiles);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
+  FwdPro pro;
+  std::memset(&pro, 0, sizeof(pro));
+  pro.sc0 = sc3; pro.sh0 = sh3; pro.out0 = (bf16_t*)fused;
+  return launch_fwd_pro<PRO_GATE_FUSION>(a, pro, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1,
+                                         const float* sh1, const void* y2, const float* sc2, const float* sh2,
+                                         const float* o, int P, const float* gamma, const void* w3, int Kpad,
+                                         const float* b3, void* local, void* attn, void* y3, float* stats3,
+                                         void* stream) {
+  const int64_t M = (int64_t)B * H * W;
+  if (M <= 0 || M >= (1ll << 31) || C != 64 || Kpad != 128 || P <= 0 || !y1 || !sc1 || !sh1 || !y2 || !sc2 ||
+      !sh2 || !o || !gamma || !w3 || !local || !attn || !y3 || !stats3)
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = (int)M; a.N = C; a.K = 2 * C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 2; a.Nd = C; a.ndest = 1;
+  a.seg[0].ptr = y1; a.seg[1].ptr = y2;
+  a.Bw = w3; a.bias = b3; a.dest[0] = y3; a.stats = stats3;
+  FwdPro pro;
+  std::memset(&pro, 0, sizeof(pro));
+  pro.sc0 = sc1; pro.sh0 = sh1; pro.sc1 = sc2; pro.sh1 = sh2; pro.o = o; pro.gamma = gamma;
+  pro.P = P; pro.H = H; pro.W = W;
+  pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
+  return launch_fwd_pro<PRO_LOCAL_ATTN>(a, pro, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

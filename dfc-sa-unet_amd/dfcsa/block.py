@@ -135,14 +135,20 @@ def block_forward(blk, xs, pool_size, training, dtype):
         pooled, qkv, A, o, Wqkv = lsa_saved
         local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
         attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-        call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
-             P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
-
-    # ---- gate + fusion ----
     y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st3 = stats(C)
-    ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
-                  bias=conv3.bias, stats=st3)
+    if not fullres and dtype == torch.bfloat16 and C == 64 and Kp3 == 128 and training and FUSED_DGRAD_GATE[0]:
+        # the local/attention merge runs in the gate conv's A-operand prologue
+        call("dfcsa_local_attn_gate_fwd", B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2), P(bn2.scale),
+             P(bn2.shift), P(o), Pp, P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), P(st3),
+             stream())
+    else:
+        if not fullres:
+            call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
+                 P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
+        # ---- gate conv ----
+        ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
+                      bias=conv3.bias, stats=st3)
     bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt, C, C, M, training)
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)

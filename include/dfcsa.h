@@ -237,6 +237,15 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
 int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
                           float* stats4, void* stream);
+/* gate conv forward with the local/attention merge in its A-operand prologue (bf16, C == 64,
+ * Kpad == 128, relu): local = relu(y1*sc1+sh1), attn = gamma*bilinear(o) + relu(y2*sc2+sh2)
+ * (dfcsa_block_local_attn's arithmetic; o fp32 [B][P][P][64]), both stored; y3 = [local | attn] .
+ * w3^T + b3 with BatchNorm partial statistics (stats3 [ceil(M/64)][2][64]).  Replaces the
+ * dfcsa_block_local_attn + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:36-38, 97-102). */
+int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
+                              const void* y2, const float* sc2, const float* sh2, const float* o, int P,
+                              const float* gamma, const void* w3, int Kpad, const float* b3, void* local,
+                              void* attn, void* y3, float* stats3, void* stream);
 /* gate-conv input gradient added into [dlocal | dattn] (bf16, C % 64 == 0, C <= 256): dlocal +=
  * (dy3 . W3t)[:, :C], dattn += (dy3 . W3t)[:, C:] (W3t = the [2C][Kpad] dgrad operand of the gate
  * conv; same bf16 roundings as dfcsa_conv_gemm's accumulate mode), and on the final dlocal the

@@ -618,3 +618,40 @@ def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M):
     assert rel(f1, f0) < 1e-6 and (f1.float() - f0.float()).abs().max().item() <= 2 ** -7 * f0.float().abs().max().item()
     assert rel(y1, y0) < 2e-3
     assert rel(st1, st0) < 1e-4
+
+
+@pytest.mark.parametrize("B,H,W,P", [(16, 224, 224, 4), (2, 36, 36, 4), (3, 14, 9, 8), (1, 5, 7, 4)])
+def test_local_attn_gate_fwd_equals_merge_plus_gemm(B, H, W, P):
+    """dfcsa_local_attn_gate_fwd (gate conv forward with the local/attention merge in its A-operand
+    prologue, C = 64) against the pair it replaces (dfcsa_block_local_attn, then the [local, attn]
+    GEMM with BN statistics): local, attn, y3 and the statistics slab; ragged M, P > H."""
+    from dfcsa._lib import call
+    from dfcsa.ops import P as Ptr, stream
+    torch.manual_seed(14)
+    bf = torch.bfloat16
+    dev = "cuda"
+    C, Kp = 64, 128
+    M = B * H * W
+    y1, y2 = (torch.randn(M, C, device=dev).to(bf) for _ in range(2))
+    sc1, sh1, sc2, sh2 = (torch.randn(C, device=dev) for _ in range(4))
+    o = torch.randn(B, P, P, C, device=dev)
+    gamma = torch.tensor([0.37], device=dev)
+    w3 = (torch.randn(C, Kp, device=dev) * 0.1).to(bf)
+    b3 = torch.randn(C, device=dev)
+    nt = ops.ntiles_gemm(M)
+    l0, a0, y30 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
+    st0 = torch.empty(nt * 2 * C, device=dev)
+    call("dfcsa_block_local_attn", ops.dt(bf), B, H, W, C, Ptr(y1), Ptr(sc1), Ptr(sh1), Ptr(y2), Ptr(sc2), Ptr(sh2),
+         Ptr(o), P, Ptr(gamma), 1, Ptr(l0), Ptr(a0), stream())
+    v = lambda t: t.view(B, H, W, C)
+    ops.conv_gemm(bf, [(v(l0), 0, 0), (v(a0), 0, 0)], C, (B, H, W), (H, W), w3, Kp, C, [v(y30)], C, bias=b3,
+                  stats=st0)
+    l1, a1, y31 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
+    st1 = torch.empty(nt * 2 * C, device=dev)
+    call("dfcsa_local_attn_gate_fwd", B, H, W, C, Ptr(y1), Ptr(sc1), Ptr(sh1), Ptr(y2), Ptr(sc2), Ptr(sh2), Ptr(o), P,
+         Ptr(gamma), Ptr(w3), Kp, Ptr(b3), Ptr(l1), Ptr(a1), Ptr(y31), Ptr(st1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(l1, l0)
+    assert rel(a1, a0) < 1e-6
+    assert rel(y31, y30) < 2e-3
+    assert rel(st1, st0) < 1e-4
