@@ -1222,10 +1222,16 @@ struct FwdPro {
   bf16_t* out1;       // - / attn
 };
 
-template <int PRO>
+template <int PRO, int C>
 __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
   using T = bf16_t;
-  constexpr int C = 64, KS = PRO == PRO_GATE_FUSION ? 3 : 2, KG = 2 * KS, NWC = 16, FN = 1, NWG = 64;
+  static_assert(C == 64 || (C == 128 && PRO == PRO_GATE_FUSION), "prologue GEMM widths");
+  constexpr int NSEG = PRO == PRO_GATE_FUSION ? 3 : 2;
+  constexpr int SPS = C / 64;                       // 64-channel K stages per source
+  constexpr int KS = NSEG * SPS, KG = 2 * KS;
+  constexpr int NWC = C / 4, FN = NWC / 16, NWG = C;  // all C output columns in one workgroup
+  constexpr int CPR = C / 8;                        // 8-channel chunks per pixel row
+  constexpr int RSTEP = 256 / CPR, NITEM = 64 / RSTEP;   // prologue rows per pass, items per lane
   constexpr int NOUT = PRO == PRO_GATE_FUSION ? 1 : 2;   // prologue stores per item
   constexpr int IMG = 64 * 128, SLOT = KS * IMG;
   constexpr int OSTR = NWG * 2 + 16;
@@ -1238,17 +1244,21 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   const int rsub = lane >> 3;
   const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
   bf16x8_t bfr[FN][KG];
-  {
-    const int n = wave * NWC + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = wave * NWC + j * 16 + (lane & 15);
 #pragma unroll
     for (int g = 0; g < KG; ++g)
-      bfr[0][g] = *(const bf16x8_t*)((const T*)args.Bw + (size_t)n * args.Kpad + g * 32 + 8 * (lane >> 4));
+      bfr[j][g] = *(const bf16x8_t*)((const T*)args.Bw + (size_t)n * args.Kpad + g * 32 + 8 * (lane >> 4));
   }
-  const float bias = args.bias ? args.bias[wave * NWC + (lane & 15)] : 0.f;
+  float bias[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) bias[j] = args.bias ? args.bias[wave * NWC + j * 16 + (lane & 15)] : 0.f;
   const void* zero = (const void*)g_zero_page;
+  // K stage st = source (st / SPS), channels (st % SPS) * 64 ..
   const T* a_src[KS];
 #pragma unroll
-  for (int i = 0; i < KS; ++i) a_src[i] = (const T*)args.seg[i].ptr + cchunk * 8;
+  for (int i = 0; i < KS; ++i) a_src[i] = (const T*)args.seg[i / SPS].ptr + (i % SPS) * 64 + cchunk * 8;
   auto issue = [&](int t, int slot) {
     char* base = smem + slot * SLOT;
 #pragma unroll
@@ -1259,8 +1269,10 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
       glds16(src, base + st * IMG + rb * 8 * 128);
     }
   };
-  // prologue items: logical chunk pc of rows pr and pr + 32
-  const int pc = tid & 7, pr = tid >> 3;
+  // prologue items: chunk pc (channels pc*8 ..) of rows pr + k*RSTEP; the chunk lives in K stage
+  // (source*SPS + pc/8) at logical 16-B chunk pc%8 of the row
+  const int pc = tid % CPR, pr = tid / CPR;
+  const int pst = pc >> 3, pch = pc & 7;
   float sc[8], sh[8], sc2[8], sh2[8];
   load8<float>(pr_.sc0 + pc * 8, sc);
   load8<float>(pr_.sh0 + pc * 8, sh);
@@ -1285,13 +1297,13 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   bool first_iter = true;
   for (; t < mtiles; t += gridDim.x, slot ^= 1) {
     const int tn = t + gridDim.x;
-    // LightSelfAttention taps of this tile's two pixels, loaded before the next tile's DMA
-    float ov[2][4][8], lw[2][4];
+    // LightSelfAttention taps of this tile's pixels, loaded before the next tile's DMA
+    float ov[NITEM][4][8], lw[NITEM][4];
     if constexpr (PRO == PRO_LOCAL_ATTN) {
       const int hw = pr_.H * pr_.W;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int m = min(t * 64 + pr + 32 * h, M - 1);
+      for (int h = 0; h < NITEM; ++h) {
+        const int m = min(t * 64 + pr + RSTEP * h, M - 1);
         const int b = m / hw, rem = m - b * hw, hh = rem / pr_.W, ww = rem - hh * pr_.W;
         int h0, h1, w0, w1;
         float lh0, lh1, lw0, lw1;
@@ -1306,15 +1318,15 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
       }
     }
     // outstanding, in issue order: DMA(t), [o taps], the previous tile's prologue + FN stats +
-    // NSTORE output stores, DMA(tn): the counted wait retires everything before DMA(tn)
+    // NSTORE output stores, DMA(tn): the counted wait retires DMA(t)
     if constexpr (PRO == PRO_GATE_FUSION) {   // no loads besides the DMAs: leave the stores in flight
       if (tn < mtiles) {
         issue(tn, slot ^ 1);
         if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + 2 * NOUT + FN + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NITEM * NOUT + FN + NSTORE) : "memory");
       } else {
         if (first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * NOUT + FN + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NITEM * NOUT + FN + NSTORE) : "memory");
       }
     } else {
       if (tn < mtiles) {
@@ -1328,22 +1340,24 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     lds_barrier();
     char* img = smem + slot * SLOT;
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const int row = pr + 32 * h, m = t * 64 + row;
-      const int off = row * 128 + swz(row, pc) * 16;
+    for (int h = 0; h < NITEM; ++h) {
+      const int row = pr + RSTEP * h, m = t * 64 + row;
+      const int off = row * 128 + swz(row, pch) * 16;
+      char* i0 = img + pst * IMG + off;                 // source 0 stage of this chunk
+      char* i1 = i0 + SPS * IMG;                        // source 1
       float y[8], l[8], f[8];
-      load8<T>((const T*)(img + off), y);
-      load8<T>((const T*)(img + IMG + off), l);
+      load8<T>((const T*)i0, y);
+      load8<T>((const T*)i1, l);
       T* sink = (T*)(g_store_sink + 4 * (tid & 63));
       if constexpr (PRO == PRO_GATE_FUSION) {
         float at[8];
-        load8<T>((const T*)(img + 2 * IMG + off), at);
+        load8<T>((const T*)(i1 + SPS * IMG), at);
 #pragma unroll
         for (int q = 0; q < 8; ++q) {
           const float g = gate_sigm(y[q] * sc[q] + sh[q]);
           f[q] = g * l[q] + (1.f - g) * at[q];
         }
-        store8<T>((T*)(img + off), f);
+        store8<T>((T*)i0, f);
         // one store per item whatever m (rows past M go to the sink): a fixed count per tile
         store8<T>(m < M ? pr_.out0 + (size_t)m * C + pc * 8 : sink, f);
       } else {
@@ -1356,8 +1370,8 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
           const float v = l[q] * sc2[q] + sh2[q];
           a2[q] = gam * upv + fmaxf(v, 0.f);
         }
-        store8<T>((T*)(img + off), f);
-        store8<T>((T*)(img + IMG + off), a2);
+        store8<T>((T*)i0, f);
+        store8<T>((T*)i1, a2);
         store8<T>(m < M ? pr_.out0 + (size_t)m * C + pc * 8 : sink, f);
         store8<T>(m < M ? pr_.out1 + (size_t)m * C + pc * 8 : sink, a2);
       }
@@ -1365,39 +1379,46 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     lds_barrier();
     f32x4_t acc[4][FN];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) acc[i][0] = {0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int g = 0; g < KG; ++g) {
       Frag<T> fa[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) read_frag<T>(img + (g >> 1) * IMG, i * 16 + (lane & 15), g & 1, lane, fa[i]);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[i][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[0][g], acc[i][0], 0, 0, 0);
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
     }
     const int m0 = t * 64;
-    {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
       float s = 0.f, q = 0.f;
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int m = m0 + i * 16 + (lane >> 4) * 4 + r;
-          const float v = m < M ? acc[i][0][r] : 0.f;
+          const float v = m < M ? acc[i][j][r] : 0.f;
           s += v;
           q += v * v;
         }
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      const int n = wave * NWC + (lane & 15);
+      const int n = wave * NWC + j * 16 + (lane & 15);
       if (lane < 32) args.stats[(size_t)t * 2 * C + (lane < 16 ? 0 : C) + n] = lane < 16 ? s : q;
     }
-    {
-      const int col = wave * NWC + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int col = wave * NWC + j * 16 + (lane & 15);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r)
-          *(T*)(otile + (i * 16 + (lane >> 4) * 4 + r) * OSTR + col * 2) = f2bf(acc[i][0][r] + bias);
+          *(T*)(otile + (i * 16 + (lane >> 4) * 4 + r) * OSTR + col * 2) = f2bf(acc[i][j][r] + bias[j]);
     }
     lds_barrier();
 #pragma unroll
@@ -1667,17 +1688,17 @@ extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void
 }
 
 namespace {
-template <int PRO>
+template <int PRO, int C>
 int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
   static int occ = 0;
   if (!occ &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO>, 256, 0) != hipSuccess || occ < 1))
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO, C>, 256, 0) != hipSuccess || occ < 1))
     occ = 1;
   const int mtiles = (a.M + 63) / 64;
   const int gx = std::min(256 * occ, mtiles);
   const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
-  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + 64.0 * a.Kpad + moved * a.M * 64.0));
-  hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
+  ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + (double)C * a.Kpad + moved * a.M * C));
+  hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1686,7 +1707,8 @@ int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
 extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
                                      const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
                                      void* fused, void* y4, float* stats4, void* stream) {
-  if (M <= 0 || C != 64 || Kpad != 192 || !y3 || !sc3 || !sh3 || !local || !attn || !w4 || !fused || !y4 || !stats4)
+  if (M <= 0 || (C != 64 && C != 128) || Kpad != 3 * C || !y3 || !sc3 || !sh3 || !local || !attn || !w4 || !fused ||
+      !y4 || !stats4)
     return DFCSA_EINVAL;
   ConvGemmArgs a;
   std::memset(&a, 0, sizeof(a));
@@ -1696,7 +1718,8 @@ extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* 
   FwdPro pro;
   std::memset(&pro, 0, sizeof(pro));
   pro.sc0 = sc3; pro.sh0 = sh3; pro.out0 = (bf16_t*)fused;
-  return launch_fwd_pro<PRO_GATE_FUSION>(a, pro, (hipStream_t)stream);
+  return C == 64 ? launch_fwd_pro<PRO_GATE_FUSION, 64>(a, pro, (hipStream_t)stream)
+                 : launch_fwd_pro<PRO_GATE_FUSION, 128>(a, pro, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1,
@@ -1718,7 +1741,7 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
   pro.sc0 = sc1; pro.sh0 = sh1; pro.sc1 = sc2; pro.sh1 = sh2; pro.o = o; pro.gamma = gamma;
   pro.P = P; pro.H = H; pro.W = W;
   pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
-  return launch_fwd_pro<PRO_LOCAL_ATTN>(a, pro, (hipStream_t)stream);
+  return launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

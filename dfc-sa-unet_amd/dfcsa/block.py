@@ -37,6 +37,8 @@ from .streams import join_branch, on_branch, on_side
 # gate fusion in its A-operand prologue (dfcsa_gate_fusion_fwd).  DFCSA_DGRAD_GATE=0 selects the
 # separate GEMM + elementwise launches everywhere
 FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
+# block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
+GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
 
 def grad_of(p):
@@ -153,7 +155,7 @@ def block_forward(blk, xs, pool_size, training, dtype):
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st4 = stats(C)
-    if dtype == torch.bfloat16 and C == 64 and Kp4 == 192 and training and FUSED_DGRAD_GATE[0]:
+    if dtype == torch.bfloat16 and C in GATE_FUSION_WIDTHS and Kp4 == 3 * C and training and FUSED_DGRAD_GATE[0]:
         # the gate fusion runs in the fusion conv's A-operand prologue (dfcsa_gate_fusion_fwd)
         call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4,
              P(conv4.bias), P(fused), P(y4), P(st4), stream())

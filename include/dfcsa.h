@@ -229,10 +229,10 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
                      const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
                      const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
                      float* partial, void* stream);
-/* fusion conv forward with the gate fusion in its A-operand prologue (bf16, C == 64, Kpad == 192):
+/* fusion conv forward with the gate fusion in its A-operand prologue (bf16, C == 64 or 128, Kpad == 3C):
  * fused = g*local + (1-g)*attn, g = sigmoid(y3*sc3+sh3) (dfcsa_gate_fuse's arithmetic), stored;
- * y4 = [fused | local | attn] . w4^T + b4 (w4 = the fusion conv's [64][192] forward operand) with
- * the BatchNorm partial statistics of dfcsa_conv_gemm (stats4 [ceil(M/64)][2][64]).  Replaces the
+ * y4 = [fused | local | attn] . w4^T + b4 (w4 = the fusion conv's [C][3C] forward operand) with
+ * the BatchNorm partial statistics of dfcsa_conv_gemm (stats4 [ceil(M/64)][2][C]).  Replaces the
  * dfcsa_gate_fuse + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:102-110). */
 int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,

@@ -588,17 +588,18 @@ def test_wgrad_1x1_multisource_wide_tile(wide, B, H, W, nsrc, NI):
     assert rel(gw.view(NI, -1, 1, 1), w.grad) < 1e-5
 
 
-@pytest.mark.parametrize("M", [16 * 224 * 224, 65536 + 37, 300])
-def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M):
+@pytest.mark.parametrize("M,C", [(16 * 224 * 224, 64), (65536 + 37, 64), (300, 64), (16 * 112 * 112, 128),
+                                 (4133, 128)])
+def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M, C):
     """dfcsa_gate_fusion_fwd (fusion conv forward with the gate fusion in its A-operand prologue,
     C = 64) against the pair it replaces (dfcsa_gate_fuse, then the [fused, local, attn] GEMM with
-    BN statistics): fused, y4 and the statistics slab; ragged M."""
+    BN statistics): fused, y4 and the statistics slab; ragged M; C = 64 and 128."""
     from dfcsa._lib import call
     from dfcsa.ops import P, stream
     torch.manual_seed(13)
     bf = torch.bfloat16
     dev = "cuda"
-    C, Kp = 64, 192
+    Kp = 3 * C
     y3, loc, att = (torch.randn(M, C, device=dev).to(bf) for _ in range(3))
     sc, sh = torch.randn(C, device=dev), torch.randn(C, device=dev)
     w4 = (torch.randn(C, Kp, device=dev) * 0.1).to(bf)
