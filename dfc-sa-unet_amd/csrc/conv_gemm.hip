@@ -977,6 +977,21 @@ struct GateEpi {
 
 __device__ __forceinline__ float gate_sigm(float x) { return 1.f / (1.f + __expf(-x)); }  // = block_ew sigm
 
+// A-operand prologue (APRO, C = 64): the A image is DMA'd as [src | y] and turned into the BatchNorm
+// backward apply  dy = gamma*invstd * (dz - coef0 - xhat*coef1),  xhat = (y - mean)*invstd, with
+// dz = src (plain: dfcsa_bn_bwd_apply) or dz = src * (y*sc + sh > 0) (relu: dfcsa_bn_bwd_apply_relu),
+// in LDS; dy is stored once (the weight gradient reads it) and multiplied from LDS.
+struct ApplyPro {
+  const bf16_t* y;
+  const float* gamma;
+  const float* coef;     // [2][64]
+  const float* mean;
+  const float* invstd;
+  const float* sc;       // relu mask (nullptr: plain apply)
+  const float* sh;
+  bf16_t* dy;
+};
+
 // F.interpolate(bilinear, align_corners=False) source taps along one axis (= block_ew bilin_axis)
 __device__ __forceinline__ void bilin_axis_c(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
   float scale = (float)in / (float)out;
@@ -995,12 +1010,15 @@ __device__ __forceinline__ void bilin_axis_c(int dst, int in, int out, int& i0, 
 // of dfcsa_bwd_relu_bn, whose read of dlocal and y1 it replaces by one read of y1).
 enum { EPI_GATE = 0, EPI_ACC_RELU_BN = 1 };
 
-template <int KP, int EPI>
-__global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles) {
+template <int KP, int EPI, bool APRO = false>
+__global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles,
+                                                         const ApplyPro ap) {
   using T = bf16_t;
+  static_assert(!APRO || KP == 64, "A prologue: C = 64");
   constexpr int NWC = EPI == EPI_GATE ? 48 : 32, FN = NWC / 16, NWG = 4 * NWC;
   constexpr int KS = KP / 64, KG = KP / 32;
-  constexpr int IMG = 64 * 128, SLOT = KS * IMG;
+  constexpr int KSD = APRO ? 2 * KS : KS;   // K stages DMA'd per tile ([src | y] with the prologue)
+  constexpr int IMG = 64 * 128, SLOT = KSD * IMG;
   constexpr int OSTR = NWG * 2 + 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
   __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
@@ -1026,16 +1044,18 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
     }
   }
   const void* zero = (const void*)g_zero_page;
-  const T* a_src[2 * KS];
+  const T* a_src[2 * KSD];
 #pragma unroll
-  for (int i = 0; i < 2 * KS; ++i) {
-    const int k = (i >> 1) * 64 + cchunk * 8;
-    a_src[i] = k < K ? (const T*)args.seg[0].ptr + k : nullptr;
+  for (int i = 0; i < 2 * KSD; ++i) {
+    const int st = i >> 1;
+    const int k = (st % KS) * 64 + cchunk * 8;
+    const T* base = (APRO && st >= KS) ? ap.y : (const T*)args.seg[0].ptr;
+    a_src[i] = k < K ? base + k : nullptr;
   }
   auto issue = [&](int t, int slot) {
     char* base = smem + slot * SLOT;
 #pragma unroll
-    for (int i = 0; i < 2 * KS; ++i) {
+    for (int i = 0; i < 2 * KSD; ++i) {
       const int st = i >> 1, rb = (i & 1) * 4 + wave;
       const int m = t * 64 + rb * 8 + rsub;
       const void* src = (m < M && a_src[i]) ? (const void*)(a_src[i] + (size_t)m * K) : zero;
@@ -1054,6 +1074,18 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
   float s0[8], s1[8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) { s0[q] = 0.f; s1[q] = 0.f; }
+  // prologue constants of channel chunk ck (C = 64: the epilogue's chunk)
+  float agk[8], ak0[8], ak1[8], amu[8], ais[8], asc[8], ash[8];
+  if constexpr (APRO) {
+    load8<float>(ap.gamma + ck * 8, agk);
+    load8<float>(ap.coef + ck * 8, ak0);
+    load8<float>(ap.coef + 64 + ck * 8, ak1);
+    load8<float>(ap.mean + ck * 8, amu);
+    load8<float>(ap.invstd + ck * 8, ais);
+    if (ap.sc) { load8<float>(ap.sc + ck * 8, asc); load8<float>(ap.sh + ck * 8, ash); }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) agk[q] *= ais[q];
+  }
 
   int t = blockIdx.x;
   if (t < mtiles) issue(t, 0);
@@ -1076,12 +1108,34 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
     }
     if (tn < mtiles) {
       issue(tn, slot ^ 1);
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KSD) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();
-    const char* img = smem + slot * SLOT;
+    char* img = smem + slot * SLOT;
+    if constexpr (APRO) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int row = rr + 32 * h, m = t * 64 + row;
+        const int off = row * 128 + swz(row, ck) * 16;
+        float dz[8], y[8], dy[8];
+        load8<T>((const T*)(img + off), dz);
+        load8<T>((const T*)(img + IMG + off), y);
+        if (ap.sc) {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) dz[q] = (y[q] * asc[q] + ash[q] > 0.f) ? dz[q] : 0.f;
+        }
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          const float xh = (y[q] - amu[q]) * ais[q];
+          dy[q] = agk[q] * (dz[q] - ak0[q] - xh * ak1[q]);
+        }
+        store8<T>((T*)(img + off), dy);
+        if (m < M) store8<T>(ap.dy + (size_t)m * 64 + ck * 8, dy);
+      }
+      lds_barrier();
+    }
     f32x4_t acc[4][FN];
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1173,11 +1227,12 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
   }
 }
 
-template <int KP, int EPI>
+template <int KP, int EPI, bool APRO = false>
 int gate_occ() {
   static int occ = 0;
-  if (!occ &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP, EPI>, 256, 0) != hipSuccess || occ < 1))
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP, EPI, APRO>, 256, 0) !=
+                   hipSuccess ||
+               occ < 1))
     occ = 1;
   return occ;
 }
@@ -1185,9 +1240,9 @@ int gate_occ() {
 // workgroups of one dfcsa_dgrad_gate / _acc_relu_bn launch (= partial rows): every CU's resident
 // slots, at most one per tile
 template <int EPI>
-int dgrad_gate_grid(int M, int C) {
+int dgrad_gate_grid(int M, int C, bool apro = false) {
   const int kp = (C + 63) / 64 * 64;
-  const int occ = kp == 64 ? gate_occ<64, EPI>() : kp == 128 ? gate_occ<128, EPI>()
+  const int occ = apro ? gate_occ<64, EPI, true>() : kp == 64 ? gate_occ<64, EPI>() : kp == 128 ? gate_occ<128, EPI>()
                   : kp == 192 ? gate_occ<192, EPI>() : gate_occ<256, EPI>();
   const int mtiles = (M + 63) / 64;
   int gx = 256 * occ;
@@ -1623,16 +1678,20 @@ namespace {
 hipStream_t st_of(void* s) { return (hipStream_t)s; }
 
 template <int EPI>
-int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, hipStream_t st) {
+int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, hipStream_t st, const ApplyPro* ap = nullptr) {
   const int M = a.M, C = a.Nd, Kpad = a.Kpad;
   const int mtiles = (M + 63) / 64;
-  dim3 grid(dgrad_gate_grid<EPI>(M, C), C / 64);
-  const double moved = EPI == EPI_GATE ? 6.0 : 7.0;   // [M][C] tensors read + written besides A
+  dim3 grid(dgrad_gate_grid<EPI>(M, C, ap != nullptr), C / 64);
+  // [M][C] tensors read + written besides A (with the prologue: y read, dy written)
+  const double moved = (EPI == EPI_GATE ? 6.0 : 7.0) + (ap ? 2.0 : 0.0);
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + (double)a.N * Kpad + moved * (double)M * C));
-  if (Kpad == 64) hipLaunchKernelGGL((dgrad_gate_kernel<64, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
-  else if (Kpad == 128) hipLaunchKernelGGL((dgrad_gate_kernel<128, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
-  else if (Kpad == 192) hipLaunchKernelGGL((dgrad_gate_kernel<192, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
-  else hipLaunchKernelGGL((dgrad_gate_kernel<256, EPI>), grid, dim3(256), 0, st, a, e, mtiles);
+  ApplyPro none;
+  std::memset(&none, 0, sizeof(none));
+  if (ap) hipLaunchKernelGGL((dgrad_gate_kernel<64, EPI, true>), grid, dim3(256), 0, st, a, e, mtiles, *ap);
+  else if (Kpad == 64) hipLaunchKernelGGL((dgrad_gate_kernel<64, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
+  else if (Kpad == 128) hipLaunchKernelGGL((dgrad_gate_kernel<128, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
+  else if (Kpad == 192) hipLaunchKernelGGL((dgrad_gate_kernel<192, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
+  else hipLaunchKernelGGL((dgrad_gate_kernel<256, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1685,6 +1744,63 @@ extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void
   e.sc = sc1; e.sh = sh1; e.mean = mean1; e.invstd = invstd1;
   e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.part = partial;
   return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, st_of(stream));
+}
+
+// dy = BatchNorm-backward apply of [src | y] (relu mask when sc != nullptr) formed in the A prologue
+extern "C" int dfcsa_dgrad_gate_apply(int M, const void* dout, const void* y4, const float* gamma4,
+                                      const float* coef4, const float* mean4, const float* invstd4,
+                                      const float* sc4, const float* sh4, void* dy4, const void* w4t,
+                                      const void* y3, const float* sc3, const float* sh3, const float* mean3,
+                                      const float* invstd3, const void* local, const void* attn, void* dlocal,
+                                      void* dattn, void* dz3, float* partial, void* stream) {
+  const int C = 64, Kpad = 64;
+  if (M <= 0 || !dout || !y4 || !gamma4 || !coef4 || !mean4 || !invstd4 || !dy4 || !w4t || !y3 || !sc3 || !sh3 ||
+      !mean3 || !invstd3 || !local || !attn || !dlocal || !dattn || !dz3 || !partial || (!sc4 != !sh4))
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M; a.N = 3 * C; a.K = C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 1; a.Nd = C;
+  a.seg[0].ptr = dout;
+  a.Bw = w4t;
+  GateEpi e;
+  e.y3 = (const bf16_t*)y3; e.local = (const bf16_t*)local; e.attn = (const bf16_t*)attn;
+  e.sc = sc3; e.sh = sh3; e.mean = mean3; e.invstd = invstd3;
+  e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.dz3 = (bf16_t*)dz3; e.part = partial;
+  ApplyPro ap;
+  ap.y = (const bf16_t*)y4; ap.gamma = gamma4; ap.coef = coef4; ap.mean = mean4; ap.invstd = invstd4;
+  ap.sc = sc4; ap.sh = sh4; ap.dy = (bf16_t*)dy4;
+  return launch_gate_epi<EPI_GATE>(a, e, (hipStream_t)stream, &ap);
+}
+
+extern "C" int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void* y3, const float* gamma3,
+                                             const float* coef3, const float* mean3, const float* invstd3,
+                                             void* dy3, const void* w3t, const void* y1, const float* sc1,
+                                             const float* sh1, const float* mean1, const float* invstd1,
+                                             void* dlocal, void* dattn, float* partial, void* stream) {
+  const int C = 64, Kpad = 64;
+  if (M <= 0 || !dz3 || !y3 || !gamma3 || !coef3 || !mean3 || !invstd3 || !dy3 || !w3t || !y1 || !sc1 || !sh1 ||
+      !mean1 || !invstd1 || !dlocal || !dattn || !partial)
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = M; a.N = 2 * C; a.K = C; a.Kpad = Kpad; a.Cseg = C; a.nseg = 1; a.Nd = C;
+  a.seg[0].ptr = dz3;
+  a.Bw = w3t;
+  GateEpi e;
+  std::memset(&e, 0, sizeof(e));
+  e.y3 = (const bf16_t*)y1;
+  e.sc = sc1; e.sh = sh1; e.mean = mean1; e.invstd = invstd1;
+  e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.part = partial;
+  ApplyPro ap;
+  std::memset(&ap, 0, sizeof(ap));
+  ap.y = (const bf16_t*)y3; ap.gamma = gamma3; ap.coef = coef3; ap.mean = mean3; ap.invstd = invstd3;
+  ap.dy = (bf16_t*)dy3;
+  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, (hipStream_t)stream, &ap);
+}
+
+extern "C" int dfcsa_dgrad_apply_parts(int M, int epi) {
+  if (M <= 0) return DFCSA_EINVAL;
+  return epi == 0 ? dgrad_gate_grid<EPI_GATE>(M, 64, true) : dgrad_gate_grid<EPI_ACC_RELU_BN>(M, 64, true);
 }
 
 namespace {

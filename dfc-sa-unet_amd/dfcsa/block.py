@@ -37,6 +37,8 @@ from .streams import join_branch, on_branch, on_side
 # gate fusion in its A-operand prologue (dfcsa_gate_fusion_fwd).  DFCSA_DGRAD_GATE=0 selects the
 # separate GEMM + elementwise launches everywhere
 FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
+# C == 64: BatchNorm-backward applies in the dgrad GEMMs' A prologue (DFCSA_APPLY_PROLOGUE=0: separate)
+APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "1") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -252,18 +254,33 @@ def block_backward(blk, s, dout, need_dx, dtype):
          P(s.res), P(blk.res_scale), None, P(dres), P(part), stream())
     coef = ops.bn_bwd_finalize(part, nte, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
                                extra=grad_of(blk.res_scale))
-    dy4 = ops.bn_bwd_apply_relu(dtype, dout, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
-    # fusion conv: dW4 (side stream) and d[fused, local, attn]
-    with on_side(dev, dy4, s.fused, s.local, s.attn):
-        ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                            [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
     dlocal = torch.empty_like(s.y4)
     dattn = torch.empty_like(s.y4)
     dz3 = torch.empty_like(s.y3)
+    fused = dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]
+    # C == 64: the BatchNorm-backward applies (dy4, dy3) run in the A-operand prologue of the fused
+    # input-gradient GEMMs below (the conv-bias gradient is the analytic zero there)
+    apro = fused and C == 64 and not ops.NUMERIC_BN_BIAS_GRAD and APPLY_PROLOGUE[0]
     # ---- gate: s = sigmoid(bn3 y3); fused = s*local + (1-s)*attn ----
-    if dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]:
+    if apro:
+        # dy4 in the prologue, the gate backward in the epilogue of the fusion conv's dgrad GEMM
+        dy4 = torch.empty_like(dout)
+        npart = _lib.LIB.dfcsa_dgrad_apply_parts(M, 0)
+        part = torch.empty(npart * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_dgrad_gate_apply", M, P(dout), P(s.y4), P(bn4m.weight), P(coef), P(bn4.mean), P(bn4.invstd),
+             P(bn4.scale), P(bn4.shift), P(dy4), P(W4t), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+    else:
+        dy4 = ops.bn_bwd_apply_relu(dtype, dout, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
+    # fusion conv: dW4 (side stream) and d[fused, local, attn]
+    with on_side(dev, dy4, s.fused, s.local, s.attn):
+        ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                            [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
+    if apro:
+        del dy4
+    elif fused:
         # the gate backward runs in the epilogue of the fusion conv's input-gradient GEMM
         # (dfused never stored; dfcsa_dgrad_gate)
         npart = _lib.LIB.dfcsa_dgrad_gate_parts(M, C)
@@ -281,14 +298,26 @@ def block_backward(blk, s, dout, need_dx, dtype):
              P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
         del dfused
     coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
-    dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
-    del dz3
+    W3t = s.pk["W3t"]
+    fused_bn1 = fused
+    if apro:
+        # dy3 in the prologue, the accumulate + BN1 sums in the epilogue of the gate conv's dgrad GEMM
+        dy3 = torch.empty_like(dz3)
+        npart1 = _lib.LIB.dfcsa_dgrad_apply_parts(M, 1)
+        part1 = torch.empty(npart1 * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_dgrad_acc_relu_bn_apply", M, P(dz3), P(s.y3), P(bn3m.weight), P(coef), P(bn3.mean),
+             P(bn3.invstd), P(dy3), P(W3t), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
+             P(dlocal), P(dattn), P(part1), stream())
+        del dz3
+    else:
+        dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
+        del dz3
     with on_side(dev, dy3):
         ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                             [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
-    W3t = s.pk["W3t"]
-    fused_bn1 = dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]
-    if fused_bn1:
+    if apro:
+        pass
+    elif fused_bn1:
         # accumulate GEMM with the local branch's BN1-backward sums in its epilogue
         npart1 = _lib.LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
         part1 = torch.empty(npart1 * 2 * C, device=dev, dtype=f32)

@@ -246,6 +246,22 @@ int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const 
                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,
                               const float* gamma, const void* w3, int Kpad, const float* b3, void* local,
                               void* attn, void* y3, float* stats3, void* stream);
+/* dfcsa_dgrad_gate / dfcsa_dgrad_acc_relu_bn at C == 64 with the BatchNorm-backward apply of their
+ * A operand in a prologue: dy4 = gamma4*invstd4*(dz4 - coef4[0] - xh4*coef4[1]) with dz4 =
+ * dout*(y4*sc4+sh4 > 0) (dfcsa_bn_bwd_apply_relu; sc4 = sh4 = NULL: dz4 = dout) and dy3 likewise from
+ * dz3 (dfcsa_bn_bwd_apply), formed in LDS from the DMA'd [dout | y4] / [dz3 | y3] image, stored
+ * once (dy4, dy3: the weight gradients read them) and multiplied.  The conv-bias gradient is the
+ * analytic zero (no bias sums).  partial rows: dfcsa_dgrad_apply_parts(M, 0 = gate / 1 = acc). */
+int dfcsa_dgrad_apply_parts(int M, int epi);
+int dfcsa_dgrad_gate_apply(int M, const void* dout, const void* y4, const float* gamma4, const float* coef4,
+                           const float* mean4, const float* invstd4, const float* sc4, const float* sh4, void* dy4,
+                           const void* w4t, const void* y3, const float* sc3, const float* sh3, const float* mean3,
+                           const float* invstd3, const void* local, const void* attn, void* dlocal, void* dattn,
+                           void* dz3, float* partial, void* stream);
+int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void* y3, const float* gamma3, const float* coef3,
+                                  const float* mean3, const float* invstd3, void* dy3, const void* w3t,
+                                  const void* y1, const float* sc1, const float* sh1, const float* mean1,
+                                  const float* invstd1, void* dlocal, void* dattn, float* partial, void* stream);
 /* gate-conv input gradient added into [dlocal | dattn] (bf16, C % 64 == 0, C <= 256): dlocal +=
  * (dy3 . W3t)[:, :C], dattn += (dy3 . W3t)[:, C:] (W3t = the [2C][Kpad] dgrad operand of the gate
  * conv; same bf16 roundings as dfcsa_conv_gemm's accumulate mode), and on the final dlocal the

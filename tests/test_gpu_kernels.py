@@ -656,3 +656,55 @@ def test_local_attn_gate_fwd_equals_merge_plus_gemm(B, H, W, P):
     assert rel(a1, a0) < 1e-6
     assert rel(y31, y30) < 2e-3
     assert rel(st1, st0) < 1e-4
+
+
+@pytest.mark.parametrize("M", [16 * 224 * 224, 65536 + 37, 300])
+def test_dgrad_apply_prologue_equals_apply_plus_gemm(M):
+    """C = 64: dfcsa_dgrad_gate_apply / dfcsa_dgrad_acc_relu_bn_apply (the BatchNorm-backward apply of
+    the A operand formed in the GEMM's prologue) against dfcsa_bn_bwd_apply_relu / _apply followed by
+    dfcsa_dgrad_gate / dfcsa_dgrad_acc_relu_bn: dy, the GEMM outputs and the partial sums."""
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P, stream
+    torch.manual_seed(15)
+    bf = torch.bfloat16
+    dev = "cuda"
+    C = Kp = 64
+    src, y, y3, loc, att, y1 = (torch.randn(M, C, device=dev).to(bf) for _ in range(6))
+    gamma, k, mu, sc, sh, mu3, sc3, sh3 = (torch.randn(C if i != 1 else 3 * C, device=dev) for i in range(8))
+    istd, istd3 = torch.rand(C, device=dev) + 0.5, torch.rand(C, device=dev) + 0.5
+    w4t = (torch.randn(3 * C, Kp, device=dev) * 0.1).to(bf)
+    w3t = (torch.randn(2 * C, Kp, device=dev) * 0.1).to(bf)
+    T = ops.dt(bf)
+    # gate: reference path
+    dy0 = torch.empty(M, C, device=dev, dtype=bf)
+    call("dfcsa_bn_bwd_apply_relu", T, M, C, P(src), P(y), P(sc), P(sh), P(mu), P(istd), P(gamma), P(k), P(dy0), None,
+         stream())
+    n0 = LIB.dfcsa_dgrad_gate_parts(M, C)
+    dl0, da0, dz0 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
+    p0 = torch.empty(n0 * 2 * C, device=dev)
+    call("dfcsa_dgrad_gate", M, C, P(dy0), P(w4t), Kp, P(y3), P(sc3), P(sh3), P(mu3), P(istd3), P(loc), P(att),
+         P(dl0), P(da0), P(dz0), P(p0), stream())
+    n1 = LIB.dfcsa_dgrad_apply_parts(M, 0)
+    dy1, dl1, da1, dz1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(4))
+    p1 = torch.empty(n1 * 2 * C, device=dev)
+    call("dfcsa_dgrad_gate_apply", M, P(src), P(y), P(gamma), P(k), P(mu), P(istd), P(sc), P(sh), P(dy1), P(w4t),
+         P(y3), P(sc3), P(sh3), P(mu3), P(istd3), P(loc), P(att), P(dl1), P(da1), P(dz1), P(p1), stream())
+    # acc: reference path (plain apply of dz3 = src)
+    dyb0 = torch.empty(M, C, device=dev, dtype=bf)
+    call("dfcsa_bn_bwd_apply", T, M, C, P(src), P(y), P(mu), P(istd), P(gamma), P(k), P(dyb0), None, stream())
+    dlb0, dab0 = loc.clone(), att.clone()
+    m0 = LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
+    q0 = torch.empty(m0 * 2 * C, device=dev)
+    call("dfcsa_dgrad_acc_relu_bn", M, C, P(dyb0), P(w3t), Kp, P(y1), P(sc3), P(sh3), P(mu3), P(istd3), P(dlb0),
+         P(dab0), P(q0), stream())
+    m1 = LIB.dfcsa_dgrad_apply_parts(M, 1)
+    dyb1 = torch.empty(M, C, device=dev, dtype=bf)
+    dlb1, dab1 = loc.clone(), att.clone()
+    q1 = torch.empty(m1 * 2 * C, device=dev)
+    call("dfcsa_dgrad_acc_relu_bn_apply", M, P(src), P(y), P(gamma), P(k), P(mu), P(istd), P(dyb1), P(w3t), P(y1),
+         P(sc3), P(sh3), P(mu3), P(istd3), P(dlb1), P(dab1), P(q1), stream())
+    torch.cuda.synchronize()
+    for a, b in ((dy1, dy0), (dl1, dl0), (da1, da0), (dz1, dz0), (dyb1, dyb0), (dlb1, dlb0), (dab1, dab0)):
+        assert rel(a, b) < 1e-5
+    assert rel(p1.view(n1, 2, C).double().sum(0), p0.view(n0, 2, C).double().sum(0)) < 1e-5
+    assert rel(q1.view(m1, 2, C).double().sum(0), q0.view(m0, 2, C).double().sum(0)) < 1e-5
