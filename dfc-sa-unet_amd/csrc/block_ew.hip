@@ -579,6 +579,189 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
 }
 
 // ---------------------------------------------------------------------------------------------
+// Encoder block output fused with the 2x2 max-pool that follows it (reference
+// models/unet_dfc_sa_res.py:113-114 then :165-172 MaxPool2d(2, 2); even H and W):
+//   forward:  out = relu(bn4 y4) + res_scale*res for the 4 pixels of a window (stored: it is the
+//             decoder's skip) and pooled = max over the window of the stored (rounded) values,
+//             first maximum / NaN wins as ATen -- one pass instead of block_out + maxpool;
+//   backward: dout = dskip + maxpool_bwd(dpooled) (ATen's routing to the first maximum of the
+//             saved out) formed per window, stored, and the dfcsa_bwd_block_out stage on it
+//             (dres = res_scale*dout; sums [dz4, dz4*xh4, dout*res]) -- one pass instead of the
+//             pooling-gradient read-modify-write + the block-output backward.
+// Thread = (pooled pixel, 8-channel chunk); the backward's per-channel sums are reduced per
+// workgroup tile of pooled pixels as in ew_red_kernel (deterministic).
+// ---------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void __launch_bounds__(256) block_out_pool_kernel(int B, int H, int W, int C, const T* __restrict__ y4,
+                                                             const float* __restrict__ sc4, const float* __restrict__ sh4,
+                                                             const T* __restrict__ res, const float* __restrict__ rs,
+                                                             T* __restrict__ out, T* __restrict__ pooled) {
+  const int Ho = H / 2, Wo = W / 2, cpp = C >> 3;
+  const int64_t total = (int64_t)B * Ho * Wo * cpp;
+  const float scal = *rs;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ck = (int)(e % cpp);
+    int64_t p = e / cpp;
+    const int ow = (int)(p % Wo);
+    p /= Wo;
+    const int oh = (int)(p % Ho);
+    const int b = (int)(p / Ho);
+    float sc[8], sh[8];
+    ld8f(sc4 + ck * 8, sc);
+    ld8f(sh4 + ck * 8, sh);
+    Raw<T> ry[4], rr[4];
+    size_t off[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      off[t] = ((size_t)(b * H + 2 * oh + (t >> 1)) * W + 2 * ow + (t & 1)) * C + ck * 8;
+      ry[t] = ldraw(y4 + off[t]);
+      rr[t] = ldraw(res + off[t]);
+    }
+    float best[8];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      float y[8], r[8], o[8];
+      unraw(ry[t], y);
+      unraw(rr[t], r);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) o[q] = fmaxf(y[q] * sc[q] + sh[q], 0.f) + scal * r[q];
+      store8<T>(out + off[t], o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float v = ElemTraits<T>::to_f(ElemTraits<T>::from_f(o[q]));   // the stored value
+        if (t == 0 || v > best[q] || isnan(v)) best[q] = v;
+      }
+    }
+    store8<T>(pooled + ((size_t)(b * Ho + oh) * Wo + ow) * C + ck * 8, best);
+  }
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) bwd_block_out_pool_kernel(const EwArgs a, const T* __restrict__ xo,
+                                                                 const T* __restrict__ dpool, T* __restrict__ dout) {
+  // a: B, H, W (full resolution), C; a0 = dskip (nullable), a1 = y4, a2 = res; sc/sh/mean/invstd (BN4);
+  // scalar = res_scale; o1 = dres; partial [ntiles][3][C]; tile_px = pooled pixels per workgroup
+  constexpr int NS = 3;
+  const int cpp = a.C >> 3;
+  const int pl = 256 / cpp;
+  const int tid = threadIdx.x;
+  const int lane_px = tid / cpp, ck = tid - lane_px * cpp;
+  const int c0 = ck * 8;
+  const bool active = lane_px < pl;
+  const int Ho = a.H / 2, Wo = a.W / 2;
+  const int Mp = a.B * Ho * Wo;
+  float acc[NS][8];
+#pragma unroll
+  for (int s = 0; s < NS; ++s)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[s][q] = 0.f;
+  const T* __restrict__ DS = (const T*)a.a0;
+  const T* __restrict__ Y = (const T*)a.a1;
+  const T* __restrict__ R = (const T*)a.a2;
+  T* __restrict__ DR = (T*)a.o1;
+  const int pbeg = blockIdx.x * a.tile_px;
+  const int pend = min(Mp, pbeg + a.tile_px);
+  if (active) {
+    float sc[8], sh[8], mu[8], is[8];
+    ld8f(a.sc + c0, sc); ld8f(a.sh + c0, sh); ld8f(a.mean + c0, mu); ld8f(a.invstd + c0, is);
+    const float scal = *a.scalar;
+    for (int pp = pbeg + lane_px; pp < pend; pp += pl) {
+      const int ow = pp % Wo, t1 = pp / Wo, oh = t1 % Ho, b = t1 / Ho;
+      size_t off[4];
+      Raw<T> rx[4], ry[4], rr[4], rs[4];
+      Raw<T> rg = ldraw(dpool + (size_t)pp * a.C + c0);
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        off[t] = ((size_t)(b * a.H + 2 * oh + (t >> 1)) * a.W + 2 * ow + (t & 1)) * a.C + c0;
+        rx[t] = ldraw(xo + off[t]);
+        ry[t] = ldraw(Y + off[t]);
+        rr[t] = ldraw(R + off[t]);
+        if (DS) rs[t] = ldraw(DS + off[t]);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      float best[8], g[8];
+      int arg[8];
+      unraw(rx[0], best);
+      unraw(rg, g);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) arg[q] = 0;
+#pragma unroll
+      for (int t = 1; t < 4; ++t) {
+        float v[8];
+        unraw(rx[t], v);
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          if (v[q] > best[q] || isnan(v[q])) { best[q] = v[q]; arg[q] = t; }
+      }
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        float d[8], y[8], r[8], dr[8];
+        if (DS) unraw(rs[t], d);
+        else {
+#pragma unroll
+          for (int q = 0; q < 8; ++q) d[q] = 0.f;
+        }
+        unraw(ry[t], y);
+        unraw(rr[t], r);
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          // dskip + pooled gradient at the window's first maximum, rounded as it is stored
+          d[q] = ElemTraits<T>::to_f(ElemTraits<T>::from_f(d[q] + ((arg[q] == t) ? g[q] : 0.f)));
+          const float z = (y[q] * sc[q] + sh[q] > 0.f) ? d[q] : 0.f;
+          dr[q] = scal * d[q];
+          acc[0][q] += z;
+          acc[1][q] += z * ((y[q] - mu[q]) * is[q]);
+          acc[2][q] += d[q] * r[q];
+        }
+        store8<T>(dout + off[t], d);
+        store8<T>(DR + off[t], dr);
+      }
+    }
+  }
+  __shared__ float red[4 * 3 * 512];
+  float* outp = a.partial + (size_t)blockIdx.x * NS * a.C;
+  const bool pow2 = (cpp & (cpp - 1)) == 0;
+  if (pow2 && cpp <= 64) {
+    const int lane = tid & 63, wave = tid >> 6;
+#pragma unroll
+    for (int s = 0; s < NS; ++s)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float v = acc[s][q];
+        for (int o = cpp; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+        acc[s][q] = v;
+      }
+    if (lane < cpp)
+#pragma unroll
+      for (int s = 0; s < NS; ++s)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[(wave * NS + s) * a.C + ck * 8 + q] = acc[s][q];
+    __syncthreads();
+    for (int e = tid; e < NS * a.C; e += 256) {
+      const int s = e / a.C, c = e - s * a.C;
+      outp[e] = (red[(0 * NS + s) * a.C + c] + red[(1 * NS + s) * a.C + c]) +
+                (red[(2 * NS + s) * a.C + c] + red[(3 * NS + s) * a.C + c]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int s = 0; s < NS; ++s) {
+    if (active) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) red[(lane_px * cpp + ck) * 8 + q] = acc[s][q];
+    }
+    __syncthreads();
+    for (int c = tid; c < a.C; c += 256) {
+      const int k = c >> 3, q = c & 7;
+      float v = 0.f;
+      for (int p2 = 0; p2 < pl; ++p2) v += red[(p2 * cpp + k) * 8 + q];
+      outp[s * a.C + c] = v;
+    }
+    __syncthreads();
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // Column sums of per-tile partial rows, fused with the per-channel finalisation that consumes them
 // (BatchNorm statistics, BatchNorm-backward coefficients, bias gradients): one launch instead of a
 // row-reduction launch + a finalize launch.  grid (ceil(C/64), R), 1024 threads = 16 parts x 64
@@ -1188,6 +1371,59 @@ extern "C" int dfcsa_rows_reduce(const float* src, int T, int rowlen, float* dst
 extern "C" int dfcsa_sum_to_scalar(const float* x, int n, float* out, void* stream) {
   if (n <= 0) return DFCSA_EINVAL;
   launch_sum_scalar(x, n, out, (hipStream_t)stream);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+// pooled pixels per workgroup tile of dfcsa_bwd_block_out_pool (a quarter of the elementwise tile)
+static int pool_tile(int C) { int t = tile_px(C) / 4; const int pl = 256 / (C / 8 > 0 ? C / 8 : 1); return t < pl ? pl : t; }
+
+extern "C" int dfcsa_block_out_pool(int dtype, int B, int H, int W, int C, const void* y4, const float* sc4,
+                                    const float* sh4, const void* res, const float* res_scale, void* out,
+                                    void* pooled, void* stream) {
+  if (C % 8 || C > 2048 || (H & 1) || (W & 1) || B <= 0 || H <= 0 || W <= 0 || !y4 || !sc4 || !sh4 || !res ||
+      !res_scale || !out || !pooled)
+    return DFCSA_EINVAL;
+  const int64_t n = (int64_t)B * (H / 2) * (W / 2) * (C / 8);
+  const int blocks = (int)std::min<int64_t>((n + 255) / 256, 65535);
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(block_out_pool_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, B, H, W, C, (const bf16_t*)y4, sc4,
+                       sh4, (const bf16_t*)res, res_scale, (bf16_t*)out, (bf16_t*)pooled);
+  else
+    hipLaunchKernelGGL(block_out_pool_kernel<float>, dim3(blocks), dim3(256), 0, st, B, H, W, C, (const float*)y4, sc4,
+                       sh4, (const float*)res, res_scale, (float*)out, (float*)pooled);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_bwd_block_out_pool_ntiles(int B, int H, int W, int C) {
+  if (C <= 0 || (H & 1) || (W & 1)) return DFCSA_EINVAL;
+  const int Mp = B * (H / 2) * (W / 2), t = pool_tile(C);
+  return (Mp + t - 1) / t;
+}
+
+extern "C" int dfcsa_bwd_block_out_pool(int dtype, int B, int H, int W, int C, const void* dskip, const void* out,
+                                        const void* dpooled, const void* y4, const float* sc4, const float* sh4,
+                                        const float* mean4, const float* invstd4, const void* res,
+                                        const float* res_scale, void* dout, void* dres, float* partial, void* stream) {
+  if (C % 8 || C > 2048 || (H & 1) || (W & 1) || B <= 0 || !out || !dpooled || !y4 || !sc4 || !sh4 || !mean4 ||
+      !invstd4 || !res || !res_scale || !dout || !dres || !partial)
+    return DFCSA_EINVAL;
+  EwArgs a = zargs(B * H * W, C);
+  a.B = B; a.H = H; a.W = W;
+  a.a0 = dskip; a.a1 = y4; a.a2 = res; a.sc = sc4; a.sh = sh4; a.mean = mean4; a.invstd = invstd4;
+  a.scalar = res_scale; a.o1 = dres; a.partial = partial;
+  a.tile_px = pool_tile(C);
+  const int Mp = B * (H / 2) * (W / 2);
+  const int blocks = (Mp + a.tile_px - 1) / a.tile_px;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(bwd_block_out_pool_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, a, (const bf16_t*)out,
+                       (const bf16_t*)dpooled, (bf16_t*)dout);
+  else
+    hipLaunchKernelGGL(bwd_block_out_pool_kernel<float>, dim3(blocks), dim3(256), 0, st, a, (const float*)out,
+                       (const float*)dpooled, (float*)dout);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

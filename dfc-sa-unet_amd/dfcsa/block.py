@@ -37,6 +37,8 @@ from .streams import join_branch, on_branch, on_side
 # gate fusion in its A-operand prologue (dfcsa_gate_fusion_fwd).  DFCSA_DGRAD_GATE=0 selects the
 # separate GEMM + elementwise launches everywhere
 FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
+# encoder blocks: the 2x2 max-pool fused into the block-output pass and its backward (DFCSA_POOL_FUSION=0: separate)
+POOL_FUSION = [os.environ.get("DFCSA_POOL_FUSION", "1") == "1"]
 # C == 64: BatchNorm-backward applies in the dgrad GEMMs' A prologue (DFCSA_APPLY_PROLOGUE=0: separate)
 APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "1") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
@@ -68,7 +70,9 @@ class _Saved:
     pass
 
 
-def block_forward(blk, xs, pool_size, training, dtype):
+def block_forward(blk, xs, pool_size, training, dtype, pool=False):
+    """Returns (out, saved), or with pool=True ((pooled, out), saved): the encoder's 2x2 max-pool
+    of the block output (reference :165-172) fused into the block-output pass when H, W are even."""
     B, H, W, Cs = xs[0].shape
     nsrc = len(xs)
     Cin_p = nsrc * Cs
@@ -168,8 +172,17 @@ def block_forward(blk, xs, pool_size, training, dtype):
                       C, bias=conv4.bias, stats=st4)
     bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt, C, C, M, training)
     out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    call("dfcsa_block_out", dt(dtype), M, C, P(y4), P(bn4.scale), P(bn4.shift), P(res), P(blk.res_scale), P(out),
-         stream())
+    pooled_out = None
+    if pool:
+        pooled_out = torch.empty((B, H // 2, W // 2, C), dtype=dtype, device=dev)
+    if pool and H % 2 == 0 and W % 2 == 0 and POOL_FUSION[0]:
+        call("dfcsa_block_out_pool", dt(dtype), B, H, W, C, P(y4), P(bn4.scale), P(bn4.shift), P(res),
+             P(blk.res_scale), P(out), P(pooled_out), stream())
+    else:
+        call("dfcsa_block_out", dt(dtype), M, C, P(y4), P(bn4.scale), P(bn4.shift), P(res), P(blk.res_scale),
+             P(out), stream())
+        if pool:
+            call("dfcsa_maxpool2_fwd", dt(dtype), B, H, W, C, P(out), P(pooled_out), stream())
 
     s.shape = (B, H, W, C, Cs, nsrc, Cin_p, Cin_real, has_res, Pp, Cq, J, N)
     s.xs = xs
@@ -177,6 +190,9 @@ def block_forward(blk, xs, pool_size, training, dtype):
     s.bn = (bn1, bn2, bn3, bn4)
     s.pooled, s.qkv, s.A, s.o, s.Wqkv = pooled, qkv, A, o, Wqkv
     s.pk = pk
+    if pool:
+        s.out = out   # the max-pool's argmax source in backward
+        return (pooled_out, out), s
     return out, s
 
 
@@ -230,7 +246,9 @@ def _build_lsa_packs(ps, lsa):
         ps.transpose(Wq, 0, 0, J, C, "WqkvT", (C, J))
 
 
-def block_backward(blk, s, dout, need_dx, dtype):
+def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
+    """pool_grads = (dpooled, dskip) for a block run with pool=True (dout unused): the block-output
+    gradient is dskip + the max-pool backward of dpooled, formed in the block-output backward pass."""
     B, H, W, C, Cs, nsrc, Cin_p, Cin_real, has_res, Pp, Cq, J, N = s.shape
     conv1, bn1m = blk.conv_branch[0], blk.conv_branch[1]
     conv2, bn2m = blk.attn_branch[0], blk.attn_branch[1]
@@ -239,20 +257,39 @@ def block_backward(blk, s, dout, need_dx, dtype):
     conv4, bn4m = blk.fusion_conv[0], blk.fusion_conv[1]
     bn1, bn2, bn3, bn4 = s.bn
     M = B * H * W
-    dev = dout.device
+    dev = s.y4.device
     T = dt(dtype)
     grid, hw = (B, H, W), (H, W)
     nte = ops.ntiles_ew(M, C)
     f32 = torch.float32
-    dout = dout.contiguous()
-
-    # ---- block output: relu(bn4 y4) + res_scale * res ----
-    # (dz4 = relu'(bn4 y4) * dout is not materialised: the apply recomputes it)
+    nbo = nte
     dres = torch.empty_like(s.y4)
-    part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
-    call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean), P(bn4.invstd),
-         P(s.res), P(blk.res_scale), None, P(dres), P(part), stream())
-    coef = ops.bn_bwd_finalize(part, nte, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
+    if pool_grads is not None:
+        dpool, dskip = pool_grads
+        dskip = dskip.contiguous() if dskip is not None else None
+        if dpool is not None and H % 2 == 0 and W % 2 == 0 and POOL_FUSION[0]:
+            # ---- max-pool backward + block output backward in one pass ----
+            dout = torch.empty_like(s.y4)
+            nbo = _lib.LIB.dfcsa_bwd_block_out_pool_ntiles(B, H, W, C)
+            part = torch.empty(nbo * 3 * C, device=dev, dtype=f32)
+            call("dfcsa_bwd_block_out_pool", T, B, H, W, C, P(dskip), P(s.out), P(dpool.contiguous()), P(s.y4),
+                 P(bn4.scale), P(bn4.shift), P(bn4.mean), P(bn4.invstd), P(s.res), P(blk.res_scale), P(dout),
+                 P(dres), P(part), stream())
+        else:
+            dout = dskip if dskip is not None else torch.zeros_like(s.y4)
+            if dpool is not None:
+                call("dfcsa_maxpool2_bwd", T, B, H, W, C, P(s.out), P(dpool.contiguous()), P(dout), stream())
+            dpool = None
+    else:
+        dpool = None
+        dout = dout.contiguous()
+    if dpool is None:
+        # ---- block output: relu(bn4 y4) + res_scale * res ----
+        # (dz4 = relu'(bn4 y4) * dout is not materialised: the apply recomputes it)
+        part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
+        call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean),
+             P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), P(part), stream())
+    coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
                                extra=grad_of(blk.res_scale))
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
@@ -503,6 +540,31 @@ class LSAFunction(torch.autograd.Function):
 
 def block_params(blk):
     return [p for p in blk.parameters()]
+
+
+class DFCBlockPoolFunction(torch.autograd.Function):
+    """DFCBlockFunction for an encoder block followed by MaxPool2d(2,2) (reference :165-172):
+    returns (pooled, out) -- out is the decoder skip -- like MaxPoolFork after the block."""
+
+    @staticmethod
+    def forward(ctx, blk, pool_size, dtype, nsrc, *args):
+        xs = list(args[:nsrc])
+        training = blk.training
+        (pooled, out), saved = block_forward(blk, xs, pool_size, training, dtype, pool=True)
+        ctx.blk, ctx.saved, ctx.dtype, ctx.nsrc, ctx.nparams = blk, saved, dtype, nsrc, len(args) - nsrc
+        ctx.training = training
+        return pooled, out
+
+    @staticmethod
+    def backward(ctx, dpooled, dskip):
+        if not ctx.training:
+            raise_eval_backward()
+        need_dx = any(ctx.needs_input_grad[4:4 + ctx.nsrc])
+        dxs = block_backward(ctx.blk, ctx.saved, None, need_dx, ctx.dtype, pool_grads=(dpooled, dskip))
+        ctx.saved = None
+        notify_grads_ready(ctx.blk)
+        grads = list(dxs) if dxs is not None else [None] * ctx.nsrc
+        return (None, None, None, None, *grads, *([None] * ctx.nparams))
 
 
 class DFCBlockFunction(torch.autograd.Function):

@@ -17,7 +17,7 @@ import torch.nn as nn
 
 import dfcsa
 from dfcsa import packs
-from dfcsa.block import DFCBlockFunction, LSAFunction
+from dfcsa.block import DFCBlockFunction, DFCBlockPoolFunction, LSAFunction
 from dfcsa.flat import FlatParams
 from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPoolFork, ResizeBilinear
 from dfcsa.ops import rup
@@ -90,6 +90,10 @@ class DynamicFusionConvAttnBlock(nn.Module):
         """xs: list of NHWC sources whose channel concat is the block input (skip concat
         never materialised)."""
         return DFCBlockFunction.apply(self, self.pool_size, dtype, len(xs), *xs, *self.parameters())
+
+    def forward_nhwc_pool(self, xs, dtype):
+        """Encoder use: (MaxPool2d(2,2)(out), out) with the pooling fused into the block."""
+        return DFCBlockPoolFunction.apply(self, self.pool_size, dtype, len(xs), *xs, *self.parameters())
 
     def forward(self, x):
         """Standalone use on NCHW fp32 input (returns NCHW fp32)."""
@@ -181,12 +185,18 @@ class UNetDFCSA(nn.Module):
         if getattr(self, "_plan_flat", None) is not flat:  # parameter storage changed: stale plan
             self._dfcsa_plan, self._plan_flat = None, flat
         planned = packs.sync_model_plan(self)  # one launch packs every conv operand of the model
-        fork = lambda t: MaxPoolFork.apply(t, dt)  # noqa: E731  (pooled, skip alias)
         h = _nchw_to_nhwc(x, dt)
-        p1, d1 = fork(self.down1.forward_nhwc([h], dt))
-        p2, d2 = fork(self.down2.forward_nhwc([p1], dt))
-        p3, d3 = fork(self.down3.forward_nhwc([p2], dt))
-        p4, d4 = fork(self.down4.forward_nhwc([p3], dt))
+
+        def enc(blk, t):
+            """encoder block + MaxPool2d(2,2) (:165-172) -> (pooled, skip); DFC blocks fuse the pooling
+            into their block-output pass, other (ablation) blocks pool through MaxPoolFork"""
+            if isinstance(blk, DynamicFusionConvAttnBlock):
+                return blk.forward_nhwc_pool([t], dt)
+            return MaxPoolFork.apply(blk.forward_nhwc([t], dt), dt)
+        p1, d1 = enc(self.down1, h)
+        p2, d2 = enc(self.down2, p1)
+        p3, d3 = enc(self.down3, p2)
+        p4, d4 = enc(self.down4, p3)
         u = self.bottleneck.forward_nhwc([p4], dt)
         for up, block, skip in ((self.up4, self.up_conv4, d4), (self.up3, self.up_conv3, d3),
                                 (self.up2, self.up_conv2, d2), (self.up1, self.up_conv1, d1)):

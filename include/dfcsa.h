@@ -197,6 +197,12 @@ int dfcsa_gate_fuse(int dtype, int M, int C, const void* y3, const float* sc3, c
 int dfcsa_block_out(int dtype, int M, int C, const void* y4, const float* sc4, const float* sh4,
                     const void* res, const float* res_scale, void* out, void* stream);
 
+/* encoder block output fused with the 2x2 max-pool after it (even H, W): out = relu(bn4(y4)) +
+ * res_scale*res (stored: the decoder skip) and pooled = MaxPool2d(2,2)(out) (first maximum, NaN
+ * wins) in one pass (reference models/unet_dfc_sa_res.py:113-114, :165-172) */
+int dfcsa_block_out_pool(int dtype, int B, int H, int W, int C, const void* y4, const float* sc4,
+                         const float* sh4, const void* res, const float* res_scale, void* out, void* pooled,
+                         void* stream);
 /* ------------------------------------------------------------------------------------------
  * Backward elementwise + per-channel reductions.  Partial slabs: [ntiles][nsum][C] fp32 with
  * ntiles = dfcsa_ew_ntiles(M, C); dz = gradient at the BatchNorm output, xh = normalised input.
@@ -207,6 +213,14 @@ int dfcsa_ew_ntiles(int M, int C);
 int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, const void* y4, const float* sc4,
                         const float* sh4, const float* mean4, const float* invstd4, const void* res,
                         const float* res_scale, void* dz4, void* dres, float* partial, void* stream);
+/* its backward: dout = dskip (NULL: 0) + maxpool_bwd(dpooled) routed by the saved `out`, stored,
+ * then dfcsa_bwd_block_out on it (dres = res_scale*dout; sums [dz4, dz4*xh4, dout*res]) in one
+ * pass; partial [dfcsa_bwd_block_out_pool_ntiles(B, H, W, C)][3][C] */
+int dfcsa_bwd_block_out_pool_ntiles(int B, int H, int W, int C);
+int dfcsa_bwd_block_out_pool(int dtype, int B, int H, int W, int C, const void* dskip, const void* out,
+                             const void* dpooled, const void* y4, const float* sc4, const float* sh4,
+                             const float* mean4, const float* invstd4, const void* res, const float* res_scale,
+                             void* dout, void* dres, float* partial, void* stream);
 /* dz = dact * (y*sc+sh > 0); sums [sum dz, sum dz*xh] */
 int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                       const float* sh, const float* mean, const float* invstd, void* dz,

@@ -708,3 +708,47 @@ def test_dgrad_apply_prologue_equals_apply_plus_gemm(M):
         assert rel(a, b) < 1e-5
     assert rel(p1.view(n1, 2, C).double().sum(0), p0.view(n0, 2, C).double().sum(0)) < 1e-5
     assert rel(q1.view(m1, 2, C).double().sum(0), q0.view(m0, 2, C).double().sum(0)) < 1e-5
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,W,C,skip", [(2, 16, 12, 64, True), (1, 8, 10, 128, False), (3, 6, 4, 16, True)])
+def test_block_out_pool_fused_equals_separate(dtype, B, H, W, C, skip):
+    """dfcsa_block_out_pool / dfcsa_bwd_block_out_pool (encoder block output + 2x2 max-pool, forward
+    and backward in one pass each) against the separate launches (dfcsa_block_out + dfcsa_maxpool2_fwd;
+    dfcsa_maxpool2_bwd into the skip gradient + dfcsa_bwd_block_out): out, pooled, dout, dres exact
+    (ties included: y4 has repeated values), the three per-channel sums to summation-order noise."""
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P, stream
+    torch.manual_seed(16)
+    dev = "cuda"
+    T = ops.dt(dtype)
+    M = B * H * W
+    y4 = (torch.randint(-3, 4, (M, C), device=dev).float() * 0.5).to(dtype)   # ties in the windows
+    res = torch.randn(M, C, device=dev).to(dtype)
+    sc, sh, mu = (torch.randn(C, device=dev) for _ in range(3))
+    istd = torch.rand(C, device=dev) + 0.5
+    rs = torch.tensor([0.3], device=dev)
+    Mp = B * (H // 2) * (W // 2)
+    out0, out1 = (torch.empty(M, C, device=dev, dtype=dtype) for _ in range(2))
+    p0, p1 = (torch.empty(Mp, C, device=dev, dtype=dtype) for _ in range(2))
+    call("dfcsa_block_out", T, M, C, P(y4), P(sc), P(sh), P(res), P(rs), P(out0), stream())
+    call("dfcsa_maxpool2_fwd", T, B, H, W, C, P(out0), P(p0), stream())
+    call("dfcsa_block_out_pool", T, B, H, W, C, P(y4), P(sc), P(sh), P(res), P(rs), P(out1), P(p1), stream())
+    gp = torch.randn(Mp, C, device=dev).to(dtype)
+    gs = torch.randn(M, C, device=dev).to(dtype) if skip else None
+    d0 = gs.clone() if skip else torch.zeros(M, C, device=dev, dtype=dtype)
+    call("dfcsa_maxpool2_bwd", T, B, H, W, C, P(out0), P(gp), P(d0), stream())
+    nte = ops.ntiles_ew(M, C)
+    dr0 = torch.empty(M, C, device=dev, dtype=dtype)
+    q0 = torch.empty(nte * 3 * C, device=dev)
+    call("dfcsa_bwd_block_out", T, M, C, P(d0), P(y4), P(sc), P(sh), P(mu), P(istd), P(res), P(rs), None, P(dr0),
+         P(q0), stream())
+    ntp = LIB.dfcsa_bwd_block_out_pool_ntiles(B, H, W, C)
+    d1, dr1 = (torch.empty(M, C, device=dev, dtype=dtype) for _ in range(2))
+    q1 = torch.empty(ntp * 3 * C, device=dev)
+    call("dfcsa_bwd_block_out_pool", T, B, H, W, C, P(gs), P(out1), P(gp), P(y4), P(sc), P(sh), P(mu), P(istd),
+         P(res), P(rs), P(d1), P(dr1), P(q1), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(out1, out0) and torch.equal(p1, p0)
+    assert torch.equal(d1, d0) and torch.equal(dr1, dr0)
+    assert rel(q1.view(ntp, 3, C).double().sum(0), q0.view(nte, 3, C).double().sum(0)) < 1e-5
