@@ -466,6 +466,39 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
       const int R = a[0], C = a[1], lds = a[2], ldd = a[3], tc = a[4];
       const int r0 = (int)(tl / tc) * 64, c0 = (int)(tl % tc) * 64;
       const int lane = tid & 63, q = tid >> 6;
+      if (t.dtype == DFCSA_DT_BF16 && lds % 8 == 0 && ldd % 8 == 0 && ((uintptr_t)t.w0 & 15) == 0 &&
+          ((uintptr_t)t.out & 15) == 0) {
+        // 16-B loads of 8 consecutive columns and 16-B stores of 8 consecutive rows (partial
+        // chunks at the R / C edges element by element)
+        for (int e = tid; e < 512; e += 256) {
+          const int i = e >> 3, k = (e & 7) * 8, rr = r0 + i, cc = c0 + k;
+          if (rr >= R) continue;
+          const bf16_t* sp = (const bf16_t*)t.w0 + (int64_t)rr * lds + cc;
+          if (cc + 8 <= C) {
+            float v[8];
+            load8<bf16_t>(sp, v);
+#pragma unroll
+            for (int j = 0; j < 8; ++j) tile[i][k + j] = v[j];
+          } else {
+            for (int j = 0; j < 8 && cc + j < C; ++j) tile[i][k + j] = bf2f(sp[j]);
+          }
+        }
+        __syncthreads();
+        for (int e = tid; e < 512; e += 256) {
+          const int ci = e >> 3, k = (e & 7) * 8, cc = c0 + ci, rr = r0 + k;
+          if (cc >= C || rr >= R) continue;
+          bf16_t* dp = (bf16_t*)t.out + (int64_t)cc * ldd + rr;
+          if (rr + 8 <= R) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v[j] = tile[k + j][ci];
+            store8<bf16_t>(dp, v);
+          } else {
+            for (int j = 0; j < 8 && rr + j < R; ++j) dp[j] = f2bf(tile[k + j][ci]);
+          }
+        }
+        break;
+      }
       for (int i = 0; i < 16; ++i) {
         const int rr = r0 + i * 4 + q, cc = c0 + lane;
         if (rr < R && cc < C) tile[i * 4 + q][lane] = load_as(t.w0, (int64_t)rr * lds + cc, t.dtype);
