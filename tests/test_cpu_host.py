@@ -345,3 +345,42 @@ def test_reference_checkpoint_loads_weights_only():
     m.load_state_dict(ck["model_state_dict"])
     assert set(ck["metrics"]) == {"loss", "iou", "dice", "best_samples", "worst_samples"}
     assert len(ck["optimizer_state_dict"]["state"]) == len(list(m.parameters()))
+
+
+@pytest.mark.parametrize("features,pool,hw,full_res", [((8, 16, 32, 64), 4, 32, False), ((8, 16, 32, 64), 8, 48, False),
+                                                       ((8, 16, 16, 32), 4, 16, True)])
+def test_model_stats_flops_match_flop_counter(features, pool, hw, full_res):
+    """utils.model_stats.forward_flops (analytic walk of the GPU model's module tree) against
+    torch.utils.flop_counter on the CPU restatement of the same forward (oracle/dfcsa_oracle.py),
+    and parameter totals / serialized size (reference model_stats.py:15-43)."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from models.model_factory import ModelFactory
+    from oracle import dfcsa_oracle as O
+    from utils import model_stats as S
+    name = "UNet_FullResAttention" if full_res else "DFC-SA-Res-Block"
+    cfg = {"model": {"name": name, "features": list(features), "pool_size": pool}, "training": {}}
+    m = ModelFactory.get_model(cfg)
+    sd = {k: v.detach().float() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 3, hw, hw)
+    with FlopCounterMode(display=False) as fc:
+        with torch.no_grad():
+            O.unet_dfc_sa_res(x, sd, pool_size=pool, training=True, bufs=None, full_res=full_res)
+    ref = fc.get_total_flops()
+    ours = S.forward_flops(m, (2, 3, hw, hw))
+    assert abs(ours - ref) <= 1e-9 * ref, (ours, ref)
+    ps = S.count_parameters(m)
+    assert ps["total"] == sum(p.numel() for p in m.parameters()) == ps["trainable"]
+    assert 0 < S.get_model_size(m) < 10
+
+
+def test_model_stats_headline_flops_pinned():
+    """The config-2 model at 224^2, P=4: 67.29 GFLOP per image forward (measured there
+    with torch.utils.flop_counter on the reference) -- fwd+bwd 201.66 = 3x forward minus the input
+    gradient of the first block."""
+    from models.model_factory import ModelFactory
+    from utils import model_stats as S
+    m = ModelFactory.get_model({"model": {"name": "DFC-SA-Res-Block", "features": [64, 128, 256, 512],
+                                          "pool_size": 4}, "training": {}})
+    f = S.forward_flops(m, (1, 3, 224, 224))
+    assert abs(f / 1e9 - 67.29) < 0.01, f / 1e9
