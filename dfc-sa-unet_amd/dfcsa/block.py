@@ -39,8 +39,12 @@ from .streams import join_branch, on_branch, on_side
 FUSED_DGRAD_GATE = [os.environ.get("DFCSA_DGRAD_GATE", "1") == "1"]
 # encoder blocks: the 2x2 max-pool fused into the block-output pass and its backward (DFCSA_POOL_FUSION=0: separate)
 POOL_FUSION = [os.environ.get("DFCSA_POOL_FUSION", "1") == "1"]
-# C == 64: BatchNorm-backward applies in the dgrad GEMMs' A prologue (DFCSA_APPLY_PROLOGUE=0: separate)
-APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "1") == "1"]
+# C == 64: BatchNorm-backward applies in the dgrad GEMMs' A prologue (DFCSA_APPLY_PROLOGUE=<dy4><dy3> flags, "00": separate)
+# [dy4 into the fusion-conv dgrad, dy3 into the gate-conv dgrad]: per-launch traces put the first at
+# 205 us against 131 + 55 us for the separate pair (the longer prologue between the DMA wait and the
+# MFMAs) and the second at 137 against 103 + ~50 us, so only the second is on by default
+APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[:1] == "1",
+                  os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[-1:] == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -299,7 +303,9 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     fused = dtype == torch.bfloat16 and C % 64 == 0 and C <= 256 and FUSED_DGRAD_GATE[0]
     # C == 64: the BatchNorm-backward applies (dy4, dy3) run in the A-operand prologue of the fused
     # input-gradient GEMMs below (the conv-bias gradient is the analytic zero there)
-    apro = fused and C == 64 and not ops.NUMERIC_BN_BIAS_GRAD and APPLY_PROLOGUE[0]
+    apro_ok = fused and C == 64 and not ops.NUMERIC_BN_BIAS_GRAD
+    apro = apro_ok and APPLY_PROLOGUE[0]           # dy4 in the fusion-conv dgrad (measured slower: off)
+    apro3 = apro_ok and APPLY_PROLOGUE[1]          # dy3 in the gate-conv dgrad
     # ---- gate: s = sigmoid(bn3 y3); fused = s*local + (1-s)*attn ----
     if apro:
         # dy4 in the prologue, the gate backward in the epilogue of the fusion conv's dgrad GEMM
@@ -337,7 +343,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
     W3t = s.pk["W3t"]
     fused_bn1 = fused
-    if apro:
+    if apro3:
         # dy3 in the prologue, the accumulate + BN1 sums in the epilogue of the gate conv's dgrad GEMM
         dy3 = torch.empty_like(dz3)
         npart1 = _lib.LIB.dfcsa_dgrad_apply_parts(M, 1)
@@ -352,7 +358,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     with on_side(dev, dy3):
         ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
                             [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
-    if apro:
+    if apro3:
         pass
     elif fused_bn1:
         # accumulate GEMM with the local branch's BN1-backward sums in its epilogue
