@@ -1345,8 +1345,11 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     o_row[it] = e / OCH;
     o_base[it] = (T*)args.dest[0] + (e - o_row[it] * OCH) * 8;
   }
+  float st_s[FN], st_q[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
   int t = blockIdx.x;
-  if (t >= mtiles) return;
+  if (t >= mtiles) return;   // never: the grid is at most one workgroup per tile
   issue(t, 0);
   int slot = 0;
   bool first_iter = true;
@@ -1373,15 +1376,15 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
       }
     }
     // outstanding, in issue order: DMA(t), [o taps], the previous tile's prologue + FN stats +
-    // NSTORE output stores, DMA(tn): the counted wait retires DMA(t)
+    // NSTORE output stores (no stats stores: kept in registers), DMA(tn): the counted wait retires DMA(t)
     if constexpr (PRO == PRO_GATE_FUSION) {   // no loads besides the DMAs: leave the stores in flight
       if (tn < mtiles) {
         issue(tn, slot ^ 1);
         if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NITEM * NOUT + FN + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NITEM * NOUT + NSTORE) : "memory");
       } else {
         if (first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NITEM * NOUT + FN + NSTORE) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NITEM * NOUT + NSTORE) : "memory");
       }
     } else {
       if (tn < mtiles) {
@@ -1449,6 +1452,8 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
     }
     const int m0 = t * 64;
+    // BatchNorm partial sums of this workgroup's tiles, kept in registers (one slab row per
+    // workgroup, written after the loop: the finalize then reads gridDim.x rows, not M/64)
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       float s = 0.f, q = 0.f;
@@ -1463,8 +1468,8 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
         }
       s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
       q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-      const int n = wave * NWC + j * 16 + (lane & 15);
-      if (lane < 32) args.stats[(size_t)t * 2 * C + (lane < 16 ? 0 : C) + n] = lane < 16 ? s : q;
+      st_s[j] += s;
+      st_q[j] += q;
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -1485,6 +1490,11 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
       T* dst = m < M ? o_base[it] + (size_t)m * C : (T*)(g_store_sink + 4 * (tid & 63));
       *(uint4*)dst = v;
     }
+  }
+#pragma unroll
+  for (int j = 0; j < FN; ++j) {
+    const int n = wave * NWC + j * 16 + (lane & 15);
+    if (lane < 32) args.stats[(size_t)blockIdx.x * 2 * C + (lane < 16 ? 0 : C) + n] = lane < 16 ? st_s[j] : st_q[j];
   }
 }
 
@@ -1805,13 +1815,18 @@ extern "C" int dfcsa_dgrad_apply_parts(int M, int epi) {
 
 namespace {
 template <int PRO, int C>
-int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
+int fwd_pro_grid(int M) {
   static int occ = 0;
   if (!occ &&
       (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO, C>, 256, 0) != hipSuccess || occ < 1))
     occ = 1;
+  return std::min(256 * occ, (M + 63) / 64);
+}
+
+template <int PRO, int C>
+int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
   const int mtiles = (a.M + 63) / 64;
-  const int gx = std::min(256 * occ, mtiles);
+  const int gx = fwd_pro_grid<PRO, C>(a.M);
   const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + (double)C * a.Kpad + moved * a.M * C));
   hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
@@ -1819,6 +1834,14 @@ int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
   return 0;
 }
 }  // namespace
+
+extern "C" int dfcsa_fwd_pro_parts(int M, int C, int pro) {
+  if (M <= 0) return DFCSA_EINVAL;
+  if (pro == 0 && C == 64) return fwd_pro_grid<PRO_GATE_FUSION, 64>(M);
+  if (pro == 0 && C == 128) return fwd_pro_grid<PRO_GATE_FUSION, 128>(M);
+  if (pro == 1 && C == 64) return fwd_pro_grid<PRO_LOCAL_ATTN, 64>(M);
+  return DFCSA_EINVAL;
+}
 
 extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
                                      const void* local, const void* attn, const void* w4, int Kpad, const float* b4,

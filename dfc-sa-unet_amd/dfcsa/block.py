@@ -149,8 +149,11 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st3 = stats(C)
+    nt3 = nt
     if not fullres and dtype == torch.bfloat16 and C == 64 and Kp3 == 128 and training and FUSED_DGRAD_GATE[0]:
-        # the local/attention merge runs in the gate conv's A-operand prologue
+        # the local/attention merge runs in the gate conv's A-operand prologue (one statistics row
+        # per workgroup)
+        nt3 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 1)
         call("dfcsa_local_attn_gate_fwd", B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2), P(bn2.scale),
              P(bn2.shift), P(o), Pp, P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), P(st3),
              stream())
@@ -161,12 +164,15 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # ---- gate conv ----
         ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
                       bias=conv3.bias, stats=st3)
-    bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt, C, C, M, training)
+    bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt3, C, C, M, training)
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st4 = stats(C)
+    nt4 = nt
     if dtype == torch.bfloat16 and C in GATE_FUSION_WIDTHS and Kp4 == 3 * C and training and FUSED_DGRAD_GATE[0]:
-        # the gate fusion runs in the fusion conv's A-operand prologue (dfcsa_gate_fusion_fwd)
+        # the gate fusion runs in the fusion conv's A-operand prologue (dfcsa_gate_fusion_fwd; one
+        # statistics row per workgroup)
+        nt4 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 0)
         call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4,
              P(conv4.bias), P(fused), P(y4), P(st4), stream())
     else:
@@ -174,7 +180,7 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
              stream())
         ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C, [y4],
                       C, bias=conv4.bias, stats=st4)
-    bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt, C, C, M, training)
+    bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt4, C, C, M, training)
     out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     pooled_out = None
     if pool:

@@ -246,15 +246,18 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
 /* fusion conv forward with the gate fusion in its A-operand prologue (bf16, C == 64 or 128, Kpad == 3C):
  * fused = g*local + (1-g)*attn, g = sigmoid(y3*sc3+sh3) (dfcsa_gate_fuse's arithmetic), stored;
  * y4 = [fused | local | attn] . w4^T + b4 (w4 = the fusion conv's [C][3C] forward operand) with
- * the BatchNorm partial statistics of dfcsa_conv_gemm (stats4 [ceil(M/64)][2][C]).  Replaces the
- * dfcsa_gate_fuse + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:102-110). */
+ * BatchNorm partial statistics (stats4 [parts][2][C], see below).  Replaces the
+ * dfcsa_gate_fuse + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:102-110).
+ * The statistics slab holds ONE row per workgroup (rows [0, dfcsa_fwd_pro_parts(M, C, 0))), the
+ * sums of that workgroup's 64-row tiles: dfcsa_bn_finalize takes that row count as ntiles. */
+int dfcsa_fwd_pro_parts(int M, int C, int pro);
 int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
                           float* stats4, void* stream);
 /* gate conv forward with the local/attention merge in its A-operand prologue (bf16, C == 64,
  * Kpad == 128, relu): local = relu(y1*sc1+sh1), attn = gamma*bilinear(o) + relu(y2*sc2+sh2)
  * (dfcsa_block_local_attn's arithmetic; o fp32 [B][P][P][64]), both stored; y3 = [local | attn] .
- * w3^T + b3 with BatchNorm partial statistics (stats3 [ceil(M/64)][2][64]).  Replaces the
+ * w3^T + b3 with BatchNorm partial statistics (one row per workgroup: dfcsa_fwd_pro_parts(M, 64, 1) rows).  Replaces the
  * dfcsa_block_local_attn + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:36-38, 97-102). */
 int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,
