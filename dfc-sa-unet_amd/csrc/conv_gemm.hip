@@ -1625,6 +1625,9 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // the 112^2 decoder dgrad, K = 1408: 204 vs 175 us for the 128x128 tile; K = 1152: equal)
     if (a.N % 256 == 0 && a.K >= 2048 && ((a.M + 255) / 256) * (a.N / 256) >= 150)
       return launch_pp<2, true, false>(a, st);
+    // the 14^2 bottleneck 3x3 fwd / dgrad (M = 3136, K >= 4608): 64x64 tiles give 392-784
+    // workgroups instead of 200-400 (tools/gemm_bench.py round 2: 111 -> 102 us, 51 -> 48 us)
+    if (a.M <= 4096 && a.N >= 512 && a.K >= 4096) return launch_glds<64, 64, 2, 2, 2>(a, st);
     if (((a.M + 127) / 128) * ((a.N + 127) / 128) < 256) {
       // still under one 128x64 workgroup per CU with a short K (the ViT GEMMs of TransUNet:
       // M = 8 x 196 rows, K = 768 / 3072): 64x64 tiles (4 waves of 32x32) double the workgroups
