@@ -121,7 +121,8 @@ def cpu_baseline(batch=16, timed_steps=2):
 def trainer_faithful_leg(model, opt, x, t, steps):
     """The reference's step loop as a user runs it: utils.trainer.Trainer.train_epoch over host
     (pinned) batches -- H2D copy per batch, the device step, and the reference's per-step host
-    syncs (loss .item(), IoU/Dice as Python floats, trainer.py:142,154-156) -- eager launches."""
+    syncs (loss .item(), IoU/Dice as Python floats, trainer.py:142,154-156); the Trainer replays
+    the step as a HIP graph (captured during the two warm-up batches)."""
     import contextlib
     import io
 
@@ -132,8 +133,8 @@ def trainer_faithful_leg(model, opt, x, t, steps):
     with contextlib.redirect_stdout(io.StringIO()), tempfile.TemporaryDirectory() as tmp:
         cfg = {"training": {"num_epochs": 1, "loss": {"type": "bce_dice", "params": {}}},
                "logging": {"log_dir": os.path.join(tmp, "l"), "images_dir": os.path.join(tmp, "i")}}
-        tr = Trainer(model, loader[:1], loader[:1], opt, x.device, cfg)
-        tr.train_epoch(0)                      # warm-up
+        tr = Trainer(model, loader[:2], loader[:1], opt, x.device, cfg)
+        tr.train_epoch(0)                      # warm-up: one eager step, then the graph capture
         torch.cuda.synchronize()
         tr.train_loader = loader
         t0 = time.perf_counter()
@@ -143,7 +144,8 @@ def trainer_faithful_leg(model, opt, x, t, steps):
     return {"value": round(steps * x.shape[0] / el, 2), "unit": "images/s", "steps": steps,
             "ms_per_step": round(el / steps * 1e3, 3),
             "how": "utils.trainer.Trainer.train_epoch over pinned host batches: H2D copy + per-step "
-                   ".item() syncs as the reference (trainer.py:115-163), eager launches, no HIP graph"}
+                   ".item() syncs as the reference (trainer.py:115-163), the step replayed as a HIP graph "
+                   "(Trainer default, training.cuda_graph)"}
 
 
 def step_pmc_bytes():

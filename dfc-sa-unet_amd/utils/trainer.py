@@ -69,12 +69,55 @@ class Trainer:
         self.start_time = time.time()
         self.num_epochs = config["training"]["num_epochs"]
         self.max_norm = 1.0
+        # HIP-graph replay of the training step (train_step); training.cuda_graph: false disables
+        self._graphs = {} if config["training"].get("cuda_graph", True) else None
+        self._graph_seen = set()
         print(f"模型將在 {self.device} 上訓練")
 
     # ------------------------------------------------------------------ one step
     def train_step(self, images, masks):
         """One device-resident training step.  Returns {'loss': 0-d tensor, 'stats': fp32[8]}
-        (see dfcsa.loss) without synchronising with the host."""
+        (see dfcsa.loss) without synchronising with the host.
+
+        With the fused optimizer on a GPU (``training.cuda_graph``, default on) the step is
+        captured once per input shape as a HIP graph (the first batch of a shape runs eagerly,
+        the second is captured and replayed, later ones replay): the ~430 kernel launches of a
+        step become one graph launch, the kernels and their order are the same, so the results
+        are the eager step's.  If capture fails the trainer keeps stepping eagerly."""
+        if (self._graphs is not None and isinstance(self.optimizer, FusedSGD) and images.is_cuda
+                and self.model.training):
+            return self._graph_step(images, masks)
+        return self._eager_step(images, masks)
+
+    def _graph_step(self, images, masks):
+        # the SGD hyper-parameters are kernel arguments baked into a capture: part of the key
+        hp = tuple(float(self.optimizer.param_groups[0][k]) for k in ("lr", "momentum", "weight_decay"))
+        key = (tuple(images.shape), tuple(masks.shape), images.dtype, masks.dtype, hp)
+        g = self._graphs.get(key)
+        if g is None:
+            if key not in self._graph_seen:       # first batch of this shape: eager (warm-up)
+                self._graph_seen.add(key)
+                return self._eager_step(images, masks)
+            si, sm = images.clone(), masks.clone()
+            graph = torch.cuda.CUDAGraph()
+            try:
+                with torch.cuda.graph(graph):     # recorded, not executed: replayed below
+                    met = self._eager_step(si, sm)
+            except RuntimeError as e:
+                print(f"HIP graph capture of the training step failed ({e}); stepping eagerly")
+                self._graphs = None
+                torch.cuda.synchronize()
+                return self._eager_step(images, masks)
+            if len(self._graphs) >= 2:           # e.g. a short last batch: keep the newest two
+                self._graphs.pop(next(iter(self._graphs)))
+            g = self._graphs[key] = (graph, si, sm, met)
+        graph, si, sm, met = g
+        si.copy_(images, non_blocking=True)
+        sm.copy_(masks, non_blocking=True)
+        graph.replay()
+        return met
+
+    def _eager_step(self, images, masks):
         self.optimizer.zero_grad()
         logits = self.model(images)
         probs = sigmoid(logits)
@@ -163,6 +206,9 @@ class Trainer:
         ckpt = torch.load(checkpoint_path.replace("\\", "/"), map_location=self.device, weights_only=True)
         self.model.load_state_dict(ckpt["model_state_dict"])
         self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
+        if self._graphs is not None:   # optimizer storage may be new: capture again
+            self._graphs.clear()
+            self._graph_seen.clear()
         for k in ("train_losses", "val_losses", "train_dice_scores", "val_dice_scores", "train_iou_scores",
                   "val_iou_scores", "best_val_loss"):
             setattr(self, k, ckpt[k])
