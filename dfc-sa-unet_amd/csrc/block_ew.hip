@@ -63,6 +63,7 @@ struct EwArgs {
   const float* tbl;     // o (fp32 [B][P][P][C]) or dpooled
   const float* scalar;  // gamma of LSA / res_scale
   float* partial;
+  int64_t partial_cap;  // capacity of `partial` in floats (checked against the launch grid)
   int tile_px;          // pixels per reduction tile
 };
 
@@ -1106,6 +1107,8 @@ int launch_red(int dtype, EwArgs a, hipStream_t st) {
   if (a.C % 8 || a.C > 2048 || a.M <= 0) return DFCSA_EINVAL;
   a.tile_px = tile_px(a.C);
   int blocks = (a.M + a.tile_px - 1) / a.tile_px;
+  // the partial slab holds one [NS][C] row per workgroup: refuse a slab shorter than the grid
+  if (a.partial && (int64_t)blocks * NSums<MODE>::v * a.C > a.partial_cap) return DFCSA_EINVAL;
   if (dtype == DFCSA_DT_BF16) hipLaunchKernelGGL((ew_red_kernel<bf16_t, MODE>), dim3(blocks), dim3(256), 0, st, a);
   else hipLaunchKernelGGL((ew_red_kernel<float, MODE>), dim3(blocks), dim3(256), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -1224,10 +1227,10 @@ extern "C" int dfcsa_block_out(int dtype, int M, int C, const void* y4, const fl
 
 extern "C" int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, const void* y4, const float* sc4,
                                    const float* sh4, const float* mean4, const float* invstd4, const void* res,
-                                   const float* res_scale, void* dz4, void* dres, float* partial, void* stream) {
+                                   const float* res_scale, void* dz4, void* dres, float* partial, int64_t partial_floats, void* stream) {
   EwArgs a = zargs(M, C);
   a.a0 = dout; a.a1 = y4; a.a2 = res; a.sc = sc4; a.sh = sh4; a.mean = mean4; a.invstd = invstd4;
-  a.scalar = res_scale; a.o0 = dz4; a.o1 = dres; a.partial = partial;
+  a.scalar = res_scale; a.o0 = dz4; a.o1 = dres; a.partial = partial; a.partial_cap = partial_floats;
   return launch_red<EW_BWD_BLOCK_OUT>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1240,10 +1243,10 @@ extern "C" int dfcsa_sum_out(int dtype, int M, int C, const void* a, const void*
 }
 
 extern "C" int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, const void* res, const float* res_scale,
-                                  void* dres, float* partial, void* stream) {
+                                  void* dres, float* partial, int64_t partial_floats, void* stream) {
   if (!dout || !res || !res_scale || !partial) return DFCSA_EINVAL;
   EwArgs e = zargs(M, C);
-  e.a0 = dout; e.a2 = res; e.scalar = res_scale; e.o1 = dres; e.partial = partial;
+  e.a0 = dout; e.a2 = res; e.scalar = res_scale; e.o1 = dres; e.partial = partial; e.partial_cap = partial_floats;
   return launch_red<EW_BWD_SUM_OUT>(dtype, e, (hipStream_t)stream);
 }
 
@@ -1256,30 +1259,30 @@ extern "C" int dfcsa_sum_into(const float* x, int n, float* out, void* stream) {
 
 extern "C" int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                                  const float* sh, const float* mean, const float* invstd, void* dz,
-                                 float* partial, void* stream) {
+                                 float* partial, int64_t partial_floats, void* stream) {
   EwArgs a = zargs(M, C);
-  a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.o0 = dz; a.partial = partial;
+  a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.o0 = dz; a.partial = partial; a.partial_cap = partial_floats;
   return launch_red<EW_BWD_RELU_BN>(dtype, a, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,
                               const float* sh3, const float* mean3, const float* invstd3, const void* local,
-                              const void* attn, void* dlocal, void* dattn, void* dz3, float* partial,
+                              const void* attn, void* dlocal, void* dattn, void* dz3, float* partial, int64_t partial_floats,
                               void* stream) {
   EwArgs a = zargs(M, C);
   a.a0 = dfused; a.a1 = y3; a.a2 = local; a.a3 = attn; a.sc = sc3; a.sh = sh3; a.mean = mean3;
-  a.invstd = invstd3; a.o0 = dlocal; a.o1 = dattn; a.o2 = dz3; a.partial = partial;
+  a.invstd = invstd3; a.o0 = dlocal; a.o1 = dattn; a.o2 = dz3; a.partial = partial; a.partial_cap = partial_floats;
   return launch_red<EW_BWD_GATE>(dtype, a, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn,
                                     const float* dpooled, int P, const void* y2, const float* sc2,
                                     const float* sh2, const float* mean2, const float* invstd2, int relu,
-                                    void* dz2, float* partial, void* stream) {
+                                    void* dz2, float* partial, int64_t partial_floats, void* stream) {
   EwArgs a = zargs(B * H * W, C);
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = dattn; a.a1 = y2; a.tbl = dpooled; a.sc = sc2; a.sh = sh2; a.mean = mean2; a.invstd = invstd2;
-  a.o0 = dz2; a.partial = partial; a.act = relu;
+  a.o0 = dz2; a.partial = partial; a.partial_cap = partial_floats; a.act = relu;
   return launch_red<EW_BWD_ATTN_ENTRY>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1305,34 +1308,34 @@ extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum,
 
 extern "C" int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
                                   const float* invstd, const float* gamma, const float* coef, void* dy,
-                                  float* bias_partial, void* stream) {
+                                  float* bias_partial, int64_t bias_partial_floats, void* stream) {
   EwArgs a = zargs(M, C);
   a.a0 = dz; a.a1 = y; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.coef = coef; a.o0 = dy;
-  a.partial = bias_partial;
+  a.partial = bias_partial; a.partial_cap = bias_partial_floats;
   return launch_red<EW_BN_BWD_APPLY>(dtype, a, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_bn_bwd_apply_relu(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                                        const float* sh, const float* mean, const float* invstd, const float* gamma,
-                                       const float* coef, void* dy, float* bias_partial, void* stream) {
+                                       const float* coef, void* dy, float* bias_partial, int64_t bias_partial_floats, void* stream) {
   if (!dact || !y || !sc || !sh || !mean || !invstd || !gamma || !coef || !dy) return DFCSA_EINVAL;
   EwArgs a = zargs(M, C);
   a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.gamma = gamma; a.coef = coef;
-  a.o0 = dy; a.partial = bias_partial;
+  a.o0 = dy; a.partial = bias_partial; a.partial_cap = bias_partial_floats;
   return launch_red<EW_BN_BWD_APPLY_RELU>(dtype, a, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, const void* dattn,
                                         const float* dpooled, int P, const void* y, const float* sc,
                                         const float* sh, const float* mean, const float* invstd, int relu,
-                                        const float* gamma, const float* coef, void* dy, float* bias_partial,
+                                        const float* gamma, const float* coef, void* dy, float* bias_partial, int64_t bias_partial_floats,
                                         void* stream) {
   if (!dattn || !dpooled || P <= 0 || !y || !sc || !sh || !mean || !invstd || !gamma || !coef || !dy)
     return DFCSA_EINVAL;
   EwArgs a = zargs(B * H * W, C);
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = dattn; a.a1 = y; a.tbl = dpooled; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.act = relu;
-  a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial;
+  a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial; a.partial_cap = bias_partial_floats;
   return launch_red<EW_BN_BWD_APPLY_ENTRY>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1353,9 +1356,9 @@ extern "C" int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, 
   return 0;
 }
 
-extern "C" int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, void* stream) {
+extern "C" int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, int64_t partial_floats, void* stream) {
   EwArgs a = zargs(M, C);
-  a.a0 = x; a.partial = partial;
+  a.a0 = x; a.partial = partial; a.partial_cap = partial_floats;
   return launch_red<EW_CHANNEL_SUM>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1406,17 +1409,18 @@ extern "C" int dfcsa_bwd_block_out_pool_ntiles(int B, int H, int W, int C) {
 extern "C" int dfcsa_bwd_block_out_pool(int dtype, int B, int H, int W, int C, const void* dskip, const void* out,
                                         const void* dpooled, const void* y4, const float* sc4, const float* sh4,
                                         const float* mean4, const float* invstd4, const void* res,
-                                        const float* res_scale, void* dout, void* dres, float* partial, void* stream) {
+                                        const float* res_scale, void* dout, void* dres, float* partial, int64_t partial_floats, void* stream) {
   if (C % 8 || C > 2048 || (H & 1) || (W & 1) || B <= 0 || !out || !dpooled || !y4 || !sc4 || !sh4 || !mean4 ||
       !invstd4 || !res || !res_scale || !dout || !dres || !partial)
     return DFCSA_EINVAL;
   EwArgs a = zargs(B * H * W, C);
   a.B = B; a.H = H; a.W = W;
   a.a0 = dskip; a.a1 = y4; a.a2 = res; a.sc = sc4; a.sh = sh4; a.mean = mean4; a.invstd = invstd4;
-  a.scalar = res_scale; a.o1 = dres; a.partial = partial;
+  a.scalar = res_scale; a.o1 = dres; a.partial = partial; a.partial_cap = partial_floats;
   a.tile_px = pool_tile(C);
   const int Mp = B * (H / 2) * (W / 2);
   const int blocks = (Mp + a.tile_px - 1) / a.tile_px;
+  if ((int64_t)blocks * 3 * C > partial_floats) return DFCSA_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DFCSA_DT_BF16)
     hipLaunchKernelGGL(bwd_block_out_pool_kernel<bf16_t>, dim3(blocks), dim3(256), 0, st, a, (const bf16_t*)out,

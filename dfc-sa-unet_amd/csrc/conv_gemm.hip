@@ -707,6 +707,370 @@ int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
   return 0;
 }
 
+// --------------------------------------------------------------------------------------------
+// 3x3 convolutions (forward and the fused 3x3 + 1x1 data gradient) on 2-D halo tiles.
+//
+// The row-tile kernels above fetch, for every one of the 9 taps, the tile's rows shifted by
+// (dh, dw): 9x the unique input per K chunk crosses L2 -> LDS, and the 128x128 tile spends a
+// 32-KB fetch per 2.1 MFLOP (64 flop/B), which bounds it at ~0.2-0.45 of MFMA peak by the
+// per-CU L2->LDS rate.  Here a workgroup owns a TW x TR block of output
+// pixels (TW | W, TR rows of the image-stacked B*H grid, TW*TR <= 256) and, per 64-channel chunk
+// of a source, DMAs its (TW+2) x (TR+2) halo into LDS ONCE; the taps of that source read their
+// shifted windows from the halo (per lane: halo pixel = p0 + dh*(TW+2) + dw; a tap that leaves the
+// lane's image reads a zero row instead, so tiles may straddle images and the pad lanes of a
+// 252-pixel tile are harmless).  Only the weight panel (BN x 64 per tap) streams per step: at
+// 256 x 128 the step moves 16 KB + ~4.8 KB of halo per 4.2 MFLOP (~200 flop/B).
+//
+// 8 waves (one workgroup per CU, ~150 KB LDS): 4 (M) x 2 (N), wave tile 64 x BN/2.  Waves 0-3
+// also stream the weight panels (3-slot ring, issued two steps ahead), waves 4-7 the halos
+// (double buffer, the next chunk's halo issued at the first tap of the current one): each wave's
+// counted vmcnt covers only its own DMA stream, so a halo in flight never holds up a weight
+// panel and vice versa; one barrier per step publishes both.  Sources = groups of segments with
+// the same tensor (the skip concat's two sources, the dgrad's dy1 taps + the two 1x1 sources).
+// Epilogue: bias, bf16 store of the valid pixels (1-3 destinations, optional accumulate), BN
+// partial statistics as ONE row per M tile (dfcsa_conv_stats_rows gives the row count).
+// --------------------------------------------------------------------------------------------
+constexpr int HALO_MAXPX = 400;                 // (TW+2)*(TR+2) <= 400 (rounded up to 8)
+constexpr int HALO_BYTES = HALO_MAXPX * 128;    // one halo buffer (64 channels, 128 B / pixel)
+
+struct HaloTap {
+  int toff;   // halo-pixel offset of the tap: dh*(TW+2) + dw
+  int bit;    // (dh+1)*3 + (dw+1): the lane's tap-validity bit
+  int kofs;   // K offset of the tap's segment (segment index * Cseg)
+};
+struct HaloGroup {
+  const void* ptr;
+  int ntaps;
+  HaloTap tap[9];
+};
+struct HaloArgs {
+  int M, N, Kpad, Cseg, BH, H, W;
+  int TW, TR, HW2, nhalo, ninstr;   // tile, halo row pitch (TW+2), halo pixels, 1-KB DMA pieces
+  int tiles_x, tiles_m;             // W / TW, M tiles
+  int ngroups, nchunk;              // sources, 64-channel chunks per source
+  HaloGroup grp[4];
+  const void* Bw;
+  const float* bias;
+  void* dest[3];
+  int Nd, accumulate;
+  float* stats;
+};
+
+template <int BN>
+__global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) {
+  using T = bf16_t;
+  constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
+  constexpr int BSLOT = BN * 128, NBS = 3;
+  constexpr int KB = BN / 32;                    // weight DMA pieces per loader wave per step
+  constexpr int KH = (HALO_MAXPX / 8 + 3) / 4;   // halo DMA pieces per loader wave (upper bound)
+  constexpr int OSTR = BN * 2 + 16;
+  constexpr int SMEM = 2 * HALO_BYTES + NBS * BSLOT + 128;
+  static_assert(256 * OSTR + 2 * 4 * 2 * BN * 4 <= SMEM, "epilogue staging fits");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+  char* const hbuf = smem;
+  char* const bbuf = smem + 2 * HALO_BYTES;
+  char* const zrow = bbuf + NBS * BSLOT;         // a zero pixel: taps leaving the image
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool hloader = wave >= 4;                // waves 4-7 stream halos, 0-3 weight panels
+  const int w4 = wave & 3;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int nN = (args.N + BN - 1) / BN;
+  const int L = xcd_remap(blockIdx.x, nN * args.tiles_m);
+  if (L < 0) return;
+  const int tn = L % nN, tm = L / nN;            // the N tiles of one M tile share an XCD
+  const int trow = tm / args.tiles_x, tcol = tm - trow * args.tiles_x;
+  const int r0 = trow * args.TR, c0 = tcol * args.TW, n0 = tn * BN;
+  const int TW = args.TW, HW2 = args.HW2, BH = args.BH, H = args.H, W = args.W;
+  const int npx = TW * args.TR;
+
+  // A rows of this lane (fragment i: tile pixel wm*64 + i*16 + lane%16): halo pixel of the
+  // centre tap and the 9-bit mask of taps that stay inside the pixel's image
+  int p0[FM];
+  unsigned tmask[FM];
+#pragma unroll
+  for (int i = 0; i < FM; ++i) {
+    const int m = wm * 64 + i * 16 + (lane & 15);
+    const int ty = m / TW, tx = m - ty * TW;
+    const int gr = r0 + ty, x = c0 + tx, y = gr % H;
+    const bool ok = m < npx && gr < BH;
+    p0[i] = (ty + 1) * HW2 + tx + 1;
+    unsigned mk = 0;
+#pragma unroll
+    for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+      for (int dw = -1; dw <= 1; ++dw)
+        mk |= (unsigned)(ok && y + dh >= 0 && y + dh < H && x + dw >= 0 && x + dw < W) << ((dh + 1) * 3 + dw + 1);
+    tmask[i] = mk;
+  }
+  const void* zero = (const void*)g_zero_page;
+  // halo pieces (waves 4-7): piece ii holds halo pixels 8ii..8ii+7; the lane fetches the chunk
+  // that the read-side swizzle expects in its LDS slot
+  int h_off[KH];
+  // weight pieces (waves 0-3): piece ii holds weight rows n0 + 8ii .. +7
+  int b_off[KB];
+  if (hloader) {
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      const int ii = min(w4 + 4 * k, args.ninstr - 1);
+      const int q = ii * 8 + (lane >> 3);
+      const int c = (lane & 7) ^ ((q >> 1) & 7);
+      const int hy = q / HW2, hx = q - hy * HW2;
+      const int gr = r0 - 1 + hy, ix = c0 - 1 + hx;
+      const bool ok = q < args.nhalo && gr >= 0 && gr < BH && ix >= 0 && ix < W;
+      h_off[k] = ok ? (gr * W + ix) * args.Cseg + c * 8 : -1;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const int nl = (w4 + 4 * k) * 8 + (lane >> 3);
+      const int n = n0 + nl;
+      const int c = (lane & 7) ^ ((nl >> 1) & 7);
+      b_off[k] = n < args.N ? n * args.Kpad + c * 8 : -1;
+    }
+  }
+  auto issue_halo = [&](int g, int cc, int buf) {
+    const T* base = (const T*)args.grp[g].ptr + cc * 64;
+    char* dst = hbuf + buf * HALO_BYTES;
+#pragma unroll
+    for (int k = 0; k < KH; ++k) {
+      if (w4 + 4 * k >= args.ninstr) break;      // wave-uniform
+      const void* src = h_off[k] >= 0 ? (const void*)(base + h_off[k]) : zero;
+      glds16(src, dst + (w4 + 4 * k) * 1024);
+    }
+  };
+  auto issue_b = [&](int kofs, int slot) {
+    char* dst = bbuf + slot * BSLOT;
+#pragma unroll
+    for (int k = 0; k < KB; ++k) {
+      const void* src = b_off[k] >= 0 ? (const void*)((const T*)args.Bw + b_off[k] + kofs) : zero;
+      glds16(src, dst + (w4 + 4 * k) * 1024);
+    }
+  };
+
+  // step = (source g, channel chunk cc, tap t); chunks j = (g, cc) in order
+  int S = 0;
+  for (int g = 0; g < args.ngroups; ++g) S += args.grp[g].ntaps;
+  S *= args.nchunk;
+  const int J = args.ngroups * args.nchunk;
+  int bg = 0, bcc = 0, bt = 0;                   // weight-prefetch cursor (two steps ahead)
+  auto badv = [&]() {
+    if (++bt == args.grp[bg].ntaps) { bt = 0; if (++bcc == args.nchunk) { bcc = 0; ++bg; } }
+  };
+  if (hloader) {
+    issue_halo(0, 0, 0);
+  } else {
+    issue_b(args.grp[0].tap[0].kofs, 0);
+    badv();
+    if (S > 1) issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, 1);
+    badv();
+  }
+  if (tid < 8) *(uint4*)(zrow + tid * 16) = make_uint4(0, 0, 0, 0);
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
+
+  int g = 0, cc = 0, t = 0, j = 0;
+  for (int s = 0; s < S; ++s) {
+    if (!hloader) {
+      if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (t == 0) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();   // publishes this step's weight panel (and, at t = 0, the chunk's halo)
+    if (!hloader) {
+      if (s + 2 < S) {
+        issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, (s + 2) % NBS);
+        badv();
+      }
+    } else if (t == 0 && j + 1 < J) {
+      const int nc = cc + 1 == args.nchunk ? 0 : cc + 1;
+      issue_halo(nc == 0 ? g + 1 : g, nc, (j + 1) & 1);
+    }
+    const HaloTap tp = args.grp[g].tap[t];
+    const char* hb = hbuf + (j & 1) * HALO_BYTES;
+    const char* bs = bbuf + (s % NBS) * BSLOT;
+    const char* abase[FM];
+    int arow[FM];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const bool ok = (tmask[i] >> tp.bit) & 1;
+      abase[i] = ok ? hb : zrow;
+      arow[i] = ok ? p0[i] + tp.toff : 0;
+    }
+#pragma unroll
+    for (int g2 = 0; g2 < 2; ++g2) {
+      Frag<T> fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) read_frag<T>(abase[i], arow[i], g2, lane, fa[i]);
+#pragma unroll
+      for (int jj = 0; jj < FN; ++jj) read_frag<T>(bs, wn * WTN + jj * 16 + (lane & 15), g2, lane, fb[jj]);
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[i], fb[jj]);
+    }
+    if (++t == args.grp[g].ntaps) {
+      t = 0;
+      ++j;
+      if (++cc == args.nchunk) { cc = 0; ++g; }
+    }
+  }
+  __syncthreads();
+
+  // ---- epilogue: accumulator element (i, jj, r) = tile pixel wm*64 + i*16 + (lane/16)*4 + r ----
+  unsigned vrow = 0;
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+      vrow |= (unsigned)(m < npx && r0 + m / TW < BH) << (i * 4 + r);
+    }
+  float* red = (float*)(smem + 256 * OSTR);      // [4 wm][2][BN]
+  if (args.stats) {
+#pragma unroll
+    for (int jj = 0; jj < FN; ++jj) {
+      float sm = 0.f, q = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float v = ((vrow >> (i * 4 + r)) & 1) ? acc[i][jj][r] : 0.f;
+          sm += v;
+          q += v * v;
+        }
+      sm += __shfl_xor(sm, 16, 64); sm += __shfl_xor(sm, 32, 64);
+      q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
+      if (lane < 16) {
+        const int col = wn * WTN + jj * 16 + lane;
+        red[(wm * 2 + 0) * BN + col] = sm;
+        red[(wm * 2 + 1) * BN + col] = q;
+      }
+    }
+  }
+  T* otile = (T*)smem;
+#pragma unroll
+  for (int jj = 0; jj < FN; ++jj) {
+    const int col = wn * WTN + jj * 16 + (lane & 15);
+    const int n = n0 + col;
+    const float bv = (args.bias && n < args.N) ? args.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        *(T*)((char*)otile + row * OSTR + col * 2) = f2bf(acc[i][jj][r] + bv);
+      }
+  }
+  __syncthreads();
+  if (args.stats && tid < BN) {
+    const int n = n0 + tid;
+    if (n < args.N) {
+      float sm = 0.f, q = 0.f;
+#pragma unroll
+      for (int w = 0; w < 4; ++w) { sm += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
+      args.stats[(size_t)tm * 2 * args.N + n] = sm;
+      args.stats[(size_t)tm * 2 * args.N + args.N + n] = q;
+    }
+  }
+  constexpr int OCH = BN / 8;
+  for (int e = tid; e < 256 * OCH; e += 512) {
+    const int row = e / OCH, ck = e - row * OCH;
+    const int ty = row / TW, tx = row - ty * TW;
+    const int n = n0 + ck * 8;
+    if (row >= npx || r0 + ty >= BH || n >= args.N) continue;
+    const size_t mg = (size_t)(r0 + ty) * W + c0 + tx;
+    float v[8];
+    load8<T>((const T*)((const char*)otile + row * OSTR + ck * 16), v);
+    const int d = n / args.Nd, col = n - d * args.Nd;
+    T* dst = (T*)args.dest[d] + (mg * args.Nd + col);
+    if (args.accumulate) {
+      float o[8];
+      load8<T>(dst, o);
+#pragma unroll
+      for (int qq = 0; qq < 8; ++qq) v[qq] += o[qq];
+    }
+    store8<T>(dst, v);
+  }
+}
+
+int g_halo_min_m = 0;   // knob 19: smallest M routed to the halo kernel (0: never; off until it beats the row tiles)
+
+// Build the halo launch for a bf16 3x3 (or fused 3x3 + 1x1) GEMM; false if it does not apply.
+bool halo_plan(const ConvGemmArgs& a, HaloArgs* h) {
+  if (g_halo_min_m <= 0 || a.M < g_halo_min_m) return false;
+  if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Ho != a.Hi || a.Wo != a.Wi || a.Cseg % 64) return false;
+  if ((int64_t)a.M * a.Cseg >= (1ll << 31) || (int64_t)a.N * a.Kpad >= (1ll << 31)) return false;
+  bool shifted = false;
+  std::memset(h, 0, sizeof(*h));
+  for (int i = 0; i < a.nseg; ++i) {
+    const ConvSeg& s = a.seg[i];
+    if (s.dh < -1 || s.dh > 1 || s.dw < -1 || s.dw > 1) return false;
+    shifted |= (s.dh || s.dw);
+    int g = 0;
+    while (g < h->ngroups && h->grp[g].ptr != s.ptr) ++g;
+    if (g == h->ngroups) {
+      if (g == 4) return false;
+      h->grp[g].ptr = s.ptr;
+      h->ngroups++;
+    }
+    HaloGroup& G = h->grp[g];
+    if (G.ntaps == 9) return false;
+    G.tap[G.ntaps].bit = (s.dh + 1) * 3 + s.dw + 1;
+    G.tap[G.ntaps].kofs = i * a.Cseg;
+    G.tap[G.ntaps].toff = s.dh * 1000 + s.dw;    // resolved once TW is known
+    G.ntaps++;
+  }
+  if (!shifted) return false;
+  const int W = a.Wo, BH = a.M / a.Wo;
+  // tile: TW | W, TR = 256 / TW rows; most valid pixels per slot, then the smallest halo
+  int bestTW = 0, bestTR = 0;
+  double best = 0.0;
+  int bestHalo = 1 << 30;
+  for (int TW = 2; TW <= 64 && TW <= W; ++TW) {
+    if (W % TW) continue;
+    const int TR = 256 / TW;
+    const int halo = (TW + 2) * (TR + 2);
+    if (((halo + 7) / 8) * 8 > HALO_MAXPX) continue;
+    const int tiles = (W / TW) * ((BH + TR - 1) / TR);
+    const double eff = (double)a.M / ((double)tiles * 256.0);
+    if (eff > best + 1e-9 || (eff > best - 1e-9 && halo < bestHalo)) { best = eff; bestTW = TW; bestTR = TR; bestHalo = halo; }
+  }
+  if (best < 0.85) return false;
+  h->M = a.M; h->N = a.N; h->Kpad = a.Kpad; h->Cseg = a.Cseg; h->BH = BH; h->H = a.Ho; h->W = W;
+  h->TW = bestTW; h->TR = bestTR; h->HW2 = bestTW + 2;
+  h->nhalo = bestHalo;
+  h->ninstr = (bestHalo + 7) / 8;
+  h->tiles_x = W / bestTW;
+  h->tiles_m = h->tiles_x * ((BH + bestTR - 1) / bestTR);
+  h->nchunk = a.Cseg / 64;
+  for (int g = 0; g < h->ngroups; ++g)
+    for (int t = 0; t < h->grp[g].ntaps; ++t) {
+      HaloTap& tp = h->grp[g].tap[t];
+      const int dh = tp.bit / 3 - 1, dw = tp.bit % 3 - 1;
+      tp.toff = dh * h->HW2 + dw;
+    }
+  h->Bw = a.Bw; h->bias = a.bias;
+  for (int i = 0; i < 3; ++i) h->dest[i] = a.dest[i];
+  h->Nd = a.Nd; h->accumulate = a.accumulate; h->stats = a.stats;
+  return true;
+}
+
+int launch_halo(const HaloArgs& h, hipStream_t st) {
+  const int bn = h.N <= 64 ? 64 : 128;
+  const int nN = (h.N + bn - 1) / bn;
+  dim3 grid(xcd_pad(nN * h.tiles_m));
+  if (bn == 64) hipLaunchKernelGGL((conv_halo_kernel<64>), grid, dim3(512), 0, st, h);
+  else hipLaunchKernelGGL((conv_halo_kernel<128>), grid, dim3(512), 0, st, h);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
 // fp32 GEMMs with few rows (the LightSelfAttention q/k/v projections and their dgrad, M = B*P*P):
 // split-reduction 16x64 tiles (small_gemm.h), plain 1x1 store with bias and column split
 __global__ void __launch_bounds__(256) small_conv_f32_kernel(const ConvGemmArgs args) {
@@ -1612,6 +1976,10 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // (waves of 32x64) beat 4-wave 64x64 ones -- twice the waves per SIMD hide the LDS and
     // DMA latency: 128x128/8 waves 690-730 TF on the 3x3 convs (vs ~600), 128x64/4 waves for
     // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
+    if (g_conv_cfg == 0) {   // 3x3 fwd / fused dgrad with M >= knob 19: 2-D halo tiles
+      HaloArgs h;
+      if (halo_plan(a, &h)) return launch_halo(h, st);
+    }
     if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (!glds_ok) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
     // N <= 64 with many rows: 256x64 / 8 waves (wave tile 32x64, twice the rows per B panel);
@@ -1653,7 +2021,9 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
 
 }  // namespace
 
-extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
+namespace {
+// descriptor -> kernel arguments (validated); the statistics row count of the launch in *rows
+int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->M <= 0 || d->N <= 0) return DFCSA_EINVAL;
   const int chunk = d->dtype == DFCSA_DT_BF16 ? 8 : 4;
   const int kst = d->dtype == DFCSA_DT_BF16 ? 64 : 32;
@@ -1661,7 +2031,7 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   if (d->ndest < 1 || d->ndest > 3 || d->Nd % 8 || (d->mode == CONV_STORE_PLAIN && d->Nd * d->ndest != d->N))
     return DFCSA_EINVAL;
   if (d->mode == CONV_STORE_SHUFFLE2 && (d->ndest != 1 || d->N != 4 * d->Nd)) return DFCSA_EINVAL;
-  ConvGemmArgs a;
+  std::memset(&a, 0, sizeof(a));
   a.M = d->M; a.N = d->N; a.K = d->nseg * d->Cseg; a.Kpad = d->Kpad; a.Cseg = d->Cseg;
   a.nseg = d->nseg;
   for (int i = 0; i < d->nseg; ++i) { a.seg[i].ptr = d->seg_ptr[i]; a.seg[i].dh = d->seg_dh[i]; a.seg[i].dw = d->seg_dw[i]; }
@@ -1675,6 +2045,26 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
   a.dbg = g_conv_dbg;
+  // statistics rows: one per 64-row M tile, or one per halo tile when the halo kernel runs it
+  HaloArgs h;
+  *rows = (d->dtype == DFCSA_DT_BF16 && g_conv_cfg == 0 && halo_plan(a, &h)) ? h.tiles_m : (d->M + 63) / 64;
+  return 0;
+}
+}  // namespace
+
+extern "C" int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d) {
+  ConvGemmArgs a;
+  int rows = 0;
+  const int rc = desc_args(d, a, &rows);
+  return rc ? rc : rows;
+}
+
+extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
+  ConvGemmArgs a;
+  int rows = 0;
+  if (const int rc = desc_args(d, a, &rows)) return rc;
+  // statistics slab: [rows][2][N]
+  if (d->stats && (int64_t)rows * 2 * d->N > d->stats_floats) return DFCSA_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   // profiling classes: the 1x1 streaming GEMMs are HBM-bound (their unit is bytes: A and the
   // weight panel read once, the output written once, read too when accumulating); the tile
@@ -1691,10 +2081,13 @@ namespace {
 hipStream_t st_of(void* s) { return (hipStream_t)s; }
 
 template <int EPI>
-int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, hipStream_t st, const ApplyPro* ap = nullptr) {
+int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, int64_t part_cap, hipStream_t st,
+                    const ApplyPro* ap = nullptr) {
   const int M = a.M, C = a.Nd, Kpad = a.Kpad;
   const int mtiles = (M + 63) / 64;
   dim3 grid(dgrad_gate_grid<EPI>(M, C, ap != nullptr), C / 64);
+  // one [2][C] partial row per workgroup column (blockIdx.x): refuse a slab shorter than the grid
+  if ((int64_t)grid.x * 2 * C > part_cap) return DFCSA_EINVAL;
   // [M][C] tensors read + written besides A (with the prologue: y read, dy written)
   const double moved = (EPI == EPI_GATE ? 6.0 : 7.0) + (ap ? 2.0 : 0.0);
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)M * Kpad + (double)a.N * Kpad + moved * (double)M * C));
@@ -1719,7 +2112,7 @@ extern "C" int dfcsa_dgrad_gate_parts(int M, int C) {
 extern "C" int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, const void* y3,
                                 const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
                                 const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
-                                float* partial, void* stream) {
+                                float* partial, int64_t partial_floats, void* stream) {
   if (M <= 0 || C <= 0 || C % 64 || C > 256 || Kpad != (C + 63) / 64 * 64) return DFCSA_EINVAL;
   if (!dy4 || !w4t || !y3 || !sc3 || !sh3 || !mean3 || !invstd3 || !local || !attn || !dlocal || !dattn || !dz3 ||
       !partial)
@@ -1733,7 +2126,7 @@ extern "C" int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, 
   e.y3 = (const bf16_t*)y3; e.local = (const bf16_t*)local; e.attn = (const bf16_t*)attn;
   e.sc = sc3; e.sh = sh3; e.mean = mean3; e.invstd = invstd3;
   e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.dz3 = (bf16_t*)dz3; e.part = partial;
-  return launch_gate_epi<EPI_GATE>(a, e, st_of(stream));
+  return launch_gate_epi<EPI_GATE>(a, e, partial_floats, st_of(stream));
 }
 
 extern "C" int dfcsa_dgrad_acc_relu_bn_parts(int M, int C) {
@@ -1743,7 +2136,7 @@ extern "C" int dfcsa_dgrad_acc_relu_bn_parts(int M, int C) {
 
 extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void* w3t, int Kpad, const void* y1,
                                        const float* sc1, const float* sh1, const float* mean1, const float* invstd1,
-                                       void* dlocal, void* dattn, float* partial, void* stream) {
+                                       void* dlocal, void* dattn, float* partial, int64_t partial_floats, void* stream) {
   if (M <= 0 || C <= 0 || C % 64 || C > 256 || Kpad != (C + 63) / 64 * 64) return DFCSA_EINVAL;
   if (!dy3 || !w3t || !y1 || !sc1 || !sh1 || !mean1 || !invstd1 || !dlocal || !dattn || !partial) return DFCSA_EINVAL;
   ConvGemmArgs a;
@@ -1756,7 +2149,7 @@ extern "C" int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void
   e.y3 = (const bf16_t*)y1;
   e.sc = sc1; e.sh = sh1; e.mean = mean1; e.invstd = invstd1;
   e.dlocal = (bf16_t*)dlocal; e.dattn = (bf16_t*)dattn; e.part = partial;
-  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, st_of(stream));
+  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, partial_floats, st_of(stream));
 }
 
 // dy = BatchNorm-backward apply of [src | y] (relu mask when sc != nullptr) formed in the A prologue
@@ -1765,7 +2158,7 @@ extern "C" int dfcsa_dgrad_gate_apply(int M, const void* dout, const void* y4, c
                                       const float* sc4, const float* sh4, void* dy4, const void* w4t,
                                       const void* y3, const float* sc3, const float* sh3, const float* mean3,
                                       const float* invstd3, const void* local, const void* attn, void* dlocal,
-                                      void* dattn, void* dz3, float* partial, void* stream) {
+                                      void* dattn, void* dz3, float* partial, int64_t partial_floats, void* stream) {
   const int C = 64, Kpad = 64;
   if (M <= 0 || !dout || !y4 || !gamma4 || !coef4 || !mean4 || !invstd4 || !dy4 || !w4t || !y3 || !sc3 || !sh3 ||
       !mean3 || !invstd3 || !local || !attn || !dlocal || !dattn || !dz3 || !partial || (!sc4 != !sh4))
@@ -1782,14 +2175,14 @@ extern "C" int dfcsa_dgrad_gate_apply(int M, const void* dout, const void* y4, c
   ApplyPro ap;
   ap.y = (const bf16_t*)y4; ap.gamma = gamma4; ap.coef = coef4; ap.mean = mean4; ap.invstd = invstd4;
   ap.sc = sc4; ap.sh = sh4; ap.dy = (bf16_t*)dy4;
-  return launch_gate_epi<EPI_GATE>(a, e, (hipStream_t)stream, &ap);
+  return launch_gate_epi<EPI_GATE>(a, e, partial_floats, (hipStream_t)stream, &ap);
 }
 
 extern "C" int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void* y3, const float* gamma3,
                                              const float* coef3, const float* mean3, const float* invstd3,
                                              void* dy3, const void* w3t, const void* y1, const float* sc1,
                                              const float* sh1, const float* mean1, const float* invstd1,
-                                             void* dlocal, void* dattn, float* partial, void* stream) {
+                                             void* dlocal, void* dattn, float* partial, int64_t partial_floats, void* stream) {
   const int C = 64, Kpad = 64;
   if (M <= 0 || !dz3 || !y3 || !gamma3 || !coef3 || !mean3 || !invstd3 || !dy3 || !w3t || !y1 || !sc1 || !sh1 ||
       !mean1 || !invstd1 || !dlocal || !dattn || !partial)
@@ -1808,7 +2201,7 @@ extern "C" int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void*
   std::memset(&ap, 0, sizeof(ap));
   ap.y = (const bf16_t*)y3; ap.gamma = gamma3; ap.coef = coef3; ap.mean = mean3; ap.invstd = invstd3;
   ap.dy = (bf16_t*)dy3;
-  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, (hipStream_t)stream, &ap);
+  return launch_gate_epi<EPI_ACC_RELU_BN>(a, e, partial_floats, (hipStream_t)stream, &ap);
 }
 
 extern "C" int dfcsa_dgrad_apply_parts(int M, int epi) {
@@ -1827,9 +2220,11 @@ int fwd_pro_grid(int M) {
 }
 
 template <int PRO, int C>
-int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, hipStream_t st) {
+int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, int64_t stats_cap, hipStream_t st) {
   const int mtiles = (a.M + 63) / 64;
   const int gx = fwd_pro_grid<PRO, C>(a.M);
+  // one [2][C] statistics row per workgroup: refuse a slab shorter than the grid
+  if ((int64_t)gx * 2 * C > stats_cap) return DFCSA_EINVAL;
   const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + (double)C * a.Kpad + moved * a.M * C));
   hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
@@ -1848,7 +2243,7 @@ extern "C" int dfcsa_fwd_pro_parts(int M, int C, int pro) {
 
 extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
                                      const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
-                                     void* fused, void* y4, float* stats4, void* stream) {
+                                     void* fused, void* y4, float* stats4, int64_t stats4_floats, void* stream) {
   if (M <= 0 || (C != 64 && C != 128) || Kpad != 3 * C || !y3 || !sc3 || !sh3 || !local || !attn || !w4 || !fused ||
       !y4 || !stats4)
     return DFCSA_EINVAL;
@@ -1860,14 +2255,14 @@ extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* 
   FwdPro pro;
   std::memset(&pro, 0, sizeof(pro));
   pro.sc0 = sc3; pro.sh0 = sh3; pro.out0 = (bf16_t*)fused;
-  return C == 64 ? launch_fwd_pro<PRO_GATE_FUSION, 64>(a, pro, (hipStream_t)stream)
-                 : launch_fwd_pro<PRO_GATE_FUSION, 128>(a, pro, (hipStream_t)stream);
+  return C == 64 ? launch_fwd_pro<PRO_GATE_FUSION, 64>(a, pro, stats4_floats, (hipStream_t)stream)
+                 : launch_fwd_pro<PRO_GATE_FUSION, 128>(a, pro, stats4_floats, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1,
                                          const float* sh1, const void* y2, const float* sc2, const float* sh2,
                                          const float* o, int P, const float* gamma, const void* w3, int Kpad,
-                                         const float* b3, void* local, void* attn, void* y3, float* stats3,
+                                         const float* b3, void* local, void* attn, void* y3, float* stats3, int64_t stats3_floats,
                                          void* stream) {
   const int64_t M = (int64_t)B * H * W;
   if (M <= 0 || M >= (1ll << 31) || C != 64 || Kpad != 128 || P <= 0 || !y1 || !sc1 || !sh1 || !y2 || !sc2 ||
@@ -1883,10 +2278,19 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
   pro.sc0 = sc1; pro.sh0 = sh1; pro.sc1 = sc2; pro.sh1 = sh2; pro.o = o; pro.gamma = gamma;
   pro.P = P; pro.H = H; pro.W = W;
   pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
-  return launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, (hipStream_t)stream);
+  return launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }
+
+extern "C" int dfcsa_get_tuning(int knob) {
+  switch (knob) {
+    case 1: return g_conv_cfg;
+    case 19: return g_halo_min_m;
+    case 20: return g_wgrad_halo;
+    default: return DFCSA_EINVAL;
+  }
+}
 
 extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 1) { g_conv_cfg = value; return 0; }
@@ -1907,5 +2311,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }
   if (knob == 14) { g_wgrad_nst = (value >= 2 && value <= 4) ? value : 2; return 0; }
+  if (knob == 19) { g_halo_min_m = value; return 0; }
+  if (knob == 20) { g_wgrad_halo = value; return 0; }
   return DFCSA_EINVAL;
 }

@@ -61,6 +61,7 @@ extern int g_wgrad_nst;
 extern int g_wgrad_noglds_f32small;
 extern int g_wgrad_big;
 extern int g_wgrad_wide_small;
+extern int g_wgrad_halo;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);
 extern int g_fra_generic;

@@ -18,6 +18,8 @@
 //
 // Replaces the weight half of ATen convolution_backward for the convolutions at reference
 // models/unet_dfc_sa_res.py:58, 66, 74, 81, 88 and ConvTranspose2d at :147-156.
+#include <cstring>
+
 #include "common.h"
 #include "dfcsa_internal.h"
 #include "small_gemm.h"
@@ -487,6 +489,239 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
                              (int*)smem);
 }
 
+// --------------------------------------------------------------------------------------------
+// 3x3 weight gradient on 2-D halo tiles (bf16).
+//
+//   dW[i][tap][c] = sum_m dY[m][i] * X[m shifted by tap][c]
+//
+// The row-tile kernel above stages, per 64-pixel K stage, a dY tile and ONE tap's shifted X rows:
+// dY is re-read once per column tile (9 taps x Cin / 128) and the input 9 times, 32 KB per
+// 2.1 MFLOP (64 flop/B).  Here a workgroup owns an output block of BI rows x (all 9 taps x one
+// 64-channel chunk of one source) and walks 128-pixel 2-D tiles (TW x TR, TW | W, rows of the
+// image-stacked grid) of its pixel range: per tile it DMAs the dY tile (128 x BI) and the X halo
+// ((TW+2) x (TR+2) x 64 channels) ONCE and runs all 9 taps from LDS -- the tap's B fragments are
+// transposed reads (ds_read_b64_tr_b16) of the halo rows p0(k) + dh*(TW+2) + dw, a tap leaving the
+// pixel's image reads a zero row.  128 x 576 x 128 x 2 flop per 55 KB (343 flop/B at BI = 128).
+// Pad pixels of a tile have zero dY rows (they add nothing).  Split-K over pixel ranges: each split
+// writes its [BI][9 taps x 64] block of the [split][NI][NJ] slab (one split: added straight into
+// the gradient), reduced in fixed split order by wgrad_reduce_kernel (deterministic).
+// 8 waves, one workgroup per CU (~130 KB LDS), dY and halo double-buffered one tile ahead.
+// --------------------------------------------------------------------------------------------
+constexpr int WH_MAXPIECE = 32;                  // halo <= 256 pixels (32 DMA pieces of 8)
+constexpr int WH_XB = WH_MAXPIECE * 1024;        // one halo image (64 channels = 128 B / pixel)
+
+struct WHaloTap {
+  int toff;   // dh*(TW+2) + dw
+  int dh;
+  int col;    // GEMM column of (tap, c = 0) for chunk 0: segment index * Cseg
+};
+struct WHaloGroup {
+  const void* ptr;
+  int ntaps;
+  WHaloTap tap[9];
+};
+struct WHaloArgs {
+  int M, NI, NJ, Cg, Cseg, BH, H, W;
+  int TW, TR, HW2, nhalo;
+  int tiles, tiles_x, per_split, splits;
+  int ngroups, nchunk, nI;
+  const void* g;
+  WHaloGroup grp[4];
+  float* slab;                                   // [splits][NI][NJ] (splits > 1)
+  int layout, ntaps, Ctot, Creal, ndst;          // direct add (splits == 1): dfcsa_wgrad_reduce's mapping
+  float* dst[3];
+};
+
+// transposed fragment read with explicit rows: lanes of group g = lane / 16 supply the addresses
+// of tile pixels kb + 8g + q (rows ra) and + 4 (rows rb), q = (lane % 16) / 4; 16 columns from col0
+template <int BW>
+__device__ __forceinline__ bf16x8_t tr_frag_rows(const char* img, int ra, int rb, int col0, int lane) {
+  const int p = lane & 3, blk = col0 >> 4;
+  const char* a0 = img + ra * (BW * 2) + blk_swz<BW>(ra, blk) * 32 + 8 * p;
+  const char* a1 = img + rb * (BW * 2) + blk_swz<BW>(rb, blk) * 32 + 8 * p;
+  v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
+  v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+  bf16x8_t f;
+  f[0] = lo[0]; f[1] = lo[1]; f[2] = lo[2]; f[3] = lo[3];
+  f[4] = hi[0]; f[5] = hi[1]; f[6] = hi[2]; f[7] = hi[3];
+  return f;
+}
+
+template <int BI>
+__global__ void __launch_bounds__(512, 1) wgrad_halo_kernel(const WHaloArgs a) {
+  using T = bf16_t;
+  constexpr int WM = BI / 32, WN = 8 / WM;       // waves: 32 output rows x (64 / WN) channels each
+  constexpr int WC = 64 / WN, FC = WC / 16;
+  constexpr int GB = 128 * BI * 2;               // dY image: 128 pixels x BI channels
+  constexpr int NIG = GB / 1024 / 8;             // dY DMA pieces per wave per tile
+  constexpr int NIX = WH_MAXPIECE / 8;           // halo DMA pieces per wave per tile
+  constexpr int CPR = BI / 8, RPI = 64 / CPR;    // dY: 16-B chunks per pixel row, rows per piece
+  constexpr int STAGE = GB + WH_XB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE + 256];
+  char* const zrow = smem + 2 * STAGE;           // a zero halo row
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave % WM, wn = wave / WM;
+  // task = ((split * ngroups + g) * nchunk + cc) * nI + it: the row tiles of one (g, cc, split)
+  // are neighbours (one XCD: they share the halo reads)
+  const int ntask = a.splits * a.ngroups * a.nchunk * a.nI;
+  const int L = xcd_remap(blockIdx.x, ntask);
+  if (L < 0) return;
+  const int it = L % a.nI;
+  const int cc = (L / a.nI) % a.nchunk;
+  const int g = (L / (a.nI * a.nchunk)) % a.ngroups;
+  const int split = L / (a.nI * a.nchunk * a.ngroups);
+  const int i0 = it * BI;
+  const int t_beg = split * a.per_split, t_end = min(a.tiles, t_beg + a.per_split);
+  const int TW = a.TW, HW2 = a.HW2, BH = a.BH, H = a.H, W = a.W, npx = a.TW * a.TR;
+  if (tid < 16) *(uint4*)(zrow + tid * 16) = make_uint4(0, 0, 0, 0);
+
+  // dY pieces: tile pixel r (row of the image), 16-B chunk (source-side swizzle of tr_frag<BI>)
+  int g_r[NIG], g_c[NIG];
+#pragma unroll
+  for (int q = 0; q < NIG; ++q) {
+    const int ins = q * 8 + wave;
+    const int r = ins * RPI + lane / CPR, pc = lane % CPR;
+    g_r[q] = r;
+    g_c[q] = i0 + ((blk_swz<BI>(r, pc >> 1) << 1) | (pc & 1)) * 8;
+  }
+  // halo pieces: halo pixel q = ins*8 + lane/8, chunk (source-side swizzle of tr_frag<64>)
+  int x_q[NIX], x_c[NIX];
+#pragma unroll
+  for (int q = 0; q < NIX; ++q) {
+    const int ins = q * 8 + wave;
+    const int hq = ins * 8 + (lane >> 3), pc = lane & 7;
+    x_q[q] = hq;
+    x_c[q] = cc * 64 + ((blk_swz<64>(hq, pc >> 1) << 1) | (pc & 1)) * 8;
+  }
+  const T* gsrc = (const T*)a.g;
+  const T* xsrc = (const T*)a.grp[g].ptr;
+  const void* zero = (const void*)g_wg_zero;
+  auto issue = [&](int tile, int buf) {
+    char* G = smem + buf * STAGE;
+    char* X = G + GB;
+    const int trow = tile / a.tiles_x, tcol = tile - trow * a.tiles_x;
+    const int r0 = trow * a.TR, c0 = tcol * TW;
+#pragma unroll
+    for (int q = 0; q < NIG; ++q) {
+      const int k = g_r[q], ty = k / TW, tx = k - ty * TW;
+      const bool ok = k < npx && r0 + ty < BH && g_c[q] < a.NI;
+      const void* src = ok ? (const void*)(gsrc + (size_t)((r0 + ty) * W + c0 + tx) * a.Cg + g_c[q]) : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(G + (q * 8 + wave) * 1024), 16, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NIX; ++q) {
+      const int hq = x_q[q], hy = hq / HW2, hx = hq - hy * HW2;
+      const int gr = r0 - 1 + hy, ix = c0 - 1 + hx;
+      const bool ok = hq < a.nhalo && gr >= 0 && gr < BH && ix >= 0 && ix < W;
+      const void* src = ok ? (const void*)(xsrc + (size_t)(gr * W + ix) * a.Cseg + x_c[q]) : zero;
+      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(X + (q * 8 + wave) * 1024), 16, 0, 0);
+    }
+  };
+
+  // B-operand rows of this lane: tile pixels k = kb + 8*(lane/16) + (lane%16)/4 (+4), kb = 32*ks
+  int pa[4], pb[4];
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks) {
+    const int k0 = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2), k1 = k0 + 4;
+    pa[ks] = (k0 / TW + 1) * HW2 + k0 % TW + 1;
+    pb[ks] = (k1 / TW + 1) * HW2 + k1 % TW + 1;
+  }
+
+  f32x4_t acc[9][2][FC];
+#pragma unroll
+  for (int t = 0; t < 9; ++t)
+#pragma unroll
+    for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) acc[t][fi][fc] = {0.f, 0.f, 0.f, 0.f};
+
+  const int ntap = a.grp[g].ntaps;
+  if (t_beg < t_end) issue(t_beg, 0);
+  for (int tile = t_beg, buf = 0; tile < t_end; ++tile, buf ^= 1) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tile + 1 < t_end) issue(tile + 1, buf ^ 1);
+    // rows of the image edges: a tap with dh = -1 (+1) leaving the pixel's image reads zeros
+    const int r0 = (tile / a.tiles_x) * a.TR;
+    unsigned up = 0, dn = 0;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int k0 = ks * 32 + 8 * (lane >> 4) + ((lane & 15) >> 2);
+      const int y0 = (r0 + k0 / TW) % H, y1 = (r0 + (k0 + 4) / TW) % H;
+      up |= (unsigned)(y0 == 0) << (2 * ks) | (unsigned)(y1 == 0) << (2 * ks + 1);
+      dn |= (unsigned)(y0 == H - 1) << (2 * ks) | (unsigned)(y1 == H - 1) << (2 * ks + 1);
+    }
+    const char* G = smem + buf * STAGE;
+    const char* X = G + GB;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8_t fa[2];
+#pragma unroll
+      for (int fi = 0; fi < 2; ++fi) fa[fi] = tr_frag<BI>(G, 32 * ks, wm * 32 + fi * 16, lane);
+#pragma unroll
+      for (int t = 0; t < 9; ++t) {
+        if (t < ntap) {
+          const WHaloTap tp = a.grp[g].tap[t];
+          const unsigned bad = tp.dh < 0 ? up : (tp.dh > 0 ? dn : 0u);
+          const bool oka = !((bad >> (2 * ks)) & 1), okb = !((bad >> (2 * ks + 1)) & 1);
+          const char* ia = oka ? X : zrow;
+          const char* ib = okb ? X : zrow;
+          const int ra = oka ? pa[ks] + tp.toff : 0, rb = okb ? pb[ks] + tp.toff : 0;
+#pragma unroll
+          for (int fc = 0; fc < FC; ++fc) {
+            // two image bases per lane: the zero row is its own image of one 128-B row
+            const int col = wn * WC + fc * 16;
+            bf16x8_t fb;
+            {
+              const int p = lane & 3, blk = col >> 4;
+              const char* a0 = ia + ra * 128 + blk_swz<64>(ra, blk) * 32 + 8 * p;
+              const char* a1 = ib + rb * 128 + blk_swz<64>(rb, blk) * 32 + 8 * p;
+              v4s_t lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a0);
+              v4s_t hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_v4s*)a1);
+              fb[0] = lo[0]; fb[1] = lo[1]; fb[2] = lo[2]; fb[3] = lo[3];
+              fb[4] = hi[0]; fb[5] = hi[1]; fb[6] = hi[2]; fb[7] = hi[3];
+            }
+#pragma unroll
+            for (int fi = 0; fi < 2; ++fi)
+              acc[t][fi][fc] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[fi], fb, acc[t][fi][fc], 0, 0, 0);
+          }
+        }
+      }
+    }
+  }
+
+  // ---- epilogue: acc[t][fi][fc][r] = dW[i0 + wm*32 + fi*16 + (lane/16)*4 + r][tap t][cc*64 + col] ----
+#pragma unroll
+  for (int t = 0; t < 9; ++t) {
+    if (t >= ntap) continue;
+    const int jb = a.grp[g].tap[t].col + cc * 64;
+#pragma unroll
+    for (int fi = 0; fi < 2; ++fi)
+#pragma unroll
+      for (int fc = 0; fc < FC; ++fc) {
+        const int j = jb + wn * WC + fc * 16 + (lane & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int i = i0 + wm * 32 + fi * 16 + (lane >> 4) * 4 + r;
+          if (i >= a.NI) continue;
+          const float v = acc[t][fi][fc][r];
+          if (a.splits > 1) {
+            a.slab[((size_t)split * a.NI + i) * a.NJ + j] = v;
+          } else {
+            // dfcsa_wgrad_reduce's layout-0 mapping: row i -> dst[i / rows], column j -> (tap, cin)
+            const int rows = a.NI / a.ndst, d = i / rows, rr = i - d * rows;
+            const int tap = j / a.Ctot, cin = j - tap * a.Ctot;
+            if (cin < a.Creal && tap < a.ntaps) {
+              float* dst = d == 0 ? a.dst[0] : (d == 1 ? a.dst[1] : a.dst[2]);
+              dst[((int64_t)rr * a.Creal + cin) * a.ntaps + tap] += v;
+            }
+          }
+        }
+      }
+  }
+}
+
 // 64 output elements per workgroup, SUB split-ranges per element (threads sub*64 + el: each group
 // of 64 threads reads 64 consecutive elements of one split -> coalesced; SUB grows with the split
 // count so that high-split launches get enough threads), 8 loads in flight per thread; the SUB
@@ -593,6 +828,67 @@ bool wide_j(const WgradArgs& a) {
   return a.NI <= 64 && ((a.NJ >= 512 && !g_wgrad_narrow) || (g_wgrad_wide_small && a.NJ > 128 && a.NJ <= 256));
 }
 
+// The halo launch of a bf16 3x3 weight gradient (layout 0, one dY tensor); false if it does not
+// apply.  BI = 64 for NI <= 64, else 128; splits = pixel ranges so that ~256 workgroups run.
+bool whalo_plan(const WgradArgs& a, int dtype, int layout, WHaloArgs* h, int* bi) {
+  if (!g_wgrad_halo || dtype != DFCSA_DT_BF16 || layout != 0 || a.ng != 1 || a.stride != 1 || a.Ho != a.Hi ||
+      a.Wo != a.Wi || a.Cseg % 64 || a.Cg % 8 || a.M < 32768)
+    return false;
+  if ((int64_t)a.M * a.Cseg >= (1ll << 31) || (int64_t)a.M * a.Cg >= (1ll << 31)) return false;
+  std::memset(h, 0, sizeof(*h));
+  bool shifted = false;
+  for (int i = 0; i < a.nseg; ++i) {
+    const ConvSeg& s = a.seg[i];
+    if (s.dh < -1 || s.dh > 1 || s.dw < -1 || s.dw > 1) return false;
+    shifted |= (s.dh || s.dw);
+    int g = 0;
+    while (g < h->ngroups && h->grp[g].ptr != s.ptr) ++g;
+    if (g == h->ngroups) {
+      if (g == 4) return false;
+      h->grp[g].ptr = s.ptr;
+      h->ngroups++;
+    }
+    WHaloGroup& G = h->grp[g];
+    if (G.ntaps == 9) return false;
+    G.tap[G.ntaps].dh = s.dh;
+    G.tap[G.ntaps].toff = s.dw;          // + dh*(TW+2) below
+    G.tap[G.ntaps].col = i * a.Cseg;
+    G.ntaps++;
+  }
+  if (!shifted) return false;
+  const int W = a.Wo, BH = a.M / a.Wo;
+  int bTW = 0, bTR = 0, bHalo = 1 << 30;
+  double best = 0.0;
+  for (int TW = 4; TW <= 64 && TW <= W; ++TW) {
+    if (W % TW) continue;
+    const int TR = 128 / TW;
+    const int halo = (TW + 2) * (TR + 2);
+    const int pmax = (127 / TW + 2) * (TW + 2) + TW + 1;   // furthest halo row a (pad) lane reads
+    if (halo > WH_MAXPIECE * 8 || pmax >= WH_MAXPIECE * 8) continue;
+    const int tiles = (W / TW) * ((BH + TR - 1) / TR);
+    const double eff = (double)a.M / ((double)tiles * 128.0);
+    if (eff > best + 1e-9 || (eff > best - 1e-9 && halo < bHalo)) { best = eff; bTW = TW; bTR = TR; bHalo = halo; }
+  }
+  if (best < 0.85) return false;
+  *bi = a.NI <= 64 ? 64 : 128;
+  h->M = a.M; h->NI = a.NI; h->NJ = a.NJ; h->Cg = a.Cg; h->Cseg = a.Cseg; h->BH = BH; h->H = a.Ho; h->W = W;
+  h->TW = bTW; h->TR = bTR; h->HW2 = bTW + 2; h->nhalo = bHalo;
+  h->tiles_x = W / bTW;
+  h->tiles = h->tiles_x * ((BH + bTR - 1) / bTR);
+  h->nchunk = a.Cseg / 64;
+  h->nI = (a.NI + *bi - 1) / *bi;
+  const int groups = h->ngroups * h->nchunk * h->nI;
+  int S = (256 + groups - 1) / groups;
+  if (S > h->tiles / 2) S = h->tiles / 2;
+  if (S < 1) S = 1;
+  h->per_split = (h->tiles + S - 1) / S;
+  h->splits = (h->tiles + h->per_split - 1) / h->per_split;
+  for (int g = 0; g < h->ngroups; ++g)
+    for (int t = 0; t < h->grp[g].ntaps; ++t) h->grp[g].tap[t].toff += h->grp[g].tap[t].dh * h->HW2;
+  h->g = a.g_ptr[0];
+  return true;
+}
+
 template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   constexpr int BJ = 128;
@@ -642,6 +938,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_wgrad_halo = 0;      // knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel (off: slower so far)
 int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6; 0 = automatic)
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
 int g_wgrad_narrow = 1;    // 0 = allow the 64x256 wgrad tile (dfcsa_set_tuning knob 8; measured slower on the L1 3x3)
@@ -672,6 +969,33 @@ void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
 }
 
 extern "C" int dfcsa_wgrad_fuse_max(void) { return g_wgrad_fuse_max; }
+
+namespace {
+void desc_to_args(const dfcsa_wgrad_desc* d, WgradArgs& a) {
+  std::memset(&a, 0, sizeof(a));
+  a.M = d->M; a.ng = d->ng; a.Cg = d->Cg; a.NI = d->ng * d->Cg;
+  for (int i = 0; i < 3; ++i) a.g_ptr[i] = i < d->ng ? d->g_ptr[i] : nullptr;
+  a.nseg = d->nseg; a.Cseg = d->Cseg; a.NJ = d->nseg * d->Cseg;
+  for (int i = 0; i < d->nseg; ++i) { a.seg[i].ptr = d->seg_ptr[i]; a.seg[i].dh = d->seg_dh[i]; a.seg[i].dw = d->seg_dw[i]; }
+  a.Ho = d->Ho; a.Wo = d->Wo; a.Hi = d->Hi; a.Wi = d->Wi; a.stride = d->stride;
+}
+}  // namespace
+
+extern "C" int dfcsa_wgrad_plan_desc(const dfcsa_wgrad_desc* d, int* splits, int* mchunk, int64_t* slab_floats) {
+  if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->ng < 1 || d->ng > 3 || !splits || !mchunk)
+    return DFCSA_EINVAL;
+  WgradArgs a;
+  desc_to_args(d, a);
+  WHaloArgs h;
+  int bi;
+  if (whalo_plan(a, d->dtype, d->layout, &h, &bi)) {
+    *splits = h.splits;
+    *mchunk = h.per_split * 128;
+    if (slab_floats) *slab_floats = h.splits > 1 ? (int64_t)h.splits * a.NI * a.NJ : 0;
+    return 0;
+  }
+  return dfcsa_wgrad_plan(d->M, a.NI, a.NJ, d->dtype, splits, mchunk, slab_floats);
+}
 
 extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk, int64_t* slab_floats) {
   if (M <= 0 || NI <= 0 || NJ <= 0 || !splits || !mchunk) return DFCSA_EINVAL;
@@ -733,6 +1057,7 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   a.fuse = d->ndst > 0 && (d->splits == 1 ||
                            (g_wgrad_fuse_all >= 0 && (d->splits <= g_wgrad_fuse_max || g_wgrad_fuse_all > 0)));
   if (!a.fuse && !d->slab) return DFCSA_EINVAL;
+  if (!a.fuse && d->slab_floats < (int64_t)d->splits * a.NI * a.NJ) return DFCSA_EINVAL;
   a.cnt = nullptr;
   if (a.fuse && d->splits > 1) {
     // ticket counters: a ring region per launch, so launches in flight on other streams never
@@ -751,6 +1076,25 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   double flops = 2.0 * a.M * a.NI * a.NJ;
   ProfScope prof(DFCSA_PROF_WGRAD, st, flops);   // the class covers the reduction launch too
+  {
+    WHaloArgs h;
+    int bi;
+    if (d->ndst > 0 && whalo_plan(a, d->dtype, d->layout, &h, &bi) && d->splits == h.splits &&
+        d->mchunk == h.per_split * 128) {
+      if (h.splits > 1 && (!d->slab || d->slab_floats < (int64_t)h.splits * a.NI * a.NJ)) return DFCSA_EINVAL;
+      h.slab = d->slab;
+      h.layout = d->layout; h.ntaps = d->ntaps; h.Ctot = d->Ctot; h.Creal = d->Creal; h.ndst = d->ndst;
+      for (int i = 0; i < 3; ++i) h.dst[i] = a.dst[i];
+      dim3 grid(xcd_pad(h.splits * h.ngroups * h.nchunk * h.nI));
+      if (bi == 64) hipLaunchKernelGGL(wgrad_halo_kernel<64>, grid, dim3(512), 0, st, h);
+      else hipLaunchKernelGGL(wgrad_halo_kernel<128>, grid, dim3(512), 0, st, h);
+      DFCSA_CHECK_LAUNCH();
+      if (h.splits > 1)
+        return launch_reduce(d->slab, h.splits, a.NI, a.NJ, d->layout, d->ntaps, d->Ctot, d->Creal, d->ndst, a.dst[0],
+                             a.dst[1], a.dst[2], st);
+      return 0;
+    }
+  }
   if (d->dtype != DFCSA_DT_BF16 && a.M <= 4096 && a.ng == 1 && a.nseg == 1 && !a.seg[0].dh && !a.seg[0].dw &&
       a.stride == 1 && d->ndst > 0 && a.Ho == a.Hi && a.Wo == a.Wi && !g_wgrad_noglds_f32small) {
     hipLaunchKernelGGL(small_wgrad_f32_kernel, dim3((a.NI + 15) / 16, (a.NJ + 63) / 64), dim3(256), 0, st, a);

@@ -64,7 +64,7 @@ class ConvDesc(ctypes.Structure):
                 ("stride", ctypes.c_int), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("mode", ctypes.c_int), ("ndest", ctypes.c_int), ("dest", ctypes.c_void_p * 3),
                 ("Nd", ctypes.c_int), ("accumulate", ctypes.c_int), ("stats", ctypes.c_void_p),
-                ("Hout", ctypes.c_int), ("Wout", ctypes.c_int)]
+                ("Hout", ctypes.c_int), ("Wout", ctypes.c_int), ("stats_floats", ctypes.c_int64)]
 
 
 class WgradDesc(ctypes.Structure):
@@ -75,7 +75,8 @@ class WgradDesc(ctypes.Structure):
                 ("Ho", ctypes.c_int), ("Wo", ctypes.c_int), ("Hi", ctypes.c_int), ("Wi", ctypes.c_int),
                 ("stride", ctypes.c_int), ("slab", ctypes.c_void_p), ("splits", ctypes.c_int),
                 ("mchunk", ctypes.c_int), ("layout", ctypes.c_int), ("ntaps", ctypes.c_int), ("Ctot", ctypes.c_int),
-                ("Creal", ctypes.c_int), ("ndst", ctypes.c_int), ("dst", ctypes.c_void_p * 3)]
+                ("Creal", ctypes.c_int), ("ndst", ctypes.c_int), ("dst", ctypes.c_void_p * 3),
+                ("slab_floats", ctypes.c_int64)]
 
 
 class PackEntry(ctypes.Structure):

@@ -18,7 +18,7 @@ from . import ops
 from ._lib import call
 from .block import grad_of
 from .ddp import notify_grads_ready
-from .ops import P, dt, rup, stream
+from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
 
 
@@ -85,7 +85,7 @@ class SumOut(torch.autograd.Function):
         nte = ops.ntiles_ew(M, C)
         part = torch.empty(nte * C, device=dout.device, dtype=torch.float32)
         dres = torch.empty_like(res) if ctx.needs_input_grad[4] else None
-        call("dfcsa_bwd_sum_out", dt(ctx.dtype), M, C, P(dout), P(res), P(ctx.rs), P(dres), P(part), stream())
+        call("dfcsa_bwd_sum_out", dt(ctx.dtype), M, C, P(dout), P(res), P(ctx.rs), P(dres), *S(part), stream())
         call("dfcsa_sum_into", P(part), nte * C, P(grad_of(ctx.rs)), stream())
         ctx.res = None
         return None, None, dout, (dout if ctx.has_b else None), dres

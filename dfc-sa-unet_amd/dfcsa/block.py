@@ -27,7 +27,7 @@ import torch.nn as nn
 from . import _lib, fra, ops
 from ._lib import call
 from .ddp import notify_grads_ready
-from .ops import P, dt, rup, stream
+from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
 from .streams import join_branch, on_branch, on_side
 
@@ -115,21 +115,21 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
     st2 = stats(N2)
-    ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
-                  [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
+    nt2 = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
+                        [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
     # the pooled attention chain (bn2 statistics -> pool -> q/k/v -> softmax core) runs on the
     # branch stream beside the 3x3 conv (streams.on_branch)
     branch = not fullres and ops._SYNC_BN is None
     with on_branch(dev, branch, y2, st2):
-        bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt, C, N2, M, training)
+        bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
         if not fullres:
             Pp = pool_size
             lsa_saved = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
     y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st1 = stats(C)
-    ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
-                  bias=conv1.bias, stats=st1)
-    bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt, C, C, M, training)
+    nt1 = ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
+                        bias=conv1.bias, stats=st1)   # (3x3 halo tiles: one statistics row per 2-D tile)
+    bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt1 if training else nt, C, C, M, training)
     join_branch(dev, branch, bn2, None if fullres else lsa_saved)
 
     if fullres:
@@ -155,15 +155,15 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # per workgroup)
         nt3 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 1)
         call("dfcsa_local_attn_gate_fwd", B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2), P(bn2.scale),
-             P(bn2.shift), P(o), Pp, P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), P(st3),
+             P(bn2.shift), P(o), Pp, P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), *S(st3),
              stream())
     else:
         if not fullres:
             call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
                  P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
         # ---- gate conv ----
-        ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
-                      bias=conv3.bias, stats=st3)
+        nt3 = ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
+                            bias=conv3.bias, stats=st3) or nt
     bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt3, C, C, M, training)
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
@@ -174,12 +174,12 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # statistics row per workgroup)
         nt4 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 0)
         call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4,
-             P(conv4.bias), P(fused), P(y4), P(st4), stream())
+             P(conv4.bias), P(fused), P(y4), *S(st4), stream())
     else:
         call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
              stream())
-        ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C, [y4],
-                      C, bias=conv4.bias, stats=st4)
+        nt4 = ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C,
+                            [y4], C, bias=conv4.bias, stats=st4) or nt
     bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt4, C, C, M, training)
     out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     pooled_out = None
@@ -284,7 +284,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             part = torch.empty(nbo * 3 * C, device=dev, dtype=f32)
             call("dfcsa_bwd_block_out_pool", T, B, H, W, C, P(dskip), P(s.out), P(dpool.contiguous()), P(s.y4),
                  P(bn4.scale), P(bn4.shift), P(bn4.mean), P(bn4.invstd), P(s.res), P(blk.res_scale), P(dout),
-                 P(dres), P(part), stream())
+                 P(dres), *S(part), stream())
         else:
             dout = dskip if dskip is not None else torch.zeros_like(s.y4)
             if dpool is not None:
@@ -298,7 +298,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         # (dz4 = relu'(bn4 y4) * dout is not materialised: the apply recomputes it)
         part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
         call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean),
-             P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), P(part), stream())
+             P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), *S(part), stream())
     coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
                                extra=grad_of(blk.res_scale))
     KpC = rup(C, ops.KALIGN)
@@ -320,7 +320,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         part = torch.empty(npart * 2 * C, device=dev, dtype=f32)
         call("dfcsa_dgrad_gate_apply", M, P(dout), P(s.y4), P(bn4m.weight), P(coef), P(bn4.mean), P(bn4.invstd),
              P(bn4.scale), P(bn4.shift), P(dy4), P(W4t), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
-             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), *S(part), stream())
     else:
         dy4 = ops.bn_bwd_apply_relu(dtype, dout, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
     # fusion conv: dW4 (side stream) and d[fused, local, attn]
@@ -335,7 +335,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         npart = _lib.LIB.dfcsa_dgrad_gate_parts(M, C)
         part = torch.empty(npart * 2 * C, device=dev, dtype=f32)
         call("dfcsa_dgrad_gate", M, C, P(dy4), P(W4t), KpC, P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
-             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), *S(part), stream())
         del dy4
     else:
         npart = nte
@@ -344,7 +344,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         del dy4
         part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
         call("dfcsa_bwd_gate", T, M, C, P(dfused), P(s.y3), P(bn3.scale), P(bn3.shift), P(bn3.mean),
-             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), P(part), stream())
+             P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), *S(part), stream())
         del dfused
     coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn3m.weight), grad_of(bn3m.bias))
     W3t = s.pk["W3t"]
@@ -356,7 +356,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         part1 = torch.empty(npart1 * 2 * C, device=dev, dtype=f32)
         call("dfcsa_dgrad_acc_relu_bn_apply", M, P(dz3), P(s.y3), P(bn3m.weight), P(coef), P(bn3.mean),
              P(bn3.invstd), P(dy3), P(W3t), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean), P(bn1.invstd),
-             P(dlocal), P(dattn), P(part1), stream())
+             P(dlocal), P(dattn), *S(part1), stream())
         del dz3
     else:
         dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
@@ -371,7 +371,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         npart1 = _lib.LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
         part1 = torch.empty(npart1 * 2 * C, device=dev, dtype=f32)
         call("dfcsa_dgrad_acc_relu_bn", M, C, P(dy3), P(W3t), KpC, P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
-             P(bn1.invstd), P(dlocal), P(dattn), P(part1), stream())
+             P(bn1.invstd), P(dlocal), P(dattn), *S(part1), stream())
     else:
         ops.conv_gemm(dtype, [(dy3, 0, 0)], C, grid, hw, W3t, KpC, 2 * C, [dlocal, dattn], C, accumulate=True)
     del dy3
@@ -387,7 +387,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
             s.fra = None
             call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-                 P(bn2.invstd), None, P(part2), stream())
+                 P(bn2.invstd), None, *S(part2), stream())
             coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
             dy2 = ops.bn_bwd_apply_relu(dtype, da, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
             del da
@@ -396,7 +396,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
             # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
             call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
-                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, None, P(part2), stream())
+                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, None, *S(part2), stream())
             coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
             dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
                                          grad_of(conv2.bias))
@@ -410,7 +410,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     else:
         part, npart = torch.empty(nte * 2 * C, device=dev, dtype=f32), nte
         call("dfcsa_bwd_relu_bn", T, M, C, P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
-             P(bn1.invstd), None, P(part), stream())
+             P(bn1.invstd), None, *S(part), stream())
     coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
     dy1 = ops.bn_bwd_apply_relu(dtype, dlocal, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
     del dlocal
@@ -545,7 +545,7 @@ class LSAFunction(torch.autograd.Function):
         dx = torch.empty_like(x)
         part = torch.empty(ops.ntiles_ew(B * H * W, C) * 2 * C, device=dev, dtype=torch.float32)
         call("dfcsa_bwd_attn_entry", dt(ctx.dtype), B, H, W, C, P(g), P(dpooled), ctx.ps, P(x), P(one), P(zero),
-             P(zero), P(one), 0, P(dx), P(part), stream())
+             P(zero), P(one), 0, P(dx), *S(part), stream())
         ctx.saved = None
         return (None, None, None, dx, *([None] * ctx.np))
 

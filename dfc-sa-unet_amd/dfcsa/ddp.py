@@ -34,7 +34,9 @@ class GradBucketReducer:
         self.group = group
         self.world = dist.get_world_size(group)
         self.flat = model.flat_params()
-        units = model.grad_units()  # [(module, lo, hi)] in flat-buffer order
+        # [(module, lo, hi)] in flat-buffer order; a model without per-module units is one unit
+        # (its single bucket is reduced by finish())
+        units = model.grad_units() if hasattr(model, "grad_units") else [(model, 0, self.flat.numel)]
         self.unit_of = {}
         self.buckets = []           # [(lo, hi, n_units)]
         cap = int(bucket_mb * (1 << 20) / 4)
@@ -82,6 +84,10 @@ class GradBucketReducer:
         main = torch.cuda.current_stream() if self.flat.grad.is_cuda else None
         if main is None:
             return dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        if dist.get_backend(self.group) == "gloo":
+            # CPU-transport rehearsal (several ranks on one GPU): host-staged and synchronous
+            streams.join()
+            return _host_allreduce(self.flat.grad[lo:hi], dist.ReduceOp.SUM, self.group)
         side = streams.side_stream(self.flat.grad.device)
         side.wait_stream(main)
         with torch.cuda.stream(side):
@@ -91,15 +97,19 @@ class GradBucketReducer:
         """Ensure every bucket has been reduced (launch stragglers), make the current stream wait.
         With ``loss``: returns a device scalar that is NaN iff some rank's loss is NaN (else 0),
         for ``FusedSGD.step(skip_if_nan=...)``."""
-        if self._pending is None:
-            return None
-        for j in range(len(self._works), len(self.buckets)):
-            lo, hi, _ = self.buckets[j]
-            self._works.append(self._launch(lo, hi))
+        if self._pending is not None:
+            for j in range(len(self._works), len(self.buckets)):
+                lo, hi, _ = self.buckets[j]
+                self._works.append(self._launch(lo, hi))
         flag = None
         if loss is not None:
+            # the NaN agreement runs whether or not the reducer was armed: a caller handing the
+            # result to FusedSGD.step(skip_if_nan=...) must never get None for a NaN loss
             flag = torch.isnan(loss.detach().reshape(1)).float()
-            self._works.append(dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
+            if flag.is_cuda and dist.get_backend(self.group) == "gloo":
+                self._works.append(_host_allreduce(flag, dist.ReduceOp.MAX, self.group))
+            else:
+                self._works.append(dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
         if self.flat.grad.is_cuda:
             streams.join()
         for w in self._works:
@@ -117,7 +127,12 @@ class GradBucketReducer:
         if not bufs:
             return
         flat = torch.cat([b.reshape(-1) for b in bufs])
-        dist.broadcast(flat, src=src, group=self.group)
+        if flat.is_cuda and dist.get_backend(self.group) == "gloo":
+            h = flat.cpu()
+            dist.broadcast(h, src=src, group=self.group)
+            flat.copy_(h)
+        else:
+            dist.broadcast(flat, src=src, group=self.group)
         o = 0
         for b in bufs:
             b.copy_(flat[o:o + b.numel()].view_as(b))
@@ -126,6 +141,33 @@ class GradBucketReducer:
     @property
     def grad_scale(self):
         return 1.0 / self.world
+
+
+class _Done:
+    def wait(self):
+        return True
+
+
+def _host_allreduce(t, op, group):
+    """all_reduce of a device tensor through the host (gloo carries CPU tensors); synchronous."""
+    h = t.cpu()
+    dist.all_reduce(h, op=op, group=group)
+    t.copy_(h)
+    return _Done()
+
+
+def allreduce_stats(stats, group=None):
+    """The Trainer's per-step metric vector (dfcsa.loss stats, fp32[8]) summed over the ranks, the
+    loss entry averaged: IoU / Dice from the summed counts are the global batch's, the loss the
+    mean of the per-replica losses (the 4-scalar metric all-reduce)."""
+    world = dist.get_world_size(group)
+    out = stats.detach().clone()
+    if out.is_cuda and dist.get_backend(group) == "gloo":
+        _host_allreduce(out, dist.ReduceOp.SUM, group)
+    else:
+        dist.all_reduce(out, op=dist.ReduceOp.SUM, group=group)
+    out[0] /= world
+    return out
 
 
 def notify_grads_ready(module):

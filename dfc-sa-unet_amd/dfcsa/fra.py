@@ -18,7 +18,7 @@ import torch
 
 from . import _lib, ops
 from ._lib import call
-from .ops import P, dt, rup, stream
+from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
 
 
@@ -92,7 +92,7 @@ def core_backward(mod, saved, dy, dtype, pk):
                          _grad_of(mod.value_conv.weight)], 1, Cq, C, layout=2)
     nt = ops.ntiles_ew(M, Jp)
     part = torch.empty(nt * Jp, device=dev, dtype=f32)
-    call("dfcsa_channel_sum", T, M, Jp, P(dqkv), P(part), stream())
+    call("dfcsa_channel_sum", T, M, Jp, P(dqkv), *S(part), stream())
     dbv = _grad_of(mod.value_conv.bias)
     tail = dbv if Jp == J else torch.zeros(Jp - 2 * Cq, device=dev, dtype=f32)
     call("dfcsa_slab_colsum3", P(part), nt, Jp, Cq, Cq, P(_grad_of(mod.query_conv.bias)),

@@ -29,6 +29,12 @@ def dt(dtype):
     raise TypeError(f"dfcsa supports bf16/fp32 activations, got {dtype}")
 
 
+def S(t):
+    """(device pointer, capacity in elements) of a slab tensor for the C ABI's `ptr, ptr_floats`
+    argument pairs (None -> NULL, 0)."""
+    return (None, 0) if t is None else (P(t), t.numel())
+
+
 def P(t):
     """device pointer of a tensor (None -> NULL); rejects host tensors."""
     if t is None:
@@ -53,7 +59,9 @@ def ntiles_ew(M, C):
 # --------------------------------------------------------------------------- GEMMs
 def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=None, stride=1,
               mode=0, accumulate=False, stats=None, out_hw=(0, 0)):
-    """segs: list of (tensor, dh, dw); grid: (B, Ho, Wo) output pixel grid; in_hw: (Hi, Wi)."""
+    """segs: list of (tensor, dh, dw); grid: (B, Ho, Wo) output pixel grid; in_hw: (Hi, Wi).
+    With `stats` (>= ceil(M/64) rows of [2][N] fp32) returns the number of statistics rows the
+    launch wrote (ntiles for bn_finalize; the 3x3 halo-tile kernel writes one per 2-D tile)."""
     B, Ho, Wo = grid
     d = _lib.ConvDesc()
     d.dtype = dt(dtype)
@@ -76,17 +84,21 @@ def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=N
     d.Nd = Nd
     d.accumulate = int(bool(accumulate))
     d.stats = P(stats)
+    d.stats_floats = stats.numel() if stats is not None else 0
     d.Hout, d.Wout = out_hw
     call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
+    if stats is not None:   # statistics rows written (the ntiles of bn_finalize)
+        return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d))
+    return None
 
 
-def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride):
+def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride, layout=0):
+    """The weight-gradient descriptor and its launch plan (dfcsa_wgrad_plan_desc: the 3x3 halo-tile
+    kernel plans its own pixel splits)."""
     B, Ho, Wo = grid
     M = B * Ho * Wo
     NI, NJ = len(gs) * Cg, len(segs) * Cseg
     splits, mchunk, floats = ctypes.c_int(), ctypes.c_int(), ctypes.c_int64()
-    call("dfcsa_wgrad_plan", M, NI, NJ, dt(dtype), ctypes.addressof(splits), ctypes.addressof(mchunk),
-         ctypes.addressof(floats))
     d = _lib.WgradDesc()
     d.dtype = dt(dtype)
     d.M, d.ng, d.Cg = M, len(gs), Cg
@@ -100,6 +112,9 @@ def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride):
     d.Ho, d.Wo = Ho, Wo
     d.Hi, d.Wi = in_hw
     d.stride = stride
+    d.layout = layout
+    call("dfcsa_wgrad_plan_desc", ctypes.addressof(d), ctypes.addressof(splits), ctypes.addressof(mchunk),
+         ctypes.addressof(floats))
     d.splits, d.mchunk = splits.value, mchunk.value
     return d, floats.value, NI, NJ
 
@@ -107,9 +122,10 @@ def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride):
 def wgrad(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride=1):
     """Split-K partials only: returns (slab, splits, NI, NJ) with slab [splits][NI][NJ] fp32 (the
     caller reduces with wgrad_reduce)."""
-    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
+    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride, layout=-1)
     slab = torch.empty(floats, device=gs[0].device, dtype=torch.float32)
     d.slab = P(slab)
+    d.slab_floats = slab.numel()
     d.ndst = 0
     call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
     return slab, d.splits, NI, NJ
@@ -124,9 +140,10 @@ def wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts):
 def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, Creal, layout=0, stride=1):
     """grads[d] += the weight gradient in the reference layout, in one dfcsa_conv_wgrad call (the
     split-K reduction runs inside the kernel, or as its second launch at high split counts)."""
-    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride)
+    d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride, layout=layout)
     slab = torch.empty(floats, device=gs[0].device, dtype=torch.float32) if d.splits > 1 else None
     d.slab = P(slab)
+    d.slab_floats = slab.numel() if slab is not None else 0
     d.layout, d.ntaps, d.Ctot, d.Creal, d.ndst = layout, ntaps, Ctot, Creal, len(grads)
     for i, t in enumerate(grads):
         d.dst[i] = P(t)
@@ -274,7 +291,7 @@ def bn_bwd_apply(dtype, dz, y, bn, gamma, coef, bias_grad):
         nt = ntiles_ew(M, C)
         part = torch.empty(nt * C, device=dz.device, dtype=torch.float32)
     call("dfcsa_bn_bwd_apply", dt(dtype), M, C, P(dz), P(y), P(bn.mean), P(bn.invstd), P(gamma), P(coef), P(dy),
-         P(part), stream())
+         *S(part), stream())
     if part is not None:
         colsum_into(part, nt, C, bias_grad)
     return dy
@@ -290,7 +307,7 @@ def bn_bwd_apply_relu(dtype, dact, y, bn, gamma, coef, bias_grad):
         nt = ntiles_ew(M, C)
         part = torch.empty(nt * C, device=dact.device, dtype=torch.float32)
     call("dfcsa_bn_bwd_apply_relu", dt(dtype), M, C, P(dact), P(y), P(bn.scale), P(bn.shift), P(bn.mean),
-         P(bn.invstd), P(gamma), P(coef), P(dy), P(part), stream())
+         P(bn.invstd), P(gamma), P(coef), P(dy), *S(part), stream())
     if part is not None:
         colsum_into(part, nt, C, bias_grad)
     return dy
@@ -307,7 +324,7 @@ def bn_bwd_apply_entry(dtype, dattn, dpooled, P_, y, bn, relu, gamma, coef, bias
         nt = ntiles_ew(M, C)
         part = torch.empty(nt * C, device=dattn.device, dtype=torch.float32)
     call("dfcsa_bn_bwd_apply_entry", dt(dtype), B, H, W, C, P(dattn), P(dpooled), P_, P(y), P(bn.scale),
-         P(bn.shift), P(bn.mean), P(bn.invstd), int(relu), P(gamma), P(coef), P(dy), P(part), stream())
+         P(bn.shift), P(bn.mean), P(bn.invstd), int(relu), P(gamma), P(coef), P(dy), *S(part), stream())
     if part is not None:
         colsum_into(part, nt, C, bias_grad)
     return dy
@@ -322,7 +339,7 @@ def channel_sum_into(dtype, x, out):
     M, C = x.numel() // x.shape[-1], x.shape[-1]
     nt = ntiles_ew(M, C)
     part = torch.empty(nt * C, device=x.device, dtype=torch.float32)
-    call("dfcsa_channel_sum", dt(dtype), M, C, P(x), P(part), stream())
+    call("dfcsa_channel_sum", dt(dtype), M, C, P(x), *S(part), stream())
     colsum_into(part, nt, C, out)
 
 

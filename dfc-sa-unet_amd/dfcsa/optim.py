@@ -109,7 +109,13 @@ class FusedSGD(torch.optim.Optimizer):
         params = self.param_groups[0]["params"]
         bufs = [self.state[p].get("momentum_buffer") if p in self.state else None for p in params]
         if not all(b is not None for b in bufs):
-            return   # no momentum yet (checkpoint taken before the first step): start fresh
+            # no momentum in the checkpoint (taken before the first step): start fresh, as
+            # torch.optim.SGD does from an empty state -- forget any momentum already held
+            self._pending_mom = None
+            if self._mom is not None:
+                self._mom.zero_()
+                self._mom_init.zero_()
+            return
         flat = getattr(params[0], "_dfcsa_flat", None)
         self._pending_mom = {id(p): b.detach().clone() for p, b in zip(params, bufs)}
         self._flat = None

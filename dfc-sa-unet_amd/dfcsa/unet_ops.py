@@ -11,7 +11,7 @@ from . import ops
 from ._lib import call
 from .block import grad_of, raise_eval_backward
 from .ddp import notify_grads_ready
-from .ops import P, dt, rup, stream
+from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
 
 
@@ -60,9 +60,9 @@ class ConvBNReLU(torch.autograd.Function):
         nt = ops.ntiles_gemm(M)
         st = torch.empty(nt * 2 * C, device=dev, dtype=torch.float32) if training else None
         y = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-        ops.conv_gemm(dtype, _taps(xs, k), Cs, (B, H, W), (H, W), pk["Wf"], rup(k * k * Cin_p, ops.KALIGN), C, [y],
-                      C, bias=conv.bias, stats=st)
-        bnst = ops.bn_finalize(bn, conv.bias, st, nt, C, C, M, training)
+        ntw = ops.conv_gemm(dtype, _taps(xs, k), Cs, (B, H, W), (H, W), pk["Wf"], rup(k * k * Cin_p, ops.KALIGN), C,
+                            [y], C, bias=conv.bias, stats=st)
+        bnst = ops.bn_finalize(bn, conv.bias, st, ntw if training else nt, C, C, M, training)
         out = ops.bn_act(dtype, y, bnst, 1)
         ctx.conv, ctx.bn, ctx.dtype, ctx.nsrc, ctx.np = conv, bn, dtype, nsrc, len(args) - nsrc
         ctx.xs, ctx.y, ctx.bnst, ctx.pk = xs, y, bnst, pk
@@ -81,7 +81,7 @@ class ConvBNReLU(torch.autograd.Function):
         dz = torch.empty_like(y)
         part = torch.empty(nte * 2 * C, device=y.device, dtype=torch.float32)
         call("dfcsa_bwd_relu_bn", dt(dtype), M, C, P(dout.contiguous()), P(y), P(bnst.scale), P(bnst.shift),
-             P(bnst.mean), P(bnst.invstd), P(dz), P(part), stream())
+             P(bnst.mean), P(bnst.invstd), P(dz), *S(part), stream())
         coef = ops.bn_bwd_finalize(part, nte, 2, C, M, grad_of(bn.weight), grad_of(bn.bias))
         dy = ops.bn_bwd_apply(dtype, dz, y, bnst, bn.weight, coef,
                               grad_of(conv.bias) if conv.bias is not None else None)

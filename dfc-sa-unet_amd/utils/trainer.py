@@ -20,13 +20,25 @@ checkpoint's ``metrics`` like the reference's) but image dumps (cv2 in the refer
 written; ``train(resume_from)`` restores the histories, the
 start epoch and the best validation Dice (the reference resets histories and best Dice,
 trainer.py:334-349 -- pass ``training.reference_resume_semantics: true`` to keep that behaviour).
+
+Data parallelism (north_star: every configs/*.yaml drops in unchanged on 1..8 GPUs; SURVEY section
+8e).  The reference is single-device (train.py:56-59).  When ``torch.distributed`` is initialised
+with more than one rank (one process per GPU, e.g. under torchrun), the same Trainer runs the
+data-parallel step: each rank takes its rows of every global batch (``dfcsa.ddp.shard_rows``),
+the flat gradient buffer is all-reduced in buckets during backward (``GradBucketReducer``; RCCL on
+its own stream, captured in the step's HIP graph), a NaN loss on any rank skips the update on every
+rank, 1/world is applied inside the fused clip + SGD pass, the per-step metric vector is summed over
+the ranks (IoU / Dice of the global batch, the mean of the replica losses), rank 0's BatchNorm
+running statistics are broadcast before validation, and only rank 0 writes checkpoints and plots.
 """
 import csv
 import os
 import time
 
 import torch
+import torch.distributed as dist
 
+from dfcsa.ddp import GradBucketReducer, allreduce_stats, shard_rows
 from dfcsa.loss import metrics_from_stats, sigmoid
 from dfcsa.optim import FusedSGD
 from utils.metrics import calculate_metrics_device
@@ -69,10 +81,22 @@ class Trainer:
         self.start_time = time.time()
         self.num_epochs = config["training"]["num_epochs"]
         self.max_norm = 1.0
-        # HIP-graph replay of the training step (train_step); training.cuda_graph: false disables
-        self._graphs = {} if config["training"].get("cuda_graph", True) else None
+        # data parallelism: one process per GPU under an initialised process group
+        self.world, self.rank, self.reducer = 1, 0, None
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            self.world, self.rank = dist.get_world_size(), dist.get_rank()
+            if not isinstance(self.optimizer, FusedSGD):
+                raise NotImplementedError("data-parallel training needs the fused SGD (torch.optim.SGD as built by "
+                                          "the reference's train.py, or dfcsa.optim.FusedSGD)")
+            self.reducer = GradBucketReducer(self.model, bucket_mb=config["training"].get("bucket_mb", 32.0))
+        # HIP-graph replay of the training step (train_step); training.cuda_graph: false disables.
+        # Host-staged (gloo) collectives cannot be captured: graphs are off for them.
+        use_graphs = config["training"].get("cuda_graph", True)
+        if self.reducer is not None and dist.get_backend() == "gloo":
+            use_graphs = False
+        self._graphs = {} if use_graphs else None
         self._graph_seen = set()
-        print(f"模型將在 {self.device} 上訓練")
+        print(f"模型將在 {self.device} 上訓練" + (f" (rank {self.rank}/{self.world})" if self.world > 1 else ""))
 
     # ------------------------------------------------------------------ one step
     def train_step(self, images, masks):
@@ -89,10 +113,47 @@ class Trainer:
             return self._graph_step(images, masks)
         return self._eager_step(images, masks)
 
+    def _storage(self):
+        """The device storage a captured step reads and writes through raw pointers: the model's
+        pack plan (tables + packed operands), the flat parameter/gradient buffers and the fused
+        optimizer's momentum / norm scratch.  Returns (signature, keep-alive objects), or
+        (None, None) when any of it is missing or stale (a plan invalidated by a new PackSet, a
+        re-flattened model after ``.to()`` / ``load_state_dict`` into new storage, an optimizer
+        re-resolved after ``load_state_dict``, a parameter frozen): the step then runs eagerly,
+        which rebuilds what is stale, and later batches capture again."""
+        m, opt = self.model, self.optimizer
+        params = opt.param_groups[0]["params"]
+        flat = getattr(params[0], "_dfcsa_flat", None)
+        plan = getattr(m, "_dfcsa_plan", None)
+        if flat is None or not flat.valid() or opt._flat is not flat or opt._mom is None:
+            return None, None
+        if hasattr(m, "_dfcsa_plan") and (plan is None or not plan.valid()):
+            return None, None
+        if not all(p.requires_grad for p in params):
+            return None, None
+        keep = (plan, flat, opt._mom, opt._mom_init, opt._partial, opt.last_norm)
+        sig = (id(plan), plan.epoch if plan is not None else -1, id(flat), flat.data.data_ptr(),
+               flat.grad.data_ptr(), opt._mom.data_ptr(), opt._mom_init.data_ptr(), opt._partial.data_ptr(),
+               opt.last_norm.data_ptr())
+        return sig, keep
+
+    def _drop_graphs(self):
+        self._graphs.clear()
+        self._graph_seen.clear()
+
     def _graph_step(self, images, masks):
         # the SGD hyper-parameters are kernel arguments baked into a capture: part of the key
         hp = tuple(float(self.optimizer.param_groups[0][k]) for k in ("lr", "momentum", "weight_decay"))
-        key = (tuple(images.shape), tuple(masks.shape), images.dtype, masks.dtype, hp)
+        shapes = (tuple(images.shape), tuple(masks.shape), images.dtype, masks.dtype, hp)
+        sig, keep = self._storage()
+        if sig is None:                           # storage changed or not yet resolved: eager
+            self._drop_graphs()
+            met = self._eager_step(images, masks)
+            sig, _ = self._storage()              # resolved by that step: it counts as the warm-up
+            if sig is not None:
+                self._graph_seen.add(shapes + (sig,))
+            return met
+        key = shapes + (sig,)
         g = self._graphs.get(key)
         if g is None:
             if key not in self._graph_seen:       # first batch of this shape: eager (warm-up)
@@ -101,21 +162,34 @@ class Trainer:
             si, sm = images.clone(), masks.clone()
             graph = torch.cuda.CUDAGraph()
             try:
-                with torch.cuda.graph(graph):     # recorded, not executed: replayed below
-                    met = self._eager_step(si, sm)
+                # thread_local: a DataLoader pin-memory thread keeps running during the capture
+                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+                    met = self._eager_step(si, sm)   # recorded, not executed: replayed below
             except RuntimeError as e:
                 print(f"HIP graph capture of the training step failed ({e}); stepping eagerly")
                 self._graphs = None
+                self._reset_host_state()
                 torch.cuda.synchronize()
                 return self._eager_step(images, masks)
             if len(self._graphs) >= 2:           # e.g. a short last batch: keep the newest two
                 self._graphs.pop(next(iter(self._graphs)))
-            g = self._graphs[key] = (graph, si, sm, met)
-        graph, si, sm, met = g
+            g = self._graphs[key] = (graph, si, sm, met, keep)
+        graph, si, sm, met, _ = g
         si.copy_(images, non_blocking=True)
         sm.copy_(masks, non_blocking=True)
         graph.replay()
         return met
+
+    def _reset_host_state(self):
+        """After a failed capture: forget host-side state the half-recorded step changed (packed
+        operands marked fresh by a plan launch that never ran, an armed bucket reducer)."""
+        for mod in self.model.modules():
+            ps = getattr(mod, "_dfcsa_pk", None)
+            if ps is not None:
+                ps.fresh = False
+        if self.reducer is not None:
+            self.reducer._pending = None
+            self.reducer._works = []
 
     def _eager_step(self, images, masks):
         self.optimizer.zero_grad()
@@ -123,6 +197,14 @@ class Trainer:
         probs = sigmoid(logits)
         met = calculate_metrics_device(probs, masks, self.loss_type, self.loss_params)
         loss = met["loss"]
+        if self.reducer is not None:
+            # data parallel: buckets all-reduced as backward finalises them, NaN agreement over the
+            # ranks, 1/world inside the fused clip + SGD, the metric vector summed over the ranks
+            self.reducer.start()
+            loss.backward()
+            skip = self.reducer.finish(loss)
+            self.optimizer.step(max_norm=self.max_norm, grad_scale=self.reducer.grad_scale, skip_if_nan=skip)
+            return {"loss": loss, "stats": allreduce_stats(met["stats"])}
         loss.backward()
         if isinstance(self.optimizer, FusedSGD):
             self.optimizer.step(max_norm=self.max_norm, skip_if_nan=loss)
@@ -137,8 +219,12 @@ class Trainer:
         running_loss = running_iou = running_dice = 0.0
         bar = tqdm(self.train_loader, desc=f"Epoch {epoch + 1}/{self.num_epochs} [Train]")
         for batch_idx, batch in enumerate(bar):
-            images = batch["image"].to(self.device, non_blocking=True)
-            masks = batch["mask"].to(self.device, non_blocking=True)
+            images, masks = batch["image"], batch["mask"]
+            if self.world > 1:   # this rank's rows of the global batch
+                lo, hi = shard_rows(images.shape[0], self.rank, self.world)
+                images, masks = images[lo:hi], masks[lo:hi]
+            images = images.to(self.device, non_blocking=True)
+            masks = masks.to(self.device, non_blocking=True)
             met = self.train_step(images, masks)
             loss = float(met["stats"][0].item())
             if loss != loss:  # NaN: the device already skipped the update (trainer.py:134-139)
@@ -158,6 +244,10 @@ class Trainer:
 
     @torch.no_grad()
     def validate_epoch(self, dataloader):
+        if self.reducer is not None:
+            # every rank evaluates rank 0's model: the BatchNorm running statistics (per replica
+            # while training) are broadcast first, as torch DDP's broadcast_buffers does
+            self.reducer.broadcast_buffers()
         self.model.eval()
         running_loss = running_iou = running_dice = 0.0
         samples = []
@@ -189,6 +279,8 @@ class Trainer:
 
     # ------------------------------------------------------------------ checkpoints
     def save_checkpoint(self, epoch, metrics, is_best=False):
+        if self.rank != 0:   # data parallel: the replicas are identical, rank 0 writes
+            return
         ckpt = {"epoch": epoch, "model_state_dict": self.model.state_dict(),
                 "optimizer_state_dict": self.optimizer.state_dict(),
                 "train_losses": self.train_losses, "val_losses": self.val_losses,
@@ -207,8 +299,7 @@ class Trainer:
         self.model.load_state_dict(ckpt["model_state_dict"])
         self.optimizer.load_state_dict(ckpt["optimizer_state_dict"])
         if self._graphs is not None:   # optimizer storage may be new: capture again
-            self._graphs.clear()
-            self._graph_seen.clear()
+            self._drop_graphs()
         for k in ("train_losses", "val_losses", "train_dice_scores", "val_dice_scores", "train_iou_scores",
                   "val_iou_scores", "best_val_loss"):
             setattr(self, k, ckpt[k])
@@ -218,6 +309,8 @@ class Trainer:
 
     # ------------------------------------------------------------------ loop
     def _write_history(self):
+        if self.rank != 0:
+            return
         with open(os.path.join(self.images_dir, "metrics.csv"), "w", newline="") as f:
             w = csv.writer(f)
             w.writerow(["epoch", "train_loss", "val_loss", "train_dice", "val_dice", "train_iou", "val_iou"])

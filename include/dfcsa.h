@@ -40,6 +40,10 @@ extern "C" {
  * k2 s2): column n = (2i + j)*Nd + co goes to dest[0][b, 2oh+i, 2ow+j, co] of Hout x Wout.
  * accumulate: dest += C.  stats (optional): per 64-row M tile t, stats[t][0][n] = sum of the
  * fp32 accumulator (without bias) over valid rows, stats[t][1][n] = sum of squares.
+ *
+ * Slab capacities: every entry point that writes a per-workgroup partial slab (the stats above,
+ * `partial`, `bias_partial`, `stats3/4`) also takes that slab's size in floats (`*_floats`), and
+ * returns DFCSA_EINVAL without launching when its grid would write past it.
  * ---------------------------------------------------------------------------------------- */
 #define CONV_STORE_PLAIN 0
 #define CONV_STORE_SHUFFLE2 1
@@ -57,9 +61,13 @@ typedef struct {
   int Nd, accumulate;
   float* stats;
   int Hout, Wout;
+  int64_t stats_floats; /* capacity of stats in floats: >= ceil(M/64)*2*N when stats != NULL */
 } dfcsa_conv_desc;
 int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream);
-int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile (ntiles = ceil(M / mtile)) */
+int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile of the row-tile kernels */
+/* statistics rows the launch of *d writes (and dfcsa_bn_finalize reads as ntiles): ceil(M / 64)
+ * for the row-tile kernels, one per 2-D tile when the bf16 3x3 halo-tile kernel runs the GEMM */
+int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d);
 
 /* ------------------------------------------------------------------------------------------
  * Weight gradient (MFMA, reduction over pixels).  Replaces the weight half of
@@ -91,8 +99,13 @@ typedef struct {
   int splits, mchunk;
   int layout, ntaps, Ctot, Creal, ndst;
   float* dst[3];
+  int64_t slab_floats;  /* capacity of slab in floats (checked against the launch) */
 } dfcsa_wgrad_desc;
 int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk, int64_t* slab_floats);
+/* the plan of the launch dfcsa_conv_wgrad will make for *d (segments, shapes, layout filled in):
+ * a bf16 3x3 weight gradient (layout 0, one dY tensor, M >= 32768) runs on 2-D halo tiles with its
+ * own pixel-range split count; everything else as dfcsa_wgrad_plan */
+int dfcsa_wgrad_plan_desc(const dfcsa_wgrad_desc* d, int* splits, int* mchunk, int64_t* slab_floats);
 int dfcsa_wgrad_fuse_max(void);
 int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
 /* grad += sum_s slab[s] (slab [splits][NI][NJ]) mapped to the reference weight layout.
@@ -212,7 +225,7 @@ int dfcsa_ew_ntiles(int M, int C);
  * sums: [sum dz4, sum dz4*xh4, sum dout*res] */
 int dfcsa_bwd_block_out(int dtype, int M, int C, const void* dout, const void* y4, const float* sc4,
                         const float* sh4, const float* mean4, const float* invstd4, const void* res,
-                        const float* res_scale, void* dz4, void* dres, float* partial, void* stream);
+                        const float* res_scale, void* dz4, void* dres, float* partial, int64_t partial_floats, void* stream);
 /* its backward: dout = dskip (NULL: 0) + maxpool_bwd(dpooled) routed by the saved `out`, stored,
  * then dfcsa_bwd_block_out on it (dres = res_scale*dout; sums [dz4, dz4*xh4, dout*res]) in one
  * pass; partial [dfcsa_bwd_block_out_pool_ntiles(B, H, W, C)][3][C] */
@@ -220,16 +233,16 @@ int dfcsa_bwd_block_out_pool_ntiles(int B, int H, int W, int C);
 int dfcsa_bwd_block_out_pool(int dtype, int B, int H, int W, int C, const void* dskip, const void* out,
                              const void* dpooled, const void* y4, const float* sc4, const float* sh4,
                              const float* mean4, const float* invstd4, const void* res, const float* res_scale,
-                             void* dout, void* dres, float* partial, void* stream);
+                             void* dout, void* dres, float* partial, int64_t partial_floats, void* stream);
 /* dz = dact * (y*sc+sh > 0); sums [sum dz, sum dz*xh] */
 int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                       const float* sh, const float* mean, const float* invstd, void* dz,
-                      float* partial, void* stream);
+                      float* partial, int64_t partial_floats, void* stream);
 /* gate: g = sigmoid(y3*sc3+sh3); dz3 = dfused*(local-attn)*g*(1-g); dlocal += dfused*g;
  * dattn += dfused*(1-g); sums [sum dz3, sum dz3*xh3] */
 int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,
                    const float* sh3, const float* mean3, const float* invstd3, const void* local,
-                   const void* attn, void* dlocal, void* dattn, void* dz3, float* partial,
+                   const void* attn, void* dlocal, void* dattn, void* dz3, float* partial, int64_t partial_floats,
                    void* stream);
 /* fusion-conv input gradient with the gate backward in the epilogue (bf16, C % 64 == 0,
  * C <= 256): [dfused | dlocal | dattn] = dy4 . W4t (W4t = dfcsa_conv_gemm's [3C][Kpad] dgrad
@@ -242,7 +255,7 @@ int dfcsa_dgrad_gate_parts(int M, int C);
 int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, const void* y3,
                      const float* sc3, const float* sh3, const float* mean3, const float* invstd3,
                      const void* local, const void* attn, void* dlocal, void* dattn, void* dz3,
-                     float* partial, void* stream);
+                     float* partial, int64_t partial_floats, void* stream);
 /* fusion conv forward with the gate fusion in its A-operand prologue (bf16, C == 64 or 128, Kpad == 3C):
  * fused = g*local + (1-g)*attn, g = sigmoid(y3*sc3+sh3) (dfcsa_gate_fuse's arithmetic), stored;
  * y4 = [fused | local | attn] . w4^T + b4 (w4 = the fusion conv's [C][3C] forward operand) with
@@ -253,7 +266,7 @@ int dfcsa_dgrad_gate(int M, int C, const void* dy4, const void* w4t, int Kpad, c
 int dfcsa_fwd_pro_parts(int M, int C, int pro);
 int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
-                          float* stats4, void* stream);
+                          float* stats4, int64_t stats4_floats, void* stream);
 /* gate conv forward with the local/attention merge in its A-operand prologue (bf16, C == 64,
  * Kpad == 128, relu): local = relu(y1*sc1+sh1), attn = gamma*bilinear(o) + relu(y2*sc2+sh2)
  * (dfcsa_block_local_attn's arithmetic; o fp32 [B][P][P][64]), both stored; y3 = [local | attn] .
@@ -262,7 +275,7 @@ int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const 
 int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,
                               const float* gamma, const void* w3, int Kpad, const float* b3, void* local,
-                              void* attn, void* y3, float* stats3, void* stream);
+                              void* attn, void* y3, float* stats3, int64_t stats3_floats, void* stream);
 /* dfcsa_dgrad_gate / dfcsa_dgrad_acc_relu_bn at C == 64 with the BatchNorm-backward apply of their
  * A operand in a prologue: dy4 = gamma4*invstd4*(dz4 - coef4[0] - xh4*coef4[1]) with dz4 =
  * dout*(y4*sc4+sh4 > 0) (dfcsa_bn_bwd_apply_relu; sc4 = sh4 = NULL: dz4 = dout) and dy3 likewise from
@@ -274,11 +287,11 @@ int dfcsa_dgrad_gate_apply(int M, const void* dout, const void* y4, const float*
                            const float* mean4, const float* invstd4, const float* sc4, const float* sh4, void* dy4,
                            const void* w4t, const void* y3, const float* sc3, const float* sh3, const float* mean3,
                            const float* invstd3, const void* local, const void* attn, void* dlocal, void* dattn,
-                           void* dz3, float* partial, void* stream);
+                           void* dz3, float* partial, int64_t partial_floats, void* stream);
 int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void* y3, const float* gamma3, const float* coef3,
                                   const float* mean3, const float* invstd3, void* dy3, const void* w3t,
                                   const void* y1, const float* sc1, const float* sh1, const float* mean1,
-                                  const float* invstd1, void* dlocal, void* dattn, float* partial, void* stream);
+                                  const float* invstd1, void* dlocal, void* dattn, float* partial, int64_t partial_floats, void* stream);
 /* gate-conv input gradient added into [dlocal | dattn] (bf16, C % 64 == 0, C <= 256): dlocal +=
  * (dy3 . W3t)[:, :C], dattn += (dy3 . W3t)[:, C:] (W3t = the [2C][Kpad] dgrad operand of the gate
  * conv; same bf16 roundings as dfcsa_conv_gemm's accumulate mode), and on the final dlocal the
@@ -288,12 +301,12 @@ int dfcsa_dgrad_acc_relu_bn_apply(int M, const void* dz3, const void* y3, const 
 int dfcsa_dgrad_acc_relu_bn_parts(int M, int C);
 int dfcsa_dgrad_acc_relu_bn(int M, int C, const void* dy3, const void* w3t, int Kpad, const void* y1,
                             const float* sc1, const float* sh1, const float* mean1, const float* invstd1,
-                            void* dlocal, void* dattn, float* partial, void* stream);
+                            void* dlocal, void* dattn, float* partial, int64_t partial_floats, void* stream);
 /* attention entry: dz2 = (dattn + adaptive_pool^T(dpooled)) * (y2*sc2+sh2 > 0) (mask only when
  * relu != 0); dpooled fp32 [B][P][P][C]; sums [sum dz2, sum dz2*xh2] */
 int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled,
                          int P, const void* y2, const float* sc2, const float* sh2, const float* mean2,
-                         const float* invstd2, int relu, void* dz2, float* partial, void* stream);
+                         const float* invstd2, int relu, void* dz2, float* partial, int64_t partial_floats, void* stream);
 /* from partial sums: coef[0][c] = mean dz, coef[1][c] = mean dz*xh; dgamma += sum dz*xh,
  * dbeta += sum dz; if nsum == 3 and extra != null: *extra += sum over c of the third sum. */
 int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count,
@@ -303,21 +316,21 @@ int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int
  * BatchNorm it is exactly zero, sum_m dy = gamma*invstd*(sum dz - M*coef0 - coef1*sum xh) = 0) */
 int dfcsa_bn_bwd_apply(int dtype, int M, int C, const void* dz, const void* y, const float* mean,
                        const float* invstd, const float* gamma, const float* coef, void* dy,
-                       float* bias_partial, void* stream);
+                       float* bias_partial, int64_t bias_partial_floats, void* stream);
 /* dfcsa_bn_bwd_apply with dz recomputed from the activation's output gradient instead of read
  * from a dz tensor (the producing stage -- dfcsa_bwd_relu_bn / dfcsa_bwd_block_out with dz = NULL
  * -- then only emits its partial sums): dz = (y*sc + sh > 0) ? dact : 0.  Replaces the BN/ReLU
  * backward of reference models/unet_dfc_sa_res.py:57-62, :65-69, :80-84 (autograd). */
 int dfcsa_bn_bwd_apply_relu(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                             const float* sh, const float* mean, const float* invstd, const float* gamma,
-                            const float* coef, void* dy, float* bias_partial, void* stream);
+                            const float* coef, void* dy, float* bias_partial, int64_t bias_partial_floats, void* stream);
 /* the same for the attention entry a = relu(bn2 y2) (reference :65-69 + the adaptive-avg-pool of
  * :24 and the residual of :38): dz = act'(bn y) * (dattn + pool_backward(dpooled)); pairs with
  * dfcsa_bwd_attn_entry(dz2 = NULL). */
 int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, const void* dattn, const float* dpooled, int P,
                              const void* y, const float* sc, const float* sh, const float* mean,
                              const float* invstd, int relu, const float* gamma, const float* coef, void* dy,
-                             float* bias_partial, void* stream);
+                             float* bias_partial, int64_t bias_partial_floats, void* stream);
 /* Two-stage reduction helper for per-tile slabs: dst[g][j] = sum of rows t in group g of
  * src[t][j] (T rows of rowlen floats, G groups of ceil(T/G) consecutive rows).  The finalize
  * entry points then reduce G rows instead of T.  dst: [G][rowlen] fp32 (caller scratch). */
@@ -328,7 +341,7 @@ int dfcsa_slab_colsum(const float* slab, int ntiles, int C, float* out, void* st
 int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, int n1, float* d0, float* d1, float* d2,
                        void* stream);
 /* per-channel partial sums of an NHWC tensor -> partial [ntiles][C] */
-int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, void* stream);
+int dfcsa_channel_sum(int dtype, int M, int C, const void* x, float* partial, int64_t partial_floats, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * LightSelfAttention on the pooled map (unet_dfc_sa_res.py:20-39).  Pooled tensors are fp32
@@ -583,7 +596,7 @@ int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, const void*
 int dfcsa_sum_out(int dtype, int M, int C, const void* a, const void* b, const void* res, const float* res_scale,
                   void* out, void* stream);
 int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, const void* res, const float* res_scale, void* dres,
-                      float* partial, void* stream);
+                      float* partial, int64_t partial_floats, void* stream);
 int dfcsa_sum_into(const float* x, int n, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
@@ -660,8 +673,12 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 6: waves per weight-gradient workgroup (4 or 8; 0 = automatic).
  * knob 7: 1 = register-staged bf16 weight gradient instead of the LDS-DMA kernel.
  * knob 8: 0 = allow the 64x256 weight-gradient tile for 64-row problems (default 1: off).
- * knob 9: 1 = generic (non-MFMA) full-resolution attention kernels (coverage tests). */
+ * knob 9: 1 = generic (non-MFMA) full-resolution attention kernels (coverage tests).
+ * knob 19: smallest M routed to the 2-D halo-tile 3x3 conv kernel (0 = never).
+ * knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel, 0 = row tiles.
+ * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
+int dfcsa_get_tuning(int knob);
 
 const char* dfcsa_version(void);
 

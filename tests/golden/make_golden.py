@@ -698,6 +698,69 @@ def gen_cfg2():
 
 
 # ----------------------------------------------------------------------------------------
+# (12b) bf16 BACKWARD calibration at the config-2 geometry (the benchmark path's dtype): the same
+#      model and batch as (12), one reference train step run three ways -- float64 (the truth), the
+#      reference under PyTorch's CPU bf16 autocast (what bf16 arithmetic alone does to it), and
+#      fp32 (cfg2_step.npz).  Stored per parameter tensor: the autocast gradient's cosine and
+#      relative distance to float64 (pre-clip), the relative distance of the autocast SGD update
+#      (clip 1.0 + SGD) to the float64 update, and per BN buffer the autocast running statistics'
+#      distance to float64's after the step.  The GPU test holds the build's bf16 step to these
+#      (utils/trainer.py:120-151, train.py:73-78).
+# ----------------------------------------------------------------------------------------
+def gen_cfg2bf16():
+    import copy
+    torch.manual_seed(12000)
+    m = ref_res.UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4, ablation_on_qk_channels=8)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    m.train()
+    gen = torch.Generator().manual_seed(12001)
+    x, t = batch(gen, (2, 3, 224, 224))
+
+    def step(model, xx, tt, autocast):
+        opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+        w0 = {n: p.detach().clone() for n, p in model.named_parameters()}
+        opt.zero_grad()
+        if autocast:
+            with torch.autocast("cpu", dtype=torch.bfloat16):
+                out = model(xx)
+            out = out.float()
+        else:
+            out = model(xx)
+        met = ref_metrics.calculate_metrics(torch.sigmoid(out), tt, "bce_dice", LOSS_PARAMS)
+        met["loss"].backward()
+        g = {n: p.grad.detach().double().clone() for n, p in model.named_parameters()}
+        torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)
+        opt.step()
+        upd = {n: (p.detach().double() - w0[n].double()) for n, p in model.named_parameters()}
+        bufs = {k: v.detach().double().clone() for k, v in model.state_dict().items() if "running" in k}
+        return g, upd, bufs
+
+    m64 = fp64_twin(m)
+    g64, u64, b64 = step(m64, x.double(), t.double(), False)
+    mac = copy.deepcopy(m)
+    gac, uac, bac = step(mac, x, t, True)
+    reln = lambda a, b: np.float64(((a - b).norm() / (b.norm() + 1e-30)).item())  # noqa: E731
+    out = {}
+    for n in g64:
+        a, b = gac[n].reshape(-1), g64[n].reshape(-1)
+        out["ac_cos." + n] = np.float64((a @ b / (a.norm() * b.norm() + 1e-300)).item())
+        out["ac_rel." + n] = reln(a, b)
+        out["ac_upd_rel." + n] = reln(uac[n], u64[n])
+        out["gnorm64." + n] = np.float64(b.norm().item())
+    for k in b64:
+        out["ac_buf_rel." + k] = reln(bac[k], b64[k])
+    ga = torch.cat([gac[n].reshape(-1) for n in g64])
+    gb = torch.cat([g64[n].reshape(-1) for n in g64])
+    out["ac_cos_all"] = np.float64((ga @ gb / (ga.norm() * gb.norm())).item())
+    out["ac_rel_all"] = reln(ga, gb)
+    print("cfg2 bf16 autocast: global grad cos", float(out["ac_cos_all"]), "rel", float(out["ac_rel_all"]))
+    save("cfg2_bf16.npz", x=np32(x), t=np32(t), **out)
+
+
+# ----------------------------------------------------------------------------------------
 # (13) Checkpoint interop: the reference Trainer (utils/trainer.py) trains the small model for one
 #      epoch of two batches, validates, and writes its checkpoint with its own save_checkpoint
 #      (:267-298; metrics with best/worst samples).  A second reference Trainer loads it with its own

@@ -495,7 +495,7 @@ def test_dgrad_gate_fused_equals_gemm_plus_gate(M, C):
     dfcsa_bwd_gate): dlocal, dattn and dz3 bit-identical (same MFMA order, same bf16 roundings),
     the BN3-backward sums equal to fp32 summation-order noise; ragged M (M % 64 != 0)."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P, stream
+    from dfcsa.ops import P, S, stream
     torch.manual_seed(11)
     bf = torch.bfloat16
     dev = "cuda"
@@ -512,14 +512,14 @@ def test_dgrad_gate_fused_equals_gemm_plus_gate(M, C):
     nte = ops.ntiles_ew(M, C)
     part0 = torch.empty(nte * 2 * C, device=dev)
     call("dfcsa_bwd_gate", ops.dt(bf), M, C, P(dfu), P(y3), P(sc), P(sh), P(mu), P(istd), P(loc), P(att), P(dl0),
-         P(da0), P(dz0), P(part0), stream())
+         P(da0), P(dz0), *S(part0), stream())
     # fused
     npart = LIB.dfcsa_dgrad_gate_parts(M, C)
     assert 1 <= npart <= (M + 63) // 64
     dl1, da1, dz1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
     part1 = torch.empty(npart * 2 * C, device=dev)
     call("dfcsa_dgrad_gate", M, C, P(dy4), P(w4t), Kp, P(y3), P(sc), P(sh), P(mu), P(istd), P(loc), P(att), P(dl1),
-         P(da1), P(dz1), P(part1), stream())
+         P(da1), P(dz1), *S(part1), stream())
     torch.cuda.synchronize()
     assert torch.equal(dl1, dl0) and torch.equal(da1, da0) and torch.equal(dz1, dz0)
     s0 = part0.view(nte, 2, C).double().sum(0)
@@ -535,7 +535,7 @@ def test_dgrad_acc_relu_bn_fused_equals_gemm_plus_sums(M, C):
     dfcsa_conv_gemm, then dfcsa_bwd_relu_bn's sums): dlocal and dattn bit-identical, the sums equal
     to fp32 summation-order noise; ragged M."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P, stream
+    from dfcsa.ops import P, S, stream
     torch.manual_seed(12)
     bf = torch.bfloat16
     dev = "cuda"
@@ -550,13 +550,13 @@ def test_dgrad_acc_relu_bn_fused_equals_gemm_plus_sums(M, C):
                   [dl0.view(1, M, 1, C), da0.view(1, M, 1, C)], C, accumulate=True)
     nte = ops.ntiles_ew(M, C)
     part0 = torch.empty(nte * 2 * C, device=dev)
-    call("dfcsa_bwd_relu_bn", ops.dt(bf), M, C, P(dl0), P(y1), P(sc), P(sh), P(mu), P(istd), None, P(part0), stream())
+    call("dfcsa_bwd_relu_bn", ops.dt(bf), M, C, P(dl0), P(y1), P(sc), P(sh), P(mu), P(istd), None, *S(part0), stream())
     npart = LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
     assert 1 <= npart <= (M + 63) // 64
     dl1, da1 = dl_in.clone(), da_in.clone()
     part1 = torch.empty(npart * 2 * C, device=dev)
     call("dfcsa_dgrad_acc_relu_bn", M, C, P(dy3), P(w3t), Kp, P(y1), P(sc), P(sh), P(mu), P(istd), P(dl1), P(da1),
-         P(part1), stream())
+         *S(part1), stream())
     torch.cuda.synchronize()
     assert torch.equal(dl1, dl0) and torch.equal(da1, da0)
     s0 = part0.view(nte, 2, C).double().sum(0)
@@ -595,7 +595,7 @@ def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M, C):
     C = 64) against the pair it replaces (dfcsa_gate_fuse, then the [fused, local, attn] GEMM with
     BN statistics): fused, y4 and the statistics totals; ragged M; C = 64 and 128."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P, stream
+    from dfcsa.ops import P, S, stream
     torch.manual_seed(13)
     bf = torch.bfloat16
     dev = "cuda"
@@ -613,7 +613,7 @@ def test_gate_fusion_fwd_equals_gate_fuse_plus_gemm(M, C):
                   bias=b4, stats=st0)
     f1, y1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(2))
     st1 = torch.empty(nt * 2 * C, device=dev)
-    call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(sc), P(sh), P(loc), P(att), P(w4), Kp, P(b4), P(f1), P(y1), P(st1),
+    call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(sc), P(sh), P(loc), P(att), P(w4), Kp, P(b4), P(f1), P(y1), *S(st1),
          stream())
     torch.cuda.synchronize()
     assert rel(f1, f0) < 1e-6 and (f1.float() - f0.float()).abs().max().item() <= 2 ** -7 * f0.float().abs().max().item()
@@ -630,7 +630,7 @@ def test_local_attn_gate_fwd_equals_merge_plus_gemm(B, H, W, P):
     prologue, C = 64) against the pair it replaces (dfcsa_block_local_attn, then the [local, attn]
     GEMM with BN statistics): local, attn, y3 and the statistics totals; ragged M, P > H."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P as Ptr, stream
+    from dfcsa.ops import P as Ptr, S, stream
     torch.manual_seed(14)
     bf = torch.bfloat16
     dev = "cuda"
@@ -653,7 +653,7 @@ def test_local_attn_gate_fwd_equals_merge_plus_gemm(B, H, W, P):
     l1, a1, y31 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
     st1 = torch.empty(nt * 2 * C, device=dev)
     call("dfcsa_local_attn_gate_fwd", B, H, W, C, Ptr(y1), Ptr(sc1), Ptr(sh1), Ptr(y2), Ptr(sc2), Ptr(sh2), Ptr(o), P,
-         Ptr(gamma), Ptr(w3), Kp, Ptr(b3), Ptr(l1), Ptr(a1), Ptr(y31), Ptr(st1), stream())
+         Ptr(gamma), Ptr(w3), Kp, Ptr(b3), Ptr(l1), Ptr(a1), Ptr(y31), *S(st1), stream())
     torch.cuda.synchronize()
     assert torch.equal(l1, l0)
     assert rel(a1, a0) < 1e-6
@@ -669,7 +669,7 @@ def test_dgrad_apply_prologue_equals_apply_plus_gemm(M):
     the A operand formed in the GEMM's prologue) against dfcsa_bn_bwd_apply_relu / _apply followed by
     dfcsa_dgrad_gate / dfcsa_dgrad_acc_relu_bn: dy, the GEMM outputs and the partial sums."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P, stream
+    from dfcsa.ops import P, S, stream
     torch.manual_seed(15)
     bf = torch.bfloat16
     dev = "cuda"
@@ -682,32 +682,32 @@ def test_dgrad_apply_prologue_equals_apply_plus_gemm(M):
     T = ops.dt(bf)
     # gate: reference path
     dy0 = torch.empty(M, C, device=dev, dtype=bf)
-    call("dfcsa_bn_bwd_apply_relu", T, M, C, P(src), P(y), P(sc), P(sh), P(mu), P(istd), P(gamma), P(k), P(dy0), None,
+    call("dfcsa_bn_bwd_apply_relu", T, M, C, P(src), P(y), P(sc), P(sh), P(mu), P(istd), P(gamma), P(k), P(dy0), None, 0,
          stream())
     n0 = LIB.dfcsa_dgrad_gate_parts(M, C)
     dl0, da0, dz0 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(3))
     p0 = torch.empty(n0 * 2 * C, device=dev)
     call("dfcsa_dgrad_gate", M, C, P(dy0), P(w4t), Kp, P(y3), P(sc3), P(sh3), P(mu3), P(istd3), P(loc), P(att),
-         P(dl0), P(da0), P(dz0), P(p0), stream())
+         P(dl0), P(da0), P(dz0), *S(p0), stream())
     n1 = LIB.dfcsa_dgrad_apply_parts(M, 0)
     dy1, dl1, da1, dz1 = (torch.empty(M, C, device=dev, dtype=bf) for _ in range(4))
     p1 = torch.empty(n1 * 2 * C, device=dev)
     call("dfcsa_dgrad_gate_apply", M, P(src), P(y), P(gamma), P(k), P(mu), P(istd), P(sc), P(sh), P(dy1), P(w4t),
-         P(y3), P(sc3), P(sh3), P(mu3), P(istd3), P(loc), P(att), P(dl1), P(da1), P(dz1), P(p1), stream())
+         P(y3), P(sc3), P(sh3), P(mu3), P(istd3), P(loc), P(att), P(dl1), P(da1), P(dz1), *S(p1), stream())
     # acc: reference path (plain apply of dz3 = src)
     dyb0 = torch.empty(M, C, device=dev, dtype=bf)
-    call("dfcsa_bn_bwd_apply", T, M, C, P(src), P(y), P(mu), P(istd), P(gamma), P(k), P(dyb0), None, stream())
+    call("dfcsa_bn_bwd_apply", T, M, C, P(src), P(y), P(mu), P(istd), P(gamma), P(k), P(dyb0), None, 0, stream())
     dlb0, dab0 = loc.clone(), att.clone()
     m0 = LIB.dfcsa_dgrad_acc_relu_bn_parts(M, C)
     q0 = torch.empty(m0 * 2 * C, device=dev)
     call("dfcsa_dgrad_acc_relu_bn", M, C, P(dyb0), P(w3t), Kp, P(y1), P(sc3), P(sh3), P(mu3), P(istd3), P(dlb0),
-         P(dab0), P(q0), stream())
+         P(dab0), *S(q0), stream())
     m1 = LIB.dfcsa_dgrad_apply_parts(M, 1)
     dyb1 = torch.empty(M, C, device=dev, dtype=bf)
     dlb1, dab1 = loc.clone(), att.clone()
     q1 = torch.empty(m1 * 2 * C, device=dev)
     call("dfcsa_dgrad_acc_relu_bn_apply", M, P(src), P(y), P(gamma), P(k), P(mu), P(istd), P(dyb1), P(w3t), P(y1),
-         P(sc3), P(sh3), P(mu3), P(istd3), P(dlb1), P(dab1), P(q1), stream())
+         P(sc3), P(sh3), P(mu3), P(istd3), P(dlb1), P(dab1), *S(q1), stream())
     torch.cuda.synchronize()
     for a, b in ((dy1, dy0), (dl1, dl0), (da1, da0), (dz1, dz0), (dyb1, dyb0), (dlb1, dlb0), (dab1, dab0)):
         assert rel(a, b) < 1e-5
@@ -723,7 +723,7 @@ def test_block_out_pool_fused_equals_separate(dtype, B, H, W, C, skip):
     dfcsa_maxpool2_bwd into the skip gradient + dfcsa_bwd_block_out): out, pooled, dout, dres exact
     (ties included: y4 has repeated values), the three per-channel sums to summation-order noise."""
     from dfcsa._lib import LIB, call
-    from dfcsa.ops import P, stream
+    from dfcsa.ops import P, S, stream
     torch.manual_seed(16)
     dev = "cuda"
     T = ops.dt(dtype)
@@ -747,12 +747,12 @@ def test_block_out_pool_fused_equals_separate(dtype, B, H, W, C, skip):
     dr0 = torch.empty(M, C, device=dev, dtype=dtype)
     q0 = torch.empty(nte * 3 * C, device=dev)
     call("dfcsa_bwd_block_out", T, M, C, P(d0), P(y4), P(sc), P(sh), P(mu), P(istd), P(res), P(rs), None, P(dr0),
-         P(q0), stream())
+         *S(q0), stream())
     ntp = LIB.dfcsa_bwd_block_out_pool_ntiles(B, H, W, C)
     d1, dr1 = (torch.empty(M, C, device=dev, dtype=dtype) for _ in range(2))
     q1 = torch.empty(ntp * 3 * C, device=dev)
     call("dfcsa_bwd_block_out_pool", T, B, H, W, C, P(gs), P(out1), P(gp), P(y4), P(sc), P(sh), P(mu), P(istd),
-         P(res), P(rs), P(d1), P(dr1), P(q1), stream())
+         P(res), P(rs), P(d1), P(dr1), *S(q1), stream())
     torch.cuda.synchronize()
     assert torch.equal(out1, out0) and torch.equal(p1, p0)
     assert torch.equal(d1, d0) and torch.equal(dr1, dr0)

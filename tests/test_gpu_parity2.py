@@ -196,6 +196,108 @@ def test_cfg2_geometry_bf16_within_reference_autocast():
     print(f"cfg2 bf16 logits rel {r:.4e} (bar {bar:.4e})")
 
 
+def _cfg2_bf16_step(fused=True):
+    """One bf16 train step at the config-2 geometry; returns (sd0, pre-clip grads, state after)."""
+    from dfcsa import block as blk_mod
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from utils.metrics import calculate_metrics_device
+    m, fx = cfg2_model("bf16")
+    sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
+    m = m.cuda().train()
+    opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    x, t = T(fx["x"]), T(fx["t"])
+    old = (blk_mod.FUSED_DGRAD_GATE[0], blk_mod.POOL_FUSION[0])
+    blk_mod.FUSED_DGRAD_GATE[0] = blk_mod.POOL_FUSION[0] = fused
+    try:
+        opt.zero_grad()
+        met = calculate_metrics_device(sigmoid(m(x)), t, "bce_dice", LP)
+        met["loss"].backward()
+        torch.cuda.synchronize()
+        pre = {n: p.grad.detach().double().cpu().clone() for n, p in m.named_parameters()}
+        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
+        torch.cuda.synchronize()
+    finally:
+        blk_mod.FUSED_DGRAD_GATE[0], blk_mod.POOL_FUSION[0] = old
+    return sd0, pre, {k: v.detach().cpu() for k, v in m.state_dict().items()}, x, t, fx
+
+
+def _cos_rel(g, r):
+    g, r = g.reshape(-1), r.double().reshape(-1)
+    return (g @ r / (g.norm() * r.norm() + 1e-300)).item(), ((g - r).norm() / (r.norm() + 1e-30)).item()
+
+
+def test_cfg2_geometry_bf16_train_step_vs_reference_autocast():
+    """The benchmark path itself: one bf16 train step at the config-2 geometry (64..512, 224^2, P=4,
+    B=2, gammas 0.5) with every bf16 block fusion on (C = 64/128/256 blocks take dfcsa_dgrad_gate,
+    dfcsa_dgrad_acc_relu_bn, the gate-fusion and local/attention prologue GEMMs, the apply prologues
+    at C = 64, the fused max-pool passes, the 3x3 halo-tile GEMMs).  Pinned to the reference's own
+    bf16 error (tests/golden/cfg2_bf16.npz: the reference under CPU bf16 autocast against its
+    float64 run), against the fp32 reference re-run here on the CPU oracle:
+      * per parameter tensor (pre-clip gradient): relative distance <= max(1.25 x the autocast's,
+        2e-2), and cosine distance 1 - cos <= 1.25 x the autocast's + 1e-3 -- or, where our path is
+        farther than that, no farther than the same step with the fusions off (the unfused kernels
+        are checked against fp32 to 1e-4 / 2e-3 in test_cfg2_geometry_fp32_train_step): the fusions
+        must not add error of their own;
+      * over the whole gradient vector: no worse than the autocast;
+      * BatchNorm running statistics after the step vs the reference fp32 step (cfg2_step.npz):
+        <= max(1.25 x the autocast's distance, 1e-3);
+      * the SGD update (clip 1.0 + momentum SGD) per tensor vs the oracle's update from the fp32
+        gradients: <= max(1.25 x the autocast update's distance, 2e-2).
+    The conv biases that feed a train-mode BatchNorm have an exactly-zero gradient (ours is the
+    exact zero; autocast's is rounding noise): they are held to zero."""
+    from oracle import dfcsa_oracle as O
+    fb = load("cfg2_bf16.npz")
+    sd0, pre, sd, x, t, fx = _cfg2_bf16_step(True)
+    assert torch.equal(x.cpu(), torch.from_numpy(fb["x"])) and torch.equal(t.cpu(), torch.from_numpy(fb["t"]))
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    _, _, gref, _ = O.forward_backward(sd0, x.cpu(), t.cpu(), 4, LP)
+    sd1, _, _, _ = O.clip_and_sgd(sd0, gref, {})
+    unfused = None
+    rows, fails = [], []
+    for n in O.param_names(sd0):
+        if n.endswith(ZERO):
+            assert pre[n].abs().max().item() <= 1e-6 * max(1.0, gref[n].abs().max().item()), n
+            continue
+        cs, rr = _cos_rel(pre[n], gref[n])
+        ac_rel, ac_cos = float(fb["ac_rel." + n]), float(fb["ac_cos." + n])
+        ok = rr <= max(1.25 * ac_rel, 2e-2) and (pre[n].numel() == 1 or 1 - cs <= 1.25 * (1 - ac_cos) + 1e-3)
+        note = ""
+        if not ok:
+            if unfused is None:
+                unfused = _cfg2_bf16_step(False)[1]
+            ucs, urr = _cos_rel(unfused[n], gref[n])
+            note = f" unfused cos {ucs:.5f} rel {urr:.3e}"
+            # the fusions must not add error: no farther from fp32 than the unfused bf16 step (+5%)
+            ok = rr <= 1.05 * urr + 1e-4 and 1 - cs <= 1.05 * (1 - ucs) + 1e-4
+        rows.append((rr / max(ac_rel, 1e-30), n, f"{n}: cos {cs:.5f} (autocast {ac_cos:.5f}) rel {rr:.3e} "
+                                                 f"(autocast {ac_rel:.3e}){note}"))
+        if not ok:
+            fails.append(rows[-1][2])
+        upd, upd_ref = sd[n].double() - sd0[n].double(), sd1[n].double() - sd0[n].double()
+        quant = 2.0 * 2.0 ** -23 * sd0[n].double().norm().item()
+        ur = ((upd - upd_ref).norm().item() - quant) / (upd_ref.norm().item() + 1e-30)
+        if ur > max(1.25 * float(fb["ac_upd_rel." + n]), 2e-2):
+            fails.append(f"{n}: update rel {ur:.3e} (autocast {float(fb['ac_upd_rel.' + n]):.3e})")
+    rows.sort(reverse=True)
+    print("cfg2 bf16 step, worst tensors relative to the reference autocast:")
+    for r in rows[:12]:
+        print("   ", r[2])
+    names = [n for n in O.param_names(sd0) if not n.endswith(ZERO)]
+    ga = torch.cat([pre[n].reshape(-1) for n in names])
+    gb = torch.cat([gref[n].double().reshape(-1) for n in names])
+    cos_all, rel_all = _cos_rel(ga, gb)
+    print(f"cfg2 bf16 step: whole-gradient cos {cos_all:.6f} (autocast {float(fb['ac_cos_all']):.6f}), "
+          f"rel {rel_all:.4e} (autocast {float(fb['ac_rel_all']):.4e})")
+    for k, v in sd.items():
+        if "running" in k:
+            bar = max(1.25 * float(fb["ac_buf_rel." + k]), 1e-3)
+            if rel(v.float(), fx["buf." + k]) > bar:
+                fails.append(f"{k}: {rel(v.float(), fx['buf.' + k]):.3e} > {bar:.3e}")
+    assert not fails, fails
+    assert cos_all >= float(fb["ac_cos_all"]) and rel_all <= float(fb["ac_rel_all"])
+
+
 # ----------------------------------------------------------------------------- checkpoint interop
 def test_reference_checkpoint_resume(tmp_path):
     """A checkpoint written by the reference's own Trainer.save_checkpoint (tests/golden/

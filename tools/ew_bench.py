@@ -6,7 +6,7 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "dfc-sa-unet_amd")]
 import torch
 from dfcsa import ops
 from dfcsa._lib import LIB, call
-from dfcsa.ops import P, stream
+from dfcsa.ops import P, S, stream
 bf = torch.bfloat16
 
 
@@ -39,12 +39,12 @@ for tile, (B, H, C) in [(tl, s) for s in [(16, 224, 64), (16, 112, 128), (16, 56
     g = torch.ones(1, device="cuda")
     E = M * C * 2
     rows = {}
-    rows["bn_bwd_apply 2R1W"] = (bench(lambda: call("dfcsa_bn_bwd_apply", 1, M, C, P(a), P(b), P(mean), P(inv), P(sc), P(coef), P(c), None, stream())), 3 * E)
-    rows["bwd_relu_bn 2R1W+sums"] = (bench(lambda: call("dfcsa_bwd_relu_bn", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), P(part), stream())), 3 * E)
-    rows["bwd_relu_bn (no dz) 2R+sums"] = (bench(lambda: call("dfcsa_bwd_relu_bn", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), None, P(part), stream())), 2 * E)
-    rows["bn_bwd_apply_relu 2R1W"] = (bench(lambda: call("dfcsa_bn_bwd_apply_relu", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(sc), P(coef), P(c), None, stream())), 3 * E)
-    rows["bwd_gate 6R3W+sums"] = (bench(lambda: call("dfcsa_bwd_gate", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), P(d), P(e), P(f), P(h), P(part), stream())), 9 * E)
-    rows["bwd_block_out 3R2W+sums"] = (bench(lambda: call("dfcsa_bwd_block_out", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), P(g), P(d), P(e), P(part), stream())), 5 * E)
+    rows["bn_bwd_apply 2R1W"] = (bench(lambda: call("dfcsa_bn_bwd_apply", 1, M, C, P(a), P(b), P(mean), P(inv), P(sc), P(coef), P(c), None, 0, stream())), 3 * E)
+    rows["bwd_relu_bn 2R1W+sums"] = (bench(lambda: call("dfcsa_bwd_relu_bn", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), *S(part), stream())), 3 * E)
+    rows["bwd_relu_bn (no dz) 2R+sums"] = (bench(lambda: call("dfcsa_bwd_relu_bn", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), None, *S(part), stream())), 2 * E)
+    rows["bn_bwd_apply_relu 2R1W"] = (bench(lambda: call("dfcsa_bn_bwd_apply_relu", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(sc), P(coef), P(c), None, 0, stream())), 3 * E)
+    rows["bwd_gate 6R3W+sums"] = (bench(lambda: call("dfcsa_bwd_gate", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), P(d), P(e), P(f), P(h), *S(part), stream())), 9 * E)
+    rows["bwd_block_out 3R2W+sums"] = (bench(lambda: call("dfcsa_bwd_block_out", 1, M, C, P(a), P(b), P(sc), P(sh), P(mean), P(inv), P(c), P(g), P(d), P(e), *S(part), stream())), 5 * E)
     rows["local_attn 2R2W"] = (bench(lambda: call("dfcsa_block_local_attn", 1, B, H, H, C, P(a), P(sc), P(sh), P(b), P(sc), P(sh), P(o), 4, P(g), 1, P(c), P(d), stream())), 4 * E)
     rows["gate_fuse 3R1W"] = (bench(lambda: call("dfcsa_gate_fuse", 1, M, C, P(a), P(sc), P(sh), P(b), P(c), P(d), stream())), 4 * E)
     rows["block_out 2R1W"] = (bench(lambda: call("dfcsa_block_out", 1, M, C, P(a), P(sc), P(sh), P(b), P(g), P(c), stream())), 3 * E)

@@ -59,9 +59,10 @@ def _per_dispatch(db, counter):
     return out
 
 
-CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<"),
-           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<"),
-           "conv1x1_stream": ("conv1x1_stream_kernel",)}
+CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel"),
+           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
+           "conv1x1_stream": ("conv1x1_stream_kernel",),
+           "fused_block_gemm": ("dgrad_gate_kernel", "gate_fusion_fwd_kernel")}
 
 
 def traffic(fdb, wdb, out, pattern="conv_gemm"):
@@ -100,13 +101,18 @@ def traffic_all(fdb, wdb, out):
         print(c, r["launches"], round(r["hbm_bytes_per_launch"] / 1e6, 2), "MB/launch")
 
 
-GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<")),
-          ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_reduce_kernel")),
+GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
+                         "small_conv_f32_kernel")),
+          ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_halo_kernel", "wgrad_reduce_kernel",
+                          "small_wgrad_f32_kernel")),
           ("conv1x1_stream", ("conv1x1_stream_kernel",)),
+          ("fused_block_gemm (1x1 GEMMs with the gate / BN prologues and epilogues)",
+           ("dgrad_gate_kernel", "gate_fusion_fwd_kernel")),
+          ("block_out_pool (block output + max-pool fwd/bwd)", ("block_out_pool_kernel",)),
           ("ew_red (BN/gate/attention backward elementwise + partial sums)", ("ew_red_kernel",)),
           ("ew_fwd (BN apply, gate fusion, block output)", ("ew_fwd_kernel",)),
           ("bn_and_slab_finalizers", ("rows_reduce_kernel", "bn_finalize_kernel", "bn_bwd_finalize_kernel",
-                                      "slab_colsum", "sum_scalar_kernel")),
+                                      "slab_colsum", "sum_scalar_kernel", "colred")),
           ("lsa (pooled attention)", ("lsa_",)),
           ("maxpool", ("maxpool2",)),
           ("optimizer", ("sumsq_kernel", "clip_sgd_kernel", "set_flag_kernel")),
