@@ -534,7 +534,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   }
   if (!a.partial) return;  // sums not wanted (e.g. the analytically-zero conv-bias gradient)
   // deterministic in-workgroup reduction over pixel lanes
-  __shared__ float red[4 * 3 * 512];
+  __shared__ __attribute__((aligned(16))) float red[4 * 3 * 512];
   float* out = a.partial + (size_t)blockIdx.x * NS * a.C;
   const bool pow2 = (cpp & (cpp - 1)) == 0;
   if (pow2 && cpp <= 64) {
@@ -549,11 +549,11 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
         for (int off = cpp; off < 64; off <<= 1) v += __shfl_xor(v, off, 64);
         acc[s][q] = v;
       }
-    if (lane < cpp)
+    if (lane < cpp)   // 16-B stores (lds_st8): no 8-way bank conflicts
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) red[(wave * NS + s) * a.C + ck * 8 + q] = acc[s][q];
+      for (int s = 0; s < NS; ++s) {
+        lds_st8(red + (wave * NS + s) * a.C + ck * 8, acc[s]);
+      }
     __syncthreads();
     for (int e = tid; e < NS * a.C; e += 256) {
       const int s = e / a.C, c = e - s * a.C;
@@ -565,8 +565,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     if (active) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[(lane_px * cpp + ck) * 8 + q] = acc[s][q];
+      lds_st8(red + (lane_px * cpp + ck) * 8, acc[s]);
     }
     __syncthreads();
     for (int c = tid; c < a.C; c += 256) {
@@ -719,7 +718,7 @@ __global__ void __launch_bounds__(256) bwd_block_out_pool_kernel(const EwArgs a,
       }
     }
   }
-  __shared__ float red[4 * 3 * 512];
+  __shared__ __attribute__((aligned(16))) float red[4 * 3 * 512];
   float* outp = a.partial + (size_t)blockIdx.x * NS * a.C;
   const bool pow2 = (cpp & (cpp - 1)) == 0;
   if (pow2 && cpp <= 64) {
@@ -732,11 +731,11 @@ __global__ void __launch_bounds__(256) bwd_block_out_pool_kernel(const EwArgs a,
         for (int o = cpp; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
         acc[s][q] = v;
       }
-    if (lane < cpp)
+    if (lane < cpp)   // 16-B stores (lds_st8): no 8-way bank conflicts
 #pragma unroll
-      for (int s = 0; s < NS; ++s)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) red[(wave * NS + s) * a.C + ck * 8 + q] = acc[s][q];
+      for (int s = 0; s < NS; ++s) {
+        lds_st8(red + (wave * NS + s) * a.C + ck * 8, acc[s]);
+      }
     __syncthreads();
     for (int e = tid; e < NS * a.C; e += 256) {
       const int s = e / a.C, c = e - s * a.C;
@@ -748,8 +747,7 @@ __global__ void __launch_bounds__(256) bwd_block_out_pool_kernel(const EwArgs a,
 #pragma unroll
   for (int s = 0; s < NS; ++s) {
     if (active) {
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[(lane_px * cpp + ck) * 8 + q] = acc[s][q];
+      lds_st8(red + (lane_px * cpp + ck) * 8, acc[s]);
     }
     __syncthreads();
     for (int c = tid; c < a.C; c += 256) {

@@ -45,6 +45,12 @@ template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float
   v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
   v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
 }
+// 8 floats into LDS as two 16-B stores (p 16-B aligned).  Eight scalar stores at a lane stride of
+// 8 words hit the same bank 8 lanes at a time; the wide stores are split over the banks.
+__device__ __forceinline__ void lds_st8(float* p, const float (&v)[8]) {
+  *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);
+  *(float4*)(p + 4) = make_float4(v[4], v[5], v[6], v[7]);
+}
 template <typename T> __device__ __forceinline__ void store8(T* p, const float (&v)[8]);
 template <> __device__ __forceinline__ void store8<float>(float* p, const float (&v)[8]) {
   *(float4*)p = make_float4(v[0], v[1], v[2], v[3]);

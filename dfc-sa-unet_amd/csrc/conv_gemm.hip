@@ -77,8 +77,9 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t 
   constexpr int FM = WTM / 16, FN = WTN / 16;
   constexpr int OSTR = BN * (int)sizeof(T) + 16;
   const int M = args.M, N = args.N;
-  // (1) BatchNorm partial statistics of the raw accumulator, per column, rows m < M only, one
-  //     slab row per 64-row sub-tile of M (so the layout does not depend on the tile shape).
+  // (1) BatchNorm partial statistics of the raw accumulator, per column, rows m < M only, ONE
+  //     slab row per M tile (dfcsa_conv_stats_rows = ceil(M / BM)): the finalize reads BM/64 x
+  //     fewer rows.
   constexpr int SUBW = WTM >= 64 ? WTM / 64 : 1;   // sub-tiles covered by one wave
   constexpr int SUBS = BM / 64;                    // sub-tiles of the workgroup tile
   float* red = (float*)smem;                       // [WM][SUBW][2][BN] after the main loop
@@ -112,24 +113,22 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t 
       }
     }
     __syncthreads();
-    for (int e = tid; e < SUBS * BN; e += NT) {
-      const int st = e / BN, c = e - st * BN;
+    for (int c = tid; c < BN; c += NT) {
       const int n = n0 + c;
-      const int row0 = m0 + st * 64;
-      if (n < N && row0 < M) {
-        float sm = 0.f, q = 0.f;
+      if (n >= N) continue;
+      float sm = 0.f, q = 0.f;
+      for (int st = 0; st < SUBS; ++st) {    // sub-tiles in order (fixed summation order)
         if (WTM >= 64) {
           const int w = (st * 64) / WTM, u = st - w * SUBW;
-          sm = red[((w * SUBW + u) * 2) * BN + c];
-          q = red[((w * SUBW + u) * 2 + 1) * BN + c];
+          sm += red[((w * SUBW + u) * 2) * BN + c];
+          q += red[((w * SUBW + u) * 2 + 1) * BN + c];
         } else {
           for (int w = 0; w < WM; ++w)
             if ((w * WTM) / 64 == st) { sm += red[(w * 2) * BN + c]; q += red[(w * 2 + 1) * BN + c]; }
         }
-        const size_t t = (size_t)(m0 / 64) + st;
-        args.stats[t * 2 * N + n] = sm;
-        args.stats[t * 2 * N + N + n] = q;
       }
+      args.stats[(size_t)m_tile * 2 * N + n] = sm;
+      args.stats[(size_t)m_tile * 2 * N + N + n] = q;
     }
     __syncthreads();
   }
@@ -320,6 +319,9 @@ conv_gemm_kernel(const ConvGemmArgs args) {
 // Two LDS buffers; one vmcnt(0) + barrier per 64-deep K stage.
 // --------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];
+// dfcsa_conv_stats_rows: the launch functions report the statistics rows of the kernel they would
+// launch instead of launching (one row per M tile / per persistent workgroup)
+thread_local int* t_dry_rows = nullptr;
 __device__ __attribute__((aligned(16))) float g_store_sink[4 * 64];   // write-only target of masked stores
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -468,6 +470,7 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
   dim3 grid(xcd_pad(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM)));
   hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -701,6 +704,7 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
 
 template <int DEPTH, bool RF, bool BAL>
 int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
+  if (t_dry_rows) { *t_dry_rows = (a.M + 255) / 256; return 0; }
   dim3 grid(xcd_pad((a.N / 256) * ((a.M + 255) / 256)));
   hipLaunchKernelGGL((conv_gemm_pp_kernel<DEPTH, RF, BAL>), grid, dim3(512), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -756,25 +760,43 @@ struct HaloArgs {
   float* stats;
 };
 
-template <int BN>
-__global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) {
+// A fragment from a halo image: two ds_read_b64 per lane, lanes 16-31 / 48-63 reading the high
+// half of their 16-B chunk first.  Fragment rows start at any halo pixel (the tap's shift), and a
+// ds_read_b128 of 16 consecutive rows at an odd start conflicts (30 % of LDS cycles, measured);
+// each 32-lane b64 group here covers 16 consecutive rows x (chunk, half) pairs that the XOR
+// swizzle spreads over all 32 8-byte bank slots, at any start row.
+__device__ __forceinline__ bf16x8_t read_frag_halo(const char* t, int row, int g2, int lane) {
+  const int chunk = 4 * g2 + (lane >> 4);
+  const char* p = t + row * 128 + swz(row, chunk) * 16;
+  const int h = (lane >> 4) & 1;
+  const uint2 x = *(const uint2*)(p + 8 * h);
+  const uint2 y = *(const uint2*)(p + 8 * (h ^ 1));
+  const uint4 r = h ? make_uint4(y.x, y.y, x.x, x.y) : make_uint4(x.x, x.y, y.x, y.y);
+  return __builtin_bit_cast(bf16x8_t, r);
+}
+
+// WM x WN waves (16: four per SIMD, one workgroup per CU); wave tile (256 / WM) x (BN / WN).
+template <int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloArgs args) {
   using T = bf16_t;
-  constexpr int WTN = BN / 2, FM = 4, FN = WTN / 16;
+  constexpr int NW = WM * WN, NT = NW * 64, NL = NW / 2;   // NL loader waves per stream
+  constexpr int WTM = 256 / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
   constexpr int BSLOT = BN * 128, NBS = 3;
-  constexpr int KB = BN / 32;                    // weight DMA pieces per loader wave per step
-  constexpr int KH = (HALO_MAXPX / 8 + 3) / 4;   // halo DMA pieces per loader wave (upper bound)
+  constexpr int KB = BN / 8 / NL;                          // weight pieces per loader wave per step
+  constexpr int KH = (HALO_MAXPX / 8 + NL - 1) / NL;       // halo pieces per loader wave (upper bound)
   constexpr int OSTR = BN * 2 + 16;
   constexpr int SMEM = 2 * HALO_BYTES + NBS * BSLOT + 128;
-  static_assert(256 * OSTR + 2 * 4 * 2 * BN * 4 <= SMEM, "epilogue staging fits");
+  static_assert(KB >= 1 && FM >= 1 && FN >= 1, "halo tiling");
+  static_assert(256 * OSTR + WM * 2 * BN * 4 <= SMEM, "epilogue staging fits");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
   char* const hbuf = smem;
   char* const bbuf = smem + 2 * HALO_BYTES;
   char* const zrow = bbuf + NBS * BSLOT;         // a zero pixel: taps leaving the image
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool hloader = wave >= 4;                // waves 4-7 stream halos, 0-3 weight panels
-  const int w4 = wave & 3;
-  const int wm = wave & 3, wn = wave >> 2;
+  const bool hloader = wave >= NL;               // the upper half streams halos, the lower weight panels
+  const int wl = wave % NL;
+  const int wm = wave % WM, wn = wave / WM;
   const int nN = (args.N + BN - 1) / BN;
   const int L = xcd_remap(blockIdx.x, nN * args.tiles_m);
   if (L < 0) return;
@@ -784,13 +806,13 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
   const int TW = args.TW, HW2 = args.HW2, BH = args.BH, H = args.H, W = args.W;
   const int npx = TW * args.TR;
 
-  // A rows of this lane (fragment i: tile pixel wm*64 + i*16 + lane%16): halo pixel of the
+  // A rows of this lane (fragment i: tile pixel wm*WTM + i*16 + lane%16): halo pixel of the
   // centre tap and the 9-bit mask of taps that stay inside the pixel's image
   int p0[FM];
   unsigned tmask[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int m = wm * 64 + i * 16 + (lane & 15);
+    const int m = wm * WTM + i * 16 + (lane & 15);
     const int ty = m / TW, tx = m - ty * TW;
     const int gr = r0 + ty, x = c0 + tx, y = gr % H;
     const bool ok = m < npx && gr < BH;
@@ -804,29 +826,28 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     tmask[i] = mk;
   }
   const void* zero = (const void*)g_zero_page;
-  // halo pieces (waves 4-7): piece ii holds halo pixels 8ii..8ii+7; the lane fetches the chunk
-  // that the read-side swizzle expects in its LDS slot
-  int h_off[KH];
-  // weight pieces (waves 0-3): piece ii holds weight rows n0 + 8ii .. +7
-  int b_off[KB];
+  // halo pieces (upper waves): piece ii holds halo pixels 8ii..8ii+7; the lane fetches the chunk
+  // that the read-side swizzle expects in its LDS slot.  Weight pieces (lower waves): piece ii
+  // holds weight rows n0 + 8ii .. +7.
+  int off[KH > KB ? KH : KB];
   if (hloader) {
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
-      const int ii = min(w4 + 4 * k, args.ninstr - 1);
+      const int ii = min(wl + NL * k, args.ninstr - 1);
       const int q = ii * 8 + (lane >> 3);
       const int c = (lane & 7) ^ ((q >> 1) & 7);
       const int hy = q / HW2, hx = q - hy * HW2;
       const int gr = r0 - 1 + hy, ix = c0 - 1 + hx;
       const bool ok = q < args.nhalo && gr >= 0 && gr < BH && ix >= 0 && ix < W;
-      h_off[k] = ok ? (gr * W + ix) * args.Cseg + c * 8 : -1;
+      off[k] = ok ? (gr * W + ix) * args.Cseg + c * 8 : -1;
     }
   } else {
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
-      const int nl = (w4 + 4 * k) * 8 + (lane >> 3);
+      const int nl = (wl + NL * k) * 8 + (lane >> 3);
       const int n = n0 + nl;
       const int c = (lane & 7) ^ ((nl >> 1) & 7);
-      b_off[k] = n < args.N ? n * args.Kpad + c * 8 : -1;
+      off[k] = n < args.N ? n * args.Kpad + c * 8 : -1;
     }
   }
   auto issue_halo = [&](int g, int cc, int buf) {
@@ -834,17 +855,17 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     char* dst = hbuf + buf * HALO_BYTES;
 #pragma unroll
     for (int k = 0; k < KH; ++k) {
-      if (w4 + 4 * k >= args.ninstr) break;      // wave-uniform
-      const void* src = h_off[k] >= 0 ? (const void*)(base + h_off[k]) : zero;
-      glds16(src, dst + (w4 + 4 * k) * 1024);
+      if (wl + NL * k >= args.ninstr) break;     // wave-uniform
+      const void* src = off[k] >= 0 ? (const void*)(base + off[k]) : zero;
+      glds16(src, dst + (wl + NL * k) * 1024);
     }
   };
   auto issue_b = [&](int kofs, int slot) {
     char* dst = bbuf + slot * BSLOT;
 #pragma unroll
     for (int k = 0; k < KB; ++k) {
-      const void* src = b_off[k] >= 0 ? (const void*)((const T*)args.Bw + b_off[k] + kofs) : zero;
-      glds16(src, dst + (w4 + 4 * k) * 1024);
+      const void* src = off[k] >= 0 ? (const void*)((const T*)args.Bw + off[k] + kofs) : zero;
+      glds16(src, dst + (wl + NL * k) * 1024);
     }
   };
 
@@ -873,65 +894,63 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
 #pragma unroll
     for (int jj = 0; jj < FN; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
 
-  int g = 0, cc = 0, t = 0, j = 0;
-  for (int s = 0; s < S; ++s) {
-    if (!hloader) {
-      if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (t == 0) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    lds_barrier();   // publishes this step's weight panel (and, at t = 0, the chunk's halo)
-    if (!hloader) {
-      if (s + 2 < S) {
-        issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, (s + 2) % NBS);
-        badv();
-      }
-    } else if (t == 0 && j + 1 < J) {
-      const int nc = cc + 1 == args.nchunk ? 0 : cc + 1;
-      issue_halo(nc == 0 ? g + 1 : g, nc, (j + 1) & 1);
-    }
-    const HaloTap tp = args.grp[g].tap[t];
+  int s = 0;
+  for (int j = 0; j < J; ++j) {
+    const int g = j / args.nchunk, cc = j - g * args.nchunk;
+    const int ntaps = args.grp[g].ntaps;
     const char* hb = hbuf + (j & 1) * HALO_BYTES;
-    const char* bs = bbuf + (s % NBS) * BSLOT;
-    const char* abase[FM];
-    int arow[FM];
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const bool ok = (tmask[i] >> tp.bit) & 1;
-      abase[i] = ok ? hb : zrow;
-      arow[i] = ok ? p0[i] + tp.toff : 0;
-    }
+    for (int t = 0; t < 9; ++t) {
+      if (t >= ntaps) break;
+      if (!hloader) {
+        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      } else if (t == 0) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      lds_barrier();   // publishes this step's weight panel (and, at t = 0, the chunk's halo)
+      if (!hloader) {
+        if (s + 2 < S) {
+          issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, (s + 2) % NBS);
+          badv();
+        }
+      } else if (t == 0 && j + 1 < J) {
+        const int nc = cc + 1 == args.nchunk ? 0 : cc + 1;
+        issue_halo(nc == 0 ? g + 1 : g, nc, (j + 1) & 1);
+      }
+      const HaloTap tp = args.grp[g].tap[t];
+      const char* bs = bbuf + (s % NBS) * BSLOT;
+      const char* abase[FM];
+      int arow[FM];
 #pragma unroll
-    for (int g2 = 0; g2 < 2; ++g2) {
-      Frag<T> fa[FM], fb[FN];
+      for (int i = 0; i < FM; ++i) {
+        const bool ok = (tmask[i] >> tp.bit) & 1;
+        abase[i] = ok ? hb : zrow;
+        arow[i] = ok ? p0[i] + tp.toff : 0;
+      }
+      bf16x8_t fa[2][FM];
+      Frag<T> fb[2][FN];
 #pragma unroll
-      for (int i = 0; i < FM; ++i) read_frag<T>(abase[i], arow[i], g2, lane, fa[i]);
+      for (int g2 = 0; g2 < 2; ++g2) {
 #pragma unroll
-      for (int jj = 0; jj < FN; ++jj) read_frag<T>(bs, wn * WTN + jj * 16 + (lane & 15), g2, lane, fb[jj]);
+        for (int i = 0; i < FM; ++i) fa[g2][i] = read_frag_halo(abase[i], arow[i], g2, lane);
 #pragma unroll
-      for (int i = 0; i < FM; ++i)
+        for (int jj = 0; jj < FN; ++jj) read_frag<T>(bs, wn * WTN + jj * 16 + (lane & 15), g2, lane, fb[g2][jj]);
+      }
 #pragma unroll
-        for (int jj = 0; jj < FN; ++jj) mma(acc[i][jj], fa[i], fb[jj]);
-    }
-    if (++t == args.grp[g].ntaps) {
-      t = 0;
-      ++j;
-      if (++cc == args.nchunk) { cc = 0; ++g; }
+      for (int g2 = 0; g2 < 2; ++g2)
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int jj = 0; jj < FN; ++jj)
+            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[g2][i], fb[g2][jj].v, acc[i][jj], 0, 0, 0);
+      ++s;
     }
   }
   __syncthreads();
 
-  // ---- epilogue: accumulator element (i, jj, r) = tile pixel wm*64 + i*16 + (lane/16)*4 + r ----
-  unsigned vrow = 0;
-#pragma unroll
-  for (int i = 0; i < FM; ++i)
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
-      vrow |= (unsigned)(m < npx && r0 + m / TW < BH) << (i * 4 + r);
-    }
-  float* red = (float*)(smem + 256 * OSTR);      // [4 wm][2][BN]
+  // ---- epilogue: accumulator element (i, jj, r) = tile pixel wm*WTM + i*16 + (lane/16)*4 + r ----
+  float* red = (float*)(smem + 256 * OSTR);      // [WM][2][BN]
   if (args.stats) {
 #pragma unroll
     for (int jj = 0; jj < FN; ++jj) {
@@ -940,7 +959,8 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const float v = ((vrow >> (i * 4 + r)) & 1) ? acc[i][jj][r] : 0.f;
+          const int m = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+          const float v = (m < npx && r0 + m / TW < BH) ? acc[i][jj][r] : 0.f;
           sm += v;
           q += v * v;
         }
@@ -963,7 +983,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
         *(T*)((char*)otile + row * OSTR + col * 2) = f2bf(acc[i][jj][r] + bv);
       }
   }
@@ -973,13 +993,13 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     if (n < args.N) {
       float sm = 0.f, q = 0.f;
 #pragma unroll
-      for (int w = 0; w < 4; ++w) { sm += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
+      for (int w = 0; w < WM; ++w) { sm += red[(w * 2) * BN + tid]; q += red[(w * 2 + 1) * BN + tid]; }
       args.stats[(size_t)tm * 2 * args.N + n] = sm;
       args.stats[(size_t)tm * 2 * args.N + args.N + n] = q;
     }
   }
   constexpr int OCH = BN / 8;
-  for (int e = tid; e < 256 * OCH; e += 512) {
+  for (int e = tid; e < 256 * OCH; e += NT) {
     const int row = e / OCH, ck = e - row * OCH;
     const int ty = row / TW, tx = row - ty * TW;
     const int n = n0 + ck * 8;
@@ -1062,11 +1082,12 @@ bool halo_plan(const ConvGemmArgs& a, HaloArgs* h) {
 }
 
 int launch_halo(const HaloArgs& h, hipStream_t st) {
+  if (t_dry_rows) { *t_dry_rows = h.tiles_m; return 0; }
   const int bn = h.N <= 64 ? 64 : 128;
   const int nN = (h.N + bn - 1) / bn;
   dim3 grid(xcd_pad(nN * h.tiles_m));
-  if (bn == 64) hipLaunchKernelGGL((conv_halo_kernel<64>), grid, dim3(512), 0, st, h);
-  else hipLaunchKernelGGL((conv_halo_kernel<128>), grid, dim3(512), 0, st, h);
+  if (bn == 64) hipLaunchKernelGGL((conv_halo_kernel<64, 8, 2>), grid, dim3(1024), 0, st, h);
+  else hipLaunchKernelGGL((conv_halo_kernel<128, 4, 4>), grid, dim3(1024), 0, st, h);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1093,6 +1114,7 @@ bool small_conv_applies(const ConvGemmArgs& a) {
 
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
   hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -1201,6 +1223,9 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   }
   constexpr bool lean = !ACC;
   const bool with_stats = args.stats != nullptr;
+  float st_s[FN], st_q[FN];
+#pragma unroll
+  for (int j = 0; j < FN; ++j) { st_s[j] = 0.f; st_q[j] = 0.f; }
   int t = blockIdx.x;
   if (t >= mtiles) return;
   issue(t, 0);
@@ -1221,11 +1246,9 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
     if (tn < mtiles) {
       issue(tn, slot ^ 1);
       if (ACC || first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
-      else if (with_stats) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NSTORE + FN) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS + NSTORE) : "memory");
     } else {
       if (ACC || first_iter) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      else if (with_stats) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE + FN) : "memory");
       else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
     }
     first_iter = false;
@@ -1247,8 +1270,9 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
     }
     const int m0 = t * 64;
-    // BatchNorm partial sums of the raw accumulator over this 64-row tile (valid rows only)
-    if (args.stats) {
+    // BatchNorm partial sums of the raw accumulator over this 64-row tile (valid rows only), kept
+    // in registers across the workgroup's tiles: ONE statistics row per workgroup (row blockIdx.x)
+    if (with_stats) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) {
         float s = 0.f, q = 0.f;
@@ -1263,14 +1287,8 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
           }
         s += __shfl_xor(s, 16, 64); s += __shfl_xor(s, 32, 64);
         q += __shfl_xor(q, 16, 64); q += __shfl_xor(q, 32, 64);
-        const int n = n0 + wave * NWC + j * 16 + (lane & 15);
-        // one store instruction per fragment column, lanes 0-15: sum, 16-31: sum of squares; it is
-        // never skipped (lanes 0-31 are always active), columns >= N (only when N % NWG != 0) go
-        // to the sink -> a fixed store count per tile
-        if (lane < 32) {
-          float* dst = n < N ? args.stats + (size_t)t * 2 * N + (lane < 16 ? 0 : N) + n : g_store_sink + lane;
-          *dst = lane < 16 ? s : q;
-        }
+        st_s[j] += s;
+        st_q[j] += q;
       }
     }
     // bias + convert into the staging tile (previous tile's stores have drained: barrier above)
@@ -1309,6 +1327,14 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
       } else {
         *(uint4*)dst = v;
       }
+    }
+  }
+  if (with_stats) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wave * NWC + j * 16 + (lane & 15);
+      if (lane < 32 && n < N)
+        args.stats[(size_t)blockIdx.x * 2 * N + (lane < 16 ? 0 : N) + n] = lane < 16 ? st_s[j] : st_q[j];
     }
   }
 }
@@ -1386,7 +1412,7 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
   constexpr int OSTR = NWG * 2 + 16;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
   __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
-  __shared__ float red[4][2][64];
+  __shared__ __attribute__((aligned(16))) float red[4][2][64];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = args.M, C = args.Nd, K = args.K;
@@ -1580,9 +1606,10 @@ __global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args
     s0[q] = a0;
     s1[q] = a1;
   }
-  if (lane < 8)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) { red[wave][0][lane * 8 + q] = s0[q]; red[wave][1][lane * 8 + q] = s1[q]; }
+  if (lane < 8) {
+    lds_st8(&red[wave][0][lane * 8], s0);
+    lds_st8(&red[wave][1][lane * 8], s1);
+  }
   __syncthreads();
   if (tid < 128) {
     const int s = tid >> 6, c = tid & 63;
@@ -1878,8 +1905,9 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   const int ny = (a.N + 4 * NWC - 1) / (4 * NWC);
   const int per_cu = g_stream_wgs > 0 ? g_stream_wgs : occ;
   int gx = (256 * per_cu + ny - 1) / ny;
-  if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
   if (gx > mtiles) gx = mtiles;
+  if (t_dry_rows) { *t_dry_rows = gx; return 0; }   // one statistics row per workgroup column
+  if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
   if (a.accumulate)
     hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
   else
@@ -2009,6 +2037,7 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
   // fp32 (parity mode + the fp32 LightSelfAttention projections): few rows (M = B*P*P) -> the
   // split-reduction small-M kernel; other small problems get 64x64 tiles
   if (g_conv_cfg != 26 && small_conv_applies(a)) {
+    if (t_dry_rows) { *t_dry_rows = 0; return 0; }   // (no statistics)
     hipLaunchKernelGGL(small_conv_f32_kernel, dim3((a.M + 15) / 16, (a.N + 63) / 64), dim3(256), 0, st, a);
     DFCSA_CHECK_LAUNCH();
     return 0;
@@ -2045,9 +2074,13 @@ int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
   a.dbg = g_conv_dbg;
-  // statistics rows: one per 64-row M tile, or one per halo tile when the halo kernel runs it
-  HaloArgs h;
-  *rows = (d->dtype == DFCSA_DT_BF16 && g_conv_cfg == 0 && halo_plan(a, &h)) ? h.tiles_m : (d->M + 63) / 64;
+  // statistics rows of the kernel launch_t picks (a dry run of the selection)
+  int r = 0;
+  t_dry_rows = &r;
+  if (d->dtype == DFCSA_DT_BF16) launch_t<bf16_t>(a, nullptr);
+  else launch_t<float>(a, nullptr);
+  t_dry_rows = nullptr;
+  *rows = r;
   return 0;
 }
 }  // namespace

@@ -96,10 +96,8 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
       }
     }
   }
-  __shared__ float red[256 * 8];
-  if (lp < pl)
-#pragma unroll
-    for (int q = 0; q < 8; ++q) red[tid * 8 + q] = acc[q];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
+  if (lp < pl) lds_st8(red + tid * 8, acc);
   __syncthreads();
   float* out = partial + (((size_t)b * P * P + n) * S + s) * C;
   for (int c = tid; c < C; c += 256) {
@@ -217,7 +215,7 @@ __device__ __forceinline__ void contrib_range(int p, int in, int out, int& lo, i
 template <typename T>
 __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int C, const T* __restrict__ d, int P,
                                                               float* __restrict__ rows) {
-  __shared__ float red[256 * 8];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
   const int h = blockIdx.x, b = blockIdx.y;
   const int cpp = C >> 3, items = P * cpp;
   const int nsl = items >= 256 ? 1 : 256 / items;
@@ -265,9 +263,7 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
       }
       continue;
     }
-    if (on)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[(sl * items + e) * 8 + q] = acc[q];
+    if (on) lds_st8(red + (sl * items + e) * 8, acc);
     __syncthreads();
     for (int k = threadIdx.x; k < items * 8; k += 256) {
       const int it = k >> 3, q = k & 7;

@@ -148,11 +148,9 @@ __global__ void im2col_input_kernel(int B, int Csrc, int Cin, int H, int W, int 
 template <int NS>
 __device__ __forceinline__ void lane_reduce_store(const float (&acc)[NS][8], int C, int cpp, int pl, int lane_px,
                                                   int ck, bool active, float* out /* [NS][C] */) {
-  __shared__ float red[256 * 8];
+  __shared__ __attribute__((aligned(16))) float red[256 * 8];
   for (int s = 0; s < NS; ++s) {
-    if (active)
-#pragma unroll
-      for (int q = 0; q < 8; ++q) red[(lane_px * cpp + ck) * 8 + q] = acc[s][q];
+    if (active) lds_st8(red + (lane_px * cpp + ck) * 8, acc[s]);
     __syncthreads();
     for (int c = threadIdx.x; c < C; c += 256) {
       const int kq = c >> 3, q = c & 7;

@@ -310,14 +310,16 @@ def test_ew_reduction_slabs_guarded_and_capacity_checked():
 
 
 def test_conv_gemm_stats_capacity():
-    """dfcsa_conv_gemm refuses a statistics slab shorter than ceil(M/64) * 2 * N floats."""
+    """dfcsa_conv_gemm writes one statistics row per M tile of the kernel it picks (the count it
+    returns, at most ceil(M/64)) and refuses a slab shorter than that many rows * 2 * N floats."""
     M, C = 64 * 5 + 3, 64
     x = rnd(1, M, 1, C)
     w = rnd(C, 64, scale=0.1)
     y = torch.empty(1, M, 1, C, dtype=bf, device=dev)
     st = Guarded((ops.ntiles_gemm(M) * 2 * C,), torch.float32)
-    ops.conv_gemm(bf, [(x, 0, 0)], C, (1, M, 1), (M, 1), w, 64, C, [y], C, stats=st.t)
+    rows = ops.conv_gemm(bf, [(x, 0, 0)], C, (1, M, 1), (M, 1), w, 64, C, [y], C, stats=st.t)
     torch.cuda.synchronize()
-    assert st.intact() and st.written()
+    assert 1 <= rows <= ops.ntiles_gemm(M)
+    assert st.intact() and not torch.isnan(st.t[:rows * 2 * C]).any()
     with pytest.raises(DfcsaError, match="invalid"):
-        ops.conv_gemm(bf, [(x, 0, 0)], C, (1, M, 1), (M, 1), w, 64, C, [y], C, stats=st.t[:-1])
+        ops.conv_gemm(bf, [(x, 0, 0)], C, (1, M, 1), (M, 1), w, 64, C, [y], C, stats=st.t[:rows * 2 * C - 1])

@@ -1,0 +1,9 @@
+mkdir -p gpurun_out/pmc_halo
+R=$GRAFT_REPO_ROOT
+cd /tmp && export TMPDIR=/tmp
+for halo in 1 0; do
+  HALO=$halo timeout -s KILL 90 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/pmc_halo/t$halo -o run -- python3 $R/tools/halo_one.py > $R/gpurun_out/pmc_halo/t$halo.log 2>&1 || exit 1
+  HALO=$halo timeout -s KILL 90 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -d $R/gpurun_out/pmc_halo/p$halo -o run -- python3 $R/tools/halo_one.py > $R/gpurun_out/pmc_halo/p$halo.log 2>&1 || exit 1
+  HALO=$halo timeout -s KILL 90 rocprofv3 --pmc SQ_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_MFMA SQ_WAIT_INST_LDS SQ_INST_CYCLES_VMEM SQ_INSTS_SMEM -d $R/gpurun_out/pmc_halo/q$halo -o run -- python3 $R/tools/halo_one.py > $R/gpurun_out/pmc_halo/q$halo.log 2>&1 || exit 1
+done
+echo pmc done
