@@ -311,12 +311,14 @@ conv_gemm_kernel(const ConvGemmArgs args) {
 
 
 // --------------------------------------------------------------------------------------------
-// bf16 hot path: operands staged by LDS-DMA (global_load_lds_dwordx4).  Each wave-instruction
-// fills one 8-row x 128-B block of the K-stage image; the XOR swizzle is applied on the SOURCE
-// side (lane -> which 16-B chunk of its row it fetches), so the fragment reads are the same
-// conflict-free ds_read_b128 as the register-staged kernel.  Zero padding (image border, K tail,
-// N tail) fetches a 1-KB zero page instead of masking, so every LDS slot is written each stage.
-// Two LDS buffers; one vmcnt(0) + barrier per 64-deep K stage.
+// bf16 hot path: operands staged by LDS-DMA (buffer_load_dwordx4 ... lds through a raw buffer
+// descriptor, blds16 below).  Each wave-instruction fills one 8-row x 128-B block of the K-stage
+// image; the XOR swizzle is applied on the SOURCE side (lane -> which 16-B chunk of its row it
+// fetches), so the fragment reads are the same conflict-free ds_read_b128 as the register-staged
+// kernel.  Zero padding (image border, N tail) is an out-of-range lane offset, which reads zeros,
+// so every LDS slot is written each stage; the stage's tap shift and K offset are scalar (the
+// descriptor base / soffset), leaving ~2 VALU per DMA (round 2's 64-bit addresses and zero-page
+// selects cost ~8).  Two LDS buffers; one vmcnt(0) + barrier per 64-deep K stage.
 // --------------------------------------------------------------------------------------------
 __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];
 // dfcsa_conv_stats_rows: the launch functions report the statistics rows of the kernel they would
@@ -329,6 +331,24 @@ typedef const __attribute__((address_space(1))) void glb_void;
 
 __device__ __forceinline__ void glds16(const void* src, char* lds_base) {
   __builtin_amdgcn_global_load_lds((glb_void*)src, (lds_void*)lds_base, 16, 0, 0);
+}
+
+// LDS-DMA through a raw buffer descriptor (buffer_load_dwordx4 ... offen lds): the base is scalar
+// (SGPRs), the lane supplies a 32-bit byte offset, and an offset >= num_records reads zeros -- the
+// zero padding of image borders and N tails costs one bit-select per lane instead of a 64-bit
+// address and two selects against a zero page.  Sources must stay below 2 GiB (host-checked).
+typedef __amdgpu_buffer_rsrc_t rsrc_t;
+constexpr unsigned kBufOOB = 0x80000000u;        // any offset >= 2^31 is out of range
+__device__ __forceinline__ rsrc_t buf_rsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+__device__ __forceinline__ void blds16(rsrc_t r, unsigned voff, unsigned soff, char* lds_base) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)lds_base, 16, (int)voff, (int)soff, 0, 0);
+}
+// voff if bit `bit` of mask is set, else out of range (v_bfe_i32 + v_bfi_b32)
+__device__ __forceinline__ unsigned sel_oob(unsigned mask, int bit, unsigned voff) {
+  const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)mask, bit, 1);
+  return (voff & m) | (kBufOOB & ~m);
 }
 
 template <int BM, int BN, int WM, int WN, int NST>
@@ -364,11 +384,13 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   // chunk and a 9-bit "tap in bounds" mask (bit (dh+1)*3 + dw+1) remain.
   const int wv = __builtin_amdgcn_readfirstlane(wave);  // wave index as a scalar (M0 bases)
   const int lane_ch = cchunk * 8;
-  int a_off[A_IN], a_tap[A_IN];
+  // per lane: byte offset of its pixel row (+ chunk) in a source, and the 9-bit tap mask; the
+  // stage's shift and channel base go into the (scalar) buffer base
+  unsigned a_off[A_IN], a_tap[A_IN];
 #pragma unroll
   for (int i = 0; i < A_IN; ++i) {
     const int m = m0 + (i * NW + wave) * 8 + rsub;
-    a_off[i] = lane_ch;
+    a_off[i] = 0;
     a_tap[i] = 0;
     if (m < M) {
       const int b = dm_div(args.dm_hw, m);
@@ -376,27 +398,25 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
       const int oh = dm_div(args.dm_w, rem);
       const int ow = rem - oh * args.dm_w.d;
       const int ih = oh * args.stride, iw = ow * args.stride;
-      a_off[i] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch;
-      int t = 0;
+      a_off[i] = 2u * (unsigned)(((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch);
+      unsigned t = 0;
 #pragma unroll
       for (int dh = -1; dh <= 1; ++dh)
 #pragma unroll
         for (int dw = -1; dw <= 1; ++dw)
-          t |= (ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+          t |= (unsigned)(ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
       a_tap[i] = t;
     }
   }
-  // B rows: pointer at K = 0 for this lane's chunk (zero page + no advance for rows >= N)
-  const char* b_ptr[B_IN];
-  int b_step[B_IN];
+  // B rows: byte offset of the lane's row + chunk at K = 0 (out of range for rows >= N); the
+  // stage's K offset is the scalar soffset
+  unsigned b_off[B_IN];
 #pragma unroll
   for (int i = 0; i < B_IN; ++i) {
     const int n = n0 + (i * NW + wave) * 8 + rsub;
-    const bool ok = n < N;
-    b_ptr[i] = ok ? (const char*)((const T*)args.Bw + (size_t)n * args.Kpad + lane_ch) : (const char*)g_zero_page;
-    b_step[i] = ok ? 128 : 0;
+    b_off[i] = n < N ? 2u * (unsigned)(n * args.Kpad + lane_ch) : kBufOOB;
   }
-  const void* zero = (const void*)g_zero_page;
+  const rsrc_t rb = buf_rsrc(args.Bw);
 
   auto issue = [&](int kt, int buf) {
     char* A = smem + buf * STAGE;
@@ -407,20 +427,11 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
     const ConvSeg sg = args.seg[seg];                     // uniform index: scalar load
     const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
     const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
-    const T* base = (const T*)sg.ptr;
+    const rsrc_t ra = buf_rsrc((const T*)sg.ptr + delta);
 #pragma unroll
-    for (int i = 0; i < A_IN; ++i) {
-      const bool ok = __builtin_amdgcn_ubfe(a_tap[i], tb, 1) != 0;
-      const void* src = ok ? (const void*)(base + (unsigned)(a_off[i] + delta)) : zero;
-      if (args.dbg & 1) src = (const char*)zero + lane_ch * 2;
-      glds16(src, A + (i * NW + wv) * 8 * 128);
-    }
+    for (int i = 0; i < A_IN; ++i) blds16(ra, sel_oob(a_tap[i], tb, a_off[i]), 0, A + (i * NW + wv) * 8 * 128);
 #pragma unroll
-    for (int i = 0; i < B_IN; ++i) {
-      const void* src = b_ptr[i] + (size_t)kt * b_step[i];
-      if (args.dbg & 2) src = (const char*)zero + lane_ch * 2;
-      glds16(src, B + (i * NW + wv) * 8 * 128);
-    }
+    for (int i = 0; i < B_IN; ++i) blds16(rb, b_off[i], (unsigned)kt * 128u, B + (i * NW + wv) * 8 * 128);
   };
 
   f32x4_t acc[FM][FN];
@@ -525,14 +536,15 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
   const int lane_ch = cchunk * 8;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
 
-  // the 4 A rows and 4 B rows this lane fetches: index q = half*2 + instruction
-  int a_off[4], a_tap[4], b_off[4];
+  // the 4 A rows and 4 B rows this lane fetches: index q = half*2 + instruction; byte offsets for
+  // the buffer-descriptor LDS-DMA (blds16: the stage's shift goes into the scalar base)
+  unsigned a_off[4], a_tap[4], b_off[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int h = q >> 1, j = q & 1;
     const int hr = (j * 8 + wave) * 8 + rsub;            // row of the half-tile image
     const int m = m0 + (hr >> 6) * 128 + h * 64 + (hr & 63);
-    a_off[q] = lane_ch;
+    a_off[q] = 0;
     a_tap[q] = 0;
     if (m < M) {
       const int b = dm_div(args.dm_hw, m);
@@ -540,20 +552,19 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
       const int oh = dm_div(args.dm_w, rem);
       const int ow = rem - oh * args.dm_w.d;
       const int ih = oh * args.stride, iw = ow * args.stride;
-      a_off[q] = ((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch;
-      int t = 0;
+      a_off[q] = 2u * (unsigned)(((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch);
+      unsigned t = 0;
 #pragma unroll
       for (int dh = -1; dh <= 1; ++dh)
 #pragma unroll
         for (int dw = -1; dw <= 1; ++dw)
-          t |= (ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+          t |= (unsigned)(ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
       a_tap[q] = t;
     }
     const int n = n0 + (hr >> 5) * 64 + h * 32 + (hr & 31);
-    b_off[q] = n * args.Kpad + lane_ch;
+    b_off[q] = 2u * (unsigned)(n * args.Kpad + lane_ch);
   }
-  const void* zero = (const void*)g_zero_page;
-  const T* Bw = (const T*)args.Bw;
+  const rsrc_t rb = buf_rsrc(args.Bw);
   const int nk = args.Kpad / 64;
   const int slast = 4 * nk - 1;
 
@@ -571,23 +582,14 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
       const ConvSeg sg = args.seg[seg];
       const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
       const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
-      const T* base = (const T*)sg.ptr;
+      const rsrc_t ra = buf_rsrc((const T*)sg.ptr + delta);
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const bool ok = __builtin_amdgcn_ubfe(a_tap[h * 2 + j], tb, 1) != 0;
-        const void* src = ok ? (const void*)(base + (unsigned)(a_off[h * 2 + j] + delta)) : zero;
-        if (args.dbg & 1) src = (const char*)zero + lane_ch * 2;
-        glds16(src, dst + (j * 8 + wv) * 1024);
-      }
+      for (int j = 0; j < 2; ++j) blds16(ra, sel_oob(a_tap[h * 2 + j], tb, a_off[h * 2 + j]), 0, dst + (j * 8 + wv) * 1024);
     } else {
       const int h = i == 1 ? 0 : 1;
       char* dst = bufp + (2 + h) * HALF;
 #pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const void* src = Bw + (unsigned)(b_off[h * 2 + j] + kt * 64);
-        if (args.dbg & 2) src = (const char*)zero + lane_ch * 2;
-        glds16(src, dst + (j * 8 + wv) * 1024);
-      }
+      for (int j = 0; j < 2; ++j) blds16(rb, b_off[h * 2 + j], (unsigned)kt * 128u, dst + (j * 8 + wv) * 1024);
     }
   };
 
@@ -715,178 +717,140 @@ int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
 // 3x3 convolutions (forward and the fused 3x3 + 1x1 data gradient) on 2-D halo tiles.
 //
 // The row-tile kernels above fetch, for every one of the 9 taps, the tile's rows shifted by
-// (dh, dw): 9x the unique input per K chunk crosses L2 -> LDS, and the 128x128 tile spends a
-// 32-KB fetch per 2.1 MFLOP (64 flop/B), which bounds it at ~0.2-0.45 of MFMA peak by the
-// per-CU L2->LDS rate.  Here a workgroup owns a TW x TR block of output
-// pixels (TW | W, TR rows of the image-stacked B*H grid, TW*TR <= 256) and, per 64-channel chunk
-// of a source, DMAs its (TW+2) x (TR+2) halo into LDS ONCE; the taps of that source read their
-// shifted windows from the halo (per lane: halo pixel = p0 + dh*(TW+2) + dw; a tap that leaves the
-// lane's image reads a zero row instead, so tiles may straddle images and the pad lanes of a
-// 252-pixel tile are harmless).  Only the weight panel (BN x 64 per tap) streams per step: at
-// 256 x 128 the step moves 16 KB + ~4.8 KB of halo per 4.2 MFLOP (~200 flop/B).
+// (dh, dw): 9x the unique input per K chunk crosses L2 -> LDS.  Here a workgroup owns a TW x TR
+// block of output pixels of ONE image (TW | W, TR | H: a tap never needs a per-pixel border
+// mask, the halo pixels outside the image are zero) and, per 64-channel chunk of a source, stages
+// its (TW+2) x (TR+2) halo in LDS once; the tap steps read their shifted windows from it.  Only
+// the weight panel (BN x 64 of one tap) streams per step.
 //
-// 8 waves (one workgroup per CU, ~150 KB LDS): 4 (M) x 2 (N), wave tile 64 x BN/2.  Waves 0-3
-// also stream the weight panels (3-slot ring, issued two steps ahead), waves 4-7 the halos
-// (double buffer, the next chunk's halo issued at the first tap of the current one): each wave's
-// counted vmcnt covers only its own DMA stream, so a halo in flight never holds up a weight
-// panel and vice versa; one barrier per step publishes both.  Sources = groups of segments with
-// the same tensor (the skip concat's two sources, the dgrad's dy1 taps + the two 1x1 sources).
+// Instruction economy (round-3 counters: the row-tile kernels issue ~5 VALU per MFMA, the
+// round-3 v1/v2 halo kernels 10-13, and the wave time goes to issue, not to the MFMA pipe):
+//  * halo pixels sit at a 160-B pitch (128 B of channels + 32 B pad): the 16 rows of a ds_read_b128
+//    fragment read are then spread over all 64 banks whatever pixel they start at (the b128 lane
+//    groups {0-3,12-15,20-27}... map rows to 40r + 4c words: distinct 4-bank spans), so the A
+//    operand of tap (dh, dw) is one b128 per fragment at (lane base + tap offset): one v_add per
+//    fragment per step, no swizzle arithmetic and no masks;
+//  * the halo is register-staged (buffer_load_dwordx4 with a raw buffer descriptor: pixels outside
+//    the image are out-of-range offsets and read as zeros), issued at the first tap of a chunk
+//    and written at its last;
+//  * the weight panel arrives by LDS-DMA through a buffer descriptor (scalar K offset per step, an
+//    out-of-range row offset for the N tail) into a 3-slot ring, two steps ahead, XOR-swizzled on
+//    the source side for conflict-free b128 reads;
+//  * the step list (K column, tap offset, chunk boundaries) is precomputed on the host.
+// 8 waves (4 x 2, wave tile 64 x BN/2), one workgroup per CU; one barrier per step.
 // Epilogue: bias, bf16 store of the valid pixels (1-3 destinations, optional accumulate), BN
-// partial statistics as ONE row per M tile (dfcsa_conv_stats_rows gives the row count).
+// partial statistics as ONE row per tile (dfcsa_conv_stats_rows gives the row count).
 // --------------------------------------------------------------------------------------------
-constexpr int HALO_MAXPX = 400;                 // (TW+2)*(TR+2) <= 400 (rounded up to 8)
-constexpr int HALO_BYTES = HALO_MAXPX * 128;    // one halo buffer (64 channels, 128 B / pixel)
+constexpr int HALO_PITCH = 160;                 // LDS bytes per halo pixel (64 channels + pad)
+constexpr int HALO_MAXSTEP = 192;               // steps (source x chunk x tap) per launch
 
-struct HaloTap {
-  int toff;   // halo-pixel offset of the tap: dh*(TW+2) + dw
-  int bit;    // (dh+1)*3 + (dw+1): the lane's tap-validity bit
-  int kofs;   // K offset of the tap's segment (segment index * Cseg)
-};
-struct HaloGroup {
-  const void* ptr;
-  int ntaps;
-  HaloTap tap[9];
-};
 struct HaloArgs {
-  int M, N, Kpad, Cseg, BH, H, W;
-  int TW, TR, HW2, nhalo, ninstr;   // tile, halo row pitch (TW+2), halo pixels, 1-KB DMA pieces
-  int tiles_x, tiles_m;             // W / TW, M tiles
-  int ngroups, nchunk;              // sources, 64-channel chunks per source
-  HaloGroup grp[4];
+  int M, N, Kpad, Cseg, H, W;
+  int tiles_x, tiles_y, tiles_m;    // W / TW, H / TR, all tiles
+  int nsteps;
+  const void* gptr[4];              // source tensors ([B][H][W][Cseg])
   const void* Bw;
   const float* bias;
   void* dest[3];
   int Nd, accumulate;
   float* stats;
+  // step s: bits 0-15 K column of the weight panel, 16-23 tap offset (dh+1)*(TW+2) + dw+1 in halo
+  // pixels, 24-25 source, 26 first tap of a chunk, 27 last tap of a chunk, 28-31 chunk index
+  unsigned step[HALO_MAXSTEP];
 };
 
-// A fragment from a halo image: two ds_read_b64 per lane, lanes 16-31 / 48-63 reading the high
-// half of their 16-B chunk first.  Fragment rows start at any halo pixel (the tap's shift), and a
-// ds_read_b128 of 16 consecutive rows at an odd start conflicts (30 % of LDS cycles, measured);
-// each 32-lane b64 group here covers 16 consecutive rows x (chunk, half) pairs that the XOR
-// swizzle spreads over all 32 8-byte bank slots, at any start row.
-__device__ __forceinline__ bf16x8_t read_frag_halo(const char* t, int row, int g2, int lane) {
-  const int chunk = 4 * g2 + (lane >> 4);
-  const char* p = t + row * 128 + swz(row, chunk) * 16;
-  const int h = (lane >> 4) & 1;
-  const uint2 x = *(const uint2*)(p + 8 * h);
-  const uint2 y = *(const uint2*)(p + 8 * (h ^ 1));
-  const uint4 r = h ? make_uint4(y.x, y.y, x.x, x.y) : make_uint4(x.x, x.y, y.x, y.y);
-  return __builtin_bit_cast(bf16x8_t, r);
-}
-
-// WM x WN waves (16: four per SIMD, one workgroup per CU); wave tile (256 / WM) x (BN / WN).
-template <int BN, int WM, int WN>
-__global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloArgs args) {
+template <int TW, int TR, int BN>
+__global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) {
   using T = bf16_t;
-  constexpr int NW = WM * WN, NT = NW * 64, NL = NW / 2;   // NL loader waves per stream
-  constexpr int WTM = 256 / WM, WTN = BN / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int WM = 4, WN = 2, NT = 512;
+  constexpr int WTN = BN / WN, FM = 4, FN = WTN / 16;
+  constexpr int HW2 = TW + 2, HPX = (TW + 2) * (TR + 2);
+  constexpr int HBUF = (HPX * HALO_PITCH + 255) / 256 * 256;
   constexpr int BSLOT = BN * 128, NBS = 3;
-  constexpr int KB = BN / 8 / NL;                          // weight pieces per loader wave per step
-  constexpr int KH = (HALO_MAXPX / 8 + NL - 1) / NL;       // halo pieces per loader wave (upper bound)
+  constexpr int KB = BN / 64;                    // weight DMA pieces per wave per step (1 KB each)
+  constexpr int HCH = HPX * 8;                   // 16-B chunks of one halo
+  constexpr int HL = (HCH + NT - 1) / NT;        // halo chunks per thread
   constexpr int OSTR = BN * 2 + 16;
-  constexpr int SMEM = 2 * HALO_BYTES + NBS * BSLOT + 128;
-  static_assert(KB >= 1 && FM >= 1 && FN >= 1, "halo tiling");
-  static_assert(256 * OSTR + WM * 2 * BN * 4 <= SMEM, "epilogue staging fits");
+  constexpr int SMEM_MAIN = 2 * HBUF + NBS * BSLOT;
+  constexpr int SMEM_EPI = 256 * OSTR + WM * 2 * BN * 4;
+  constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
+  static_assert(TW * TR <= 256 && SMEM <= 160 * 1024 && FN >= 1, "halo tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  char* const hbuf = smem;
-  char* const bbuf = smem + 2 * HALO_BYTES;
-  char* const zrow = bbuf + NBS * BSLOT;         // a zero pixel: taps leaving the image
+  char* const bbuf = smem + 2 * HBUF;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const bool hloader = wave >= NL;               // the upper half streams halos, the lower weight panels
-  const int wl = wave % NL;
   const int wm = wave % WM, wn = wave / WM;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
   const int nN = (args.N + BN - 1) / BN;
   const int L = xcd_remap(blockIdx.x, nN * args.tiles_m);
   if (L < 0) return;
-  const int tn = L % nN, tm = L / nN;            // the N tiles of one M tile share an XCD
-  const int trow = tm / args.tiles_x, tcol = tm - trow * args.tiles_x;
-  const int r0 = trow * args.TR, c0 = tcol * args.TW, n0 = tn * BN;
-  const int TW = args.TW, HW2 = args.HW2, BH = args.BH, H = args.H, W = args.W;
-  const int npx = TW * args.TR;
+  const int tn = L % nN, tm = L / nN;            // the N tiles of one pixel tile share an XCD
+  const int tx = tm % args.tiles_x, rest = tm / args.tiles_x;
+  const int ty = rest % args.tiles_y, img = rest / args.tiles_y;
+  const int y0 = ty * TR, x0 = tx * TW, n0 = tn * BN;
+  const int H = args.H, W = args.W;
 
-  // A rows of this lane (fragment i: tile pixel wm*WTM + i*16 + lane%16): halo pixel of the
-  // centre tap and the 9-bit mask of taps that stay inside the pixel's image
-  int p0[FM];
-  unsigned tmask[FM];
+  // halo staging: thread chunk e = tid + k*NT -> halo pixel e/8, 16-B chunk e%8
+  unsigned hoff[HL];
+  int hlds[HL];
+#pragma unroll
+  for (int k = 0; k < HL; ++k) {
+    const int e = tid + k * NT;
+    const int q = e >> 3, c = e & 7;
+    const int hy = q / HW2, hx = q - hy * HW2;
+    const int y = y0 - 1 + hy, x = x0 - 1 + hx;
+    const bool ok = e < HCH && y >= 0 && y < H && x >= 0 && x < W;
+    hoff[k] = ok ? 2u * (unsigned)((((img * H + y) * W + x) * args.Cseg) + c * 8) : kBufOOB;
+    hlds[k] = e < HCH ? q * HALO_PITCH + c * 16 : -1;
+  }
+  // weight panel DMA: piece p = wave + 8k holds panel rows 8p..8p+7; the lane fetches the logical
+  // chunk that read_frag's swizzle expects in its LDS slot
+  unsigned boff[KB];
+#pragma unroll
+  for (int k = 0; k < KB; ++k) {
+    const int nl = (wave + 8 * k) * 8 + (lane >> 3);
+    const int c = (lane & 7) ^ ((nl >> 1) & 7);
+    const int n = n0 + nl;
+    boff[k] = n < args.N ? 2u * (unsigned)(n * args.Kpad + c * 8) : kBufOOB;
+  }
+  const rsrc_t rb = buf_rsrc(args.Bw);
+  auto issue_b = [&](int s) {
+    const unsigned w = args.step[s];
+    char* dst = bbuf + (s % NBS) * BSLOT;
+#pragma unroll
+    for (int k = 0; k < KB; ++k) blds16(rb, boff[k], 2u * (w & 0xffffu), dst + (wv + 8 * k) * 1024);
+  };
+  typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+  u32x4_t hreg[HL];
+  auto load_halo = [&](unsigned w) {
+    const rsrc_t rs = buf_rsrc(args.gptr[(w >> 24) & 3]);
+    const unsigned soff = (w >> 28) * 128u;      // chunk cc: channels 64cc..64cc+63
+#pragma unroll
+    for (int k = 0; k < HL; ++k) hreg[k] = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)hoff[k], (int)soff, 0);
+  };
+  auto store_halo = [&](int buf) {
+#pragma unroll
+    for (int k = 0; k < HL; ++k)
+      if (hlds[k] >= 0) *(u32x4_t*)(smem + buf * HBUF + hlds[k]) = hreg[k];
+  };
+
+  // A fragment bases: tile pixel m = wm*64 + 16i + lane%16 -> halo pixel of tap (-1, -1)
+  int abase[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
-    const int m = wm * WTM + i * 16 + (lane & 15);
-    const int ty = m / TW, tx = m - ty * TW;
-    const int gr = r0 + ty, x = c0 + tx, y = gr % H;
-    const bool ok = m < npx && gr < BH;
-    p0[i] = (ty + 1) * HW2 + tx + 1;
-    unsigned mk = 0;
-#pragma unroll
-    for (int dh = -1; dh <= 1; ++dh)
-#pragma unroll
-      for (int dw = -1; dw <= 1; ++dw)
-        mk |= (unsigned)(ok && y + dh >= 0 && y + dh < H && x + dw >= 0 && x + dw < W) << ((dh + 1) * 3 + dw + 1);
-    tmask[i] = mk;
+    const int m = wm * 64 + i * 16 + (lane & 15);
+    const int r = m / TW, c = m - r * TW;
+    abase[i] = (m < TW * TR ? (r * HW2 + c) * HALO_PITCH : 0) + (lane >> 4) * 16;
   }
-  const void* zero = (const void*)g_zero_page;
-  // halo pieces (upper waves): piece ii holds halo pixels 8ii..8ii+7; the lane fetches the chunk
-  // that the read-side swizzle expects in its LDS slot.  Weight pieces (lower waves): piece ii
-  // holds weight rows n0 + 8ii .. +7.
-  int off[KH > KB ? KH : KB];
-  if (hloader) {
+  // B fragment offsets in a ring slot: row wn*WTN + 16jj + lane%16, logical chunk 4g2 + lane/16
+  int bofs[FN][2];
 #pragma unroll
-    for (int k = 0; k < KH; ++k) {
-      const int ii = min(wl + NL * k, args.ninstr - 1);
-      const int q = ii * 8 + (lane >> 3);
-      const int c = (lane & 7) ^ ((q >> 1) & 7);
-      const int hy = q / HW2, hx = q - hy * HW2;
-      const int gr = r0 - 1 + hy, ix = c0 - 1 + hx;
-      const bool ok = q < args.nhalo && gr >= 0 && gr < BH && ix >= 0 && ix < W;
-      off[k] = ok ? (gr * W + ix) * args.Cseg + c * 8 : -1;
-    }
-  } else {
+  for (int jj = 0; jj < FN; ++jj)
 #pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const int nl = (wl + NL * k) * 8 + (lane >> 3);
-      const int n = n0 + nl;
-      const int c = (lane & 7) ^ ((nl >> 1) & 7);
-      off[k] = n < args.N ? n * args.Kpad + c * 8 : -1;
+    for (int g2 = 0; g2 < 2; ++g2) {
+      const int row = wn * WTN + jj * 16 + (lane & 15);
+      bofs[jj][g2] = row * 128 + swz(row, 4 * g2 + (lane >> 4)) * 16;
     }
-  }
-  auto issue_halo = [&](int g, int cc, int buf) {
-    const T* base = (const T*)args.grp[g].ptr + cc * 64;
-    char* dst = hbuf + buf * HALO_BYTES;
-#pragma unroll
-    for (int k = 0; k < KH; ++k) {
-      if (wl + NL * k >= args.ninstr) break;     // wave-uniform
-      const void* src = off[k] >= 0 ? (const void*)(base + off[k]) : zero;
-      glds16(src, dst + (wl + NL * k) * 1024);
-    }
-  };
-  auto issue_b = [&](int kofs, int slot) {
-    char* dst = bbuf + slot * BSLOT;
-#pragma unroll
-    for (int k = 0; k < KB; ++k) {
-      const void* src = off[k] >= 0 ? (const void*)((const T*)args.Bw + off[k] + kofs) : zero;
-      glds16(src, dst + (wl + NL * k) * 1024);
-    }
-  };
-
-  // step = (source g, channel chunk cc, tap t); chunks j = (g, cc) in order
-  int S = 0;
-  for (int g = 0; g < args.ngroups; ++g) S += args.grp[g].ntaps;
-  S *= args.nchunk;
-  const int J = args.ngroups * args.nchunk;
-  int bg = 0, bcc = 0, bt = 0;                   // weight-prefetch cursor (two steps ahead)
-  auto badv = [&]() {
-    if (++bt == args.grp[bg].ntaps) { bt = 0; if (++bcc == args.nchunk) { bcc = 0; ++bg; } }
-  };
-  if (hloader) {
-    issue_halo(0, 0, 0);
-  } else {
-    issue_b(args.grp[0].tap[0].kofs, 0);
-    badv();
-    if (S > 1) issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, 1);
-    badv();
-  }
-  if (tid < 8) *(uint4*)(zrow + tid * 16) = make_uint4(0, 0, 0, 0);
 
   f32x4_t acc[FM][FN];
 #pragma unroll
@@ -894,62 +858,61 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloAr
 #pragma unroll
     for (int jj = 0; jj < FN; ++jj) acc[i][jj] = {0.f, 0.f, 0.f, 0.f};
 
-  int s = 0;
-  for (int j = 0; j < J; ++j) {
-    const int g = j / args.nchunk, cc = j - g * args.nchunk;
-    const int ntaps = args.grp[g].ntaps;
-    const char* hb = hbuf + (j & 1) * HALO_BYTES;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-      if (t >= ntaps) break;
-      if (!hloader) {
-        if (s + 1 < S) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      } else if (t == 0) {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  const int S = args.nsteps;
+  load_halo(args.step[0]);
+  store_halo(0);                                 // (the compiler waits for the loads)
+  issue_b(0);
+  if (S > 1) issue_b(1);
+  int hb = 0;                                    // halo buffer of the current chunk
+  int hs = -8;                                   // step that issued the halo loads in flight
+  for (int s = 0; s < S; ++s) {
+    const unsigned w = args.step[s];
+    // this step's weight panel: vmcnt is in order, so the panel issued two steps ago is complete
+    // once at most the later ones are in flight -- the next step's panel, plus, for the two steps
+    // after a halo issue, that halo's HL loads (issued after panel s+2; the wait of step hs+3
+    // retires them)
+    if (s + 1 >= S) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (s - hs <= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB + HL) : "memory");
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
+    lds_barrier();   // publishes this step's weight panel (and, at a chunk's first tap, its halo)
+    if (s + 2 < S) issue_b(s + 2);
+    const bool more = s + 1 < S;
+    if (((w >> 26) & 1) && !((w >> 27) & 1 && !more)) {
+      // first tap of a chunk: fetch the next chunk's halo (the step after this chunk's last tap)
+      int u = s;
+      while (u < S && !((args.step[u] >> 27) & 1)) ++u;
+      if (u + 1 < S) {
+        load_halo(args.step[u + 1]);
+        hs = s;
       }
-      lds_barrier();   // publishes this step's weight panel (and, at t = 0, the chunk's halo)
-      if (!hloader) {
-        if (s + 2 < S) {
-          issue_b(args.grp[bg].tap[bt].kofs + bcc * 64, (s + 2) % NBS);
-          badv();
-        }
-      } else if (t == 0 && j + 1 < J) {
-        const int nc = cc + 1 == args.nchunk ? 0 : cc + 1;
-        issue_halo(nc == 0 ? g + 1 : g, nc, (j + 1) & 1);
-      }
-      const HaloTap tp = args.grp[g].tap[t];
-      const char* bs = bbuf + (s % NBS) * BSLOT;
-      const char* abase[FM];
-      int arow[FM];
+    }
+    const int toff = hb * HBUF + (int)((w >> 16) & 0xffu) * HALO_PITCH;
+    const char* bs = bbuf + (s % NBS) * BSLOT;
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bool ok = (tmask[i] >> tp.bit) & 1;
-        abase[i] = ok ? hb : zrow;
-        arow[i] = ok ? p0[i] + tp.toff : 0;
-      }
-      bf16x8_t fa[2][FM];
-      Frag<T> fb[2][FN];
+    for (int g2 = 0; g2 < 2; ++g2) {
+      bf16x8_t fa[FM], fb[FN];
 #pragma unroll
-      for (int g2 = 0; g2 < 2; ++g2) {
+      for (int i = 0; i < FM; ++i) fa[i] = *(const bf16x8_t*)(smem + abase[i] + toff + 64 * g2);
 #pragma unroll
-        for (int i = 0; i < FM; ++i) fa[g2][i] = read_frag_halo(abase[i], arow[i], g2, lane);
+      for (int jj = 0; jj < FN; ++jj) fb[jj] = *(const bf16x8_t*)(bs + bofs[jj][g2]);
 #pragma unroll
-        for (int jj = 0; jj < FN; ++jj) read_frag<T>(bs, wn * WTN + jj * 16 + (lane & 15), g2, lane, fb[g2][jj]);
-      }
+      for (int i = 0; i < FM; ++i)
 #pragma unroll
-      for (int g2 = 0; g2 < 2; ++g2)
-#pragma unroll
-        for (int i = 0; i < FM; ++i)
-#pragma unroll
-          for (int jj = 0; jj < FN; ++jj)
-            acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[g2][i], fb[g2][jj].v, acc[i][jj], 0, 0, 0);
-      ++s;
+        for (int jj = 0; jj < FN; ++jj)
+          acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
+    }
+    if (((w >> 27) & 1) && more) {
+      // last tap of a chunk: the next chunk's halo goes to the other buffer (read from the next
+      // step on, after its barrier; that buffer's last reader was the previous chunk)
+      hb ^= 1;
+      store_halo(hb);
+      hs = -8;
     }
   }
   __syncthreads();
 
-  // ---- epilogue: accumulator element (i, jj, r) = tile pixel wm*WTM + i*16 + (lane/16)*4 + r ----
+  // ---- epilogue: accumulator element (i, jj, r) = tile pixel wm*64 + 16i + 4(lane/16) + r ----
+  constexpr int NPX = TW * TR;
   float* red = (float*)(smem + 256 * OSTR);      // [WM][2][BN]
   if (args.stats) {
 #pragma unroll
@@ -959,8 +922,8 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloAr
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int m = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
-          const float v = (m < npx && r0 + m / TW < BH) ? acc[i][jj][r] : 0.f;
+          const int m = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
+          const float v = m < NPX ? acc[i][jj][r] : 0.f;
           sm += v;
           q += v * v;
         }
@@ -983,7 +946,7 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloAr
     for (int i = 0; i < FM; ++i)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int row = wm * WTM + i * 16 + (lane >> 4) * 4 + r;
+        const int row = wm * 64 + i * 16 + (lane >> 4) * 4 + r;
         *(T*)((char*)otile + row * OSTR + col * 2) = f2bf(acc[i][jj][r] + bv);
       }
   }
@@ -999,12 +962,12 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloAr
     }
   }
   constexpr int OCH = BN / 8;
-  for (int e = tid; e < 256 * OCH; e += NT) {
+  for (int e = tid; e < NPX * OCH; e += NT) {
     const int row = e / OCH, ck = e - row * OCH;
-    const int ty = row / TW, tx = row - ty * TW;
+    const int r = row / TW, c = row - r * TW;
     const int n = n0 + ck * 8;
-    if (row >= npx || r0 + ty >= BH || n >= args.N) continue;
-    const size_t mg = (size_t)(r0 + ty) * W + c0 + tx;
+    if (n >= args.N) continue;
+    const size_t mg = (size_t)(img * H + y0 + r) * W + x0 + c;
     float v[8];
     load8<T>((const T*)((const char*)otile + row * OSTR + ck * 16), v);
     const int d = n / args.Nd, col = n - d * args.Nd;
@@ -1019,75 +982,84 @@ __global__ void __launch_bounds__(WM * WN * 64, 1) conv_halo_kernel(const HaloAr
   }
 }
 
-int g_halo_min_m = 0;   // knob 19: smallest M routed to the halo kernel (0: never; off until it beats the row tiles)
+int g_halo_min_m = 0;   // knob 19: smallest M routed to the halo kernel (0: never)
 
 // Build the halo launch for a bf16 3x3 (or fused 3x3 + 1x1) GEMM; false if it does not apply.
-bool halo_plan(const ConvGemmArgs& a, HaloArgs* h) {
+// Tile shapes: 16 x 16 (W, H multiples of 16: the 224^2 / 112^2 levels), 8 x 28 (56^2),
+// 14 x 14 (28^2).  *tw / *tr return the shape.
+bool halo_plan(const ConvGemmArgs& a, HaloArgs* h, int* tw, int* tr) {
   if (g_halo_min_m <= 0 || a.M < g_halo_min_m) return false;
   if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Ho != a.Hi || a.Wo != a.Wi || a.Cseg % 64) return false;
-  if ((int64_t)a.M * a.Cseg >= (1ll << 31) || (int64_t)a.N * a.Kpad >= (1ll << 31)) return false;
-  bool shifted = false;
+  const int H = a.Ho, W = a.Wo;
+  if ((int64_t)a.M * a.Cseg * 2 >= (1ll << 31) || (int64_t)a.N * a.Kpad * 2 >= (1ll << 31) || a.Kpad > 65535)
+    return false;
+  int TW, TR;
+  if (W % 16 == 0 && H % 16 == 0) { TW = 16; TR = 16; }
+  else if (W % 8 == 0 && H % 28 == 0) { TW = 8; TR = 28; }
+  else if (W % 14 == 0 && H % 14 == 0) { TW = 14; TR = 14; }
+  else return false;
   std::memset(h, 0, sizeof(*h));
+  // sources: segments grouped by tensor, in first-appearance order; each segment = one tap
+  const void* src[4];
+  int nsrc = 0, gseg[DFCSA_MAX_SEG];
+  bool shifted = false;
   for (int i = 0; i < a.nseg; ++i) {
     const ConvSeg& s = a.seg[i];
     if (s.dh < -1 || s.dh > 1 || s.dw < -1 || s.dw > 1) return false;
     shifted |= (s.dh || s.dw);
     int g = 0;
-    while (g < h->ngroups && h->grp[g].ptr != s.ptr) ++g;
-    if (g == h->ngroups) {
-      if (g == 4) return false;
-      h->grp[g].ptr = s.ptr;
-      h->ngroups++;
+    while (g < nsrc && src[g] != s.ptr) ++g;
+    if (g == nsrc) {
+      if (nsrc == 4) return false;
+      src[nsrc++] = s.ptr;
     }
-    HaloGroup& G = h->grp[g];
-    if (G.ntaps == 9) return false;
-    G.tap[G.ntaps].bit = (s.dh + 1) * 3 + s.dw + 1;
-    G.tap[G.ntaps].kofs = i * a.Cseg;
-    G.tap[G.ntaps].toff = s.dh * 1000 + s.dw;    // resolved once TW is known
-    G.ntaps++;
+    gseg[i] = g;
   }
   if (!shifted) return false;
-  const int W = a.Wo, BH = a.M / a.Wo;
-  // tile: TW | W, TR = 256 / TW rows; most valid pixels per slot, then the smallest halo
-  int bestTW = 0, bestTR = 0;
-  double best = 0.0;
-  int bestHalo = 1 << 30;
-  for (int TW = 2; TW <= 64 && TW <= W; ++TW) {
-    if (W % TW) continue;
-    const int TR = 256 / TW;
-    const int halo = (TW + 2) * (TR + 2);
-    if (((halo + 7) / 8) * 8 > HALO_MAXPX) continue;
-    const int tiles = (W / TW) * ((BH + TR - 1) / TR);
-    const double eff = (double)a.M / ((double)tiles * 256.0);
-    if (eff > best + 1e-9 || (eff > best - 1e-9 && halo < bestHalo)) { best = eff; bestTW = TW; bestTR = TR; bestHalo = halo; }
-  }
-  if (best < 0.85) return false;
-  h->M = a.M; h->N = a.N; h->Kpad = a.Kpad; h->Cseg = a.Cseg; h->BH = BH; h->H = a.Ho; h->W = W;
-  h->TW = bestTW; h->TR = bestTR; h->HW2 = bestTW + 2;
-  h->nhalo = bestHalo;
-  h->ninstr = (bestHalo + 7) / 8;
-  h->tiles_x = W / bestTW;
-  h->tiles_m = h->tiles_x * ((BH + bestTR - 1) / bestTR);
-  h->nchunk = a.Cseg / 64;
-  for (int g = 0; g < h->ngroups; ++g)
-    for (int t = 0; t < h->grp[g].ntaps; ++t) {
-      HaloTap& tp = h->grp[g].tap[t];
-      const int dh = tp.bit / 3 - 1, dw = tp.bit % 3 - 1;
-      tp.toff = dh * h->HW2 + dw;
+  const int nchunk = a.Cseg / 64;
+  if (nchunk > 15) return false;
+  int ns = 0;
+  for (int g = 0; g < nsrc; ++g)
+    for (int cc = 0; cc < nchunk; ++cc) {
+      int first = ns, cnt = 0;
+      for (int i = 0; i < a.nseg; ++i) {
+        if (gseg[i] != g) continue;
+        if (ns == HALO_MAXSTEP) return false;
+        const unsigned kcol = (unsigned)(i * a.Cseg + cc * 64);
+        const unsigned toff = (unsigned)((a.seg[i].dh + 1) * (TW + 2) + a.seg[i].dw + 1);
+        h->step[ns++] = kcol | (toff << 16) | ((unsigned)g << 24) | ((unsigned)cc << 28);
+        ++cnt;
+      }
+      h->step[first] |= 1u << 26;
+      h->step[first + cnt - 1] |= 1u << 27;
     }
+  h->nsteps = ns;
+  for (int g = 0; g < nsrc; ++g) h->gptr[g] = src[g];
+  h->M = a.M; h->N = a.N; h->Kpad = a.Kpad; h->Cseg = a.Cseg; h->H = H; h->W = W;
+  h->tiles_x = W / TW; h->tiles_y = H / TR;
+  h->tiles_m = (a.M / (H * W)) * h->tiles_x * h->tiles_y;
   h->Bw = a.Bw; h->bias = a.bias;
   for (int i = 0; i < 3; ++i) h->dest[i] = a.dest[i];
   h->Nd = a.Nd; h->accumulate = a.accumulate; h->stats = a.stats;
+  *tw = TW; *tr = TR;
   return true;
 }
 
-int launch_halo(const HaloArgs& h, hipStream_t st) {
+template <int TW, int TR>
+void launch_halo_t(const HaloArgs& h, hipStream_t st) {
+  if (h.N <= 64) {
+    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 64>), dim3(xcd_pad(h.tiles_m)), dim3(512), 0, st, h);
+  } else {
+    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 128>), dim3(xcd_pad(((h.N + 127) / 128) * h.tiles_m)), dim3(512), 0,
+                       st, h);
+  }
+}
+
+int launch_halo(const HaloArgs& h, int tw, hipStream_t st) {
   if (t_dry_rows) { *t_dry_rows = h.tiles_m; return 0; }
-  const int bn = h.N <= 64 ? 64 : 128;
-  const int nN = (h.N + bn - 1) / bn;
-  dim3 grid(xcd_pad(nN * h.tiles_m));
-  if (bn == 64) hipLaunchKernelGGL((conv_halo_kernel<64, 8, 2>), grid, dim3(1024), 0, st, h);
-  else hipLaunchKernelGGL((conv_halo_kernel<128, 4, 4>), grid, dim3(1024), 0, st, h);
+  if (tw == 16) launch_halo_t<16, 16>(h, st);
+  else if (tw == 8) launch_halo_t<8, 28>(h, st);
+  else launch_halo_t<14, 14>(h, st);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1972,7 +1944,10 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     }
     // LDS-DMA kernels need shifts in [-1, 1] and 64-aligned segments (scalar address
     // generation); everything else (the 8-channel first layer) takes the register-staged tile
-    const bool glds_ok = shifts_small(a) && a.Cseg % 64 == 0;
+    // (the LDS-DMA tile kernel addresses its sources and weights with 32-bit buffer offsets)
+    const bool glds_ok = shifts_small(a) && a.Cseg % 64 == 0 &&
+                         (int64_t)(a.M / (a.Ho * a.Wo)) * a.Hi * a.Wi * a.Cseg * 2 < (1ll << 31) &&
+                         (int64_t)a.N * a.Kpad * 2 < (1ll << 31);
     if (glds_ok) {
       switch (g_conv_cfg) {
         case 3: return launch_glds<128, 64, 2, 1>(a, st);
@@ -2006,7 +1981,8 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     // N <= 64 (530 TF on the L1 3x3, equal to the register-staged tile on the small-K 1x1s).
     if (g_conv_cfg == 0) {   // 3x3 fwd / fused dgrad with M >= knob 19: 2-D halo tiles
       HaloArgs h;
-      if (halo_plan(a, &h)) return launch_halo(h, st);
+      int tw, tr;
+      if (halo_plan(a, &h, &tw, &tr)) return launch_halo(h, tw, st);
     }
     if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (!glds_ok) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
@@ -2340,6 +2316,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 12) { g_wgrad_fuse_all = value; return 0; }
   if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
   if (knob == 15) { g_conv_dbg = value; return 0; }
+  if (knob == 21) { g_wgrad_nosimple = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

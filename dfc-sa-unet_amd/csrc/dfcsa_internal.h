@@ -39,6 +39,10 @@ struct WgradArgs {
   int fuse, nsplit, layout, ntaps, Ctot, Creal, ndst;
   float* dst[3];
   unsigned* cnt;
+  // simple geometry (stride 1, input grid = output grid, shifts in [-1, 1]): the LDS-DMA kernel
+  // tracks each X slot's (row, column) incrementally, 64 pixels per stage = adv_w columns and
+  // adv_h rows (mod H)
+  int simple, adv_w, adv_h;
 };
 
 // profiling hook (prof.cpp)
@@ -62,6 +66,7 @@ extern int g_wgrad_noglds_f32small;
 extern int g_wgrad_big;
 extern int g_wgrad_wide_small;
 extern int g_wgrad_halo;
+extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);
 extern int g_fra_generic;

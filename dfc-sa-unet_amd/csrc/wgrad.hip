@@ -349,7 +349,22 @@ __device__ __attribute__((aligned(16))) uint4 g_wg_zero[64];
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void glb_void_t;
 
-template <int BI, int BJ, int WM, int WN, int NST>
+// LDS-DMA issued from inline asm (cdna_hip_programming.md, glds16_asm): the compiler does not
+// count it, so it inserts no vmcnt(0) of its own before the next fragment reads -- with the
+// builtin it cannot tell the stage being filled from the stage being read and drains every DMA
+// before the MFMAs (measured in the round-2 ISA of this kernel: one vmcnt(0) per stage).  The
+// kernel waits for its DMAs itself (counted vmcnt + barrier), and the loop issues no other
+// vector-memory operation.  lds_dst: wave-uniform LDS byte address.
+__device__ __forceinline__ void glds16_asm(const void* gsrc, const char* lds_dst) {
+  const unsigned dst = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(dst)
+               : "memory");
+}
+
+template <int BI, int BJ, int WM, int WN, int NST, bool SIMPLE = false>
 __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArgs args, int nsplit) {
   constexpr int NW = WM * WN;
   using T = bf16_t;
@@ -368,6 +383,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);   // DMA destinations: scalar (M0)
   // XCD-aware order: all column/row tiles of one pixel split (and neighbouring splits) run on
   // one XCD, so the 9 shifted taps of a 3x3 gather hit that XCD's L2 instead of HBM
   const int nJ = (args.NJ + BJ - 1) / BJ, nI = (args.NI + BI - 1) / BI;
@@ -413,6 +429,29 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     }
   }
   const void* zero = (const void*)g_wg_zero;
+  // SIMPLE geometry: the X source of slot q at pixel m is x_base[q] + m*Cseg (the shift folded in),
+  // valid while the shifted (row, column) stays inside the image; (row, column) of the slot's
+  // pixel are advanced by 64 pixels per issued stage instead of divided out every stage
+  const T* x_base[NI_X];
+  int x_dh[NI_X], x_dw[NI_X], x_oh[NI_X], x_ow[NI_X];
+  if constexpr (SIMPLE) {
+#pragma unroll
+    for (int q = 0; q < NI_X; ++q) {
+      x_base[q] = nullptr;
+      x_dh[q] = x_dw[q] = 0;
+      const int m = mbeg + x_row[q];
+      const int b = dm_div(args.dm_hw, m);
+      const int rem = m - b * args.dm_hw.d;
+      x_oh[q] = dm_div(args.dm_w, rem);
+      x_ow[q] = rem - x_oh[q] * args.dm_w.d;
+      if (x_seg[q] >= 0) {
+        const ConvSeg sg = segtab[x_seg[q]];
+        x_dh[q] = sg.dh;
+        x_dw[q] = sg.dw;
+        x_base[q] = (const T*)sg.ptr + ((sg.dh * args.Wi + sg.dw) * args.Cseg + x_ch[q]);
+      }
+    }
+  }
 
   auto issue = [&](int kt, int buf) {
     char* G = smem + buf * STAGE;
@@ -422,7 +461,23 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     for (int q = 0; q < NI_G; ++q) {
       const int m = mb + g_row[q];
       const void* src = (g_src[q] && m < mend) ? (const void*)(g_src[q] + (size_t)m * args.Cg) : zero;
-      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(G + (q * NW + wave) * 1024), 16, 0, 0);
+      glds16_asm(src, G + (q * NW + wv) * 1024);
+    }
+    if constexpr (SIMPLE) {
+#pragma unroll
+      for (int q = 0; q < NI_X; ++q) {
+        const int m = mb + x_row[q];
+        const bool ok = x_base[q] && m < mend && (unsigned)(x_oh[q] + x_dh[q]) < (unsigned)args.Hi &&
+                        (unsigned)(x_ow[q] + x_dw[q]) < (unsigned)args.Wi;
+        const void* src = ok ? (const void*)(x_base[q] + (size_t)m * args.Cseg) : zero;
+        glds16_asm(src, X + (q * NW + wv) * 1024);
+        int ow = x_ow[q] + args.adv_w, oh = x_oh[q] + args.adv_h;
+        if (ow >= args.Wi) { ow -= args.Wi; ++oh; }
+        if (oh >= args.Hi) oh -= args.Hi;
+        x_ow[q] = ow;
+        x_oh[q] = oh;
+      }
+      return;
     }
 #pragma unroll
     for (int q = 0; q < NI_X; ++q) {
@@ -438,7 +493,7 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
         if (ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi)
           src = (const void*)((const T*)sg.ptr + ((size_t)((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + x_ch[q]));
       }
-      __builtin_amdgcn_global_load_lds((glb_void_t*)src, (lds_void_t*)(X + (q * NW + wave) * 1024), 16, 0, 0);
+      glds16_asm(src, X + (q * NW + wv) * 1024);
     }
   };
 
@@ -919,6 +974,8 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4>), g1, dim3(512), 0, st, a, splits);
         else if (waves == 8 && g_wgrad_nst == 3)
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3>), g1, dim3(512), 0, st, a, splits);
+        else if (waves == 8 && a.simple)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2, true>), g1, dim3(512), 0, st, a, splits);
         else if (waves == 8)
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2>), g1, dim3(512), 0, st, a, splits);
         else
@@ -951,6 +1008,7 @@ int g_wgrad_fuse_all = 0;  // knob 12: 1 = reduce in-kernel at any split count, 
 // <= 4 splits, 1149 at <= 16), so the fused path stays selectable, tested, and off.
 int g_wgrad_fuse_max = 0;
 int g_wgrad_noglds_f32small = 0;  // knob 16: 1 = fp32 small-M wgrads take the generic tiles
+int g_wgrad_nosimple = 0;         // knob 21: 1 = the divide-per-stage X addressing (A/B of the incremental one)
 
 // output tile of the wgrad kernel a launch uses (launch_wgrad's choice)
 int g_wgrad_big = 0;        // knob 17: big wgrad tiles (wgrad_big_mode)
@@ -1047,6 +1105,10 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   a.dm_cseg = make_divmod(d->Cseg); a.dm_cg = make_divmod(d->Cg);
   a.slab = d->slab; a.mchunk = d->mchunk;
   a.nsplit = d->splits;
+  a.simple = d->stride == 1 && d->Hi == d->Ho && d->Wi == d->Wo && !g_wgrad_nosimple;
+  for (int i = 0; i < d->nseg && a.simple; ++i)
+    a.simple = d->seg_dh[i] >= -1 && d->seg_dh[i] <= 1 && d->seg_dw[i] >= -1 && d->seg_dw[i] <= 1;
+  if (a.simple) { a.adv_w = 64 % d->Wo; a.adv_h = (64 / d->Wo) % d->Ho; }
   a.layout = d->layout; a.ntaps = d->ntaps; a.Ctot = d->Ctot; a.Creal = d->Creal; a.ndst = d->ndst;
   for (int i = 0; i < 3; ++i) a.dst[i] = i < d->ndst ? d->dst[i] : nullptr;
   if (d->ndst > 0) {

@@ -38,8 +38,10 @@ extern "C" {
  * weight: [N][Kpad] of dtype, Kpad >= nseg*Cseg, multiple of 64 (bf16) / 32 (f32), zero-padded.
  * mode PLAIN: columns [d*Nd, (d+1)*Nd) go to dest[d] ([M][Nd]).  mode SHUFFLE2 (ConvTranspose
  * k2 s2): column n = (2i + j)*Nd + co goes to dest[0][b, 2oh+i, 2ow+j, co] of Hout x Wout.
- * accumulate: dest += C.  stats (optional): per 64-row M tile t, stats[t][0][n] = sum of the
- * fp32 accumulator (without bias) over valid rows, stats[t][1][n] = sum of squares.
+ * accumulate: dest += C.  stats (optional): one row per workgroup M tile t of the kernel the call
+ * picks (64..256 rows, or the tiles a persistent streaming workgroup visits), stats[t][0][n] = sum
+ * of the fp32 accumulator (without bias) over its valid rows, stats[t][1][n] = sum of squares;
+ * dfcsa_conv_stats_rows gives the number of rows the call writes.
  *
  * Slab capacities: every entry point that writes a per-workgroup partial slab (the stats above,
  * `partial`, `bias_partial`, `stats3/4`) also takes that slab's size in floats (`*_floats`), and
@@ -61,12 +63,13 @@ typedef struct {
   int Nd, accumulate;
   float* stats;
   int Hout, Wout;
-  int64_t stats_floats; /* capacity of stats in floats: >= ceil(M/64)*2*N when stats != NULL */
+  int64_t stats_floats; /* capacity of stats in floats: >= dfcsa_conv_stats_rows(d)*2*N (<= ceil(M/64)*2*N) */
 } dfcsa_conv_desc;
 int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream);
 int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile of the row-tile kernels */
-/* statistics rows the launch of *d writes (and dfcsa_bn_finalize reads as ntiles): ceil(M / 64)
- * for the row-tile kernels, one per 2-D tile when the bf16 3x3 halo-tile kernel runs the GEMM */
+/* statistics rows the launch of *d writes (and dfcsa_bn_finalize reads as ntiles): one per M tile
+ * of the row-tile kernels (ceil(M / BM), BM = 64..256), one per workgroup of the persistent 1x1
+ * streaming kernel, one per 2-D tile of the bf16 3x3 halo-tile kernel */
 int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d);
 
 /* ------------------------------------------------------------------------------------------

@@ -1,11 +1,12 @@
 """The 2-D halo-tile 3x3 implicit GEMM (conv_halo_kernel, csrc/conv_gemm.hip) against a torch
 reference of the same GEMM and against the row-tile kernels it replaces.
 
-Covers the tile shapes the host picks per width (16 x 16 at W = 224 / 112, 8 x 32 at W = 56,
-4 x 64 at W = 28, 14 x 18 at W = 14: tiles that straddle images, 252-pixel tiles with pad lanes),
-ragged last tiles, the two-source forward (the decoder's skip concat), the fused 3x3 + 1x1 data
-gradient (three sources, 11 segments), bias / statistics / three destinations / accumulate, NaN
-guards around every output, and the full-size layers of the benchmark against the row-tile kernel.
+Covers the three tile shapes (16 x 16 when 16 | W and 16 | H -- the 224^2 / 112^2 levels --, 8 x 28
+at 56^2, 14 x 14 at 28^2 / 14^2; tiles never straddle images, halo pixels outside the image are
+zero), non-square images, a shape no tile fits (the row-tile kernel runs), the two-source forward
+(the decoder's skip concat), the fused 3x3 + 1x1 data gradient (three sources, 11 segments),
+bias / statistics / three destinations / accumulate / N tails, NaN guards around every output,
+and the full-size layers of the benchmark against the row-tile kernel.
 Reference: models/unet_dfc_sa_res.py:58-59 (3x3 conv), :182-200 (cat), the conv backward.
 """
 import pytest
@@ -51,6 +52,14 @@ def run(segs, Cseg, grid, w, Kp, N, dests, Nd, bias=None, stats=None, accumulate
     return rows
 
 
+def halo_tiles(B, H, W):
+    """statistics rows of the halo kernel (one per tile), or None when no tile shape fits"""
+    for tw, tr in ((16, 16), (8, 28), (14, 14)):
+        if W % tw == 0 and H % tr == 0:
+            return B * (H // tr) * (W // tw)
+    return None
+
+
 def guarded(shape, fill=float("nan")):
     n = 1
     for s in shape:
@@ -65,7 +74,8 @@ def intact(buf, n):
 
 @pytest.mark.parametrize("B,H,W,Cs,nsrc,N", [
     (16, 14, 14, 64, 1, 128), (3, 28, 28, 64, 2, 64), (2, 56, 56, 128, 1, 256), (1, 112, 112, 64, 2, 128),
-    (1, 20, 36, 64, 1, 64), (2, 12, 32, 128, 1, 192), (1, 224, 224, 64, 1, 64)])
+    (1, 20, 36, 64, 1, 64), (2, 12, 32, 128, 1, 192), (1, 224, 224, 64, 1, 64), (2, 32, 48, 64, 1, 64),
+    (1, 28, 56, 64, 1, 192), (3, 14, 28, 128, 2, 64)])
 def test_halo_forward_vs_torch(B, H, W, Cs, nsrc, N):
     torch.manual_seed(B * 1000 + H * 10 + W + N)
     xs = [torch.randn(B, H, W, Cs, device=dev).to(bf) for _ in range(nsrc)]
@@ -80,6 +90,8 @@ def test_halo_forward_vs_torch(B, H, W, Cs, nsrc, N):
     st = torch.full((ops.ntiles_gemm(M) * 2 * N,), float("nan"), device=dev)
     rows = run(segs, Cs, (B, H, W), w, Kp, N, [y], N, bias=bias, stats=st)
     assert rows <= ops.ntiles_gemm(M)
+    if halo_tiles(B, H, W) is not None:
+        assert rows == halo_tiles(B, H, W), "the halo kernel did not run"
     assert intact(buf, y.numel()) and not torch.isnan(y).any()
     assert rel(y.reshape(M, N), ref + bias.double()) < 5e-3
     s = st[:rows * 2 * N].view(rows, 2, N).double().sum(0)
@@ -92,7 +104,8 @@ def test_halo_forward_vs_torch(B, H, W, Cs, nsrc, N):
 
 
 @pytest.mark.parametrize("B,H,W,C,Cin,nd", [(2, 28, 28, 64, 128, 2), (1, 56, 56, 128, 64, 1),
-                                            (9, 14, 14, 128, 256, 2), (1, 112, 112, 64, 128, 2)])
+                                            (9, 14, 14, 128, 256, 2), (1, 112, 112, 64, 128, 2),
+                                            (2, 32, 16, 64, 192, 3)])
 def test_halo_fused_dgrad_vs_torch(B, H, W, C, Cin, nd):
     """The block input gradient: 9 taps of dy1 (shifts 1-kh, 1-kw) + dy2 + dres (1x1) in one GEMM,
     the N = Cin columns split over nd source gradients."""

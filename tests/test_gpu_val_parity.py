@@ -12,7 +12,7 @@ Twenty SGD steps amplify rounding: the reference's own fp32 run and its float64 
 oracle in float64) drift apart by up to 1e-3 in the step loss and 3e-4 in validation Dice by step
 20 here (4e-3 / 5e-3 at lr 0.1).  Bars: validation Dice and IoU within max(1e-3, 3 x that fp32-vs-
 float64 distance) of the oracle's fp32 run; step losses and the validation loss within
-max(1e-3, 3 x the reference's fp32-vs-float64 distance of that step) relative; parameters after
+max(1e-3, 3 x the largest fp32-vs-float64 distance of the reference up to that step) relative; parameters after
 20 steps within max(1e-3, 3 x the reference's fp32-vs-float64 distance) over the whole state
 vector."""
 import os
@@ -80,8 +80,10 @@ def test_twenty_steps_then_validation_match_the_oracle(tmp_path):
           f"{va['loss']:.6f} / {vl:.6f}; last train loss {losses[-1]:.6f} / {losses_ref[-1]:.6f}")
     print("step loss rel, HIP vs oracle fp32:   ", " ".join(f"{abs(a - b) / b:.1e}" for a, b in zip(losses, losses_ref)))
     print("step loss rel, oracle fp32 vs fp64:  ", " ".join(f"{abs(a - b) / b:.1e}" for a, b in zip(losses_ref, losses64)))
+    env = 0.0   # the reference's fp32-vs-float64 drift so far (its envelope: one step's value is noisy)
     for i, (a, b, c) in enumerate(zip(losses, losses_ref, losses64)):
-        assert abs(a - b) <= max(1e-3, 3 * abs(b - c) / abs(c)) * abs(b), (i, a, b, c)
+        env = max(env, abs(b - c) / abs(c))
+        assert abs(a - b) <= max(1e-3, 3 * env) * abs(b), (i, a, b, c)
     assert abs(va["loss"] - vl) <= max(1e-3, 3 * abs(vl - vl64) / abs(vl64)) * abs(vl)
     assert vd > 0.05, "the validation Dice is trivial: nothing is compared"
     assert abs(va["dice"] - vd) <= max(1e-3, 3 * abs(vd - vd64))
