@@ -339,7 +339,9 @@ def main():
         classes = ((1, "conv_gemm (implicit-GEMM conv fwd/dgrad, LDS-DMA tiles)", "conv_gemm", "mfma"),
                    (2, "conv_wgrad (weight-gradient GEMM)", "conv_wgrad", "mfma"),
                    (3, "fra (full-resolution attention fwd/bwd, bf16 MFMA)", "fra", "mfma"),
-                   (4, "conv1x1_stream (1x1 conv GEMMs, K <= 256, HBM-streaming)", "conv1x1_stream", "hbm"))
+                   (4, "conv1x1_stream (1x1 conv GEMMs with K <= 256 and the fused block GEMMs -- gate backward "
+                       "in the dgrad epilogue, gate fusion / local-attention merge in the forward prologue; HBM-streaming)",
+                    "conv1x1_stream", "hbm"))
         for c, _, _, _ in classes:
             L.LIB.dfcsa_prof_enable(c, 1)
         for _ in range(args.steps):

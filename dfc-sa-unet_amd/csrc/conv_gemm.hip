@@ -154,8 +154,14 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t 
     int row = e / OCH, cc = e % OCH;
     int m = m0 + row, n = n0 + cc * 8;
     if (m >= M || n >= N) continue;
-    float v[8];
     const T* src = (const T*)((const char*)otile + row * OSTR + cc * 8 * sizeof(T));
+    if (sizeof(T) == 2 && !args.accumulate && args.mode == CONV_STORE_PLAIN) {
+      // the staged bf16 values are the output: a 16-B copy (no unpack / repack)
+      const int d = n / args.Nd, col = n - d * args.Nd;
+      *(uint4*)((T*)args.dest[d] + ((size_t)m * args.Nd + col)) = *(const uint4*)src;
+      continue;
+    }
+    float v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) v[q] = ElemTraits<T>::to_f(src[q]);
     T* dst;
@@ -759,8 +765,13 @@ struct HaloArgs {
   unsigned step[HALO_MAXSTEP];
 };
 
-template <int TW, int TR, int BN>
-__global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) {
+// NBUF = 2: two halo buffers (the next chunk's halo is written while the current one is read),
+// one workgroup per CU.  NBUF = 1 (BN = 64): one halo buffer, ~76 KB of LDS and <= 128 VGPRs, so
+// two workgroups share a CU and one's prologue / barrier waits overlap the other's MFMAs; the next
+// chunk's halo (already in registers) is written after the first barrier of that chunk, and a
+// second barrier publishes it.
+template <int TW, int TR, int BN, int NBUF>
+__global__ void __launch_bounds__(512, NBUF == 1 ? 2 : 1) conv_halo_kernel(const HaloArgs args) {
   using T = bf16_t;
   constexpr int WM = 4, WN = 2, NT = 512;
   constexpr int WTN = BN / WN, FM = 4, FN = WTN / 16;
@@ -771,12 +782,12 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
   constexpr int HCH = HPX * 8;                   // 16-B chunks of one halo
   constexpr int HL = (HCH + NT - 1) / NT;        // halo chunks per thread
   constexpr int OSTR = BN * 2 + 16;
-  constexpr int SMEM_MAIN = 2 * HBUF + NBS * BSLOT;
+  constexpr int SMEM_MAIN = NBUF * HBUF + NBS * BSLOT;
   constexpr int SMEM_EPI = 256 * OSTR + WM * 2 * BN * 4;
   constexpr int SMEM = SMEM_MAIN > SMEM_EPI ? SMEM_MAIN : SMEM_EPI;
   static_assert(TW * TR <= 256 && SMEM <= 160 * 1024 && FN >= 1, "halo tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
-  char* const bbuf = smem + 2 * HBUF;
+  char* const bbuf = smem + NBUF * HBUF;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave % WM, wn = wave / WM;
@@ -865,6 +876,7 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
   if (S > 1) issue_b(1);
   int hb = 0;                                    // halo buffer of the current chunk
   int hs = -8;                                   // step that issued the halo loads in flight
+  bool pending = false;                          // NBUF = 1: a loaded halo waits for the next chunk
   for (int s = 0; s < S; ++s) {
     const unsigned w = args.step[s];
     // this step's weight panel: vmcnt is in order, so the panel issued two steps ago is complete
@@ -875,6 +887,13 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     else if (s - hs <= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB + HL) : "memory");
     else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(KB) : "memory");
     lds_barrier();   // publishes this step's weight panel (and, at a chunk's first tap, its halo)
+    if constexpr (NBUF == 1) {
+      if (pending) {   // every wave is past the previous chunk's reads: overwrite, then publish
+        store_halo(0);
+        lds_barrier();
+        pending = false;
+      }
+    }
     if (s + 2 < S) issue_b(s + 2);
     const bool more = s + 1 < S;
     if (((w >> 26) & 1) && !((w >> 27) & 1 && !more)) {
@@ -902,10 +921,14 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
           acc[i][jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[jj], acc[i][jj], 0, 0, 0);
     }
     if (((w >> 27) & 1) && more) {
-      // last tap of a chunk: the next chunk's halo goes to the other buffer (read from the next
-      // step on, after its barrier; that buffer's last reader was the previous chunk)
-      hb ^= 1;
-      store_halo(hb);
+      if constexpr (NBUF == 2) {
+        // last tap of a chunk: the next chunk's halo goes to the other buffer (read from the next
+        // step on, after its barrier; that buffer's last reader was the previous chunk)
+        hb ^= 1;
+        store_halo(hb);
+      } else {
+        pending = true;
+      }
       hs = -8;
     }
   }
@@ -968,10 +991,14 @@ __global__ void __launch_bounds__(512, 1) conv_halo_kernel(const HaloArgs args) 
     const int n = n0 + ck * 8;
     if (n >= args.N) continue;
     const size_t mg = (size_t)(img * H + y0 + r) * W + x0 + c;
-    float v[8];
-    load8<T>((const T*)((const char*)otile + row * OSTR + ck * 16), v);
     const int d = n / args.Nd, col = n - d * args.Nd;
     T* dst = (T*)args.dest[d] + (mg * args.Nd + col);
+    if (!args.accumulate) {
+      *(uint4*)dst = *(const uint4*)((const char*)otile + row * OSTR + ck * 16);
+      continue;
+    }
+    float v[8];
+    load8<T>((const T*)((const char*)otile + row * OSTR + ck * 16), v);
     if (args.accumulate) {
       float o[8];
       load8<T>(dst, o);
@@ -1045,12 +1072,22 @@ bool halo_plan(const ConvGemmArgs& a, HaloArgs* h, int* tw, int* tr) {
   return true;
 }
 
+int g_halo_variant = 0;   // knob 22: 0 = BN 64 single-buffer for N <= 64, BN 128 double-buffer above; 1 = BN 64 always;
+                          // 2 = the double-buffered one-workgroup-per-CU kernel always
+
 template <int TW, int TR>
 void launch_halo_t(const HaloArgs& h, hipStream_t st) {
-  if (h.N <= 64) {
-    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 64>), dim3(xcd_pad(h.tiles_m)), dim3(512), 0, st, h);
+  if (g_halo_variant == 2) {
+    if (h.N <= 64)
+      hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 64, 2>), dim3(xcd_pad(h.tiles_m)), dim3(512), 0, st, h);
+    else
+      hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 128, 2>), dim3(xcd_pad(((h.N + 127) / 128) * h.tiles_m)), dim3(512),
+                         0, st, h);
+  } else if (h.N <= 64 || g_halo_variant == 1) {
+    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 64, 1>), dim3(xcd_pad(((h.N + 63) / 64) * h.tiles_m)), dim3(512), 0,
+                       st, h);
   } else {
-    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 128>), dim3(xcd_pad(((h.N + 127) / 128) * h.tiles_m)), dim3(512), 0,
+    hipLaunchKernelGGL((conv_halo_kernel<TW, TR, 128, 2>), dim3(xcd_pad(((h.N + 127) / 128) * h.tiles_m)), dim3(512), 0,
                        st, h);
   }
 }
@@ -2317,6 +2354,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 13) { g_wgrad_fuse_max = value >= 0 ? (value <= 16 ? value : 16) : 0; return 0; }
   if (knob == 15) { g_conv_dbg = value; return 0; }
   if (knob == 21) { g_wgrad_nosimple = value; return 0; }
+  if (knob == 22) { g_halo_variant = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -61,7 +61,11 @@ def _per_dispatch(db, counter):
 
 CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel"),
            "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
-           "conv1x1_stream": ("conv1x1_stream_kernel",),
+           # bench.py's class 4 (DFCSA_PROF_CONV_STREAM) times the streaming 1x1 GEMMs AND the fused
+           # block GEMMs (dfcsa_dgrad_gate*, dfcsa_gate_fusion_fwd, dfcsa_local_attn_gate_fwd): the
+           # same union here, so roofline.traffic matches the timed launches; the fused ones alone
+           # as fused_block_gemm
+           "conv1x1_stream": ("conv1x1_stream_kernel", "dgrad_gate_kernel", "gate_fusion_fwd_kernel"),
            "fused_block_gemm": ("dgrad_gate_kernel", "gate_fusion_fwd_kernel")}
 
 
@@ -180,10 +184,15 @@ def sq(db, out):
             r["mfma_busy_frac"] = d["SQ_VALU_MFMA_BUSY_CYCLES"] / (d["GRBM_GUI_ACTIVE"] / 8.0 * 1024.0)
         if d.get("SQ_LDS_IDX_ACTIVE"):
             r["lds_bank_conflict_frac"] = d.get("SQ_LDS_BANK_CONFLICT", 0.0) / d["SQ_LDS_IDX_ACTIVE"]
+        if d.get("SQ_INSTS_MFMA") and "SQ_INSTS_VALU" in d:
+            r["valu_per_mfma"] = d["SQ_INSTS_VALU"] / d["SQ_INSTS_MFMA"]   # SQ_INSTS_VALU counts the MFMAs too
+        if d.get("SQ_WAVE_CYCLES") and "SQ_WAIT_ANY" in d:
+            r["wait_any_frac"] = d["SQ_WAIT_ANY"] / d["SQ_WAVE_CYCLES"]
         res[g] = r
     res["_definition"] = ("mfma_busy_frac = SQ_VALU_MFMA_BUSY_CYCLES / (GRBM_GUI_ACTIVE / 8 XCDs * 1024 SIMDs), "
                           "summed over the group's dispatches; lds_bank_conflict_frac = SQ_LDS_BANK_CONFLICT / "
-                          "SQ_LDS_IDX_ACTIVE")
+                          "SQ_LDS_IDX_ACTIVE; valu_per_mfma = SQ_INSTS_VALU / SQ_INSTS_MFMA (VALU includes the "
+                          "MFMAs); wait_any_frac = SQ_WAIT_ANY / SQ_WAVE_CYCLES")
     json.dump(res, open(out, "w"), indent=1)
     for g, r in res.items():
         if g[0] != "_":
