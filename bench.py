@@ -114,6 +114,8 @@ def cpu_baseline(batch=16, timed_steps=2):
     el = time.perf_counter() - t0
     return {"value": round(timed_steps * batch / el, 4), "unit": "images/s", "cores": threads, "kind": "port",
             "cpu_model": cpu_model_name(), "affinity_cpus": aff,
+            "core_share": (f"{threads}-core share (OMP_NUM_THREADS={omp} of {aff} affinity CPUs: the box's CPU "
+                           f"share for one GPU's job)" if omp > 0 and omp < aff else f"all {aff} affinity CPUs"),
             "sample": f"{timed_steps} timed train steps (after 1 warm-up) of B={batch} 3x224x224 images, P=4, "
                       f"features 64..512: oracle/dfcsa_oracle.py fp32 eager PyTorch on {threads} host threads"}
 

@@ -2119,6 +2119,9 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   const double sbytes = 2.0 * ((double)a.M * a.Kpad + (double)a.N * a.Kpad + (double)a.M * a.N * (a.accumulate ? 2 : 1));
   ProfScope prof(streamed ? DFCSA_PROF_CONV_STREAM : DFCSA_PROF_CONV_GEMM, st,
                  streamed ? sbytes : 2.0 * a.M * a.N * a.K);
+  if (dfcsa_shapelog())
+    fprintf(stderr, "SHAPE conv M=%d N=%d K=%d Kpad=%d nseg=%d Cseg=%d Ho=%d Wo=%d acc=%d dt=%d\n", a.M, a.N, a.K,
+            a.Kpad, a.nseg, a.Cseg, a.Ho, a.Wo, a.accumulate, d->dtype);
   return d->dtype == DFCSA_DT_BF16 ? launch_t<bf16_t>(a, st) : launch_t<float>(a, st);
 }
 
@@ -2355,6 +2358,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 15) { g_conv_dbg = value; return 0; }
   if (knob == 21) { g_wgrad_nosimple = value; return 0; }
   if (knob == 22) { g_halo_variant = value; return 0; }
+  if (knob == 23) { g_wgrad_reduce_old = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -66,9 +66,14 @@ extern int g_wgrad_noglds_f32small;
 extern int g_wgrad_big;
 extern int g_wgrad_wide_small;
 extern int g_wgrad_halo;
+extern int g_wgrad_reduce_old;
 extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);
 extern int g_fra_generic;
 extern int g_fra_occ;
 extern int g_ew_tile_elems;
+
+// DFCSA_SHAPELOG=1: one stderr line per conv / wgrad launch (shape analysis against a kernel
+// trace, tools/shape_trace.py); off by default
+bool dfcsa_shapelog();

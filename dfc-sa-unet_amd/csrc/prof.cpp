@@ -3,6 +3,7 @@
 // region without a separate profiler run.
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -74,3 +75,8 @@ extern "C" int dfcsa_prof_read(int c, double* total_ms, int64_t* launches, doubl
 }
 
 extern "C" const char* dfcsa_version(void) { return "libdfcsa 0.1 gfx950"; }
+
+bool dfcsa_shapelog() {
+  static const bool on = std::getenv("DFCSA_SHAPELOG") != nullptr;
+  return on;
+}

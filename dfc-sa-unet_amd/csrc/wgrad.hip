@@ -18,6 +18,7 @@
 //
 // Replaces the weight half of ATen convolution_backward for the convolutions at reference
 // models/unet_dfc_sa_res.py:58, 66, 74, 81, 88 and ConvTranspose2d at :147-156.
+#include <cstdio>
 #include <cstring>
 
 #include "common.h"
@@ -845,10 +846,80 @@ __global__ void __launch_bounds__(64 * SUB) wgrad_reduce_kernel(const float* __r
   reduce_dst_add(e, NI, NJ, layout, ntaps, Ctot, Creal, ndst, d0, d1, d2, s);
 }
 
+// Low split counts (the deep layers: 3-16 splits of a [NI][taps x Ctot] slab of up to 19 MB per
+// split): one workgroup per (row i, 64-channel chunk), its 4 waves take the taps round-robin, each
+// lane issues all the split loads of its element at once (<= 16 in flight) and sums them in split
+// order; the [64][T] tile is transposed through LDS so the read-modify-write of the weight
+// gradient walks 64*T consecutive floats of the reference layout ([Cout][Cin][kh][kw]: taps
+// fastest; ConvTranspose2d [Cin][Cout][2][2]) instead of 4-B scatters at a T-float stride.
+// T == 1: the waves take four consecutive 64-channel chunks.
+template <int MAXS>
+__global__ void __launch_bounds__(256) wgrad_reduce_tap_kernel(const float* __restrict__ slab, int splits, int NI,
+                                                               int NJ, int layout, int T, int Ctot, int Creal,
+                                                               int ndst, float* d0, float* d1, float* d2) {
+  __shared__ float tile[4 * 64 * 9 + 4];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i = blockIdx.y;
+  const int64_t total = (int64_t)NI * NJ;
+  const int cw = T == 1 ? 256 : 64;                  // channels per workgroup
+  const int c0 = blockIdx.x * cw;
+  // taps handled by this wave: T > 1 -> t = wave, wave + 4, ...; T == 1 -> t = 0, channel block wave
+  const int tstep = T == 1 ? T : 4;
+  const int cl = T == 1 ? wave * 64 + lane : lane;   // channel within the chunk
+  for (int t = T == 1 ? 0 : wave; t < T; t += tstep) {
+    const int c = c0 + cl;
+    float v[MAXS];
+    const bool ok = c < Ctot;
+    const float* p = slab + (int64_t)i * NJ + (int64_t)t * Ctot + c;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s) v[s] = (ok && s < splits) ? p[(int64_t)s * total] : 0.f;
+    float acc = 0.f;
+#pragma unroll
+    for (int s = 0; s < MAXS; ++s)
+      if (s < splits) acc += v[s];
+    tile[cl * T + t] = acc;
+  }
+  __syncthreads();
+  // destination: rows of the reference layout, channels c0 .. c0 + cw (clipped to Creal), T
+  // consecutive floats per channel
+  float* dst;
+  int r, creal;
+  if (layout == 0) {
+    const int rows = NI / ndst, d = i / rows;
+    r = i - d * rows;
+    dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
+    creal = Creal;
+  } else {
+    r = i;
+    dst = d0;
+    creal = Ctot;
+  }
+  const int nc = min(cw, creal - c0);
+  if (nc <= 0) return;
+  float* base = dst + ((int64_t)r * creal + c0) * T;
+  for (int e = threadIdx.x; e < nc * T; e += 256) base[e] += tile[e];
+}
+
 int launch_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps, int Ctot, int Creal, int ndst,
                   float* d0, float* d1, float* d2, hipStream_t st) {
   const int64_t total = (int64_t)NI * NJ;
   const int blocks = (int)((total + 63) / 64);
+  const int T = layout == 0 ? ntaps : 4;
+  if (!g_wgrad_reduce_old && layout != 2 && splits <= 16 && T <= 9 && (int64_t)T * Ctot <= NJ && NI <= 65535) {
+    const int cw = T == 1 ? 256 : 64;
+    dim3 grid((Ctot + cw - 1) / cw, NI);
+    if (splits <= 4)
+      hipLaunchKernelGGL(wgrad_reduce_tap_kernel<4>, grid, dim3(256), 0, st, slab, splits, NI, NJ, layout, T, Ctot,
+                         Creal, ndst, d0, d1, d2);
+    else if (splits <= 8)
+      hipLaunchKernelGGL(wgrad_reduce_tap_kernel<8>, grid, dim3(256), 0, st, slab, splits, NI, NJ, layout, T, Ctot,
+                         Creal, ndst, d0, d1, d2);
+    else
+      hipLaunchKernelGGL(wgrad_reduce_tap_kernel<16>, grid, dim3(256), 0, st, slab, splits, NI, NJ, layout, T, Ctot,
+                         Creal, ndst, d0, d1, d2);
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
   // >= ~16 splits per thread keeps the loads in flight; more sub-ranges when the blocks are few
   if (splits >= 128 && blocks < 1024)
     hipLaunchKernelGGL(wgrad_reduce_kernel<16>, dim3(blocks), dim3(1024), 0, st, slab, splits, NI, NJ, layout, ntaps,
@@ -995,6 +1066,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_wgrad_reduce_old = 0;  // knob 23: 1 = the element-order reduction for every split count
 int g_wgrad_halo = 0;      // knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel (off: slower so far)
 int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6; 0 = automatic)
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
@@ -1138,6 +1210,9 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   double flops = 2.0 * a.M * a.NI * a.NJ;
   ProfScope prof(DFCSA_PROF_WGRAD, st, flops);   // the class covers the reduction launch too
+  if (dfcsa_shapelog())
+    fprintf(stderr, "SHAPE wgrad M=%d NI=%d NJ=%d nseg=%d Cseg=%d splits=%d mchunk=%d fuse=%d dt=%d\n", a.M, a.NI,
+            a.NJ, a.nseg, a.Cseg, d->splits, d->mchunk, a.fuse, d->dtype);
   {
     WHaloArgs h;
     int bi;

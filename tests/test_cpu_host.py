@@ -374,6 +374,73 @@ def test_model_stats_flops_match_flop_counter(features, pool, hw, full_res):
     assert 0 < S.get_model_size(m) < 10
 
 
+ZOO_NAMES = ["UNet_Baseline", "UNet_AttentionOnly", "UNet_AdditionFusion", "UNet_ConcatFusion",
+             "UNet_EncoderOnlyDFC", "UNet_DecoderOnlyDFC", "UNet_BothStandardConv"]
+
+
+@pytest.mark.parametrize("name", ZOO_NAMES)
+def test_model_stats_flops_zoo(name):
+    """forward_flops of every ablation-zoo model (the reference counts each with ptflops,
+    model_stats.py:164-165) against torch.utils.flop_counter on the oracle's restatement of the
+    same graph with that model's blocks."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from models.model_factory import ModelFactory
+    from oracle import dfcsa_oracle as O
+    from utils import model_stats as S
+    cfg = {"model": {"name": name, "features": [8, 16, 32, 64], "pool_size": 4}, "training": {}}
+    m = ModelFactory.get_model(cfg)
+    sd = {k: v.detach().float() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 3, 32, 32)
+    with FlopCounterMode(display=False) as fc:
+        with torch.no_grad():
+            O.unet_dfc_sa_res(x, sd, pool_size=4, training=True, bufs=None, zoo=name)
+    ref = fc.get_total_flops()
+    ours = S.forward_flops(m, (2, 3, 32, 32))
+    assert abs(ours - ref) <= 1e-9 * ref, (ours, ref)
+
+
+@pytest.mark.parametrize("hw", [64, 37])
+def test_model_stats_flops_unet(hw):
+    """forward_flops of UNet (config 1; odd sizes exercise the ceil-mode pooling and the crop)
+    against torch.utils.flop_counter on the oracle's UNet."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from models.model_factory import ModelFactory
+    from oracle import dfcsa_oracle as O
+    from utils import model_stats as S
+    m = ModelFactory.get_model({"model": {"name": "UNet"}, "training": {}})
+    sd = {k: v.detach().float() for k, v in m.state_dict().items()}
+    x = torch.randn(1, 3, hw, hw)
+    with FlopCounterMode(display=False) as fc:
+        with torch.no_grad():
+            O.unet(x, sd, training=True, bufs=None)
+    ref = fc.get_total_flops()
+    ours = S.forward_flops(m, (1, 3, hw, hw))
+    assert abs(ours - ref) <= 1e-9 * ref, (ours, ref)
+
+
+def test_model_stats_flops_transunet():
+    """forward_flops of TransUNet on the reduced R50-ViT config of the fixtures (32x32 input, two
+    ViT layers) against torch.utils.flop_counter on the oracle's TransUNet."""
+    from torch.utils.flop_counter import FlopCounterMode
+
+    from models.transformer_unet import TransUNet
+    from oracle import dfcsa_oracle as O
+    from test_oracle_golden import transunet_small_config
+    from utils import model_stats as S
+    c = transunet_small_config()
+    m = TransUNet(c, img_size=32, num_classes=1)
+    sd = {k: v.detach().float() for k, v in m.state_dict().items()}
+    x = torch.randn(2, 3, 32, 32)
+    with FlopCounterMode(display=False) as fc:
+        with torch.no_grad():
+            O.transunet(x, sd, heads=c.transformer.num_heads, training=True, bufs=None)
+    ref = fc.get_total_flops()
+    ours = S.forward_flops(m, (2, 3, 32, 32))
+    assert abs(ours - ref) <= 1e-9 * ref, (ours, ref)
+
+
 def test_model_stats_headline_flops_pinned():
     """The config-2 model at 224^2, P=4: 67.29 GFLOP per image forward (measured there
     with torch.utils.flop_counter on the reference) -- fwd+bwd 201.66 = 3x forward minus the input

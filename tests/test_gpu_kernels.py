@@ -758,3 +758,42 @@ def test_block_out_pool_fused_equals_separate(dtype, B, H, W, C, skip):
     assert torch.equal(out1, out0) and torch.equal(p1, p0)
     assert torch.equal(d1, d0) and torch.equal(dr1, dr0)
     assert rel(q1.view(ntp, 3, C).double().sum(0), q0.view(nte, 3, C).double().sum(0)) < 1e-5
+
+
+def _reduce_ref(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst):
+    """torch restatement of dfcsa_wgrad_reduce: sum the split slabs, then map the [NI][NJ] GEMM
+    element (i, j) into the reference weight layouts (wgrad.hip reduce_dst_add)."""
+    s = slab[:splits * NI * NJ].view(splits, NI, NJ).double().sum(0)
+    if layout == 0:
+        rows = NI // ndst
+        g = s[:, :ntaps * Ctot].view(NI, ntaps, Ctot)[:, :, :Creal].permute(0, 2, 1)   # [NI][Creal][taps]
+        return [g[d * rows:(d + 1) * rows].reshape(-1) for d in range(ndst)]
+    g = s.view(NI, 4, Ctot).permute(0, 2, 1)                                        # ConvT [Cin][Cout][4]
+    return [g.reshape(-1)]
+
+
+@pytest.mark.parametrize("layout,ntaps,NI,Ctot,Creal,ndst,extra", [
+    (0, 9, 64, 128, 128, 1, 0), (0, 9, 96, 72, 67, 2, 8), (0, 1, 48, 512, 512, 3, 0), (0, 9, 16, 8, 3, 1, 0),
+    (1, 4, 40, 96, 96, 1, 0)])
+@pytest.mark.parametrize("splits", [1, 3, 7, 16, 17, 40])
+def test_wgrad_reduce_layouts(layout, ntaps, NI, Ctot, Creal, ndst, extra, splits):
+    """The split-K reduction into the reference weight layouts (Conv2d [Cout][Cin][kh][kw] with K
+    padding columns and channel padding, three stacked destinations, ConvTranspose2d [Cin][Cout][2][2]):
+    the tap-transposing kernel (<= 16 splits) and the element-order kernel (knob 23 / > 16 splits)
+    against a float64 torch reduction; each destination starts non-zero (the reduction adds)."""
+    import dfcsa
+    torch.manual_seed(splits + 31 * NI)
+    T = ntaps if layout == 0 else 4
+    NJ = T * Ctot + extra
+    slab = torch.randn(splits * NI * NJ, device="cuda")
+    ref = _reduce_ref(slab.cpu(), splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst)
+    for old in (0, 1):
+        dfcsa.set_tuning(23, old)
+        try:
+            dsts = [torch.full((r.numel(),), 0.5, device="cuda") for r in ref]
+            ops.wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts)
+            torch.cuda.synchronize()
+        finally:
+            dfcsa.set_tuning(23, 0)
+        for d, r in zip(dsts, ref):
+            assert (d.double().cpu() - 0.5 - r).abs().max().item() < 1e-5 * max(1.0, splits ** 0.5)
