@@ -357,7 +357,7 @@ __device__ __forceinline__ unsigned sel_oob(unsigned mask, int bit, unsigned vof
   return (voff & m) | (kBufOOB & ~m);
 }
 
-template <int BM, int BN, int WM, int WN, int NST>
+template <int BM, int BN, int WM, int WN, int NST, bool SPLIT = false>
 __global__ void __launch_bounds__(WM* WN * 64)
 conv_gemm_glds_kernel(const ConvGemmArgs args) {
   using T = bf16_t;
@@ -375,8 +375,12 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int nN = (args.N + BN - 1) / BN;
-  const int L = xcd_remap(blockIdx.x, nN * ((args.M + BM - 1) / BM));
-  if (L < 0) return;
+  const int ntiles = nN * ((args.M + BM - 1) / BM);
+  const int L0 = xcd_remap(blockIdx.x, SPLIT ? ntiles * args.ksplit : ntiles);
+  if (L0 < 0) return;
+  // split-K: consecutive workgroups take the splits of one tile (the same XCD's L2 holds its A rows)
+  const int split = SPLIT ? L0 % args.ksplit : 0;
+  const int L = SPLIT ? L0 / args.ksplit : L0;
   const int n_tile = L % nN, m_tile = L / nN;  // the N tiles of one M tile share an XCD
   const int m0 = m_tile * BM, n0 = n_tile * BN;
   const int M = args.M, N = args.N;
@@ -448,10 +452,12 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
 
   // NST-deep ring: stages kt+1 .. kt+NST-2 stay in flight while stage kt is multiplied; the
   // only vector-memory ops in the loop are the DMAs, so a counted vmcnt isolates stage kt.
-  const int nk = args.Kpad / 64;
+  // (split-K: this workgroup's stages kb .. kb + nk - 1 of the K range; ring slots by local index)
+  const int kb = SPLIT ? split * args.kper : 0;
+  const int nk = SPLIT ? min(args.kper, args.Kpad / 64 - kb) : args.Kpad / 64;
 #pragma unroll
   for (int s = 0; s < NST - 1; ++s)
-    if (s < nk) issue(s, s);
+    if (s < nk) issue(kb + s, s);
   for (int kt = 0; kt < nk; ++kt) {
     const int after = min(NST - 2, nk - 1 - kt);
     if constexpr (NST >= 4) {
@@ -465,7 +471,7 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     lds_barrier();   // the DMA ring stays in flight (a __syncthreads fence would drain it)
-    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    if (kt + NST - 1 < nk) issue(kb + kt + NST - 1, (kt + NST - 1) % NST);
     const char* A = smem + (kt % NST) * STAGE;
     const char* B = A + BM * 128;
 #pragma unroll
@@ -481,8 +487,225 @@ conv_gemm_glds_kernel(const ConvGemmArgs args) {
         for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
     }
   }
+  if constexpr (SPLIT) {
+    // partial tile in the accumulator's own layout: [tile][split][wave][fragment][lane][4]
+    float* out = args.kwork + (((size_t)L * args.ksplit + split) * NW + wave) * (FM * FN * 256) + lane * 4;
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) *(f32x4_t*)(out + (i * FN + j) * 256) = acc[i][j];
+    return;
+  }
   __syncthreads();
   conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wm, wn);
+}
+
+// split-K epilogue launch: one workgroup per output tile sums the tile's ksplit partials in split
+// order (each lane its own accumulator fragments: 16-B loads, coalesced per wave) and runs the
+// tile kernel's epilogue (BN statistics row, bias, bf16 store) on the sum
+template <int BM, int BN, int WM, int WN>
+__global__ void __launch_bounds__(WM* WN * 64) conv_splitk_epi_kernel(const ConvGemmArgs args) {
+  using T = bf16_t;
+  constexpr int NW = WM * WN;
+  constexpr int FM = BM / WM / 16, FN = BN / WN / 16;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  __shared__ __attribute__((aligned(16))) char smem[BM * OSTR > 2 * WM * BN * 4 ? BM * OSTR : 2 * WM * BN * 4];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nN = (args.N + BN - 1) / BN;
+  const int L = xcd_remap(blockIdx.x, nN * ((args.M + BM - 1) / BM));
+  if (L < 0) return;
+  const int n_tile = L % nN, m_tile = L / nN;
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+  const float* base = args.kwork + ((size_t)L * args.ksplit * NW + wave) * (FM * FN * 256) + lane * 4;
+  for (int s = 0; s < args.ksplit; ++s) {
+    const float* p = base + (size_t)s * NW * (FM * FN * 256);
+    f32x4_t v[FM][FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) v[i][j] = *(const f32x4_t*)(p + (i * FN + j) * 256);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) acc[i][j] += v[i][j];
+  }
+  conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m_tile * BM, n_tile * BN, m_tile, tid, lane, wm, wn);
+}
+
+// --------------------------------------------------------------------------------------------
+// Same tile kernel with 32-deep K slots in a deeper ring (NST slots of (BM + BN) x 64 B): at
+// 128x128 four slots take the LDS of two 64-deep stages, so two workgroups still share a CU, but
+// each slot's DMA is issued NST - 1 slots (not one stage) ahead of its use -- the round-3
+// counters put the 64-deep kernel's waves 52 % in waits with one stage of MFMAs (~210 ns) to
+// cover an L2 fetch.  Slot image: 64-B rows (4 chunks of 16 B), 16 rows per 1-KB DMA; physical
+// chunk = logical ^ f(row) with f = {0, 2, 3, 1}[(row >> 2) & 3], which makes the fragment
+// reads (lane -> row lane & 15, logical chunk lane >> 4) conflict-free in every ds_read_b128
+// lane group; the DMA applies it on the source side as the 64-deep kernel does.
+// --------------------------------------------------------------------------------------------
+__device__ __forceinline__ int swz32(int r) { return (0x78 >> (2 * ((r >> 2) & 3))) & 3; }
+
+template <int BM, int BN, int WM, int WN, int NST>
+__global__ void __launch_bounds__(WM* WN * 64)
+conv_gemm_glds32_kernel(const ConvGemmArgs args) {
+  using T = bf16_t;
+  constexpr int NW = WM * WN, NT = NW * 64;
+  constexpr int A_IN = BM / (16 * NW), B_IN = BN / (16 * NW);
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int FM = WTM / 16, FN = WTN / 16;
+  constexpr int STAGE = (BM + BN) * 64;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  constexpr int SMEM = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
+  constexpr int OPS = A_IN + B_IN;
+  static_assert(A_IN >= 1 && B_IN >= 1 && NST >= 3 && NST <= 6, "glds32 tiling");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int nN = (args.N + BN - 1) / BN;
+  const int L = xcd_remap(blockIdx.x, nN * ((args.M + BM - 1) / BM));
+  if (L < 0) return;
+  const int n_tile = L % nN, m_tile = L / nN;
+  const int m0 = m_tile * BM, n0 = n_tile * BN;
+  const int M = args.M, N = args.N;
+  // DMA: lane -> row (lane >> 2) of a 16-row block, physical chunk lane & 3
+  const int rsub = lane >> 2;
+  const int cchunk = (lane & 3) ^ swz32(rsub);
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int lane_ch = cchunk * 8;
+  unsigned a_off[A_IN], a_tap[A_IN];
+#pragma unroll
+  for (int i = 0; i < A_IN; ++i) {
+    const int m = m0 + (i * NW + wave) * 16 + rsub;
+    a_off[i] = 0;
+    a_tap[i] = 0;
+    if (m < M) {
+      const int b = dm_div(args.dm_hw, m);
+      const int rem = m - b * args.dm_hw.d;
+      const int oh = dm_div(args.dm_w, rem);
+      const int ow = rem - oh * args.dm_w.d;
+      const int ih = oh * args.stride, iw = ow * args.stride;
+      a_off[i] = 2u * (unsigned)(((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch);
+      unsigned t = 0;
+#pragma unroll
+      for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+        for (int dw = -1; dw <= 1; ++dw)
+          t |= (unsigned)(ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+      a_tap[i] = t;
+    }
+  }
+  unsigned b_off[B_IN];
+#pragma unroll
+  for (int i = 0; i < B_IN; ++i) {
+    const int n = n0 + (i * NW + wave) * 16 + rsub;
+    b_off[i] = n < N ? 2u * (unsigned)(n * args.Kpad + lane_ch) : kBufOOB;
+  }
+  const rsrc_t rb = buf_rsrc(args.Bw);
+
+  auto issue = [&](int kt, int buf) {
+    char* A = smem + buf * STAGE;
+    char* B = A + BM * 64;
+    const int k0 = kt * 32;
+    const int seg = dm_div(args.dm_cseg, k0);
+    const int ch0 = k0 - seg * args.Cseg;
+    const ConvSeg sg = args.seg[seg];
+    const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
+    const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
+    const rsrc_t ra = buf_rsrc((const T*)sg.ptr + delta);
+#pragma unroll
+    for (int i = 0; i < A_IN; ++i) blds16(ra, sel_oob(a_tap[i], tb, a_off[i]), 0, A + (i * NW + wv) * 1024);
+#pragma unroll
+    for (int i = 0; i < B_IN; ++i) blds16(rb, b_off[i], (unsigned)kt * 64u, B + (i * NW + wv) * 1024);
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  // fragment read offsets (bytes within a slot image): row (lane & 15) + 16 i, logical chunk lane >> 4
+  const int frow = lane & 15;
+  const int fch = ((lane >> 4) ^ swz32(frow)) * 16;
+  const int nk = args.Kpad / 32;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(NST - 2, nk - 1 - kt);   // slots still allowed in flight
+    switch (after) {
+      case 4: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(4 * OPS) : "memory"); break;
+      case 3: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * OPS) : "memory"); break;
+      case 2: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory"); break;
+      case 1: asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory"); break;
+      default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+    }
+    lds_barrier();
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* A = smem + (kt % NST) * STAGE;
+    const char* B = A + BM * 64;
+    Frag<T> fa[FM], fb[FN];
+#pragma unroll
+    for (int i = 0; i < FM; ++i) fa[i].v = *(const bf16x8_t*)(A + (wm * WTM + i * 16 + frow) * 64 + fch);
+#pragma unroll
+    for (int j = 0; j < FN; ++j) fb[j].v = *(const bf16x8_t*)(B + (wn * WTN + j * 16 + frow) * 64 + fch);
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) mma(acc[i][j], fa[i], fb[j]);
+  }
+  __syncthreads();
+  conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wm, wn);
+}
+
+template <int BM, int BN, int WM, int WN, int NST>
+int launch_glds32(const ConvGemmArgs& a, hipStream_t st) {
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
+  dim3 grid(xcd_pad(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM)));
+  hipLaunchKernelGGL((conv_gemm_glds32_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+thread_local int64_t* t_dry_work = nullptr;   // dfcsa_conv_work_floats: the split-K workspace
+
+// split-K plan of a 128x128 tile launch: ksplit, kper (64-deep stages per split); 1 = no split.
+// Few tiles (< 256: the 14^2 / 28^2 layers and TransUNet's ViT rows) with a long K (>= 32 stages)
+// get ~600 workgroups of >= 12 stages each.
+int g_splitk = 1;   // knob 25: 0 = never split
+void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
+  *ksplit = 1;
+  *kper = a.Kpad / 64;
+  const int tiles = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const int nk = a.Kpad / 64;
+  if (!g_splitk || tiles >= 256 || nk < 32) return;
+  int s = (600 + tiles - 1) / tiles;
+  s = std::min(s, nk / 12);
+  if (s < 2) return;
+  int per = (nk + s - 1) / s;
+  s = (nk + per - 1) / per;
+  *ksplit = s;
+  *kper = per;
+}
+
+int launch_splitk(ConvGemmArgs a, int ksplit, int kper, hipStream_t st) {
+  const int tiles = ((a.N + 127) / 128) * ((a.M + 127) / 128);
+  const int64_t need = (int64_t)tiles * ksplit * 128 * 128;
+  if (t_dry_rows) { *t_dry_rows = (a.M + 127) / 128; if (t_dry_work) *t_dry_work = need; return 0; }
+  if (!a.kwork || a.kwork_floats < need) return DFCSA_EINVAL;
+  a.ksplit = ksplit;
+  a.kper = kper;
+  hipLaunchKernelGGL((conv_gemm_glds_kernel<128, 128, 4, 2, 2, true>), dim3(xcd_pad(tiles * ksplit)), dim3(512), 0,
+                     st, a);
+  DFCSA_CHECK_LAUNCH();
+  hipLaunchKernelGGL((conv_splitk_epi_kernel<128, 128, 4, 2>), dim3(xcd_pad(tiles)), dim3(512), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
@@ -2009,6 +2232,13 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
         case 23: if (a.N % 256 == 0) return launch_pp<2, false, true>(a, st); break;
         case 24: if (a.N % 256 == 0) return launch_pp<1, false, false>(a, st); break;
         case 25: if (a.N % 256 == 0) return launch_pp<2, true, true>(a, st); break;
+        case 29: { int ks, kp; const int g = g_splitk; g_splitk = 1; splitk_plan(a, &ks, &kp); g_splitk = g;
+                   if (ks > 1 && (a.kwork || t_dry_work)) return launch_splitk(a, ks, kp, st); break; }
+        case 30: return launch_glds32<128, 128, 4, 2, 4>(a, st);
+        case 31: return launch_glds32<128, 128, 2, 2, 4>(a, st);
+        case 32: return launch_glds32<128, 128, 4, 2, 5>(a, st);
+        case 34: return launch_glds32<128, 64, 4, 1, 4>(a, st);
+        case 35: return launch_glds32<128, 128, 4, 2, 3>(a, st);
         default: break;
       }
     }
@@ -2023,6 +2253,13 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
     }
     if (g_conv_cfg != 7 && try_stream(a, st) == 0) return 0;
     if (!glds_ok) return a.N <= 64 ? launch_cfg<T, 128, 64, 4, 1>(a, st) : launch_cfg<T, 128, 128, 2, 2>(a, st);
+    // few 128x128 tiles and a long K: split the K range (fixed-order reduction in the epilogue
+    // launch; measured against the 64x64 / 128x64 tiles in profiles/r03b_splitk.jsonl)
+    if (a.N > 64 && (a.kwork || t_dry_work)) {
+      int ks, kp;
+      splitk_plan(a, &ks, &kp);
+      if (ks > 1) return launch_splitk(a, ks, kp, st);
+    }
     // N <= 64 with many rows: 256x64 / 8 waves (wave tile 32x64, twice the rows per B panel);
     // fewer than one workgroup of 128x128 per CU (the 14^2 level, 28^2 with N <= 256): 128x64 doubles the
     // workgroup count (gemm_bench: bottleneck dgrad 123 -> 108 us, bottleneck fwd 59 -> 52 us).
@@ -2087,6 +2324,8 @@ int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   a.accumulate = d->accumulate; a.stats = d->stats;
   a.Hout = d->Hout; a.Wout = d->Wout;
   a.dbg = g_conv_dbg;
+  a.kwork = d->work;
+  a.kwork_floats = d->work ? d->work_floats : 0;
   // statistics rows of the kernel launch_t picks (a dry run of the selection)
   int r = 0;
   t_dry_rows = &r;
@@ -2097,6 +2336,16 @@ int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   return 0;
 }
 }  // namespace
+
+extern "C" int64_t dfcsa_conv_work_floats(const dfcsa_conv_desc* d) {
+  ConvGemmArgs a;
+  int rows = 0;
+  int64_t need = 0;
+  t_dry_work = &need;
+  const int rc = desc_args(d, a, &rows);
+  t_dry_work = nullptr;
+  return rc ? rc : need;
+}
 
 extern "C" int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d) {
   ConvGemmArgs a;
@@ -2359,6 +2608,8 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 21) { g_wgrad_nosimple = value; return 0; }
   if (knob == 22) { g_halo_variant = value; return 0; }
   if (knob == 23) { g_wgrad_reduce_old = value; return 0; }
+  if (knob == 24) { g_wgrad_nst64 = value; return 0; }
+  if (knob == 25) { g_splitk = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

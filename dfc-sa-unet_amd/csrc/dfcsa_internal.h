@@ -22,6 +22,11 @@ struct ConvGemmArgs {
   float* stats;
   int Hout, Wout;
   int dbg;   // timing experiments only (knob 15): 1 = A operand from the zero page, 2 = B
+  // split-K (dfcsa_conv_desc.work): fp32 partial tiles of ksplit K ranges of kper 64-deep stages,
+  // summed in split order by the epilogue launch; kwork == nullptr: never split
+  float* kwork;
+  int64_t kwork_floats;
+  int ksplit, kper;
 };
 
 struct WgradArgs {
@@ -67,6 +72,7 @@ extern int g_wgrad_big;
 extern int g_wgrad_wide_small;
 extern int g_wgrad_halo;
 extern int g_wgrad_reduce_old;
+extern int g_wgrad_nst64;
 extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);

@@ -755,6 +755,148 @@ __global__ void batch_sum_kernel(int B, int64_t L, const T* __restrict__ x, floa
   }
 }
 
+// ------------------------------------------------------------ attention-probability dropout
+// Attention.forward with attention_dropout_rate > 0 in training (transformer_unet.py:146-151):
+// probs = softmax(q k^T * scale); ctx = attn_dropout(probs) @ v.  The score matrix of the ViT
+// (N = 196 tokens) is small, so this path materialises the UNDROPPED probabilities (fp32
+// [B*heads][N][N]) for the backward and regenerates the dropout mask from the counter-based key
+// (keep(i), i = (bh*N + n)*N + m).  One workgroup per query row (forward, dq) or key row (dk, dv).
+// Backward: dPd = dctx v^T; dP = dPd * keep / (1 - p); dS = P (dP - rowsum(P dP));
+// dq = scale dS k; dk = scale dS^T q; dv = Pd^T dctx.
+__device__ __forceinline__ float block_sum256(float v, float* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return (red[0] + red[1]) + (red[2] + red[3]);
+}
+__device__ __forceinline__ float block_max256(float v, float* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  return fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) mha_drop_fwd_kernel(int N, int heads, int dh, int ldq, float scale,
+                                                           const T* __restrict__ qkv, float p,
+                                                           const int64_t* __restrict__ rng, int site,
+                                                           float* __restrict__ probs, T* __restrict__ ctx) {
+  extern __shared__ float sm[];   // q [dh] | e [N] | red [4]
+  float* q = sm;
+  float* e = sm + dh;
+  float* red = e + N;
+  const int n = blockIdx.x, bh = blockIdx.y, b = bh / heads, h = bh - b * heads, D = heads * dh;
+  const T* base = qkv + (size_t)b * N * ldq;
+  for (int c = threadIdx.x; c < dh; c += 256) q[c] = ElemTraits<T>::to_f(base[(size_t)n * ldq + h * dh + c]);
+  __syncthreads();
+  float mx = -INFINITY;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const T* k = base + (size_t)m * ldq + D + h * dh;
+    float s = 0.f;
+    for (int c = 0; c < dh; ++c) s += q[c] * ElemTraits<T>::to_f(k[c]);
+    s *= scale;
+    e[m] = s;
+    mx = fmaxf(mx, s);
+  }
+  mx = block_max256(mx, red);
+  float sum = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float v = __expf(e[m] - mx);
+    e[m] = v;
+    sum += v;
+  }
+  sum = block_sum256(sum, red);
+  const float inv = 1.f / sum, kscale = 1.f / (1.f - p);
+  const uint64_t key = drop_key(rng, site);
+  const int64_t row = ((int64_t)bh * N + n) * N;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float pr = e[m] * inv;
+    probs[row + m] = pr;
+    e[m] = keep_elem(key, row + m, p) ? pr * kscale : 0.f;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < dh; c += 256) {
+    float acc = 0.f;
+    for (int m = 0; m < N; ++m) acc += e[m] * ElemTraits<T>::to_f(base[(size_t)m * ldq + 2 * D + h * dh + c]);
+    ctx[((size_t)b * N + n) * D + h * dh + c] = ElemTraits<T>::from_f(acc);
+  }
+}
+
+// query row n: dS row -> dscores, dq
+template <typename T>
+__global__ void __launch_bounds__(256) mha_drop_bwd_rows_kernel(int N, int heads, int dh, int ldq, float scale,
+                                                                const T* __restrict__ qkv, const T* __restrict__ dctx,
+                                                                const float* __restrict__ probs, float p,
+                                                                const int64_t* __restrict__ rng, int site,
+                                                                float* __restrict__ dscores, T* __restrict__ dqkv) {
+  extern __shared__ float sm[];   // dctx row [dh] | dS [N] | red [4]
+  float* dor = sm;
+  float* ds = sm + dh;
+  float* red = ds + N;
+  const int n = blockIdx.x, bh = blockIdx.y, b = bh / heads, h = bh - b * heads, D = heads * dh;
+  const T* base = qkv + (size_t)b * N * ldq;
+  for (int c = threadIdx.x; c < dh; c += 256) dor[c] = ElemTraits<T>::to_f(dctx[((size_t)b * N + n) * D + h * dh + c]);
+  __syncthreads();
+  const float kscale = 1.f / (1.f - p);
+  const uint64_t key = drop_key(rng, site);
+  const int64_t row = ((int64_t)bh * N + n) * N;
+  float dot = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const T* v = base + (size_t)m * ldq + 2 * D + h * dh;
+    float s = 0.f;
+    for (int c = 0; c < dh; ++c) s += dor[c] * ElemTraits<T>::to_f(v[c]);
+    const float dp = keep_elem(key, row + m, p) ? s * kscale : 0.f;
+    ds[m] = dp;
+    dot += probs[row + m] * dp;
+  }
+  dot = block_sum256(dot, red);
+  for (int m = threadIdx.x; m < N; m += 256) {
+    const float g = probs[row + m] * (ds[m] - dot);
+    ds[m] = g;
+    dscores[row + m] = g;
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < dh; c += 256) {
+    float acc = 0.f;
+    for (int m = 0; m < N; ++m) acc += ds[m] * ElemTraits<T>::to_f(base[(size_t)m * ldq + D + h * dh + c]);
+    dqkv[((size_t)b * N + n) * ldq + h * dh + c] = ElemTraits<T>::from_f(acc * scale);
+  }
+}
+
+// key row m: dk, dv
+template <typename T>
+__global__ void __launch_bounds__(256) mha_drop_bwd_cols_kernel(int N, int heads, int dh, int ldq, float scale,
+                                                                const T* __restrict__ qkv, const T* __restrict__ dctx,
+                                                                const float* __restrict__ probs, float p,
+                                                                const int64_t* __restrict__ rng, int site,
+                                                                const float* __restrict__ dscores,
+                                                                T* __restrict__ dqkv) {
+  extern __shared__ float sm[];   // dS column [N] | Pd column [N]
+  float* dsc = sm;
+  float* pd = sm + N;
+  const int m = blockIdx.x, bh = blockIdx.y, b = bh / heads, h = bh - b * heads, D = heads * dh;
+  const float kscale = 1.f / (1.f - p);
+  const uint64_t key = drop_key(rng, site);
+  for (int n = threadIdx.x; n < N; n += 256) {
+    const int64_t i = ((int64_t)bh * N + n) * N + m;
+    dsc[n] = dscores[i];
+    pd[n] = keep_elem(key, i, p) ? probs[i] * kscale : 0.f;
+  }
+  __syncthreads();
+  const T* base = qkv + (size_t)b * N * ldq;
+  for (int c = threadIdx.x; c < dh; c += 256) {
+    float dk = 0.f, dv = 0.f;
+    for (int n = 0; n < N; ++n) {
+      dk += dsc[n] * ElemTraits<T>::to_f(base[(size_t)n * ldq + h * dh + c]);
+      dv += pd[n] * ElemTraits<T>::to_f(dctx[((size_t)b * N + n) * D + h * dh + c]);
+    }
+    dqkv[((size_t)b * N + m) * ldq + D + h * dh + c] = ElemTraits<T>::from_f(dk * scale);
+    dqkv[((size_t)b * N + m) * ldq + 2 * D + h * dh + c] = ElemTraits<T>::from_f(dv);
+  }
+}
+
 __global__ void rng_advance_kernel(int64_t* rng) {
   if (threadIdx.x == 0 && blockIdx.x == 0) rng[1] += 1;
 }
@@ -1581,6 +1723,49 @@ extern "C" int dfcsa_mha_fwd(int dtype, int B, int N, int heads, int dh, int ldq
                                 (hipStream_t)stream);
   return mha_dispatch<float>(dh, B, N, heads, ldq, scale, qkv, nullptr, nullptr, nullptr, lse, nullptr, ctx, 0,
                              (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_mha_drop_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,
+                                  float p, const int64_t* rng, int site, float* probs, void* ctx, void* stream) {
+  if (B <= 0 || N <= 0 || N > 8192 || heads <= 0 || dh <= 0 || ldq < 3 * heads * dh || p < 0.f || p >= 1.f || !rng ||
+      !probs)
+    return DFCSA_EINVAL;
+  const dim3 grid(N, B * heads);
+  const size_t sm = (size_t)(dh + N + 4) * sizeof(float);
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(mha_drop_fwd_kernel<bf16_t>, grid, dim3(256), sm, (hipStream_t)stream, N, heads, dh, ldq, scale,
+                       (const bf16_t*)qkv, p, rng, site, probs, (bf16_t*)ctx);
+  else
+    hipLaunchKernelGGL(mha_drop_fwd_kernel<float>, grid, dim3(256), sm, (hipStream_t)stream, N, heads, dh, ldq, scale,
+                       (const float*)qkv, p, rng, site, probs, (float*)ctx);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_mha_drop_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,
+                                  const void* dctx, const float* probs, float p, const int64_t* rng, int site,
+                                  float* dscores, void* dqkv, void* stream) {
+  if (B <= 0 || N <= 0 || N > 8192 || heads <= 0 || dh <= 0 || ldq < 3 * heads * dh || p < 0.f || p >= 1.f || !rng ||
+      !probs || !dscores)
+    return DFCSA_EINVAL;
+  const dim3 grid(N, B * heads);
+  hipStream_t st = (hipStream_t)stream;
+  const size_t sm1 = (size_t)(dh + N + 4) * sizeof(float), sm2 = (size_t)2 * N * sizeof(float);
+  if (dtype == DFCSA_DT_BF16) {
+    hipLaunchKernelGGL(mha_drop_bwd_rows_kernel<bf16_t>, grid, dim3(256), sm1, st, N, heads, dh, ldq, scale,
+                       (const bf16_t*)qkv, (const bf16_t*)dctx, probs, p, rng, site, dscores, (bf16_t*)dqkv);
+    DFCSA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(mha_drop_bwd_cols_kernel<bf16_t>, grid, dim3(256), sm2, st, N, heads, dh, ldq, scale,
+                       (const bf16_t*)qkv, (const bf16_t*)dctx, probs, p, rng, site, dscores, (bf16_t*)dqkv);
+  } else {
+    hipLaunchKernelGGL(mha_drop_bwd_rows_kernel<float>, grid, dim3(256), sm1, st, N, heads, dh, ldq, scale,
+                       (const float*)qkv, (const float*)dctx, probs, p, rng, site, dscores, (float*)dqkv);
+    DFCSA_CHECK_LAUNCH();
+    hipLaunchKernelGGL(mha_drop_bwd_cols_kernel<float>, grid, dim3(256), sm2, st, N, heads, dh, ldq, scale,
+                       (const float*)qkv, (const float*)dctx, probs, p, rng, site, dscores, (float*)dqkv);
+  }
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_mha_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,

@@ -59,6 +59,9 @@ __device__ __forceinline__ void wgrad_dst_add(const WgradArgs& a, int i, int j, 
     if (i >= 2 * a.Ctot + a.Creal) return;
     const int d = i < a.Ctot ? 0 : (i < 2 * a.Ctot ? 1 : 2);
     a.dst[d][(int64_t)(i - d * a.Ctot) * a.NJ + j] += v;
+  } else if (a.layout == 3) {
+    if (i < a.Ctot) a.dst[0][(int64_t)i * a.NJ + j] += v;
+    else if (j >= a.Ctot) a.dst[1][(int64_t)(i - a.Ctot) * (a.NJ - a.Ctot) + (j - a.Ctot)] += v;
   } else {
     const int ij = j / a.Ctot, co = j - ij * a.Ctot;
     a.dst[0][((int64_t)i * a.Ctot + co) * 4 + ij] += v;
@@ -799,6 +802,12 @@ __device__ __forceinline__ void reduce_dst_add(int64_t e, int NI, int NJ, int la
     const int d = i < Ctot ? 0 : (i < 2 * Ctot ? 1 : 2);
     float* dst = d == 0 ? d0 : (d == 1 ? d1 : d2);
     dst[(int64_t)(i - d * Ctot) * NJ + j] += s;
+  } else if (layout == 3) {
+    // two 1x1 weight gradients sharing their inputs' trailing columns (the DFC block's fusion conv
+    // over [fused | local | attn] and gate conv over [local | attn]): rows [0, Ctot) -> d0 over all
+    // NJ columns; rows [Ctot, 2 Ctot) -> d1 over the columns [Ctot, NJ)
+    if (i < Ctot) d0[(int64_t)i * NJ + j] += s;
+    else if (j >= Ctot) d1[(int64_t)(i - Ctot) * (NJ - Ctot) + (j - Ctot)] += s;
   } else {
     // ConvTranspose2d weight [Cin][Cout][2][2]; i = ci, j = ij*Cout + co (Ctot = Cout)
     int ij = j / Ctot, co = j - ij * Ctot;
@@ -847,7 +856,7 @@ __global__ void __launch_bounds__(64 * SUB) wgrad_reduce_kernel(const float* __r
 }
 
 // Low split counts (the deep layers: 3-16 splits of a [NI][taps x Ctot] slab of up to 19 MB per
-// split): one workgroup per (row i, 64-channel chunk), its 4 waves take the taps round-robin, each
+// split; multi-tap layers up to 64 splits, in chunks of MAXS): one workgroup per (row i, 64-channel chunk), its 4 waves take the taps round-robin, each
 // lane issues all the split loads of its element at once (<= 16 in flight) and sums them in split
 // order; the [64][T] tile is transposed through LDS so the read-modify-write of the weight
 // gradient walks 64*T consecutive floats of the reference layout ([Cout][Cin][kh][kw]: taps
@@ -868,15 +877,17 @@ __global__ void __launch_bounds__(256) wgrad_reduce_tap_kernel(const float* __re
   const int cl = T == 1 ? wave * 64 + lane : lane;   // channel within the chunk
   for (int t = T == 1 ? 0 : wave; t < T; t += tstep) {
     const int c = c0 + cl;
-    float v[MAXS];
     const bool ok = c < Ctot;
     const float* p = slab + (int64_t)i * NJ + (int64_t)t * Ctot + c;
-#pragma unroll
-    for (int s = 0; s < MAXS; ++s) v[s] = (ok && s < splits) ? p[(int64_t)s * total] : 0.f;
     float acc = 0.f;
+    for (int s0 = 0; s0 < splits; s0 += MAXS) {   // MAXS loads in flight, summed in split order
+      float v[MAXS];
 #pragma unroll
-    for (int s = 0; s < MAXS; ++s)
-      if (s < splits) acc += v[s];
+      for (int s = 0; s < MAXS; ++s) v[s] = (ok && s0 + s < splits) ? p[(int64_t)(s0 + s) * total] : 0.f;
+#pragma unroll
+      for (int s = 0; s < MAXS; ++s)
+        if (s0 + s < splits) acc += v[s];
+    }
     tile[cl * T + t] = acc;
   }
   __syncthreads();
@@ -905,7 +916,10 @@ int launch_reduce(const float* slab, int splits, int NI, int NJ, int layout, int
   const int64_t total = (int64_t)NI * NJ;
   const int blocks = (int)((total + 63) / 64);
   const int T = layout == 0 ? ntaps : 4;
-  if (!g_wgrad_reduce_old && layout != 2 && splits <= 16 && T <= 9 && (int64_t)T * Ctot <= NJ && NI <= 65535) {
+  // (taps > 1 up to 64 splits: the 3x3 layers at 224^2 - 56^2 run 28 - 56; the high-split 1x1
+  // reductions already write coalesced and keep the split-parallel kernel below)
+  if (!g_wgrad_reduce_old && layout != 2 && layout != 3 && (splits <= 16 || (T > 1 && splits <= 64)) && T <= 9 &&
+      (int64_t)T * Ctot <= NJ && NI <= 65535) {
     const int cw = T == 1 ? 256 : 64;
     dim3 grid((Ctot + cw - 1) / cw, NI);
     if (splits <= 4)
@@ -1015,6 +1029,14 @@ bool whalo_plan(const WgradArgs& a, int dtype, int layout, WHaloArgs* h, int* bi
   return true;
 }
 
+// LDS-DMA ring depth of the wgrad tile kernel: knob 14 forces it for every launch; knob 24 (>= 0)
+// gives the 64-row tiles (NI <= 64: 24 KB stages, so three stages still leave two workgroups per
+// CU) their own depth
+inline int wgrad_nst(const WgradArgs& a, int BI) {
+  if (BI == 64 && g_wgrad_nst64 >= 2) return g_wgrad_nst64;
+  return g_wgrad_nst;
+}
+
 template <typename T, int BI>
 int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
   constexpr int BJ = 128;
@@ -1041,9 +1063,14 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
       } else {
         dim3 g1(xcd_pad(grid.x * grid.y * splits));
         constexpr int WM8 = BI == 64 ? 2 : 4, WN8 = BI == 64 ? 4 : 2;
-        if (waves == 8 && g_wgrad_nst >= 4)
+        const int nst = wgrad_nst(a, BI);
+        if (waves == 8 && nst >= 4 && a.simple)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4, true>), g1, dim3(512), 0, st, a, splits);
+        else if (waves == 8 && nst >= 4)
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8 && g_wgrad_nst == 3)
+        else if (waves == 8 && nst == 3 && a.simple)
+          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3, true>), g1, dim3(512), 0, st, a, splits);
+        else if (waves == 8 && nst == 3)
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3>), g1, dim3(512), 0, st, a, splits);
         else if (waves == 8 && a.simple)
           hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2, true>), g1, dim3(512), 0, st, a, splits);
@@ -1066,6 +1093,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_wgrad_nst64 = 0;       // knob 24: ring depth of the 64-row tiles (0 = follow knob 14)
 int g_wgrad_reduce_old = 0;  // knob 23: 1 = the element-order reduction for every split count
 int g_wgrad_halo = 0;      // knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel (off: slower so far)
 int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6; 0 = automatic)
@@ -1184,7 +1212,10 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   a.layout = d->layout; a.ntaps = d->ntaps; a.Ctot = d->Ctot; a.Creal = d->Creal; a.ndst = d->ndst;
   for (int i = 0; i < 3; ++i) a.dst[i] = i < d->ndst ? d->dst[i] : nullptr;
   if (d->ndst > 0) {
-    if (d->layout == 2 ? (d->ndst != 3 || d->Ctot <= 0 || 2 * d->Ctot > a.NI) : (a.NI % d->ndst != 0)) return DFCSA_EINVAL;
+    if (d->layout == 2 ? (d->ndst != 3 || d->Ctot <= 0 || 2 * d->Ctot > a.NI)
+                       : d->layout == 3 ? (d->ndst != 2 || d->Ctot <= 0 || a.NI != 2 * d->Ctot || a.NJ <= d->Ctot)
+                                        : (a.NI % d->ndst != 0))
+      return DFCSA_EINVAL;
     if (d->Ctot <= 0) return DFCSA_EINVAL;
   }
   // one split: the kernel adds its tile straight into dst (no slab, no second launch)
@@ -1253,7 +1284,9 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
 extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                                   int Ctot, int Creal, int ndst, float* const* dst, void* stream) {
   if (!slab || !dst || ndst < 1 || ndst > 3) return DFCSA_EINVAL;
-  if (layout == 2 ? (ndst != 3 || Ctot <= 0 || 2 * Ctot > NI) : (NI % ndst != 0)) return DFCSA_EINVAL;
+  if (layout == 2 ? (ndst != 3 || Ctot <= 0 || 2 * Ctot > NI)
+                  : layout == 3 ? (ndst != 2 || Ctot <= 0 || NI != 2 * Ctot || NJ <= Ctot) : (NI % ndst != 0))
+    return DFCSA_EINVAL;
   return launch_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
                        ndst > 2 ? dst[2] : nullptr, (hipStream_t)stream);
 }

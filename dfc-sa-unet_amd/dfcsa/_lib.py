@@ -31,9 +31,9 @@ def parse_header(path=HEADER_PATH):
     text = open(path).read()
     text = re.sub(r"/\*.*?\*/", " ", text, flags=re.S)
     protos = {}
-    for m in re.finditer(r"\b(int|const\s+char\s*\*)\s*(dfcsa_\w+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
+    for m in re.finditer(r"\b(int64_t|int|const\s+char\s*\*)\s*(dfcsa_\w+)\s*\(([^;{]*?)\)\s*;", text, flags=re.S):
         ret, name, args = m.group(1), m.group(2), m.group(3)
-        restype = ctypes.c_char_p if "char" in ret else ctypes.c_int
+        restype = ctypes.c_char_p if "char" in ret else (ctypes.c_int64 if ret == "int64_t" else ctypes.c_int)
         argtypes = []
         args = args.strip()
         if args and args != "void":
@@ -64,7 +64,8 @@ class ConvDesc(ctypes.Structure):
                 ("stride", ctypes.c_int), ("weight", ctypes.c_void_p), ("bias", ctypes.c_void_p),
                 ("mode", ctypes.c_int), ("ndest", ctypes.c_int), ("dest", ctypes.c_void_p * 3),
                 ("Nd", ctypes.c_int), ("accumulate", ctypes.c_int), ("stats", ctypes.c_void_p),
-                ("Hout", ctypes.c_int), ("Wout", ctypes.c_int), ("stats_floats", ctypes.c_int64)]
+                ("Hout", ctypes.c_int), ("Wout", ctypes.c_int), ("stats_floats", ctypes.c_int64),
+                ("work", ctypes.c_void_p), ("work_floats", ctypes.c_int64)]
 
 
 class WgradDesc(ctypes.Structure):

@@ -45,6 +45,9 @@ POOL_FUSION = [os.environ.get("DFCSA_POOL_FUSION", "1") == "1"]
 # MFMAs) and the second at 137 against 103 + ~50 us, so only the second is on by default
 APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[:1] == "1",
                   os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[-1:] == "1"]
+# bf16 blocks with C <= 128: the fusion conv's and the gate conv's weight gradients as one GEMM over
+# [fused | local | attn] (wgrad layout 3; DFCSA_PAIR_WGRAD=0: two launches)
+PAIR_WGRAD = [os.environ.get("DFCSA_PAIR_WGRAD", "1") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -323,10 +326,15 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
              P(bn3.invstd), P(s.local), P(s.attn), P(dlocal), P(dattn), P(dz3), *S(part), stream())
     else:
         dy4 = ops.bn_bwd_apply_relu(dtype, dout, s.y4, bn4, bn4m.weight, coef, grad_of(conv4.bias))
-    # fusion conv: dW4 (side stream) and d[fused, local, attn]
-    with on_side(dev, dy4, s.fused, s.local, s.attn):
-        ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                            [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
+    # fusion conv: dW4 (side stream) and d[fused, local, attn].  C <= 128 (HBM-bound 1x1 weight
+    # gradients at 224^2 / 112^2): dW4 waits for dy3 and runs as ONE GEMM with the gate conv's dW3
+    # (G = [dy4 | dy3] over [fused | local | attn], layout 3): local and attn are read once
+    pair_wgrad = dtype == torch.bfloat16 and C <= 128 and PAIR_WGRAD[0]
+    dy4_keep = dy4 if pair_wgrad else None
+    if not pair_wgrad:
+        with on_side(dev, dy4, s.fused, s.local, s.attn):
+            ops.conv_wgrad_into(dtype, [dy4], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                                [grad_of(conv4.weight)], 1, 3 * C, 3 * C)
     if apro:
         del dy4
     elif fused:
@@ -361,9 +369,15 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     else:
         dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
         del dz3
-    with on_side(dev, dy3):
-        ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                            [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
+    if pair_wgrad:
+        with on_side(dev, dy4_keep, dy3, s.fused, s.local, s.attn):
+            ops.conv_wgrad_into(dtype, [dy4_keep, dy3], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C,
+                                grid, hw, [grad_of(conv4.weight), grad_of(conv3.weight)], 1, C, 3 * C, layout=3)
+        del dy4_keep
+    else:
+        with on_side(dev, dy3):
+            ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
+                                [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
     if apro3:
         pass
     elif fused_bn1:

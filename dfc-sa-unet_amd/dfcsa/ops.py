@@ -57,6 +57,9 @@ def ntiles_ew(M, C):
 
 
 # --------------------------------------------------------------------------- GEMMs
+_SPLITK_MAX_M = 65536   # split-K applies to few-tile launches only (dfcsa_conv_work_floats decides)
+
+
 def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=None, stride=1,
               mode=0, accumulate=False, stats=None, out_hw=(0, 0)):
     """segs: list of (tensor, dh, dw); grid: (B, Ho, Wo) output pixel grid; in_hw: (Hi, Wi).
@@ -86,6 +89,13 @@ def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=N
     d.stats = P(stats)
     d.stats_floats = stats.numel() if stats is not None else 0
     d.Hout, d.Wout = out_hw
+    work = None
+    if d.dtype == _lib.DT_BF16 and d.M <= _SPLITK_MAX_M:
+        # split-K workspace of a few-tile, long-K launch (stream-ordered torch allocation, graph-safe)
+        wf = _lib.LIB.dfcsa_conv_work_floats(ctypes.addressof(d))
+        if wf > 0:
+            work = torch.empty(wf, device=weight.device, dtype=torch.float32)
+            d.work, d.work_floats = P(work), wf
     call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
     if stats is not None:   # statistics rows written (the ntiles of bn_finalize)
         return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d))

@@ -490,7 +490,16 @@ class ViTBlock(torch.autograd.Function):
                         bias=pk["bqkv"])
         scale = 1.0 / math.sqrt(dh)
         flash = None
-        if _flash_mha(dtype, dh):
+        probs = None
+        if p_attn > 0:
+            # attn_dropout on the probabilities (:151): materialised-score path, mask regenerated
+            # in the backward from (rng, site + 3)
+            cx = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
+            probs = _f32((B * heads * N * N,), dev)
+            lse = None
+            call("dfcsa_mha_drop_fwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), float(p_attn), P(rng),
+                 site + 3, P(probs), P(cx), stream())
+        elif _flash_mha(dtype, dh):
             cx, flash = mha_flash_forward(dtype, qkv, B, N, heads, dh)
             cx = cx.view(B, gh, gw, D)
             lse = None
@@ -518,6 +527,7 @@ class ViTBlock(torch.autograd.Function):
         ctx.cfg = (p, p_attn, rng, site, heads, dh, scale, F)
         ctx.t = (h, y1, mr1, qkv, cx, lse, h1, y2, mr2, f, g)
         ctx.flash = flash
+        ctx.probs = probs
         return out
 
     @staticmethod
@@ -553,7 +563,14 @@ class ViTBlock(torch.autograd.Function):
         bias_grad_into(dtype, da, att.out.bias)
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
-        if ctx.flash is not None:
+        if ctx.probs is not None:
+            dqkv = torch.empty_like(qkv)
+            dscores = _f32((B * heads * N * N,), dev)
+            call("dfcsa_mha_drop_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(dcx), P(ctx.probs),
+                 float(p_attn), P(rng), site + 3, P(dscores), P(dqkv), stream())
+            ctx.probs = None
+            del dscores
+        elif ctx.flash is not None:
             dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh).view_as(qkv)
             ctx.flash = None
         else:

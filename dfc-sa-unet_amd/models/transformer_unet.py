@@ -329,17 +329,17 @@ class TransUNet(nn.Module):
 
         emb = self.transformer.embeddings
         tcfg = self.config.transformer
-        if training and tcfg["attention_dropout_rate"] > 0:
-            raise NotImplementedError("attention-probability dropout (attention_dropout_rate > 0) is not built")
         p = float(tcfg["dropout_rate"]) if training else 0.0
+        # attn_dropout + proj_dropout (:139-140, :151, :156): both at attention_dropout_rate
+        p_attn = float(tcfg["attention_dropout_rate"]) if training else 0.0
         rng = self._dropout_rng(x.device)
-        if p > 0:
+        if p > 0 or p_attn > 0:
             call("dfcsa_rng_advance", P(rng), stream())
 
         h, features = emb.hybrid_model.forward_nhwc(x, dtype, self)
         t = PatchEmbed.apply(h, emb, dtype, p, rng, *emb.patch_embeddings.parameters(), emb.position_embeddings)
         for i, blk in enumerate(self.transformer.encoder.layer):
-            t = ViTBlock.apply(t, blk, dtype, p, 0.0, rng, 16 + 4 * i, *blk.parameters())
+            t = ViTBlock.apply(t, blk, dtype, p, p_attn, rng, 16 + 4 * i, *blk.parameters())
         enc = self.transformer.encoder.encoder_norm
         t = LayerNormOut.apply(t, enc, dtype, *enc.parameters())
         y = self.decoder.forward_nhwc(t, features, dtype)

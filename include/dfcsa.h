@@ -64,6 +64,8 @@ typedef struct {
   float* stats;
   int Hout, Wout;
   int64_t stats_floats; /* capacity of stats in floats: >= dfcsa_conv_stats_rows(d)*2*N (<= ceil(M/64)*2*N) */
+  float* work;          /* split-K workspace (optional): a bf16 launch with few 128x128 tiles and a long K */
+  int64_t work_floats;  /* splits its K range over workgroups when work holds dfcsa_conv_work_floats(d) */
 } dfcsa_conv_desc;
 int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream);
 int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile of the row-tile kernels */
@@ -71,6 +73,10 @@ int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile of the row-tile kernels
  * of the row-tile kernels (ceil(M / BM), BM = 64..256), one per workgroup of the persistent 1x1
  * streaming kernel, one per 2-D tile of the bf16 3x3 halo-tile kernel */
 int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d);
+/* fp32 workspace the launch of *d splits its K range into (fixed-order partial-tile reduction in a
+ * second launch that also runs the epilogue); 0 when it does not split.  A caller that passes no
+ * workspace (work == NULL) gets the unsplit kernel. */
+int64_t dfcsa_conv_work_floats(const dfcsa_conv_desc* d);
 
 /* ------------------------------------------------------------------------------------------
  * Weight gradient (MFMA, reduction over pixels).  Replaces the weight half of
@@ -117,7 +123,11 @@ int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
  *  layout 1 (ConvTranspose2d): row = ci, column j = ij*Cout + co -> dst[ci][co][ij].
  *  layout 2 (stacked 1x1 q/k/v): rows [0,Ctot) -> dst[0], [Ctot,2Ctot) -> dst[1],
  *     [2Ctot, 2Ctot+Creal) -> dst[2], later rows (GEMM padding) dropped; dst[d][row - base][j]
- *     with NJ columns (ndst must be 3). */
+ *     with NJ columns (ndst must be 3).
+ *  layout 3 (two 1x1 convs over shared trailing inputs: the DFC block's fusion conv over
+ *           [fused | local | attn] and gate conv over [local | attn], one GEMM with G = [dy4 | dy3]):
+ *           rows [0,Ctot) -> dst[0][i][j] over all NJ columns; rows [Ctot,2Ctot) -> dst[1][i-Ctot][j-Ctot]
+ *           for j >= Ctot (the [dy3 x fused] block is discarded); ndst must be 2. */
 int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                        int Ctot, int Creal, int ndst, float* const* dst, void* stream);
 
@@ -570,6 +580,16 @@ int dfcsa_mha_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float sca
                   float* lse, void* stream);
 int dfcsa_mha_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,
                   const void* ctx, const void* dctx, const float* lse, float* dvec, void* dqkv, void* stream);
+/* The same core with attention-probability dropout (attn_dropout, :147-151, attention_dropout_rate
+ * = p > 0 in training): ctx = (keep * softmax(q k^T * scale) / (1 - p)) v, keep from the
+ * counter-based dropout key (rng, site) of element (bh*N + n)*N + m.  probs [B*heads][N][N] fp32
+ * receives the undropped probabilities (the backward's input); dscores [B*heads][N][N] fp32 is
+ * backward scratch.  Any dh; N <= 8192 (one workgroup per query / key row, materialised scores). */
+int dfcsa_mha_drop_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv, float p,
+                       const int64_t* rng, int site, float* probs, void* ctx, void* stream);
+int dfcsa_mha_drop_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,
+                       const void* dctx, const float* probs, float p, const int64_t* rng, int site, float* dscores,
+                       void* dqkv, void* stream);
 /* nn.UpsamplingBilinear2d(scale_factor=2) (align_corners=True, :262): [B][Hi][Wi][C] -> [B][2Hi][2Wi][C];
  * bwd is a deterministic gather into dx [B][Hi][Wi][C] */
 int dfcsa_upsample2_ac(int dtype, int B, int C, int Hi, int Wi, const void* x, void* out, void* stream);

@@ -775,7 +775,7 @@ def _reduce_ref(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst):
 @pytest.mark.parametrize("layout,ntaps,NI,Ctot,Creal,ndst,extra", [
     (0, 9, 64, 128, 128, 1, 0), (0, 9, 96, 72, 67, 2, 8), (0, 1, 48, 512, 512, 3, 0), (0, 9, 16, 8, 3, 1, 0),
     (1, 4, 40, 96, 96, 1, 0)])
-@pytest.mark.parametrize("splits", [1, 3, 7, 16, 17, 40])
+@pytest.mark.parametrize("splits", [1, 3, 7, 16, 17, 40, 56, 70])
 def test_wgrad_reduce_layouts(layout, ntaps, NI, Ctot, Creal, ndst, extra, splits):
     """The split-K reduction into the reference weight layouts (Conv2d [Cout][Cin][kh][kw] with K
     padding columns and channel padding, three stacked destinations, ConvTranspose2d [Cin][Cout][2][2]):
@@ -797,3 +797,86 @@ def test_wgrad_reduce_layouts(layout, ntaps, NI, Ctot, Creal, ndst, extra, split
             dfcsa.set_tuning(23, 0)
         for d, r in zip(dsts, ref):
             assert (d.double().cpu() - 0.5 - r).abs().max().item() < 1e-5 * max(1.0, splits ** 0.5)
+
+
+@pytest.mark.parametrize("B,H,Cs,nsrc,taps,N", [(4, 14, 512, 2, 9, 512), (16, 14, 1024, 1, 11, 512), (3, 13, 256, 1, 9, 136),
+                                               (8, 14, 1024, 3, 1, 1024)])
+def test_conv_splitk_matches_unsplit(B, H, Cs, nsrc, taps, N):
+    """Split-K launch (few 128x128 tiles, long K: the 14^2 bottleneck / 28^2 layers) against the
+    unsplit kernel (knob 25 = 0) and a torch fp32 reference: outputs and BN statistics; partial M /
+    N tiles included; the split plan is visible through dfcsa_conv_work_floats."""
+    import ctypes
+
+    import dfcsa
+    from dfcsa import _lib
+    torch.manual_seed(5)
+    bf = torch.bfloat16
+    xs = [q(torch.randn(B, Cs, H, H), bf) for _ in range(nsrc)]
+    xh = [nhwc(x, bf) for x in xs]
+    if taps == 9:
+        segs = [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xh]
+    elif taps == 11:
+        segs = [(xh[0], 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(xh[0], 0, 0), (xh[0], 0, 0)]
+    else:
+        segs = [(x, 0, 0) for x in xh]
+    K = len(segs) * Cs
+    Kp = ops.rup(K, 64)
+    w = q(torch.randn(N, Kp) * 0.02, bf)
+    b = torch.randn(N)
+    M = B * H * H
+    outs, sts = [], []
+    for knob in (1, 0):
+        dfcsa.set_tuning(25, knob)
+        try:
+            y = torch.full((B, H, H, N), float("nan"), dtype=bf, device="cuda")
+            stats = torch.full((ops.ntiles_gemm(M) * 2 * N,), float("nan"), device="cuda")
+            rows = ops.conv_gemm(bf, segs, Cs, (B, H, H), (H, H), w.to("cuda", bf), Kp, N, [y], N, bias=b.cuda(),
+                                 stats=stats)
+            torch.cuda.synchronize()
+        finally:
+            dfcsa.set_tuning(25, 1)
+        outs.append(y.float().cpu())
+        sts.append(stats[:rows * 2 * N].view(-1, 2, N).sum(0).cpu())
+    # the reference: the same gathered operand as one GEMM
+    cols = []
+    for t, dh, dw in segs:
+        tc = t.float().cpu()
+        sh = torch.zeros_like(tc)
+        hs, he = max(0, -dh), H - max(0, dh)
+        ws, we = max(0, -dw), H - max(0, dw)
+        sh[:, hs:he, ws:we] = tc[:, hs + dh:he + dh, ws + dw:we + dw]
+        cols.append(sh.reshape(M, Cs))
+    A = torch.cat(cols, 1)
+    acc = A @ w[:, :K].t()
+    ref = acc + b
+    for o, st in zip(outs, sts):
+        assert torch.isfinite(o).all()
+        assert rel(o.reshape(M, N), ref) < 1e-2
+        assert rel(st[0], acc.sum(0)) < 1e-4 and rel(st[1], (acc * acc).sum(0)) < 1e-4
+    assert rel(outs[0], outs[1]) < 5e-3
+
+
+@pytest.mark.parametrize("B,H,C", [(2, 20, 64), (1, 37, 128), (16, 56, 64)])
+def test_wgrad_pair_layout3(B, H, C):
+    """The fusion conv's and the gate conv's weight gradients as one GEMM (G = [dy4 | dy3] over
+    [fused | local | attn], layout 3) against the two separate launches and a torch fp32 reference."""
+    torch.manual_seed(C + H)
+    bf = torch.bfloat16
+    xs = [q(torch.randn(B, C, H, H), bf) for _ in range(3)]            # fused, local, attn
+    g4, g3 = (q(torch.randn(B, C, H, H) * 0.1, bf) for _ in range(2))
+    xh = [nhwc(x, bf) for x in xs]
+    segs = [(x, 0, 0) for x in xh]
+    w4 = torch.zeros(C, 3 * C, 1, 1, device="cuda")
+    w3 = torch.zeros(C, 2 * C, 1, 1, device="cuda")
+    ops.conv_wgrad_into(bf, [nhwc(g4, bf), nhwc(g3, bf)], C, segs, C, (B, H, H), (H, H), [w4, w3], 1, C, 3 * C,
+                        layout=3)
+    s4 = torch.zeros_like(w4)
+    s3 = torch.zeros_like(w3)
+    ops.conv_wgrad_into(bf, [nhwc(g4, bf)], C, segs, C, (B, H, H), (H, H), [s4], 1, 3 * C, 3 * C)
+    ops.conv_wgrad_into(bf, [nhwc(g3, bf)], C, segs[1:], C, (B, H, H), (H, H), [s3], 1, 2 * C, 2 * C)
+    torch.cuda.synchronize()
+    X = torch.cat(xs, 1).permute(0, 2, 3, 1).reshape(-1, 3 * C)
+    r4 = g4.permute(0, 2, 3, 1).reshape(-1, C).t() @ X
+    r3 = g3.permute(0, 2, 3, 1).reshape(-1, C).t() @ X[:, C:]
+    assert rel(w4.view(C, -1), r4) < 1e-5 and rel(w3.view(C, -1), r3) < 1e-5
+    assert rel(w4, s4) < 1e-6 and rel(w3, s3) < 1e-6

@@ -121,6 +121,89 @@ def test_mha_fwd_bwd(B, N, heads, dh, dtype, tol):
         assert rel(dqkv[..., i * D:(i + 1) * D], dqr[..., i * D:(i + 1) * D]) < 3 * tol, i
 
 
+def _keep_mask(rng0, rng1, site, n, p):
+    """numpy restatement of the counter-based dropout keep(i) of csrc/transunet.hip (drop_key,
+    mix64, keep_elem) for element indices 0 .. n-1."""
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+    with np.errstate(over="ignore"):
+        key = (np.uint64(rng0) * np.uint64(0x100000001B3)) ^ (np.uint64(rng1) << np.uint64(20)) ^ \
+            (np.uint64(site) << np.uint64(52))
+        z = key ^ (np.arange(n, dtype=np.uint64) * np.uint64(0xD6E8FEB86659FD93))
+        z = (z + np.uint64(0x9E3779B97F4A7C15)) & M
+        z = ((z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)) & M
+        z = ((z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)) & M
+        z = z ^ (z >> np.uint64(31))
+    u = ((z >> np.uint64(32)) >> np.uint64(8)).astype(np.float32) * np.float32(1.0 / 16777216.0)
+    return u >= np.float32(p)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
+@pytest.mark.parametrize("B,N,heads,dh,p", [(2, 196, 12, 64, 0.1), (3, 50, 4, 32, 0.3), (1, 7, 2, 16, 0.5)])
+def test_mha_attention_dropout(B, N, heads, dh, p, dtype, tol):
+    """Attention-probability dropout (Attention.forward :146-151 with attention_dropout_rate = p):
+    the kernel's mask regenerated here from the same counter-based key, ctx = (keep * P / (1 - p)) v
+    and the q / k / v gradients against torch autograd with that mask; the stored probabilities are
+    the undropped softmax; the keep rate is 1 - p."""
+    call, P, dt, stream = lib()
+    torch.manual_seed(N + 7 * heads)
+    D = heads * dh
+    qkv = (torch.randn(B, N, 3 * D, device="cuda") * 1.5).to(dtype)
+    rng = torch.tensor([987654321, 5], dtype=torch.int64, device="cuda")
+    site = 19
+    keep = torch.from_numpy(_keep_mask(987654321, 5, site, B * heads * N * N, p)).view(B, heads, N, N)
+    qr = qkv.float().cpu().clone().requires_grad_(True)
+    q, k, v = (qr[..., i * D:(i + 1) * D].reshape(B, N, heads, dh).permute(0, 2, 1, 3) for i in range(3))
+    a = torch.softmax(q @ k.transpose(-1, -2) / math.sqrt(dh), dim=-1)
+    yr = ((a * keep / (1 - p)) @ v).permute(0, 2, 1, 3).reshape(B, N, D)
+    g = torch.randn_like(yr)
+    dqr = torch.autograd.grad(yr, qr, g)[0]
+    ctx = torch.empty((B, N, D), dtype=dtype, device="cuda")
+    probs = torch.empty(B * heads * N * N, device="cuda")
+    scale = 1.0 / math.sqrt(dh)
+    call("dfcsa_mha_drop_fwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), p, P(rng), site, P(probs), P(ctx),
+         stream())
+    torch.cuda.synchronize()
+    assert rel(probs.cpu().view(B, heads, N, N), a.detach()) < max(tol, 1e-6)
+    assert rel(ctx, yr) < tol
+    dqkv = torch.empty_like(qkv)
+    dscores = torch.empty_like(probs)
+    call("dfcsa_mha_drop_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(g.to("cuda", dtype)), P(probs), p,
+         P(rng), site, P(dscores), P(dqkv), stream())
+    torch.cuda.synchronize()
+    for i in range(3):
+        assert rel(dqkv[..., i * D:(i + 1) * D], dqr[..., i * D:(i + 1) * D]) < 3 * tol, i
+    if B * heads * N * N > 100000:
+        assert abs(keep.float().mean().item() - (1 - p)) < 0.01
+
+
+def test_transunet_attention_dropout_train_step():
+    """TransUNet with attention_dropout_rate > 0 (attn_dropout on the probabilities + proj_dropout):
+    a train-mode forward/backward runs on the dropout path with finite gradients that differ from
+    the p = 0 step, two steps draw different masks, and eval mode ignores the rate."""
+    torch.manual_seed(0)
+    m, fx = _small_model("fp32")
+    x = torch.from_numpy(fx["x"]).cuda()
+    m.config.transformer["attention_dropout_rate"] = 0.0
+    m.eval()
+    with torch.no_grad():
+        y_eval0 = m(x).clone()
+    m.config.transformer["attention_dropout_rate"] = 0.2
+    with torch.no_grad():
+        y_eval = m(x).clone()
+    assert torch.equal(y_eval, y_eval0)
+    m.train()
+    outs, grads = [], []
+    for _ in range(2):
+        m.zero_grad(set_to_none=False)
+        y = m(x)
+        y.square().mean().backward()
+        outs.append(y.detach().clone())
+        grads.append(m.transformer.encoder.layer[0].attn.query.weight.grad.detach().clone())
+    assert all(torch.isfinite(o).all() for o in outs) and all(torch.isfinite(gq).all() for gq in grads)
+    assert not torch.equal(outs[0], outs[1])
+    m.config.transformer["attention_dropout_rate"] = 0.0
+
+
 @pytest.mark.parametrize("B,N,heads", [(2, 196, 12), (1, 130, 2), (3, 4, 2)])
 def test_mha_flash_bf16(B, N, heads):
     """bf16 ViT attention on the MFMA flash kernels (head-major relayout, q pre-scaled): against the

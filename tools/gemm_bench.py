@@ -39,9 +39,18 @@ for name, H, Cs, nsrc, ntaps, N in SHAPES:
     stats = torch.empty(ops.ntiles_gemm(M) * 2 * N, device="cuda")
     flops = 2.0 * M * N * K
     row = {"shape": name, "M": M, "N": N, "K": K}
+    ref = None
     for c in cfgs:
         LIB.dfcsa_set_tuning(1, c)
         run = lambda: ops.conv_gemm(bf, segs, Cs, (B, H, H), (H, H), w, Kp, N, [y], N, stats=stats)
+        if os.environ.get("GEMM_CHECK"):
+            y.zero_()
+            run()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = y.clone()
+            else:
+                row[f"{c}_maxdiff"] = (y.float() - ref.float()).abs().max().item()
         for _ in range(3):
             run()
         torch.cuda.synchronize()

@@ -1,0 +1,11 @@
+# A/B of environment settings on the bench (same box, 2 rounds): gpu_ab_envs.sh "<label>:<VAR=v VAR2=v2>" ...
+mkdir -p gpurun_out
+cd $GRAFT_REPO_ROOT
+B="--no-cpu-baseline --no-val-dice --no-trainer-faithful"
+for rep in 1 2; do
+  for arm in "$@"; do
+    lab=${arm%%:*}; envs=${arm#*:}
+    env $envs timeout -k 10 300 python bench.py $B > gpurun_out/ab_${lab}_$rep.json 2> gpurun_out/ab_${lab}_$rep.err || { echo "bench $lab failed"; exit 1; }
+    python3 -c "import json;d=json.load(open('gpurun_out/ab_${lab}_$rep.json'));print('$lab', $rep, d['value'], d['ms_per_step'])"
+  done
+done
