@@ -675,15 +675,17 @@ int launch_glds32(const ConvGemmArgs& a, hipStream_t st) {
 thread_local int64_t* t_dry_work = nullptr;   // dfcsa_conv_work_floats: the split-K workspace
 
 // split-K plan of a 128x128 tile launch: ksplit, kper (64-deep stages per split); 1 = no split.
-// Few tiles (< 256: the 14^2 / 28^2 layers and TransUNet's ViT rows) with a long K (>= 32 stages)
-// get ~600 workgroups of >= 12 stages each.
+// Few tiles (< 150: the 14^2 bottleneck dgrad) with a long K (>= 64 stages) get ~600 workgroups of
+// >= 12 stages each.
 int g_splitk = 1;   // knob 25: 0 = never split
 void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
   *ksplit = 1;
   *kper = a.Kpad / 64;
   const int tiles = ((a.N + 127) / 128) * ((a.M + 127) / 128);
   const int nk = a.Kpad / 64;
-  if (!g_splitk || tiles >= 256 || nk < 32) return;
+  // measured (profiles/r03b_splitk.jsonl): the 14^2 3x3 dgrad (100 tiles, 176 stages) 93 -> 63 us;
+  // at 200 tiles / 72 stages (the 14^2 forward) the 64x64 tile stays faster (50 vs 57 us)
+  if (!g_splitk || tiles >= 150 || nk < 64) return;
   int s = (600 + tiles - 1) / tiles;
   s = std::min(s, nk / 12);
   if (s < 2) return;
