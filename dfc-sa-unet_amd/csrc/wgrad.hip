@@ -549,6 +549,181 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
 }
 
 // --------------------------------------------------------------------------------------------
+// bf16 weight gradient with buffer-descriptor LDS-DMA on 64-channel sub-images (simple geometry:
+// stride 1, same-size input, shifts in [-1, 1]; Cseg % 64 == 0 and Cg % 64 == 0).
+//
+// The stage images of wgrad_glds_kernel are [64 pixels][BI | BJ channels]; a 1-KB DMA then spans
+// channel blocks of different sources / taps, so every lane carries its own 64-bit source pointer
+// and zero-page select (~8 VALU per DMA, 7.9 VALU per MFMA measured on the 224^2 3x3 layer).  Here
+// each operand tile is cut into [64 pixels][64 channels] sub-images (128-B rows, the blk_swz<64>
+// swizzle of the BI = 64 images): one sub-image lies inside ONE dY tensor / ONE tap segment, so its
+// source base, tap shift and channel offset are wave-uniform (a scalar buffer descriptor), the
+// stage's pixel advance is the scalar soffset, and a lane adds only its fixed row/chunk offset and a
+// tap-validity select (sel_oob: offset >= 2^31 reads zeros).  Wave w fills rows 8w .. 8w + 7 of
+// every sub-image, so a lane's pixel is the same in all its DMAs of a stage: its (row, column) is
+// tracked incrementally and the 9 tap-validity bits are formed once per stage.
+// --------------------------------------------------------------------------------------------
+// The DMA is issued from inline asm (as glds16_asm above): with the builtin the compiler cannot
+// tell the ring slot being filled from the one the transposed reads use and drains every DMA
+// (s_waitcnt vmcnt(0)) before the fragment reads.  Descriptor words: base, stride 0,
+// num_records 2^31 - 1, the raw-buffer flags of __builtin_amdgcn_make_buffer_rsrc(.., 0x00020000).
+typedef int wrsrc_t __attribute__((ext_vector_type(4)));
+constexpr unsigned kWOOB = 0x80000000u;
+__device__ __forceinline__ wrsrc_t wbuf(const void* base) {
+  const uint64_t a = (uint64_t)base;
+  wrsrc_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((int)(uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((int)((uint32_t)(a >> 32) & 0xffffu));
+  r[2] = 0x7fffffff;
+  r[3] = 0x00020000;
+  return r;
+}
+__device__ __forceinline__ void wblds16(wrsrc_t r, unsigned voff, unsigned soff, const char* lds_dst) {
+  const unsigned dst = (unsigned)(size_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %4\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, %3 offen lds\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(r), "s"(soff), "s"(dst)
+               : "memory");
+}
+
+// voff if bit `bit` of mask is set, else out of range
+__device__ __forceinline__ unsigned sel_oob_w(unsigned mask, int bit, unsigned voff) {
+  const unsigned m = (unsigned)__builtin_amdgcn_sbfe((int)mask, bit, 1);
+  return (voff & m) | (kWOOB & ~m);
+}
+
+template <int BI, int NST>
+__global__ void __launch_bounds__(512) wgrad_bd_kernel(const WgradArgs args, int nsplit) {
+  using T = bf16_t;
+  constexpr int BJ = 128, NW = 8;
+  constexpr int WM = BI == 64 ? 2 : 4, WN = BI == 64 ? 4 : 2;
+  constexpr int WTM = BI / WM, WTN = BJ / WN, FM = WTM / 16, FN = WTN / 16;
+  constexpr int GS = BI / 64, XS = BJ / 64;            // sub-images per operand
+  constexpr int SUB = 64 * 128;                        // bytes of one [64 px][64 ch] sub-image
+  constexpr int STAGE = (GS + XS) * SUB;
+  constexpr int OPS = GS + XS;                         // DMAs per wave per stage
+  __shared__ __attribute__((aligned(16))) char smem[NST * STAGE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int nJ = (args.NJ + BJ - 1) / BJ, nI = (args.NI + BI - 1) / BI;
+  const int L = xcd_remap(blockIdx.x, nJ * nI * nsplit);
+  if (L < 0) return;
+  const int j0 = (L % nJ) * BJ, i0 = ((L / nJ) % nI) * BI, split = L / (nJ * nI);
+  const int mbeg = split * args.mchunk;
+  const int mend = min(args.M, mbeg + args.mchunk);
+
+  // lane -> (row, physical 16-B chunk) of its 1-KB DMA piece; logical channel via the swizzle
+  const int prow = 8 * wave + (lane >> 3), pc = lane & 7;
+  const int lc = ((blk_swz<64>(prow, pc >> 1) << 1) | (pc & 1)) * 8;
+  // G sub-images: scalar bases (tensor, channel block); X sub-images: segment base + tap shift
+  wrsrc_t gr[GS], xr[XS];
+  int xtb[XS];
+  bool gon[GS], xon[XS];
+#pragma unroll
+  for (int s = 0; s < GS; ++s) {
+    const int i = i0 + s * 64;
+    gon[s] = i < args.NI;
+    const int grp = gon[s] ? i / args.Cg : 0;
+    gr[s] = wbuf((const T*)args.g_ptr[grp] + (gon[s] ? i - grp * args.Cg : 0));
+  }
+#pragma unroll
+  for (int s = 0; s < XS; ++s) {
+    const int j = j0 + s * 64;
+    xon[s] = j < args.NJ;
+    const int sg = xon[s] ? j / args.Cseg : 0;
+    const ConvSeg seg = args.seg[sg];
+    const int ch0 = xon[s] ? j - sg * args.Cseg : 0;
+    xr[s] = wbuf((const T*)seg.ptr + ((seg.dh * args.Wi + seg.dw) * args.Cseg + ch0));
+    xtb[s] = (seg.dh + 1) * 3 + seg.dw + 1;
+  }
+  // lane offsets at the split's first pixel (+ 64 pixels per stage through soffset)
+  const unsigned goff = 2u * (unsigned)((mbeg + prow) * args.Cg + lc);
+  const unsigned xoff = 2u * (unsigned)((mbeg + prow) * args.Cseg + lc);
+  const unsigned gstep = 2u * 64u * (unsigned)args.Cg, xstep = 2u * 64u * (unsigned)args.Cseg;
+  // (row, column) of the lane's pixel, advanced 64 pixels per issued stage
+  int oh, ow;
+  {
+    const int m = mbeg + prow;
+    const int b = dm_div(args.dm_hw, m);
+    const int rem = m - b * args.dm_hw.d;
+    oh = dm_div(args.dm_w, rem);
+    ow = rem - oh * args.dm_w.d;
+  }
+
+  auto issue = [&](int kt, int buf) {
+    char* G = smem + buf * STAGE;
+    char* X = G + GS * SUB;
+    const bool in = mbeg + kt * 64 + prow < mend;
+    // tap-validity bits of the lane's pixel: bit (dh + 1) * 3 + dw + 1
+    const unsigned up = oh > 0, dn = oh + 1 < args.Hi, lf = ow > 0, rt = ow + 1 < args.Wi;
+    const unsigned rowm = 0x7u & (0u - up), rowc = 0x38u, rowd = 0x1C0u & (0u - dn);
+    const unsigned colm = 0x49u & (0u - lf), colc = 0x92u, colr = 0x124u & (0u - rt);
+    const unsigned mask = in ? ((rowm | rowc | rowd) & (colm | colc | colr)) : 0u;
+    const unsigned gmask = in ? 0x10u : 0u;   // G: the pixel row only (bit 4 = centre)
+#pragma unroll
+    for (int s = 0; s < GS; ++s)
+      wblds16(gr[s], gon[s] ? sel_oob_w(gmask, 4, goff) : kWOOB, (unsigned)kt * gstep, G + s * SUB + wv * 1024);
+#pragma unroll
+    for (int s = 0; s < XS; ++s)
+      wblds16(xr[s], xon[s] ? sel_oob_w(mask, xtb[s], xoff) : kWOOB, (unsigned)kt * xstep, X + s * SUB + wv * 1024);
+    int nw = ow + args.adv_w, nh = oh + args.adv_h;
+    if (nw >= args.Wi) { nw -= args.Wi; ++nh; }
+    if (nh >= args.Hi) nh -= args.Hi;
+    ow = nw;
+    oh = nh;
+  };
+
+  f32x4_t acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+  const int nk = (mend > mbeg) ? (mend - mbeg + 63) / 64 : 0;
+#pragma unroll
+  for (int s = 0; s < NST - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int kt = 0; kt < nk; ++kt) {
+    const int after = min(NST - 2, nk - 1 - kt);
+    if constexpr (NST >= 3) {
+      if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    lds_barrier();
+    if (kt + NST - 1 < nk) issue(kt + NST - 1, (kt + NST - 1) % NST);
+    const char* G = smem + (kt % NST) * STAGE;
+    const char* X = G + GS * SUB;
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      bf16x8_t fa[FM], fb[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int c = wm * WTM + i * 16;
+        fa[i] = tr_frag<64>(G + (c >> 6) * SUB, 32 * g, c & 63, lane);
+      }
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        const int c = wn * WTN + j * 16;
+        fb[j] = tr_frag<64>(X + (c >> 6) * SUB, 32 * g, c & 63, lane);
+      }
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+  wgrad_epilogue<FM, FN, NW>(args, acc, L % (nJ * nI), split, i0 + wm * WTM, j0 + wn * WTN, lane, wave, tid,
+                             (int*)smem);
+}
+
+// --------------------------------------------------------------------------------------------
 // 3x3 weight gradient on 2-D halo tiles (bf16).
 //
 //   dW[i][tap][c] = sum_m dY[m][i] * X[m shifted by tap][c]
@@ -1055,6 +1230,14 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
         DFCSA_CHECK_LAUNCH();
         return 0;
       }
+      // buffer-descriptor kernel on 64-channel sub-images (knob 26 = 0: the pointer-DMA kernel)
+      if (g_wgrad_bd && a.simple && a.Cseg % 64 == 0 && a.Cg % 64 == 0 && !wide_j(a) &&
+          (int64_t)a.M * a.Cseg * 2 < (1ll << 31) && (int64_t)a.M * a.Cg * 2 < (1ll << 31)) {
+        dim3 gb(xcd_pad(grid.x * grid.y * splits));
+        hipLaunchKernelGGL((wgrad_bd_kernel<BI, 2>), gb, dim3(512), 0, st, a, splits);
+        DFCSA_CHECK_LAUNCH();
+        return 0;
+      }
       // 1-D grid (x = padded tile count, y = splits count carrier): see the XCD remap in the kernel
       if (BI == 64 && wide_j(a)) {
         dim3 g2(xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits), splits);
@@ -1093,6 +1276,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_wgrad_bd = 1;          // knob 26: buffer-descriptor wgrad kernel (simple geometry)
 int g_wgrad_nst64 = 0;       // knob 24: ring depth of the 64-row tiles (0 = follow knob 14)
 int g_wgrad_reduce_old = 0;  // knob 23: 1 = the element-order reduction for every split count
 int g_wgrad_halo = 0;      // knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel (off: slower so far)

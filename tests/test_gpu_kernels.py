@@ -880,3 +880,39 @@ def test_wgrad_pair_layout3(B, H, C):
     r3 = g3.permute(0, 2, 3, 1).reshape(-1, C).t() @ X[:, C:]
     assert rel(w4.view(C, -1), r4) < 1e-5 and rel(w3.view(C, -1), r3) < 1e-5
     assert rel(w4, s4) < 1e-6 and rel(w3, s3) < 1e-6
+
+
+@pytest.mark.parametrize("B,H,W,Cs,nsrc,taps,NI,NG", [(2, 20, 20, 64, 2, 9, 64, 1), (3, 14, 14, 128, 1, 9, 128, 1),
+                                                      (1, 37, 29, 64, 1, 9, 256, 1), (4, 28, 28, 64, 2, 1, 64, 2),
+                                                      (2, 56, 56, 64, 3, 1, 64, 1), (16, 7, 7, 256, 1, 9, 512, 1)])
+def test_wgrad_buffer_descriptor_kernel(B, H, W, Cs, nsrc, taps, NI, NG):
+    """The buffer-descriptor weight-gradient kernel (64-channel sub-images, knob 26) against the
+    pointer-DMA kernel: bit-identical (same images, same MFMA order), and against torch fp32."""
+    import dfcsa
+    torch.manual_seed(B * H + Cs)
+    bf = torch.bfloat16
+    xs = [q(torch.randn(B, Cs, H, W), bf) for _ in range(nsrc)]
+    gs = [q(torch.randn(B, NI, H, W) * 0.1, bf) for _ in range(NG)]
+    xh = [nhwc(x, bf) for x in xs]
+    gh = [nhwc(g, bf) for g in gs]
+    if taps == 9:
+        segs = [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for x in xh]
+    else:
+        segs = [(x, 0, 0) for x in xh]
+    k = 3 if taps == 9 else 1
+    outs = []
+    for bd in (1, 0):
+        dfcsa.set_tuning(26, bd)
+        try:
+            grads = [torch.zeros(NI, nsrc * Cs, k, k, device="cuda") for _ in range(NG)]
+            ops.conv_wgrad_into(bf, gh, NI, segs, Cs, (B, H, W), (H, W), grads, taps, nsrc * Cs, nsrc * Cs)
+            torch.cuda.synchronize()
+        finally:
+            dfcsa.set_tuning(26, 1)
+        outs.append(grads)
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+    x = torch.cat(xs, 1)
+    for g, dw in zip(gs, outs[0]):
+        ref = torch.nn.grad.conv2d_weight(x, (NI, nsrc * Cs, k, k), g, padding=k // 2)
+        assert rel(dw, ref) < 1e-5
