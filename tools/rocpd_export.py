@@ -59,8 +59,9 @@ def _per_dispatch(db, counter):
     return out
 
 
-CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel"),
-           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
+CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
+                         "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel"),
+           "conv_wgrad": ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
            # bench.py's class 4 (DFCSA_PROF_CONV_STREAM) times the streaming 1x1 GEMMs AND the fused
            # block GEMMs (dfcsa_dgrad_gate*, dfcsa_gate_fusion_fwd, dfcsa_local_attn_gate_fwd): the
            # same union here, so roofline.traffic matches the timed launches; the fused ones alone
@@ -106,9 +107,9 @@ def traffic_all(fdb, wdb, out):
 
 
 GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
-                         "small_conv_f32_kernel")),
-          ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_kernel<", "wgrad_halo_kernel", "wgrad_reduce_kernel",
-                          "small_wgrad_f32_kernel")),
+                         "small_conv_f32_kernel", "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel")),
+          ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel",
+                          "wgrad_reduce", "small_wgrad_f32_kernel")),
           ("conv1x1_stream", ("conv1x1_stream_kernel",)),
           ("fused_block_gemm (1x1 GEMMs with the gate / BN prologues and epilogues)",
            ("dgrad_gate_kernel", "gate_fusion_fwd_kernel")),
