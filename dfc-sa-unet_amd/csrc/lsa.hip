@@ -519,6 +519,147 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
   return 0;
 }
 
+// Fused pooled-attention backward for P <= 4 (N <= 16 tokens) and C % 64 == 0, one workgroup per
+// image: the column pass of the upsample backward (du = sum_h wy(pi, h) rows[h][pj]; dO = gamma du;
+// dgamma partial o . du), the softmax-attention backward (dA = dO v^T, dE = A (dA - rowsum(A dA)),
+// dq = dE k, dk = dE^T q, dv = A^T dO) in one launch instead of three (lsa_up_bwd_cols,
+// lsa_attn_bwd_rows / _cols: 256 + 2 x 256 latency-bound workgroups on the branch stream's
+// critical path).  Channels stream in blocks of 64: thread (pj, c) accumulates du for every pi
+// over the H rows in order; thread (n, m) accumulates dA[n][m] over the channel blocks.  dgamma:
+// per-image partials summed by the last workgroup in image order (deterministic).
+__global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq, int P, const float* __restrict__ rows,
+                                                           const float* __restrict__ o, const float* gamma,
+                                                           const float* __restrict__ qkv, const float* __restrict__ A,
+                                                           float* __restrict__ dqkv, float* __restrict__ gpart,
+                                                           unsigned* cnt, float* gamma_grad) {
+  constexpr int NMAX = 16, CB = 64;
+  __shared__ float dO[NMAX][CB + 1];
+  __shared__ float vch[NMAX][CB + 1];
+  __shared__ float As[NMAX][NMAX];
+  __shared__ float dE[NMAX][NMAX];
+  __shared__ float red[8];
+  __shared__ double rd[256];
+  __shared__ int flag;
+  const int b = blockIdx.x, t = threadIdx.x, N = P * P, J = 2 * Cq + C;
+  const float gm = *gamma;
+  const float* Ab = A + (size_t)b * N * N;
+  if (t < N * N) As[t / N][t % N] = Ab[t];
+  // upsample-column thread: (pj, channel cl) of a 64-channel block
+  const int pj = t / CB, cl = t % CB;
+  const bool upt = pj < P;
+  // attention pair thread: (n, m)
+  const int pn = t / NMAX, pm = t % NMAX;
+  const bool pair = pn < N && pm < N;
+  const float* qb = qkv + (size_t)b * N * J;
+  float da = 0.f, gsum = 0.f;
+  for (int cb = 0; cb < C; cb += CB) {
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+    if (upt) {
+      const float* rp = rows + ((size_t)b * H * P + pj) * C + cb + cl;
+      int h = 0;
+      for (; h + 3 < H; h += 4) {      // four rows in flight, summed in row order
+        float v[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) v[u] = rp[(size_t)(h + u) * P * C];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          int i0, i1;
+          float l0, l1;
+          bilin_axis(h + u, P, H, i0, i1, l0, l1);
+#pragma unroll
+          for (int pi = 0; pi < 4; ++pi) acc[pi] += ((i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f)) * v[u];
+        }
+      }
+      for (; h < H; ++h) {
+        int i0, i1;
+        float l0, l1;
+        bilin_axis(h, P, H, i0, i1, l0, l1);
+        const float v = rp[(size_t)h * P * C];
+#pragma unroll
+        for (int pi = 0; pi < 4; ++pi) acc[pi] += ((i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f)) * v;
+      }
+#pragma unroll
+      for (int pi = 0; pi < 4; ++pi)
+        if (pi < P) {
+          const int n = pi * P + pj;
+          gsum += o[((size_t)b * N + n) * C + cb + cl] * acc[pi];
+          dO[n][cl] = gm * acc[pi];
+        }
+    }
+    for (int e = t; e < N * CB; e += 256) vch[e / CB][e % CB] = qb[(size_t)(e / CB) * J + 2 * Cq + cb + e % CB];
+    __syncthreads();
+    if (pair) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int c = 0; c < CB; ++c) s += dO[pn][c] * vch[pm][c];
+      da += s;
+    }
+    // dv[m][c] = sum_n A[n][m] dO[n][c]: thread -> token m, four channels
+    {
+      const int m = t / 16, c0 = (t % 16) * 4;
+      if (m < N) {
+        float dv[4] = {0.f, 0.f, 0.f, 0.f};
+        for (int n = 0; n < N; ++n) {
+          const float a = As[n][m];
+#pragma unroll
+          for (int u = 0; u < 4; ++u) dv[u] += a * dO[n][c0 + u];
+        }
+        float* out = dqkv + ((size_t)b * N + m) * J + 2 * Cq + cb + c0;
+#pragma unroll
+        for (int u = 0; u < 4; ++u) out[u] = dv[u];
+      }
+    }
+    __syncthreads();
+  }
+  // dE = A (dA - rowsum(A dA)): the 16 pairs of a query row are 16 consecutive lanes
+  {
+    float w = pair ? As[pn][pm] * da : 0.f;
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) w += __shfl_xor(w, off, 16);
+    if (pair) dE[pn][pm] = As[pn][pm] * (da - w);
+  }
+  __syncthreads();
+  // dq[n][c] = sum_m dE[n][m] k[m][c]; dk[m][c] = sum_n dE[n][m] q[n][c]
+  for (int e = t; e < N * Cq; e += 256) {
+    const int n = e / Cq, c = e % Cq;
+    float dq = 0.f, dk = 0.f;
+    for (int m = 0; m < N; ++m) {
+      dq += dE[n][m] * qb[(size_t)m * J + Cq + c];
+      dk += dE[m][n] * qb[(size_t)m * J + c];
+    }
+    dqkv[((size_t)b * N + n) * J + c] = dq;
+    dqkv[((size_t)b * N + n) * J + Cq + c] = dk;
+  }
+  gsum = block_reduce_sum(gsum, red);
+  if (!gamma_grad) {
+    if (t == 0) gpart[b] = gsum;
+    return;
+  }
+  if (t == 0) st_sc1_dw(gpart + b, gsum);
+  if (!wg_last_of(cnt, gridDim.x, &flag)) return;
+  double v = 0.0;
+  for (int i = t; i < (int)gridDim.x; i += 256) v += (double)ld_sc1_f(gpart + i);
+  rd[t] = v;
+  __syncthreads();
+  for (int k = 128; k > 0; k >>= 1) {
+    if (t < k) rd[t] += rd[t + k];
+    __syncthreads();
+  }
+  if (t == 0) *gamma_grad += (float)rd[0];
+}
+
+extern "C" int dfcsa_lsa_core_bwd(int B, int H, int C, int Cq, int P, const float* rows, const float* o,
+                                  const float* gamma, const float* qkv, const float* A, float* dqkv, float* gpart,
+                                  float* gamma_grad, void* stream) {
+  if (B <= 0 || H <= 0 || P < 1 || P > 4 || C % 64 || Cq <= 0 || !gpart) return DFCSA_EINVAL;
+  unsigned* cnt = nullptr;
+  if (gamma_grad && !(cnt = dfcsa_ticket_alloc(1))) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(lsa_core_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, H, C, Cq, P, rows, o, gamma,
+                     qkv, A, dqkv, gpart, cnt, gamma_grad);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const float* o,
                                      const float* gamma, float* dO, float* gpart, int* ngpart, float* gamma_grad,
                                      void* stream) {

@@ -48,6 +48,10 @@ APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[:1] == "1",
 # bf16 blocks with C <= 128: the fusion conv's and the gate conv's weight gradients as one GEMM over
 # [fused | local | attn] (wgrad layout 3; DFCSA_PAIR_WGRAD=0: two launches)
 PAIR_WGRAD = [os.environ.get("DFCSA_PAIR_WGRAD", "1") == "1"]
+# P <= 4: the pooled-attention backward (upsample column pass + softmax attention) in one launch
+# per image (DFCSA_LSA_CORE_BWD=1).  Off: 16 workgroups cannot keep enough loads in flight for the
+# column pass (A/B 1409 vs 1434 img/s, profiles/r03b_ab_lsa_core_bwd.jsonl)
+LSA_CORE_BWD = [os.environ.get("DFCSA_LSA_CORE_BWD", "0") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -502,13 +506,19 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
     J = 2 * Cq + C
     rows = torch.empty(B * H * Pp * C, device=dev, dtype=f32)
     call("dfcsa_lsa_up_bwd_rows", dt(dtype), B, H, W, C, P(dattn), Pp, P(rows), stream())
-    dO = torch.empty((B, N, C), device=dev, dtype=f32)
-    gpart = torch.empty(B * N, device=dev, dtype=f32)
-    call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
-         P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
-    dE = torch.empty((B, N, N), device=dev, dtype=f32)
     dqkv = torch.empty((B, N, J), device=dev, dtype=f32)
-    call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
+    if Pp <= 4 and C % 64 == 0 and LSA_CORE_BWD[0]:
+        # upsample column pass + attention backward in one launch per image (dgamma in-kernel)
+        gpart = torch.empty(B, device=dev, dtype=f32)
+        call("dfcsa_lsa_core_bwd", B, H, C, Cq, Pp, P(rows), P(o), P(lsa.gamma), P(qkv), P(A), P(dqkv), P(gpart),
+             P(grad_of(lsa.gamma)), stream())
+    else:
+        dO = torch.empty((B, N, C), device=dev, dtype=f32)
+        gpart = torch.empty(B * N, device=dev, dtype=f32)
+        call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
+             P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
+        dE = torch.empty((B, N, N), device=dev, dtype=f32)
+        call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
     dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
     qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
     if _lsa_gemm_ok(C, J):

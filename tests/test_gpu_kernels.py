@@ -916,3 +916,37 @@ def test_wgrad_buffer_descriptor_kernel(B, H, W, Cs, nsrc, taps, NI, NG):
     for g, dw in zip(gs, outs[0]):
         ref = torch.nn.grad.conv2d_weight(x, (NI, nsrc * Cs, k, k), g, padding=k // 2)
         assert rel(dw, ref) < 1e-5
+
+
+@pytest.mark.parametrize("B,H,C,P", [(2, 14, 64, 4), (3, 37, 128, 4), (16, 224, 64, 4), (4, 14, 1024, 4), (2, 9, 64, 2)])
+def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
+    """dfcsa_lsa_core_bwd (one launch per image) against dfcsa_lsa_up_bwd_cols + dfcsa_lsa_attn_bwd
+    on the same upsample-backward rows: dq / dk / dv and dgamma."""
+    from dfcsa._lib import LIB  # noqa: F401
+    from dfcsa._lib import call
+    from dfcsa.ops import P as ptr, stream
+    torch.manual_seed(B + H + C)
+    N, Cq = P * P, C // 8
+    J = 2 * Cq + C
+    rows = torch.randn(B * H * P * C, device="cuda")
+    o = torch.randn(B, N, C, device="cuda")
+    gamma = torch.tensor([0.37], device="cuda")
+    qkv = torch.randn(B, N, J, device="cuda")
+    A = torch.softmax(torch.randn(B, N, N, device="cuda"), -1)
+    d1 = torch.full((B, N, J), float("nan"), device="cuda")
+    g1 = torch.zeros(1, device="cuda")
+    gp1 = torch.empty(B, device="cuda")
+    call("dfcsa_lsa_core_bwd", B, H, C, Cq, P, ptr(rows), ptr(o), ptr(gamma), ptr(qkv), ptr(A), ptr(d1), ptr(gp1),
+         ptr(g1), stream())
+    dO = torch.empty(B, N, C, device="cuda")
+    gp2 = torch.empty(B * N, device="cuda")
+    g2 = torch.zeros(1, device="cuda")
+    call("dfcsa_lsa_up_bwd_cols", B, H, C, P, ptr(rows), ptr(o), ptr(gamma), ptr(dO), ptr(gp2), None, ptr(g2),
+         stream())
+    dE = torch.empty(B, N, N, device="cuda")
+    d2 = torch.full((B, N, J), float("nan"), device="cuda")
+    call("dfcsa_lsa_attn_bwd", B, N, C, Cq, ptr(qkv), ptr(A), ptr(dO), ptr(dE), ptr(d2), stream())
+    torch.cuda.synchronize()
+    assert torch.isfinite(d1).all()
+    assert rel(d1, d2) < 1e-5
+    assert abs(g1.item() - g2.item()) <= 1e-5 * max(1.0, abs(g2.item()))
