@@ -519,126 +519,150 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
   return 0;
 }
 
-// Fused pooled-attention backward for P <= 4 (N <= 16 tokens) and C % 64 == 0, one workgroup per
-// image: the column pass of the upsample backward (du = sum_h wy(pi, h) rows[h][pj]; dO = gamma du;
-// dgamma partial o . du), the softmax-attention backward (dA = dO v^T, dE = A (dA - rowsum(A dA)),
-// dq = dE k, dk = dE^T q, dv = A^T dO) in one launch instead of three (lsa_up_bwd_cols,
-// lsa_attn_bwd_rows / _cols: 256 + 2 x 256 latency-bound workgroups on the branch stream's
-// critical path).  Channels stream in blocks of 64: thread (pj, c) accumulates du for every pi
-// over the H rows in order; thread (n, m) accumulates dA[n][m] over the channel blocks.  dgamma:
-// per-image partials summed by the last workgroup in image order (deterministic).
+// Fused pooled-attention backward, token-parallel: grid (N, B), one workgroup per (token, image)
+// as lsa_up_bwd_cols, so the column pass keeps its 256-workgroup memory parallelism.  Each
+// workgroup forms dO[n] (column pass of the upsample backward, kept in LDS and published with
+// write-through stores), runs query row n of the softmax backward (dA[n][m] = dO[n] . v[m],
+// dE[n][m] = A (dA - rowsum(A dA)), dq[n] = dE[n] k) and publishes dE[n]; the LAST workgroup of the
+// image (ticket) forms dk = dE^T q and dv = A^T dO for the image's tokens from the published rows;
+// the last of all adds dgamma (partials in token order).  Replaces lsa_up_bwd_cols +
+// lsa_attn_bwd_rows + lsa_attn_bwd_cols (three dependent launches on the backward's critical path).
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+__device__ __forceinline__ float4 ld_sc1_f4(const float* p) {
+  f4v_t v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_sc1_f4(float* p, float a, float b, float c, float d) {
+  f4v_t v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
 __global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq, int P, const float* __restrict__ rows,
                                                            const float* __restrict__ o, const float* gamma,
                                                            const float* __restrict__ qkv, const float* __restrict__ A,
-                                                           float* __restrict__ dqkv, float* __restrict__ gpart,
-                                                           unsigned* cnt, float* gamma_grad) {
-  constexpr int NMAX = 16, CB = 64;
-  __shared__ float dO[NMAX][CB + 1];
-  __shared__ float vch[NMAX][CB + 1];
-  __shared__ float As[NMAX][NMAX];
-  __shared__ float dE[NMAX][NMAX];
-  __shared__ float red[8];
+                                                           float* __restrict__ dqkv, float* dOg, float* dEg,
+                                                           float* gpart, unsigned* cnt, float* gamma_grad) {
+  __shared__ float red[256 + 8];
   __shared__ double rd[256];
+  __shared__ float dor[1024];
+  __shared__ float da[16];
+  __shared__ float dEs[16][17];
   __shared__ int flag;
-  const int b = blockIdx.x, t = threadIdx.x, N = P * P, J = 2 * Cq + C;
+  const int n = blockIdx.x, b = blockIdx.y, N = P * P, J = 2 * Cq + C, t = threadIdx.x;
+  const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
-  const float* Ab = A + (size_t)b * N * N;
-  if (t < N * N) As[t / N][t % N] = Ab[t];
-  // upsample-column thread: (pj, channel cl) of a 64-channel block
-  const int pj = t / CB, cl = t % CB;
-  const bool upt = pj < P;
-  // attention pair thread: (n, m)
-  const int pn = t / NMAX, pm = t % NMAX;
-  const bool pair = pn < N && pm < N;
   const float* qb = qkv + (size_t)b * N * J;
-  float da = 0.f, gsum = 0.f;
-  for (int cb = 0; cb < C; cb += CB) {
-    float acc[4] = {0.f, 0.f, 0.f, 0.f};
-    if (upt) {
-      const float* rp = rows + ((size_t)b * H * P + pj) * C + cb + cl;
-      int h = 0;
-      for (; h + 3 < H; h += 4) {      // four rows in flight, summed in row order
-        float v[4];
-#pragma unroll
-        for (int u = 0; u < 4; ++u) v[u] = rp[(size_t)(h + u) * P * C];
+  // ---- column pass of the upsample backward for token n (lsa_up_bwd_cols' slicing) ----
+  const int nsl = C >= 256 ? 1 : 256 / C;
+  const int cw = nsl == 1 ? 256 : C;
+  const int sl = t / cw, cl = t - sl * cw;
+  int lo, hi;
+  contrib_range(pi, P, H, lo, hi);
+  float gsum = 0.f;
+  for (int cb = 0; cb < C; cb += cw) {
+    const int c = cb + cl;
+    float sacc = 0.f;
+    if (c < C && sl < nsl) {
+      for (int h0 = lo + sl; h0 < hi; h0 += 4 * nsl) {
+        float wt[4], v[4];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
-          int i0, i1;
-          float l0, l1;
-          bilin_axis(h + u, P, H, i0, i1, l0, l1);
-#pragma unroll
-          for (int pi = 0; pi < 4; ++pi) acc[pi] += ((i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f)) * v[u];
+          const int h = h0 + u * nsl;
+          wt[u] = 0.f;
+          if (h < hi) {
+            int i0, i1;
+            float l0, l1;
+            bilin_axis(h, P, H, i0, i1, l0, l1);
+            wt[u] = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
+          }
+          v[u] = wt[u] != 0.f ? rows[(((size_t)b * H + h) * P + pj) * C + c] : 0.f;
         }
-      }
-      for (; h < H; ++h) {
-        int i0, i1;
-        float l0, l1;
-        bilin_axis(h, P, H, i0, i1, l0, l1);
-        const float v = rp[(size_t)h * P * C];
 #pragma unroll
-        for (int pi = 0; pi < 4; ++pi) acc[pi] += ((i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f)) * v;
-      }
-#pragma unroll
-      for (int pi = 0; pi < 4; ++pi)
-        if (pi < P) {
-          const int n = pi * P + pj;
-          gsum += o[((size_t)b * N + n) * C + cb + cl] * acc[pi];
-          dO[n][cl] = gm * acc[pi];
-        }
-    }
-    for (int e = t; e < N * CB; e += 256) vch[e / CB][e % CB] = qb[(size_t)(e / CB) * J + 2 * Cq + cb + e % CB];
-    __syncthreads();
-    if (pair) {
-      float s = 0.f;
-#pragma unroll 8
-      for (int c = 0; c < CB; ++c) s += dO[pn][c] * vch[pm][c];
-      da += s;
-    }
-    // dv[m][c] = sum_n A[n][m] dO[n][c]: thread -> token m, four channels
-    {
-      const int m = t / 16, c0 = (t % 16) * 4;
-      if (m < N) {
-        float dv[4] = {0.f, 0.f, 0.f, 0.f};
-        for (int n = 0; n < N; ++n) {
-          const float a = As[n][m];
-#pragma unroll
-          for (int u = 0; u < 4; ++u) dv[u] += a * dO[n][c0 + u];
-        }
-        float* out = dqkv + ((size_t)b * N + m) * J + 2 * Cq + cb + c0;
-#pragma unroll
-        for (int u = 0; u < 4; ++u) out[u] = dv[u];
+        for (int u = 0; u < 4; ++u)
+          if (wt[u] != 0.f) sacc += wt[u] * v[u];
       }
     }
-    __syncthreads();
-  }
-  // dE = A (dA - rowsum(A dA)): the 16 pairs of a query row are 16 consecutive lanes
-  {
-    float w = pair ? As[pn][pm] * da : 0.f;
-#pragma unroll
-    for (int off = 8; off > 0; off >>= 1) w += __shfl_xor(w, off, 16);
-    if (pair) dE[pn][pm] = As[pn][pm] * (da - w);
+    if (nsl > 1) {
+      if (sl < nsl) red[t] = sacc;
+      __syncthreads();
+      sacc = 0.f;
+      if (sl == 0)
+        for (int s2 = 0; s2 < nsl; ++s2) sacc += red[s2 * cw + cl];
+      __syncthreads();
+    }
+    if (sl == 0 && c < C) {
+      gsum += o[((size_t)b * N + n) * C + c] * sacc;
+      dor[c] = gm * sacc;
+    }
   }
   __syncthreads();
-  // dq[n][c] = sum_m dE[n][m] k[m][c]; dk[m][c] = sum_n dE[n][m] q[n][c]
-  for (int e = t; e < N * Cq; e += 256) {
-    const int n = e / Cq, c = e % Cq;
-    float dq = 0.f, dk = 0.f;
-    for (int m = 0; m < N; ++m) {
-      dq += dE[n][m] * qb[(size_t)m * J + Cq + c];
-      dk += dE[m][n] * qb[(size_t)m * J + c];
+  // publish dO[n] (write-through: read back by the image's last workgroup)
+  float* dOn = dOg + ((size_t)b * N + n) * C;
+  for (int c4 = t * 4; c4 < C; c4 += 1024) st_sc1_f4(dOn + c4, dor[c4], dor[c4 + 1], dor[c4 + 2], dor[c4 + 3]);
+  // ---- query row n: dA[m] = dO[n] . v[m] (wave per key, lanes over channels) ----
+  const int wave = t >> 6, lane = t & 63;
+  for (int m = wave; m < N; m += 4) {
+    const float* v = qb + (size_t)m * J + 2 * Cq;
+    float sv = 0.f;
+    for (int c = lane; c < C; c += 64) sv += dor[c] * v[c];
+    sv = wave_sum(sv);
+    if (lane == 0) da[m] = sv;
+  }
+  __syncthreads();
+  const float* An = A + ((size_t)b * N + n) * N;
+  if (t < 64) {
+    float w = t < N ? An[t] * da[t] : 0.f;
+    w = wave_sum(w);
+    if (t < N) {
+      const float g = An[t] * (da[t] - w);
+      dEs[0][t] = g;
+      st_sc1_dw(dEg + ((size_t)b * N + n) * N + t, g);
     }
-    dqkv[((size_t)b * N + n) * J + c] = dq;
-    dqkv[((size_t)b * N + n) * J + Cq + c] = dk;
+  }
+  __syncthreads();
+  for (int c = t; c < Cq; c += 256) {
+    float sq = 0.f;
+    for (int m = 0; m < N; ++m) sq += dEs[0][m] * qb[(size_t)m * J + Cq + c];
+    dqkv[((size_t)b * N + n) * J + c] = sq;
   }
   gsum = block_reduce_sum(gsum, red);
-  if (!gamma_grad) {
-    if (t == 0) gpart[b] = gsum;
-    return;
+  if (t == 0) st_sc1_dw(gpart + (size_t)b * N + n, gsum);
+  // ---- the image's last workgroup: dk = dE^T q, dv = A^T dO over its N tokens ----
+  if (wg_last_of(cnt + 1 + b, N, &flag)) {
+    if (t < N * N) dEs[t / N][t % N] = ld_sc1_f(dEg + (size_t)b * N * N + t);
+    __syncthreads();
+    for (int e = t; e < N * Cq; e += 256) {
+      const int m = e / Cq, c = e - m * Cq;
+      float sk = 0.f;
+      for (int nn = 0; nn < N; ++nn) sk += dEs[nn][m] * qb[(size_t)nn * J + c];
+      dqkv[((size_t)b * N + m) * J + Cq + c] = sk;
+    }
+    const float* Ab = A + (size_t)b * N * N;
+    for (int c4 = t * 4; c4 < C; c4 += 1024) {
+      float4 dv[16];
+#pragma unroll
+      for (int m = 0; m < 16; ++m) dv[m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int nn = 0; nn < N; ++nn) {
+        const float4 d = ld_sc1_f4(dOg + ((size_t)b * N + nn) * C + c4);
+#pragma unroll
+        for (int m = 0; m < 16; ++m)
+          if (m < N) {
+            const float a = Ab[nn * N + m];
+            dv[m].x += a * d.x; dv[m].y += a * d.y; dv[m].z += a * d.z; dv[m].w += a * d.w;
+          }
+      }
+#pragma unroll
+      for (int m = 0; m < 16; ++m)
+        if (m < N) *(float4*)(dqkv + ((size_t)b * N + m) * J + 2 * Cq + c4) = dv[m];
+    }
   }
-  if (t == 0) st_sc1_dw(gpart + b, gsum);
-  if (!wg_last_of(cnt, gridDim.x, &flag)) return;
+  if (!gamma_grad) return;
+  // ---- dgamma: the last workgroup of all sums the token partials in order ----
+  if (!wg_last_of(cnt, gridDim.x * gridDim.y, &flag)) return;
   double v = 0.0;
-  for (int i = t; i < (int)gridDim.x; i += 256) v += (double)ld_sc1_f(gpart + i);
+  const int total = gridDim.x * gridDim.y;
+  for (int i = t; i < total; i += 256) v += (double)ld_sc1_f(gpart + i);
   rd[t] = v;
   __syncthreads();
   for (int k = 128; k > 0; k >>= 1) {
@@ -649,13 +673,14 @@ __global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq,
 }
 
 extern "C" int dfcsa_lsa_core_bwd(int B, int H, int C, int Cq, int P, const float* rows, const float* o,
-                                  const float* gamma, const float* qkv, const float* A, float* dqkv, float* gpart,
-                                  float* gamma_grad, void* stream) {
-  if (B <= 0 || H <= 0 || P < 1 || P > 4 || C % 64 || Cq <= 0 || !gpart) return DFCSA_EINVAL;
-  unsigned* cnt = nullptr;
-  if (gamma_grad && !(cnt = dfcsa_ticket_alloc(1))) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(lsa_core_bwd_kernel, dim3(B), dim3(256), 0, (hipStream_t)stream, H, C, Cq, P, rows, o, gamma,
-                     qkv, A, dqkv, gpart, cnt, gamma_grad);
+                                  const float* gamma, const float* qkv, const float* A, float* dqkv, float* dO,
+                                  float* dE, float* gpart, float* gamma_grad, void* stream) {
+  if (B <= 0 || H <= 0 || P < 1 || P > 4 || C % 8 || C > 1024 || Cq <= 0 || Cq % 2 || !gpart || !dO || !dE)
+    return DFCSA_EINVAL;
+  unsigned* cnt = dfcsa_ticket_alloc(1 + B);
+  if (!cnt) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(lsa_core_bwd_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, Cq, P, rows, o,
+                     gamma, qkv, A, dqkv, dO, dE, gpart, cnt, gamma_grad);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -48,9 +48,11 @@ APPLY_PROLOGUE = [os.environ.get("DFCSA_APPLY_PROLOGUE", "01")[:1] == "1",
 # bf16 blocks with C <= 128: the fusion conv's and the gate conv's weight gradients as one GEMM over
 # [fused | local | attn] (wgrad layout 3; DFCSA_PAIR_WGRAD=0: two launches)
 PAIR_WGRAD = [os.environ.get("DFCSA_PAIR_WGRAD", "1") == "1"]
-# P <= 4: the pooled-attention backward (upsample column pass + softmax attention) in one launch
-# per image (DFCSA_LSA_CORE_BWD=1).  Off: 16 workgroups cannot keep enough loads in flight for the
-# column pass (A/B 1409 vs 1434 img/s, profiles/r03b_ab_lsa_core_bwd.jsonl)
+# P <= 4: the pooled-attention backward (upsample column pass + softmax attention) in one
+# token-parallel launch with last-arriver dk / dv (DFCSA_LSA_CORE_BWD=1).  Off: measured slower
+# than the three launches (1416 / 1420 vs 1433 / 1435 img/s; a one-workgroup-per-image version
+# 1409 vs 1434): the last arriver's write-through hand-off costs more than the launches it saves
+# (profiles/r03b_ab_lsa_core_bwd.jsonl)
 LSA_CORE_BWD = [os.environ.get("DFCSA_LSA_CORE_BWD", "0") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
@@ -507,11 +509,13 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
     rows = torch.empty(B * H * Pp * C, device=dev, dtype=f32)
     call("dfcsa_lsa_up_bwd_rows", dt(dtype), B, H, W, C, P(dattn), Pp, P(rows), stream())
     dqkv = torch.empty((B, N, J), device=dev, dtype=f32)
-    if Pp <= 4 and C % 64 == 0 and LSA_CORE_BWD[0]:
-        # upsample column pass + attention backward in one launch per image (dgamma in-kernel)
-        gpart = torch.empty(B, device=dev, dtype=f32)
-        call("dfcsa_lsa_core_bwd", B, H, C, Cq, Pp, P(rows), P(o), P(lsa.gamma), P(qkv), P(A), P(dqkv), P(gpart),
-             P(grad_of(lsa.gamma)), stream())
+    if Pp <= 4 and C % 8 == 0 and Cq % 2 == 0 and C <= 1024 and LSA_CORE_BWD[0]:
+        # upsample column pass + attention backward in one launch (dk / dv and dgamma by last arrivers)
+        dO = torch.empty((B, N, C), device=dev, dtype=f32)
+        dE = torch.empty((B, N, N), device=dev, dtype=f32)
+        gpart = torch.empty(B * N, device=dev, dtype=f32)
+        call("dfcsa_lsa_core_bwd", B, H, C, Cq, Pp, P(rows), P(o), P(lsa.gamma), P(qkv), P(A), P(dqkv), P(dO), P(dE),
+             P(gpart), P(grad_of(lsa.gamma)), stream())
     else:
         dO = torch.empty((B, N, C), device=dev, dtype=f32)
         gpart = torch.empty(B * N, device=dev, dtype=f32)

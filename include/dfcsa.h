@@ -381,11 +381,12 @@ int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* rows, const f
                           const float* gamma, float* dO, float* gpart, int* ngpart, float* gamma_grad,
                           void* stream);
 /* attention core backward -> dqkv [B][N][2Cq+C]; dE scratch [B][N][N] */
-/* P <= 4, C % 64 == 0: dfcsa_lsa_up_bwd_cols + dfcsa_lsa_attn_bwd in one launch (one workgroup per
- * image): dqkv [B][N][2Cq+C] from the upsample-backward rows; gpart [B] scratch; dgamma added to
- * *gamma_grad (last workgroup, image order). */
+/* P <= 4, C <= 1024, C % 8 == 0, Cq even: dfcsa_lsa_up_bwd_cols + dfcsa_lsa_attn_bwd in one launch (one
+ * workgroup per token and image; the image's last workgroup forms dk / dv): dqkv [B][N][2Cq+C];
+ * dO [B][N][C], dE [B][N][N], gpart [B*N] scratch; dgamma added to *gamma_grad (last workgroup). */
 int dfcsa_lsa_core_bwd(int B, int H, int C, int Cq, int P, const float* rows, const float* o, const float* gamma,
-                       const float* qkv, const float* A, float* dqkv, float* gpart, float* gamma_grad, void* stream);
+                       const float* qkv, const float* A, float* dqkv, float* dO, float* dE, float* gpart,
+                       float* gamma_grad, void* stream);
 int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv, const float* A, const float* dO,
                        float* dE, float* dqkv, void* stream);
 /* projection backward: dW[j][c] += sum_bn dqkv[bn][j]*pooled[bn][c] (w layout [2Cq+C][C]);

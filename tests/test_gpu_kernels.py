@@ -918,7 +918,8 @@ def test_wgrad_buffer_descriptor_kernel(B, H, W, Cs, nsrc, taps, NI, NG):
         assert rel(dw, ref) < 1e-5
 
 
-@pytest.mark.parametrize("B,H,C,P", [(2, 14, 64, 4), (3, 37, 128, 4), (16, 224, 64, 4), (4, 14, 1024, 4), (2, 9, 64, 2)])
+@pytest.mark.parametrize("B,H,C,P", [(2, 14, 64, 4), (3, 37, 128, 4), (16, 224, 64, 4), (4, 14, 1024, 4), (2, 9, 64, 2),
+                                     (2, 11, 16, 3), (16, 28, 512, 4)])
 def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
     """dfcsa_lsa_core_bwd (one launch per image) against dfcsa_lsa_up_bwd_cols + dfcsa_lsa_attn_bwd
     on the same upsample-backward rows: dq / dk / dv and dgamma."""
@@ -936,8 +937,11 @@ def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
     d1 = torch.full((B, N, J), float("nan"), device="cuda")
     g1 = torch.zeros(1, device="cuda")
     gp1 = torch.empty(B, device="cuda")
-    call("dfcsa_lsa_core_bwd", B, H, C, Cq, P, ptr(rows), ptr(o), ptr(gamma), ptr(qkv), ptr(A), ptr(d1), ptr(gp1),
-         ptr(g1), stream())
+    sdO = torch.empty(B, N, C, device="cuda")
+    sdE = torch.empty(B, N, N, device="cuda")
+    gp1 = torch.empty(B * N, device="cuda")
+    call("dfcsa_lsa_core_bwd", B, H, C, Cq, P, ptr(rows), ptr(o), ptr(gamma), ptr(qkv), ptr(A), ptr(d1), ptr(sdO),
+         ptr(sdE), ptr(gp1), ptr(g1), stream())
     dO = torch.empty(B, N, C, device="cuda")
     gp2 = torch.empty(B * N, device="cuda")
     g2 = torch.zeros(1, device="cuda")
