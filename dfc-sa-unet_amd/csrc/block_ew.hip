@@ -65,7 +65,22 @@ struct EwArgs {
   float* partial;
   int64_t partial_cap;  // capacity of `partial` in floats (checked against the launch grid)
   int tile_px;          // pixels per reduction tile
+  // adaptive-avg-pool backward lookups (pool_bwd_add): pixel -> (image, row, column) by
+  // multiply-shift division; pool_exact: P divides H and W (one window per pixel, area pool_inv)
+  DivMod dm_hw, dm_w, dm_ph, dm_pw;
+  int pool_exact;
+  float pool_inv;
 };
+
+// host: fill the pool-backward lookup fields for an H x W map pooled to P x P
+static void set_pool_geom(EwArgs& a) {
+  a.dm_hw = make_divmod(a.H * a.W);
+  a.dm_w = make_divmod(a.W);
+  a.pool_exact = (a.P > 0 && a.H % a.P == 0 && a.W % a.P == 0) ? 1 : 0;
+  a.dm_ph = make_divmod(a.pool_exact ? a.H / a.P : 1);
+  a.dm_pw = make_divmod(a.pool_exact ? a.W / a.P : 1);
+  a.pool_inv = a.pool_exact ? 1.f / (float)((a.H / a.P) * (a.W / a.P)) : 0.f;
+}
 
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
   float4 a = *(const float4*)p, b = *(const float4*)(p + 4);
@@ -177,8 +192,7 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
           }
           float y2[8];
           unraw(in[u][1], y2);
-          const int hw = a.H * a.W;
-          const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
+          const int b = dm_div(a.dm_hw, m), rem = m - b * a.dm_hw.d, h = dm_div(a.dm_w, rem), w = rem - h * a.W;
           int h0, h1, w0, w1;
           float lh0, lh1, lw0, lw1;
           bilin_axis(h, a.P, a.H, h0, h1, lh0, lh1);
@@ -324,9 +338,18 @@ template <> struct NSums<EW_BWD_SUM_OUT> { static constexpr int v = 1; };
 // dpooled ([B][P][P][C] fp32), i.e. the sum over the pooling windows containing (h, w) of
 // dpooled / window size (windows rows [floor(i*H/P), ceil((i+1)*H/P)) as torch's adaptive pool).
 __device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, float (&add)[8]) {
-  const int hw = a.H * a.W;
-  const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - h * a.W;
+  const int b = dm_div(a.dm_hw, m), rem = m - b * a.dm_hw.d, h = dm_div(a.dm_w, rem), w = rem - h * a.W;
   const int P = a.P;
+  if (a.pool_exact) {
+    // P divides H and W: the pixel lies in exactly one window of area (H/P)(W/P); the same
+    // 1 / area as the general path below
+    const int pi = dm_div(a.dm_ph, h), pj = dm_div(a.dm_pw, w);
+    float v[8];
+    ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) add[q] = v[q] * a.pool_inv;
+    return;
+  }
   const int pi0 = (h * P) / a.H, pi1 = ((h + 1) * P + a.H - 1) / a.H - 1;
   const int pj0 = (w * P) / a.W, pj1 = ((w + 1) * P + a.W - 1) / a.W - 1;
 #pragma unroll
@@ -1206,6 +1229,7 @@ extern "C" int dfcsa_block_local_attn(int dtype, int B, int H, int W, int C, con
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = y1; a.sc = sc1; a.sh = sh1; a.a1 = y2; a.sc2 = sc2; a.sh2 = sh2; a.tbl = o; a.scalar = gamma;
   a.o0 = y1 ? local : nullptr; a.o1 = attn; a.act = relu;
+  set_pool_geom(a);
   return launch_fwd<EW_LOCAL_ATTN>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1281,6 +1305,8 @@ extern "C" int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = dattn; a.a1 = y2; a.tbl = dpooled; a.sc = sc2; a.sh = sh2; a.mean = mean2; a.invstd = invstd2;
   a.o0 = dz2; a.partial = partial; a.partial_cap = partial_floats; a.act = relu;
+  if (P <= 0) return DFCSA_EINVAL;
+  set_pool_geom(a);
   return launch_red<EW_BWD_ATTN_ENTRY>(dtype, a, (hipStream_t)stream);
 }
 
@@ -1334,6 +1360,7 @@ extern "C" int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, c
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = dattn; a.a1 = y; a.tbl = dpooled; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.act = relu;
   a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial; a.partial_cap = bias_partial_floats;
+  set_pool_geom(a);
   return launch_red<EW_BN_BWD_APPLY_ENTRY>(dtype, a, (hipStream_t)stream);
 }
 
