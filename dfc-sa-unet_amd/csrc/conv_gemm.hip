@@ -1328,16 +1328,20 @@ int launch_halo(const HaloArgs& h, int tw, hipStream_t st) {
 
 // fp32 GEMMs with few rows (the LightSelfAttention q/k/v projections and their dgrad, M = B*P*P):
 // split-reduction 16x64 tiles (small_gemm.h), plain 1x1 store with bias and column split
-__global__ void __launch_bounds__(256) small_conv_f32_kernel(const ConvGemmArgs args) {
-  __shared__ float lds[4 * 16 * 64];
+// K >= 256: 8 waves, 4 blocks of 16 in flight per wave (the 14^2 / 28^2 projections, K = 512-1280,
+// were latency-bound at 11-25 us with 4 waves and 2 blocks in flight)
+template <int NWV, int UNR>
+__global__ void __launch_bounds__(NWV * 64) small_conv_f32_kernel(const ConvGemmArgs args) {
+  __shared__ float lds[NWV * 16 * 64];
   const float* A = (const float*)args.seg[0].ptr;
   const float* Bw = (const float*)args.Bw;
-  small_gemm_tile<false>(A, args.Cseg, Bw, args.Kpad, args.M, args.N, args.K, blockIdx.x * 16, blockIdx.y * 64, lds,
-                         [&](int m, int n, float v) {
-                           if (args.bias) v += args.bias[n];
-                           const int d = n / args.Nd, col = n - d * args.Nd;
-                           ((float*)args.dest[d])[(size_t)m * args.Nd + col] = v;
-                         });
+  auto st = [&](int m, int n, float v) {
+    if (args.bias) v += args.bias[n];
+    const int d = n / args.Nd, col = n - d * args.Nd;
+    ((float*)args.dest[d])[(size_t)m * args.Nd + col] = v;
+  };
+  small_gemm_tile<false, decltype(st), NWV, UNR>(A, args.Cseg, Bw, args.Kpad, args.M, args.N, args.K, blockIdx.x * 16,
+                                                 blockIdx.y * 64, lds, st);
 }
 
 bool small_conv_applies(const ConvGemmArgs& a) {
@@ -2290,7 +2294,9 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
   // split-reduction small-M kernel; other small problems get 64x64 tiles
   if (g_conv_cfg != 26 && small_conv_applies(a)) {
     if (t_dry_rows) { *t_dry_rows = 0; return 0; }   // (no statistics)
-    hipLaunchKernelGGL(small_conv_f32_kernel, dim3((a.M + 15) / 16, (a.N + 63) / 64), dim3(256), 0, st, a);
+    const dim3 sg((a.M + 15) / 16, (a.N + 63) / 64);
+    if (a.K >= 256 && g_small8) hipLaunchKernelGGL((small_conv_f32_kernel<8, 4>), sg, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((small_conv_f32_kernel<4, 2>), sg, dim3(256), 0, st, a);
     DFCSA_CHECK_LAUNCH();
     return 0;
   }
@@ -2613,6 +2619,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 24) { g_wgrad_nst64 = value; return 0; }
   if (knob == 25) { g_splitk = value; return 0; }
   if (knob == 26) { g_wgrad_bd = value; return 0; }
+  if (knob == 27) { g_small8 = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -15,20 +15,22 @@
 
 typedef float sg_f32x4 __attribute__((ext_vector_type(4)));
 
-template <bool TN, class Store>
+// NWV waves (blockDim = 64 NWV) split the reduction; UNR blocks of 16 are loaded before any is
+// multiplied (the K loop is latency-bound: one L2 round trip per UNR blocks).  lds: NWV*16*64 floats.
+template <bool TN, class Store, int NWV = 4, int UNR = 2>
 __device__ __forceinline__ void small_gemm_tile(const float* __restrict__ Pm, int ldp, const float* __restrict__ Qm,
                                                 int ldq, int Pn, int Qn, int R, int p0, int q0, float* lds,
                                                 Store store) {
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int l16 = lane & 15, kk = lane >> 4;
   const int nb = (R + 15) / 16;
-  const int b0 = (w * nb) / 4, b1 = ((w + 1) * nb) / 4;
+  const int b0 = (w * nb) / NWV, b1 = ((w + 1) * nb) / NWV;
   sg_f32x4 acc[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) acc[j] = {0.f, 0.f, 0.f, 0.f};
   const int p = p0 + l16;
   const bool pin = p < Pn;
-#pragma unroll 2
+#pragma unroll UNR
   for (int rb = b0; rb < b1; ++rb) {
     const int r = rb * 16 + 4 * kk;
     float pa[4], qa[4][4];
@@ -58,17 +60,22 @@ __device__ __forceinline__ void small_gemm_tile(const float* __restrict__ Pm, in
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[j] = __builtin_amdgcn_mfma_f32_16x16x4f32(pa[t], qa[j][t], acc[j], 0, 0, 0);
   }
-  // partial tiles of the 4 waves -> LDS [4][16][64], summed in wave order
+  // partial tiles of the NWV waves -> LDS [NWV][16][64], summed in wave order
 #pragma unroll
   for (int j = 0; j < 4; ++j)
 #pragma unroll
     for (int rr = 0; rr < 4; ++rr) lds[(w * 16 + kk * 4 + rr) * 64 + j * 16 + l16] = acc[j][rr];
   __syncthreads();
-#pragma unroll
-  for (int e4 = 0; e4 < 4; ++e4) {
-    const int e = tid * 4 + e4;
+  for (int e = tid; e < 1024; e += NWV * 64) {
     const int pr = e >> 6, qc = e & 63;
-    const float s = ((lds[e] + lds[1024 + e]) + lds[2048 + e]) + lds[3072 + e];
+    float s;
+    if constexpr (NWV == 4) {
+      s = ((lds[e] + lds[1024 + e]) + lds[2048 + e]) + lds[3072 + e];
+    } else {
+      s = 0.f;
+#pragma unroll
+      for (int v = 0; v < NWV; ++v) s += lds[v * 1024 + e];
+    }
     const int pp = p0 + pr, qq = q0 + qc;
     if (pp < Pn && qq < Qn) store(pp, qq, s);
   }

@@ -993,13 +993,15 @@ __device__ __forceinline__ void reduce_dst_add(int64_t e, int NI, int NJ, int la
 // fp32 weight gradient over few pixel rows (the LightSelfAttention projections, M = B*P*P): the
 // whole reduction in one launch (split over the 4 waves of a 16x64 tile, small_gemm.h), added
 // straight into the destination layout -- no split-K slab, no reduce launch
-__global__ void __launch_bounds__(256) small_wgrad_f32_kernel(const WgradArgs a) {
-  __shared__ float lds[4 * 16 * 64];
-  small_gemm_tile<true>((const float*)a.g_ptr[0], a.NI, (const float*)a.seg[0].ptr, a.Cseg, a.NI, a.NJ, a.M,
-                        blockIdx.x * 16, blockIdx.y * 64, lds, [&](int i, int j, float v) {
-                          reduce_dst_add((int64_t)i * a.NJ + j, a.NI, a.NJ, a.layout, a.ntaps, a.Ctot, a.Creal,
-                                         a.ndst, a.dst[0], a.dst[1], a.dst[2], v);
-                        });
+template <int NWV, int UNR>
+__global__ void __launch_bounds__(NWV * 64) small_wgrad_f32_kernel(const WgradArgs a) {
+  __shared__ float lds[NWV * 16 * 64];
+  auto st = [&](int i, int j, float v) {
+    reduce_dst_add((int64_t)i * a.NJ + j, a.NI, a.NJ, a.layout, a.ntaps, a.Ctot, a.Creal, a.ndst, a.dst[0], a.dst[1],
+                   a.dst[2], v);
+  };
+  small_gemm_tile<true, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, (const float*)a.seg[0].ptr, a.Cseg,
+                                                a.NI, a.NJ, a.M, blockIdx.x * 16, blockIdx.y * 64, lds, st);
 }
 
 template <int SUB>
@@ -1276,6 +1278,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 }  // namespace
 
+int g_small8 = 1;            // knob 27: 0 = the 4-wave small fp32 GEMM tiles (LightSelfAttention projections)
 int g_wgrad_bd = 1;          // knob 26: buffer-descriptor wgrad kernel (simple geometry)
 int g_wgrad_nst64 = 0;       // knob 24: ring depth of the 64-row tiles (0 = follow knob 14)
 int g_wgrad_reduce_old = 0;  // knob 23: 1 = the element-order reduction for every split count
@@ -1449,7 +1452,9 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   }
   if (d->dtype != DFCSA_DT_BF16 && a.M <= 4096 && a.ng == 1 && a.nseg == 1 && !a.seg[0].dh && !a.seg[0].dw &&
       a.stride == 1 && d->ndst > 0 && a.Ho == a.Hi && a.Wo == a.Wi && !g_wgrad_noglds_f32small) {
-    hipLaunchKernelGGL(small_wgrad_f32_kernel, dim3((a.NI + 15) / 16, (a.NJ + 63) / 64), dim3(256), 0, st, a);
+    const dim3 sg((a.NI + 15) / 16, (a.NJ + 63) / 64);
+    if (g_small8) hipLaunchKernelGGL((small_wgrad_f32_kernel<8, 4>), sg, dim3(512), 0, st, a);
+    else hipLaunchKernelGGL((small_wgrad_f32_kernel<4, 2>), sg, dim3(256), 0, st, a);
     DFCSA_CHECK_LAUNCH();
     return 0;
   }

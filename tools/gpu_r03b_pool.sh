@@ -3,5 +3,10 @@ cd $GRAFT_REPO_ROOT
 timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_zoo.py -k "block or lsa or model or attn or local or zoo" -x -q -rs --timeout 200 --timeout-method thread > gpurun_out/pool_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/pool_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-bash tools/gpu_ab_tree.sh
-for f in gpurun_out/ab_base_*.json gpurun_out/ab_new_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', d['value'], d['ms_per_step'])"; done
+B="--no-cpu-baseline --no-val-dice --no-trainer-faithful"
+for i in 1 2; do
+  (cd _ab_base && timeout -k 10 300 python bench.py $B > ../gpurun_out/ab_base_$i.json 2> ../gpurun_out/ab_base_$i.err) || exit 1
+  timeout -k 10 300 python bench.py $B > gpurun_out/ab_new_$i.json 2> gpurun_out/ab_new_$i.err || exit 1
+  DFCSA_TUNE=27=0 timeout -k 10 300 python bench.py $B > gpurun_out/ab_nosmall8_$i.json 2> gpurun_out/ab_nosmall8_$i.err || exit 1
+done
+for f in gpurun_out/ab_base_*.json gpurun_out/ab_new_*.json gpurun_out/ab_nosmall8_*.json; do python3 -c "import json;d=json.load(open('$f'));print('$f', d['value'], d['ms_per_step'])"; done
