@@ -70,6 +70,7 @@ struct EwArgs {
   DivMod dm_hw, dm_w, dm_ph, dm_pw;
   int pool_exact;
   float pool_inv;
+  float bil_sh, bil_sw;   // bilinear upsample source scales P / H, P / W (host-computed quotients)
 };
 
 // host: fill the pool-backward lookup fields for an H x W map pooled to P x P
@@ -80,6 +81,8 @@ static void set_pool_geom(EwArgs& a) {
   a.dm_ph = make_divmod(a.pool_exact ? a.H / a.P : 1);
   a.dm_pw = make_divmod(a.pool_exact ? a.W / a.P : 1);
   a.pool_inv = a.pool_exact ? 1.f / (float)((a.H / a.P) * (a.W / a.P)) : 0.f;
+  a.bil_sh = a.H > 0 ? (float)a.P / (float)a.H : 0.f;
+  a.bil_sw = a.W > 0 ? (float)a.P / (float)a.W : 0.f;
 }
 
 __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
@@ -90,6 +93,14 @@ __device__ __forceinline__ void ld8f(const float* p, float (&v)[8]) {
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + __expf(-x)); }
 
 // PyTorch upsample_bilinear2d (align_corners=False) source index/lambda for one axis.
+__device__ __forceinline__ void bilin_axis_s(int dst, int in, float scale, int& i0, int& i1, float& l0, float& l1) {
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
 __device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
   float scale = (float)in / (float)out;
   float src = scale * ((float)dst + 0.5f) - 0.5f;
@@ -195,8 +206,8 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
           const int b = dm_div(a.dm_hw, m), rem = m - b * a.dm_hw.d, h = dm_div(a.dm_w, rem), w = rem - h * a.W;
           int h0, h1, w0, w1;
           float lh0, lh1, lw0, lw1;
-          bilin_axis(h, a.P, a.H, h0, h1, lh0, lh1);
-          bilin_axis(w, a.P, a.W, w0, w1, lw0, lw1);
+          bilin_axis_s(h, a.P, a.bil_sh, h0, h1, lh0, lh1);
+          bilin_axis_s(w, a.P, a.bil_sw, w0, w1, lw0, lw1);
           const float* ob = a.tbl + (size_t)b * a.P * a.P * a.C + c0;
           float o00[8], o01[8], o10[8], o11[8];
           ld8f(ob + (size_t)(h0 * a.P + w0) * a.C, o00);
@@ -270,12 +281,11 @@ __global__ void __launch_bounds__(256) ew_fwd_kernel(const EwArgs a) {
       }
       float y2[8];
       load8<T>(A1 + off, y2);
-      const int hw = a.H * a.W;
-      const int b = m / hw, rem = m - b * hw, h = rem / a.W, w = rem - (rem / a.W) * a.W;
+      const int b = dm_div(a.dm_hw, m), rem = m - b * a.dm_hw.d, h = dm_div(a.dm_w, rem), w = rem - h * a.W;
       int h0, h1, w0, w1;
       float lh0, lh1, lw0, lw1;
-      bilin_axis(h, a.P, a.H, h0, h1, lh0, lh1);
-      bilin_axis(w, a.P, a.W, w0, w1, lw0, lw1);
+      bilin_axis_s(h, a.P, a.bil_sh, h0, h1, lh0, lh1);
+      bilin_axis_s(w, a.P, a.bil_sw, w0, w1, lw0, lw1);
       const float* ob = a.tbl + (size_t)b * a.P * a.P * a.C + c0;
       float o00[8], o01[8], o10[8], o11[8];
       ld8f(ob + (size_t)(h0 * a.P + w0) * a.C, o00);

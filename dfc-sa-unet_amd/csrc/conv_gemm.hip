@@ -561,7 +561,7 @@ conv_gemm_glds32_kernel(const ConvGemmArgs args) {
   constexpr int OSTR = BN * (int)sizeof(T) + 16;
   constexpr int SMEM = (NST * STAGE > BM * OSTR) ? NST * STAGE : BM * OSTR;
   constexpr int OPS = A_IN + B_IN;
-  static_assert(A_IN >= 1 && B_IN >= 1 && NST >= 3 && NST <= 6, "glds32 tiling");
+  static_assert(A_IN >= 1 && B_IN >= 1 && NST >= 2 && NST <= 6, "glds32 tiling");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1621,8 +1621,8 @@ struct ApplyPro {
 };
 
 // F.interpolate(bilinear, align_corners=False) source taps along one axis (= block_ew bilin_axis)
-__device__ __forceinline__ void bilin_axis_c(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
-  float scale = (float)in / (float)out;
+// scale = (float)in / (float)out, computed once on the host (the same correctly rounded quotient)
+__device__ __forceinline__ void bilin_axis_c(int dst, int in, float scale, int& i0, int& i1, float& l0, float& l1) {
   float src = scale * ((float)dst + 0.5f) - 0.5f;
   if (src < 0.f) src = 0.f;
   i0 = (int)src;
@@ -1904,6 +1904,8 @@ struct FwdPro {
   int P, H, W;
   bf16_t* out0;       // fused / local
   bf16_t* out1;       // - / attn
+  DivMod dm_hw, dm_w; // pixel -> (image, row, column) by multiply-shift
+  float sh, sw;       // bilinear source scales P / H, P / W
 };
 
 template <int PRO, int C>
@@ -1987,15 +1989,14 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     // LightSelfAttention taps of this tile's pixels, loaded before the next tile's DMA
     float ov[NITEM][4][8], lw[NITEM][4];
     if constexpr (PRO == PRO_LOCAL_ATTN) {
-      const int hw = pr_.H * pr_.W;
 #pragma unroll
       for (int h = 0; h < NITEM; ++h) {
         const int m = min(t * 64 + pr + RSTEP * h, M - 1);
-        const int b = m / hw, rem = m - b * hw, hh = rem / pr_.W, ww = rem - hh * pr_.W;
+        const int b = dm_div(pr_.dm_hw, m), rem = m - b * pr_.dm_hw.d, hh = dm_div(pr_.dm_w, rem), ww = rem - hh * pr_.W;
         int h0, h1, w0, w1;
         float lh0, lh1, lw0, lw1;
-        bilin_axis_c(hh, pr_.P, pr_.H, h0, h1, lh0, lh1);
-        bilin_axis_c(ww, pr_.P, pr_.W, w0, w1, lw0, lw1);
+        bilin_axis_c(hh, pr_.P, pr_.sh, h0, h1, lh0, lh1);
+        bilin_axis_c(ww, pr_.P, pr_.sw, w0, w1, lw0, lw1);
         const float* ob = pr_.o + (size_t)b * pr_.P * pr_.P * C + pc * 8;
         load8<float>(ob + (size_t)(h0 * pr_.P + w0) * C, ov[h][0]);
         load8<float>(ob + (size_t)(h0 * pr_.P + w1) * C, ov[h][1]);
@@ -2245,6 +2246,8 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
         case 32: return launch_glds32<128, 128, 4, 2, 5>(a, st);
         case 34: return launch_glds32<128, 64, 4, 1, 4>(a, st);
         case 35: return launch_glds32<128, 128, 4, 2, 3>(a, st);
+        case 36: return launch_glds32<128, 128, 4, 2, 2>(a, st);
+        case 37: return launch_glds32<128, 128, 2, 2, 2>(a, st);
         default: break;
       }
     }
@@ -2583,6 +2586,8 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
   std::memset(&pro, 0, sizeof(pro));
   pro.sc0 = sc1; pro.sh0 = sh1; pro.sc1 = sc2; pro.sh1 = sh2; pro.o = o; pro.gamma = gamma;
   pro.P = P; pro.H = H; pro.W = W;
+  pro.dm_hw = make_divmod(H * W); pro.dm_w = make_divmod(W);
+  pro.sh = (float)P / (float)H; pro.sw = (float)P / (float)W;
   pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
   return launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream);
 }
