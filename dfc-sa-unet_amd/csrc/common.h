@@ -45,6 +45,33 @@ template <> __device__ __forceinline__ void load8<bf16_t>(const bf16_t* p, float
   v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
   v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
 }
+// 8 elements kept raw between the load and its use (bf16: one 16-B word, 4 VGPRs instead of 8),
+// so that many loads can be in flight at a low register count
+template <typename T> struct Raw8;
+template <> struct Raw8<bf16_t> { uint4 a; };
+template <> struct Raw8<float> { uint4 a, b; };
+__device__ __forceinline__ void ld_raw8(const bf16_t* p, Raw8<bf16_t>& r) { r.a = *(const uint4*)p; }
+__device__ __forceinline__ void ld_raw8(const float* p, Raw8<float>& r) {
+  r.a = *(const uint4*)p;
+  r.b = *(const uint4*)(p + 4);
+}
+__device__ __forceinline__ void cvt8(const Raw8<bf16_t>& r, float (&v)[8]) {
+  const uint4 u = r.a;
+  v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+  v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+  v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+}
+__device__ __forceinline__ void cvt8(const Raw8<float>& r, float (&v)[8]) {
+  v[0] = __uint_as_float(r.a.x); v[1] = __uint_as_float(r.a.y); v[2] = __uint_as_float(r.a.z);
+  v[3] = __uint_as_float(r.a.w); v[4] = __uint_as_float(r.b.x); v[5] = __uint_as_float(r.b.y);
+  v[6] = __uint_as_float(r.b.z); v[7] = __uint_as_float(r.b.w);
+}
+// base + a 32-bit byte offset: lets the compiler use the scalar-base + 32-bit-offset address form
+// (one VGPR per address instead of two)
+template <typename T> __device__ __forceinline__ const T* at_bytes(const T* base, unsigned byte_off) {
+  return (const T*)((const char*)base + byte_off);
+}
 // 8 floats into LDS as two 16-B stores (p 16-B aligned).  Eight scalar stores at a lane stride of
 // 8 words hit the same bank 8 lanes at a time; the wide stores are split over the banks.
 __device__ __forceinline__ void lds_st8(float* p, const float (&v)[8]) {

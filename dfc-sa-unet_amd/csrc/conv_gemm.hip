@@ -2625,6 +2625,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 25) { g_splitk = value; return 0; }
   if (knob == 26) { g_wgrad_bd = value; return 0; }
   if (knob == 27) { g_small8 = value; return 0; }
+  if (knob == 28) { g_lsa_rows_old = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -75,6 +75,7 @@ extern int g_wgrad_reduce_old;
 extern int g_wgrad_nst64;
 extern int g_wgrad_bd;
 extern int g_small8;
+extern int g_lsa_rows_old;  // knob 28: 1 = the item-owner LightSelfAttention upsample-backward row kernel
 extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);

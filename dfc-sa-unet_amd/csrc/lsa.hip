@@ -14,11 +14,22 @@
 #include "common.h"
 #include "dfcsa_internal.h"
 
+int g_lsa_rows_old = 0;
+
 namespace {
 
 __device__ __forceinline__ int win_lo(int i, int H, int P) { return (i * H) / P; }
 __device__ __forceinline__ int win_hi(int i, int H, int P) { return ((i + 1) * H + P - 1) / P; }
 
+// scale = (float)in / (float)out (a loop computes it once: the same correctly rounded quotient)
+__device__ __forceinline__ void bilin_axis_s(int dst, int in, float scale, int& i0, int& i1, float& l0, float& l1) {
+  float src = scale * ((float)dst + 0.5f) - 0.5f;
+  if (src < 0.f) src = 0.f;
+  i0 = (int)src;
+  i1 = i0 + ((i0 < in - 1) ? 1 : 0);
+  l1 = fminf(fmaxf(src - (float)i0, 0.f), 1.f);
+  l0 = 1.f - l1;
+}
 __device__ __forceinline__ void bilin_axis(int dst, int in, int out, int& i0, int& i1, float& l0, float& l1) {
   float scale = (float)in / (float)out;
   float src = scale * ((float)dst + 0.5f) - 0.5f;
@@ -66,7 +77,9 @@ int pool_splits(int H, int P) {
   return s < 1 ? 1 : s;
 }
 
-// grid (S, N, B): row slice s of window n of image b
+// grid (S, N, B): row slice s of window n of image b.  One load in flight per lane at 45 VGPRs:
+// occupancy hides the latency (an eight-loads-in-flight variant at 108 VGPRs measured slower,
+// profiles/r03c_lsa_bench.jsonl)
 template <typename T>
 __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, const T* __restrict__ y2,
                                                        const float* __restrict__ sc, const float* __restrict__ sh,
@@ -209,6 +222,73 @@ __device__ __forceinline__ void contrib_range(int p, int in, int out, int& lo, i
   if (hi > out) hi = out;
 }
 
+// P <= PM: the same row reduction with every source column read once.  Lanes (column slice sl,
+// 8-channel chunk ck) walk the row's columns w = sl, sl + nsl, ... eight loads in flight
+// (unconditional: a load under a branch is waited for before the branch joins), each column
+// adding its two bilinear weights into acc[pj] (the other pj get weight 0).  The slices are
+// reduced by a butterfly inside the wave (power-of-two cpp < 64), then <= 4 partials per output
+// through LDS.
+template <typename T, int PM>
+__global__ void __launch_bounds__(256) lsa_up_bwd_rows_pix_kernel(int H, int W, int C, const T* __restrict__ d, int P,
+                                                                  float* __restrict__ rows) {
+  __shared__ __attribute__((aligned(16))) float red[4 * PM * 512];
+  const int h = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+  const int cpp = C >> 3, nsl = 256 / cpp;
+  const int sl = tid / cpp, ck = tid - sl * cpp, c0 = ck * 8;
+  const T* row = d + ((size_t)b * H + h) * W * C;   // 32-bit element offsets below
+  const float bsc = (float)P / (float)W;
+  float acc[PM][8];
+#pragma unroll
+  for (int j = 0; j < PM; ++j)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[j][q] = 0.f;
+  if (sl < nsl) {
+    constexpr int U = 8;
+    for (int w0 = sl; w0 < W; w0 += U * nsl) {
+      Raw8<T> r[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) ld_raw8(at_bytes(row, (unsigned)((min(w0 + u * nsl, W - 1) * C + c0) * (int)sizeof(T))), r[u]);
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int w = w0 + u * nsl;
+        float v[8];
+        cvt8(r[u], v);
+        int i0, i1;
+        float l0, l1;
+        bilin_axis_s(min(w, W - 1), P, bsc, i0, i1, l0, l1);
+        if (w >= W) l0 = l1 = 0.f;
+#pragma unroll
+        for (int j = 0; j < PM; ++j) {
+          const float wt = (i0 == j ? l0 : 0.f) + (i1 == j ? l1 : 0.f);
+#pragma unroll
+          for (int q = 0; q < 8; ++q) acc[j][q] += wt * v[q];
+        }
+      }
+    }
+  }
+  const bool bfly = cpp < 64 && (cpp & (cpp - 1)) == 0;
+  if (bfly) {
+    for (int off = cpp; off < 64; off <<= 1)
+#pragma unroll
+      for (int j = 0; j < PM; ++j)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[j][q] += __shfl_xor(acc[j][q], off);
+  }
+  const int nslot = bfly ? 4 : nsl;
+  const int slot = bfly ? (tid >> 6) : sl;
+  if (sl < nsl && (!bfly || (tid & 63) < cpp))
+#pragma unroll
+    for (int j = 0; j < PM; ++j)
+      if (j < P) lds_st8(red + ((size_t)(slot * P + j) * C + c0), acc[j]);
+  __syncthreads();
+  float* out = rows + ((size_t)b * H + h) * P * C;
+  for (int k = tid; k < P * C; k += 256) {
+    float v = 0.f;
+    for (int s2 = 0; s2 < nslot; ++s2) v += red[(size_t)s2 * P * C + k];
+    out[k] = v;
+  }
+}
+
 // grid (H, B): rows[b][h][pj][c] = sum_w wx(pj, w) * dattn[b][h][w][c].  Work items (pj, 8
 // channels) x NSL slices of the w range, so all 256 threads stream the row (P * C / 8 items alone
 // leave most of the workgroup idle at C = 64); slices are combined in a fixed order through LDS.
@@ -220,6 +300,7 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
   const int cpp = C >> 3, items = P * cpp;
   const int nsl = items >= 256 ? 1 : 256 / items;
   const T* row = d + ((size_t)b * H + h) * W * C;
+  const float bsc = (float)P / (float)W;   // bilinear source scale along W
   for (int base = 0; base < items; base += 256) {
     const int e = base + threadIdx.x % (nsl == 1 ? 256 : items), sl = nsl == 1 ? 0 : threadIdx.x / items;
     const bool on = e < items && sl < nsl;
@@ -240,7 +321,7 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
           if (w < hi) {
             int i0, i1;
             float l0, l1;
-            bilin_axis(w, P, W, i0, i1, l0, l1);
+            bilin_axis_s(w, P, bsc, i0, i1, l0, l1);
             wt[u] = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
           }
           if (wt[u] != 0.f) load8<T>(row + (size_t)w * C + c0, v[u]);
@@ -288,6 +369,7 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
   const int n = blockIdx.x, b = blockIdx.y, N = P * P;
   const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
+  const float bsc = (float)P / (float)H;   // bilinear source scale along H
   const int nsl = C >= 256 ? 1 : 256 / C;
   const int cw = nsl == 1 ? 256 : C;
   const int sl = threadIdx.x / cw, cl = threadIdx.x - sl * cw;
@@ -298,23 +380,21 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
     const int c = cb + cl;
     float s = 0.f;
     if (c < C && sl < nsl) {
-      for (int h0 = lo + sl; h0 < hi; h0 += 4 * nsl) {  // 4 independent loads in flight
-        float wt[4], v[4];
+      // 8 independent loads in flight, unconditional (rows past the range clamped, weight 0): a
+      // load under a branch is waited for before the branch joins
+      for (int h0 = lo + sl; h0 < hi; h0 += 8 * nsl) {
+        float wt[8], v[8];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-          const int h = h0 + u * nsl;
-          wt[u] = 0.f;
-          if (h < hi) {
-            int i0, i1;
-            float l0, l1;
-            bilin_axis(h, P, H, i0, i1, l0, l1);
-            wt[u] = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
-          }
-          v[u] = wt[u] != 0.f ? rows[(((size_t)b * H + h) * P + pj) * C + c] : 0.f;
+        for (int u = 0; u < 8; ++u) {
+          const int h = min(h0 + u * nsl, hi - 1);
+          int i0, i1;
+          float l0, l1;
+          bilin_axis_s(h, P, bsc, i0, i1, l0, l1);
+          wt[u] = h0 + u * nsl < hi ? (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f) : 0.f;
+          v[u] = rows[(((size_t)b * H + h) * P + pj) * C + c];
         }
 #pragma unroll
-        for (int u = 0; u < 4; ++u)
-          if (wt[u] != 0.f) s += wt[u] * v[u];
+        for (int u = 0; u < 8; ++u) s += wt[u] * v[u];
       }
     }
     if (nsl > 1) {
@@ -387,6 +467,86 @@ __global__ void __launch_bounds__(256) lsa_attn_bwd_rows_kernel(int N, int C, in
     float s = 0.f;
     for (int m = 0; m < N; ++m) s += da[m] * base[(size_t)m * J + Cq + c];
     dqkv[((size_t)b * N + n) * J + c] = s;
+  }
+}
+
+// N <= 16: the same query-row backward with the value rows staged in LDS 256 channels at a time
+// (every lane's loads of a chunk in flight at once; the generic kernel above walks the keys one
+// wave at a time, a dependent L2 round trip per key), the 16 dots accumulated by 16-lane groups
+// and reduced with a butterfly; the key rows for dq staged the same way.
+__global__ void __launch_bounds__(256) lsa_attn_bwd_rows16_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
+                                                                  const float* __restrict__ A,
+                                                                  const float* __restrict__ dO, float* __restrict__ dE,
+                                                                  float* __restrict__ dqkv) {
+  constexpr int CH = 256;
+  __shared__ __attribute__((aligned(16))) float vs[16][CH + 4];
+  __shared__ __attribute__((aligned(16))) float ds[CH];
+  __shared__ float dEs[16];
+  const int n = blockIdx.x, b = blockIdx.y, J = 2 * Cq + C, t = threadIdx.x;
+  const float* base = qkv + (size_t)b * N * J;
+  const float* dOn = dO + ((size_t)b * N + n) * C;
+  const int m = t >> 4, seg = t & 15;    // dot (n, m): lanes seg of group m
+  const float a = A[((size_t)b * N + n) * N + min(m, N - 1)];   // used for m < N only
+  float part = 0.f;
+  for (int c0 = 0; c0 < C; c0 += CH) {
+    const int cw = min(CH, C - c0);
+    __syncthreads();
+{   // unconditional (clamped) loads, all four in flight before the LDS stores
+      float4 r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = t + 256 * k, mm = e / (CH / 4), c4 = (e % (CH / 4)) * 4;
+        r[k] = *(const float4*)(base + (size_t)min(mm, N - 1) * J + 2 * Cq + c0 + min(c4, cw - 4));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = t + 256 * k;
+        *(float4*)&vs[e / (CH / 4)][(e % (CH / 4)) * 4] = r[k];
+      }
+    }
+    if (t * 4 < cw) *(float4*)&ds[t * 4] = *(const float4*)(dOn + c0 + t * 4);
+    __syncthreads();
+    if (m < N)
+      for (int c = seg; c < cw; c += 16) part += ds[c] * vs[m][c];
+  }
+#pragma unroll
+  for (int off = 8; off > 0; off >>= 1) part += __shfl_xor(part, off, 16);
+  // part (every lane of group m) = dA[n][m]; dot = sum_m A[n][m] dA[n][m] over the 16 group leaders
+  float w = (seg == 0 && m < N) ? a * part : 0.f;
+  w = wave_sum(w);
+  __shared__ float wred[4];
+  if ((t & 63) == 0) wred[t >> 6] = w;
+  __syncthreads();
+  const float dot = (wred[0] + wred[1]) + (wred[2] + wred[3]);
+  if (seg == 0 && m < N) {
+    const float g = a * (part - dot);
+    dEs[m] = g;
+    dE[((size_t)b * N + n) * N + m] = g;
+  }
+  __syncthreads();
+  // dq[n][c] = sum_m dE[n][m] k[m][c] (Cq <= 256: one staged chunk of the key rows)
+  for (int c0 = 0; c0 < Cq; c0 += CH) {
+    const int cw = min(CH, Cq - c0);
+    __syncthreads();
+{   // unconditional (clamped) loads, all four in flight before the LDS stores
+      float4 r[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = t + 256 * k, mm = e / (CH / 4), c4 = (e % (CH / 4)) * 4;
+        r[k] = *(const float4*)(base + (size_t)min(mm, N - 1) * J + Cq + c0 + min(c4, cw - 4));
+      }
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int e = t + 256 * k;
+        *(float4*)&vs[e / (CH / 4)][(e % (CH / 4)) * 4] = r[k];
+      }
+    }
+    __syncthreads();
+    for (int c = t; c < cw; c += 256) {
+      float sq = 0.f;
+      for (int mm = 0; mm < N; ++mm) sq += dEs[mm] * vs[mm][c];
+      dqkv[((size_t)b * N + n) * J + c0 + c] = sq;
+    }
   }
 }
 
@@ -509,7 +669,17 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
                                      void* stream) {
   if (C % 8) return DFCSA_EINVAL;
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DFCSA_DT_BF16)
+  // the column-owner kernel: P <= 4 and nslot * P * C <= 4 * 4 * 512 LDS floats
+  const int cpp = C / 8, nsl = cpp <= 256 ? 256 / cpp : 0;
+  const bool bfly = cpp < 64 && (cpp & (cpp - 1)) == 0;
+  if (P <= 4 && nsl > 0 && (size_t)(bfly ? 4 : nsl) * P * C <= 4 * 4 * 512 && !g_lsa_rows_old) {
+    if (dtype == DFCSA_DT_BF16)
+      hipLaunchKernelGGL((lsa_up_bwd_rows_pix_kernel<bf16_t, 4>), dim3(H, B), dim3(256), 0, st, H, W, C,
+                         (const bf16_t*)dattn, P, rows);
+    else
+      hipLaunchKernelGGL((lsa_up_bwd_rows_pix_kernel<float, 4>), dim3(H, B), dim3(256), 0, st, H, W, C,
+                         (const float*)dattn, P, rows);
+  } else if (dtype == DFCSA_DT_BF16)
     hipLaunchKernelGGL(lsa_up_bwd_rows_kernel<bf16_t>, dim3(H, B), dim3(256), 0, st, H, W, C, (const bf16_t*)dattn,
                        P, rows);
   else
@@ -552,6 +722,7 @@ __global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq,
   const int n = blockIdx.x, b = blockIdx.y, N = P * P, J = 2 * Cq + C, t = threadIdx.x;
   const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
+  const float bsc = (float)P / (float)H;
   const float* qb = qkv + (size_t)b * N * J;
   // ---- column pass of the upsample backward for token n (lsa_up_bwd_cols' slicing) ----
   const int nsl = C >= 256 ? 1 : 256 / C;
@@ -573,7 +744,7 @@ __global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq,
           if (h < hi) {
             int i0, i1;
             float l0, l1;
-            bilin_axis(h, P, H, i0, i1, l0, l1);
+            bilin_axis_s(h, P, bsc, i0, i1, l0, l1);
             wt[u] = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
           }
           v[u] = wt[u] != 0.f ? rows[(((size_t)b * H + h) * P + pj) * C + c] : 0.f;
@@ -701,7 +872,10 @@ extern "C" int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv,
                                   float* dE, float* dqkv, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   size_t shm1 = (size_t)(C + N + 8) * sizeof(float);
-  hipLaunchKernelGGL(lsa_attn_bwd_rows_kernel, dim3(N, B), dim3(256), shm1, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  if (N <= 16 && C % 4 == 0 && Cq % 4 == 0)
+    hipLaunchKernelGGL(lsa_attn_bwd_rows16_kernel, dim3(N, B), dim3(256), 0, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  else
+    hipLaunchKernelGGL(lsa_attn_bwd_rows_kernel, dim3(N, B), dim3(256), shm1, st, N, C, Cq, qkv, A, dO, dE, dqkv);
   DFCSA_CHECK_LAUNCH();
   size_t shm2 = (size_t)(2 * N) * sizeof(float);
   hipLaunchKernelGGL(lsa_attn_bwd_cols_kernel, dim3(N, B), dim3(256), shm2, st, N, C, Cq, qkv, A, dO, dE, dqkv);

@@ -705,6 +705,14 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 9: 1 = generic (non-MFMA) full-resolution attention kernels (coverage tests).
  * knob 19: smallest M routed to the 2-D halo-tile 3x3 conv kernel (0 = never).
  * knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel, 0 = row tiles.
+ * knob 21: 1 = divide-per-stage X addressing in the weight-gradient tile kernel.
+ * knob 22: halo-tile conv variant (0 = by N, 1 = BN 64 always).
+ * knob 23: 1 = element-order weight-gradient split reduction for every split count.
+ * knob 24: LDS-DMA ring depth of the 64-row weight-gradient tiles (0 = follow knob 14).
+ * knob 25: 0 = never split K in the forward / dgrad implicit GEMM.
+ * knob 26: 0 = pointer-DMA weight-gradient kernel instead of the buffer-descriptor one.
+ * knob 27: 0 = 4-wave small fp32 GEMM tiles (LightSelfAttention projections).
+ * knob 28: 1 = item-owner LightSelfAttention upsample-backward row kernel.
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -954,3 +954,47 @@ def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
     assert torch.isfinite(d1).all()
     assert rel(d1, d2) < 1e-5
     assert abs(g1.item() - g2.item()) <= 1e-5 * max(1.0, abs(g2.item()))
+
+
+def _bilinear_matrix(out, inp):
+    """[out][inp] weights of F.interpolate(bilinear, align_corners=False) along one axis."""
+    eye = torch.eye(inp, dtype=torch.float64).view(inp, 1, inp, 1)
+    return F.interpolate(eye, size=(out, 1), mode="bilinear", align_corners=False)[:, 0, :, 0].T
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,W,C,P", [(16, 224, 224, 64, 4), (2, 14, 14, 1024, 4), (3, 28, 28, 512, 4),
+                                       (2, 13, 17, 24, 3), (2, 9, 11, 192, 2), (1, 7, 5, 2048, 4), (2, 10, 6, 8, 1),
+                                       (2, 20, 12, 64, 8)])
+def test_lsa_up_bwd_rows_and_pool(B, H, W, C, P, dtype):
+    """The column-owner upsample-backward row kernel (and the item-owner one, knob 28) against the
+    transposed bilinear matrix, and the BN+ReLU adaptive average pool against PyTorch (fp64 CPU)."""
+    import dfcsa
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P as ptr, stream
+    torch.manual_seed(H * W + C)
+    d = torch.randn(B, H, W, C).to(dtype)
+    ref = torch.einsum("bhwc,wp->bhpc", d.double(), _bilinear_matrix(W, P))
+    dc = d.cuda()
+    for old in (0, 1):
+        dfcsa.set_tuning(28, old)
+        try:
+            rows = torch.full((B * H * P * C,), float("nan"), device="cuda")
+            call("dfcsa_lsa_up_bwd_rows", ops.dt(dtype), B, H, W, C, ptr(dc), P, ptr(rows), stream())
+            torch.cuda.synchronize()
+        finally:
+            dfcsa.set_tuning(28, 0)
+        assert rel(rows.view(B, H, P, C), ref) < 1e-6, old
+    sc = torch.rand(C) + 0.5
+    sh = torch.randn(C) * 0.3
+    scc, shc = sc.cuda(), sh.cuda()   # kept alive across the launches
+    S = LIB.dfcsa_lsa_pool_splits(H, P)
+    part = torch.full((B * P * P * S * C,), float("nan"), device="cuda")
+    pooled = torch.empty(B, P * P, C, device="cuda")
+    call("dfcsa_lsa_pool", ops.dt(dtype), B, H, W, C, ptr(dc), ptr(scc), ptr(shc), P, 1, ptr(part),
+         stream())
+    call("dfcsa_lsa_pooled", B, H, W, C, P, ptr(part), ptr(pooled), stream())
+    torch.cuda.synchronize()
+    act = torch.relu(d.double() * sc.double() + sh.double()).permute(0, 3, 1, 2)
+    pref = F.adaptive_avg_pool2d(act, P).permute(0, 2, 3, 1).reshape(B, P * P, C)
+    assert rel(pooled, pref) < 1e-6

@@ -1,9 +1,9 @@
 mkdir -p gpurun_out
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_zoo.py tests/test_gpu_parity2.py -k "block or lsa or model or attn or local or zoo or cfg2" -x -q -rs --timeout 200 --timeout-method thread > gpurun_out/bil_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_zoo.py tests/test_gpu_parity2.py -k "block or lsa or model or attn or local or zoo or cfg2 or fra or pool" -x -q -rs --timeout 200 --timeout-method thread > gpurun_out/bil_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/bil_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
-GEMM_SHAPES="L1 3x3,L2 3x3 fwd,L2 3x3 dgrad,L4 3x3 fwd" GEMM_CHECK=1 timeout -k 10 300 python3 tools/gemm_bench.py 14,36,37,0 > gpurun_out/glds32b.jsonl 2> gpurun_out/glds32b.err || exit 1
+
 B="--no-cpu-baseline --no-val-dice --no-trainer-faithful"
 for i in 1 2; do
   (cd _ab_base && timeout -k 10 300 python bench.py $B > ../gpurun_out/ab_base_$i.json 2> ../gpurun_out/ab_base_$i.err) || exit 1
