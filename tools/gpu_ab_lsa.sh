@@ -2,7 +2,7 @@
 # the tree A/B (working tree against _ab_base/).
 mkdir -p gpurun_out
 cd $GRAFT_REPO_ROOT
-timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_zoo.py tests/test_gpu_parity2.py -k "block or lsa or model or attn or local or zoo or cfg2 or fra or pool" -x -q -rs --timeout 200 --timeout-method thread > gpurun_out/lsa_tests.log 2>&1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_model.py tests/test_gpu_kernels.py tests/test_gpu_zoo.py tests/test_gpu_parity2.py -k "block or lsa or model or attn or local or zoo or cfg2 or fra or pool or entry" -x -q -rs --timeout 200 --timeout-method thread > gpurun_out/lsa_tests.log 2>&1
 rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/lsa_tests.log
 if [ $rc -ne 0 ]; then exit $rc; fi
 bash tools/gpu_ab_ktrace.sh || exit 1
