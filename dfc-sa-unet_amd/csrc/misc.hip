@@ -434,11 +434,19 @@ __device__ __forceinline__ void store_as(void* out, int64_t i, int dtype, float 
 __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* __restrict__ tab, int n) {
   __shared__ float tile[64][65];
   const int64_t task = blockIdx.x;
-  int lo = 0, hi = n - 1;  // last entry with start <= task
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (tab[mid].start <= task) lo = mid; else hi = mid - 1;
+  // last entry with start <= task = (number of entries with start <= task) - 1 (starts ascend,
+  // start[0] = 0): every lane tests four entries per 256, all loads in flight, counted by ballot
+  // (a binary search was eight dependent L2 round trips per workgroup)
+  int cnt = 0;
+  const int lane64 = threadIdx.x & 63;
+  for (int base = 0; base < n; base += 256) {
+    int64_t st[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) st[u] = tab[min(base + u * 64 + lane64, n - 1)].start;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) cnt += __popcll(__ballot(base + u * 64 + lane64 < n && st[u] <= task));
   }
+  const int lo = cnt - 1;
   const dfcsa_pack_entry& t = tab[lo];
   const int64_t tl = task - t.start;
   if (tl >= t.count) return;
@@ -446,18 +454,46 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
   const int tid = threadIdx.x;
   switch (t.kind) {
     case DFCSA_PACK_ROWS: {
-      // out[(row0 + co)*Kpad + tap*Cpad + ci] = w[co][ci][tap]; the source row is contiguous
+      // out[(row0 + co)*Kpad + tap*Cpad + ci] = w[co][ci][tap].  The task's rows (or, for rows
+      // longer than 4096 floats, one row's input-channel chunk) are a contiguous source block of
+      // <= 4096 floats: it is staged in LDS by sixteen unconditional loads per lane, all in flight
+      // (clamped index past the end), and written in output order (consecutive ci: coalesced),
+      // reading LDS at a stride of ntaps.
       const int Cout = a[0], Cin = a[1], ntaps = a[2], Cpad = a[3], Kpad = a[4], row0 = a[5], per = a[6];
       const int nrow = Cin * ntaps;
-      for (int r = 0; r < per; ++r) {
-        const int co = (int)tl * per + r;
-        if (co >= Cout) break;
-        const float* src = t.w0 + (size_t)co * nrow;
-        const int64_t ob = (int64_t)(row0 + co) * Kpad;
-        for (int e = tid; e < nrow; e += 256) {
-          const int tap = e / Cin, ci = e - tap * Cin;
-          store_as(t.out, ob + tap * Cpad + ci, t.dtype, src[ci * ntaps + tap]);
+      const int co0 = (int)tl * per, nr = min(per, Cout - co0);
+      const bool vec = t.dtype == DFCSA_DT_BF16 && Cin % 8 == 0 && Cpad % 8 == 0 && Kpad % 8 == 0 &&
+                       ((uintptr_t)t.out & 15) == 0;
+      const int ccmax = nrow <= 4096 ? Cin : max(vec ? 8 : 1, (4096 / ntaps) & (vec ? ~7 : ~0));
+      float* buf = &tile[0][0];   // 4160 floats
+      const float* __restrict__ w = t.w0;
+      for (int c0 = 0; c0 < Cin; c0 += ccmax) {
+        const int cc = min(ccmax, Cin - c0), rl = cc * ntaps, n = nr * rl;   // n <= 4096
+        const float* __restrict__ src = w + (size_t)co0 * nrow + (size_t)c0 * ntaps;
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = src[min(tid + u * 256, n - 1)];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (tid + u * 256 < n) buf[tid + u * 256] = v[u];
+        __syncthreads();
+        if (vec) {
+          // 8 consecutive ci of one tap per lane: one 16-B store (cc % 8 == 0)
+          for (int o = tid * 8; o < n; o += 256 * 8) {
+            const int r = o / rl, rem = o - r * rl, tap = rem / cc, ci = rem - tap * cc;
+            float v8[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) v8[j] = buf[r * rl + (ci + j) * ntaps + tap];
+            store8<bf16_t>((bf16_t*)t.out + (int64_t)(row0 + co0 + r) * Kpad + tap * Cpad + c0 + ci, v8);
+          }
+        } else {
+          for (int o = tid; o < n; o += 256) {
+            const int r = o / rl, rem = o - r * rl, tap = rem / cc, ci = rem - tap * cc;
+            store_as(t.out, (int64_t)(row0 + co0 + r) * Kpad + tap * Cpad + c0 + ci, t.dtype,
+                     buf[r * rl + ci * ntaps + tap]);
+          }
         }
+        __syncthreads();
       }
       break;
     }
