@@ -1368,7 +1368,10 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
 // workgroup, and the small LDS footprint lets several workgroups share a CU.  Waves split the
 // columns, so per-column BatchNorm partial sums of a 64-row tile need no cross-wave reduction.
 // --------------------------------------------------------------------------------------------
-template <int NWC, int KP, bool ACC>
+// SH: segments with (dh, dw) pixel shifts (a 3x3 conv whose 9 * Cin fits K <= 256, i.e. the
+// first layer: Cin = 8, K = 72): each 8-channel chunk's row is the shifted pixel of its segment,
+// the zero page outside the image; Ho = Hi, Wo = Wi, stride 1.
+template <int NWC, int KP, bool ACC, bool SH = false>
 __global__ void __launch_bounds__(256)
 conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   using T = bf16_t;
@@ -1415,22 +1418,44 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   // pointers once (a per-lane index into the kernel-argument segment table is a vector load that
   // the compiler follows with a full vmcnt drain -- not inside the streaming loop).
   const T* a_src[2 * KS];
+  int a_dh[SH ? 2 * KS : 1], a_dw[SH ? 2 * KS : 1];
 #pragma unroll
   for (int i = 0; i < 2 * KS; ++i) {
     const int k = (i >> 1) * 64 + cchunk * 8;
     a_src[i] = nullptr;
+    if constexpr (SH) { a_dh[i] = 0; a_dw[i] = 0; }
     if (k < K) {
       const int seg = dm_div(args.dm_cseg, k);
       a_src[i] = (const T*)args.seg[seg].ptr + (k - seg * args.Cseg);
+      if constexpr (SH) { a_dh[i] = args.seg[seg].dh; a_dw[i] = args.seg[seg].dw; }
     }
   }
   auto issue = [&](int t, int slot) {
     char* base = smem + slot * SLOT;
+    // SH: (image, row, column) of this lane's two A rows of the tile
+    int pb[2] = {0, 0}, ph[2] = {0, 0}, pw[2] = {0, 0};
+    if constexpr (SH) {
+#pragma unroll
+      for (int r2 = 0; r2 < 2; ++r2) {
+        const int m = t * 64 + (r2 * 4 + wave) * 8 + rsub;
+        pb[r2] = dm_div(args.dm_hw, m);
+        const int rem = m - pb[r2] * args.dm_hw.d;
+        ph[r2] = dm_div(args.dm_w, rem);
+        pw[r2] = rem - ph[r2] * args.dm_w.d;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < 2 * KS; ++i) {
       const int st = i >> 1, rb = (i & 1) * 4 + wave;
       const int m = t * 64 + rb * 8 + rsub;
-      const void* src = (m < M && a_src[i]) ? (const void*)(a_src[i] + (size_t)m * args.Cseg) : zero;
+      const void* src = zero;
+      if constexpr (SH) {
+        const int ih = ph[i & 1] + a_dh[i], iw = pw[i & 1] + a_dw[i];
+        if (m < M && a_src[i] && ih >= 0 && ih < args.Hi && iw >= 0 && iw < args.Wi)
+          src = (const void*)(a_src[i] + ((size_t)(pb[i & 1] * args.Hi + ih) * args.Wi + iw) * args.Cseg);
+      } else {
+        if (m < M && a_src[i]) src = (const void*)(a_src[i] + (size_t)m * args.Cseg);
+      }
       glds16(src, base + st * IMG + rb * 8 * 128);
     }
   };
@@ -2147,7 +2172,12 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   if (gx > mtiles) gx = mtiles;
   if (t_dry_rows) { *t_dry_rows = gx; return 0; }   // one statistics row per workgroup column
   if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
-  if (a.accumulate)
+  bool shifted = false;
+  for (int i = 0; i < a.nseg; ++i) shifted = shifted || a.seg[i].dh || a.seg[i].dw;
+  if (shifted) {
+    if (a.accumulate) return DFCSA_EINVAL;
+    hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, false, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
+  } else if (a.accumulate)
     hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
   else
     hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, false>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
@@ -2156,10 +2186,13 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
 }
 
 // the streaming kernel serves 1x1 (no shift, stride 1, plain store) bf16 GEMMs with K <= 256
+// (and, knob 30 on, the shifted-segment 3x3 with 9 * Cin <= 256: the first layer, Cin = 8)
+int g_stream_shift = 1;   // knob 30
 bool stream_applies(const ConvGemmArgs& a) {
   if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return false;
-  for (int i = 0; i < a.nseg; ++i)
-    if (a.seg[i].dh || a.seg[i].dw) return false;
+  bool shifted = false;
+  for (int i = 0; i < a.nseg; ++i) shifted = shifted || a.seg[i].dh || a.seg[i].dw;
+  if (shifted && (!g_stream_shift || a.accumulate || a.Cseg % 8)) return false;
   return a.Ho == a.Hi && a.Wo == a.Wi;
 }
 
@@ -2626,6 +2659,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 26) { g_wgrad_bd = value; return 0; }
   if (knob == 27) { g_small8 = value; return 0; }
   if (knob == 28) { g_lsa_rows_old = value; return 0; }
+  if (knob == 30) { g_stream_shift = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

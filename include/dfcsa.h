@@ -713,6 +713,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 26: 0 = pointer-DMA weight-gradient kernel instead of the buffer-descriptor one.
  * knob 27: 0 = 4-wave small fp32 GEMM tiles (LightSelfAttention projections).
  * knob 28: 1 = item-owner LightSelfAttention upsample-backward row kernel.
+ * knob 30: 0 = no streaming kernel for shifted-segment (3x3, 9 * Cin <= 256) convs.
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -488,6 +488,42 @@ def test_conv1x1_streaming_kernel(Cs, nsrc, C, nd, acc, bias, stats, force):
         assert rel(s[1], (a * a).sum((0, 2, 3))) < 1e-3
 
 
+@pytest.mark.parametrize("stream_shift", [1, 0])
+@pytest.mark.parametrize("B,H,W", [(3, 150, 147), (2, 224, 224)])
+def test_first_layer_3x3_streaming(B, H, W, stream_shift):
+    """The first-layer 3x3 conv (Cin = 3 padded to 8, K = 72): the streaming GEMM with shifted
+    segments (knob 30 on) and the tile kernel (off) against torch fp32 on the bf16-rounded
+    operands, bias and BN partial sums, ragged last tile and image borders."""
+    import dfcsa
+    torch.manual_seed(H + W)
+    dtype = torch.bfloat16
+    x = q(torch.randn(B, 3, H, W), dtype)
+    w = q(torch.randn(64, 3, 3, 3) * 0.2, dtype)
+    b = torch.randn(64)
+    ref = F.conv2d(x, w, b, padding=1)
+    xp = torch.zeros(B, H, W, 8, dtype=dtype, device="cuda")
+    xp[..., :3] = nhwc(x, dtype)
+    w8 = torch.zeros(64, 8, 3, 3)
+    w8[:, :3] = w
+    Kp = ops.rup(9 * 8, ops.KALIGN)
+    wp = ops.pack_conv_w(dtype, w8.cuda(), 8, Kp)
+    M = B * H * W
+    out = torch.empty((B, H, W, 64), dtype=dtype, device="cuda")
+    st = torch.full((ops.ntiles_gemm(M) * 2 * 64,), float("nan"), device="cuda")
+    segs = [(xp, kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+    dfcsa.set_tuning(30, stream_shift)
+    try:
+        rows = ops.conv_gemm(dtype, segs, 8, (B, H, W), (H, W), wp, Kp, 64, [out], 64, bias=b.cuda(), stats=st)
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(30, 1)
+    assert rel(nchw(out), ref) < 1e-2
+    s = st[:rows * 2 * 64].view(-1, 2, 64).sum(0).cpu()
+    a = ref - b.view(1, -1, 1, 1)
+    assert rel(s[0], a.sum((0, 2, 3))) < 1e-3
+    assert rel(s[1], (a * a).sum((0, 2, 3))) < 1e-3
+
+
 @pytest.mark.parametrize("M,C", [(65536 + 37, 64), (4 * 28 * 28, 128), (2 * 56 * 56 + 5, 256), (300, 64),
                                  (16 * 224 * 224, 64), (16 * 112 * 112, 128), (16 * 56 * 56, 256)])
 def test_dgrad_gate_fused_equals_gemm_plus_gate(M, C):
