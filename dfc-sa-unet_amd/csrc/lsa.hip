@@ -551,6 +551,46 @@ __global__ void __launch_bounds__(256) lsa_attn_bwd_rows16_kernel(int N, int C, 
 }
 
 // grid (N, B): key/value row m -> dk[b][m][:], dv[b][m][:]
+// N <= 16: the same key-column backward with the n loop unrolled to 16 unconditional loads in
+// flight per output (rows past N clamped, weight 0 -- the same products summed in the same order;
+// the generic loop issued them four at a time)
+__global__ void __launch_bounds__(256) lsa_attn_bwd_cols16_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
+                                                                  const float* __restrict__ A,
+                                                                  const float* __restrict__ dO,
+                                                                  const float* __restrict__ dE,
+                                                                  float* __restrict__ dqkv) {
+  __shared__ float de[16], ac[16];
+  const int m = blockIdx.x, b = blockIdx.y, J = 2 * Cq + C;
+  if (threadIdx.x < 16) {
+    const int n = threadIdx.x, nc = min(n, N - 1);
+    const float dv = dE[((size_t)b * N + nc) * N + m], av = A[((size_t)b * N + nc) * N + m];
+    de[n] = n < N ? dv : 0.f;
+    ac[n] = n < N ? av : 0.f;
+  }
+  __syncthreads();
+  const float* base = qkv + (size_t)b * N * J;
+  const float* dOb = dO + (size_t)b * N * C;
+  float* out = dqkv + ((size_t)b * N + m) * J;
+  for (int c = threadIdx.x; c < Cq; c += 256) {
+    float v[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) v[n] = base[(size_t)min(n, N - 1) * J + c];
+    float s = 0.f;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) s += de[n] * v[n];
+    out[Cq + c] = s;
+  }
+  for (int c = threadIdx.x; c < C; c += 256) {
+    float v[16];
+#pragma unroll
+    for (int n = 0; n < 16; ++n) v[n] = dOb[(size_t)min(n, N - 1) * C + c];
+    float s = 0.f;
+#pragma unroll
+    for (int n = 0; n < 16; ++n) s += ac[n] * v[n];
+    out[2 * Cq + c] = s;
+  }
+}
+
 __global__ void __launch_bounds__(256) lsa_attn_bwd_cols_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
                                                                 const float* __restrict__ A,
                                                                 const float* __restrict__ dO,
@@ -878,7 +918,10 @@ extern "C" int dfcsa_lsa_attn_bwd(int B, int N, int C, int Cq, const float* qkv,
     hipLaunchKernelGGL(lsa_attn_bwd_rows_kernel, dim3(N, B), dim3(256), shm1, st, N, C, Cq, qkv, A, dO, dE, dqkv);
   DFCSA_CHECK_LAUNCH();
   size_t shm2 = (size_t)(2 * N) * sizeof(float);
-  hipLaunchKernelGGL(lsa_attn_bwd_cols_kernel, dim3(N, B), dim3(256), shm2, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  if (N <= 16)
+    hipLaunchKernelGGL(lsa_attn_bwd_cols16_kernel, dim3(N, B), dim3(256), 0, st, N, C, Cq, qkv, A, dO, dE, dqkv);
+  else
+    hipLaunchKernelGGL(lsa_attn_bwd_cols_kernel, dim3(N, B), dim3(256), shm2, st, N, C, Cq, qkv, A, dO, dE, dqkv);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
