@@ -224,6 +224,10 @@ def main():
     ap.add_argument("--no-trainer-faithful", action="store_true", help="skip the Trainer.train_epoch rate")
     ap.add_argument("--sync-bn", action="store_true",
                     help="opt-in SyncBatchNorm over the ranks (default: per-replica BN, standard DDP)")
+    ap.add_argument("--ddp-rehearsal", action="store_true",
+                    help="one GPU: run the N > 1 code path (RCCL group of world size 1, bucket reducer, "
+                         "graph-captured collectives, teardown) -- the multi-GPU path's test on a one-GPU box")
+    ap.add_argument("--bucket-mb", type=float, default=32.0)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -231,11 +235,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
+    ddp = world > 1 or args.ddp_rehearsal
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
+    elif ddp:   # world size 1: an in-process store, no rendezvous
+        dist.init_process_group("nccl", store=dist.HashStore(), rank=0, world_size=1, device_id=dev)
 
     import dfcsa._lib as L
-    from dfcsa.ddp import GradBucketReducer, shard_rows
+    from dfcsa.ddp import GradBucketReducer, capture_step, shard_rows, shutdown
     from dfcsa.loss import bce_dice, sigmoid
     from dfcsa.optim import FusedSGD
     from models.model_factory import ModelFactory
@@ -264,11 +271,11 @@ def main():
     t = tg[lo:hi].to(dev)
     del xg, tg
 
-    if world > 1 and args.sync_bn:
+    if ddp and args.sync_bn:
         from dfcsa import ops as dfops
         dfops.set_sync_bn()
     model(x)  # materialise the flat parameter/gradient storage and packed operands first
-    reducer = GradBucketReducer(model) if world > 1 else None
+    reducer = GradBucketReducer(model, bucket_mb=args.bucket_mb) if ddp else None
     scale = reducer.grad_scale if reducer else 1.0
 
     def step():
@@ -283,7 +290,7 @@ def main():
         return stats
 
     def barrier():
-        if world > 1:
+        if ddp:
             dist.barrier()
 
     for _ in range(args.warmup):
@@ -301,11 +308,9 @@ def main():
         with torch.cuda.stream(side):
             step()
         torch.cuda.current_stream().wait_stream(side)
-        graph = torch.cuda.CUDAGraph()
         try:
-            with torch.cuda.graph(graph):
-                gstats = step()
-            torch.cuda.synchronize()
+            # thread_local capture with the NCCL watchdog drained first (dfcsa.ddp.capture_step)
+            graph, gstats = capture_step(step)
         except RuntimeError as e:  # e.g. a collective the runtime cannot capture: time eager steps
             log(f"[rank {rank}] HIP graph capture failed ({e}); timing eager steps")
             graph = None
@@ -325,7 +330,7 @@ def main():
     torch.cuda.synchronize()
     barrier()
     el = time.perf_counter() - t0
-    if world > 1:
+    if ddp:
         te = torch.tensor([el], device=dev, dtype=torch.float64)
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         el = te.item()
@@ -421,14 +426,15 @@ def main():
                "config": {"workload": (f"DFC-SA-Res P={args.pool} features 64..512 {S}x{S} train step" if headline
                                        else f"{spec['label']} {S}x{S} train step"),
                           "per_gpu_batch": B, "global_batch": B * world, "img": S, "pool_size": args.pool,
-                          "parallelism": f"dp{world}", "sync_bn": bool(world > 1 and args.sync_bn), "final_loss": round(final_loss, 5),
+                          "parallelism": f"dp{world}", "sync_bn": bool(ddp and args.sync_bn), "final_loss": round(final_loss, 5),
+                          "ddp_path": ddp,
                           "model_tflops": round(value * gflop / 1e3, 2) if gflop else None},
                "roofline": roof, "step_roofline": step_roof, "trainer_faithful": faithful,
                "cpu_baseline": cpu, "val_dice": vdice}
         print(json.dumps(out), flush=True)
-    if world > 1:
-        dist.barrier()
-        dist.destroy_process_group()
+    # release the step graph (its RCCL kernels reference the communicator) before the process
+    # group is destroyed; then every rank exits 0
+    shutdown(graph)
 
 
 if __name__ == "__main__":

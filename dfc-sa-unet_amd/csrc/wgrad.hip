@@ -1421,6 +1421,8 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
     wgrad_tile(a.NI, a.NJ, d->dtype, &BI, &BJ);
     const int tiles = ((a.NI + BI - 1) / BI) * ((a.NJ + BJ - 1) / BJ);
     if (tiles > kCntRing) return DFCSA_EINVAL;
+    // the in-kernel reduction writes tiled partials [tile][split][BI][BJ] into the slab
+    if (!d->slab || d->slab_floats < (int64_t)tiles * d->splits * BI * BJ) return DFCSA_EINVAL;
     if (next + tiles > kCntRing) next = 0;
     a.cnt = ring + next;
     next += tiles;

@@ -22,10 +22,18 @@ design:
     every rank (torch DDP's broadcast_buffers); call it before validation or checkpointing so all
     ranks evaluate and save the same model.
 """
+import time
+
 import torch
 import torch.distributed as dist
 
 from . import streams
+
+# ProcessGroupNCCL's watchdog thread polls the completion events of the eager collectives it
+# tracks about every 100 ms and drops completed ones.  A HIP-graph capture must not begin while it
+# still holds any (see capture_step): waiting this long after a device synchronisation lets it
+# drain its list first.
+WATCHDOG_DRAIN_S = 0.3
 
 
 class GradBucketReducer:
@@ -57,6 +65,24 @@ class GradBucketReducer:
                 m._dfcsa_reducer = self
         self._pending = None
         self._works = []
+        self.broadcast_parameters()
+
+    @torch.no_grad()
+    def broadcast_parameters(self, src=0):
+        """Make every replica start from rank ``src``'s parameters and BatchNorm buffers (torch
+        DDP does this at construction): one broadcast of the flat parameter buffer, one of the
+        floating-point buffers.  Replica consistency then does not rest on every process having
+        drawn the same initialisation from its RNG."""
+        if self.world <= 1 or not dist.is_initialized():
+            return
+        data = self.flat.data
+        if data.is_cuda and dist.get_backend(self.group) == "gloo":
+            h = data.cpu()
+            dist.broadcast(h, src=src, group=self.group)
+            data.copy_(h)
+        else:
+            dist.broadcast(data, src=src, group=self.group)
+        self.broadcast_buffers(src)
 
     def start(self):
         """Arm for one backward pass."""
@@ -156,12 +182,15 @@ def _host_allreduce(t, op, group):
     return _Done()
 
 
-def allreduce_stats(stats, group=None):
+def allreduce_stats(stats, group=None, weight=1.0):
     """The Trainer's per-step metric vector (dfcsa.loss stats, fp32[8]) summed over the ranks, the
     loss entry averaged: IoU / Dice from the summed counts are the global batch's, the loss the
-    mean of the per-replica losses (the 4-scalar metric all-reduce)."""
+    mean of the per-replica losses, each weighted by its ``shard_weight`` (the
+    4-scalar metric all-reduce).  A rank without rows passes zeros."""
     world = dist.get_world_size(group)
     out = stats.detach().clone()
+    if weight != 1.0:
+        out[0] *= weight
     if out.is_cuda and dist.get_backend(group) == "gloo":
         _host_allreduce(out, dist.ReduceOp.SUM, group)
     else:
@@ -177,8 +206,52 @@ def notify_grads_ready(module):
 
 
 def shard_rows(n, rank, world):
-    """Rows [lo, hi) of a global batch of n owned by `rank` (global batch split evenly)."""
-    if n % world:
-        raise ValueError(f"global batch {n} is not divisible by world size {world}")
-    per = n // world
-    return rank * per, (rank + 1) * per
+    """Rows [lo, hi) of a global batch of n owned by `rank`.  The split is as even as it can be:
+    the first n % world ranks take one row more, and with n < world the last ranks take none (a
+    dataset whose length is not a multiple of batch x world ends on such a ragged batch; the
+    reference's DataLoader keeps it, utils/data_loader.py:153-159)."""
+    per, rem = divmod(int(n), world)
+    lo = rank * per + min(rank, rem)
+    return lo, lo + per + (1 if rank < rem else 0)
+
+
+def shard_weight(n, rank, world):
+    """The factor this rank's loss gradient is scaled by so that the all-reduced SUM times 1/world
+    is the row-weighted mean of the per-replica gradients, sum_r (n_r / n) g_r (= the plain mean
+    when the batch divides evenly, where the factor is exactly 1)."""
+    lo, hi = shard_rows(n, rank, world)
+    return (hi - lo) * world / n if n else 0.0
+
+
+def capture_step(fn):
+    """Capture one call of ``fn`` (a whole training step) as a HIP graph; returns (graph, fn's
+    result).  Two rules make the capture safe beside RCCL:
+      * thread_local capture mode: in the default global mode the HIP runtime refuses stream-unsafe
+        calls from EVERY thread while the capture is open, and ProcessGroupNCCL's watchdog thread
+        calls hipEventQuery on the eager collectives it tracks -- the refusal surfaces as an
+        exception in the watchdog, which terminates the process (SIGABRT, "Exception raised from
+        run at ProcessGroupNCCL.cpp");
+      * nothing tracked: the device is synchronised and the watchdog given WATCHDOG_DRAIN_S to drop
+        the completed eager works before the capture opens (collectives issued during a capture are
+        not handed to the watchdog)."""
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized():
+        time.sleep(WATCHDOG_DRAIN_S)
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph, capture_error_mode="thread_local"):
+        out = fn()
+    torch.cuda.synchronize()
+    return graph, out
+
+
+def shutdown(*graphs):
+    """Leave a (data-parallel) run cleanly: release the captured graphs first -- a graph holding
+    RCCL kernels references the communicator, and tearing the communicator down under it aborts
+    -- then drain the device, meet the other ranks and destroy the process group."""
+    for g in graphs:
+        if g is not None:
+            g.reset()
+    torch.cuda.synchronize()
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+        dist.destroy_process_group()

@@ -17,8 +17,9 @@ The forward runs NHWC through dfcsa/transunet_ops.py:
   SegmentationHead (:272-276)      SegHead3x3 -> NCHW fp32 logits
 
 Dropout (rate 0.1 in the stock config) uses counter-based masks on the device (statistically
-equivalent to nn.Dropout, not the same random stream); attention-probability dropout is 0 in the
-reference config and is not built for p > 0.
+equivalent to nn.Dropout, not the same random stream); attention-probability dropout (0 in the
+reference config) runs for p > 0 on materialised-score kernels (dfcsa_mha_drop_fwd/bwd, N = 196)
+with the mask regenerated from the same counter-based key in the backward.
 """
 import torch
 import torch.nn as nn

@@ -189,6 +189,55 @@ def _collate_list(batch):
     return batch
 
 
+class RankShardedLoader:
+    """The training loader of one data-parallel rank: every rank draws the SAME global permutation
+    (a torch.Generator seeded with seed + epoch, identical on every rank, independent of the
+    process's global RNG), cuts it into global batches of ``batch_size`` and loads only its own rows
+    of each (``dfcsa.ddp.shard_rows``: as even as possible, the last ragged batch included, as the
+    reference's DataLoader keeps it).  Each batch carries ``global_rows`` = the global batch's size,
+    so the Trainer neither re-shards it nor mis-weights a short shard; a rank without rows in a batch
+    gets {'image': None, 'mask': None, 'global_rows': n} and steps with zero gradients."""
+
+    def __init__(self, dataset, batch_size, rank, world, seed=0, shuffle=True, wrap=None, **dl_kwargs):
+        self.dataset, self.batch_size, self.rank, self.world = dataset, int(batch_size), rank, world
+        self.seed, self.shuffle, self.wrap, self.dl_kwargs = int(seed), shuffle, wrap, dl_kwargs
+        self.epoch = 0
+
+    def set_epoch(self, epoch):
+        self.epoch = int(epoch)
+
+    def __len__(self):
+        return (len(self.dataset) + self.batch_size - 1) // self.batch_size
+
+    def global_batches(self):
+        n = len(self.dataset)
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            order = torch.randperm(n, generator=g).tolist()
+        else:
+            order = list(range(n))
+        return [order[i:i + self.batch_size] for i in range(0, n, self.batch_size)]
+
+    def __iter__(self):
+        from dfcsa.ddp import shard_rows
+        glob = self.global_batches()
+        local = []
+        for b in glob:
+            lo, hi = shard_rows(len(b), self.rank, self.world)
+            local.append(b[lo:hi])
+        loader = DataLoader(self.dataset, batch_sampler=[ix for ix in local if ix], **self.dl_kwargs)
+        if self.wrap is not None:
+            loader = self.wrap(loader)
+        it = iter(loader)
+        for b, ix in zip(glob, local):
+            if not ix:
+                yield {"image": None, "mask": None, "filename": [], "global_rows": len(b)}
+                continue
+            batch = next(it)
+            batch["global_rows"] = len(b)
+            yield batch
+
+
 # ------------------------------------------------------------------ factory
 class DataLoaderFactory:
     """Same config keys as the reference (data_loader.py:75-98): dataset.{train_dir, val_dir,
@@ -215,7 +264,17 @@ class DataLoaderFactory:
                                ExtToTensor(), ExtNormalize()])
         return ExtCompose([ExtResize(self.img_size), ExtToTensor(), ExtNormalize()])
 
+    @staticmethod
+    def _rank_world():
+        import torch.distributed as dist
+        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+
     def _loader(self, is_train):
+        rank, world = self._rank_world()
+        if is_train and world > 1:
+            return self._sharded_train_loader(rank, world)
         if self.synthetic:
             n = int(self.synthetic) if is_train else max(1, int(self.synthetic) // 4)
             dataset = SyntheticEllipses(n, self.img_size, seed=42 if is_train else 43)
@@ -231,6 +290,22 @@ class DataLoaderFactory:
                                           transform=self.get_transforms(is_train), img_size=self.img_size)
         return DataLoader(dataset, batch_size=self.batch_size, shuffle=is_train, num_workers=self.num_workers,
                           pin_memory=torch.cuda.is_available())
+
+    def _sharded_train_loader(self, rank, world):
+        """Data parallel (a process group of > 1 ranks): this rank's rows of every global batch."""
+        seed = int(self.config["training"].get("seed", 0))
+        if self.synthetic:
+            ds = SyntheticEllipses(int(self.synthetic), self.img_size, seed=42)
+            return RankShardedLoader(ds, self.batch_size, rank, world, seed, num_workers=self.num_workers)
+        if self.gpu_augment:
+            from utils.augment import PairedTransformGPU
+            ds = SegmentationDataset(self.train_dir, img_size=self.img_size, raw_augmentation=bool(self.use_augmentation))
+            tf = PairedTransformGPU(self.img_size, device="cuda")
+            return RankShardedLoader(ds, self.batch_size, rank, world, seed, num_workers=self.num_workers,
+                                     collate_fn=_collate_list, wrap=lambda dl: DeviceBatches(dl, tf))
+        ds = SegmentationDataset(self.train_dir, transform=self.get_transforms(True), img_size=self.img_size)
+        return RankShardedLoader(ds, self.batch_size, rank, world, seed, num_workers=self.num_workers,
+                                 pin_memory=torch.cuda.is_available())
 
     def get_train_loader(self):
         return self._loader(True)

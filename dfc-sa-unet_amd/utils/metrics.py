@@ -7,16 +7,17 @@ from 'weight_bce' / 'weight_dice' (defaults 1.0) -- NOT from the yaml's 'bce_wei
 'dice_weight' keys, exactly like the reference.  The thresholded IoU/Dice are counted over
 the whole flattened batch.
 
-Only 'bce_dice' (the loss every config uses) runs on the MI355X kernels; the reference's
-'dice', 'tversky' and 'joint' losses are not built (they raise NotImplementedError), and an
-unknown type raises ValueError as in the reference.
+'bce_dice' (the loss every config uses) and 'dice' (the reference's default when a config names no
+loss, :251-252 -> dice_loss :6-24, smooth 1) run on the MI355X kernels -- 'dice' is the same fused
+reduction with the BCE weight 0; the reference's 'tversky' and 'joint' losses (no config uses them)
+are not built and raise NotImplementedError; an unknown type raises ValueError as in the reference.
 """
 import torch
 import torch.nn as nn
 
 from dfcsa.loss import bce_dice, metrics_from_stats
 
-_NOT_BUILT = ("dice", "tversky", "joint")
+_NOT_BUILT = ("tversky", "joint")
 
 
 def dice_loss(pred, target, smooth=1.0):
@@ -50,8 +51,11 @@ def calculate_metrics_device(pred, target, loss_type="dice", loss_params=None):
     if loss_type == "bce_dice":
         loss, stats = bce_dice(pred, target, loss_params.get("weight_bce", 1.0), loss_params.get("weight_dice", 1.0))
         return {"loss": loss, "stats": stats}
+    if loss_type == "dice":   # reference :251-252: dice_loss(pred, target) = 1 - (2 sum pt + 1)/(sum p + sum t + 1)
+        loss, stats = bce_dice(pred, target, 0.0, 1.0)
+        return {"loss": loss, "stats": stats}
     if loss_type in _NOT_BUILT:
-        raise NotImplementedError(f"loss type {loss_type!r} is not built on the MI355X path (only 'bce_dice')")
+        raise NotImplementedError(f"loss type {loss_type!r} is not built on the MI355X path (only 'bce_dice' and 'dice')")
     raise ValueError(f"不支持的損失函數類型: {loss_type}")
 
 

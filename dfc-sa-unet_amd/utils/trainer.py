@@ -24,12 +24,20 @@ trainer.py:334-349 -- pass ``training.reference_resume_semantics: true`` to keep
 Data parallelism (north_star: every configs/*.yaml drops in unchanged on 1..8 GPUs; SURVEY section
 8e).  The reference is single-device (train.py:56-59).  When ``torch.distributed`` is initialised
 with more than one rank (one process per GPU, e.g. under torchrun), the same Trainer runs the
-data-parallel step: each rank takes its rows of every global batch (``dfcsa.ddp.shard_rows``),
+data-parallel step: each rank takes its rows of every global batch (``dfcsa.ddp.shard_rows``;
+a loader from ``DataLoaderFactory`` under the process group already yields only this rank's rows),
 the flat gradient buffer is all-reduced in buckets during backward (``GradBucketReducer``; RCCL on
 its own stream, captured in the step's HIP graph), a NaN loss on any rank skips the update on every
 rank, 1/world is applied inside the fused clip + SGD pass, the per-step metric vector is summed over
 the ranks (IoU / Dice of the global batch, the mean of the replica losses), rank 0's BatchNorm
 running statistics are broadcast before validation, and only rank 0 writes checkpoints and plots.
+Replicas start from rank 0's parameters (broadcast when the reducer is built).  A global batch that
+does not divide evenly (the last batch of most epochs) is split as evenly as it can be; each rank's
+loss gradient is weighted by n_rank * world / n so the reduced step is the row-weighted mean of the
+replica gradients, and a rank left without rows takes part in the collectives with zero gradients.
+``training.data_parallel: true`` builds the reducer even in a one-rank group (a rehearsal of the
+multi-GPU step on one GPU).  Call ``close()`` before ``dist.destroy_process_group()``: it releases
+the captured graphs, which hold RCCL kernels referencing the communicator.
 """
 import csv
 import os
@@ -38,7 +46,7 @@ import time
 import torch
 import torch.distributed as dist
 
-from dfcsa.ddp import GradBucketReducer, allreduce_stats, shard_rows
+from dfcsa.ddp import GradBucketReducer, allreduce_stats, capture_step, shard_rows, shard_weight
 from dfcsa.loss import metrics_from_stats, sigmoid
 from dfcsa.optim import FusedSGD
 from utils.metrics import calculate_metrics_device
@@ -83,7 +91,8 @@ class Trainer:
         self.max_norm = 1.0
         # data parallelism: one process per GPU under an initialised process group
         self.world, self.rank, self.reducer = 1, 0, None
-        if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        if dist.is_available() and dist.is_initialized() and (
+                dist.get_world_size() > 1 or config["training"].get("data_parallel", False)):
             self.world, self.rank = dist.get_world_size(), dist.get_rank()
             if not isinstance(self.optimizer, FusedSGD):
                 raise NotImplementedError("data-parallel training needs the fused SGD (torch.optim.SGD as built by "
@@ -94,6 +103,7 @@ class Trainer:
         use_graphs = config["training"].get("cuda_graph", True)
         if self.reducer is not None and dist.get_backend() == "gloo":
             use_graphs = False
+        self._weight = 1.0   # this rank's loss-gradient weight for the current batch (shard_weight)
         self._graphs = {} if use_graphs else None
         self._graph_seen = set()
         print(f"模型將在 {self.device} 上訓練" + (f" (rank {self.rank}/{self.world})" if self.world > 1 else ""))
@@ -112,6 +122,15 @@ class Trainer:
                 and self.model.training):
             return self._graph_step(images, masks)
         return self._eager_step(images, masks)
+
+    def close(self):
+        """Release the captured step graphs (call before dist.destroy_process_group())."""
+        if self._graphs:
+            for g in self._graphs.values():
+                g[0].reset()
+            self._drop_graphs()
+        if torch.cuda.is_available():
+            torch.cuda.synchronize()
 
     def _storage(self):
         """The device storage a captured step reads and writes through raw pointers: the model's
@@ -144,7 +163,7 @@ class Trainer:
     def _graph_step(self, images, masks):
         # the SGD hyper-parameters are kernel arguments baked into a capture: part of the key
         hp = tuple(float(self.optimizer.param_groups[0][k]) for k in ("lr", "momentum", "weight_decay"))
-        shapes = (tuple(images.shape), tuple(masks.shape), images.dtype, masks.dtype, hp)
+        shapes = (tuple(images.shape), tuple(masks.shape), images.dtype, masks.dtype, hp, self._weight)
         sig, keep = self._storage()
         if sig is None:                           # storage changed or not yet resolved: eager
             self._drop_graphs()
@@ -160,11 +179,10 @@ class Trainer:
                 self._graph_seen.add(key)
                 return self._eager_step(images, masks)
             si, sm = images.clone(), masks.clone()
-            graph = torch.cuda.CUDAGraph()
             try:
-                # thread_local: a DataLoader pin-memory thread keeps running during the capture
-                with torch.cuda.graph(graph, capture_error_mode="thread_local"):
-                    met = self._eager_step(si, sm)   # recorded, not executed: replayed below
+                # thread_local capture (a DataLoader pin-memory thread and ProcessGroupNCCL's watchdog
+                # keep running during the capture), see dfcsa.ddp.capture_step
+                graph, met = capture_step(lambda: self._eager_step(si, sm))   # replayed below
             except RuntimeError as e:
                 print(f"HIP graph capture of the training step failed ({e}); stepping eagerly")
                 self._graphs = None
@@ -201,10 +219,13 @@ class Trainer:
             # data parallel: buckets all-reduced as backward finalises them, NaN agreement over the
             # ranks, 1/world inside the fused clip + SGD, the metric vector summed over the ranks
             self.reducer.start()
-            loss.backward()
+            if self._weight != 1.0:   # a ragged global batch: row-weighted mean over the replicas
+                loss.backward(torch.full_like(loss, self._weight))
+            else:
+                loss.backward()
             skip = self.reducer.finish(loss)
             self.optimizer.step(max_norm=self.max_norm, grad_scale=self.reducer.grad_scale, skip_if_nan=skip)
-            return {"loss": loss, "stats": allreduce_stats(met["stats"])}
+            return {"loss": loss, "stats": allreduce_stats(met["stats"], weight=self._weight)}
         loss.backward()
         if isinstance(self.optimizer, FusedSGD):
             self.optimizer.step(max_norm=self.max_norm, skip_if_nan=loss)
@@ -214,18 +235,45 @@ class Trainer:
                 self.optimizer.step()
         return met
 
+    def _null_step(self):
+        """Data parallel, a rank without rows in this global batch: zero gradients through the same
+        collective sequence (every bucket, the NaN flag, the metric vector) and the same SGD step,
+        so the replicas stay identical."""
+        self.optimizer.zero_grad()
+        zero = torch.zeros((), dtype=torch.float32, device=self.device)
+        self.reducer.start()
+        skip = self.reducer.finish(zero)
+        self.optimizer.step(max_norm=self.max_norm, grad_scale=self.reducer.grad_scale, skip_if_nan=skip)
+        stats = torch.zeros(8, dtype=torch.float32, device=self.device)
+        return {"loss": zero, "stats": allreduce_stats(stats, weight=0.0)}
+
+    def _local_rows(self, batch):
+        """(images, masks) of this rank and its loss-gradient weight.  A batch from a rank-sharded
+        loader carries 'global_rows' (its rows are already this rank's, possibly none)."""
+        images, masks = batch["image"], batch["mask"]
+        if self.reducer is None:
+            return images, masks, 1.0
+        n = batch.get("global_rows")
+        if n is None:     # a global batch: take this rank's rows
+            n = images.shape[0]
+            lo, hi = shard_rows(n, self.rank, self.world)
+            images, masks = images[lo:hi], masks[lo:hi]
+        return images, masks, shard_weight(n, self.rank, self.world)
+
     def train_epoch(self, epoch):
         self.model.train()
+        if hasattr(self.train_loader, "set_epoch"):   # a rank-sharded loader reshuffles per epoch
+            self.train_loader.set_epoch(epoch)
         running_loss = running_iou = running_dice = 0.0
         bar = tqdm(self.train_loader, desc=f"Epoch {epoch + 1}/{self.num_epochs} [Train]")
         for batch_idx, batch in enumerate(bar):
-            images, masks = batch["image"], batch["mask"]
-            if self.world > 1:   # this rank's rows of the global batch
-                lo, hi = shard_rows(images.shape[0], self.rank, self.world)
-                images, masks = images[lo:hi], masks[lo:hi]
-            images = images.to(self.device, non_blocking=True)
-            masks = masks.to(self.device, non_blocking=True)
-            met = self.train_step(images, masks)
+            images, masks, self._weight = self._local_rows(batch)
+            if images is None or images.shape[0] == 0:
+                met = self._null_step()
+            else:
+                images = images.to(self.device, non_blocking=True)
+                masks = masks.to(self.device, non_blocking=True)
+                met = self.train_step(images, masks)
             loss = float(met["stats"][0].item())
             if loss != loss:  # NaN: the device already skipped the update (trainer.py:134-139)
                 print(f"Warning: NaN loss detected at batch {batch_idx}\n  Skipping this batch...")

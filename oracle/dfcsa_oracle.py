@@ -323,19 +323,23 @@ def bce_dice_loss(p, t, w_bce=1.0, w_dice=1.0, smooth=1.0):
 
 
 def calculate_metrics(p, t, loss_type="bce_dice", loss_params=None):
-    """utils/metrics.py:211-264 for loss_type 'bce_dice' (the only type any config uses).
+    """utils/metrics.py:211-264 for loss_type 'bce_dice' (the type every config uses) and 'dice'
+    (the Trainer's default type, :251-252).
     Note the reference reads 'weight_bce'/'weight_dice' (defaults 1.0), NOT the yaml's
     'bce_weight'/'dice_weight' keys."""
-    if loss_type != "bce_dice":
-        raise ValueError(f"oracle only restates loss_type 'bce_dice', got {loss_type!r}")
+    if loss_type not in ("bce_dice", "dice"):
+        raise ValueError(f"oracle only restates loss_types 'bce_dice' and 'dice', got {loss_type!r}")
     loss_params = loss_params or {}
     b = (p > 0.5).float()
     inter = (b * t).sum().item()
     union = (b + t).sum().item() - inter
     iou = inter / (union + 1e-7)
     dice = (2.0 * inter) / (b.sum().item() + t.sum().item() + 1e-7)
-    loss = bce_dice_loss(p, t, loss_params.get("weight_bce", 1.0),
-                         loss_params.get("weight_dice", 1.0))
+    if loss_type == "dice":   # utils/metrics.py:251-252 -> dice_loss :6-24
+        loss = bce_dice_loss(p, t, 0.0, 1.0)
+    else:
+        loss = bce_dice_loss(p, t, loss_params.get("weight_bce", 1.0),
+                             loss_params.get("weight_dice", 1.0))
     return {"loss": loss, "iou": iou, "dice": dice}
 
 

@@ -299,6 +299,27 @@ def gen_metrics():
     save("metrics_bce_dice.npz", **out)
 
 
+def gen_metrics_dice():
+    """The reference's 'dice' loss type (calculate_metrics :251-252 -> dice_loss :6-24): loss, IoU,
+    Dice and dL/dp on the cases of gen_metrics (p at exactly 0 and 1 included, an empty mask)."""
+    rng = np.random.default_rng(4000)
+    p = rng.uniform(0, 1, size=(2, 1, 16, 16)).astype(np.float32)
+    t = (rng.uniform(size=(2, 1, 16, 16)) > 0.5).astype(np.float32)
+    p_edge = p.copy()
+    p_edge[0, 0, 0, :4] = [0.0, 1.0, 0.5, 0.5]
+    t_edge = t.copy()
+    t_edge[0, 0, 0, :4] = [1.0, 0.0, 1.0, 0.0]
+    out = {}
+    for k, (pp, tt) in {"random": (p, t), "edge_clamp": (p_edge, t_edge), "empty_mask": (p, np.zeros_like(t)),
+                        "all_low": (p * 0.4, t)}.items():
+        pt = torch.tensor(pp, requires_grad=True)
+        met = ref_metrics.calculate_metrics(pt, torch.tensor(tt), "dice", {})
+        met["loss"].backward()
+        out.update({k + ".p": pp, k + ".t": tt, k + ".loss": np32(met["loss"]), k + ".iou": np.float64(met["iou"]),
+                    k + ".dice": np.float64(met["dice"]), k + ".dp": np32(pt.grad)})
+    save("metrics_dice.npz", **out)
+
+
 # ----------------------------------------------------------------------------------------
 # (5) DDP parity target: mean over 4 shards (2 images each) of per-shard gradients (local BN,
 #     per-shard Dice), from identical initial weights.  Also 2 shards of 4.
@@ -707,16 +728,17 @@ def gen_cfg2():
 #      distance to float64's after the step.  The GPU test holds the build's bf16 step to these
 #      (utils/trainer.py:120-151, train.py:73-78).
 # ----------------------------------------------------------------------------------------
-def gen_cfg2bf16():
+def _bf16_step_fixture(fname, pool, seed, bseed, extra=False):
     import copy
-    torch.manual_seed(12000)
-    m = ref_res.UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4, ablation_on_qk_channels=8)
+    torch.manual_seed(seed)
+    m = ref_res.UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=pool, ablation_on_qk_channels=8)
     with torch.no_grad():
         for n, p in m.named_parameters():
             if n.endswith("gamma"):
                 p.fill_(0.5)
+    init = {"init_sum." + k: np.float64(v.double().sum()) for k, v in m.state_dict().items() if v.is_floating_point()}
     m.train()
-    gen = torch.Generator().manual_seed(12001)
+    gen = torch.Generator().manual_seed(bseed)
     x, t = batch(gen, (2, 3, 224, 224))
 
     def step(model, xx, tt, autocast):
@@ -736,12 +758,12 @@ def gen_cfg2bf16():
         opt.step()
         upd = {n: (p.detach().double() - w0[n].double()) for n, p in model.named_parameters()}
         bufs = {k: v.detach().double().clone() for k, v in model.state_dict().items() if "running" in k}
-        return g, upd, bufs
+        return g, upd, bufs, out.detach(), met
 
     m64 = fp64_twin(m)
-    g64, u64, b64 = step(m64, x.double(), t.double(), False)
+    g64, u64, b64, o64, _ = step(m64, x.double(), t.double(), False)
     mac = copy.deepcopy(m)
-    gac, uac, bac = step(mac, x, t, True)
+    gac, uac, bac, oac, _ = step(mac, x, t, True)
     reln = lambda a, b: np.float64(((a - b).norm() / (b.norm() + 1e-30)).item())  # noqa: E731
     out = {}
     for n in g64:
@@ -756,8 +778,32 @@ def gen_cfg2bf16():
     gb = torch.cat([g64[n].reshape(-1) for n in g64])
     out["ac_cos_all"] = np.float64((ga @ gb / (ga.norm() * gb.norm())).item())
     out["ac_rel_all"] = reln(ga, gb)
-    print("cfg2 bf16 autocast: global grad cos", float(out["ac_cos_all"]), "rel", float(out["ac_rel_all"]))
-    save("cfg2_bf16.npz", x=np32(x), t=np32(t), **out)
+    if extra:
+        # the fp32 reference step on the same weights (the forward bar and the BN buffers after it)
+        m32 = copy.deepcopy(m)
+        _, _, b32, o32, met32 = step(m32, x, t, False)
+        out.update(init)
+        out["logits"] = np32(o32)
+        out["loss"] = np32(met32["loss"])
+        out["iou"], out["dice"] = np.float64(met32["iou"]), np.float64(met32["dice"])
+        out["ac_logits_rel"] = reln(oac.double(), o32.double())
+        out["ac_logits_rel64"] = reln(oac.double(), o64.double())
+        out.update({"buf." + k: np32(v) for k, v in b32.items()})
+        print(fname, "autocast logits rel", float(out["ac_logits_rel"]))
+    print(fname, "bf16 autocast: global grad cos", float(out["ac_cos_all"]), "rel", float(out["ac_rel_all"]))
+    save(fname, x=np32(x), t=np32(t), **out)
+
+
+def gen_cfg2bf16():
+    _bf16_step_fixture("cfg2_bf16.npz", 4, 12000, 12001)
+
+
+# (12c) Config-3 geometry (config_dfc-sa-res-block.yaml: pool_size 8) at 224^2, 64..512, B = 2 -- the
+#       P = 8 path (N = 64 tokens, non-divisible 28 -> 8 and 14 -> 8 pooling windows) of the DDP
+#       benchmark: the same three-way step as (12b) from its own seed, plus the fp32 reference's logits,
+#       loss / IoU / Dice, BN buffers and the seeded-init checksums.
+def gen_cfg3bf16():
+    _bf16_step_fixture("cfg3_bf16.npz", 8, 14000, 14001, extra=True)
 
 
 # ----------------------------------------------------------------------------------------

@@ -180,6 +180,8 @@ def test_metrics_loss_types():
         calculate_metrics(p, t, "tversky")
     with pytest.raises(RuntimeError):  # bce_dice on host tensors: no CPU fallback
         calculate_metrics(p, t, "bce_dice")
+    with pytest.raises(RuntimeError):  # 'dice' runs on the same kernel: no CPU fallback either
+        calculate_metrics(p, t, "dice")
 
 
 def test_flat_params_views_and_grads():
@@ -451,3 +453,60 @@ def test_model_stats_headline_flops_pinned():
                                           "pool_size": 4}, "training": {}})
     f = S.forward_flops(m, (1, 3, 224, 224))
     assert abs(f / 1e9 - 67.29) < 0.01, f / 1e9
+
+
+def test_shard_rows_ragged_and_weights():
+    """ragged global batches split as evenly as possible (the last ranks may get none); the
+    per-rank loss weights make (sum of weighted replica gradients) / world the row-weighted mean."""
+    from dfcsa.ddp import shard_rows, shard_weight
+    for n in (1, 3, 7, 8, 16, 17):
+        for world in (1, 2, 3, 8):
+            spans = [shard_rows(n, r, world) for r in range(world)]
+            assert spans[0][0] == 0 and spans[-1][1] == n
+            assert all(a[1] == b[0] for a, b in zip(spans, spans[1:]))
+            sizes = [hi - lo for lo, hi in spans]
+            assert max(sizes) - min(sizes) <= 1
+            ws = [shard_weight(n, r, world) for r in range(world)]
+            assert abs(sum(ws) / world - 1.0) < 1e-12
+            assert all(abs(w * world / world - s / n * world) < 1e-12 for w, s in zip(ws, sizes))
+            if n % world == 0:
+                assert all(w == 1.0 for w in ws)
+
+
+def test_rank_sharded_loader_partitions_global_batches():
+    """Every rank draws the same global permutation (seed + epoch, independent of the global RNG) and
+    loads only its rows; the ranks' rows of each batch together are that global batch; a rank without
+    rows in a batch gets a placeholder carrying global_rows."""
+    from utils.data_loader import RankShardedLoader
+
+    class DS(torch.utils.data.Dataset):
+        def __len__(self):
+            return 9
+
+        def __getitem__(self, i):
+            return {"image": torch.full((1, 2, 2), float(i)), "mask": torch.zeros(1, 2, 2)}
+
+    world = 4
+    for epoch in (0, 1):
+        per_rank = []
+        for r in range(world):
+            torch.manual_seed(1000 + r)   # a rank's own RNG state must not matter
+            ld = RankShardedLoader(DS(), 5, r, world, seed=3)
+            ld.set_epoch(epoch)
+            per_rank.append(list(ld))
+        glob = RankShardedLoader(DS(), 5, 0, world, seed=3)
+        glob.set_epoch(epoch)
+        gb = glob.global_batches()
+        assert len(gb) == 2 and [len(b) for b in gb] == [5, 4]
+        for bi, b in enumerate(gb):
+            got = []
+            for r in range(world):
+                batch = per_rank[r][bi]
+                assert batch["global_rows"] == len(b)
+                if batch["image"] is not None:
+                    got += [int(v) for v in batch["image"][:, 0, 0, 0].tolist()]
+            assert got == b
+    e0 = RankShardedLoader(DS(), 5, 0, world, seed=3).global_batches()
+    ld = RankShardedLoader(DS(), 5, 0, world, seed=3)
+    ld.set_epoch(1)
+    assert ld.global_batches() != e0

@@ -261,6 +261,60 @@ def test_fullres_model_bf16_train_step():
     assert np.isfinite(met["loss"].item()) and np.isfinite(opt.last_norm.item())
 
 
+@pytest.mark.timeout(600)
+def test_fullres_model_512_bf16_train_step_factory():
+    """Config 5 at its geometry (config_ablation3_full_res_attn.yaml overlaid as BASELINE states it:
+    UNet_FullResAttention, features 64..512, 512^2, bf16), built through ModelFactory, B = 1: the
+    level-1 / level-9 attention runs over N = 262,144 tokens and level 2 / 8 over 65,536 (the kernels
+    at exactly these N and widths are checked against torch fp32 in test_gpu_fra_longn.py).  One train
+    step: logits within 5e-2 of the fp32 mode (generic fp32 attention kernels) on the same weights and
+    batch, loss within 1e-2, every gradient and the clipped norm finite and nonzero, every parameter
+    finite after the SGD step, and the attention gammas' gradients nonzero on every level."""
+    from dfcsa.loss import sigmoid
+    from dfcsa.optim import FusedSGD
+    from models.model_factory import ModelFactory
+    from models.unet_dfc_sa_ablation_attention import UNet_FullResAttention
+    from utils.metrics import calculate_metrics_device
+    cfg = {"model": {"name": "UNet_FullResAttention", "in_channels": 3, "out_channels": 1,
+                     "features": [64, 128, 256, 512], "precision": "bf16"},
+           "dataset": {"img_size": [512, 512]}, "training": {}}
+    torch.manual_seed(13)
+    m16 = ModelFactory.get_model(cfg)
+    with torch.no_grad():
+        for n, p in m16.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    m32 = UNet_FullResAttention(3, 1, [64, 128, 256, 512], precision="fp32")
+    m32.load_state_dict(m16.state_dict())
+    m32, m16 = m32.cuda().train(), m16.cuda().train()
+    g = torch.Generator().manual_seed(14)
+    x = torch.randn(1, 3, 512, 512, generator=g).cuda()
+    t = (torch.rand(1, 1, 512, 512, generator=g) > 0.5).float().cuda()
+    with torch.no_grad():
+        l32 = m32(x)
+        ref = calculate_metrics_device(sigmoid(l32), t, "bce_dice", {})["loss"].item()
+    del m32
+    torch.cuda.empty_cache()
+    opt = FusedSGD(m16.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt.zero_grad()
+    l16 = m16(x)
+    met = calculate_metrics_device(sigmoid(l16), t, "bce_dice", {})
+    met["loss"].backward()
+    torch.cuda.synchronize()
+    r = rel(l16, l32)
+    print(f"512^2 full-resolution model: bf16 vs fp32 logits rel {r:.3e}, loss {met['loss'].item():.6f} vs {ref:.6f}")
+    assert r < 5e-2
+    assert abs(met["loss"].item() - ref) <= 1e-2 * abs(ref)
+    for n, p in m16.named_parameters():
+        assert torch.isfinite(p.grad).all(), n
+        if n.endswith("gamma"):
+            assert p.grad.abs().item() > 0, n
+    opt.step(max_norm=1.0, skip_if_nan=met["loss"])
+    torch.cuda.synchronize()
+    assert np.isfinite(opt.last_norm.item()) and opt.last_norm.item() > 0
+    assert all(torch.isfinite(p).all() for p in m16.parameters())
+
+
 # ----------------------------------------------------------------------------- plain U-Net (config 1)
 @pytest.mark.parametrize("name,seed,precision,tol", [("unet_small.npz", 6000, "fp32", 1e-4),
                                                      ("unet_cfg1.npz", 6001, "fp32", 1e-4),

@@ -291,6 +291,27 @@ def test_loss_and_metrics_kernel(golden):
         assert rel(p.grad, ref) < 1e-5
 
 
+def test_dice_loss_type_matches_reference(golden):
+    """calculate_metrics(..., 'dice') (reference utils/metrics.py:251-252 -> dice_loss :6-24) against
+    the reference's own outputs (metrics_dice.npz): loss, IoU, Dice, dL/dp -- p at exactly 0 and 1 (the
+    zero-weight BCE term must not leak a non-finite value) and an empty mask included."""
+    from dfcsa.loss import metrics_from_stats
+    from utils.metrics import calculate_metrics, calculate_metrics_device
+    fx = golden("metrics_dice.npz")
+    for c in sorted({k.split(".")[0] for k in fx}):
+        p = torch.tensor(fx[c + ".p"], device="cuda", requires_grad=True)
+        t = torch.tensor(fx[c + ".t"], device="cuda")
+        met = calculate_metrics_device(p, t, "dice", {})
+        met["loss"].backward()
+        iou, dice = metrics_from_stats(met["stats"])
+        assert abs(met["loss"].item() - float(fx[c + ".loss"])) < 1e-5 * max(1.0, abs(float(fx[c + ".loss"]))), c
+        assert abs(iou - float(fx[c + ".iou"])) < 1e-9 and abs(dice - float(fx[c + ".dice"])) < 1e-9, c
+        assert torch.isfinite(p.grad).all(), c
+        assert rel(p.grad, torch.tensor(fx[c + ".dp"])) < 1e-5, c
+        m2 = calculate_metrics(p.detach(), t, "dice")
+        assert abs(m2["dice"] - float(fx[c + ".dice"])) < 1e-9
+
+
 def test_clip_sgd_matches_torch():
     from dfcsa.flat import FlatParams
     from dfcsa.optim import FusedSGD

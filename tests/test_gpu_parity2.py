@@ -8,6 +8,7 @@ fixture batch and 5 seeded batches (1.20e-2 .. 1.33e-2), cfg2_step.npz at the co
 per batch; loss, IoU and Dice are held to the plain 1e-2; thresholded predictions must agree
 exactly on every pixel whose fp32 logit is farther than EPS from the 0.5-probability boundary.
 """
+import json
 import os
 import socket
 
@@ -196,35 +197,112 @@ def test_cfg2_geometry_bf16_within_reference_autocast():
     print(f"cfg2 bf16 logits rel {r:.4e} (bar {bar:.4e})")
 
 
-def _cfg2_bf16_step(fused=True):
-    """One bf16 train step at the config-2 geometry; returns (sd0, pre-clip grads, state after)."""
-    from dfcsa import block as blk_mod
+def seeded_model(precision, pool, seed, fx):
+    """A fixture's 64..512 model: torch.manual_seed(seed), pool ``pool``, gammas 0.5, checked against
+    the fixture's seeded-init checksums (same module tree / creation order as the reference)."""
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    torch.manual_seed(seed)
+    m = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=pool, ablation_on_qk_channels=8, precision=precision)
+    with torch.no_grad():
+        for n, p in m.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.5)
+    for k, v in m.state_dict().items():
+        if v.is_floating_point():
+            assert abs(v.double().sum().item() - float(fx["init_sum." + k])) <= 1e-6 * max(1.0, abs(float(fx["init_sum." + k]))), k
+    return m
+
+
+def _bf16_step(m, fx):
+    """One bf16 train step of model ``m`` on the fixture batch (every bf16 block fusion on); returns
+    (sd0, pre-clip grads, state after, x, t, logits, metrics)."""
     from dfcsa.loss import sigmoid
     from dfcsa.optim import FusedSGD
     from utils.metrics import calculate_metrics_device
-    m, fx = cfg2_model("bf16")
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     m = m.cuda().train()
     opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
     x, t = T(fx["x"]), T(fx["t"])
-    old = (blk_mod.FUSED_DGRAD_GATE[0], blk_mod.POOL_FUSION[0])
-    blk_mod.FUSED_DGRAD_GATE[0] = blk_mod.POOL_FUSION[0] = fused
-    try:
-        opt.zero_grad()
-        met = calculate_metrics_device(sigmoid(m(x)), t, "bce_dice", LP)
-        met["loss"].backward()
-        torch.cuda.synchronize()
-        pre = {n: p.grad.detach().double().cpu().clone() for n, p in m.named_parameters()}
-        opt.step(max_norm=1.0, skip_if_nan=met["loss"])
-        torch.cuda.synchronize()
-    finally:
-        blk_mod.FUSED_DGRAD_GATE[0], blk_mod.POOL_FUSION[0] = old
-    return sd0, pre, {k: v.detach().cpu() for k, v in m.state_dict().items()}, x, t, fx
+    opt.zero_grad()
+    logits = m(x)
+    met = calculate_metrics_device(sigmoid(logits), t, "bce_dice", LP)
+    met["loss"].backward()
+    torch.cuda.synchronize()
+    pre = {n: p.grad.detach().double().cpu().clone() for n, p in m.named_parameters()}
+    opt.step(max_norm=1.0, skip_if_nan=met["loss"])
+    torch.cuda.synchronize()
+    return sd0, pre, {k: v.detach().cpu() for k, v in m.state_dict().items()}, x, t, logits.detach(), met
 
 
 def _cos_rel(g, r):
     g, r = g.reshape(-1), r.double().reshape(-1)
     return (g @ r / (g.norm() * r.norm() + 1e-300)).item(), ((g - r).norm() / (r.norm() + 1e-30)).item()
+
+
+def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32):
+    """The bar of test_cfg2_geometry_bf16_train_step_vs_reference_autocast (docstring there), against
+    the fp32 oracle re-run on this host at pool size ``pool``; ``fb`` holds the reference's autocast
+    distances.  Prints every tensor's distances (worst first)."""
+    from oracle import dfcsa_oracle as O
+    SMALL = 4096
+    assert torch.equal(x.cpu(), torch.from_numpy(fb["x"])) and torch.equal(t.cpu(), torch.from_numpy(fb["t"]))
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    _, _, gref, _ = O.forward_backward(sd0, x.cpu(), t.cpu(), pool, LP)
+    sd1, _, _, _ = O.clip_and_sgd(sd0, gref, {})
+    rows, fails = [], []
+    sm = {"err": 0.0, "ac": 0.0, "uerr": 0.0, "uac": 0.0}
+    for n in O.param_names(sd0):
+        if n.endswith(ZERO):
+            assert pre[n].abs().max().item() <= 1e-6 * max(1.0, gref[n].abs().max().item()), n
+            continue
+        cs, rr = _cos_rel(pre[n], gref[n])
+        ac_rel, ac_cos = float(fb["ac_rel." + n]), float(fb["ac_cos." + n])
+        ac_urel = float(fb["ac_upd_rel." + n])
+        upd, upd_ref = sd[n].double() - sd0[n].double(), sd1[n].double() - sd0[n].double()
+        quant = 2.0 * 2.0 ** -23 * sd0[n].double().norm().item()
+        uerr = max(0.0, (upd - upd_ref).norm().item() - quant)
+        ur = uerr / (upd_ref.norm().item() + 1e-30)
+        if pre[n].numel() < SMALL:
+            gn = gref[n].double().norm().item()
+            sm["err"] += (rr * gn) ** 2
+            sm["ac"] += (ac_rel * gn) ** 2
+            sm["uerr"] += uerr ** 2
+            sm["uac"] += (ac_urel * upd_ref.norm().item()) ** 2
+            ok = rr <= 5 * ac_rel + 2e-2 and ur <= 5 * ac_urel + 2e-2
+        else:
+            ok = rr <= max(1.25 * ac_rel, 2e-2) and 1 - cs <= 1.25 * (1 - ac_cos) + 1e-3
+            if ur > max(1.25 * ac_urel, 2e-2):
+                fails.append(f"{n}: update rel {ur:.3e} (autocast {ac_urel:.3e})")
+        rows.append((rr / max(ac_rel, 1e-30), n, f"{n}: cos {cs:.5f} (autocast {ac_cos:.5f}) rel {rr:.3e} "
+                                                 f"(autocast {ac_rel:.3e}) update rel {ur:.3e} (autocast "
+                                                 f"{ac_urel:.3e})"))
+        if not ok:
+            fails.append(rows[-1][2])
+    rows.sort(reverse=True)
+    print(f"{tag} bf16 step, every tensor relative to the reference autocast (worst first):")
+    for r in rows:
+        print("   ", r[2])
+    g_small, g_ac = sm["err"] ** 0.5, sm["ac"] ** 0.5
+    u_small, u_ac = sm["uerr"] ** 0.5, sm["uac"] ** 0.5
+    print(f"{tag} bf16 step, small tensors as one vector: gradient error {g_small:.4e} (autocast {g_ac:.4e}), "
+          f"update error {u_small:.4e} (autocast {u_ac:.4e})")
+    if g_small > 1.25 * g_ac:
+        fails.append(f"small-tensor gradient error {g_small:.4e} > 1.25 x autocast {g_ac:.4e}")
+    if u_small > 1.25 * u_ac + 1e-12:
+        fails.append(f"small-tensor update error {u_small:.4e} > 1.25 x autocast {u_ac:.4e}")
+    names = [n for n in O.param_names(sd0) if not n.endswith(ZERO)]
+    ga = torch.cat([pre[n].reshape(-1) for n in names])
+    gb = torch.cat([gref[n].double().reshape(-1) for n in names])
+    cos_all, rel_all = _cos_rel(ga, gb)
+    print(f"{tag} bf16 step: whole-gradient cos {cos_all:.6f} (autocast {float(fb['ac_cos_all']):.6f}), "
+          f"rel {rel_all:.4e} (autocast {float(fb['ac_rel_all']):.4e})")
+    for k, v in sd.items():
+        if "running" in k:
+            bar = max(1.25 * float(fb["ac_buf_rel." + k]), 1e-3)
+            if rel(v.float(), bufs_fp32["buf." + k]) > bar:
+                fails.append(f"{k}: {rel(v.float(), bufs_fp32['buf.' + k]):.3e} > {bar:.3e}")
+    assert not fails, fails
+    assert cos_all >= float(fb["ac_cos_all"]) and rel_all <= float(fb["ac_rel_all"])
 
 
 def test_cfg2_geometry_bf16_train_step_vs_reference_autocast():
@@ -234,10 +312,9 @@ def test_cfg2_geometry_bf16_train_step_vs_reference_autocast():
     at C = 64, the fused max-pool passes).  Pinned to the reference's own bf16 error
     (tests/golden/cfg2_bf16.npz: the reference under CPU bf16 autocast against its float64 run),
     against the fp32 reference re-run here on the CPU oracle:
-      * weight tensors (>= SMALL elements, pre-clip gradient): relative distance <= max(1.25 x the
-        autocast's, 2e-2) and cosine distance 1 - cos <= 1.25 x the autocast's + 1e-3 -- or, where
-        our path is farther than that, no farther than the same step with the fusions off (+5%): the
-        fusions must not add error of their own;
+      * weight tensors (>= 4096 elements, pre-clip gradient): relative distance <= max(1.25 x the
+        autocast's, 2e-2) and cosine distance 1 - cos <= 1.25 x the autocast's + 1e-3, every one of
+        them (no fall-back bar);
       * the small tensors (biases, BatchNorm affine, the gamma / res_scale scalars): each of their
         elements is one reduction over B*H*W pixels whose bf16 error is rounding noise around a
         small, heavily cancelling sum, so one tensor's distance is a single noise sample (the
@@ -252,76 +329,26 @@ def test_cfg2_geometry_bf16_train_step_vs_reference_autocast():
         fp32 gradients: <= max(1.25 x the autocast update's distance, 2e-2).
     The conv biases that feed a train-mode BatchNorm have an exactly-zero gradient (ours is the
     exact zero; autocast's is rounding noise): they are held to zero."""
-    from oracle import dfcsa_oracle as O
-    SMALL = 4096
+    fx = load("cfg2_step.npz")
     fb = load("cfg2_bf16.npz")
-    sd0, pre, sd, x, t, fx = _cfg2_bf16_step(True)
-    assert torch.equal(x.cpu(), torch.from_numpy(fb["x"])) and torch.equal(t.cpu(), torch.from_numpy(fb["t"]))
-    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    _, _, gref, _ = O.forward_backward(sd0, x.cpu(), t.cpu(), 4, LP)
-    sd1, _, _, _ = O.clip_and_sgd(sd0, gref, {})
-    unfused = None
-    rows, fails = [], []
-    sm = {"err": 0.0, "ac": 0.0, "uerr": 0.0, "uac": 0.0}
-    for n in O.param_names(sd0):
-        if n.endswith(ZERO):
-            assert pre[n].abs().max().item() <= 1e-6 * max(1.0, gref[n].abs().max().item()), n
-            continue
-        cs, rr = _cos_rel(pre[n], gref[n])
-        ac_rel, ac_cos = float(fb["ac_rel." + n]), float(fb["ac_cos." + n])
-        ac_urel = float(fb["ac_upd_rel." + n])
-        upd, upd_ref = sd[n].double() - sd0[n].double(), sd1[n].double() - sd0[n].double()
-        quant = 2.0 * 2.0 ** -23 * sd0[n].double().norm().item()
-        uerr = max(0.0, (upd - upd_ref).norm().item() - quant)
-        ur = uerr / (upd_ref.norm().item() + 1e-30)
-        note = ""
-        if pre[n].numel() < SMALL:
-            gn = gref[n].double().norm().item()
-            sm["err"] += (rr * gn) ** 2
-            sm["ac"] += (ac_rel * gn) ** 2
-            sm["uerr"] += uerr ** 2
-            sm["uac"] += (ac_urel * upd_ref.norm().item()) ** 2
-            ok = rr <= 5 * ac_rel + 2e-2 and ur <= 5 * ac_urel + 2e-2
-        else:
-            ok = rr <= max(1.25 * ac_rel, 2e-2) and 1 - cs <= 1.25 * (1 - ac_cos) + 1e-3
-            if not ok:
-                if unfused is None:
-                    unfused = _cfg2_bf16_step(False)[1]
-                ucs, urr = _cos_rel(unfused[n], gref[n])
-                note = f" unfused cos {ucs:.5f} rel {urr:.3e}"
-                ok = rr <= 1.05 * urr + 1e-4 and 1 - cs <= 1.05 * (1 - ucs) + 1e-4
-            if ur > max(1.25 * ac_urel, 2e-2):
-                fails.append(f"{n}: update rel {ur:.3e} (autocast {ac_urel:.3e})")
-        rows.append((rr / max(ac_rel, 1e-30), n, f"{n}: cos {cs:.5f} (autocast {ac_cos:.5f}) rel {rr:.3e} "
-                                                 f"(autocast {ac_rel:.3e}) update rel {ur:.3e} (autocast "
-                                                 f"{ac_urel:.3e}){note}"))
-        if not ok:
-            fails.append(rows[-1][2])
-    rows.sort(reverse=True)
-    print("cfg2 bf16 step, worst tensors relative to the reference autocast:")
-    for r in rows[:12]:
-        print("   ", r[2])
-    g_small, g_ac = sm["err"] ** 0.5, sm["ac"] ** 0.5
-    u_small, u_ac = sm["uerr"] ** 0.5, sm["uac"] ** 0.5
-    print(f"cfg2 bf16 step, small tensors as one vector: gradient error {g_small:.4e} (autocast {g_ac:.4e}), "
-          f"update error {u_small:.4e} (autocast {u_ac:.4e})")
-    if g_small > 1.25 * g_ac:
-        fails.append(f"small-tensor gradient error {g_small:.4e} > 1.25 x autocast {g_ac:.4e}")
-    if u_small > 1.25 * u_ac + 1e-12:
-        fails.append(f"small-tensor update error {u_small:.4e} > 1.25 x autocast {u_ac:.4e}")
-    names = [n for n in O.param_names(sd0) if not n.endswith(ZERO)]
-    ga = torch.cat([pre[n].reshape(-1) for n in names])
-    gb = torch.cat([gref[n].double().reshape(-1) for n in names])
-    cos_all, rel_all = _cos_rel(ga, gb)
-    print(f"cfg2 bf16 step: whole-gradient cos {cos_all:.6f} (autocast {float(fb['ac_cos_all']):.6f}), "
-          f"rel {rel_all:.4e} (autocast {float(fb['ac_rel_all']):.4e})")
-    for k, v in sd.items():
-        if "running" in k:
-            bar = max(1.25 * float(fb["ac_buf_rel." + k]), 1e-3)
-            if rel(v.float(), fx["buf." + k]) > bar:
-                fails.append(f"{k}: {rel(v.float(), fx['buf.' + k]):.3e} > {bar:.3e}")
-    assert not fails, fails
-    assert cos_all >= float(fb["ac_cos_all"]) and rel_all <= float(fb["ac_rel_all"])
+    sd0, pre, sd, x, t, _, _ = _bf16_step(seeded_model("bf16", 4, 12000, fx), fx)
+    _check_bf16_step_vs_autocast("cfg2", fb, 4, sd0, pre, sd, x, t, fx)
+
+
+def test_cfg3_geometry_bf16_train_step_vs_reference_autocast():
+    """Config 3 (config_dfc-sa-res-block.yaml: pool_size 8) at its benchmark geometry -- 64..512,
+    224^2, B = 2 per GPU, bf16 -- one train step through the benchmark path: the P = 8 attention (N =
+    64 tokens, non-divisible 28 -> 8 / 14 -> 8 pooling windows) and every bf16 block fusion.  Pinned
+    to tests/golden/cfg3_bf16.npz (the reference under CPU bf16 autocast against its float64 run,
+    plus its fp32 step): logits within max(1e-2, the autocast's own logits error), loss / IoU / Dice
+    1e-2, confident pixels identical; then the gradient / update / BatchNorm bar of the config-2 test
+    (no fall-back bar)."""
+    fb = load("cfg3_bf16.npz")
+    sd0, pre, sd, x, t, logits, met = _bf16_step(seeded_model("bf16", 8, 14000, fb), fb)
+    r, bar = bf16_bar_check(logits, met["loss"].item(), met["stats"], fb["logits"], fb["loss"], fb["iou"], fb["dice"],
+                            fb["ac_logits_rel"], fb["t"])
+    print(f"cfg3 bf16 logits rel {r:.4e} (bar {bar:.4e}; reference autocast {float(fb['ac_logits_rel']):.4e})")
+    _check_bf16_step_vs_autocast("cfg3", fb, 8, sd0, pre, sd, x, t, fb)
 
 
 # ----------------------------------------------------------------------------- checkpoint interop
@@ -465,21 +492,44 @@ def test_ddp_step_hip_backward_with_grad_scale():
         assert rel(p.detach().cpu() - sd0[n], sd1[n] - sd0[n]) < 3e-3, n   # the SGD update
 
 
-def test_rccl_bucket_reducer_graph_replay_equals_eager():
-    """bench.py's multi-GPU step rehearsed on one GPU (tools/rccl_graph_check.py, in a child process so
-    the RCCL communicator lives and dies with it): an RCCL (backend 'nccl') group of world size 1,
-    the bucket reducer forced to several buckets, the NaN-agreement flag, and the whole step
-    captured in one HIP graph; 2 graph replays after 1 eager step equal 3 eager steps."""
-    import json
+def _run_child_logged(name, argv, timeout):
+    """Run a child process with its FULL stdout / stderr kept in files next to the test log
+    (gpurun_out/<name>.{out,err}; DFCSA_TEST_LOGDIR overrides), so an abort's own message survives."""
     import subprocess
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    logdir = os.environ.get("DFCSA_TEST_LOGDIR", os.path.join(root, "gpurun_out"))
+    os.makedirs(logdir, exist_ok=True)
     env = dict(os.environ, MASTER_ADDR="127.0.0.1")
     env.pop("MASTER_PORT", None)
-    r = subprocess.run([sys.executable, os.path.join(root, "tools", "rccl_graph_check.py")], capture_output=True,
-                       text=True, timeout=240, env=env)
-    line = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
-    err = "\n".join(ln for ln in r.stderr.splitlines() if not ln.lstrip().startswith("frame #"))
-    assert r.returncode == 0 and line, (r.returncode, r.stdout[-2000:], err[-4000:])
-    res = json.loads(line[-1])
+    out_p, err_p = os.path.join(logdir, name + ".out"), os.path.join(logdir, name + ".err")
+    with open(out_p, "w") as fo, open(err_p, "w") as fe:
+        r = subprocess.run([sys.executable] + argv, stdout=fo, stderr=fe, text=True, timeout=timeout, env=env, cwd=root)
+    out, err = open(out_p).read(), open(err_p).read()
+    line = [ln for ln in out.splitlines() if ln.startswith("{")]
+    assert r.returncode == 0 and line, (r.returncode, f"full logs: {out_p} {err_p}", out[-1500:], err[-3000:])
+    return json.loads(line[-1])
+
+
+def test_rccl_bucket_reducer_graph_replay_equals_eager():
+    """The multi-GPU step rehearsed on one GPU (tools/rccl_graph_check.py, in a child process so the
+    RCCL communicator lives and dies with it): an RCCL (backend 'nccl') group of world size 1, the
+    bucket reducer forced to several buckets, the NaN-agreement flag, and the whole step captured in
+    one HIP graph (thread_local capture, watchdog drained: dfcsa.ddp.capture_step); 2 graph replays
+    after 1 eager step equal 3 eager steps; the drop-in Trainer with training.data_parallel captures
+    and replays its reducer step equal to its eager step; the child tears down as bench.py does
+    (dfcsa.ddp.shutdown) and must exit 0."""
+    res = _run_child_logged("rccl_graph_check", [os.path.join("tools", "rccl_graph_check.py")], 300)
     assert res["ok"], res
+
+
+def test_bench_ddp_path_exits_cleanly():
+    """bench.py's N > 1 code path on one GPU (--ddp-rehearsal: RCCL group of world size 1, bucket
+    reducer, graph-captured step with its collectives, the max-over-ranks timing all-reduce, the
+    kernel-timing leg, then the teardown): one JSON line and exit status 0."""
+    res = _run_child_logged("bench_ddp_rehearsal",
+                            ["bench.py", "--ddp-rehearsal", "--img", "64", "--batch", "4", "--steps", "3",
+                             "--warmup", "2", "--bucket-mb", "4", "--no-cpu-baseline", "--no-val-dice",
+                             "--no-trainer-faithful"], 300)
+    assert res["config"]["ddp_path"] is True and res["launch"] == "hip_graph", res
+    assert res["value"] > 0 and res["roofline"] is not None, res

@@ -167,3 +167,44 @@ def test_trainer_data_parallel_two_ranks(tmp_path):
     assert abs(float(r0["iou"]) - inter / (sb + st - inter + 1e-7)) < 1e-3
     assert os.path.exists(tmp_path / "logs" / "r0" / "checkpoints" / "checkpoint_epoch_1.pth")
     assert not os.path.exists(tmp_path / "logs" / "r1" / "checkpoints" / "checkpoint_epoch_1.pth")
+
+
+def test_trainer_data_parallel_ragged_batches(tmp_path):
+    """data-parallel training over global batches that do not divide over the ranks.  Two
+    gloo ranks run one epoch of a 7-image batch (rows 4 / 3) and a 1-image batch (rank 1 without rows,
+    stepping with zero gradients through the same collectives); rank 1 starts from perturbed weights,
+    which the reducer's broadcast from rank 0 replaces.  Expected: each step applies the row-weighted
+    mean of the per-replica reference gradients, sum_r (n_r / n) g_r (the CPU oracle: clip + SGD with
+    momentum over both steps), and the replicas end identical."""
+    from oracle import dfcsa_oracle as O
+    worker = os.path.join(ROOT, "tools", "trainer_ddp_check.py")
+    sk = socket.socket()
+    sk.bind(("127.0.0.1", 0))
+    port = str(sk.getsockname()[1])
+    sk.close()
+    outs = [str(tmp_path / f"r{r}.npz") for r in range(2)]
+    procs = [subprocess.Popen([sys.executable, worker, str(r), "2", port, outs[r], str(tmp_path / "logs"), "ragged"],
+                              env=dict(os.environ), cwd=ROOT) for r in range(2)]
+    for p in procs:
+        assert p.wait(timeout=240) == 0
+    r0, r1 = (dict(np.load(o)) for o in outs)
+    dd = dict(np.load(os.path.join(GOLDEN, "ddp_shards.npz")))
+    fx = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
+    sd = {k[4:]: torch.from_numpy(v) for k, v in fx.items() if k.startswith("sd0.")}
+    sd0 = dict(sd)
+    x, t = torch.from_numpy(dd["x"]), torch.from_numpy(dd["t"])
+    mom = {}
+    for rows in ([(0, 4), (4, 7)], [(7, 8)]):
+        n = sum(b - a for a, b in rows)
+        g = None
+        for a, b in rows:   # rank 0's shard first: its BN buffers are the ones rank 0 keeps
+            _, _, gr, _ = O.forward_backward(sd, x[a:b], t[a:b], 4, LP)
+            w = (b - a) / n
+            g = {k: w * v for k, v in gr.items()} if g is None else {k: g[k] + w * v for k, v in gr.items()}
+        sd, mom, _, _ = O.clip_and_sgd(sd, g, mom)
+    for n in O.param_names(sd0):
+        assert np.array_equal(r0["param." + n], r1["param." + n]), n       # identical replicas
+        if n.endswith(ZERO):
+            continue
+        upd, upd_ref = r0["param." + n] - sd0[n].numpy(), (sd[n] - sd0[n]).numpy()
+        assert rel(upd, upd_ref) < 3e-3, n

@@ -119,6 +119,18 @@ def test_metrics():
         close(p.grad, fx[c + ".dp"], rtol=1e-5, atol=1e-7)
 
 
+def test_metrics_dice_type():
+    """The reference's 'dice' loss type (metrics_dice.npz: p at exactly 0 / 1, an empty mask)."""
+    fx = dict(np.load(os.path.join(GOLDEN, "metrics_dice.npz")))
+    for c in sorted({k.split(".")[0] for k in fx}):
+        p = T(fx[c + ".p"]).requires_grad_(True)
+        m = O.calculate_metrics(p, T(fx[c + ".t"]), "dice", {})
+        close(m["loss"], fx[c + ".loss"], rtol=1e-6)
+        assert abs(m["iou"] - fx[c + ".iou"]) < 1e-9 and abs(m["dice"] - fx[c + ".dice"]) < 1e-9
+        m["loss"].backward()
+        close(p.grad, fx[c + ".dp"], rtol=1e-5, atol=1e-7)
+
+
 def test_ddp_shard_means():
     base = dict(np.load(os.path.join(GOLDEN, "model_small.npz")))
     sd = sd_from(base, "sd0.")

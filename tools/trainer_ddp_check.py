@@ -5,7 +5,12 @@ Trainer shards each batch by rank, all-reduces the flat gradient buffer, applies
 clip + SGD, sums the metric vector over the ranks, broadcasts rank 0's BatchNorm statistics before
 validating and writes checkpoints on rank 0 only.  Writes this rank's results to an .npz.
 
-  python tools/trainer_ddp_check.py RANK WORLD PORT OUT.npz LOGDIR
+  python tools/trainer_ddp_check.py RANK WORLD PORT OUT.npz LOGDIR [ragged]
+
+``ragged``: one epoch of two global batches that do not divide over the ranks -- the first 7 images
+(rows 4 / 3 at world 2) and the 8th image alone (rank 1 has no rows: zero gradients through the same
+collectives) -- with rank 1's replica deliberately started from perturbed weights (the reducer's
+broadcast from rank 0 must undo that).  Writes the parameters after the epoch.
 """
 import os
 import sys
@@ -37,6 +42,21 @@ def main():
                            "save_best_worst_samples": 1}}
         batches = [{"image": torch.from_numpy(dd["x"]), "mask": torch.from_numpy(dd["t"]),
                     "filename": [f"s{i}" for i in range(8)]}]
+        if len(sys.argv) > 6 and sys.argv[6] == "ragged":
+            x, t = torch.from_numpy(dd["x"]), torch.from_numpy(dd["t"])
+            rb = [{"image": x[:7], "mask": t[:7]}, {"image": x[7:], "mask": t[7:]}]
+            if rank == 1:
+                with torch.no_grad():
+                    for p in model.parameters():
+                        p.add_(0.01)
+            model.cuda()
+            tr = Trainer(model, rb, rb[:1], opt, dev, cfg)
+            loss, iou, dice = tr.train_epoch(0)
+            torch.cuda.synchronize()
+            res = {"loss": np.float64(loss), "iou": np.float64(iou), "dice": np.float64(dice)}
+            res.update({"param." + n: p.detach().cpu().numpy() for n, p in model.named_parameters()})
+            np.savez(out, **res)
+            return
         tr = Trainer(model, batches, batches, opt, dev, cfg)
         loss, iou, dice = tr.train_epoch(0)
         torch.cuda.synchronize()
