@@ -303,7 +303,7 @@ def main():
     # graph launch.  Inputs are static (resident) tensors; nothing in the step syncs the host.
     graph = None
     if not args.no_graph:
-        side = torch.cuda.Stream()
+        side = torch.cuda.Stream(priority=int(os.environ.get("DFCSA_PRIO_MAIN", "0")))
         side.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(side):
             step()

@@ -16,6 +16,7 @@
 // dy = gamma*invstd*(dz - mean(dz) - xhat*mean(dz*xhat)) that also emits the conv-bias partial
 // sums.  Nothing uses float atomics: results are bitwise reproducible.
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -850,7 +851,7 @@ __device__ __forceinline__ void ld_sc1_d12(const double* const (&p)[12], double 
 // the column totals in tot[].  Column c of sum k of row t: src[t * rowlen + k * kstride + c].
 template <int NS>
 __device__ bool colred_block(const float* src, int T, int rowlen, int kstride, int C, int per, unsigned* cnt,
-                             double* scr, double (&tot)[NS], double (*sh)[16][64], int* flag) {
+                             double* scr, double (&tot)[NS], double (*sh)[16][64], int* flag, int acq) {
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   const int R = gridDim.y, g = blockIdx.y;
@@ -898,7 +899,7 @@ __device__ bool colred_block(const float* src, int T, int rowlen, int kstride, i
     const unsigned old = __hip_atomic_fetch_add(cnt + blockIdx.x, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *flag = old == (unsigned)(R - 1);
     if (*flag) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
       __hip_atomic_store(cnt + blockIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next launch
     }
   }
@@ -950,13 +951,13 @@ __device__ bool colred_block(const float* src, int T, int rowlen, int kstride, i
 __global__ void __launch_bounds__(1024) bn_finalize_kernel(
     const float* __restrict__ stats, int ntiles, int per, unsigned* cnt, double* scr, int C, int ld, int count, const float* bias,
     const float* gamma, const float* beta, float* rmean, float* rvar, int64_t* nbt, float momentum, float eps,
-    int training, float* scale, float* shift, float* mean, float* invstd) {
+    int training, float* scale, float* shift, float* mean, float* invstd, int acq) {
   __shared__ double sh[2][16][64];
   __shared__ int flag;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double tot[2] = {0.0, 0.0};
-  if (training && !colred_block<2>(stats, ntiles, 2 * ld, ld, C, per, cnt, scr, tot, sh, &flag)) return;
+  if (training && !colred_block<2>(stats, ntiles, 2 * ld, ld, C, per, cnt, scr, tot, sh, &flag, acq)) return;
   if (part == 0 && c < C) {
     float mu, var, istd;
     if (training) {
@@ -992,13 +993,13 @@ template <int NS>
 __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __restrict__ partial, int ntiles, int per,
                                                                unsigned* cnt, double* scr, int C, int count, float* coef,
                                                                float* dgamma, float* dbeta, float* third,
-                                                               float* extra) {
+                                                               float* extra, int acq) {
   __shared__ double sh[NS][16][64];
   __shared__ int flag;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double tot[NS];
-  if (!colred_block<NS>(partial, ntiles, NS * C, C, C, per, cnt, scr, tot, sh, &flag)) return;
+  if (!colred_block<NS>(partial, ntiles, NS * C, C, C, per, cnt, scr, tot, sh, &flag, acq)) return;
   if (part == 0 && c < C) {
     coef[c] = (float)(tot[0] / count);
     coef[C + c] = (float)(tot[1] / count);
@@ -1018,7 +1019,7 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
         const unsigned old = __hip_atomic_fetch_add(cnt2, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         flag = old == gridDim.x - 1;
         if (flag) {
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          if (acq) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
           __hip_atomic_store(cnt2, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -1045,13 +1046,13 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
 // out[c] += sum_t slab[t][c]; columns split over up to three destinations at n0, n0 + n1
 __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int per,
                                                            unsigned* cnt, double* scr, int C, int n0, int n1, float* d0,
-                                                           float* d1, float* d2) {
+                                                           float* d1, float* d2, int acq) {
   __shared__ double sh[1][16][64];
   __shared__ int flag;
   const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
   const int c = blockIdx.x * 64 + cl;
   double tot[1];
-  if (!colred_block<1>(slab, ntiles, C, 0, C, per, cnt, scr, tot, sh, &flag)) return;
+  if (!colred_block<1>(slab, ntiles, C, 0, C, per, cnt, scr, tot, sh, &flag, acq)) return;
   if (part == 0 && c < C) {
     const double s = tot[0];
     if (c < n0) d0[c] += (float)s;
@@ -1163,7 +1164,50 @@ struct RedPlan {
   int R = 1, per = 1;
   unsigned* cnt = nullptr;
   double* scr = nullptr;
+  int acq = 1;   // 1: the last arriver takes an agent-scope acquire before reading the hand-offs
 };
+// Ticket counters and hand-off scratch.  With DFCSA_RED_ACQ=0 they are allocated with hipMalloc at
+// first use (eager, before any graph capture): on that memory the hand-off is the measured acquire-free form of
+// MI355X_MICROARCH.md (Valid forms, hand-off table row 1: every hand-off byte stored sc1 and drained
+// by vmcnt(0) in every storing wave, one lane's agent-scope atomic add behind a workgroup barrier,
+// the last adder told by the returned value, every load of the bytes an 8-B sc1 load after its add
+// returned / behind the barrier it then joins), which saves the ~1.7 us buffer_inv of the acquire on
+// every finalize.  Otherwise (default) the code object's arrays and the acquire are used.
+static int red_mem(unsigned** ring, double** scr) {
+  static unsigned* r = nullptr;
+  static double* sc = nullptr;
+  static int acq = -1;
+  if (acq < 0) {
+    unsigned* a = nullptr;
+    double* b = nullptr;
+    // default: the code-object arrays with the acquire; DFCSA_RED_ACQ=0 selects the acquire-free
+    // form on hipMalloc memory (same-box A/B of the default bench: 1554 / 1554 img/s against 1571 /
+    // 1558 with the acquire -- no gain, so the documented-safe form stays the default)
+    const char* force = getenv("DFCSA_RED_ACQ");
+    if (force && force[0] == '0' && hipMalloc((void**)&a, sizeof(unsigned) * kRedRing) == hipSuccess &&
+        hipMalloc((void**)&b, sizeof(double) * kRedScr) == hipSuccess) {
+      static unsigned zero[kRedRing];   // zero-initialised
+      if (hipMemcpy(a, zero, sizeof(zero), hipMemcpyHostToDevice) == hipSuccess) {
+        r = a;
+        sc = b;
+        acq = 0;
+      }
+    }
+    if (acq < 0) {
+      if (a) (void)hipFree(a);
+      if (b) (void)hipFree(b);
+      (void)hipGetLastError();
+      if (hipGetSymbolAddress((void**)&r, HIP_SYMBOL(g_red_cnt)) != hipSuccess ||
+          hipGetSymbolAddress((void**)&sc, HIP_SYMBOL(g_red_scr)) != hipSuccess)
+        return -1;
+      acq = 1;
+    }
+  }
+  *ring = r;
+  *scr = sc;
+  return acq;
+}
+
 static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
   int R = (T + 127) / 128;
   if (R > 64) R = 64;
@@ -1179,19 +1223,22 @@ static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
   p->per = per;
   p->cnt = nullptr;
   const int need = nblk + extra;
+  unsigned* ring = nullptr;
+  double* scr = nullptr;
   if (R > 1 || extra) {
-    static unsigned* ring = nullptr;
+    const int acq = red_mem(&ring, &scr);
+    if (acq < 0) return DFCSA_EINVAL;
+    p->acq = acq;
+  }
+  if (R > 1 || extra) {
     static int next = 0;
-    if (!ring && hipGetSymbolAddress((void**)&ring, HIP_SYMBOL(g_red_cnt)) != hipSuccess) return DFCSA_EINVAL;
     if (need > kRedRing) return DFCSA_EINVAL;
     if (next + need > kRedRing) next = 0;
     p->cnt = ring + next;
     next += need;
   }
   if (R > 1) {
-    static double* scr = nullptr;
     static int64_t snext = 0;
-    if (!scr && hipGetSymbolAddress((void**)&scr, HIP_SYMBOL(g_red_scr)) != hipSuccess) return DFCSA_EINVAL;
     const int64_t words = (int64_t)nblk * R * ns * 64;
     if (words > kRedScr) return DFCSA_EINVAL;
     if (snext + words > kRedScr) snext = 0;
@@ -1219,7 +1266,7 @@ extern "C" int dfcsa_bn_finalize(const float* stats, int ntiles, int C, int ld, 
   if (training && red_plan(ntiles, nblk, 2, 0, &rp)) return DFCSA_EINVAL;
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(nblk, rp.R), dim3(1024), 0, (hipStream_t)stream, stats, ntiles,
                      rp.per, rp.cnt, rp.scr, C, ld, count, conv_bias, gamma, beta, running_mean, running_var, nbt, momentum,
-                     eps, training, scale, shift, mean, invstd);
+                     eps, training, scale, shift, mean, invstd, rp.acq);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1332,10 +1379,10 @@ extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum,
   if (red_plan(ntiles, nblk, nsum, third ? 1 : 0, &rp)) return DFCSA_EINVAL;
   if (nsum == 3)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
-                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, third, third ? extra : nullptr);
+                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, third, third ? extra : nullptr, rp.acq);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
-                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, nullptr, nullptr);
+                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, nullptr, nullptr, rp.acq);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -1386,7 +1433,7 @@ extern "C" int dfcsa_slab_colsum3(const float* slab, int ntiles, int C, int n0, 
   RedPlan rp;
   if (red_plan(ntiles, nblk, 1, 0, &rp)) return DFCSA_EINVAL;
   hipLaunchKernelGGL(slab_colsum_kernel, dim3(nblk, rp.R), dim3(1024), 0, (hipStream_t)stream, slab, ntiles, rp.per,
-                     rp.cnt, rp.scr, C, n0, n1, d0, d1, d2);
+                     rp.cnt, rp.scr, C, n0, n1, d0, d1, d2, rp.acq);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -2655,6 +2655,8 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 1: return g_conv_cfg;
     case 19: return g_halo_min_m;
     case 20: return g_wgrad_halo;
+    case 31: return g_wgrad_coop;
+    case 32: return g_wgrad_coop_launches;
     default: return DFCSA_EINVAL;
   }
 }
@@ -2683,6 +2685,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 27) { g_small8 = value; return 0; }
   if (knob == 28) { g_lsa_rows_old = value; return 0; }
   if (knob == 30) { g_stream_shift = value; return 0; }
+  if (knob == 31) { g_wgrad_coop = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

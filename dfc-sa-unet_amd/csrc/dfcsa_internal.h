@@ -48,6 +48,10 @@ struct WgradArgs {
   // tracks each X slot's (row, column) incrementally, 64 pixels per stage = adv_w columns and
   // adv_h rows (mod H)
   int simple, adv_w, adv_h;
+  // cooperative split-K reduction (coop = 1, the whole grid co-resident): every split publishes its
+  // partial tile, waits at the tile's ticket for the others, then reduces ONE slice of the tile over
+  // all splits in split order and adds it into dst (no slab reduction launch)
+  int coop;
 };
 
 // profiling hook (prof.cpp)
@@ -74,6 +78,8 @@ extern int g_wgrad_halo;
 extern int g_wgrad_reduce_old;
 extern int g_wgrad_nst64;
 extern int g_wgrad_bd;
+extern int g_wgrad_coop_launches;
+extern int g_wgrad_coop;   // knob 31: cooperative in-launch split-K reduction (0 = separate reduction launch)
 extern int g_small8;
 extern int g_lsa_rows_old;  // knob 28: 1 = the item-owner LightSelfAttention upsample-backward row kernel
 extern int g_wgrad_nosimple;

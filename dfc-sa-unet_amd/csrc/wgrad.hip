@@ -164,6 +164,106 @@ __device__ __forceinline__ void wgrad_epilogue(const WgradArgs& a, f32x4_t (&acc
     }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Cooperative split-K reduction (args.coop; the host enables it only when the whole grid fits on
+// the chip at once, so every split of a tile is resident or will become resident without waiting
+// for a spinning workgroup).  Each workgroup
+//   1. publishes its partial tile with write-through (sc1) stores, [tile][split][wave][frag][lane][4];
+//   2. takes an arrival ticket on the tile's counter and waits (one lane, s_sleep poll of an sc1
+//      load, bounded) until all nsplit partials are published, then one agent-scope acquire;
+//   3. reduces ONE slice of the tile -- float4 positions [split*TQ/nsplit, (split+1)*TQ/nsplit) --
+//      over all splits: the slice's positions x P parts of consecutive split ranges, each summed in
+//      split order, the parts combined in LDS in part order (fixed order: bit-identical run to
+//      run), and adds it into the weight gradient in the reference layout (each element owned by
+//      exactly one lane: no atomics);
+//   4. departs (second ticket); the last departure re-zeroes the counter for the next launch.
+// So the reduction work is spread over every workgroup of the tile (each reads as many bytes as it
+// wrote) instead of a serial last arriver or a separate reduction launch over an HBM slab.
+// A poll that exceeds kCoopSpin (~0.1 s: never in a correct launch) sets g_wgrad_coop_err and
+// proceeds -- a wrong gradient, reported by dfcsa_wgrad_coop_errors(), never a hung GPU.
+// ---------------------------------------------------------------------------------------------
+constexpr int kCoopSpin = 1 << 18;
+__device__ int g_wgrad_coop_err;
+
+template <int FM, int FN, int NW, int WN, int WTM, int WTN>
+__device__ __forceinline__ void wgrad_coop(const WgradArgs& a, f32x4_t (&acc)[FM][FN], int tile, int split, int i0,
+                                           int j0, int lane, int wave, int tid, float* lds) {
+  constexpr int NF = FM * FN;
+  constexpr int TILEF = NW * NF * 256;   // floats of one partial tile
+  constexpr int TQ = TILEF / 4;          // float4 positions
+  constexpr int NT = NW * 64;
+  const int ns = a.nsplit;
+  float* tb = a.slab + (size_t)tile * ns * TILEF;
+  {
+    float* mine = tb + (size_t)split * TILEF + (size_t)(wave * NF) * 256 + lane * 4;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) st_sc1_x4(mine + f * 256, acc[f / FN][f % FN]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0) {
+    __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int it = 0;
+    while (__hip_atomic_load(a.cnt + tile, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)ns) {
+      __builtin_amdgcn_s_sleep(2);
+      if (++it > kCoopSpin) {
+        __hip_atomic_store(&g_wgrad_coop_err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+  const int q0 = (int)((int64_t)split * TQ / ns), q1 = (int)((int64_t)(split + 1) * TQ / ns);
+  const int q = q1 - q0;
+  if (q > 0) {
+    const int P = q >= NT ? 1 : NT / q;                // parts (split ranges) per position
+    const int part = q >= NT ? 0 : tid / q;
+    const int s0 = (int)((int64_t)part * ns / P), s1 = (int)((int64_t)(part + 1) * ns / P);
+    f32x4_t* red = (f32x4_t*)lds;                      // [P][q] partial sums when P > 1
+    for (int p = (q >= NT ? tid : tid % q); p < q && part < P; p += (q >= NT ? NT : q)) {
+      const float* src = tb + (size_t)(q0 + p) * 4;
+      f32x4_t sum = {0.f, 0.f, 0.f, 0.f};
+      for (int s = s0; s < s1; s += 4) {
+        f32x4_t v[4];
+        const float* ptr[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) ptr[u] = src + (size_t)min(s + u, s1 - 1) * TILEF;
+        ld_sc1_x4x4(ptr[0], ptr[1], ptr[2], ptr[3], v[0], v[1], v[2], v[3]);
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if (s + u < s1) sum += v[u];
+      }
+      if (P > 1) red[part * q + p] = sum;
+      else {
+        // position -> (wave, fragment, lane) of the accumulator layout -> (row, column)
+        const int pw = (q0 + p) / (NF * 64), pf = ((q0 + p) / 64) % NF, pl = (q0 + p) & 63;
+        const int row = i0 + (pw / WN) * WTM + (pf / FN) * 16 + (pl >> 4) * 4;
+        const int col = j0 + (pw % WN) * WTN + (pf % FN) * 16 + (pl & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wgrad_dst_add(a, row + r, col, sum[r]);
+      }
+    }
+    if (P > 1) {
+      __syncthreads();
+      for (int p = tid; p < q; p += NT) {
+        f32x4_t sum = red[p];
+        for (int u = 1; u < P; ++u) sum += red[u * q + p];
+        const int pw = (q0 + p) / (NF * 64), pf = ((q0 + p) / 64) % NF, pl = (q0 + p) & 63;
+        const int row = i0 + (pw / WN) * WTM + (pf / FN) * 16 + (pl >> 4) * 4;
+        const int col = j0 + (pw % WN) * WTN + (pf % FN) * 16 + (pl & 15);
+#pragma unroll
+        for (int r = 0; r < 4; ++r) wgrad_dst_add(a, row + r, col, sum[r]);
+      }
+    }
+  }
+  __syncthreads();
+  if (tid == 0) {
+    const unsigned old = __hip_atomic_fetch_add(a.cnt + tile, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == (unsigned)(2 * ns - 1)) __hip_atomic_store(a.cnt + tile, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 // bf16: rows of BW channels = BW*2 bytes; chunk (8 channels) ch of row r
 template <int BW>
@@ -544,6 +644,10 @@ __global__ void __launch_bounds__(WM * WN * 64) wgrad_glds_kernel(const WgradArg
     }
   }
 
+  if (args.coop) {
+    wgrad_coop<FM, FN, NW, WN, WTM, WTN>(args, acc, L % (nJ * nI), split, i0, j0, lane, wave, tid, (float*)smem);
+    return;
+  }
   wgrad_epilogue<FM, FN, NW>(args, acc, L % (nJ * nI), split, i0 + wm * WTM, j0 + wn * WTN, lane, wave, tid,
                              (int*)smem);
 }
@@ -719,6 +823,10 @@ __global__ void __launch_bounds__(512) wgrad_bd_kernel(const WgradArgs args, int
     }
   }
   __syncthreads();
+  if (args.coop) {
+    wgrad_coop<FM, FN, NW, WN, WTM, WTN>(args, acc, L % (nJ * nI), split, i0, j0, lane, wave, tid, (float*)smem);
+    return;
+  }
   wgrad_epilogue<FM, FN, NW>(args, acc, L % (nJ * nI), split, i0 + wm * WTM, j0 + wn * WTN, lane, wave, tid,
                              (int*)smem);
 }
@@ -1214,9 +1322,64 @@ inline int wgrad_nst(const WgradArgs& a, int BI) {
   return g_wgrad_nst;
 }
 
+// ticket counters for `tiles` output tiles of one launch: a region of the ring per launch, so launches
+// in flight on other streams never share one (each tile's counter is zero on entry and re-zeroed by
+// the launch itself)
+unsigned* wgrad_cnt_region(int tiles) {
+  static unsigned* ring = nullptr;
+  static int next = 0;
+  if (tiles > kCntRing) return nullptr;
+  if (!ring && hipGetSymbolAddress((void**)&ring, HIP_SYMBOL(g_wg_cnt)) != hipSuccess) return nullptr;
+  if (next + tiles > kCntRing) next = 0;
+  unsigned* r = ring + next;
+  next += tiles;
+  return r;
+}
+
+}  // namespace
+int g_wgrad_coop_launches = 0;   // host count of cooperative launches (dfcsa_get_tuning(32), tests)
+namespace {
+
+// workgroups of `kern` (at `threads` per workgroup) that fit on the device at once (cached)
+template <typename K>
+int coop_capacity(K kern, int threads) {
+  static int cached[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
+  if (!cached[dev]) {
+    int nb = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kern, threads, 0) != hipSuccess) return 0;
+    if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return 0;
+    cached[dev] = nb * cus > 0 ? nb * cus : -1;
+  }
+  return cached[dev] > 0 ? cached[dev] : 0;
+}
+
+// launch `kern` on `grid` workgroups, with the cooperative split-K reduction when asked for and the
+// whole grid fits on the device at once (otherwise the caller's separate reduction runs)
+template <typename K>
+int launch_wg(K kern, int grid, int threads, int BI, int BJ, const WgradArgs& a0, int splits, bool want_coop,
+              bool* coop_used, hipStream_t st) {
+  WgradArgs a = a0;
+  a.coop = 0;
+  if (want_coop && splits > 1 && grid <= coop_capacity(kern, threads)) {
+    const int tiles = ((a.NI + BI - 1) / BI) * ((a.NJ + BJ - 1) / BJ);
+    if ((a.cnt = wgrad_cnt_region(tiles)) != nullptr) {
+      a.coop = 1;
+      a.nsplit = splits;
+    }
+  }
+  *coop_used = a.coop != 0;
+  g_wgrad_coop_launches += a.coop;
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(threads), 0, st, a, splits);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
 template <typename T, int BI>
-int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
+int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st, bool want_coop, bool* coop_used) {
   constexpr int BJ = 128;
+  *coop_used = false;
   dim3 grid((a.NJ + BJ - 1) / BJ, (a.NI + BI - 1) / BI, splits);
   // 8 waves (32x64 wave tiles) hide more latency: LDS-DMA + 8 waves measured best or equal on
   // every shape of the step (tools/wgrad_bench.py; 5-15 % on the 3x3 layers)
@@ -1225,47 +1388,38 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
     if (!g_wgrad_noglds) {
       if (const int bm = wgrad_big_mode(a.NI, a.NJ, g_wgrad_big)) {
         const int bi = bm == 3 ? 128 : 256, bj = bm == 2 ? 128 : 256;
-        dim3 gb(xcd_pad(((a.NJ + bj - 1) / bj) * ((a.NI + bi - 1) / bi) * splits));
-        if (bm == 1) hipLaunchKernelGGL((wgrad_glds_kernel<256, 256, 2, 4, 2>), gb, dim3(512), 0, st, a, splits);
-        else if (bm == 2) hipLaunchKernelGGL((wgrad_glds_kernel<256, 128, 4, 2, 2>), gb, dim3(512), 0, st, a, splits);
-        else hipLaunchKernelGGL((wgrad_glds_kernel<128, 256, 2, 4, 2>), gb, dim3(512), 0, st, a, splits);
-        DFCSA_CHECK_LAUNCH();
-        return 0;
+        const int gb = xcd_pad(((a.NJ + bj - 1) / bj) * ((a.NI + bi - 1) / bi) * splits);
+        if (bm == 1)
+          return launch_wg(wgrad_glds_kernel<256, 256, 2, 4, 2>, gb, 512, bi, bj, a, splits, want_coop, coop_used, st);
+        if (bm == 2)
+          return launch_wg(wgrad_glds_kernel<256, 128, 4, 2, 2>, gb, 512, bi, bj, a, splits, want_coop, coop_used, st);
+        return launch_wg(wgrad_glds_kernel<128, 256, 2, 4, 2>, gb, 512, bi, bj, a, splits, want_coop, coop_used, st);
       }
       // buffer-descriptor kernel on 64-channel sub-images (knob 26 = 0: the pointer-DMA kernel)
       if (g_wgrad_bd && a.simple && a.Cseg % 64 == 0 && a.Cg % 64 == 0 && !wide_j(a) &&
-          (int64_t)a.M * a.Cseg * 2 < (1ll << 31) && (int64_t)a.M * a.Cg * 2 < (1ll << 31)) {
-        dim3 gb(xcd_pad(grid.x * grid.y * splits));
-        hipLaunchKernelGGL((wgrad_bd_kernel<BI, 2>), gb, dim3(512), 0, st, a, splits);
-        DFCSA_CHECK_LAUNCH();
-        return 0;
-      }
-      // 1-D grid (x = padded tile count, y = splits count carrier): see the XCD remap in the kernel
-      if (BI == 64 && wide_j(a)) {
-        dim3 g2(xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits), splits);
-        g2.y = 1;
-        hipLaunchKernelGGL((wgrad_glds_kernel<64, 256, 2, 4, 2>), g2, dim3(512), 0, st, a, splits);
-      } else {
-        dim3 g1(xcd_pad(grid.x * grid.y * splits));
-        constexpr int WM8 = BI == 64 ? 2 : 4, WN8 = BI == 64 ? 4 : 2;
-        const int nst = wgrad_nst(a, BI);
-        if (waves == 8 && nst >= 4 && a.simple)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4, true>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8 && nst >= 4)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 4>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8 && nst == 3 && a.simple)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3, true>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8 && nst == 3)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 3>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8 && a.simple)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2, true>), g1, dim3(512), 0, st, a, splits);
-        else if (waves == 8)
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, WM8, WN8, 2>), g1, dim3(512), 0, st, a, splits);
-        else
-          hipLaunchKernelGGL((wgrad_glds_kernel<BI, BJ, 2, 2, 2>), g1, dim3(256), 0, st, a, splits);
-      }
-      DFCSA_CHECK_LAUNCH();
-      return 0;
+          (int64_t)a.M * a.Cseg * 2 < (1ll << 31) && (int64_t)a.M * a.Cg * 2 < (1ll << 31))
+        return launch_wg(wgrad_bd_kernel<BI, 2>, xcd_pad(grid.x * grid.y * splits), 512, BI, BJ, a, splits, want_coop,
+                         coop_used, st);
+      // 1-D grid (x = padded tile count): see the XCD remap in the kernel
+      if (BI == 64 && wide_j(a))
+        return launch_wg(wgrad_glds_kernel<64, 256, 2, 4, 2>, xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits),
+                         512, BI, 256, a, splits, want_coop, coop_used, st);
+      const int g1 = xcd_pad(grid.x * grid.y * splits);
+      constexpr int WM8 = BI == 64 ? 2 : 4, WN8 = BI == 64 ? 4 : 2;
+      const int nst = wgrad_nst(a, BI);
+      if (waves == 8 && nst >= 4 && a.simple)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 4, true>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      if (waves == 8 && nst >= 4)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 4>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      if (waves == 8 && nst == 3 && a.simple)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 3, true>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      if (waves == 8 && nst == 3)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 3>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      if (waves == 8 && a.simple)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 2, true>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      if (waves == 8)
+        return launch_wg(wgrad_glds_kernel<BI, BJ, WM8, WN8, 2>, g1, 512, BI, BJ, a, splits, want_coop, coop_used, st);
+      return launch_wg(wgrad_glds_kernel<BI, BJ, 2, 2, 2>, g1, 256, BI, BJ, a, splits, want_coop, coop_used, st);
     }
   }
   if (waves == 8)
@@ -1280,6 +1434,7 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st) {
 
 int g_small8 = 1;            // knob 27: 0 = the 4-wave small fp32 GEMM tiles (LightSelfAttention projections)
 int g_wgrad_bd = 1;          // knob 26: buffer-descriptor wgrad kernel (simple geometry)
+int g_wgrad_coop = 0;        // knob 31: cooperative in-launch split-K reduction when the grid fits the chip
 int g_wgrad_nst64 = 0;       // knob 24: ring depth of the 64-row tiles (0 = follow knob 14)
 int g_wgrad_reduce_old = 0;  // knob 23: 1 = the element-order reduction for every split count
 int g_wgrad_halo = 0;      // knob 20: 1 = 3x3 weight gradients on the 2-D halo-tile kernel (off: slower so far)
@@ -1314,6 +1469,18 @@ void wgrad_tile(int NI, int NJ, int dtype, int* BI, int* BJ) {
 }
 
 extern "C" int dfcsa_wgrad_fuse_max(void) { return g_wgrad_fuse_max; }
+
+extern "C" int dfcsa_wgrad_coop_errors(int reset) {
+  int v = 0;
+  if (hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_wgrad_coop_err), sizeof(int), 0, hipMemcpyDeviceToHost) != hipSuccess)
+    return DFCSA_EINVAL;
+  if (reset && v) {
+    const int z = 0;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_wgrad_coop_err), &z, sizeof(int), 0, hipMemcpyHostToDevice) != hipSuccess)
+      return DFCSA_EINVAL;
+  }
+  return v;
+}
 
 namespace {
 void desc_to_args(const dfcsa_wgrad_desc* d, WgradArgs& a) {
@@ -1411,21 +1578,20 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   if (!a.fuse && !d->slab) return DFCSA_EINVAL;
   if (!a.fuse && d->slab_floats < (int64_t)d->splits * a.NI * a.NJ) return DFCSA_EINVAL;
   a.cnt = nullptr;
-  if (a.fuse && d->splits > 1) {
-    // ticket counters: a ring region per launch, so launches in flight on other streams never
-    // share one (each tile's last arriver re-zeroes its counter)
-    static unsigned* ring = nullptr;
-    static int next = 0;
-    if (!ring && hipGetSymbolAddress((void**)&ring, HIP_SYMBOL(g_wg_cnt)) != hipSuccess) return DFCSA_EINVAL;
+  a.coop = 0;
+  bool want_coop = false;
+  {
     int BI, BJ;
     wgrad_tile(a.NI, a.NJ, d->dtype, &BI, &BJ);
     const int tiles = ((a.NI + BI - 1) / BI) * ((a.NJ + BJ - 1) / BJ);
-    if (tiles > kCntRing) return DFCSA_EINVAL;
-    // the in-kernel reduction writes tiled partials [tile][split][BI][BJ] into the slab
-    if (!d->slab || d->slab_floats < (int64_t)tiles * d->splits * BI * BJ) return DFCSA_EINVAL;
-    if (next + tiles > kCntRing) next = 0;
-    a.cnt = ring + next;
-    next += tiles;
+    const bool tiled_fits = d->slab && d->slab_floats >= (int64_t)tiles * d->splits * BI * BJ;
+    if (a.fuse && d->splits > 1) {
+      // the in-kernel reduction writes tiled partials [tile][split][BI][BJ] into the slab
+      if (!tiled_fits) return DFCSA_EINVAL;
+      if (!(a.cnt = wgrad_cnt_region(tiles))) return DFCSA_EINVAL;
+    }
+    // cooperative reduction (bf16 tile kernels; the launch function checks that the grid fits)
+    want_coop = g_wgrad_coop && !a.fuse && d->ndst > 0 && d->splits > 1 && d->dtype == DFCSA_DT_BF16 && tiled_fits;
   }
   hipStream_t st = (hipStream_t)stream;
   double flops = 2.0 * a.M * a.NI * a.NJ;
@@ -1461,12 +1627,15 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
     return 0;
   }
   int rc;
+  bool coop = false;
   if (d->dtype == DFCSA_DT_BF16)
-    rc = a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st) : launch_wgrad<bf16_t, 128>(a, d->splits, st);
+    rc = a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st, want_coop, &coop)
+                    : launch_wgrad<bf16_t, 128>(a, d->splits, st, want_coop, &coop);
   else
-    rc = a.NI <= 64 ? launch_wgrad<float, 64>(a, d->splits, st) : launch_wgrad<float, 128>(a, d->splits, st);
+    rc = a.NI <= 64 ? launch_wgrad<float, 64>(a, d->splits, st, false, &coop)
+                    : launch_wgrad<float, 128>(a, d->splits, st, false, &coop);
   if (rc) return rc;
-  if (d->ndst > 0 && !a.fuse)
+  if (d->ndst > 0 && !a.fuse && !coop)
     return launch_reduce(d->slab, d->splits, a.NI, a.NJ, d->layout, d->ntaps, d->Ctot, d->Creal, d->ndst, a.dst[0],
                          a.dst[1], a.dst[2], st);
   return 0;

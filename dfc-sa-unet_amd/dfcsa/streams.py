@@ -19,17 +19,25 @@ _SIDE = {}
 _JOIN_QUEUED = [False]
 import os
 
-# Off by default: the overlapped wgrad GEMMs contend with the dgrad chain for CUs/LDS/L2 about as
-# much as they fill idle time (round 1: 979 vs 1044 img/s; round 2 with the branch stream, same-box
-# A/B: 1245 on vs 1251 off).  DFCSA_SIDE_STREAM=1 enables.
-ENABLED = [os.environ.get("DFCSA_SIDE_STREAM", "0") == "1"]
+# On by default since round 4: with the round-3 kernels the backward's dgrad chain is a string of
+# latency-bound launches (BatchNorm finalizers on 1-16 workgroups, the pooled-attention backward on
+# 16-224) that leave most CUs idle, and the HBM-streaming weight-gradient GEMMs fill them (same-box
+# A/B of the default bench: 1497 / 1499 on vs 1469 / 1473 img/s off; round 2, when the dgrad chain
+# was GEMM-bound: 1245 on vs 1251 off).  DFCSA_SIDE_STREAM=0 disables.
+ENABLED = [os.environ.get("DFCSA_SIDE_STREAM", "1") == "1"]
+
+
+# HIP stream priorities (torch: lower value = higher priority): the weight-gradient side stream and
+# the attention branch stream are created with these (DFCSA_PRIO_SIDE / DFCSA_PRIO_BRANCH)
+PRIO_SIDE = int(os.environ.get("DFCSA_PRIO_SIDE", "0"))
+PRIO_BRANCH = int(os.environ.get("DFCSA_PRIO_BRANCH", "0"))
 
 
 def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        s = torch.cuda.Stream(device=idx, priority=PRIO_SIDE)
         _SIDE[idx] = s
     return s
 
@@ -86,7 +94,7 @@ def branch_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _BRANCH.get(idx)
     if s is None:
-        s = torch.cuda.Stream(device=idx)
+        s = torch.cuda.Stream(device=idx, priority=PRIO_BRANCH)
         _BRANCH[idx] = s
     return s
 

@@ -116,6 +116,12 @@ int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk,
  * own pixel-range split count; everything else as dfcsa_wgrad_plan */
 int dfcsa_wgrad_plan_desc(const dfcsa_wgrad_desc* d, int* splits, int* mchunk, int64_t* slab_floats);
 int dfcsa_wgrad_fuse_max(void);
+/* Split-K weight gradients whose grid fits on the device at once reduce their partials INSIDE the
+ * launch (cooperative: every split reduces one slice of its tile over all splits, in split order;
+ * tuning knob 31 = 0 selects the separate dfcsa_wgrad_reduce launch).  A wait that exceeded its
+ * bound (never in a correct launch) is recorded instead of hanging: returns the sticky error flag
+ * (0 = none) and clears it when reset != 0.  Synchronous (reads a device word). */
+int dfcsa_wgrad_coop_errors(int reset);
 int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
 /* grad += sum_s slab[s] (slab [splits][NI][NJ]) mapped to the reference weight layout.
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin

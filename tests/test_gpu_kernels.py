@@ -138,6 +138,51 @@ def test_wgrad_fused_split_reduction(dtype, B, Cs, C, H, fuse_all):
     assert torch.equal(outs[0], outs[1]), "fused split-K reduction is not bitwise reproducible"
 
 
+@pytest.mark.parametrize("B,Cs,nsrc,C,H,W,taps", [(16, 64, 2, 64, 56, 56, 1), (16, 64, 1, 128, 56, 56, 1),
+                                                   (8, 64, 2, 64, 28, 28, 9), (4, 512, 1, 256, 14, 14, 9),
+                                                   (4, 256, 3, 512, 14, 14, 1), (3, 64, 1, 72, 17, 13, 9)])
+def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
+    """Split-K weight gradients reduced INSIDE the launch (knob 31, default on when the grid fits the
+    chip): every split reduces one slice of its tile over all splits in split order.  bf16-exact
+    operands against torch fp32 (1e-5: fp32 accumulation only), the separate slab reduction (knob 31 =
+    0) to 1e-6, bitwise repeatable, accumulating into the gradient, no bounded wait ever exceeded.
+    Shapes: the 224^2-like many-split 1x1 (hundreds of splits of one tile), multi-source 3x3, the deep
+    3x3 with few splits, ragged channel counts (C = 72)."""
+    import dfcsa
+    from dfcsa._lib import LIB
+    torch.manual_seed(11)
+    dtype = torch.bfloat16
+    xs = [q(torch.randn(B, Cs, H, W), dtype) for _ in range(nsrc)]
+    g = q(torch.randn(B, C, H, W), dtype)
+    w = torch.zeros(C, nsrc * Cs, 3 if taps == 9 else 1, 3 if taps == 9 else 1, requires_grad=True)
+    F.conv2d(torch.cat(xs, 1), w, padding=1 if taps == 9 else 0).backward(g)
+    ref = w.grad + 0.5
+    xh = [nhwc(t, dtype) for t in xs]
+    gh = nhwc(g, dtype)
+    segs = ([(t, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for t in xh] if taps == 9
+            else [(t, 0, 0) for t in xh])
+    LIB.dfcsa_wgrad_coop_errors(1)
+    outs = {}
+    try:
+        for coop in (1, 0, 1):
+            dfcsa.set_tuning(31, coop)
+            before = LIB.dfcsa_get_tuning(32)
+            gw = torch.full(w.shape, 0.5, device="cuda")
+            ops.conv_wgrad_into(dtype, [gh], C, segs, Cs, (B, H, W), (H, W), [gw], taps, nsrc * Cs, nsrc * Cs)
+            torch.cuda.synchronize()
+            used = LIB.dfcsa_get_tuning(32) - before
+            outs.setdefault(coop, []).append((gw, used))
+    finally:
+        dfcsa.set_tuning(31, 1)
+    assert LIB.dfcsa_wgrad_coop_errors(1) == 0
+    (a, ua), (b, _) = outs[1]
+    (c, uc), = outs[0]
+    assert ua >= 1 and uc == 0, (ua, uc)
+    assert rel(a, ref) < 1e-5, rel(a, ref)
+    assert rel(a, c) < 1e-6, rel(a, c)
+    assert torch.equal(a, b), "cooperative split-K reduction is not bitwise reproducible"
+
+
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-6), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,Cs,nsrc,C,H,W", [(2, 8, 1, 16, 9, 7), (3, 64, 2, 64, 14, 14), (2, 32, 1, 136, 20, 20)])
 @pytest.mark.parametrize("variant", [(0, 0, 1), (1, 4, 1), (1, 8, 1), (0, 4, 1), (0, 8, 0)])  # knobs 7, 6, 8

@@ -249,7 +249,7 @@ def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32):
     torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
     _, _, gref, _ = O.forward_backward(sd0, x.cpu(), t.cpu(), pool, LP)
     sd1, _, _, _ = O.clip_and_sgd(sd0, gref, {})
-    rows, fails = [], []
+    rows, fails, scal = [], [], []
     sm = {"err": 0.0, "ac": 0.0, "uerr": 0.0, "uac": 0.0}
     for n in O.param_names(sd0):
         if n.endswith(ZERO):
@@ -268,7 +268,12 @@ def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32):
             sm["ac"] += (ac_rel * gn) ** 2
             sm["uerr"] += uerr ** 2
             sm["uac"] += (ac_urel * upd_ref.norm().item()) ** 2
-            ok = rr <= 5 * ac_rel + 2e-2 and ur <= 5 * ac_urel + 2e-2
+            if pre[n].numel() == 1:
+                # a scalar (gamma, res_scale): judged below against the pooled autocast noise
+                scal.append((n, rr * gn, ac_rel * gn, uerr, ac_urel * upd_ref.norm().item()))
+                ok = True
+            else:
+                ok = rr <= 5 * ac_rel + 2e-2 and ur <= 5 * ac_urel + 2e-2
         else:
             ok = rr <= max(1.25 * ac_rel, 2e-2) and 1 - cs <= 1.25 * (1 - ac_cos) + 1e-3
             if ur > max(1.25 * ac_urel, 2e-2):
@@ -282,6 +287,18 @@ def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32):
     print(f"{tag} bf16 step, every tensor relative to the reference autocast (worst first):")
     for r in rows:
         print("   ", r[2])
+    # scalars: each is ONE cancelling sum over B*H*W pixels, so one autocast distance is a single draw
+    # of the bf16 noise (cfg2: 0.02 .. 6.3 relative across the 18 of them); the sanity bar per scalar
+    # is 5 x the autocast's absolute error pooled (RMS) over all the model's scalars, for the gradient
+    # and for the SGD update
+    if scal:
+        ac_g = (sum(c[2] ** 2 for c in scal) / len(scal)) ** 0.5
+        ac_u = (sum(c[4] ** 2 for c in scal) / len(scal)) ** 0.5
+        print(f"{tag} bf16 step, scalars: pooled autocast abs error gradient {ac_g:.3e}, update {ac_u:.3e}")
+        for n, eg, _, eu, _ in scal:
+            if eg > 5 * ac_g or eu > 5 * ac_u + 1e-12:
+                fails.append(f"{n}: abs gradient error {eg:.3e} (pooled autocast {ac_g:.3e}), update {eu:.3e} "
+                             f"(pooled autocast {ac_u:.3e})")
     g_small, g_ac = sm["err"] ** 0.5, sm["ac"] ** 0.5
     u_small, u_ac = sm["uerr"] ** 0.5, sm["uac"] ** 0.5
     print(f"{tag} bf16 step, small tensors as one vector: gradient error {g_small:.4e} (autocast {g_ac:.4e}), "
@@ -320,8 +337,10 @@ def test_cfg2_geometry_bf16_train_step_vs_reference_autocast():
         small, heavily cancelling sum, so one tensor's distance is a single noise sample (the
         autocast's own distance on down4's gamma is 6.3).  They are pinned as ONE vector:
         || ours - fp32 || <= 1.25 x || autocast - fp32 || over all of them (the autocast's per-tensor
-        distances recombined exactly: sum_i (ac_rel_i * ||g_i||)^2), each tensor within 5 x its
-        autocast distance + 2e-2 as a sanity bar, and the same for the SGD update;
+        distances recombined exactly: sum_i (ac_rel_i * ||g_i||)^2), each vector tensor within 5 x its
+        autocast distance + 2e-2 as a sanity bar, each scalar within 5 x the autocast's absolute
+        error pooled (RMS) over the model's scalars (one scalar's autocast distance is a single
+        noise draw), and the same for the SGD update;
       * over the whole gradient vector: no worse than the autocast;
       * BatchNorm running statistics after the step vs the reference fp32 step (cfg2_step.npz):
         <= max(1.25 x the autocast's distance, 1e-3);

@@ -1,7 +1,7 @@
 # A/B of environment settings on the bench (same box, 2 rounds): gpu_ab_envs.sh "<label>:<VAR=v VAR2=v2>" ...
 mkdir -p gpurun_out
 cd $GRAFT_REPO_ROOT
-B="--no-cpu-baseline --no-val-dice --no-trainer-faithful"
+B="--no-cpu-baseline --no-val-dice --no-trainer-faithful --no-kernel-timing --steps 40"
 for rep in 1 2; do
   for arm in "$@"; do
     lab=${arm%%:*}; envs=${arm#*:}
