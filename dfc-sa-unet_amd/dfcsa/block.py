@@ -54,6 +54,11 @@ PAIR_WGRAD = [os.environ.get("DFCSA_PAIR_WGRAD", "1") == "1"]
 # 1409 vs 1434): the last arriver's write-through hand-off costs more than the launches it saves
 # (profiles/r03b_ab_lsa_core_bwd.jsonl)
 LSA_CORE_BWD = [os.environ.get("DFCSA_LSA_CORE_BWD", "0") == "1"]
+# backward: DFCSA_DX_FIRST=1 issues the block input-gradient GEMM before the input-side weight
+# gradients on the side stream (default: after them).  Same-box A/B, 150 steps x 3: 1526 / 1528 /
+# 1526 img/s first against 1550 / 1540 / 1547 after -- the weight gradients started early overlap the
+# latency-bound stretches that follow better than they hurt the dgrad they start beside
+DX_FIRST = [os.environ.get("DFCSA_DX_FIRST", "0") == "1"]
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -436,6 +441,21 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     del dlocal
     join_branch(dev, branch, dy2)
 
+    # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM (critical path) ----
+    # (order against the side-stream weight gradients: DX_FIRST)
+    dxs = None
+
+    def input_grad():
+        Kx = rup(11 * C, ops.KALIGN)
+        Wdx = s.pk["Wdx"]  # [W1^T | W2^T | Wres^T or I] side by side
+        segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dy2, 0, 0), (dres, 0, 0)]
+        out = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
+        ops.conv_gemm(dtype, segs, C, grid, hw, Wdx, Kx, Cin_p, out, Cs)
+        return out
+
+    if need_dx and DX_FIRST[0]:
+        dxs = input_grad()
+
     # ---- weight gradients of the input-side convs (side stream) ----
     xs = s.xs
     with on_side(dev, dy1, dy2, dres, *xs):
@@ -447,15 +467,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         else:
             ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw, [grad_of(conv2.weight)], 1,
                                 Cin_p, Cin_real)
-    if not need_dx:
-        return None
-
-    # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM ----
-    Kx = rup(11 * C, ops.KALIGN)
-    Wdx = s.pk["Wdx"]  # [W1^T | W2^T | Wres^T or I] side by side
-    segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dy2, 0, 0), (dres, 0, 0)]
-    dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
-    ops.conv_gemm(dtype, segs, C, grid, hw, Wdx, Kx, Cin_p, dxs, Cs)
+    if need_dx and not DX_FIRST[0]:
+        dxs = input_grad()
     return dxs
 
 

@@ -111,13 +111,18 @@ class ConvTranspose2x2(torch.autograd.Function):
         Cout = mod.out_channels
         g = g.contiguous()
         segs = [(g, i, j) for i in range(2) for j in range(2)]
-        # weight / bias gradients (side stream)
+        # input gradient first (critical path), then the weight / bias gradients on the side stream
+        # (see dfcsa.block.block_backward: the dgrad launched first keeps its CUs)
+        from .block import DX_FIRST
+        dx = None
+        if ctx.needs_input_grad[0] and DX_FIRST[0]:
+            dx = torch.empty_like(x)
+            ops.conv_gemm(dtype, segs, Cout, (B, h, w), (2 * h, 2 * w), ctx.Wb, ctx.Kb, Cin, [dx], Cin, stride=2)
         with on_side(x.device, x, g):
             ops.conv_wgrad_into(dtype, [x], Cin, segs, Cout, (B, h, w), (2 * h, 2 * w), [grad_of(mod.weight)],
                                 ntaps=4, Ctot=Cout, Creal=Cout, layout=1, stride=2)
             ops.channel_sum_into(dtype, g, grad_of(mod.bias))
-        dx = None
-        if ctx.needs_input_grad[0]:
+        if ctx.needs_input_grad[0] and not DX_FIRST[0]:
             dx = torch.empty_like(x)
             ops.conv_gemm(dtype, segs, Cout, (B, h, w), (2 * h, 2 * w), ctx.Wb, ctx.Kb, Cin, [dx], Cin, stride=2)
         notify_grads_ready(mod)

@@ -1,8 +1,8 @@
 # A/B of environment settings on the bench (same box, 2 rounds): gpu_ab_envs.sh "<label>:<VAR=v VAR2=v2>" ...
 mkdir -p gpurun_out
 cd $GRAFT_REPO_ROOT
-B="--no-cpu-baseline --no-val-dice --no-trainer-faithful --no-kernel-timing --steps 40"
-for rep in 1 2; do
+B="--no-cpu-baseline --no-val-dice --no-trainer-faithful --no-kernel-timing --steps 150 --warmup 10"
+for rep in 1 2 3; do
   for arm in "$@"; do
     lab=${arm%%:*}; envs=${arm#*:}
     env $envs timeout -k 10 300 python bench.py $B > gpurun_out/ab_${lab}_$rep.json 2> gpurun_out/ab_${lab}_$rep.err || { echo "bench $lab failed"; exit 1; }
