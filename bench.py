@@ -184,7 +184,7 @@ def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
     xva, tva = stack(SyntheticEllipses(n_val, (img, img), seed=43), n_val)
     torch.manual_seed(0)
     model = ModelFactory.get_model(cfg).to(dev).train()
-    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4, zero_after_step=True)
     g = torch.Generator().manual_seed(7)
     for s in range(steps):
         idx = torch.randint(0, n_train, (batch,), generator=g).to(dev)
@@ -258,7 +258,7 @@ def main():
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):   # the factory's messages: stdout carries ONE JSON line
         model = ModelFactory.get_model(cfg).to(dev).train()
-    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
+    opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4, zero_after_step=True)
 
     B, S = args.batch, args.img
     gb = B * world

@@ -52,6 +52,8 @@ struct WgradArgs {
   // partial tile, waits at the tile's ticket for the others, then reduces ONE slice of the tile over
   // all splits in split order and adds it into dst (no slab reduction launch)
   int coop;
+  // layout 2: bias gradients (column sums of G) added by the small fp32 kernel, bdst[0] != NULL
+  float* bdst[3];
 };
 
 // profiling hook (prof.cpp)

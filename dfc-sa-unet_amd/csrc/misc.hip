@@ -431,8 +431,20 @@ __device__ __forceinline__ void store_as(void* out, int64_t i, int dtype, float 
   else ((float*)out)[i] = v;
 }
 
+// LDS slot of staged element s in the ROWS case: one pad float after every q = 8*ntaps floats.
+// A lane reads 8 consecutive ci of one tap (a stride of ntaps), the lanes of a group a stride of
+// 8*ntaps apart: unpadded, 1x1-like and 2x2 (ConvTranspose) rows put 4-32 lanes on one bank; padded,
+// rows of >= 128 channels are conflict-free (<= 2-way below).  s < 4096 and q <= 8*49, so the
+// float quotient is exact.
+__device__ __forceinline__ int rows_slot(int s, float rq) { return s + (int)(((float)s + 0.5f) * rq); }
+// 64 x 64 transpose tile: row stride 69 (odd, >= 64 + 4) plus 4 words after 32 rows and after
+// 32 columns, so the 8-wide row chunks written by a ds_write_b32 group (4 rows x 8 chunks) and the
+// 8-row column chunks it reads (4 columns x 8 chunks) both fall on 32 distinct banks, and so do
+// the scalar path's rows (32 columns) and columns (32 rows, stride 69 = 5 mod 32)
+__device__ __forceinline__ int tile_at(int r, int c) { return r * 69 + c + 4 * ((r >> 5) + (c >> 5)); }
+
 __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* __restrict__ tab, int n) {
-  __shared__ float tile[64][65];
+  __shared__ float smem[4420];   // ROWS: 4096 staged floats + pads (q >= 16); TRANSPOSE: tile_at < 4420
   const int64_t task = blockIdx.x;
   // last entry with start <= task = (number of entries with start <= task) - 1 (starts ascend,
   // start[0] = 0): every lane tests four entries per 256, all loads in flight, counted by ballot
@@ -458,15 +470,34 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
       // longer than 4096 floats, one row's input-channel chunk) are a contiguous source block of
       // <= 4096 floats: it is staged in LDS by sixteen unconditional loads per lane, all in flight
       // (clamped index past the end), and written in output order (consecutive ci: coalesced),
-      // reading LDS at a stride of ntaps.
+      // reading LDS at a stride of ntaps (padded, rows_slot).  A 1x1 conv (ntaps = 1) is a plain
+      // row copy and skips the staging.
       const int Cout = a[0], Cin = a[1], ntaps = a[2], Cpad = a[3], Kpad = a[4], row0 = a[5], per = a[6];
       const int nrow = Cin * ntaps;
       const int co0 = (int)tl * per, nr = min(per, Cout - co0);
+      const float* __restrict__ w = t.w0;
       const bool vec = t.dtype == DFCSA_DT_BF16 && Cin % 8 == 0 && Cpad % 8 == 0 && Kpad % 8 == 0 &&
                        ((uintptr_t)t.out & 15) == 0;
+      if (ntaps == 1) {
+        const float* __restrict__ src = w + (size_t)co0 * Cin;
+        const int n1 = nr * Cin;
+        if (vec && ((uintptr_t)w & 15) == 0) {
+          for (int o = tid * 8; o < n1; o += 256 * 8) {
+            const int r = o / Cin, ci = o - r * Cin;
+            const float4 x0 = *(const float4*)(src + o), x1 = *(const float4*)(src + o + 4);
+            const float v8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+            store8<bf16_t>((bf16_t*)t.out + (int64_t)(row0 + co0 + r) * Kpad + ci, v8);
+          }
+        } else {
+          for (int o = tid; o < n1; o += 256) {
+            const int r = o / Cin, ci = o - r * Cin;
+            store_as(t.out, (int64_t)(row0 + co0 + r) * Kpad + ci, t.dtype, src[o]);
+          }
+        }
+        break;
+      }
       const int ccmax = nrow <= 4096 ? Cin : max(vec ? 8 : 1, (4096 / ntaps) & (vec ? ~7 : ~0));
-      float* buf = &tile[0][0];   // 4160 floats
-      const float* __restrict__ w = t.w0;
+      const float rq = 1.f / (float)(8 * ntaps);
       for (int c0 = 0; c0 < Cin; c0 += ccmax) {
         const int cc = min(ccmax, Cin - c0), rl = cc * ntaps, n = nr * rl;   // n <= 4096
         const float* __restrict__ src = w + (size_t)co0 * nrow + (size_t)c0 * ntaps;
@@ -475,22 +506,23 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
         for (int u = 0; u < 16; ++u) v[u] = src[min(tid + u * 256, n - 1)];
 #pragma unroll
         for (int u = 0; u < 16; ++u)
-          if (tid + u * 256 < n) buf[tid + u * 256] = v[u];
+          if (tid + u * 256 < n) smem[rows_slot(tid + u * 256, rq)] = v[u];
         __syncthreads();
         if (vec) {
           // 8 consecutive ci of one tap per lane: one 16-B store (cc % 8 == 0)
           for (int o = tid * 8; o < n; o += 256 * 8) {
             const int r = o / rl, rem = o - r * rl, tap = rem / cc, ci = rem - tap * cc;
+            const int s0 = r * rl + ci * ntaps + tap;
             float v8[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v8[j] = buf[r * rl + (ci + j) * ntaps + tap];
+            for (int j = 0; j < 8; ++j) v8[j] = smem[rows_slot(s0 + j * ntaps, rq)];
             store8<bf16_t>((bf16_t*)t.out + (int64_t)(row0 + co0 + r) * Kpad + tap * Cpad + c0 + ci, v8);
           }
         } else {
           for (int o = tid; o < n; o += 256) {
             const int r = o / rl, rem = o - r * rl, tap = rem / cc, ci = rem - tap * cc;
             store_as(t.out, (int64_t)(row0 + co0 + r) * Kpad + tap * Cpad + c0 + ci, t.dtype,
-                     buf[r * rl + ci * ntaps + tap]);
+                     smem[rows_slot(r * rl + ci * ntaps + tap, rq)]);
           }
         }
         __syncthreads();
@@ -514,9 +546,9 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
             float v[8];
             load8<bf16_t>(sp, v);
 #pragma unroll
-            for (int j = 0; j < 8; ++j) tile[i][k + j] = v[j];
+            for (int j = 0; j < 8; ++j) smem[tile_at(i, k + j)] = v[j];
           } else {
-            for (int j = 0; j < 8 && cc + j < C; ++j) tile[i][k + j] = bf2f(sp[j]);
+            for (int j = 0; j < 8 && cc + j < C; ++j) smem[tile_at(i, k + j)] = bf2f(sp[j]);
           }
         }
         __syncthreads();
@@ -527,22 +559,22 @@ __global__ void __launch_bounds__(256) pack_plan_kernel(const dfcsa_pack_entry* 
           if (rr + 8 <= R) {
             float v[8];
 #pragma unroll
-            for (int j = 0; j < 8; ++j) v[j] = tile[k + j][ci];
+            for (int j = 0; j < 8; ++j) v[j] = smem[tile_at(k + j, ci)];
             store8<bf16_t>(dp, v);
           } else {
-            for (int j = 0; j < 8 && rr + j < R; ++j) dp[j] = f2bf(tile[k + j][ci]);
+            for (int j = 0; j < 8 && rr + j < R; ++j) dp[j] = f2bf(smem[tile_at(k + j, ci)]);
           }
         }
         break;
       }
       for (int i = 0; i < 16; ++i) {
         const int rr = r0 + i * 4 + q, cc = c0 + lane;
-        if (rr < R && cc < C) tile[i * 4 + q][lane] = load_as(t.w0, (int64_t)rr * lds + cc, t.dtype);
+        if (rr < R && cc < C) smem[tile_at(i * 4 + q, lane)] = load_as(t.w0, (int64_t)rr * lds + cc, t.dtype);
       }
       __syncthreads();
       for (int i = 0; i < 16; ++i) {
         const int cc = c0 + i * 4 + q, rr = r0 + lane;
-        if (rr < R && cc < C) store_as(t.out, (int64_t)cc * ldd + rr, t.dtype, tile[lane][i * 4 + q]);
+        if (rr < R && cc < C) store_as(t.out, (int64_t)cc * ldd + rr, t.dtype, smem[tile_at(lane, i * 4 + q)]);
       }
       break;
     }

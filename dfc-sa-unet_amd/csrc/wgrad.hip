@@ -1110,6 +1110,27 @@ __global__ void __launch_bounds__(NWV * 64) small_wgrad_f32_kernel(const WgradAr
   };
   small_gemm_tile<true, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, (const float*)a.seg[0].ptr, a.Cseg,
                                                 a.NI, a.NJ, a.M, blockIdx.x * 16, blockIdx.y * 64, lds, st);
+  if (!a.bdst[0] || blockIdx.y != 0) return;
+  // layout 2 bias gradients of this workgroup's 16 rows i: sum over the M pixel rows of G[m][i]
+  // (fp64, parts of M/(4 NWV) rows in row order, then the parts in order -- fixed order)
+  constexpr int NPART = NWV * 4;
+  __syncthreads();   // lds is free again (the tile's partial sums were consumed)
+  double* red = (double*)lds;   // [NPART][16]
+  const int il = threadIdx.x & 15, part = threadIdx.x >> 4;
+  const int i = blockIdx.x * 16 + il;
+  const float* __restrict__ g = (const float*)a.g_ptr[0];
+  double sm = 0.0;
+  if (i < a.NI) {
+    const int per = (a.M + NPART - 1) / NPART, m0 = part * per, m1 = min(a.M, m0 + per);
+    for (int m = m0; m < m1; ++m) sm += (double)g[(size_t)m * a.NI + i];
+  }
+  red[part * 16 + il] = sm;
+  __syncthreads();
+  if (part != 0 || i >= a.NI || i >= 2 * a.Ctot + a.Creal) return;
+  double tot = 0.0;
+  for (int q = 0; q < NPART; ++q) tot += red[q * 16 + il];
+  const int d = i < a.Ctot ? 0 : (i < 2 * a.Ctot ? 1 : 2);
+  a.bdst[d][i - d * a.Ctot] += (float)tot;
 }
 
 template <int SUB>
@@ -1543,6 +1564,10 @@ extern "C" int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, i
   return 0;
 }
 
+namespace {
+int launch_wgrad_any(WgradArgs& a, const dfcsa_wgrad_desc* d, hipStream_t st);
+}  // namespace
+
 extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->ng < 1 || d->ng > 3) return DFCSA_EINVAL;
   if (d->Cg % 8 || d->Cseg % 8 || d->mchunk <= 0 || d->splits <= 0) return DFCSA_EINVAL;
@@ -1572,6 +1597,10 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
       return DFCSA_EINVAL;
     if (d->Ctot <= 0) return DFCSA_EINVAL;
   }
+  const bool want_bias = d->bias_dst[0] != nullptr;
+  if (want_bias && (d->layout != 2 || d->ndst != 3 || d->ng != 1 || !d->bias_dst[1] || !d->bias_dst[2]))
+    return DFCSA_EINVAL;
+  for (int i = 0; i < 3; ++i) a.bdst[i] = nullptr;
   // one split: the kernel adds its tile straight into dst (no slab, no second launch)
   a.fuse = d->ndst > 0 && (d->splits == 1 ||
                            (g_wgrad_fuse_all >= 0 && (d->splits <= g_wgrad_fuse_max || g_wgrad_fuse_all > 0)));
@@ -1602,7 +1631,7 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   {
     WHaloArgs h;
     int bi;
-    if (d->ndst > 0 && whalo_plan(a, d->dtype, d->layout, &h, &bi) && d->splits == h.splits &&
+    if (d->ndst > 0 && !want_bias && whalo_plan(a, d->dtype, d->layout, &h, &bi) && d->splits == h.splits &&
         d->mchunk == h.per_split * 128) {
       if (h.splits > 1 && (!d->slab || d->slab_floats < (int64_t)h.splits * a.NI * a.NJ)) return DFCSA_EINVAL;
       h.slab = d->slab;
@@ -1621,13 +1650,28 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
   if (d->dtype != DFCSA_DT_BF16 && a.M <= 4096 && a.ng == 1 && a.nseg == 1 && !a.seg[0].dh && !a.seg[0].dw &&
       a.stride == 1 && d->ndst > 0 && a.Ho == a.Hi && a.Wo == a.Wi && !g_wgrad_noglds_f32small) {
     const dim3 sg((a.NI + 15) / 16, (a.NJ + 63) / 64);
+    if (want_bias) for (int i = 0; i < 3; ++i) a.bdst[i] = d->bias_dst[i];
     if (g_small8) hipLaunchKernelGGL((small_wgrad_f32_kernel<8, 4>), sg, dim3(512), 0, st, a);
     else hipLaunchKernelGGL((small_wgrad_f32_kernel<4, 2>), sg, dim3(256), 0, st, a);
     DFCSA_CHECK_LAUNCH();
     return 0;
   }
+  a.coop = want_coop ? 1 : 0;   // (launch_wgrad_any's request flag; cleared before any launch)
+  if (want_bias) {   // the other kernels: the column sums of G by one launch after the weight gradient
+    const int rc = launch_wgrad_any(a, d, st);
+    if (rc) return rc;
+    return dfcsa_slab_colsum3((const float*)a.g_ptr[0], a.M, std::min(a.NI, 2 * d->Ctot + d->Creal), d->Ctot,
+                              d->Ctot, d->bias_dst[0], d->bias_dst[1], d->bias_dst[2], stream);
+  }
+  return launch_wgrad_any(a, d, st);
+}
+
+namespace {
+int launch_wgrad_any(WgradArgs& a, const dfcsa_wgrad_desc* d, hipStream_t st) {
   int rc;
   bool coop = false;
+  const bool want_coop = a.coop != 0;
+  a.coop = 0;
   if (d->dtype == DFCSA_DT_BF16)
     rc = a.NI <= 64 ? launch_wgrad<bf16_t, 64>(a, d->splits, st, want_coop, &coop)
                     : launch_wgrad<bf16_t, 128>(a, d->splits, st, want_coop, &coop);
@@ -1640,6 +1684,7 @@ extern "C" int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream) {
                          a.dst[1], a.dst[2], st);
   return 0;
 }
+}  // namespace
 
 extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ, int layout, int ntaps,
                                   int Ctot, int Creal, int ndst, float* const* dst, void* stream) {

@@ -77,7 +77,7 @@ class WgradDesc(ctypes.Structure):
                 ("stride", ctypes.c_int), ("slab", ctypes.c_void_p), ("splits", ctypes.c_int),
                 ("mchunk", ctypes.c_int), ("layout", ctypes.c_int), ("ntaps", ctypes.c_int), ("Ctot", ctypes.c_int),
                 ("Creal", ctypes.c_int), ("ndst", ctypes.c_int), ("dst", ctypes.c_void_p * 3),
-                ("slab_floats", ctypes.c_int64)]
+                ("slab_floats", ctypes.c_int64), ("bias_dst", ctypes.c_void_p * 3)]
 
 
 class PackEntry(ctypes.Structure):

@@ -147,9 +147,11 @@ def wgrad_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, dsts):
          ctypes.addressof(arr), stream())
 
 
-def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, Creal, layout=0, stride=1):
+def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, Creal, layout=0, stride=1,
+                    bias_grads=None):
     """grads[d] += the weight gradient in the reference layout, in one dfcsa_conv_wgrad call (the
-    split-K reduction runs inside the kernel, or as its second launch at high split counts)."""
+    split-K reduction runs inside the kernel, or as its second launch at high split counts).
+    bias_grads (layout 2: three tensors): += the pixel sums of G, the stacked 1x1 biases' gradients."""
     d, floats, NI, NJ = _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride, layout=layout)
     slab = torch.empty(floats, device=gs[0].device, dtype=torch.float32) if d.splits > 1 else None
     d.slab = P(slab)
@@ -157,6 +159,9 @@ def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, 
     d.layout, d.ntaps, d.Ctot, d.Creal, d.ndst = layout, ntaps, Ctot, Creal, len(grads)
     for i, t in enumerate(grads):
         d.dst[i] = P(t)
+    if bias_grads is not None:
+        for i, t in enumerate(bias_grads):
+            d.bias_dst[i] = P(t)
     call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
 
 

@@ -4,7 +4,12 @@ Replaces, in one device pass and without host synchronisation:
   torch.nn.utils.clip_grad_norm_(model.parameters(), max_norm=1.0)   utils/trainer.py:149
   torch.optim.SGD(lr, momentum, weight_decay).step()                  train.py:73-78, trainer.py:151
 with torch's semantics (weight decay added to the gradient before momentum; first step
-initialises the buffer to the gradient; p.grad holds the clipped gradient afterwards).
+initialises the buffer to the gradient -- the buffer starts at zero, so momentum * 0 + d is that
+first step exactly; p.grad holds the clipped gradient afterwards).
+
+``zero_after_step=True`` (bench.py, the Trainer) has the same pass write zeros to the gradients
+instead of the clipped values, and the next ``zero_grad`` then skips its memset; the weights and
+momentum are the same either way.
 """
 import ctypes
 
@@ -16,7 +21,8 @@ from .ops import P, stream
 
 
 class FusedSGD(torch.optim.Optimizer):
-    def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, dampening=0.0, nesterov=False):
+    def __init__(self, params, lr=0.01, momentum=0.0, weight_decay=0.0, dampening=0.0, nesterov=False,
+                 zero_after_step=False):
         if dampening != 0.0 or nesterov:
             raise NotImplementedError("FusedSGD implements the reference's SGD (no dampening/nesterov)")
         super().__init__(params, dict(lr=lr, momentum=momentum, weight_decay=weight_decay, dampening=0.0,
@@ -30,6 +36,8 @@ class FusedSGD(torch.optim.Optimizer):
         self._partial = None
         self._pending_mom = None   # momentum buffers loaded before the flat storage existed
         self.last_norm = None
+        self.zero_after_step = zero_after_step
+        self._grads_zeroed = False  # the last step() zeroed the gradients (zero_after_step)
 
     @classmethod
     def from_torch_sgd(cls, opt):
@@ -59,7 +67,6 @@ class FusedSGD(torch.optim.Optimizer):
         if flat is not self._flat:
             self._flat = flat
             self._mom = torch.zeros_like(flat.data)
-            self._mom_init = torch.zeros(1, dtype=torch.int32, device=flat.device)
             self._partial = torch.empty(LIB.dfcsa_sumsq_nparts(flat.numel), dtype=torch.float64,
                                         device=flat.device)
             self.last_norm = torch.zeros(1, dtype=torch.float32, device=flat.device)
@@ -69,14 +76,16 @@ class FusedSGD(torch.optim.Optimizer):
                 if pending is not None:
                     view.copy_(pending[id(p)])
                 self.state[p]["momentum_buffer"] = view
-            if pending is not None:
-                self._mom_init.fill_(1)   # resumed: the next step continues the loaded momentum
         return flat
 
     def zero_grad(self, set_to_none=True):
         flat = getattr(self.param_groups[0]["params"][0], "_dfcsa_flat", None)
         if flat is not None and flat.valid():
-            flat.zero_grad()  # one memset; grads stay views of the flat buffer
+            if self._grads_zeroed and flat is self._flat:
+                flat.attach_grads()   # the last step() already wrote zeros
+            else:
+                flat.zero_grad()  # one memset; grads stay views of the flat buffer
+            self._grads_zeroed = False
         else:
             super().zero_grad(set_to_none)
 
@@ -96,9 +105,10 @@ class FusedSGD(torch.optim.Optimizer):
             nparts, mn = self._partial.numel(), float(max_norm)
         else:
             nparts, mn = 0, float("inf")
-        call("dfcsa_clip_sgd", ctypes.c_int64(n), P(flat.data), P(flat.grad), P(self._mom), P(self._partial),
+        call("dfcsa_clip_sgd2", ctypes.c_int64(n), P(flat.data), P(flat.grad), P(self._mom), P(self._partial),
              nparts, mn, float(grad_scale), float(g["lr"]), float(g["momentum"]), float(g["weight_decay"]),
-             P(self._mom_init), P(skip_if_nan), P(self.last_norm), stream())
+             int(bool(self.zero_after_step)), P(skip_if_nan), P(self.last_norm), stream())
+        self._grads_zeroed = bool(self.zero_after_step)
         return loss
 
     def load_state_dict(self, state_dict):
@@ -114,7 +124,6 @@ class FusedSGD(torch.optim.Optimizer):
             self._pending_mom = None
             if self._mom is not None:
                 self._mom.zero_()
-                self._mom_init.zero_()
             return
         flat = getattr(params[0], "_dfcsa_flat", None)
         self._pending_mom = {id(p): b.detach().clone() for p, b in zip(params, bufs)}

@@ -66,6 +66,8 @@ class Trainer:
         # the reference's train.py builds torch.optim.SGD(model.parameters(), ...): run it as the
         # fused device pass (same update; clip_grad_norm_ included)
         self.optimizer = FusedSGD.from_torch_sgd(optimizer) or optimizer
+        if isinstance(self.optimizer, FusedSGD):
+            self.optimizer.zero_after_step = True   # the loop never reads p.grad after a step
         self.train_loader = train_loader
         self.val_loader = val_loader
         self.loss_type = config["training"].get("loss", {}).get("type", "dice")
@@ -150,9 +152,9 @@ class Trainer:
             return None, None
         if not all(p.requires_grad for p in params):
             return None, None
-        keep = (plan, flat, opt._mom, opt._mom_init, opt._partial, opt.last_norm)
+        keep = (plan, flat, opt._mom, opt._partial, opt.last_norm)
         sig = (id(plan), plan.epoch if plan is not None else -1, id(flat), flat.data.data_ptr(),
-               flat.grad.data_ptr(), opt._mom.data_ptr(), opt._mom_init.data_ptr(), opt._partial.data_ptr(),
+               flat.grad.data_ptr(), opt._mom.data_ptr(), opt._partial.data_ptr(),
                opt.last_norm.data_ptr())
         return sig, keep
 

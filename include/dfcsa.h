@@ -109,6 +109,11 @@ typedef struct {
   int layout, ntaps, Ctot, Creal, ndst;
   float* dst[3];
   int64_t slab_floats;  /* capacity of slab in floats (checked against the launch) */
+  /* layout 2 (stacked q/k/v 1x1 rows) with ndst == 3: bias_dst[0] != NULL also adds the pixel sums
+   * of G (sum_m G[m][i], the three biases' gradients) into bias_dst[0..2] with the row mapping of
+   * the weights -- in the weight-gradient launch where the kernel allows it, else by one column-sum
+   * launch after it (the result of dfcsa_slab_colsum3 on G either way) */
+  float* bias_dst[3];
 } dfcsa_wgrad_desc;
 int dfcsa_wgrad_plan(int M, int NI, int NJ, int dtype, int* splits, int* mchunk, int64_t* slab_floats);
 /* the plan of the launch dfcsa_conv_wgrad will make for *d (segments, shapes, layout filled in):
@@ -459,6 +464,13 @@ int dfcsa_sumsq_partial(int64_t n, const float* g, double* partial, void* stream
 int dfcsa_clip_sgd(int64_t n, float* w, float* g, float* buf, const double* partial, int nparts,
                    float max_norm, float grad_scale, float lr, float momentum, float weight_decay,
                    int* mom_init, const float* skip_if_nan, float* norm_out, void* stream);
+/* dfcsa_clip_sgd with a momentum buffer that starts at zero instead of a first-step flag
+ * (buf = momentum * 0 + d == d exactly: torch's first step, one launch instead of two);
+ * zero_grad != 0 writes zeros to g instead of the clipped gradient (also on a skipped step), so
+ * the caller's next zero_grad needs no memset pass. */
+int dfcsa_clip_sgd2(int64_t n, float* w, float* g, float* buf, const double* partial, int nparts,
+                    float max_norm, float grad_scale, float lr, float momentum, float weight_decay,
+                    int zero_grad, const float* skip_if_nan, float* norm_out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
  * Full-resolution self-attention (models/unet_dfc_sa_ablation_attention.py:15-26, the attention

@@ -39,7 +39,7 @@ def test_ctypes_binding_loads_and_parses_header():
 def test_descriptor_layouts_match_c(tmp_path):
     from dfcsa import _lib
     fields = [("dfcsa_conv_desc", _lib.ConvDesc, ("weight", "Wout")),
-              ("dfcsa_wgrad_desc", _lib.WgradDesc, ("slab", "mchunk", "ndst", "dst")),
+              ("dfcsa_wgrad_desc", _lib.WgradDesc, ("slab", "mchunk", "ndst", "dst", "bias_dst")),
               ("dfcsa_pack_entry", _lib.PackEntry, ("w0", "a")),
               ("dfcsa_wstd_entry", _lib.WstdEntry, ("K", "pad")),
               ("dfcsa_resample_desc", _lib.ResampleDesc, ("kk", "row0")),

@@ -445,7 +445,7 @@ def test_conv_large_tiles_bf16(B, H, Cs, nsrc, C, k3, cfg):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
-@pytest.mark.parametrize("cin,C", [(40, 64), (64, 64), (8, 16)])
+@pytest.mark.parametrize("cin,C", [(40, 64), (64, 64), (8, 16), (3, 16), (512, 64)])
 def test_pack_plan_matches_single_packs(dtype, cin, C):
     """The two-phase pack plan (row permutes, then 64x64 tile transposes) reproduces the
     per-weight pack kernels bit for bit for a DFC block (with and without a residual conv), its
@@ -1100,3 +1100,32 @@ def test_lsa_up_bwd_rows_and_pool(B, H, W, C, P, dtype):
     act = torch.relu(d.double() * sc.double() + sh.double()).permute(0, 3, 1, 2)
     pref = F.adaptive_avg_pool2d(act, P).permute(0, 2, 3, 1).reshape(B, P * P, C)
     assert rel(pooled, pref) < 1e-6
+
+
+@pytest.mark.parametrize("M,Cq,C", [(256, 8, 64), (256, 16, 128), (5000, 8, 64)])
+def test_wgrad_layout2_bias_sums(M, Cq, C):
+    """The LightSelfAttention projection backward: q/k/v weight gradients (layout 2) and, in the same
+    dfcsa_conv_wgrad call, the bias gradients (pixel sums of dqkv) -- inside the small fp32 kernel at
+    M <= 4096, by the column-sum launch after the weight gradient otherwise -- against torch fp32 and
+    the separate dfcsa_slab_colsum3 launch, accumulated onto existing gradients."""
+    from dfcsa._lib import call
+    torch.manual_seed(M + C)
+    J = 2 * Cq + C
+    g = torch.randn(M, J, device="cuda")
+    x = torch.randn(M, C, device="cuda")
+    ws = [torch.randn(Cq, C, 1, 1, device="cuda"), torch.randn(Cq, C, 1, 1, device="cuda"),
+          torch.randn(C, C, 1, 1, device="cuda")]
+    bs = [torch.randn(Cq, device="cuda"), torch.randn(Cq, device="cuda"), torch.randn(C, device="cuda")]
+    w0 = [w.clone() for w in ws]
+    b0 = [b.clone() for b in bs]
+    ops.conv_wgrad_into(torch.float32, [g], J, [(x, 0, 0)], C, (1, M, 1), (M, 1), ws, 1, Cq, C, layout=2,
+                        bias_grads=bs)
+    sep = [b.clone() for b in b0]
+    call("dfcsa_slab_colsum3", ops.P(g), M, J, Cq, Cq, ops.P(sep[0]), ops.P(sep[1]), ops.P(sep[2]), ops.stream())
+    torch.cuda.synchronize()
+    dw = g.t() @ x
+    db = g.sum(0)
+    for k, (lo, hi) in enumerate(((0, Cq), (Cq, 2 * Cq), (2 * Cq, J))):
+        assert rel(ws[k].view(hi - lo, C) - w0[k].view(hi - lo, C), dw[lo:hi]) < 1e-5
+        assert rel(bs[k] - b0[k], db[lo:hi]) < 1e-5
+        assert (bs[k] - sep[k]).abs().max().item() <= 1e-5 * (1 + sep[k].abs().max().item())

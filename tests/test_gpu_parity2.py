@@ -463,6 +463,38 @@ def test_clip_sgd_nan_semantics():
     assert all(torch.isnan(p).all() for p in model.parameters())
 
 
+def test_clip_sgd_zero_after_step_same_update():
+    """zero_after_step (bench.py, Trainer): the fused pass writes zeros to the gradients instead of
+    the clipped values -- on a NaN-skipped step too -- and the weights and momentum are bit-identical
+    to the default pass over the same steps (resumed momentum included)."""
+    from dfcsa.optim import FusedSGD
+    x = T(load("model_small.npz")["x1"])
+    models, opts = [], []
+    for zero in (False, True):
+        torch.manual_seed(0)
+        m = small_model("fp32")
+        m(x)
+        models.append(m)
+        opts.append(FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4, zero_after_step=zero))
+    gen = torch.Generator(device="cuda").manual_seed(3)
+    skips = [None, torch.tensor([float("nan")], device="cuda"), torch.tensor([0.5], device="cuda"), None]
+    for skip in skips:
+        grads = [torch.randn(p.shape, device="cuda", generator=gen) * 0.05 for p in models[0].parameters()]
+        for m, opt in zip(models, opts):
+            opt.zero_grad()
+            assert all(torch.count_nonzero(p.grad) == 0 for p in m.parameters())
+            for p, g in zip(m.parameters(), grads):
+                p.grad.copy_(g)
+            opt.step(max_norm=1.0, skip_if_nan=skip)
+        torch.cuda.synchronize()
+        assert torch.equal(opts[0]._mom, opts[1]._mom)
+        assert torch.equal(opts[0].last_norm, opts[1].last_norm)
+        for p, q in zip(*(m.parameters() for m in models)):
+            assert torch.equal(p, q)
+        assert all(torch.count_nonzero(p.grad) == 0 for p in models[1].parameters())
+    assert any(torch.count_nonzero(p.grad) > 0 for p in models[0].parameters())
+
+
 def test_eval_mode_backward_is_refused():
     """the backward kernels are train-mode BatchNorm; a backward through an eval-mode
     forward raises instead of returning wrong gradients."""

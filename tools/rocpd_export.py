@@ -120,7 +120,7 @@ GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gem
                                       "slab_colsum", "sum_scalar_kernel", "colred")),
           ("lsa (pooled attention)", ("lsa_",)),
           ("maxpool", ("maxpool2",)),
-          ("optimizer", ("sumsq_kernel", "clip_sgd_kernel", "set_flag_kernel")),
+          ("optimizer", ("sumsq_kernel", "clip_sgd", "set_flag_kernel")),
           ("pack_plan", ("pack_plan_kernel",)),
           ("loss/head/input", ("bce_dice", "sigmoid", "head_", "pack_input")))
 
@@ -139,7 +139,7 @@ def _dispatch_rows(db, counter):
 
 
 def _last_step(rows):
-    ends = [i for i, (_, n, _) in enumerate(rows) if "clip_sgd_kernel" in n]
+    ends = [i for i, (_, n, _) in enumerate(rows) if "clip_sgd" in n]
     if len(ends) < 2:
         raise SystemExit("need >= 2 clip_sgd dispatches (2 steps) in the counter pass")
     return rows[ends[-2] + 1: ends[-1] + 1]

@@ -11,7 +11,7 @@ def main():
     db, top = sys.argv[1], int(sys.argv[2]) if len(sys.argv) > 2 else 40
     c = sqlite3.connect(db)
     rows = list(c.execute("select name, grid_x, grid_y, grid_z, workgroup_x, duration, start, end from kernels order by start"))
-    ends = [i for i, r in enumerate(rows) if "clip_sgd_kernel" in r[0]]
+    ends = [i for i, r in enumerate(rows) if "clip_sgd" in r[0]]
     step = rows[ends[-2] + 1: ends[-1] + 1]
     wall = (step[-1][7] - step[0][6]) / 1e6
     busy = sum(r[5] for r in step) / 1e6
