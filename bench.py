@@ -278,13 +278,15 @@ def main():
     reducer = GradBucketReducer(model, bucket_mb=args.bucket_mb) if ddp else None
     scale = reducer.grad_scale if reducer else 1.0
 
+    one = torch.ones((), device=dev)   # the root gradient, a persistent tensor (no fill per step)
+
     def step():
         opt.zero_grad()
         p = sigmoid(model(x))
         loss, stats = bce_dice(p, t, 1.0, 1.0)   # 'bce_dice' with the yaml's (ignored) weight keys
         if reducer:
             reducer.start()
-        loss.backward()
+        loss.backward(one)
         skip = reducer.finish(loss) if reducer else loss   # NaN on any rank -> every rank skips
         opt.step(max_norm=1.0, grad_scale=scale, skip_if_nan=skip)
         return stats

@@ -1371,9 +1371,13 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
 // SH: segments with (dh, dw) pixel shifts (a 3x3 conv whose 9 * Cin fits K <= 256, i.e. the
 // first layer: Cin = 8, K = 72): each 8-channel chunk's row is the shifted pixel of its segment,
 // the zero page outside the image; Ho = Hi, Wo = Wi, stride 1.
-template <int NWC, int KP, bool ACC, bool SH = false>
+// SHUF: ConvTranspose2d(k=2, s=2) store (CONV_STORE_SHUFFLE2): column n = (i*2 + j)*Nd + co of
+// input pixel (b, oh, ow) goes to output pixel (b, 2oh+i, 2ow+j), channel co -- 16-B chunks of 8
+// consecutive co stay contiguous, so the stores are the plain kernel's with a per-row base.
+template <int NWC, int KP, bool ACC, bool SH = false, bool SHUF = false>
 __global__ void __launch_bounds__(256)
 conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
+  static_assert(!(SHUF && (ACC || SH)), "shuffle store: plain, unshifted");
   using T = bf16_t;
   constexpr int KS = KP / 64;               // 64-wide K stages (one 64x128B LDS image each)
   constexpr int KG = KP / 32;               // 32-wide MFMA k groups
@@ -1481,7 +1485,10 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
     o_ld[it] = args.Nd;
     if (n < N) {
       const int d = n / args.Nd;
-      o_base[it] = (T*)args.dest[d] + (n - d * args.Nd);
+      if constexpr (SHUF)   // d = i*2 + j: output row offset i, column offset j
+        o_base[it] = (T*)args.dest[0] + ((size_t)((d >> 1) * args.Wout + (d & 1)) * args.Nd + (n - d * args.Nd));
+      else
+        o_base[it] = (T*)args.dest[d] + (n - d * args.Nd);
     }
   }
   constexpr bool lean = !ACC;
@@ -1574,7 +1581,15 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
       const int m = m0 + row;
       uint4 v = *(const uint4*)(otile + row * OSTR + cc * 16);
       const bool ok = m < M && o_base[it];
-      T* dst = ok ? o_base[it] + (size_t)m * o_ld[it] : (T*)(g_store_sink + 4 * (tid & 63));
+      size_t moff;
+      if constexpr (SHUF) {   // input pixel m = (b, oh, ow) -> output pixel (b, 2oh, 2ow)
+        const int b = dm_div(args.dm_hw, m), rem = m - b * args.dm_hw.d;
+        const int oh = dm_div(args.dm_w, rem), ow = rem - oh * args.dm_w.d;
+        moff = (size_t)((b * args.Hout + 2 * oh) * args.Wout + 2 * ow) * args.Nd;
+      } else {
+        moff = (size_t)m * o_ld[it];
+      }
+      T* dst = ok ? o_base[it] + moff : (T*)(g_store_sink + 4 * (tid & 63));
       if constexpr (lean) {   // branch-free: exactly one store instruction per iteration
         *(uint4*)dst = v;
         continue;
@@ -2197,7 +2212,10 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
   bool shifted = false;
   for (int i = 0; i < a.nseg; ++i) shifted = shifted || a.seg[i].dh || a.seg[i].dw;
-  if (shifted) {
+  if (a.mode == CONV_STORE_SHUFFLE2) {
+    if (a.accumulate || shifted) return DFCSA_EINVAL;
+    hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, false, false, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
+  } else if (shifted) {
     if (a.accumulate) return DFCSA_EINVAL;
     hipLaunchKernelGGL((conv1x1_stream_kernel<NWC, KP, false, true>), dim3(gx, ny), dim3(256), 0, st, a, mtiles);
   } else if (a.accumulate)
@@ -2211,8 +2229,15 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
 // the streaming kernel serves 1x1 (no shift, stride 1, plain store) bf16 GEMMs with K <= 256
 // (and, knob 30 on, the shifted-segment 3x3 with 9 * Cin <= 256: the first layer, Cin = 8)
 int g_stream_shift = 1;   // knob 30
+int g_stream_min_m = 4 * 64 * 256;   // knob 33: smallest M the streaming kernel takes
+int g_stream_shuf = 1;               // knob 34: ConvTranspose2d (shuffle-store) GEMMs on the streaming kernel
 bool stream_applies(const ConvGemmArgs& a) {
-  if (a.mode != CONV_STORE_PLAIN || a.stride != 1 || a.Kpad > 256 || a.M < 4 * 64 * 256) return false;
+  const bool shuf = a.mode == CONV_STORE_SHUFFLE2 && g_stream_shuf && !a.accumulate && a.Nd % 8 == 0 &&
+                    a.ndest == 1 && a.Hout == 2 * a.Ho && a.Wout == 2 * a.Wo;
+  if ((a.mode != CONV_STORE_PLAIN && !shuf) || a.stride != 1 || a.Kpad > 256 || a.M < g_stream_min_m) return false;
+  if (shuf)
+    for (int i = 0; i < a.nseg; ++i)
+      if (a.seg[i].dh || a.seg[i].dw) return false;
   bool shifted = false;
   for (int i = 0; i < a.nseg; ++i) shifted = shifted || a.seg[i].dh || a.seg[i].dw;
   if (shifted && (!g_stream_shift || a.accumulate || a.Cseg % 8)) return false;
@@ -2657,6 +2682,8 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 20: return g_wgrad_halo;
     case 31: return g_wgrad_coop;
     case 32: return g_wgrad_coop_launches;
+    case 33: return g_stream_min_m;
+    case 34: return g_stream_shuf;
     default: return DFCSA_EINVAL;
   }
 }
@@ -2686,6 +2713,8 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 28) { g_lsa_rows_old = value; return 0; }
   if (knob == 30) { g_stream_shift = value; return 0; }
   if (knob == 31) { g_wgrad_coop = value; return 0; }
+  if (knob == 33) { g_stream_min_m = value; return 0; }
+  if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

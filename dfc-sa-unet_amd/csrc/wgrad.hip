@@ -1102,22 +1102,21 @@ __device__ __forceinline__ void reduce_dst_add(int64_t e, int NI, int NJ, int la
 // whole reduction in one launch (split over the 4 waves of a 16x64 tile, small_gemm.h), added
 // straight into the destination layout -- no split-K slab, no reduce launch
 template <int NWV, int UNR>
-__global__ void __launch_bounds__(NWV * 64) small_wgrad_f32_kernel(const WgradArgs a) {
-  __shared__ float lds[NWV * 16 * 64];
+__device__ __forceinline__ void small_wgrad_tile(const WgradArgs& a, int bx, int by, float* lds) {
   auto st = [&](int i, int j, float v) {
     reduce_dst_add((int64_t)i * a.NJ + j, a.NI, a.NJ, a.layout, a.ntaps, a.Ctot, a.Creal, a.ndst, a.dst[0], a.dst[1],
                    a.dst[2], v);
   };
   small_gemm_tile<true, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, (const float*)a.seg[0].ptr, a.Cseg,
-                                                a.NI, a.NJ, a.M, blockIdx.x * 16, blockIdx.y * 64, lds, st);
-  if (!a.bdst[0] || blockIdx.y != 0) return;
+                                                a.NI, a.NJ, a.M, bx * 16, by * 64, lds, st);
+  if (!a.bdst[0] || by != 0) return;
   // layout 2 bias gradients of this workgroup's 16 rows i: sum over the M pixel rows of G[m][i]
   // (fp64, parts of M/(4 NWV) rows in row order, then the parts in order -- fixed order)
   constexpr int NPART = NWV * 4;
   __syncthreads();   // lds is free again (the tile's partial sums were consumed)
   double* red = (double*)lds;   // [NPART][16]
   const int il = threadIdx.x & 15, part = threadIdx.x >> 4;
-  const int i = blockIdx.x * 16 + il;
+  const int i = bx * 16 + il;
   const float* __restrict__ g = (const float*)a.g_ptr[0];
   double sm = 0.0;
   if (i < a.NI) {
@@ -1131,6 +1130,39 @@ __global__ void __launch_bounds__(NWV * 64) small_wgrad_f32_kernel(const WgradAr
   for (int q = 0; q < NPART; ++q) tot += red[q * 16 + il];
   const int d = i < a.Ctot ? 0 : (i < 2 * a.Ctot ? 1 : 2);
   a.bdst[d][i - d * a.Ctot] += (float)tot;
+}
+
+// fp32 weight gradient over few pixel rows (the LightSelfAttention projections, M = B*P*P): the
+// whole reduction in one launch (split over the waves of a 16x64 tile, small_gemm.h), added
+// straight into the destination layout -- no split-K slab, no reduce launch
+template <int NWV, int UNR>
+__global__ void __launch_bounds__(NWV * 64) small_wgrad_f32_kernel(const WgradArgs a) {
+  __shared__ float lds[NWV * 16 * 64];
+  small_wgrad_tile<NWV, UNR>(a, blockIdx.x, blockIdx.y, lds);
+}
+
+// The same weight gradient and, in the same launch, the 1x1 conv's input gradient from the same G:
+// dx[m][n] = sum_i G[m][i] * wt[n][i] (wt: the transposed weight, rows of kpad floats).  Workgroups
+// [0, nw) take the weight-gradient tiles, the rest the 16 x 64 input-gradient tiles -- the two
+// GEMMs only read G, so one launch replaces two on the attention backward chain.
+struct SmallDgrad {
+  const float* wt;
+  float* dx;
+  int kpad, N, nwx, nw, ndx;
+};
+template <int NWV, int UNR>
+__global__ void __launch_bounds__(NWV * 64) small_wgrad_dgrad_f32_kernel(const WgradArgs a, const SmallDgrad d) {
+  __shared__ float lds[NWV * 16 * 64];
+  int b = blockIdx.x;
+  if (b < d.nw) {
+    small_wgrad_tile<NWV, UNR>(a, b % d.nwx, b / d.nwx, lds);
+    return;
+  }
+  b -= d.nw;
+  const int bx = b % d.ndx, by = b / d.ndx;
+  auto st = [&](int m, int n, float v) { d.dx[(size_t)m * d.N + n] = v; };
+  small_gemm_tile<false, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, d.wt, d.kpad, a.M, d.N, a.NI,
+                                                 bx * 16, by * 64, lds, st);
 }
 
 template <int SUB>
@@ -1694,4 +1726,55 @@ extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ,
     return DFCSA_EINVAL;
   return launch_reduce(slab, splits, NI, NJ, layout, ntaps, Ctot, Creal, ndst, dst[0], ndst > 1 ? dst[1] : nullptr,
                        ndst > 2 ? dst[2] : nullptr, (hipStream_t)stream);
+}
+
+// dfcsa_conv_wgrad(d) and dx = G * wt^T (a 1x1 conv's input gradient from the same G), one launch
+// when the small fp32 kernels apply to both, else the two calls one after the other
+extern "C" int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx,
+                                         void* stream) {
+  if (!d || !wt || !dx || N <= 0 || kpad < d->ng * d->Cg || kpad % 4) return DFCSA_EINVAL;
+  const int NI = d->ng * d->Cg;
+  const bool small = d->dtype != DFCSA_DT_BF16 && d->M <= 4096 && d->ng == 1 && d->nseg == 1 && !d->seg_dh[0] &&
+                     !d->seg_dw[0] && d->stride == 1 && d->ndst > 0 && d->Ho == d->Hi && d->Wo == d->Wi &&
+                     !g_wgrad_noglds_f32small && NI % 4 == 0;
+  if (!small) {
+    if (const int rc = dfcsa_conv_wgrad(d, stream)) return rc;
+    dfcsa_conv_desc c;
+    std::memset(&c, 0, sizeof(c));
+    c.dtype = d->dtype; c.M = d->M; c.N = N; c.Kpad = kpad; c.Cseg = NI; c.nseg = 1;
+    c.seg_ptr[0] = d->g_ptr[0];
+    c.Ho = d->Ho; c.Wo = d->Wo; c.Hi = d->Ho; c.Wi = d->Wo; c.stride = 1;
+    c.weight = wt; c.mode = 0; c.ndest = 1; c.dest[0] = dx; c.Nd = N;
+    return dfcsa_conv_gemm(&c, stream);
+  }
+  // validation and argument setup of dfcsa_conv_wgrad, small-kernel path
+  if (d->Cg % 8 || d->Cseg % 8) return DFCSA_EINVAL;
+  if (d->layout == 2 ? (d->ndst != 3 || d->Ctot <= 0 || 2 * d->Ctot > NI)
+                     : d->layout == 3 ? (d->ndst != 2 || d->Ctot <= 0 || NI != 2 * d->Ctot || d->Cseg <= d->Ctot)
+                                      : (NI % d->ndst != 0 || d->Ctot <= 0))
+    return DFCSA_EINVAL;
+  const bool want_bias = d->bias_dst[0] != nullptr;
+  if (want_bias && (d->layout != 2 || d->ndst != 3 || !d->bias_dst[1] || !d->bias_dst[2])) return DFCSA_EINVAL;
+  WgradArgs a;
+  std::memset(&a, 0, sizeof(a));
+  a.M = d->M; a.ng = 1; a.Cg = d->Cg; a.NI = NI;
+  a.g_ptr[0] = d->g_ptr[0];
+  a.nseg = 1; a.Cseg = d->Cseg; a.NJ = d->Cseg;
+  a.seg[0].ptr = d->seg_ptr[0];
+  a.Ho = d->Ho; a.Wo = d->Wo; a.Hi = d->Hi; a.Wi = d->Wi; a.stride = 1;
+  a.layout = d->layout; a.ntaps = d->ntaps; a.Ctot = d->Ctot; a.Creal = d->Creal; a.ndst = d->ndst;
+  for (int i = 0; i < 3; ++i) a.dst[i] = i < d->ndst ? d->dst[i] : nullptr;
+  if (want_bias) for (int i = 0; i < 3; ++i) a.bdst[i] = d->bias_dst[i];
+  SmallDgrad s;
+  s.wt = wt; s.dx = dx; s.kpad = kpad; s.N = N;
+  s.nwx = (NI + 15) / 16;
+  s.nw = s.nwx * ((a.NJ + 63) / 64);
+  s.ndx = (d->M + 15) / 16;
+  const int grid = s.nw + s.ndx * ((N + 63) / 64);
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_WGRAD, st, 2.0 * d->M * NI * (a.NJ + N));
+  if (g_small8) hipLaunchKernelGGL((small_wgrad_dgrad_f32_kernel<8, 4>), dim3(grid), dim3(512), 0, st, a, s);
+  else hipLaunchKernelGGL((small_wgrad_dgrad_f32_kernel<4, 2>), dim3(grid), dim3(256), 0, st, a, s);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }

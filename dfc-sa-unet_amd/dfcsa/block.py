@@ -540,15 +540,12 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
     qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
     if _lsa_gemm_ok(C, J):
         BN = B * N
-        # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums (in the same launch),
-        # dpooled = dqkv Wqkv; the stacked q/k/v rows go straight into the three weight / bias gradients
-        ops.conv_wgrad_into(f32, [dqkv], J, [(pooled, 0, 0)], C, (1, BN, 1), (BN, 1),
-                            [grad_of(qw), grad_of(kw), grad_of(vw)], 1, Cq, C, layout=2,
-                            bias_grads=[grad_of(lsa.query_conv.bias), grad_of(lsa.key_conv.bias),
-                                        grad_of(lsa.value_conv.bias)])
-        Kj = rup(J, ops.KALIGN)
-        WT = pk["WT"]
-        ops.conv_gemm(f32, [(dqkv, 0, 0)], J, (1, BN, 1), (BN, 1), WT, Kj, C, [dpooled], C)
+        # dW = dqkv^T pooled (pixel reduction GEMM), db = column sums and dpooled = dqkv Wqkv, all
+        # in one launch; the stacked q/k/v rows go straight into the three weight / bias gradients
+        ops.conv_wgrad_dgrad1x1(f32, dqkv, J, pooled, C, BN, [grad_of(qw), grad_of(kw), grad_of(vw)], 1, Cq, C,
+                                pk["WT"], rup(J, ops.KALIGN), C, dpooled, layout=2,
+                                bias_grads=[grad_of(lsa.query_conv.bias), grad_of(lsa.key_conv.bias),
+                                            grad_of(lsa.value_conv.bias)])
     else:
         call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
              P(grad_of(qw)), P(grad_of(kw)), P(grad_of(vw)), P(grad_of(lsa.query_conv.bias)),

@@ -51,6 +51,7 @@ class BCEDice(torch.autograd.Function):
         ctx.save_for_backward(p, t, stats)
         ctx.w = (float(w_bce), float(w_dice))
         ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)   # no zero-filled gradient for the stats output
         return stats[0], stats
 
     @staticmethod

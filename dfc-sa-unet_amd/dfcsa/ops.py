@@ -165,6 +165,24 @@ def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, 
     call("dfcsa_conv_wgrad", ctypes.addressof(d), stream())
 
 
+def conv_wgrad_dgrad1x1(dtype, g, Cg, x, Cx, M, grads, ntaps, Ctot, Creal, wt, kpad, N, dx, layout=0,
+                        bias_grads=None):
+    """conv_wgrad_into over G = g [M][Cg], X = x [M][Cx] (1x1, one row grid of M pixels) and, in the
+    same launch where the small fp32 kernels apply, dx [M][N] = g * wt^T (the 1x1 conv's input
+    gradient; wt [N][kpad] is its dfcsa_conv_gemm operand)."""
+    d, floats, NI, NJ = _wgrad_desc(dtype, [g], Cg, [(x, 0, 0)], Cx, (1, M, 1), (M, 1), 1, layout=layout)
+    slab = torch.empty(floats, device=g.device, dtype=torch.float32) if d.splits > 1 else None
+    d.slab = P(slab)
+    d.slab_floats = slab.numel() if slab is not None else 0
+    d.layout, d.ntaps, d.Ctot, d.Creal, d.ndst = layout, ntaps, Ctot, Creal, len(grads)
+    for i, t in enumerate(grads):
+        d.dst[i] = P(t)
+    if bias_grads is not None:
+        for i, t in enumerate(bias_grads):
+            d.bias_dst[i] = P(t)
+    call("dfcsa_conv_wgrad_dgrad1x1", ctypes.addressof(d), P(wt), kpad, N, P(dx), stream())
+
+
 # --------------------------------------------------------------------------- packing
 def pack_conv_w(dtype, w, Cpad, Kpad, out=None, row0=0, rows=None):
     Cout, Cin = w.shape[0], w.shape[1]

@@ -221,14 +221,12 @@ class Trainer:
             # data parallel: buckets all-reduced as backward finalises them, NaN agreement over the
             # ranks, 1/world inside the fused clip + SGD, the metric vector summed over the ranks
             self.reducer.start()
-            if self._weight != 1.0:   # a ragged global batch: row-weighted mean over the replicas
-                loss.backward(torch.full_like(loss, self._weight))
-            else:
-                loss.backward()
+            # a ragged global batch: row-weighted mean over the replicas
+            loss.backward(self._root_grad(loss, self._weight))
             skip = self.reducer.finish(loss)
             self.optimizer.step(max_norm=self.max_norm, grad_scale=self.reducer.grad_scale, skip_if_nan=skip)
             return {"loss": loss, "stats": allreduce_stats(met["stats"], weight=self._weight)}
-        loss.backward()
+        loss.backward(self._root_grad(loss, 1.0))
         if isinstance(self.optimizer, FusedSGD):
             self.optimizer.step(max_norm=self.max_norm, skip_if_nan=loss)
         else:
@@ -236,6 +234,16 @@ class Trainer:
                 torch.nn.utils.clip_grad_norm_(self.model.parameters(), max_norm=self.max_norm)
                 self.optimizer.step()
         return met
+
+    def _root_grad(self, loss, w):
+        """The loss's root gradient (w), a persistent device scalar per value: no fill kernel per
+        step, and a fixed address inside a captured step."""
+        cache = self.__dict__.setdefault("_root_grads", {})
+        key = (float(w), loss.device, loss.dtype, tuple(loss.shape))
+        g = cache.get(key)
+        if g is None:
+            g = cache[key] = torch.full_like(loss, float(w))
+        return g
 
     def _null_step(self):
         """Data parallel, a rank without rows in this global batch: zero gradients through the same

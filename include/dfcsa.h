@@ -128,6 +128,12 @@ int dfcsa_wgrad_fuse_max(void);
  * (0 = none) and clears it when reset != 0.  Synchronous (reads a device word). */
 int dfcsa_wgrad_coop_errors(int reset);
 int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
+/* dfcsa_conv_wgrad(d) plus the input gradient of a 1x1 conv from the same G (ng = 1):
+ * dx[m][n] = sum_i G[m][i] * wt[n * kpad + i] for n < N (wt: the transposed weight, the
+ * dfcsa_conv_gemm operand of that dgrad), in ONE launch when both fit the small fp32 kernels
+ * (M <= 4096, 1x1, fp32, one split); otherwise the two calls in order.  The LightSelfAttention
+ * projection backward (dW_q/k/v, db_q/k/v, dpooled) is one launch this way. */
+int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx, void* stream);
 /* grad += sum_s slab[s] (slab [splits][NI][NJ]) mapped to the reference weight layout.
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
  *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.

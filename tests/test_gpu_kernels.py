@@ -1129,3 +1129,67 @@ def test_wgrad_layout2_bias_sums(M, Cq, C):
         assert rel(ws[k].view(hi - lo, C) - w0[k].view(hi - lo, C), dw[lo:hi]) < 1e-5
         assert rel(bs[k] - b0[k], db[lo:hi]) < 1e-5
         assert (bs[k] - sep[k]).abs().max().item() <= 1e-5 * (1 + sep[k].abs().max().item())
+
+
+@pytest.mark.parametrize("M,Cq,C", [(256, 8, 64), (64, 16, 128), (5000, 8, 64)])
+def test_wgrad_dgrad1x1_one_launch(M, Cq, C):
+    """dfcsa_conv_wgrad_dgrad1x1 (the LightSelfAttention projection backward): the layout-2 weight and
+    bias gradients and dpooled = dqkv * W in one launch (M <= 4096) or two (M > 4096), against torch
+    fp32 and the separate calls."""
+    from dfcsa.block import rup
+    torch.manual_seed(M + Cq)
+    J = 2 * Cq + C
+    g = torch.randn(M, J, device="cuda")
+    x = torch.randn(M, C, device="cuda")
+    W = torch.randn(J, C, device="cuda")               # stacked q/k/v weights [J][C]
+    Kj = rup(J, ops.KALIGN)
+    WT = torch.zeros(C, Kj, device="cuda")
+    WT[:, :J] = W.t()
+    ws = [torch.zeros(Cq, C, 1, 1, device="cuda"), torch.zeros(Cq, C, 1, 1, device="cuda"),
+          torch.zeros(C, C, 1, 1, device="cuda")]
+    bs = [torch.zeros(Cq, device="cuda"), torch.zeros(Cq, device="cuda"), torch.zeros(C, device="cuda")]
+    dx = torch.empty(M, C, device="cuda")
+    ops.conv_wgrad_dgrad1x1(torch.float32, g, J, x, C, M, ws, 1, Cq, C, WT, Kj, C, dx, layout=2, bias_grads=bs)
+    ws2 = [torch.zeros_like(w) for w in ws]
+    bs2 = [torch.zeros_like(b) for b in bs]
+    ops.conv_wgrad_into(torch.float32, [g], J, [(x, 0, 0)], C, (1, M, 1), (M, 1), ws2, 1, Cq, C, layout=2,
+                        bias_grads=bs2)
+    dx2 = torch.empty(M, C, device="cuda")
+    ops.conv_gemm(torch.float32, [(g, 0, 0)], J, (1, M, 1), (M, 1), WT, Kj, C, [dx2], C)
+    torch.cuda.synchronize()
+    assert rel(dx, g @ W) < 1e-5 and torch.equal(dx, dx2)
+    dw = g.t() @ x
+    for k, (lo, hi) in enumerate(((0, Cq), (Cq, 2 * Cq), (2 * Cq, J))):
+        assert rel(ws[k].view(hi - lo, C), dw[lo:hi]) < 1e-5 and torch.equal(ws[k], ws2[k])
+        assert rel(bs[k], g[:, lo:hi].sum(0)) < 1e-5 and torch.equal(bs[k], bs2[k])
+
+
+@pytest.mark.parametrize("B,h,w,Cin,Cout", [(2, 5, 7, 64, 16), (4, 28, 28, 256, 128), (3, 13, 9, 128, 64),
+                                            (16, 56, 56, 128, 64)])
+def test_conv_transpose_fwd_streaming(B, h, w, Cin, Cout):
+    """The ConvTranspose2d(2, 2) forward GEMM on the streaming 1x1 kernel (shuffle store, knob 34;
+    knob 33 = 0 lets it take every M) against the tile kernel (knob 34 = 0) and torch."""
+    from dfcsa.functions import ConvTranspose2x2
+    bf = torch.bfloat16
+    torch.manual_seed(Cin + h)
+    mod = torch.nn.ConvTranspose2d(Cin, Cout, 2, 2).cuda()
+    with torch.no_grad():
+        mod.weight.copy_(q(mod.weight.cpu(), bf).cuda())
+    x = q(torch.randn(B, Cin, h, w), bf)
+    xh = nhwc(x, bf)
+    outs = []
+    old33 = ops._lib.LIB.dfcsa_get_tuning(33)
+    try:
+        for knob34 in (1, 0):
+            ops._lib.LIB.dfcsa_set_tuning(33, 0)
+            ops._lib.LIB.dfcsa_set_tuning(34, knob34)
+            with torch.no_grad():
+                outs.append(ConvTranspose2x2.apply(xh, mod, bf, *mod.parameters()).clone())
+        torch.cuda.synchronize()
+    finally:
+        ops._lib.LIB.dfcsa_set_tuning(33, old33)
+        ops._lib.LIB.dfcsa_set_tuning(34, 1)
+    with torch.no_grad():
+        ref = torch.nn.functional.conv_transpose2d(x, mod.weight.cpu(), mod.bias.cpu(), stride=2)
+    assert rel(outs[0].float(), outs[1].float()) < 4e-3   # same K order; a bf16 rounding flip at most
+    assert rel(nchw(outs[0]), ref) < 1e-2

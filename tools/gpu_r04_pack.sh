@@ -3,8 +3,10 @@
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pack or layout2 or lsa" tests/test_gpu_model.py > gpurun_out/t_pack.log 2>&1 || { tail -30 gpurun_out/t_pack.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pack or layout2 or lsa or dgrad1x1 or conv_transpose" tests/test_gpu_model.py > gpurun_out/t_pack.log 2>&1 || { tail -30 gpurun_out/t_pack.log; exit 1; }
 tail -1 gpurun_out/t_pack.log
+timeout -k 10 180 python tools/stream_minm_bench.py > gpurun_out/stream_minm.jsonl 2> gpurun_out/stream_minm.err || exit 1
+cat gpurun_out/stream_minm.jsonl
 AB_BASE=_ab_prev bash tools/gpu_ab_ktrace.sh || exit 1
 cd /tmp && export TMPDIR=/tmp
 B="--steps 2 --warmup 1 --no-kernel-timing --no-graph --no-cpu-baseline --no-val-dice --no-trainer-faithful"
