@@ -7,7 +7,8 @@ construction gives the reference's initial weights): widths 64..1024 hard-coded 
 ReLU), Down = MaxPool2d(2, ceil_mode=True) + DoubleConv, Up = ConvTranspose2d(k2, s2) + crop-to-match
 + cat([skip, up]) + DoubleConv, OutConv = 1x1.  Activations are NHWC in the compute dtype; the
 convolutions run on the implicit GEMM, the skip concat is a second GEMM source segment.
-``bilinear=True`` (nn.Upsample(align_corners=True) in Up, unet.py:36-37) is not built.
+``bilinear=True`` (nn.Upsample(scale_factor=2, bilinear, align_corners=True) in Up, unet.py:36-37;
+down4 and the up blocks at half width, unet.py:78-88) upsamples with dfcsa_upsample2_ac.
 """
 import torch
 import torch.nn as nn
@@ -17,6 +18,7 @@ from dfcsa import packs
 from dfcsa.flat import ALIGN, FlatParams
 from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC
 from dfcsa.ops import rup
+from dfcsa.transunet_ops import Upsample2x
 from dfcsa.unet_ops import ConvBNReLU, Crop, MaxPool2x2Ceil
 
 
@@ -54,13 +56,18 @@ class Up(nn.Module):
     def __init__(self, in_channels, out_channels, bilinear=True):
         super().__init__()
         if bilinear:
-            raise NotImplementedError("Up(bilinear=True) (nn.Upsample align_corners=True, reference unet.py:36-37) "
-                                      "is not built on the MI355X path; config 1 uses ConvTranspose2d")
-        self.up = nn.ConvTranspose2d(in_channels, in_channels // 2, kernel_size=2, stride=2)
+            self.up = nn.Upsample(scale_factor=2, mode="bilinear", align_corners=True)
+        else:
+            self.up = nn.ConvTranspose2d(in_channels, in_channels // 2, kernel_size=2, stride=2)
         self.conv = DoubleConv(in_channels, out_channels)
 
     def forward_nhwc(self, x1, x2, dtype):
-        x1 = ConvTranspose2x2.apply(x1, self.up, dtype, *self.up.parameters())
+        if isinstance(self.up, nn.Upsample):
+            if x1.shape[-1] % 8:
+                raise ValueError("bilinear Up needs a channel count divisible by 8")
+            x1 = Upsample2x.apply(x1, dtype)
+        else:
+            x1 = ConvTranspose2x2.apply(x1, self.up, dtype, *self.up.parameters())
         h1, w1, h2, w2 = x1.shape[1], x1.shape[2], x2.shape[1], x2.shape[2]
         dy, dx = h2 - h1, w2 - w1
         if dy < 0 or dx < 0:          # crop the upsampled map (reference :50-51)
@@ -70,6 +77,8 @@ class Up(nn.Module):
         return self.conv.forward_nhwc([x2, x1], dtype)   # torch.cat([x2, x1], dim=1)
 
     def units(self):
+        if isinstance(self.up, nn.Upsample):
+            return self.conv.units()
         return [(self.up, [self.up])] + self.conv.units()
 
 

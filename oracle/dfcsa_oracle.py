@@ -199,9 +199,10 @@ def unet_dfc_sa_res(x, sd, pool_size=8, training=True, bufs=None, full_res=False
 
 
 def unet(x, sd, training=True, bufs=None):
-    """models/unet.py:69-101 with bilinear=False: DoubleConv (:6-18), Down = MaxPool2d(2,
-    ceil_mode=True) + DoubleConv (:21-30), Up = ConvTranspose2d(k2, s2) + crop + cat([skip, up]) +
-    DoubleConv (:33-58), OutConv 1x1 (:61-66)."""
+    """models/unet.py:69-101: DoubleConv (:6-18), Down = MaxPool2d(2, ceil_mode=True) + DoubleConv
+    (:21-30), Up = ConvTranspose2d(k2, s2) -- or, bilinear=True (no up.weight in the state_dict),
+    nn.Upsample(scale_factor=2, bilinear, align_corners=True) (:36-37) -- + crop + cat([skip, up])
+    + DoubleConv (:33-58), OutConv 1x1 (:61-66)."""
     def dconv(t, n):
         for i in (0, 3):
             t = F.relu(batch_norm(conv(t, sd, f"{n}.conv.{i}", padding=1), sd, f"{n}.conv.{i + 1}", training, bufs))
@@ -211,7 +212,10 @@ def unet(x, sd, training=True, bufs=None):
         xs.append(dconv(F.max_pool2d(xs[-1], 2, ceil_mode=True), f"down{i}.mpconv.1"))
     u = xs[4]
     for i, skip in zip(range(1, 5), (xs[3], xs[2], xs[1], xs[0])):
-        u = F.conv_transpose2d(u, sd[f"up{i}.up.weight"], sd[f"up{i}.up.bias"], stride=2)
+        if f"up{i}.up.weight" in sd:
+            u = F.conv_transpose2d(u, sd[f"up{i}.up.weight"], sd[f"up{i}.up.bias"], stride=2)
+        else:
+            u = F.interpolate(u, scale_factor=2, mode="bilinear", align_corners=True)
         dy, dx = skip.shape[2] - u.shape[2], skip.shape[3] - u.shape[3]
         if dy < 0 or dx < 0:
             u = u[:, :, :skip.shape[2], :skip.shape[3]]

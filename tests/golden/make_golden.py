@@ -350,38 +350,48 @@ def gen_ddp():
 # ----------------------------------------------------------------------------------------
 # (6) Config 1 plumbing: plain UNet (widths hard-coded 64..1024) at 64x64, batch 2.
 # ----------------------------------------------------------------------------------------
+def _unet_run(seed, shape, name, bilinear=False):
+    """One seeded reference UNet forward/backward at `shape` (see gen_unet)."""
+    torch.manual_seed(seed)
+    m = ref_unet.UNet(3, 1, bilinear=bilinear)
+    init = {"init_sum." + k: np.float64(v.double().sum()) for k, v in m.state_dict().items()
+            if v.is_floating_point()}
+    m.train()
+    m64 = fp64_twin(m)
+    x = torch.randn(*shape)
+    t = (torch.rand(shape[0], 1, shape[2], shape[3]) > 0.5).float()
+    out = m(x)
+    met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", {})
+    met["loss"].backward()
+    met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", {})
+    met64["loss"].backward()
+    n = sum(p.numel() for p in m.parameters())
+    keep = [k for k, p in m.named_parameters()
+            if p.numel() <= 4096 or k in ("inc.conv.0.weight", "outc.conv.weight")]
+    g64 = dict(m64.named_parameters())
+    small = {"grad." + k: np32(p.grad) for k, p in m.named_parameters() if k in keep}
+    small.update({"grad64." + k: np32(g64[k].grad) for k in keep})
+    norms = {"gnorm." + k: np.float64(p.grad.double().norm()) for k, p in m.named_parameters()}
+    bufs = {"buf." + k: v.numpy().copy() for k, v in m.state_dict().items() if "running" in k}
+    save(name, x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]), iou=np.float64(met["iou"]),
+         dice=np.float64(met["dice"]), nparams=np.int64(n), **init, **small, **norms, **bufs,
+         **fp64_noise(m, m64))
+
+
 def gen_unet():
     """20x20 (odd sizes: ceil-mode pooling 20->10->5->3->2 and both crop branches) and the
     config-1 size 64x64, batch 2.  The 31 M parameters are not stored: the test builds the model
     under the same seed (module tree and init order are the reference's) and checks per-tensor
     init sums first; gradients are stored for the small tensors plus per-tensor norms."""
-    def run(seed, shape, name):
-        torch.manual_seed(seed)
-        m = ref_unet.UNet(3, 1, bilinear=False)
-        init = {"init_sum." + k: np.float64(v.double().sum()) for k, v in m.state_dict().items()
-                if v.is_floating_point()}
-        m.train()
-        m64 = fp64_twin(m)
-        x = torch.randn(*shape)
-        t = (torch.rand(shape[0], 1, shape[2], shape[3]) > 0.5).float()
-        out = m(x)
-        met = ref_metrics.calculate_metrics(torch.sigmoid(out), t, "bce_dice", {})
-        met["loss"].backward()
-        met64 = ref_metrics.calculate_metrics(torch.sigmoid(m64(x.double())), t.double(), "bce_dice", {})
-        met64["loss"].backward()
-        n = sum(p.numel() for p in m.parameters())
-        keep = [k for k, p in m.named_parameters()
-                if p.numel() <= 4096 or k in ("inc.conv.0.weight", "outc.conv.weight")]
-        g64 = dict(m64.named_parameters())
-        small = {"grad." + k: np32(p.grad) for k, p in m.named_parameters() if k in keep}
-        small.update({"grad64." + k: np32(g64[k].grad) for k in keep})
-        norms = {"gnorm." + k: np.float64(p.grad.double().norm()) for k, p in m.named_parameters()}
-        bufs = {"buf." + k: v.numpy().copy() for k, v in m.state_dict().items() if "running" in k}
-        save(name, x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]), iou=np.float64(met["iou"]),
-             dice=np.float64(met["dice"]), nparams=np.int64(n), **init, **small, **norms, **bufs,
-             **fp64_noise(m, m64))
-    run(6000, (2, 3, 20, 20), "unet_small.npz")
-    run(6001, (2, 3, 64, 64), "unet_cfg1.npz")
+    _unet_run(6000, (2, 3, 20, 20), "unet_small.npz")
+    _unet_run(6001, (2, 3, 64, 64), "unet_cfg1.npz")
+
+
+def gen_unet_bilinear():
+    """UNet(bilinear=True) (nn.Upsample align_corners=True in Up, unet.py:36-37; half-width down4 and
+    decoder): 20x20 (ceil-mode pooling and both crop branches) and 64x64, batch 2."""
+    _unet_run(6002, (2, 3, 20, 20), "unet_bilinear_small.npz", bilinear=True)
+    _unet_run(6003, (2, 3, 64, 64), "unet_bilinear_64.npz", bilinear=True)
 
 
 # ----------------------------------------------------------------------------------------
@@ -874,7 +884,7 @@ def gen_ckpt():
 
 if __name__ == "__main__":
     torch.set_num_threads(8)
-    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "fullres", "transunet", "inference", "zoo",
+    which = sys.argv[1:] or ["lsa", "block", "model", "metrics", "ddp", "unet", "unet_bilinear", "fullres", "transunet", "inference", "zoo",
                              "bf16calib", "cfg2", "ckpt"]
     for w in which:
         globals()["gen_" + w]()

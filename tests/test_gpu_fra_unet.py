@@ -318,16 +318,20 @@ def test_fullres_model_512_bf16_train_step_factory():
 # ----------------------------------------------------------------------------- plain U-Net (config 1)
 @pytest.mark.parametrize("name,seed,precision,tol", [("unet_small.npz", 6000, "fp32", 1e-4),
                                                      ("unet_cfg1.npz", 6001, "fp32", 1e-4),
-                                                     ("unet_cfg1.npz", 6001, "bf16", 2e-2)])
+                                                     ("unet_cfg1.npz", 6001, "bf16", 2e-2),
+                                                     ("unet_bilinear_small.npz", 6002, "fp32", 1e-4),
+                                                     ("unet_bilinear_64.npz", 6003, "fp32", 1e-4),
+                                                     ("unet_bilinear_64.npz", 6003, "bf16", 2e-2)])
 def test_unet_matches_reference(name, seed, precision, tol):
     """Seeded reference initialisation + one forward/backward: logits, loss, Dice/IoU, gradient
-    norms of every tensor and the full gradients of the small ones (fixture), BN running stats."""
+    norms of every tensor and the full gradients of the small ones (fixture), BN running stats.
+    unet_bilinear_*: UNet(bilinear=True) (nn.Upsample align_corners=True, reference unet.py:36-37)."""
     from dfcsa.loss import sigmoid
     from models.unet import UNet
     from utils.metrics import calculate_metrics
     fx = dict(np.load(os.path.join(GOLDEN, name)))
     torch.manual_seed(seed)
-    m = UNet(3, 1, precision=precision).cuda().train()
+    m = UNet(3, 1, bilinear=name.startswith("unet_bilinear"), precision=precision).cuda().train()
     logits = m(T(fx["x"]))
     met = calculate_metrics(sigmoid(logits), T(fx["t"]), "bce_dice", {})
     met["loss"].backward()

@@ -190,16 +190,19 @@ def test_full_res_model():
         close(grads[k], fx["grad." + k], rtol=1e-3, atol=1e-5)
 
 
-@pytest.mark.parametrize("name,seed", [("unet_small.npz", 6000), ("unet_cfg1.npz", 6001)])
-def test_unet_oracle_and_seeded_init(name, seed):
+@pytest.mark.parametrize("name,seed,bilinear", [("unet_small.npz", 6000, False), ("unet_cfg1.npz", 6001, False),
+                                                ("unet_bilinear_small.npz", 6002, True),
+                                                ("unet_bilinear_64.npz", 6003, True)])
+def test_unet_oracle_and_seeded_init(name, seed, bilinear):
     """The build's UNet module tree reproduces the reference's seeded initialisation (per-tensor
-    sums) and the oracle reproduces the reference's logits, loss, metrics and gradients."""
+    sums) and the oracle reproduces the reference's logits, loss, metrics and gradients; bilinear:
+    nn.Upsample(align_corners=True) in Up and the half-width decoder (reference unet.py:36-37, 78-88)."""
     from models.unet import UNet
     fx = dict(np.load(os.path.join(GOLDEN, name)))
     torch.manual_seed(seed)
-    m = UNet(3, 1)
+    m = UNet(3, 1, bilinear=bilinear)
     sd = {k: v.detach().clone() for k, v in m.state_dict().items()}
-    assert sum(p.numel() for p in m.parameters()) == int(fx["nparams"]) == 31043521
+    assert sum(p.numel() for p in m.parameters()) == int(fx["nparams"]) == (13395329 if bilinear else 31043521)
     for k, v in sd.items():
         if v.is_floating_point():
             assert abs(v.double().sum().item() - float(fx["init_sum." + k])) <= 1e-9 * max(1.0, abs(float(fx["init_sum." + k]))), k
