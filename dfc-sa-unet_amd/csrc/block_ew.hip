@@ -1043,6 +1043,48 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_kernel(const float* __re
   }
 }
 
+// bn_bwd_finalize<2> for the attention entry of a DFC block, whose dz2 = r * (dattn + pool_bwd(dpooled))
+// (r = relu'(bn2 y2)): the partial rows hold only the dattn part (dfcsa_bwd_relu_bn over dattn), and
+// the pool part is the [B][N][C] contraction
+//   sum_m r dz_pool = sum_{b,n} dpooled[b][n] / area_n * R[b][n],
+//   sum_m r dz_pool xhat = sum_{b,n} dpooled[b][n] / area_n * invstd * (Y[b][n] - mean * R[b][n])
+// with the forward pool's window sums R = sum r, Y = sum r*y2 (wsum [B][N][2][C]).  The 16 parts of
+// the finalising workgroup take the (b, n) entries round-robin; parts combine in order (fp64).
+__global__ void __launch_bounds__(1024) bn_bwd_finalize_pool_kernel(
+    const float* __restrict__ partial, int ntiles, int per, unsigned* cnt, double* scr, int C, int count, float* coef,
+    float* dgamma, float* dbeta, const float* __restrict__ dpooled, const float* __restrict__ wsum, int B, int H, int W,
+    int P, const float* __restrict__ mean, const float* __restrict__ invstd, int acq) {
+  __shared__ double sh[2][16][64];
+  __shared__ int flag;
+  const int cl = threadIdx.x & 63, part = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  double tot[2];
+  if (!colred_block<2>(partial, ntiles, 2 * C, C, C, per, cnt, scr, tot, sh, &flag, acq)) return;
+  __syncthreads();   // sh is reused below
+  double e0 = 0.0, e1 = 0.0;
+  if (c < C) {
+    const int N = P * P;
+    const double mu = (double)mean[c], is = (double)invstd[c];
+    for (int e = part; e < B * N; e += 16) {
+      const int n = e % N, pi = n / P, pj = n - pi * P;
+      const int area = (((pi + 1) * H + P - 1) / P - (pi * H) / P) * (((pj + 1) * W + P - 1) / P - (pj * W) / P);
+      const double d = (double)dpooled[(size_t)e * C + c] / (double)area;
+      const double R = (double)wsum[(size_t)e * 2 * C + c], Y = (double)wsum[(size_t)e * 2 * C + C + c];
+      e0 += d * R;
+      e1 += d * is * (Y - mu * R);
+    }
+  }
+  sh[0][part][cl] = e0;
+  sh[1][part][cl] = e1;
+  __syncthreads();
+  if (part != 0 || c >= C) return;
+  for (int p = 0; p < 16; ++p) { tot[0] += sh[0][p][cl]; tot[1] += sh[1][p][cl]; }
+  coef[c] = (float)(tot[0] / count);
+  coef[C + c] = (float)(tot[1] / count);
+  if (dgamma) dgamma[c] += (float)tot[1];
+  if (dbeta) dbeta[c] += (float)tot[0];
+}
+
 // out[c] += sum_t slab[t][c]; columns split over up to three destinations at n0, n0 + n1
 __global__ void __launch_bounds__(1024) slab_colsum_kernel(const float* __restrict__ slab, int ntiles, int per,
                                                            unsigned* cnt, double* scr, int C, int n0, int n1, float* d0,
@@ -1383,6 +1425,22 @@ extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum,
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
                        rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, nullptr, nullptr, rp.acq);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_bn_bwd_finalize_pool(const float* partial, int ntiles, int C, int count, float* coef,
+                                          float* dgamma, float* dbeta, const float* dpooled, const float* wsum, int B,
+                                          int H, int W, int P, const float* mean, const float* invstd, void* stream) {
+  if (!partial || ntiles <= 0 || C <= 0 || count <= 0 || !coef || !dpooled || !wsum || !mean || !invstd || B <= 0 ||
+      P <= 0 || H < P || W < P)
+    return DFCSA_EINVAL;
+  const int nblk = (C + 63) / 64;
+  RedPlan rp;
+  if (red_plan(ntiles, nblk, 2, 0, &rp)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(bn_bwd_finalize_pool_kernel, dim3(nblk, rp.R), dim3(1024), 0, (hipStream_t)stream, partial,
+                     ntiles, rp.per, rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, dpooled, wsum, B, H, W, P, mean,
+                     invstd, rp.acq);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -80,10 +80,11 @@ int pool_splits(int H, int P) {
 // grid (S, N, B): row slice s of window n of image b.  One load in flight per lane at 45 VGPRs:
 // occupancy hides the latency (an eight-loads-in-flight variant at 108 VGPRs measured slower,
 // profiles/r03c_lsa_bench.jsonl)
-template <typename T>
+template <typename T, bool WS = false>
 __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, const T* __restrict__ y2,
                                                        const float* __restrict__ sc, const float* __restrict__ sh,
-                                                       int P, int S, int relu, float* __restrict__ partial) {
+                                                       int P, int S, int relu, float* __restrict__ partial,
+                                                       float* __restrict__ wpart) {
   const int s = blockIdx.x, n = blockIdx.y, b = blockIdx.z;
   const int pi = n / P, pj = n - pi * P;
   const int hs = win_lo(pi, H, P), he = win_hi(pi, H, P);
@@ -94,6 +95,12 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
   const int cpp = C >> 3, pl = 256 / cpp;
   const int tid = threadIdx.x, lp = tid / cpp, ck = tid - lp * cpp, c0 = ck * 8;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  // WS: the window sums the attention-entry backward needs (relu mask r = [bn(y) > 0]):
+  // sum r and sum r*y, so that backward's pool term is a [B][N][C] contraction
+  float accr[WS ? 8 : 1], accy[WS ? 8 : 1];
+  if constexpr (WS)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) { accr[q] = 0.f; accy[q] = 0.f; }
   if (lp < pl) {
     float a[8], bb[8];
     for (int q = 0; q < 8; ++q) { a[q] = sc[c0 + q]; bb[q] = sh[c0 + q]; }
@@ -106,24 +113,44 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
       for (int q = 0; q < 8; ++q) {
         const float t = v[q] * a[q] + bb[q];
         acc[q] += relu ? fmaxf(t, 0.f) : t;
+        if constexpr (WS) {
+          const float r = (!relu || t > 0.f) ? 1.f : 0.f;
+          accr[q] += r;
+          accy[q] += r * v[q];
+        }
       }
     }
   }
   __shared__ __attribute__((aligned(16))) float red[256 * 8];
-  if (lp < pl) lds_st8(red + tid * 8, acc);
-  __syncthreads();
-  float* out = partial + (((size_t)b * P * P + n) * S + s) * C;
-  for (int c = tid; c < C; c += 256) {
-    const int k = c >> 3, q = c & 7;
-    float v = 0.f;
-    for (int p = 0; p < pl; ++p) v += red[(p * cpp + k) * 8 + q];
-    out[c] = v;
+  for (int k = 0; k < (WS ? 3 : 1); ++k) {
+    if (k) __syncthreads();
+    if (lp < pl) {
+      if constexpr (WS) {
+        if (k == 1) lds_st8(red + tid * 8, accr);
+        else if (k == 2) lds_st8(red + tid * 8, accy);
+        else lds_st8(red + tid * 8, acc);
+      } else {
+        lds_st8(red + tid * 8, acc);
+      }
+    }
+    __syncthreads();
+    // k = 0: partial [B][N][S][C]; k = 1, 2: wpart [B][N][S][2][C]
+    float* out = k == 0 ? partial + (((size_t)b * P * P + n) * S + s) * C
+                        : wpart + ((((size_t)b * P * P + n) * S + s) * 2 + (k - 1)) * C;
+    for (int c = tid; c < C; c += 256) {
+      const int kk = c >> 3, q = c & 7;
+      float v = 0.f;
+      for (int p = 0; p < pl; ++p) v += red[(p * cpp + kk) * 8 + q];
+      out[c] = v;
+    }
   }
 }
 
-// grid (N, B): pooled[b][n][c] = sum of the S partial slices / window area
+// grid (N, B): pooled[b][n][c] = sum of the S partial slices / window area; with wpart, also the
+// window sums wsum[b][n][2][c] (sum r, sum r*y over the window, summed over the S slices)
 __global__ void __launch_bounds__(256) lsa_pooled_kernel(int H, int W, int C, int P, int S,
-                                                         const float* __restrict__ partial, float* __restrict__ pooled) {
+                                                         const float* __restrict__ partial, float* __restrict__ pooled,
+                                                         const float* __restrict__ wpart, float* __restrict__ wsum) {
   const int n = blockIdx.x, b = blockIdx.y, N = P * P;
   const int pi = n / P, pj = n - pi * P;
   const float inv = 1.f / (float)((win_hi(pi, H, P) - win_lo(pi, H, P)) * (win_hi(pj, W, P) - win_lo(pj, W, P)));
@@ -132,6 +159,13 @@ __global__ void __launch_bounds__(256) lsa_pooled_kernel(int H, int W, int C, in
     float s = 0.f;
     for (int k = 0; k < S; ++k) s += p[(size_t)k * C + c];
     pooled[((size_t)b * N + n) * C + c] = s * inv;
+  }
+  if (!wpart) return;
+  const float* q = wpart + (((size_t)b * N + n) * S) * 2 * C;
+  for (int e = threadIdx.x; e < 2 * C; e += 256) {
+    float s = 0.f;
+    for (int k = 0; k < S; ++k) s += q[(size_t)k * 2 * C + e];
+    wsum[((size_t)b * N + n) * 2 * C + e] = s;
   }
 }
 
@@ -662,28 +696,48 @@ __global__ void __launch_bounds__(256) lsa_proj_dx_kernel(int C, int Cq, const f
 
 extern "C" int dfcsa_lsa_pool_splits(int H, int P) { return pool_splits(H, P); }
 
-extern "C" int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
-                              const float* sh2, int P, int relu, float* partial, void* stream) {
+extern "C" int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                                 const float* sh2, int P, int relu, float* partial, float* wpart, void* stream) {
   if (C % 8 || C > 2048 || P <= 0) return DFCSA_EINVAL;
   const int S = pool_splits(H, P);
   dim3 grid(S, P * P, B);
   hipStream_t st = (hipStream_t)stream;
-  if (dtype == DFCSA_DT_BF16)
-    hipLaunchKernelGGL(lsa_pool_kernel<bf16_t>, grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2, sh2, P, S,
-                       relu, partial);
-  else
-    hipLaunchKernelGGL(lsa_pool_kernel<float>, grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2, P, S,
-                       relu, partial);
+  if (dtype == DFCSA_DT_BF16) {
+    if (wpart)
+      hipLaunchKernelGGL((lsa_pool_kernel<bf16_t, true>), grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2,
+                         sh2, P, S, relu, partial, wpart);
+    else
+      hipLaunchKernelGGL((lsa_pool_kernel<bf16_t, false>), grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2,
+                         sh2, P, S, relu, partial, wpart);
+  } else {
+    if (wpart)
+      hipLaunchKernelGGL((lsa_pool_kernel<float, true>), grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2,
+                         P, S, relu, partial, wpart);
+    else
+      hipLaunchKernelGGL((lsa_pool_kernel<float, false>), grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2,
+                         P, S, relu, partial, wpart);
+  }
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                              const float* sh2, int P, int relu, float* partial, void* stream) {
+  return dfcsa_lsa_pool_ws(dtype, B, H, W, C, y2, sc2, sh2, P, relu, partial, nullptr, stream);
+}
+
+extern "C" int dfcsa_lsa_pooled_ws(int B, int H, int W, int C, int P, const float* partial, float* pooled,
+                                   const float* wpart, float* wsum, void* stream) {
+  if ((wpart == nullptr) != (wsum == nullptr)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(lsa_pooled_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, W, C, P,
+                     pool_splits(H, P), partial, pooled, wpart, wsum);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
 
 extern "C" int dfcsa_lsa_pooled(int B, int H, int W, int C, int P, const float* partial, float* pooled,
                                 void* stream) {
-  hipLaunchKernelGGL(lsa_pooled_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, W, C, P,
-                     pool_splits(H, P), partial, pooled);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
+  return dfcsa_lsa_pooled_ws(B, H, W, C, P, partial, pooled, nullptr, nullptr, stream);
 }
 
 extern "C" int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,

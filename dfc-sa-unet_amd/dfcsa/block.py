@@ -138,7 +138,8 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
         if not fullres:
             Pp = pool_size
-            lsa_saved = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk)
+            lsa_saved = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk,
+                                         window_sums=training and ENTRY_WS[0] and ops._SYNC_BN is None)
     y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st1 = stats(C)
     nt1 = ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
@@ -158,7 +159,8 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # ---- LightSelfAttention on the pooled map ----
         s.fra = None
         J, N = 2 * Cq + C, Pp * Pp
-        pooled, qkv, A, o, Wqkv = lsa_saved
+        pooled, qkv, A, o, Wqkv = lsa_saved[:5]
+        s.wsum = lsa_saved[5] if len(lsa_saved) > 5 else None
         local = torch.empty((B, H, W, C), dtype=dtype, device=dev)
         attn = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
@@ -404,29 +406,49 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     # the attention chain (LightSelfAttention backward -> attention entry -> bn2 backward) runs
     # on the branch stream beside the local branch's bn1 backward (streams.on_branch)
     branch = s.fra is None and ops._SYNC_BN is None
-    with on_branch(dev, branch, dattn):
-        # (dz2 is not materialised: the apply recomputes it from the same inputs)
-        part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
-        if s.fra is not None:
-            # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
-            da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
-            s.fra = None
-            call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-                 P(bn2.invstd), None, *S(part2), stream())
-            coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
-            dy2 = ops.bn_bwd_apply_relu(dtype, da, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
-            del da
-        else:
-            # ---- LightSelfAttention ----
+    wsum = getattr(s, "wsum", None)
+    if s.fra is None and wsum is not None:
+        # the attention chain's statistics without a pass after it: the dattn part of the entry's
+        # BN2-backward sums on this stream, beside the attention backward on the branch; the
+        # pool part is a [B][N][C] contraction with the forward pool's window sums, inside the
+        # finalize (dfcsa_bn_bwd_finalize_pool)
+        with on_branch(dev, branch, dattn):
             dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
-            # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
-            call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
-                 P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, None, *S(part2), stream())
-            coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+        part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+        call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+             P(bn2.invstd), None, *S(part2), stream())
+        with on_branch(dev, branch, part2, dattn, wsum):
+            coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias), dpooled,
+                                             wsum, B, H, W, Pp, bn2)
             dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
                                          grad_of(conv2.bias))
-            del dpooled
-        del part2, coef2
+            del dpooled, coef2
+        del part2
+        s.wsum = None
+    else:
+        with on_branch(dev, branch, dattn):
+            # (dz2 is not materialised: the apply recomputes it from the same inputs)
+            part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+            if s.fra is not None:
+                # ---- full-resolution attention: da = dattn + projections' dgrad; then relu(bn2 y2) ----
+                da = fra.core_backward(lsa, s.fra, dattn, dtype, s.pk)
+                s.fra = None
+                call("dfcsa_bwd_relu_bn", T, M, C, P(da), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+                     P(bn2.invstd), None, *S(part2), stream())
+                coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+                dy2 = ops.bn_bwd_apply_relu(dtype, da, s.y2, bn2, bn2m.weight, coef2, grad_of(conv2.bias))
+                del da
+            else:
+                # ---- LightSelfAttention ----
+                dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
+                # ---- attention entry: a = relu(bn2 y2) feeds the pool and the attn residual ----
+                call("dfcsa_bwd_attn_entry", T, B, H, W, C, P(dattn), P(dpooled), Pp, P(s.y2), P(bn2.scale),
+                     P(bn2.shift), P(bn2.mean), P(bn2.invstd), 1, None, *S(part2), stream())
+                coef2 = ops.bn_bwd_finalize(part2, nte, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+                dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
+                                             grad_of(conv2.bias))
+                del dpooled
+            del part2, coef2
     del dattn
 
     # ---- local branch: relu(bn1 y1) (dz1 recomputed by the apply, not materialised) ----
@@ -472,13 +494,21 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     return dxs
 
 
+# the attention-entry BN2-backward statistics from the forward pool's window sums (no full-resolution
+# pass after the attention backward); DFCSA_ENTRY_WS=0 restores the dfcsa_bwd_attn_entry pass
+ENTRY_WS = [os.environ.get("DFCSA_ENTRY_WS", "1") == "1"]
+
+
 def _lsa_gemm_ok(C, J):
     return C % 8 == 0 and J % 8 == 0 and C >= 64
 
 
-def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk):
+def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_sums=False):
     """LightSelfAttention up to the pooled output o (unet_dfc_sa_res.py:24-34): pool of
-    act(y*scale + shift) -> q/k/v 1x1 convs -> softmax(q k^T) -> o = v A^T (all fp32)."""
+    act(y*scale + shift) -> q/k/v 1x1 convs -> softmax(q k^T) -> o = v A^T (all fp32).
+    window_sums: also return the pool windows' sums of the relu mask r and of r*y ([B][N][2][C],
+    dfcsa_lsa_pooled_ws) for the attention-entry backward (dfcsa_bn_bwd_finalize_pool); on the
+    projection-GEMM path only (otherwise the 6th element is None)."""
     B, H, W, C = y.shape
     dev = y.device
     f32 = torch.float32
@@ -488,13 +518,17 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk):
     J = 2 * Cq + C
     S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
-    call("dfcsa_lsa_pool", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), stream())
+    ws = window_sums and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
+    wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
+    wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
+    call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), P(wpart),
+         stream())
     bqkv = pk["bqkv"]
     pooled = torch.empty((B, N, C), device=dev, dtype=f32)
     qkv = torch.empty((B, N, J), device=dev, dtype=f32)
     if _lsa_gemm_ok(C, J):
         # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
-        call("dfcsa_lsa_pooled", B, H, W, C, Pp, P(part), P(pooled), stream())
+        call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
         Kp = rup(C, ops.KALIGN)
         Wp = pk["Wp"]
         ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), Wp, Kp, J, [qkv], J, bias=bqkv)
@@ -505,6 +539,8 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk):
     A = torch.empty((B, N, N), device=dev, dtype=f32)
     o = torch.empty((B, N, C), device=dev, dtype=f32)
     call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
+    if window_sums:
+        return pooled, qkv, A, o, Wqkv, wsum
     return pooled, qkv, A, o, Wqkv
 
 

@@ -317,6 +317,19 @@ def bn_bwd_finalize(partial, ntiles, nsum, C, count, dgamma, dbeta, extra=None):
     return coef
 
 
+def bn_bwd_finalize_pool(partial, ntiles, C, count, dgamma, dbeta, dpooled, wsum, B, H, W, P_, bn):
+    """bn_bwd_finalize (2 sums) of a DFC block's attention entry: `partial` holds the dattn part of
+    the sums, the pool-backward part comes from the forward pool's window sums (dfcsa_bn_bwd_finalize_pool)."""
+    coef = torch.empty(3 * C, device=partial.device, dtype=torch.float32)
+    if _SKIP_FIN:
+        return coef
+    if _SYNC_BN is not None:
+        raise NotImplementedError("the window-sum entry statistics are per replica (SyncBN uses the entry pass)")
+    call("dfcsa_bn_bwd_finalize_pool", P(partial), ntiles, C, count, P(coef), P(dgamma), P(dbeta), P(dpooled),
+         P(wsum), B, H, W, P_, P(bn.mean), P(bn.invstd), stream())
+    return coef
+
+
 # The gradient of a conv bias that feeds a train-mode BatchNorm is exactly zero:
 #   sum_m dy_m = gamma*invstd*(sum_m dz_m - M*mean(dz) - mean(dz*xh)*sum_m xh_m) = 0  (sum xh = 0).
 # The reference's autograd evaluates it in floating point (rounding noise ~1e-7 of the weight

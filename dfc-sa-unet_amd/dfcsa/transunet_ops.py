@@ -374,7 +374,11 @@ class PatchEmbed(torch.autograd.Function):
     def forward(ctx, x, emb, dtype, p, rng, *params):
         conv, pos = emb.patch_embeddings, emb.position_embeddings
         if conv.kernel_size != (1, 1) or conv.stride != (1, 1):
-            raise NotImplementedError("patch embeddings with patch size > 1 (img_size != 16 * grid) are not built")
+            # the reference cannot run this either: patch size = img // 16 // grid > 1 gives
+            # (img / 16 / patch)^2 tokens but (img / 16)^2 position embeddings, and the add in
+            # Embeddings.forward fails (reference models/transformer_unet.py:175-199)
+            raise NotImplementedError("patch embeddings with patch size > 1 (img_size != 16 * grid) are not built "
+                                      "(the reference's position-embedding add fails for them as well)")
         B, h, w, Cin = x.shape
         D = conv.out_channels
         if pos.shape[1] != h * w:

@@ -229,6 +229,8 @@ class SegmentationHead(nn.Sequential):
     def __init__(self, in_channels, out_channels, kernel_size=3, upsampling=1):
         conv2d = nn.Conv2d(in_channels, out_channels, kernel_size=kernel_size, padding=kernel_size // 2)
         if upsampling > 1:
+            # the reference's TransUNet builds its head with the default upsampling = 1
+            # (reference models/transformer_unet.py:355-358); only a standalone head could ask for more
             raise NotImplementedError("SegmentationHead upsampling > 1 is not built (TransUNet uses 1)")
         super().__init__(conv2d, nn.Identity())
 

@@ -341,6 +341,15 @@ int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* datt
  * dbeta += sum dz; if nsum == 3 and extra != null: *extra += sum over c of the third sum. */
 int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count,
                           float* coef, float* dgamma, float* dbeta, float* extra, void* stream);
+/* dfcsa_bn_bwd_finalize (nsum = 2) for a DFC block's attention entry: `partial` holds the sums of
+ * dfcsa_bwd_relu_bn over dattn alone, and the launch adds the pool-backward part from the forward
+ * pool's window sums (dfcsa_lsa_pooled_ws: wsum [B][P*P][2][C]) and dpooled [B][P*P][C]:
+ *   sum r*pb = sum_{b,n} dpooled/area_n * R,  sum r*pb*xhat = sum dpooled/area_n * invstd*(Y - mean*R)
+ * -- the same coefficients as dfcsa_bwd_attn_entry's statistics, without its full-resolution pass
+ * after the attention backward (adaptive windows of an H x W map pooled to P x P). */
+int dfcsa_bn_bwd_finalize_pool(const float* partial, int ntiles, int C, int count, float* coef, float* dgamma,
+                               float* dbeta, const float* dpooled, const float* wsum, int B, int H, int W, int P,
+                               const float* mean, const float* invstd, void* stream);
 /* dy = gamma*invstd*(dz - coef0 - xh*coef1); partial column sums of dy -> bias_partial
  * [ntiles][C] (conv bias gradient; NULL = not computed: for a conv feeding a train-mode
  * BatchNorm it is exactly zero, sum_m dy = gamma*invstd*(sum dz - M*coef0 - coef1*sum xh) = 0) */
@@ -383,6 +392,15 @@ int dfcsa_lsa_pool(int dtype, int B, int H, int W, int C, const void* y2, const 
                    const float* sh2, int P, int relu, float* partial, void* stream);
 /* pooled = partial sums / window area  ([B][N][C] fp32) */
 int dfcsa_lsa_pooled(int B, int H, int W, int C, int P, const float* partial, float* pooled, void* stream);
+/* dfcsa_lsa_pool / dfcsa_lsa_pooled that also form the window sums of the relu mask of the pooled
+ * activation, r = [y*sc + sh > 0] (r = 1 without relu): wpart [B][N][S][2][C] (S =
+ * dfcsa_lsa_pool_splits) holds per-slice sum r and sum r*y, and the pooled launch reduces them into
+ * wsum [B][N][2][C].  The attention-entry backward then needs no full-resolution statistics pass of
+ * its own (dfcsa_bn_bwd_finalize_pool). */
+int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                      const float* sh2, int P, int relu, float* partial, float* wpart, void* stream);
+int dfcsa_lsa_pooled_ws(int B, int H, int W, int C, int P, const float* partial, float* pooled,
+                        const float* wpart, float* wsum, void* stream);
 /* pooled = partial sums / window area; qkv = pooled @ wT + b  (wT: [C][2Cq+C] fp32) */
 int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,
                   const float* bias, float* pooled, float* qkv, void* stream);

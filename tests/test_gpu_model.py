@@ -260,3 +260,40 @@ def test_trainer_resume(tmp_path, reference_semantics):
     else:
         assert tr2.epochs == [1, 2, 3] and tr2.train_losses[:2] == tr.train_losses
         assert len(tr2.val_dice_scores) == 3
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("B,cin,C,H,W,P", [(2, 64, 64, 16, 16, 4), (2, 32, 64, 14, 14, 4), (3, 64, 128, 28, 20, 8),
+                                          (2, 128, 128, 13, 11, 4)])
+def test_block_entry_window_sums_equal_entry_pass(dtype, B, cin, C, H, W, P):
+    """The attention entry's BN2-backward statistics from the forward pool's window sums
+    (dfcsa_lsa_pooled_ws + dfcsa_bn_bwd_finalize_pool, default) against the full-resolution entry
+    pass (dfcsa_bwd_attn_entry, DFCSA_ENTRY_WS=0): exact and adaptive (overlapping) windows; every
+    parameter gradient and the input gradient agree to the summation-order rounding."""
+    from dfcsa import block as dblock
+    from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock
+    torch.manual_seed(H * W + C)
+    blk = DynamicFusionConvAttnBlock(cin, C, pool_size=P).cuda().train()
+    with torch.no_grad():
+        blk.attn_branch[3].gamma.fill_(0.7)   # a live attention path
+    blk.compute_dtype = dtype
+    x = torch.randn(B, cin, H, W, device="cuda")
+    g = torch.randn(B, C, H, W, device="cuda")
+    res = []
+    for ws in (True, False):
+        dblock.ENTRY_WS[0] = ws
+        try:
+            blk.zero_grad(set_to_none=True)
+            xi = x.clone().requires_grad_(True)
+            blk(xi).backward(g)
+            torch.cuda.synchronize()
+        finally:
+            dblock.ENTRY_WS[0] = True
+        res.append((xi.grad.clone(), {n: p.grad.clone() for n, p in blk.named_parameters()}))
+    tol = 1e-5 if dtype == torch.float32 else 2e-2
+    assert rel(res[0][0], res[1][0]) < tol
+    for n, g0 in res[0][1].items():
+        g1 = res[1][1][n]
+        if n.endswith("attn_branch.0.bias") or n.endswith("conv_branch.0.bias"):
+            continue   # exactly zero in both (the BN-preceded conv bias)
+        assert rel(g0, g1) < tol, (n, rel(g0, g1))
