@@ -379,7 +379,7 @@ __device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, flo
 }
 
 template <typename T, int MODE>
-__global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
+__device__ __forceinline__ void ew_red_body(const EwArgs& a, const int bx) {
   constexpr int NS = NSums<MODE>::v;
   const int cpp = a.C >> 3;                   // chunks per pixel (<= 256)
   const int pl = 256 / cpp;                   // pixel lanes
@@ -402,7 +402,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   T* __restrict__ O0 = (T*)a.o0;
   T* __restrict__ O1 = (T*)a.o1;
   T* __restrict__ O2 = (T*)a.o2;
-  const int mbeg = blockIdx.x * a.tile_px;
+  const int mbeg = bx * a.tile_px;
   const int mend = min(a.M, mbeg + a.tile_px);
   float sc[8], sh[8], mu[8], is[8];
   float gk[8], k0[8], k1[8];   // BN_BWD_APPLY: gamma*invstd, coef0, coef1 (loop-invariant per lane)
@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
   if (!a.partial) return;  // sums not wanted (e.g. the analytically-zero conv-bias gradient)
   // deterministic in-workgroup reduction over pixel lanes
   __shared__ __attribute__((aligned(16))) float red[4 * 3 * 512];
-  float* out = a.partial + (size_t)blockIdx.x * NS * a.C;
+  float* out = a.partial + (size_t)bx * NS * a.C;
   const bool pow2 = (cpp & (cpp - 1)) == 0;
   if (pow2 && cpp <= 64) {
     // lanes l and l ^ (k*cpp) hold the same channels: butterfly over the wave's pixel lanes,
@@ -610,6 +610,19 @@ __global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
     }
     __syncthreads();
   }
+}
+
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) ew_red_kernel(const EwArgs a) {
+  ew_red_body<T, MODE>(a, blockIdx.x);
+}
+
+// two independent reductions of one mode in one launch (workgroups [0, n0) take `a`, the rest `b`):
+// e.g. the local branch's and the attention entry's BN-backward sums of a DFC block
+template <typename T, int MODE>
+__global__ void __launch_bounds__(256) ew_red_pair_kernel(const EwArgs a, const EwArgs b, int n0) {
+  if ((int)blockIdx.x < n0) ew_red_body<T, MODE>(a, blockIdx.x);
+  else ew_red_body<T, MODE>(b, blockIdx.x - n0);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1384,6 +1397,29 @@ extern "C" int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, cons
   EwArgs a = zargs(M, C);
   a.a0 = dact; a.a1 = y; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.o0 = dz; a.partial = partial; a.partial_cap = partial_floats;
   return launch_red<EW_BWD_RELU_BN>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bwd_relu_bn_pair(int dtype, int M, int C, const void* dact0, const void* y0, const float* sc0,
+                                      const float* sh0, const float* mean0, const float* invstd0, float* partial0,
+                                      const void* dact1, const void* y1, const float* sc1, const float* sh1,
+                                      const float* mean1, const float* invstd1, float* partial1,
+                                      int64_t partial_floats, void* stream) {
+  EwArgs a = zargs(M, C), b = zargs(M, C);
+  a.a0 = dact0; a.a1 = y0; a.sc = sc0; a.sh = sh0; a.mean = mean0; a.invstd = invstd0;
+  a.partial = partial0; a.partial_cap = partial_floats;
+  b.a0 = dact1; b.a1 = y1; b.sc = sc1; b.sh = sh1; b.mean = mean1; b.invstd = invstd1;
+  b.partial = partial1; b.partial_cap = partial_floats;
+  if (C % 8 || C > 2048 || M <= 0 || !partial0 || !partial1) return DFCSA_EINVAL;
+  a.tile_px = b.tile_px = tile_px(C);
+  const int blocks = (M + a.tile_px - 1) / a.tile_px;
+  if ((int64_t)blocks * 2 * C > partial_floats) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL((ew_red_pair_kernel<bf16_t, EW_BWD_RELU_BN>), dim3(2 * blocks), dim3(256), 0, st, a, b, blocks);
+  else
+    hipLaunchKernelGGL((ew_red_pair_kernel<float, EW_BWD_RELU_BN>), dim3(2 * blocks), dim3(256), 0, st, a, b, blocks);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
 }
 
 extern "C" int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,

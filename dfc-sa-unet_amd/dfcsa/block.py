@@ -407,6 +407,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     # on the branch stream beside the local branch's bn1 backward (streams.on_branch)
     branch = s.fra is None and ops._SYNC_BN is None
     wsum = getattr(s, "wsum", None)
+    local_part = None
     if s.fra is None and wsum is not None:
         # the attention chain's statistics without a pass after it: the dattn part of the entry's
         # BN2-backward sums on this stream, beside the attention backward on the branch; the
@@ -415,8 +416,14 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         with on_branch(dev, branch, dattn):
             dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
         part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
-        call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-             P(bn2.invstd), None, *S(part2), stream())
+        if fused_bn1:
+            call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+                 P(bn2.invstd), None, *S(part2), stream())
+        else:   # with the local branch's BN1-backward sums in the same launch
+            local_part = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+            call("dfcsa_bwd_relu_bn_pair", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+                 P(bn2.invstd), P(part2), P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
+                 P(bn1.invstd), P(local_part), part2.numel(), stream())
         with on_branch(dev, branch, part2, dattn, wsum):
             coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias), dpooled,
                                              wsum, B, H, W, Pp, bn2)
@@ -452,7 +459,9 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     del dattn
 
     # ---- local branch: relu(bn1 y1) (dz1 recomputed by the apply, not materialised) ----
-    if fused_bn1:
+    if local_part is not None:   # formed beside the attention entry's sums (dfcsa_bwd_relu_bn_pair)
+        part, npart = local_part, nte
+    elif fused_bn1:
         part, npart = part1, npart1
     else:
         part, npart = torch.empty(nte * 2 * C, device=dev, dtype=f32), nte

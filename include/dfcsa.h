@@ -268,6 +268,15 @@ int dfcsa_bwd_block_out_pool(int dtype, int B, int H, int W, int C, const void* 
 int dfcsa_bwd_relu_bn(int dtype, int M, int C, const void* dact, const void* y, const float* sc,
                       const float* sh, const float* mean, const float* invstd, void* dz,
                       float* partial, int64_t partial_floats, void* stream);
+/* two dfcsa_bwd_relu_bn statistics passes (dz not stored) of the same shape in one launch:
+ * (dact0, y0, bn 0) -> partial0 and (dact1, y1, bn 1) -> partial1, each of dfcsa_ew_ntiles(M, C) rows
+ * of [2][C] (partial_floats: the capacity of each) -- a DFC block's local-branch and attention-entry
+ * BatchNorm-backward sums */
+int dfcsa_bwd_relu_bn_pair(int dtype, int M, int C, const void* dact0, const void* y0, const float* sc0,
+                           const float* sh0, const float* mean0, const float* invstd0, float* partial0,
+                           const void* dact1, const void* y1, const float* sc1, const float* sh1,
+                           const float* mean1, const float* invstd1, float* partial1, int64_t partial_floats,
+                           void* stream);
 /* gate: g = sigmoid(y3*sc3+sh3); dz3 = dfused*(local-attn)*g*(1-g); dlocal += dfused*g;
  * dattn += dfused*(1-g); sums [sum dz3, sum dz3*xh3] */
 int dfcsa_bwd_gate(int dtype, int M, int C, const void* dfused, const void* y3, const float* sc3,

@@ -1193,3 +1193,26 @@ def test_conv_transpose_fwd_streaming(B, h, w, Cin, Cout):
         ref = torch.nn.functional.conv_transpose2d(x, mod.weight.cpu(), mod.bias.cpu(), stride=2)
     assert rel(outs[0].float(), outs[1].float()) < 4e-3   # same K order; a bf16 rounding flip at most
     assert rel(nchw(outs[0]), ref) < 1e-2
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C", [(4096, 64), (3000, 128), (50176, 256)])
+def test_bwd_relu_bn_pair_equals_two_launches(dtype, M, C):
+    """dfcsa_bwd_relu_bn_pair: two BatchNorm-backward statistics passes in one launch, bit-identical
+    to two dfcsa_bwd_relu_bn launches."""
+    from dfcsa._lib import LIB, call
+    torch.manual_seed(M + C)
+    t = lambda: torch.randn(M, C, device="cuda").to(dtype)   # noqa: E731
+    v = lambda: torch.randn(C, device="cuda")                 # noqa: E731
+    d0, y0, d1, y1 = t(), t(), t(), t()
+    bn = [(v(), v(), v(), v().abs() + 0.5) for _ in range(2)]
+    nt = LIB.dfcsa_ew_ntiles(M, C)
+    pa, pb = torch.empty(nt * 2 * C, device="cuda"), torch.empty(nt * 2 * C, device="cuda")
+    qa, qb = torch.empty_like(pa), torch.empty_like(pb)
+    dt = 1 if dtype == torch.bfloat16 else 0
+    call("dfcsa_bwd_relu_bn_pair", dt, M, C, P(d0), P(y0), *[P(x) for x in bn[0]], P(pa), P(d1), P(y1),
+         *[P(x) for x in bn[1]], P(pb), pa.numel(), stream())
+    call("dfcsa_bwd_relu_bn", dt, M, C, P(d0), P(y0), *[P(x) for x in bn[0]], None, P(qa), qa.numel(), stream())
+    call("dfcsa_bwd_relu_bn", dt, M, C, P(d1), P(y1), *[P(x) for x in bn[1]], None, P(qb), qb.numel(), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(pa, qa) and torch.equal(pb, qb)

@@ -3,7 +3,7 @@
 mkdir -p gpurun_out
 R=$GRAFT_REPO_ROOT
 cd $R
-timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pack or layout2 or lsa or dgrad1x1 or conv_transpose" > gpurun_out/t_pack.log 2>&1 || { tail -30 gpurun_out/t_pack.log; exit 1; }
+timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_kernels.py -k "pack or layout2 or lsa or dgrad1x1 or conv_transpose or relu_bn_pair" > gpurun_out/t_pack.log 2>&1 || { tail -30 gpurun_out/t_pack.log; exit 1; }
 tail -1 gpurun_out/t_pack.log
 timeout -k 10 300 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_model.py tests/test_gpu_fra_unet.py::test_unet_matches_reference tests/test_gpu_parity2.py -k "not rccl and not bench_ddp" > gpurun_out/t_pack2.log 2>&1 || { tail -30 gpurun_out/t_pack2.log; exit 1; }
 tail -1 gpurun_out/t_pack2.log
