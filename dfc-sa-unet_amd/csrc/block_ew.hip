@@ -1074,17 +1074,38 @@ __global__ void __launch_bounds__(1024) bn_bwd_finalize_pool_kernel(
   double tot[2];
   if (!colred_block<2>(partial, ntiles, 2 * C, C, C, per, cnt, scr, tot, sh, &flag, acq)) return;
   __syncthreads();   // sh is reused below
+  // 1 / window area per pooled position n (adaptive windows), once per workgroup
+  __shared__ float inv_area[256];
+  const int N = P * P;
+  for (int n = threadIdx.x; n < N && n < 256; n += 1024) {
+    const int pi = n / P, pj = n - pi * P;
+    inv_area[n] = 1.f / (float)((((pi + 1) * H + P - 1) / P - (pi * H) / P) * (((pj + 1) * W + P - 1) / P - (pj * W) / P));
+  }
+  __syncthreads();
   double e0 = 0.0, e1 = 0.0;
   if (c < C) {
-    const int N = P * P;
     const double mu = (double)mean[c], is = (double)invstd[c];
-    for (int e = part; e < B * N; e += 16) {
-      const int n = e % N, pi = n / P, pj = n - pi * P;
-      const int area = (((pi + 1) * H + P - 1) / P - (pi * H) / P) * (((pj + 1) * W + P - 1) / P - (pj * W) / P);
-      const double d = (double)dpooled[(size_t)e * C + c] / (double)area;
-      const double R = (double)wsum[(size_t)e * 2 * C + c], Y = (double)wsum[(size_t)e * 2 * C + C + c];
-      e0 += d * R;
-      e1 += d * is * (Y - mu * R);
+    const int BNn = B * N;
+    const float rN = 1.f / (float)N;
+    // part p takes entries p, p + 16, ...; eight entries' loads in flight per round, summed in order
+    for (int eb = part; eb < BNn; eb += 16 * 8) {
+      float d[8], r[8], y[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = min(eb + 16 * u, BNn - 1);
+        d[u] = dpooled[(size_t)e * C + c];
+        r[u] = wsum[(size_t)e * 2 * C + c];
+        y[u] = wsum[(size_t)e * 2 * C + C + c];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = eb + 16 * u;
+        if (e >= BNn) break;
+        const int n = e - N * (int)(((float)e + 0.5f) * rN);   // e mod N (exact: e < 2^20)
+        const double dd = (double)d[u] * (double)(N <= 256 ? inv_area[n] : 0.f);
+        e0 += dd * (double)r[u];
+        e1 += dd * is * ((double)y[u] - mu * (double)r[u]);
+      }
     }
   }
   sh[0][part][cl] = e0;
@@ -1469,7 +1490,7 @@ extern "C" int dfcsa_bn_bwd_finalize_pool(const float* partial, int ntiles, int 
                                           float* dgamma, float* dbeta, const float* dpooled, const float* wsum, int B,
                                           int H, int W, int P, const float* mean, const float* invstd, void* stream) {
   if (!partial || ntiles <= 0 || C <= 0 || count <= 0 || !coef || !dpooled || !wsum || !mean || !invstd || B <= 0 ||
-      P <= 0 || H < P || W < P)
+      P <= 0 || P * P > 256 || H <= 0 || W <= 0 || (int64_t)B * P * P >= (1 << 20))
     return DFCSA_EINVAL;
   const int nblk = (C + 63) / 64;
   RedPlan rp;

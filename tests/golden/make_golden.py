@@ -373,9 +373,15 @@ def _unet_run(seed, shape, name, bilinear=False):
     small.update({"grad64." + k: np32(g64[k].grad) for k in keep})
     norms = {"gnorm." + k: np.float64(p.grad.double().norm()) for k, p in m.named_parameters()}
     bufs = {"buf." + k: v.numpy().copy() for k, v in m.state_dict().items() if "running" in k}
+    extra = {}
+    if bilinear:   # the reference's own bf16 error on this batch (CPU autocast, same weights): the bf16 bar
+        torch.manual_seed(seed)
+        mac = ref_unet.UNet(3, 1, bilinear=True).train()
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            extra["logits_bf16_autocast"] = np32(mac(x).float())
     save(name, x=np32(x), t=np32(t), logits=np32(out), loss=np32(met["loss"]), iou=np.float64(met["iou"]),
          dice=np.float64(met["dice"]), nparams=np.int64(n), **init, **small, **norms, **bufs,
-         **fp64_noise(m, m64))
+         **fp64_noise(m, m64), **extra)
 
 
 def gen_unet():

@@ -335,6 +335,11 @@ def test_unet_matches_reference(name, seed, precision, tol):
     logits = m(T(fx["x"]))
     met = calculate_metrics(sigmoid(logits), T(fx["t"]), "bce_dice", {})
     met["loss"].backward()
+    if precision == "bf16" and "logits_bf16_autocast" in fx:
+        # no farther from the fp32 reference than 1.25x the reference's own bf16 autocast run
+        ac = rel(fx["logits_bf16_autocast"], fx["logits"])
+        print(f"{name} bf16 logits rel {rel(logits, fx['logits']):.4e} (reference autocast {ac:.4e})")
+        tol = max(tol, 1.25 * ac)
     assert rel(logits, fx["logits"]) < tol
     assert abs(met["loss"].item() - float(fx["loss"])) < tol * abs(float(fx["loss"]))
     if precision == "fp32":

@@ -1157,7 +1157,7 @@ def test_wgrad_dgrad1x1_one_launch(M, Cq, C):
     dx2 = torch.empty(M, C, device="cuda")
     ops.conv_gemm(torch.float32, [(g, 0, 0)], J, (1, M, 1), (M, 1), WT, Kj, C, [dx2], C)
     torch.cuda.synchronize()
-    assert rel(dx, g @ W) < 1e-5 and torch.equal(dx, dx2)
+    assert rel(dx, g @ W) < 1e-5 and rel(dx, dx2) < 1e-6   # (the one-launch kernel splits K over 8 waves)
     dw = g.t() @ x
     for k, (lo, hi) in enumerate(((0, Cq), (Cq, 2 * Cq), (2 * Cq, J))):
         assert rel(ws[k].view(hi - lo, C), dw[lo:hi]) < 1e-5 and torch.equal(ws[k], ws2[k])
@@ -1201,6 +1201,7 @@ def test_bwd_relu_bn_pair_equals_two_launches(dtype, M, C):
     """dfcsa_bwd_relu_bn_pair: two BatchNorm-backward statistics passes in one launch, bit-identical
     to two dfcsa_bwd_relu_bn launches."""
     from dfcsa._lib import LIB, call
+    from dfcsa.ops import P, stream
     torch.manual_seed(M + C)
     t = lambda: torch.randn(M, C, device="cuda").to(dtype)   # noqa: E731
     v = lambda: torch.randn(C, device="cuda")                 # noqa: E731
