@@ -351,11 +351,20 @@ def main():
                    (4, "conv1x1_stream (1x1 conv GEMMs with K <= 256 and the fused block GEMMs -- gate backward "
                        "in the dgrad epilogue, gate fusion / local-attention merge in the forward prologue; HBM-streaming)",
                     "conv1x1_stream", "hbm"))
+        # the side / branch streams are serialised for this pass: a class's launch durations are then
+        # its kernels' own (concurrent with the other streams' work, a launch's event-to-event time
+        # also counts the CUs it shares)
+        from dfcsa import streams as _streams
+        saved = (_streams.ENABLED[0], _streams.BRANCH_ENABLED[0])
+        _streams.ENABLED[0] = _streams.BRANCH_ENABLED[0] = False
         for c, _, _, _ in classes:
             L.LIB.dfcsa_prof_enable(c, 1)
-        for _ in range(args.steps):
-            step()
-        torch.cuda.synchronize()
+        try:
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+        finally:
+            _streams.ENABLED[0], _streams.BRANCH_ENABLED[0] = saved
         cls = {}
         for c, name, key, bound in classes:
             ms, n, fl = ctypes.c_double(), ctypes.c_int64(), ctypes.c_double()
@@ -378,6 +387,8 @@ def main():
         ach, peak, unit = rate(dom)
         traffic, tsrc = pmc_traffic(dom_key) if headline else (None, None)   # PMC passes cover the headline
         roof = {"bound": bound, "kernel": name, "achieved": round(ach, 2), "peak": peak, "unit": unit,
+                "timing": "HIP events around each launch of the class, the same K steps launched eagerly "
+                          "with the side and branch streams serialised",
                 "frac": round(ach / peak, 4), "traffic": traffic, "traffic_unit": "bytes/launch",
                 "traffic_source": tsrc,
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),

@@ -109,18 +109,18 @@ def traffic_all(fdb, wdb, out):
 GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
                          "small_conv_f32_kernel", "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel")),
           ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel",
-                          "wgrad_reduce", "small_wgrad_f32_kernel")),
+                          "wgrad_reduce", "small_wgrad_f32_kernel", "small_wgrad_dgrad_f32_kernel")),
           ("conv1x1_stream", ("conv1x1_stream_kernel",)),
           ("fused_block_gemm (1x1 GEMMs with the gate / BN prologues and epilogues)",
            ("dgrad_gate_kernel", "gate_fusion_fwd_kernel")),
           ("block_out_pool (block output + max-pool fwd/bwd)", ("block_out_pool_kernel",)),
-          ("ew_red (BN/gate/attention backward elementwise + partial sums)", ("ew_red_kernel",)),
+          ("ew_red (BN/gate/attention backward elementwise + partial sums)", ("ew_red_kernel", "ew_red_pair_kernel")),
           ("ew_fwd (BN apply, gate fusion, block output)", ("ew_fwd_kernel",)),
-          ("bn_and_slab_finalizers", ("rows_reduce_kernel", "bn_finalize_kernel", "bn_bwd_finalize_kernel",
+          ("bn_and_slab_finalizers", ("rows_reduce_kernel", "bn_finalize_kernel", "bn_bwd_finalize_kernel", "bn_bwd_finalize_pool",
                                       "slab_colsum", "sum_scalar_kernel", "colred")),
           ("lsa (pooled attention)", ("lsa_",)),
           ("maxpool", ("maxpool2",)),
-          ("optimizer", ("sumsq_kernel", "clip_sgd", "set_flag_kernel")),
+          ("optimizer", ("sumsq_kernel", "clip_sgd")),
           ("pack_plan", ("pack_plan_kernel",)),
           ("loss/head/input", ("bce_dice", "sigmoid", "head_", "pack_input")))
 
