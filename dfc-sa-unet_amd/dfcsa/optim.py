@@ -7,7 +7,7 @@ with torch's semantics (weight decay added to the gradient before momentum; firs
 initialises the buffer to the gradient -- the buffer starts at zero, so momentum * 0 + d is that
 first step exactly; p.grad holds the clipped gradient afterwards).
 
-``zero_after_step=True`` (bench.py, the Trainer) has the same pass write zeros to the gradients
+``zero_after_step=True`` (bench.py) has the same pass write zeros to the gradients
 instead of the clipped values, and the next ``zero_grad`` then skips its memset; the weights and
 momentum are the same either way.
 """

@@ -66,8 +66,6 @@ class Trainer:
         # the reference's train.py builds torch.optim.SGD(model.parameters(), ...): run it as the
         # fused device pass (same update; clip_grad_norm_ included)
         self.optimizer = FusedSGD.from_torch_sgd(optimizer) or optimizer
-        if isinstance(self.optimizer, FusedSGD):
-            self.optimizer.zero_after_step = True   # the loop never reads p.grad after a step
         self.train_loader = train_loader
         self.val_loader = val_loader
         self.loss_type = config["training"].get("loss", {}).get("type", "dice")
