@@ -1149,6 +1149,12 @@ struct SmallDgrad {
   const float* wt;
   float* dx;
   int kpad, N, nwx, nw, ndx;
+  // optional pool contraction (dfcsa_conv_wgrad_dgrad1x1_pool): wsum [M][2][N], rows [ndx][2][N]
+  const float* wsum;
+  const float* mean;
+  const float* invstd;
+  float* rows;
+  int H, W, P;
 };
 template <int NWV, int UNR>
 __global__ void __launch_bounds__(NWV * 64) small_wgrad_dgrad_f32_kernel(const WgradArgs a, const SmallDgrad d) {
@@ -1160,9 +1166,43 @@ __global__ void __launch_bounds__(NWV * 64) small_wgrad_dgrad_f32_kernel(const W
   }
   b -= d.nw;
   const int bx = b % d.ndx, by = b / d.ndx;
-  auto st = [&](int m, int n, float v) { d.dx[(size_t)m * d.N + n] = v; };
+  if (!d.rows) {
+    auto st = [&](int m, int n, float v) { d.dx[(size_t)m * d.N + n] = v; };
+    small_gemm_tile<false, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, d.wt, d.kpad, a.M, d.N, a.NI,
+                                                   bx * 16, by * 64, lds, st);
+    return;
+  }
+  // with the pool contraction: each stored dpooled value also enters its column's two sums over the
+  // tile's 16 rows (LDS [2][16][64], summed in row order below)
+  __shared__ float cs[2][16][64];
+  __shared__ float inv_area[16];
+  const int NP = d.P * d.P;
+  if (threadIdx.x < 16) {
+    const int n = (bx * 16 + threadIdx.x) % NP, pi = n / d.P, pj = n - pi * d.P;
+    inv_area[threadIdx.x] = 1.f / (float)((((pi + 1) * d.H + d.P - 1) / d.P - (pi * d.H) / d.P) *
+                                         (((pj + 1) * d.W + d.P - 1) / d.P - (pj * d.W) / d.P));
+  }
+  for (int e = threadIdx.x; e < 2 * 16 * 64; e += NWV * 64) (&cs[0][0][0])[e] = 0.f;
+  __syncthreads();
+  auto st = [&](int m, int n, float v) {
+    d.dx[(size_t)m * d.N + n] = v;
+    const int r = m - bx * 16, c = n - by * 64;
+    const float dd = v * inv_area[r];
+    const float R = d.wsum[((size_t)m * 2) * d.N + n], Y = d.wsum[((size_t)m * 2 + 1) * d.N + n];
+    cs[0][r][c] = dd * R;
+    cs[1][r][c] = dd * d.invstd[n] * (Y - d.mean[n] * R);
+  };
   small_gemm_tile<false, decltype(st), NWV, UNR>((const float*)a.g_ptr[0], a.NI, d.wt, d.kpad, a.M, d.N, a.NI,
                                                  bx * 16, by * 64, lds, st);
+  __syncthreads();
+  if (threadIdx.x < 128) {
+    const int k = threadIdx.x >> 6, c = threadIdx.x & 63, n = by * 64 + c;
+    if (n < d.N) {
+      float s = 0.f;
+      for (int r = 0; r < 16; ++r) s += cs[k][r][c];
+      d.rows[((size_t)bx * 2 + k) * d.N + n] = s;
+    }
+  }
 }
 
 template <int SUB>
@@ -1730,14 +1770,18 @@ extern "C" int dfcsa_wgrad_reduce(const float* slab, int splits, int NI, int NJ,
 
 // dfcsa_conv_wgrad(d) and dx = G * wt^T (a 1x1 conv's input gradient from the same G), one launch
 // when the small fp32 kernels apply to both, else the two calls one after the other
-extern "C" int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx,
-                                         void* stream) {
+extern "C" int dfcsa_conv_wgrad_dgrad1x1_pool(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx,
+                                              const dfcsa_pool_contract* pc, void* stream) {
   if (!d || !wt || !dx || N <= 0 || kpad < d->ng * d->Cg || kpad % 4) return DFCSA_EINVAL;
+  if (pc && (!pc->wsum || !pc->mean || !pc->invstd || !pc->rows || pc->P <= 0 || pc->H <= 0 || pc->W <= 0 ||
+             d->M % (pc->P * pc->P)))
+    return DFCSA_EINVAL;
   const int NI = d->ng * d->Cg;
   const bool small = d->dtype != DFCSA_DT_BF16 && d->M <= 4096 && d->ng == 1 && d->nseg == 1 && !d->seg_dh[0] &&
                      !d->seg_dw[0] && d->stride == 1 && d->ndst > 0 && d->Ho == d->Hi && d->Wo == d->Wi &&
                      !g_wgrad_noglds_f32small && NI % 4 == 0;
   if (!small) {
+    if (pc) return DFCSA_EINVAL;   // the contraction rows come from the small kernel only
     if (const int rc = dfcsa_conv_wgrad(d, stream)) return rc;
     dfcsa_conv_desc c;
     std::memset(&c, 0, sizeof(c));
@@ -1766,7 +1810,12 @@ extern "C" int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float*
   for (int i = 0; i < 3; ++i) a.dst[i] = i < d->ndst ? d->dst[i] : nullptr;
   if (want_bias) for (int i = 0; i < 3; ++i) a.bdst[i] = d->bias_dst[i];
   SmallDgrad s;
+  std::memset(&s, 0, sizeof(s));
   s.wt = wt; s.dx = dx; s.kpad = kpad; s.N = N;
+  if (pc) {
+    s.wsum = pc->wsum; s.mean = pc->mean; s.invstd = pc->invstd; s.rows = pc->rows;
+    s.H = pc->H; s.W = pc->W; s.P = pc->P;
+  }
   s.nwx = (NI + 15) / 16;
   s.nw = s.nwx * ((a.NJ + 63) / 64);
   s.ndx = (d->M + 15) / 16;
@@ -1777,4 +1826,9 @@ extern "C" int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float*
   else hipLaunchKernelGGL((small_wgrad_dgrad_f32_kernel<4, 2>), dim3(grid), dim3(256), 0, st, a, s);
   DFCSA_CHECK_LAUNCH();
   return 0;
+}
+
+extern "C" int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx,
+                                         void* stream) {
+  return dfcsa_conv_wgrad_dgrad1x1_pool(d, wt, kpad, N, dx, nullptr, stream);
 }

@@ -99,6 +99,11 @@ class ResampleDesc(ctypes.Structure):
                 ("row0", ctypes.c_int), ("pad", ctypes.c_int)]
 
 
+class PoolContract(ctypes.Structure):
+    _fields_ = [("wsum", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p),
+                ("rows", ctypes.c_void_p), ("H", ctypes.c_int), ("W", ctypes.c_int), ("P", ctypes.c_int)]
+
+
 class AugDesc(ctypes.Structure):
     _fields_ = [("img", ctypes.c_void_p), ("mask", ctypes.c_void_p), ("xtab", ctypes.c_void_p),
                 ("ytab", ctypes.c_void_p), ("m", ctypes.c_double * 6), ("fix", ctypes.c_int * 6),

@@ -413,9 +413,16 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         # BN2-backward sums on this stream, beside the attention backward on the branch; the
         # pool part is a [B][N][C] contraction with the forward pool's window sums, inside the
         # finalize (dfcsa_bn_bwd_finalize_pool)
-        with on_branch(dev, branch, dattn):
-            dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk)
-        part2 = torch.empty(nte * 2 * C, device=dev, dtype=f32)
+        # the pool part as extra partial rows written by the projection backward (B*P*P <= 4096: the
+        # one-launch small kernel), else by the finalize (dfcsa_bn_bwd_finalize_pool)
+        Np = Pp * Pp
+        rows_in_proj = B * Np <= 4096 and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
+        ncr = (B * Np + 15) // 16 if rows_in_proj else 0
+        part2 = torch.empty((nte + ncr) * 2 * C, device=dev, dtype=f32)
+        pool_rows = (wsum, bn2.mean, bn2.invstd, P(part2) + nte * 2 * C * 4, H, W) if rows_in_proj else None
+        with on_branch(dev, branch, dattn, part2, wsum):
+            dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
+                                        pool_rows=pool_rows)
         if fused_bn1:
             call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
                  P(bn2.invstd), None, *S(part2), stream())
@@ -425,8 +432,11 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
                  P(bn2.invstd), P(part2), P(dlocal), P(s.y1), P(bn1.scale), P(bn1.shift), P(bn1.mean),
                  P(bn1.invstd), P(local_part), part2.numel(), stream())
         with on_branch(dev, branch, part2, dattn, wsum):
-            coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias), dpooled,
-                                             wsum, B, H, W, Pp, bn2)
+            if rows_in_proj:
+                coef2 = ops.bn_bwd_finalize(part2, nte + ncr, 2, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias))
+            else:
+                coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias),
+                                                 dpooled, wsum, B, H, W, Pp, bn2)
             dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
                                          grad_of(conv2.bias))
             del dpooled, coef2
@@ -553,9 +563,11 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     return pooled, qkv, A, o, Wqkv
 
 
-def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
+def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
     """Backward of gamma * bilinear(o) (unet_dfc_sa_res.py:36-38) through the attention core;
-    accumulates gamma/q/k/v parameter gradients and returns d(pooled) [B][N][C] fp32."""
+    accumulates gamma/q/k/v parameter gradients and returns d(pooled) [B][N][C] fp32.
+    pool_rows = (wsum, mean, invstd, rows_ptr, H, W): the projection backward also writes the attention
+    entry's pool-backward BatchNorm rows (dfcsa_conv_wgrad_dgrad1x1_pool)."""
     pooled, qkv, A, o, Wqkv = saved
     B, H, W, C = dattn.shape
     dev = dattn.device
@@ -590,7 +602,8 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk):
         ops.conv_wgrad_dgrad1x1(f32, dqkv, J, pooled, C, BN, [grad_of(qw), grad_of(kw), grad_of(vw)], 1, Cq, C,
                                 pk["WT"], rup(J, ops.KALIGN), C, dpooled, layout=2,
                                 bias_grads=[grad_of(lsa.query_conv.bias), grad_of(lsa.key_conv.bias),
-                                            grad_of(lsa.value_conv.bias)])
+                                            grad_of(lsa.value_conv.bias)],
+                                pool=None if pool_rows is None else pool_rows + (Pp,))
     else:
         call("dfcsa_lsa_proj_bwd", B, N, C, Cq, P(dqkv), P(pooled), P(Wqkv),
              P(grad_of(qw)), P(grad_of(kw)), P(grad_of(vw)), P(grad_of(lsa.query_conv.bias)),

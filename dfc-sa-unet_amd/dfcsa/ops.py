@@ -166,10 +166,11 @@ def conv_wgrad_into(dtype, gs, Cg, segs, Cseg, grid, in_hw, grads, ntaps, Ctot, 
 
 
 def conv_wgrad_dgrad1x1(dtype, g, Cg, x, Cx, M, grads, ntaps, Ctot, Creal, wt, kpad, N, dx, layout=0,
-                        bias_grads=None):
+                        bias_grads=None, pool=None):
     """conv_wgrad_into over G = g [M][Cg], X = x [M][Cx] (1x1, one row grid of M pixels) and, in the
     same launch where the small fp32 kernels apply, dx [M][N] = g * wt^T (the 1x1 conv's input
-    gradient; wt [N][kpad] is its dfcsa_conv_gemm operand)."""
+    gradient; wt [N][kpad] is its dfcsa_conv_gemm operand).  pool = (wsum, mean, invstd, rows, H, W,
+    P): also the attention entry's pool-backward BatchNorm rows (dfcsa_conv_wgrad_dgrad1x1_pool)."""
     d, floats, NI, NJ = _wgrad_desc(dtype, [g], Cg, [(x, 0, 0)], Cx, (1, M, 1), (M, 1), 1, layout=layout)
     slab = torch.empty(floats, device=g.device, dtype=torch.float32) if d.splits > 1 else None
     d.slab = P(slab)
@@ -180,7 +181,14 @@ def conv_wgrad_dgrad1x1(dtype, g, Cg, x, Cx, M, grads, ntaps, Ctot, Creal, wt, k
     if bias_grads is not None:
         for i, t in enumerate(bias_grads):
             d.bias_dst[i] = P(t)
-    call("dfcsa_conv_wgrad_dgrad1x1", ctypes.addressof(d), P(wt), kpad, N, P(dx), stream())
+    if pool is None:
+        call("dfcsa_conv_wgrad_dgrad1x1", ctypes.addressof(d), P(wt), kpad, N, P(dx), stream())
+        return
+    wsum, mean, invstd, rows, H, W, P_ = pool
+    pc = _lib.PoolContract()
+    pc.wsum, pc.mean, pc.invstd, pc.rows = P(wsum), P(mean), P(invstd), rows
+    pc.H, pc.W, pc.P = H, W, P_
+    call("dfcsa_conv_wgrad_dgrad1x1_pool", ctypes.addressof(d), P(wt), kpad, N, P(dx), ctypes.addressof(pc), stream())
 
 
 # --------------------------------------------------------------------------- packing

@@ -134,6 +134,22 @@ int dfcsa_conv_wgrad(const dfcsa_wgrad_desc* d, void* stream);
  * (M <= 4096, 1x1, fp32, one split); otherwise the two calls in order.  The LightSelfAttention
  * projection backward (dW_q/k/v, db_q/k/v, dpooled) is one launch this way. */
 int dfcsa_conv_wgrad_dgrad1x1(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx, void* stream);
+/* dfcsa_conv_wgrad_dgrad1x1 for the LightSelfAttention backward of a DFC block, whose dx is dpooled
+ * [B][P*P][N]: the same launch also writes the attention entry's pool-backward BatchNorm sums as
+ * ceil(M/16) extra partial rows of [2][N] (rows[t][0][c] = sum over its 16 pooled positions of
+ * dpooled/area * R, rows[t][1][c] = the same of dpooled/area * invstd*(Y - mean*R); R, Y: the
+ * window sums of dfcsa_lsa_pooled_ws), so that dfcsa_bn_bwd_finalize over the dattn rows of
+ * dfcsa_bwd_relu_bn plus these rows gives the entry's coefficients.  Small fp32 path only (M <=
+ * 4096); DFCSA_EINVAL otherwise. */
+typedef struct {
+  const float* wsum;     /* [B][P*P][2][N] */
+  const float* mean;     /* [N] */
+  const float* invstd;   /* [N] */
+  float* rows;           /* ceil(M/16) x [2][N] */
+  int H, W, P;
+} dfcsa_pool_contract;
+int dfcsa_conv_wgrad_dgrad1x1_pool(const dfcsa_wgrad_desc* d, const float* wt, int kpad, int N, float* dx,
+                                   const dfcsa_pool_contract* pc, void* stream);
 /* grad += sum_s slab[s] (slab [splits][NI][NJ]) mapped to the reference weight layout.
  *  layout 0 (Conv2d): rows split over ndst tensors of NI/ndst rows; column j = tap*Ctot + cin
  *     -> dst[row][cin][tap] (Conv2d weight [Cout][Cin][kh][kw]); cin >= Creal skipped.

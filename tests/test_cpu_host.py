@@ -43,7 +43,8 @@ def test_descriptor_layouts_match_c(tmp_path):
               ("dfcsa_pack_entry", _lib.PackEntry, ("w0", "a")),
               ("dfcsa_wstd_entry", _lib.WstdEntry, ("K", "pad")),
               ("dfcsa_resample_desc", _lib.ResampleDesc, ("kk", "row0")),
-              ("dfcsa_aug_desc", _lib.AugDesc, ("m", "fix", "rotate", "mask_w"))]
+              ("dfcsa_aug_desc", _lib.AugDesc, ("m", "fix", "rotate", "mask_w")),
+              ("dfcsa_pool_contract", _lib.PoolContract, ("rows", "H", "P"))]
     exprs = []
     want = []
     for cname, py, names in fields:

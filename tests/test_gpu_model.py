@@ -264,10 +264,12 @@ def test_trainer_resume(tmp_path, reference_semantics):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
 @pytest.mark.parametrize("B,cin,C,H,W,P", [(2, 64, 64, 16, 16, 4), (2, 32, 64, 14, 14, 4), (3, 64, 128, 28, 20, 8),
-                                          (2, 128, 128, 13, 11, 4)])
+                                          (2, 128, 128, 13, 11, 4), (17, 64, 64, 16, 16, 16)])
 def test_block_entry_window_sums_equal_entry_pass(dtype, B, cin, C, H, W, P):
     """The attention entry's BN2-backward statistics from the forward pool's window sums
-    (dfcsa_lsa_pooled_ws + dfcsa_bn_bwd_finalize_pool, default) against the full-resolution entry
+    (dfcsa_lsa_pooled_ws; the pool part as partial rows of the projection backward,
+    dfcsa_conv_wgrad_dgrad1x1_pool, or -- B*P*P > 4096, the last case -- inside
+    dfcsa_bn_bwd_finalize_pool; default) against the full-resolution entry
     pass (dfcsa_bwd_attn_entry, DFCSA_ENTRY_WS=0): exact and adaptive (overlapping) windows; every
     parameter gradient and the input gradient agree to the summation-order rounding."""
     from dfcsa import block as dblock
