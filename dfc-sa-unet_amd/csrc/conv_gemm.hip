@@ -2684,6 +2684,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 32: return g_wgrad_coop_launches;
     case 33: return g_stream_min_m;
     case 34: return g_stream_shuf;
+    case 35: return g_lsa_cols_nt;
     default: return DFCSA_EINVAL;
   }
 }
@@ -2715,6 +2716,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 31) { g_wgrad_coop = value; return 0; }
   if (knob == 33) { g_stream_min_m = value; return 0; }
   if (knob == 34) { g_stream_shuf = value; return 0; }
+  if (knob == 35) { g_lsa_cols_nt = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

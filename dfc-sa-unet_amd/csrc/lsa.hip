@@ -15,6 +15,7 @@
 #include "dfcsa_internal.h"
 
 int g_lsa_rows_old = 0;
+int g_lsa_cols_nt = 1024;   // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
 
 namespace {
 
@@ -393,19 +394,22 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
 
 // grid (N, B): du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du.
 // Channels x NSL slices of the h range (all 256 threads busy at C = 64), combined in LDS.
-__global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
-                                                              const float* __restrict__ o, const float* gamma,
-                                                              float* __restrict__ dO, float* __restrict__ gpart,
-                                                              unsigned* cnt, float* gamma_grad) {
-  __shared__ float red[256 + 8];
-  __shared__ double rd[256];
+// NT = 1024 for C <= 128: four times the row slices per output (the 224^2 level's ~84 source rows
+// per pooled row were ~21 dependent loads per lane with 256 threads)
+template <int NT>
+__global__ void __launch_bounds__(NT) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
+                                                             const float* __restrict__ o, const float* gamma,
+                                                             float* __restrict__ dO, float* __restrict__ gpart,
+                                                             unsigned* cnt, float* gamma_grad) {
+  __shared__ float red[NT + 32];
+  __shared__ double rd[NT];
   __shared__ int flag;
   const int n = blockIdx.x, b = blockIdx.y, N = P * P;
   const int pi = n / P, pj = n - pi * P;
   const float gm = *gamma;
   const float bsc = (float)P / (float)H;   // bilinear source scale along H
-  const int nsl = C >= 256 ? 1 : 256 / C;
-  const int cw = nsl == 1 ? 256 : C;
+  const int nsl = C >= NT ? 1 : NT / C;
+  const int cw = nsl == 1 ? NT : C;
   const int sl = threadIdx.x / cw, cl = threadIdx.x - sl * cw;
   int lo, hi;
   contrib_range(pi, P, H, lo, hi);
@@ -445,7 +449,7 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
       dO[idx] = gm * s;
     }
   }
-  gsum = block_reduce_sum(gsum, red + 256);
+  gsum = block_reduce_sum(gsum, red + NT);
   if (!gamma_grad) {
     if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
     return;
@@ -455,10 +459,10 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_cols_kernel(int H, int C, int 
   if (!wg_last_of(cnt, gridDim.x * gridDim.y, &flag)) return;
   double v = 0.0;
   const int total = gridDim.x * gridDim.y;
-  for (int i = threadIdx.x; i < total; i += 256) v += (double)ld_sc1_f(gpart + i);
+  for (int i = threadIdx.x; i < total; i += NT) v += (double)ld_sc1_f(gpart + i);
   rd[threadIdx.x] = v;
   __syncthreads();
-  for (int k = 128; k > 0; k >>= 1) {
+  for (int k = NT / 2; k > 0; k >>= 1) {
     if (threadIdx.x < k) rd[threadIdx.x] += rd[threadIdx.x + k];
     __syncthreads();
   }
@@ -955,7 +959,11 @@ extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* ro
                                      void* stream) {
   unsigned* cnt = nullptr;
   if (gamma_grad && !(cnt = dfcsa_ticket_alloc(1))) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(lsa_up_bwd_cols_kernel, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, P, rows, o,
+if (C <= 128 && g_lsa_cols_nt > 256)
+    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<1024>, dim3(P * P, B), dim3(1024), 0, (hipStream_t)stream, H, C, P, rows, o,
+                     gamma, dO, gpart, cnt, gamma_grad);
+  else
+    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<256>, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, P, rows, o,
                      gamma, dO, gpart, cnt, gamma_grad);
   DFCSA_CHECK_LAUNCH();
   if (ngpart) *ngpart = B * P * P;
