@@ -15,7 +15,7 @@
 #include "dfcsa_internal.h"
 
 int g_lsa_rows_old = 0;
-int g_lsa_cols_nt = 1024;   // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
+int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
 
 namespace {
 

@@ -126,15 +126,15 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     # ---- attention entry / residual 1x1 conv, then the local branch 3x3 conv ----
     Cq = lsa.query_conv.out_channels
     fullres = getattr(lsa, "full_resolution", False)
-    y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-    res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
-    st2 = stats(N2)
-    nt2 = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
-                        [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
-    # the pooled attention chain (bn2 statistics -> pool -> q/k/v -> softmax core) runs on the
-    # branch stream beside the 3x3 conv (streams.on_branch)
+    # the attention entry / residual 1x1 conv and the pooled attention chain (bn2 statistics -> pool
+    # -> q/k/v -> softmax core) run on the branch stream beside the 3x3 conv (streams.on_branch)
     branch = not fullres and ops._SYNC_BN is None
-    with on_branch(dev, branch, y2, st2):
+    with on_branch(dev, branch, *xs):
+        y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+        res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
+        st2 = stats(N2)
+        nt2 = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
+                            [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
         bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
         if not fullres:
             Pp = pool_size
@@ -145,7 +145,7 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     nt1 = ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
                         bias=conv1.bias, stats=st1)   # (3x3 halo tiles: one statistics row per 2-D tile)
     bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt1 if training else nt, C, C, M, training)
-    join_branch(dev, branch, bn2, None if fullres else lsa_saved)
+    join_branch(dev, branch, bn2, None if fullres else lsa_saved, y2, res if has_res else None)
 
     if fullres:
         # ---- FullResolutionAttention (unet_dfc_sa_ablation_attention.py:42-47, :71-75) on the
@@ -239,15 +239,27 @@ def _build_block_packs(ps, blk, dtype, Cin_p, C, has_res):
     KpC = rup(C, ops.KALIGN)
     ps.transpose(W4p, 0, 0, C, 3 * C, "W4t", (3 * C, KpC))
     ps.transpose(W3p, 0, 0, C, 2 * C, "W3t", (2 * C, KpC))
-    wdx = (Cin_p, rup(11 * C, ops.KALIGN))
-    for tap in range(9):
-        ps.transpose(W1p, 0, tap * Cin_p, C, Cin_p, "Wdx", wdx, dc0=tap * C)
-    ps.transpose(W2p, 0, 0, C, Cin_p, "Wdx", wdx, dc0=9 * C)
-    if has_res:
-        ps.transpose(W2p, C, 0, C, Cin_p, "Wdx", wdx, dc0=10 * C)
-    else:  # identity residual: constant identity block (written once)
-        ps.buffer("Wdx", wdx, dtype)[:, 10 * C:11 * C].copy_(torch.eye(C, dtype=dtype, device=ps.device))
     att = blk.attn_branch[3]
+    if not getattr(att, "full_resolution", False) and SPLIT_DX[0]:
+        # the block-input gradient in two GEMMs (block_backward): WdxA = [W1p(tap)^T for 9 taps | Wres^T
+        # or I] before the attention chain's dy2 arrives, WdxB = W2p^T accumulated after it
+        wa, wb = (Cin_p, rup(10 * C, ops.KALIGN)), (Cin_p, rup(C, ops.KALIGN))
+        for tap in range(9):
+            ps.transpose(W1p, 0, tap * Cin_p, C, Cin_p, "WdxA", wa, dc0=tap * C)
+        if has_res:
+            ps.transpose(W2p, C, 0, C, Cin_p, "WdxA", wa, dc0=9 * C)
+        else:  # identity residual: constant identity block (written once)
+            ps.buffer("WdxA", wa, dtype)[:, 9 * C:10 * C].copy_(torch.eye(C, dtype=dtype, device=ps.device))
+        ps.transpose(W2p, 0, 0, C, Cin_p, "WdxB", wb)
+    else:
+        wdx = (Cin_p, rup(11 * C, ops.KALIGN))
+        for tap in range(9):
+            ps.transpose(W1p, 0, tap * Cin_p, C, Cin_p, "Wdx", wdx, dc0=tap * C)
+        ps.transpose(W2p, 0, 0, C, Cin_p, "Wdx", wdx, dc0=9 * C)
+        if has_res:
+            ps.transpose(W2p, C, 0, C, Cin_p, "Wdx", wdx, dc0=10 * C)
+        else:  # identity residual: constant identity block (written once)
+            ps.buffer("Wdx", wdx, dtype)[:, 10 * C:11 * C].copy_(torch.eye(C, dtype=dtype, device=ps.device))
     if getattr(att, "full_resolution", False):
         fra.build_packs(ps, att, dtype)
     else:
@@ -480,6 +492,31 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     coef = ops.bn_bwd_finalize(part, npart, 2, C, M, grad_of(bn1m.weight), grad_of(bn1m.bias))
     dy1 = ops.bn_bwd_apply_relu(dtype, dlocal, s.y1, bn1, bn1m.weight, coef, grad_of(conv1.bias))
     del dlocal
+    xs = s.xs
+    if "WdxA" in s.pk.t:
+        # ---- split input gradient: the 3x3 dgrad over dy1 (+ the residual's 1x1 / identity over dres)
+        #      and conv1's weight gradient start while the attention chain still runs on the branch
+        #      stream; dy2's 1x1 dgrad is accumulated after the join ----
+        with on_side(dev, dy1, *xs):
+            ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
+                                Cin_p, Cin_real)
+        dxs = None
+        if need_dx:
+            segs = [(dy1, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)] + [(dres, 0, 0)]
+            dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
+            ops.conv_gemm(dtype, segs, C, grid, hw, s.pk["WdxA"], rup(10 * C, ops.KALIGN), Cin_p, dxs, Cs)
+        join_branch(dev, branch, dy2)
+        if need_dx:
+            ops.conv_gemm(dtype, [(dy2, 0, 0)], C, grid, hw, s.pk["WdxB"], rup(C, ops.KALIGN), Cin_p, dxs, Cs,
+                          accumulate=True)
+        with on_side(dev, dy2, dres, *xs):
+            if has_res:
+                ops.conv_wgrad_into(dtype, [dy2, dres], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
+                                    [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
+            else:
+                ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
+                                    [grad_of(conv2.weight)], 1, Cin_p, Cin_real)
+        return dxs
     join_branch(dev, branch, dy2)
 
     # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM (critical path) ----
@@ -498,7 +535,6 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         dxs = input_grad()
 
     # ---- weight gradients of the input-side convs (side stream) ----
-    xs = s.xs
     with on_side(dev, dy1, dy2, dres, *xs):
         ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
                             Cin_p, Cin_real)
@@ -512,6 +548,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         dxs = input_grad()
     return dxs
 
+
+# the block-input gradient split around the attention chain's join (block_backward):
+# DFCSA_SPLIT_DX=0 restores the single 11-segment GEMM after the join
+SPLIT_DX = [os.environ.get("DFCSA_SPLIT_DX", "1") == "1"]
 
 # the attention-entry BN2-backward statistics from the forward pool's window sums (no full-resolution
 # pass after the attention backward); DFCSA_ENTRY_WS=0 restores the dfcsa_bwd_attn_entry pass

@@ -483,7 +483,13 @@ def test_pack_plan_matches_single_packs(dtype, cin, C):
     want = ops.pack_t3(dtype, cin, K(11 * C), [conv1.weight, conv2.weight,
                                                 blk.residual_conv.weight if has_res else None],
                        identity_last=not has_res)
-    assert torch.equal(ps["Wdx"], want)
+    if "Wdx" in ps.t:
+        assert torch.equal(ps["Wdx"], want)
+    else:   # the split block-input gradient operands: [W1 taps | Wres or I] and W2
+        wa, wb = ps["WdxA"], ps["WdxB"]
+        assert torch.equal(wa[:, :9 * C], want[:, :9 * C]) and torch.equal(wa[:, 9 * C:10 * C], want[:, 10 * C:11 * C])
+        assert not wa[:, 10 * C:].any()
+        assert torch.equal(wb[:, :C], want[:, 9 * C:10 * C]) and not wb[:, C:].any()
     lsa = blk.attn_branch[3]
     qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
     Cq = qw.shape[0]
