@@ -549,9 +549,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     return dxs
 
 
-# the block-input gradient split around the attention chain's join (block_backward):
-# DFCSA_SPLIT_DX=0 restores the single 11-segment GEMM after the join
-SPLIT_DX = [os.environ.get("DFCSA_SPLIT_DX", "1") == "1"]
+# the block-input gradient split around the attention chain's join (block_backward), opt-in with
+# DFCSA_SPLIT_DX=1: measured slower (same-box A/B 1531 vs 1566 img/s) -- the 3x3 dgrad GEMM issued
+# before the join takes the CUs the latency-bound attention chain needs, so the join comes later
+SPLIT_DX = [os.environ.get("DFCSA_SPLIT_DX", "0") == "1"]
 
 # the attention-entry BN2-backward statistics from the forward pool's window sums (no full-resolution
 # pass after the attention backward); DFCSA_ENTRY_WS=0 restores the dfcsa_bwd_attn_entry pass
