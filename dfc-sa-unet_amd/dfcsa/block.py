@@ -395,14 +395,19 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         dy3 = ops.bn_bwd_apply(dtype, dz3, s.y3, bn3, bn3m.weight, coef, grad_of(conv3.bias))
         del dz3
     if pair_wgrad:
-        with on_side(dev, dy4_keep, dy3, s.fused, s.local, s.attn):
-            ops.conv_wgrad_into(dtype, [dy4_keep, dy3], C, [(s.fused, 0, 0), (s.local, 0, 0), (s.attn, 0, 0)], C,
-                                grid, hw, [grad_of(conv4.weight), grad_of(conv3.weight)], 1, C, 3 * C, layout=3)
+        def gate_wgrads(dy4k=dy4_keep, dy3k=dy3, fused_=s.fused, local_=s.local, attn_=s.attn):
+            with on_side(dev, dy4k, dy3k, fused_, local_, attn_):
+                ops.conv_wgrad_into(dtype, [dy4k, dy3k], C, [(fused_, 0, 0), (local_, 0, 0), (attn_, 0, 0)], C,
+                                    grid, hw, [grad_of(conv4.weight), grad_of(conv3.weight)], 1, C, 3 * C, layout=3)
         del dy4_keep
     else:
-        with on_side(dev, dy3):
-            ops.conv_wgrad_into(dtype, [dy3], C, [(s.local, 0, 0), (s.attn, 0, 0)], C, grid, hw,
-                                [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
+        def gate_wgrads(dy3k=dy3, local_=s.local, attn_=s.attn):
+            with on_side(dev, dy3k):
+                ops.conv_wgrad_into(dtype, [dy3k], C, [(local_, 0, 0), (attn_, 0, 0)], C, grid, hw,
+                                    [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
+    if not WGRAD_LATE[0]:
+        gate_wgrads()
+        gate_wgrads = None
     if apro3:
         pass
     elif fused_bn1:
@@ -506,6 +511,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             dxs = [torch.empty((B, H, W, Cs), dtype=dtype, device=dev) for _ in range(nsrc)]
             ops.conv_gemm(dtype, segs, C, grid, hw, s.pk["WdxA"], rup(10 * C, ops.KALIGN), Cin_p, dxs, Cs)
         join_branch(dev, branch, dy2)
+        if gate_wgrads is not None:
+            gate_wgrads()
         if need_dx:
             ops.conv_gemm(dtype, [(dy2, 0, 0)], C, grid, hw, s.pk["WdxB"], rup(C, ops.KALIGN), Cin_p, dxs, Cs,
                           accumulate=True)
@@ -518,6 +525,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
                                     [grad_of(conv2.weight)], 1, Cin_p, Cin_real)
         return dxs
     join_branch(dev, branch, dy2)
+    if gate_wgrads is not None:
+        gate_wgrads()
 
     # ---- input gradient: 3x3 dgrad + both 1x1 dgrads in one implicit GEMM (critical path) ----
     # (order against the side-stream weight gradients: DX_FIRST)
@@ -553,6 +562,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
 # DFCSA_SPLIT_DX=1: measured slower (same-box A/B 1531 vs 1566 img/s) -- the 3x3 dgrad GEMM issued
 # before the join takes the CUs the latency-bound attention chain needs, so the join comes later
 SPLIT_DX = [os.environ.get("DFCSA_SPLIT_DX", "0") == "1"]
+
+# the gate / fusion convs' weight gradients issued on the side stream after the attention chain's
+# join instead of before it (DFCSA_WGRAD_LATE=1): keeps their GEMM off the CUs the chain needs
+WGRAD_LATE = [os.environ.get("DFCSA_WGRAD_LATE", "0") == "1"]
 
 # the attention-entry BN2-backward statistics from the forward pool's window sums (no full-resolution
 # pass after the attention backward); DFCSA_ENTRY_WS=0 restores the dfcsa_bwd_attn_entry pass
