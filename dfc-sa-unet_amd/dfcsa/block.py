@@ -563,9 +563,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
 # before the join takes the CUs the latency-bound attention chain needs, so the join comes later
 SPLIT_DX = [os.environ.get("DFCSA_SPLIT_DX", "0") == "1"]
 
-# the gate / fusion convs' weight gradients issued on the side stream after the attention chain's
-# join instead of before it (DFCSA_WGRAD_LATE=1): keeps their GEMM off the CUs the chain needs
-WGRAD_LATE = [os.environ.get("DFCSA_WGRAD_LATE", "0") == "1"]
+# the gate / fusion convs' weight gradients are issued on the side stream after the attention chain's
+# join, not before it: their GEMM then stays off the CUs the latency-bound chain needs (same-box A/B
+# 1594 vs 1565 img/s); DFCSA_WGRAD_LATE=0 restores the early issue
+WGRAD_LATE = [os.environ.get("DFCSA_WGRAD_LATE", "1") == "1"]
 
 # the attention-entry BN2-backward statistics from the forward pool's window sums (no full-resolution
 # pass after the attention backward); DFCSA_ENTRY_WS=0 restores the dfcsa_bwd_attn_entry pass
