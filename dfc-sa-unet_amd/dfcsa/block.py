@@ -126,15 +126,26 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     # ---- attention entry / residual 1x1 conv, then the local branch 3x3 conv ----
     Cq = lsa.query_conv.out_channels
     fullres = getattr(lsa, "full_resolution", False)
-    # the attention entry / residual 1x1 conv and the pooled attention chain (bn2 statistics -> pool
-    # -> q/k/v -> softmax core) run on the branch stream beside the 3x3 conv (streams.on_branch)
+    # the pooled attention chain (bn2 statistics -> pool -> q/k/v -> softmax core) runs on the branch
+    # stream beside the 3x3 conv (streams.on_branch); on maps of >= ENTRY_ON_BRANCH_HW pixels the
+    # attention entry / residual 1x1 conv runs there too (at small maps the chain's fixed launch
+    # latencies already outlast the 3x3 conv)
     branch = not fullres and ops._SYNC_BN is None
+    entry_on_branch = H * W >= ENTRY_ON_BRANCH_HW[0]
+
+    def entry_conv():
+        y2_ = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+        res_ = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
+        st2_ = stats(N2)
+        nt2_ = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
+                             [y2_, res_] if has_res else [y2_], C, bias=b2, stats=st2_)
+        return y2_, res_, st2_, nt2_
+
+    if not entry_on_branch:
+        y2, res, st2, nt2 = entry_conv()
     with on_branch(dev, branch, *xs):
-        y2 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
-        res = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
-        st2 = stats(N2)
-        nt2 = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
-                            [y2, res] if has_res else [y2], C, bias=b2, stats=st2)
+        if entry_on_branch:
+            y2, res, st2, nt2 = entry_conv()
         bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
         if not fullres:
             Pp = pool_size
@@ -557,6 +568,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         dxs = input_grad()
     return dxs
 
+
+# smallest H*W whose attention entry conv runs on the branch stream (block_forward);
+# DFCSA_ENTRY_ON_BRANCH_HW, 0 = every level
+ENTRY_ON_BRANCH_HW = [int(os.environ.get("DFCSA_ENTRY_ON_BRANCH_HW", "0"))]
 
 # the block-input gradient split around the attention chain's join (block_backward), opt-in with
 # DFCSA_SPLIT_DX=1: measured slower (same-box A/B 1531 vs 1566 img/s) -- the 3x3 dgrad GEMM issued
