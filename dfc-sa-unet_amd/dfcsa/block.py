@@ -24,9 +24,9 @@ import os
 import torch
 import torch.nn as nn
 
-from . import _lib, fra, ops
+from . import _lib, fra, ops, streams
 from ._lib import call
-from .ddp import notify_grads_ready
+from .ddp import ARMED, notify_grads_ready
 from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
 from .streams import join_branch, on_branch, on_side
@@ -534,6 +534,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             else:
                 ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
                                     [grad_of(conv2.weight)], 1, Cin_p, Cin_real)
+        streams.flush_deferred()
         return dxs
     join_branch(dev, branch, dy2)
     if gate_wgrads is not None:
@@ -555,19 +556,31 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         dxs = input_grad()
 
     # ---- weight gradients of the input-side convs (side stream) ----
-    with on_side(dev, dy1, dy2, dres, *xs):
-        ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
-                            Cin_p, Cin_real)
-        if has_res:
-            ops.conv_wgrad_into(dtype, [dy2, dres], C, [(x, 0, 0) for x in xs], Cs, grid, hw,
-                                [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
-        else:
-            ops.conv_wgrad_into(dtype, [dy2], C, [(x, 0, 0) for x in xs], Cs, grid, hw, [grad_of(conv2.weight)], 1,
+    def input_wgrads(dy1_=dy1, dy2_=dy2, dres_=dres, xs_=xs):
+        with on_side(dev, dy1_, dy2_, dres_, *xs_):
+            ops.conv_wgrad_into(dtype, [dy1_], C, _conv3x3_segments(xs_), Cs, grid, hw, [grad_of(conv1.weight)], 9,
                                 Cin_p, Cin_real)
+            if has_res:
+                ops.conv_wgrad_into(dtype, [dy2_, dres_], C, [(x, 0, 0) for x in xs_], Cs, grid, hw,
+                                    [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
+            else:
+                ops.conv_wgrad_into(dtype, [dy2_], C, [(x, 0, 0) for x in xs_], Cs, grid, hw,
+                                    [grad_of(conv2.weight)], 1, Cin_p, Cin_real)
+
+    defer = DEFER_WGRAD[0] and ARMED[0] == 0 and streams.ENABLED[0]
+    if not defer:
+        input_wgrads()
     if need_dx and not DX_FIRST[0]:
         dxs = input_grad()
+    streams.flush_deferred()     # the previous block's deferred weight gradients (DEFER_WGRAD)
+    if defer:
+        streams.defer(input_wgrads)
     return dxs
 
+
+# the input-side convs' weight gradients of a block issued one block later in the backward (after the
+# next block's input-gradient GEMM) instead of right after its own join: DFCSA_DEFER_WGRAD=1
+DEFER_WGRAD = [os.environ.get("DFCSA_DEFER_WGRAD", "0") == "1"]
 
 # smallest H*W whose attention entry conv runs on the branch stream (block_forward);
 # DFCSA_ENTRY_ON_BRANCH_HW, 0 = every level

@@ -29,6 +29,10 @@ import torch.distributed as dist
 
 from . import streams
 
+# armed bucket reducers (between start() and finish()): a bucket is all-reduced as soon as its
+# modules' backward has issued their gradient launches, so no gradient launch may be deferred then
+ARMED = [0]
+
 # ProcessGroupNCCL's watchdog thread polls the completion events of the eager collectives it
 # tracks about every 100 ms and drops completed ones.  A HIP-graph capture must not begin while it
 # still holds any (see capture_step): waiting this long after a device synchronisation lets it
@@ -86,6 +90,7 @@ class GradBucketReducer:
 
     def start(self):
         """Arm for one backward pass."""
+        ARMED[0] += 1
         self._pending = [len(b[2]) for b in self.buckets]
         self._works = []
         self._launched = [False] * len(self.buckets)
@@ -140,6 +145,8 @@ class GradBucketReducer:
             streams.join()
         for w in self._works:
             w.wait()
+        if self._pending is not None:
+            ARMED[0] -= 1
         self._pending = None
         if flag is None:
             return None

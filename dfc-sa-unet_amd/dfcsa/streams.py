@@ -42,7 +42,22 @@ def side_stream(device):
     return s
 
 
+# side-stream work deferred to a later point of the backward (block_backward, DFCSA_DEFER_WGRAD):
+# run by the next flush_deferred() and, at the latest, by the end-of-backward join
+_DEFERRED = []
+
+
+def defer(fn):
+    _DEFERRED.append(fn)
+
+
+def flush_deferred():
+    while _DEFERRED:
+        _DEFERRED.pop(0)()
+
+
 def _join():
+    flush_deferred()
     _JOIN_QUEUED[0] = False
     cur = torch.cuda.current_stream()
     for s in _SIDE.values():
