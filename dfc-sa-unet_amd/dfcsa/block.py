@@ -536,6 +536,13 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
                                     [grad_of(conv2.weight)], 1, Cin_p, Cin_real)
         streams.flush_deferred()
         return dxs
+    # the last block of the backward (no input gradient): the main stream has nothing left to do, so
+    # conv1's weight gradient (dy1 is final) starts before the join instead of after it (LAST_EARLY)
+    early1 = not need_dx and LAST_EARLY[0]
+    if early1:
+        with on_side(dev, dy1, *xs):
+            ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
+                                Cin_p, Cin_real)
     join_branch(dev, branch, dy2)
     if gate_wgrads is not None:
         gate_wgrads()
@@ -558,8 +565,9 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     # ---- weight gradients of the input-side convs (side stream) ----
     def input_wgrads(dy1_=dy1, dy2_=dy2, dres_=dres, xs_=xs):
         with on_side(dev, dy1_, dy2_, dres_, *xs_):
-            ops.conv_wgrad_into(dtype, [dy1_], C, _conv3x3_segments(xs_), Cs, grid, hw, [grad_of(conv1.weight)], 9,
-                                Cin_p, Cin_real)
+            if not early1:
+                ops.conv_wgrad_into(dtype, [dy1_], C, _conv3x3_segments(xs_), Cs, grid, hw,
+                                    [grad_of(conv1.weight)], 9, Cin_p, Cin_real)
             if has_res:
                 ops.conv_wgrad_into(dtype, [dy2_, dres_], C, [(x, 0, 0) for x in xs_], Cs, grid, hw,
                                     [grad_of(conv2.weight), grad_of(blk.residual_conv.weight)], 1, Cin_p, Cin_real)
@@ -577,6 +585,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         streams.defer(input_wgrads)
     return dxs
 
+
+# the backward's last block (no input gradient): conv1's weight gradient issued before the attention
+# chain's join (DFCSA_LAST_EARLY=1)
+LAST_EARLY = [os.environ.get("DFCSA_LAST_EARLY", "0") == "1"]
 
 # the input-side convs' weight gradients of a block issued one block later in the backward (after the
 # next block's input-gradient GEMM) instead of right after its own join: DFCSA_DEFER_WGRAD=1
