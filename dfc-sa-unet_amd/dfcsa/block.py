@@ -416,7 +416,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             with on_side(dev, dy3k):
                 ops.conv_wgrad_into(dtype, [dy3k], C, [(local_, 0, 0), (attn_, 0, 0)], C, grid, hw,
                                     [grad_of(conv3.weight)], 1, 2 * C, 2 * C)
-    if not WGRAD_LATE[0]:
+    if not WGRAD_LATE[0] or (not need_dx and LAST_EARLY[0] >= 2):
         gate_wgrads()
         gate_wgrads = None
     if apro3:
@@ -538,7 +538,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         return dxs
     # the last block of the backward (no input gradient): the main stream has nothing left to do, so
     # conv1's weight gradient (dy1 is final) starts before the join instead of after it (LAST_EARLY)
-    early1 = not need_dx and LAST_EARLY[0]
+    early1 = not need_dx and LAST_EARLY[0] >= 1
     if early1:
         with on_side(dev, dy1, *xs):
             ops.conv_wgrad_into(dtype, [dy1], C, _conv3x3_segments(xs), Cs, grid, hw, [grad_of(conv1.weight)], 9,
@@ -587,8 +587,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
 
 
 # the backward's last block (no input gradient): conv1's weight gradient issued before the attention
-# chain's join (DFCSA_LAST_EARLY=1)
-LAST_EARLY = [os.environ.get("DFCSA_LAST_EARLY", "0") == "1"]
+# chain's join (DFCSA_LAST_EARLY=1), and the gate / fusion weight gradients too (=2)
+LAST_EARLY = [int(os.environ.get("DFCSA_LAST_EARLY", "0"))]
 
 # the input-side convs' weight gradients of a block issued one block later in the backward (after the
 # next block's input-gradient GEMM) instead of right after its own join: DFCSA_DEFER_WGRAD=1
