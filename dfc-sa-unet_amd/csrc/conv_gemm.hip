@@ -1974,7 +1974,7 @@ struct FwdPro {
 template <int PRO, int C>
 __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
   using T = bf16_t;
-  static_assert(C == 64 || (C == 128 && PRO == PRO_GATE_FUSION), "prologue GEMM widths");
+  static_assert(C == 64 || C == 128, "prologue GEMM widths");
   constexpr int NSEG = PRO == PRO_GATE_FUSION ? 3 : 2;
   constexpr int SPS = C / 64;                       // 64-channel K stages per source
   constexpr int KS = NSEG * SPS, KG = 2 * KS;
@@ -2628,6 +2628,7 @@ extern "C" int dfcsa_fwd_pro_parts(int M, int C, int pro) {
   if (pro == 0 && C == 64) return fwd_pro_grid<PRO_GATE_FUSION, 64>(M);
   if (pro == 0 && C == 128) return fwd_pro_grid<PRO_GATE_FUSION, 128>(M);
   if (pro == 1 && C == 64) return fwd_pro_grid<PRO_LOCAL_ATTN, 64>(M);
+  if (pro == 1 && C == 128) return fwd_pro_grid<PRO_LOCAL_ATTN, 128>(M);
   return DFCSA_EINVAL;
 }
 
@@ -2655,7 +2656,7 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
                                          const float* b3, void* local, void* attn, void* y3, float* stats3, int64_t stats3_floats,
                                          void* stream) {
   const int64_t M = (int64_t)B * H * W;
-  if (M <= 0 || M >= (1ll << 31) || C != 64 || Kpad != 128 || P <= 0 || !y1 || !sc1 || !sh1 || !y2 || !sc2 ||
+  if (M <= 0 || M >= (1ll << 31) || (C != 64 && C != 128) || Kpad != 2 * C || P <= 0 || !y1 || !sc1 || !sh1 || !y2 || !sc2 ||
       !sh2 || !o || !gamma || !w3 || !local || !attn || !y3 || !stats3)
     return DFCSA_EINVAL;
   ConvGemmArgs a;
@@ -2670,7 +2671,8 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
   pro.dm_hw = make_divmod(H * W); pro.dm_w = make_divmod(W);
   pro.sh = (float)P / (float)H; pro.sw = (float)P / (float)W;
   pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
-  return launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream);
+  return C == 64 ? launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream)
+                 : launch_fwd_pro<PRO_LOCAL_ATTN, 128>(a, pro, stats3_floats, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

@@ -59,6 +59,8 @@ LSA_CORE_BWD = [os.environ.get("DFCSA_LSA_CORE_BWD", "0") == "1"]
 # 1526 img/s first against 1550 / 1540 / 1547 after -- the weight gradients started early overlap the
 # latency-bound stretches that follow better than they hurt the dgrad they start beside
 DX_FIRST = [os.environ.get("DFCSA_DX_FIRST", "0") == "1"]
+# block widths whose gate conv takes the local/attention prologue (DFCSA_LOCAL_ATTN_WIDTHS=64,128)
+LOCAL_ATTN_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_LOCAL_ATTN_WIDTHS", "64,128").split(",") if c)
 # block widths whose fusion conv takes the gate-fusion prologue (DFCSA_GATE_FUSION_WIDTHS=64,128)
 GATE_FUSION_WIDTHS = tuple(int(c) for c in os.environ.get("DFCSA_GATE_FUSION_WIDTHS", "64,128").split(",") if c)
 
@@ -177,7 +179,8 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     y3 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st3 = stats(C)
     nt3 = nt
-    if not fullres and dtype == torch.bfloat16 and C == 64 and Kp3 == 128 and training and FUSED_DGRAD_GATE[0]:
+    if not fullres and dtype == torch.bfloat16 and C in LOCAL_ATTN_WIDTHS and Kp3 == 2 * C and training and \
+            FUSED_DGRAD_GATE[0]:
         # the local/attention merge runs in the gate conv's A-operand prologue (one statistics row
         # per workgroup)
         nt3 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 1)

@@ -322,10 +322,10 @@ int dfcsa_fwd_pro_parts(int M, int C, int pro);
 int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
                           float* stats4, int64_t stats4_floats, void* stream);
-/* gate conv forward with the local/attention merge in its A-operand prologue (bf16, C == 64,
- * Kpad == 128, relu): local = relu(y1*sc1+sh1), attn = gamma*bilinear(o) + relu(y2*sc2+sh2)
- * (dfcsa_block_local_attn's arithmetic; o fp32 [B][P][P][64]), both stored; y3 = [local | attn] .
- * w3^T + b3 with BatchNorm partial statistics (one row per workgroup: dfcsa_fwd_pro_parts(M, 64, 1) rows).  Replaces the
+/* gate conv forward with the local/attention merge in its A-operand prologue (bf16, C == 64 or 128
+ * (round 4), Kpad == 2C, relu): local = relu(y1*sc1+sh1), attn = gamma*bilinear(o) + relu(y2*sc2+sh2)
+ * (dfcsa_block_local_attn's arithmetic; o fp32 [B][P][P][C]), both stored; y3 = [local | attn] .
+ * w3^T + b3 with BatchNorm partial statistics (one row per workgroup: dfcsa_fwd_pro_parts(M, C, 1) rows).  Replaces the
  * dfcsa_block_local_attn + dfcsa_conv_gemm pair (reference models/unet_dfc_sa_res.py:36-38, 97-102). */
 int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,

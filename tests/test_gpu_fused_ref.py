@@ -231,10 +231,11 @@ def test_gate_fusion_fwd_vs_torch(M, C):
         call("dfcsa_gate_fusion_fwd", *args, *short_by_one(st.t), stream())
 
 
-@pytest.mark.parametrize("B,H,W,Pp", [(3, 37, 29, 4), (4, 112, 112, 4), (2, 14, 9, 8)])
-def test_local_attn_gate_fwd_vs_torch(B, H, W, Pp):
-    torch.manual_seed(500 + H)
-    C, Kp = 64, 128
+@pytest.mark.parametrize("B,H,W,Pp,C", [(3, 37, 29, 4, 64), (4, 112, 112, 4, 64), (2, 14, 9, 8, 64),
+                                        (3, 37, 29, 4, 128), (4, 56, 56, 4, 128), (2, 14, 9, 8, 128)])
+def test_local_attn_gate_fwd_vs_torch(B, H, W, Pp, C):
+    torch.manual_seed(500 + H + C)
+    Kp = 2 * C
     M = B * H * W
     y1, y2 = rnd(M, C), rnd(M, C)
     sc1, sh1, sc2, sh2 = (torch.randn(C, device=dev) for _ in range(4))
