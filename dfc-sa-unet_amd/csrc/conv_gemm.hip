@@ -1930,7 +1930,12 @@ int gate_occ() {
 }
 
 // workgroups of one dfcsa_dgrad_gate / _acc_relu_bn launch (= partial rows): every CU's resident
-// slots, at most one per tile
+// slots, at most one per tile.  Knob 36: the C / 64 column blocks (grid.y) share the resident
+// slots (grid.x = slots / column blocks), so every workgroup is resident from the start and loads
+// its weight fragments once, instead of C / 64 successive grids of slot-many workgroups (0 = old).
+// Same-box A/B (tools/gpu_r04_gate36.sh): the C = 256 kernels 105 -> 88 and 68 -> 51 us, C = 128
+// acc 60 -> 54 us; step 1587 / 1597 / 1602 -> 1604 / 1607 / 1609 img/s.
+int g_gate_grid_div = 1;   // knob 36
 template <int EPI>
 int dgrad_gate_grid(int M, int C, bool apro = false) {
   const int kp = (C + 63) / 64 * 64;
@@ -1938,6 +1943,7 @@ int dgrad_gate_grid(int M, int C, bool apro = false) {
                   : kp == 192 ? gate_occ<192, EPI>() : gate_occ<256, EPI>();
   const int mtiles = (M + 63) / 64;
   int gx = 256 * occ;
+  if (g_gate_grid_div) gx = std::max(1, gx / ((C + 63) / 64));
   return gx > mtiles ? mtiles : gx;
 }
 
@@ -2687,6 +2693,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 33: return g_stream_min_m;
     case 34: return g_stream_shuf;
     case 35: return g_lsa_cols_nt;
+    case 36: return g_gate_grid_div;
     default: return DFCSA_EINVAL;
   }
 }
@@ -2719,6 +2726,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 33) { g_stream_min_m = value; return 0; }
   if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
+  if (knob == 36) { g_gate_grid_div = value; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -781,6 +781,12 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 27: 0 = 4-wave small fp32 GEMM tiles (LightSelfAttention projections).
  * knob 28: 1 = item-owner LightSelfAttention upsample-backward row kernel.
  * knob 30: 0 = no streaming kernel for shifted-segment (3x3, 9 * Cin <= 256) convs.
+ * knob 31: 1 = cooperative in-launch split-K weight-gradient reduction.
+ * knob 33: smallest M the 1x1 streaming GEMM takes (default 65536).
+ * knob 34: 0 = ConvTranspose2d forward GEMMs on the tile kernels instead of the streaming one.
+ * knob 35: threads of the LightSelfAttention upsample-backward column kernel at C <= 128.
+ * knob 36: 0 = one slot-sized grid per column block in the fused gate dgrad kernels (default 1:
+ *          the C / 64 column blocks share the resident slots, grid.x = slots / (C / 64)).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);
