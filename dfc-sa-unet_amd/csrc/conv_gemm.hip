@@ -1374,8 +1374,14 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
 // SHUF: ConvTranspose2d(k=2, s=2) store (CONV_STORE_SHUFFLE2): column n = (i*2 + j)*Nd + co of
 // input pixel (b, oh, ow) goes to output pixel (b, 2oh+i, 2ow+j), channel co -- 16-B chunks of 8
 // consecutive co stay contiguous, so the stores are the plain kernel's with a per-row base.
+// register budget for two waves per SIMD (two resident workgroups) on the wide-column variants,
+// whose default allocation (264-440 VGPR+AGPR) leaves one (not the accumulating 64 x 128 one: it
+// spills at 256)
+template <int NWC, int KP, bool ACC>
+constexpr int stream_wpe() { return NWC >= 48 && !(ACC && NWC * KP >= 64 * 128) ? 2 : 1; }
+
 template <int NWC, int KP, bool ACC, bool SH = false, bool SHUF = false>
-__global__ void __launch_bounds__(256)
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_wpe<NWC, KP, ACC>())))
 conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   static_assert(!(SHUF && (ACC || SH)), "shuffle store: plain, unshifted");
   using T = bf16_t;
@@ -1678,9 +1684,15 @@ __device__ __forceinline__ void bilin_axis_c(int dst, int in, float scale, int& 
 // of dfcsa_bwd_relu_bn, whose read of dlocal and y1 it replaces by one read of y1).
 enum { EPI_GATE = 0, EPI_ACC_RELU_BN = 1 };
 
+// waves per SIMD the compiler budgets registers for: 2 for the variants whose allocation lands just
+// above 256 VGPR+AGPR (one resident workgroup per CU otherwise): the 224^2 gate and acc/apply
+// variants (280 and 264) and the 112^2 gate variant (272)
+template <int KP, int EPI, bool APRO>
+constexpr int gate_wpe() { return (KP == 64 || (KP == 128 && EPI == 0)) ? 2 : 1; }
+
 template <int KP, int EPI, bool APRO = false>
-__global__ void __launch_bounds__(256) dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles,
-                                                         const ApplyPro ap) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gate_wpe<KP, EPI, APRO>())))
+dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const ApplyPro ap) {
   using T = bf16_t;
   static_assert(!APRO || KP == 64, "A prologue: C = 64");
   constexpr int NWC = EPI == EPI_GATE ? 48 : 32, FN = NWC / 16, NWG = 4 * NWC;
