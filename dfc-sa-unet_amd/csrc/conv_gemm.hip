@@ -1380,6 +1380,8 @@ int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
 template <int NWC, int KP, bool ACC>
 constexpr int stream_wpe() { return NWC >= 48 && !(ACC && NWC * KP >= 64 * 128) ? 2 : 1; }
 
+__device__ __forceinline__ int osw(int row) { return ((row >> 2) & 3) << 1; }
+
 template <int NWC, int KP, bool ACC, bool SH = false, bool SHUF = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(stream_wpe<NWC, KP, ACC>())))
 conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
@@ -1391,7 +1393,11 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
   constexpr int NWG = 4 * NWC;              // columns per workgroup
   constexpr int IMG = 64 * 128;             // bytes of one stage image
   constexpr int SLOT = KS * IMG;
-  constexpr int OSTR = NWG * 2 + 16;        // output staging row stride (bytes)
+  // output staging tile: unpadded rows (NWG * 2 bytes), 16-B chunk c of row r stored at chunk
+  // c ^ osw(r); the 1 KB the padding took lets the K = 256 variants keep two workgroups per CU
+  // (80 KiB each): the bf16 stores of rows r, r + 4, r + 8, r + 12 (one instruction) land in four
+  // different chunk pairs, the 16-B row reads stay whole rows
+  constexpr int OSTR = NWG * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
   // separate LDS object: the waitcnt pass then knows the output staging reads cannot alias the
   // in-flight LDS-DMA images (one shared array makes it drain vmcnt before every staging read)
@@ -1576,7 +1582,7 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
           const int row = i * 16 + (lane >> 4) * 4 + r;
-          *(T*)(otile + row * OSTR + col * 2) = f2bf(acc[i][j][r] + bias[j]);
+          *(T*)(otile + row * OSTR + (((col >> 3) ^ osw(row)) << 4) + (col & 7) * 2) = f2bf(acc[i][j][r] + bias[j]);
         }
     }
     lds_barrier();
@@ -1585,7 +1591,7 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
       const int e = tid + it * 256;
       const int row = o_row[it], cc = e - row * OCH;
       const int m = m0 + row;
-      uint4 v = *(const uint4*)(otile + row * OSTR + cc * 16);
+      uint4 v = *(const uint4*)(otile + row * OSTR + ((cc ^ osw(row)) << 4));
       const bool ok = m < M && o_base[it];
       size_t moff;
       if constexpr (SHUF) {   // input pixel m = (b, oh, ow) -> output pixel (b, 2oh, 2ow)
