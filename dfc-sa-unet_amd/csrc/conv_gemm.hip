@@ -2258,7 +2258,11 @@ int g_stream_shuf = 1;               // knob 34: ConvTranspose2d (shuffle-store)
 bool stream_applies(const ConvGemmArgs& a) {
   const bool shuf = a.mode == CONV_STORE_SHUFFLE2 && g_stream_shuf && !a.accumulate && a.Nd % 8 == 0 &&
                     a.ndest == 1 && a.Hout == 2 * a.Ho && a.Wout == 2 * a.Wo;
-  if ((a.mode != CONV_STORE_PLAIN && !shuf) || a.stride != 1 || a.Kpad > 256 || a.M < g_stream_min_m) return false;
+  // M >= knob 33, or half of it with N >= 512 (the 56^2 N = 512 GEMMs and ConvTranspose: 25 / 32 / 30 us
+  // against 28 / 35 / 38 us on the tile kernel since two K = 256 workgroups fit per CU,
+  // profiles/r04d_ab_stream_otile.txt; N = 256 and the 28^2 shapes stay on the tile kernel)
+  const bool big = a.M >= g_stream_min_m || (a.M >= g_stream_min_m / 2 && a.N >= 512);
+  if ((a.mode != CONV_STORE_PLAIN && !shuf) || a.stride != 1 || a.Kpad > 256 || !big) return false;
   if (shuf)
     for (int i = 0; i < a.nseg; ++i)
       if (a.seg[i].dh || a.seg[i].dw) return false;
