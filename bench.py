@@ -206,6 +206,12 @@ def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
 
 
 def main():
+    # stdout carries exactly ONE JSON line (rank 0).  RCCL prints its version banner to stdout when a
+    # communicator comes up, and other libraries may print too: keep a private handle on the real
+    # stdout for the JSON line and point fd 1 at stderr for everything else.
+    json_fd = os.dup(1)
+    sys.stdout.flush()
+    os.dup2(2, 1)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
@@ -255,9 +261,7 @@ def main():
            "training": {"learning_rate": 0.01, "momentum": 0.9, "weight_decay": 1e-4}}
     headline = args.model == "dfc"
     torch.manual_seed(0)
-    import contextlib
-    with contextlib.redirect_stdout(sys.stderr):   # the factory's messages: stdout carries ONE JSON line
-        model = ModelFactory.get_model(cfg).to(dev).train()
+    model = ModelFactory.get_model(cfg).to(dev).train()   # its messages go to stderr (fd 1 redirected)
     opt = FusedSGD(model.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4, zero_after_step=True)
 
     B, S = args.batch, args.img
@@ -337,6 +341,8 @@ def main():
         dist.all_reduce(te, op=dist.ReduceOp.MAX)
         el = te.item()
     final_loss = stats[0].item()
+    import dfcsa
+    dfcsa.check_wgrad_coop()   # knob 31 (opt-in) must not have produced a partially reduced tile
 
     # Dominant-kernel timing: the same K steps again, launched eagerly with the per-class HIP
     # event hook on (a graph replay cannot bracket individual kernels).
@@ -444,7 +450,7 @@ def main():
                           "model_tflops": round(value * gflop / 1e3, 2) if gflop else None},
                "roofline": roof, "step_roofline": step_roof, "trainer_faithful": faithful,
                "cpu_baseline": cpu, "val_dice": vdice}
-        print(json.dumps(out), flush=True)
+        os.write(json_fd, (json.dumps(out) + "\n").encode())
     # release the step graph (its RCCL kernels reference the communicator) before the process
     # group is destroyed; then every rank exits 0
     shutdown(graph)

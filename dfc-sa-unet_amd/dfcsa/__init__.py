@@ -21,6 +21,17 @@ def set_tuning(knob, value):
         raise ValueError(f"unknown tuning knob {knob}")
 
 
+def check_wgrad_coop():
+    """Fail loudly if the opt-in cooperative split-K weight-gradient reduction (knob 31) ever ran
+    out of its bounded wait.  That reduction assumes every workgroup of its grid is co-resident;
+    with the side and branch streams sharing the CUs a split can wait past the bound, and the tile
+    is then reduced from partial sums -- a wrong gradient whose only trace is this sticky device
+    flag.  No-op when the knob is off (the default), so it costs nothing on the shipped path."""
+    if _LIB.dfcsa_get_tuning(31) and _LIB.dfcsa_wgrad_coop_errors(0):
+        raise RuntimeError("cooperative split-K weight-gradient reduction (knob 31) exceeded its bounded "
+                           "wait: gradients of this run are wrong; leave knob 31 off with concurrent streams")
+
+
 for _kv in filter(None, os.environ.get("DFCSA_TUNE", "").split(",")):   # e.g. DFCSA_TUNE=2=1024
     _k, _v = _kv.split("=")
     set_tuning(_k, _v)

@@ -89,7 +89,9 @@ class GradBucketReducer:
         self.broadcast_buffers(src)
 
     def start(self):
-        """Arm for one backward pass."""
+        """Arm for one backward pass (re-arming an armed reducer first disarms it: the ARMED count
+        stays one per armed reducer whatever happened to the previous pass)."""
+        self._disarm()
         ARMED[0] += 1
         self._pending = [len(b[2]) for b in self.buckets]
         self._works = []
@@ -124,6 +126,19 @@ class GradBucketReducer:
         with torch.cuda.stream(side):
             return dist.all_reduce(self.flat.grad[lo:hi], op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
+    def _disarm(self):
+        """Idempotent: drop this reducer's ARMED count iff it is armed."""
+        if self._pending is not None:
+            ARMED[0] -= 1
+            self._pending = None
+
+    def abort(self):
+        """Forget an armed backward without reducing (an exception between start() and finish(), a
+        failed graph capture): the ARMED count returns, so deferred weight gradients are allowed
+        again, and no stale bucket state leaks into the next pass."""
+        self._disarm()
+        self._works = []
+
     def finish(self, loss=None):
         """Ensure every bucket has been reduced (launch stragglers), make the current stream wait.
         With ``loss``: returns a device scalar that is NaN iff some rank's loss is NaN (else 0),
@@ -141,13 +156,13 @@ class GradBucketReducer:
                 self._works.append(_host_allreduce(flag, dist.ReduceOp.MAX, self.group))
             else:
                 self._works.append(dist.all_reduce(flag, op=dist.ReduceOp.MAX, group=self.group, async_op=True))
-        if self.flat.grad.is_cuda:
-            streams.join()
-        for w in self._works:
-            w.wait()
-        if self._pending is not None:
-            ARMED[0] -= 1
-        self._pending = None
+        try:
+            if self.flat.grad.is_cuda:
+                streams.join()
+            for w in self._works:
+                w.wait()
+        finally:
+            self._disarm()
         if flag is None:
             return None
         return torch.where(flag > 0, torch.full_like(flag, float("nan")), torch.zeros_like(flag))
@@ -232,15 +247,19 @@ def shard_weight(n, rank, world):
 
 def capture_step(fn):
     """Capture one call of ``fn`` (a whole training step) as a HIP graph; returns (graph, fn's
-    result).  Two rules make the capture safe beside RCCL:
-      * thread_local capture mode: in the default global mode the HIP runtime refuses stream-unsafe
-        calls from EVERY thread while the capture is open, and ProcessGroupNCCL's watchdog thread
-        calls hipEventQuery on the eager collectives it tracks -- the refusal surfaces as an
-        exception in the watchdog, which terminates the process (SIGABRT, "Exception raised from
-        run at ProcessGroupNCCL.cpp");
-      * nothing tracked: the device is synchronised and the watchdog given WATCHDOG_DRAIN_S to drop
-        the completed eager works before the capture opens (collectives issued during a capture are
-        not handed to the watchdog)."""
+    result).
+
+    The fix for the round-3 abort is the capture mode: ``thread_local``.  In torch's default
+    global mode the HIP runtime refuses stream-unsafe calls from EVERY thread while a capture is
+    open, and ProcessGroupNCCL's watchdog thread calls hipEventQuery on the eager collectives it
+    tracks -- the refusal surfaced as an exception in the watchdog, which terminated the process
+    (SIGABRT, "Exception raised from run at ProcessGroupNCCL.cpp").  In thread-local mode only the
+    capturing thread is restricted, so the watchdog's polls are legal.
+
+    The device synchronisation and the WATCHDOG_DRAIN_S pause before the capture are a margin, not
+    the fix: they let the watchdog drop the completed warm-up collectives first, so nothing it
+    tracks is in flight while the capture is open (collectives issued during a capture are not
+    handed to the watchdog)."""
     torch.cuda.synchronize()
     if dist.is_available() and dist.is_initialized():
         time.sleep(WATCHDOG_DRAIN_S)

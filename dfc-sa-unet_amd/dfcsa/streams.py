@@ -51,6 +51,11 @@ def defer(fn):
     _DEFERRED.append(fn)
 
 
+def clear_deferred():
+    """Drop queued deferred launches without running them (after an aborted / failed capture)."""
+    _DEFERRED.clear()
+
+
 def flush_deferred():
     while _DEFERRED:
         _DEFERRED.pop(0)()

@@ -46,6 +46,8 @@ import time
 import torch
 import torch.distributed as dist
 
+import dfcsa
+from dfcsa import streams
 from dfcsa.ddp import GradBucketReducer, allreduce_stats, capture_step, shard_rows, shard_weight
 from dfcsa.loss import metrics_from_stats, sigmoid
 from dfcsa.optim import FusedSGD
@@ -206,8 +208,8 @@ class Trainer:
             if ps is not None:
                 ps.fresh = False
         if self.reducer is not None:
-            self.reducer._pending = None
-            self.reducer._works = []
+            self.reducer.abort()
+        streams.clear_deferred()   # closures of the half-recorded step must not run in a later backward
 
     def _eager_step(self, images, masks):
         self.optimizer.zero_grad()
@@ -219,9 +221,13 @@ class Trainer:
             # data parallel: buckets all-reduced as backward finalises them, NaN agreement over the
             # ranks, 1/world inside the fused clip + SGD, the metric vector summed over the ranks
             self.reducer.start()
-            # a ragged global batch: row-weighted mean over the replicas
-            loss.backward(self._root_grad(loss, self._weight))
-            skip = self.reducer.finish(loss)
+            try:
+                # a ragged global batch: row-weighted mean over the replicas
+                loss.backward(self._root_grad(loss, self._weight))
+                skip = self.reducer.finish(loss)
+            except BaseException:
+                self.reducer.abort()   # no leaked ARMED count / bucket state after a failed pass
+                raise
             self.optimizer.step(max_norm=self.max_norm, grad_scale=self.reducer.grad_scale, skip_if_nan=skip)
             return {"loss": loss, "stats": allreduce_stats(met["stats"], weight=self._weight)}
         loss.backward(self._root_grad(loss, 1.0))
@@ -295,6 +301,7 @@ class Trainer:
             if hasattr(bar, "set_postfix"):
                 bar.set_postfix({"loss": running_loss / (batch_idx + 1), "iou": running_iou / (batch_idx + 1),
                                  "dice": running_dice / (batch_idx + 1)})
+        dfcsa.check_wgrad_coop()
         n = len(self.train_loader)
         return running_loss / n, running_iou / n, running_dice / n
 

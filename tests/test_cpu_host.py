@@ -239,6 +239,28 @@ def test_ddp_bucket_plan():
     assert all(a[0] == b[1] for a, b in zip(spans, spans[1:]))  # contiguous, no gaps
     assert r.grad_scale == 0.5
 
+    # ARMED accounting: one count per armed reducer whatever happens between start()
+    # and finish() -- a failed pass (abort), a re-arm without finish, an exception inside finish()
+    from dfcsa import ddp as D
+    base = D.ARMED[0]
+    r.start()
+    assert D.ARMED[0] == base + 1
+    r.abort()
+    assert D.ARMED[0] == base and r._pending is None
+    r.abort()                                   # idempotent
+    assert D.ARMED[0] == base
+    r.start()
+    r.start()                                   # re-arming does not leak a count
+    assert D.ARMED[0] == base + 1
+
+    class Boom:
+        def wait(self):
+            raise RuntimeError("collective failed")
+    r._works = [Boom() for _ in r.buckets]
+    with pytest.raises(RuntimeError):
+        r.finish()
+    assert D.ARMED[0] == base and r._pending is None
+
 
 def _ddp_worker(rank, world, port, out_q):
     import torch.distributed as dist

@@ -142,8 +142,8 @@ def test_wgrad_fused_split_reduction(dtype, B, Cs, C, H, fuse_all):
                                                    (8, 64, 2, 64, 28, 28, 9), (4, 512, 1, 256, 14, 14, 9),
                                                    (4, 256, 3, 512, 14, 14, 1), (3, 64, 1, 72, 17, 13, 9)])
 def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
-    """Split-K weight gradients reduced INSIDE the launch (knob 31, default on when the grid fits the
-    chip): every split reduces one slice of its tile over all splits in split order.  bf16-exact
+    """Split-K weight gradients reduced INSIDE the launch (knob 31, opt-in -- the library default is
+    off -- and used only when the grid fits the chip): every split reduces one slice of its tile over all splits in split order.  bf16-exact
     operands against torch fp32 (1e-5: fp32 accumulation only), the separate slab reduction (knob 31 =
     0) to 1e-6, bitwise repeatable, accumulating into the gradient, no bounded wait ever exceeded.
     Shapes: the 224^2-like many-split 1x1 (hundreds of splits of one tile), multi-source 3x3, the deep
@@ -163,6 +163,7 @@ def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
             else [(t, 0, 0) for t in xh])
     LIB.dfcsa_wgrad_coop_errors(1)
     outs = {}
+    saved = LIB.dfcsa_get_tuning(31)   # restore the library's setting (default 0), not a fixed value
     try:
         for coop in (1, 0, 1):
             dfcsa.set_tuning(31, coop)
@@ -173,7 +174,7 @@ def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
             used = LIB.dfcsa_get_tuning(32) - before
             outs.setdefault(coop, []).append((gw, used))
     finally:
-        dfcsa.set_tuning(31, 1)
+        dfcsa.set_tuning(31, saved)
     assert LIB.dfcsa_wgrad_coop_errors(1) == 0
     (a, ua), (b, _) = outs[1]
     (c, uc), = outs[0]

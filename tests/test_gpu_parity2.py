@@ -213,16 +213,16 @@ def seeded_model(precision, pool, seed, fx):
     return m
 
 
-def _bf16_step(m, fx):
-    """One bf16 train step of model ``m`` on the fixture batch (every bf16 block fusion on); returns
-    (sd0, pre-clip grads, state after, x, t, logits, metrics)."""
+def _bf16_step(m, fx, xt=None):
+    """One bf16 train step of model ``m`` on the fixture batch (or ``xt`` = (x, t) on the host; every
+    bf16 block fusion on); returns (sd0, pre-clip grads, state after, x, t, logits, metrics)."""
     from dfcsa.loss import sigmoid
     from dfcsa.optim import FusedSGD
     from utils.metrics import calculate_metrics_device
     sd0 = {k: v.detach().clone() for k, v in m.state_dict().items()}
     m = m.cuda().train()
     opt = FusedSGD(m.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
-    x, t = T(fx["x"]), T(fx["t"])
+    x, t = (T(fx["x"]), T(fx["t"])) if xt is None else (xt[0].cuda(), xt[1].cuda())
     opt.zero_grad()
     logits = m(x)
     met = calculate_metrics_device(sigmoid(logits), t, "bce_dice", LP)
@@ -239,15 +239,19 @@ def _cos_rel(g, r):
     return (g @ r / (g.norm() * r.norm() + 1e-300)).item(), ((g - r).norm() / (r.norm() + 1e-30)).item()
 
 
-def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32):
+def _check_bf16_step_vs_autocast(tag, fb, pool, sd0, pre, sd, x, t, bufs_fp32, oracle=None):
     """The bar of test_cfg2_geometry_bf16_train_step_vs_reference_autocast (docstring there), against
-    the fp32 oracle re-run on this host at pool size ``pool``; ``fb`` holds the reference's autocast
+    the fp32 oracle re-run on this host at pool size ``pool`` (or its result ``oracle`` =
+    O.forward_backward(...) when the caller already ran it); ``fb`` holds the reference's autocast
     distances.  Prints every tensor's distances (worst first)."""
     from oracle import dfcsa_oracle as O
     SMALL = 4096
-    assert torch.equal(x.cpu(), torch.from_numpy(fb["x"])) and torch.equal(t.cpu(), torch.from_numpy(fb["t"]))
-    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
-    _, _, gref, _ = O.forward_backward(sd0, x.cpu(), t.cpu(), pool, LP)
+    if "x" in fb:
+        assert torch.equal(x.cpu(), torch.from_numpy(fb["x"])) and torch.equal(t.cpu(), torch.from_numpy(fb["t"]))
+    if oracle is None:
+        torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+        oracle = O.forward_backward(sd0, x.cpu(), t.cpu(), pool, LP)
+    _, _, gref, _ = oracle
     sd1, _, _, _ = O.clip_and_sgd(sd0, gref, {})
     rows, fails, scal = [], [], []
     sm = {"err": 0.0, "ac": 0.0, "uerr": 0.0, "uac": 0.0}
@@ -368,6 +372,49 @@ def test_cfg3_geometry_bf16_train_step_vs_reference_autocast():
                             fb["ac_logits_rel"], fb["t"])
     print(f"cfg3 bf16 logits rel {r:.4e} (bar {bar:.4e}; reference autocast {float(fb['ac_logits_rel']):.4e})")
     _check_bf16_step_vs_autocast("cfg3", fb, 8, sd0, pre, sd, x, t, fb)
+
+
+def test_timed_config_b16_bf16_train_step_vs_oracle_and_reference_autocast():
+    """The configuration bench.py times, end to end: 64..512, 224^2, P = 4, **B = 16**, bf16, every
+    default route.  At B = 16 the step takes routes no B = 2 test reaches -- M = 16 x H x W puts the
+    56^2 N >= 512 1x1 GEMMs and ConvTransposes on the mid-M streaming kernel (M >= 32768), and the
+    weight-gradient split plans and split-K choices are functions of M.  One step from a seeded init
+    (torch.manual_seed(16000), gammas 0.5; init checksums vs the reference's), on the batch
+    tests/golden/make_golden.py (12d) drew from seed 16001 (regenerated here, checked against the
+    fixture's checksums), against:
+      * the fp32 oracle run on this host's CPU (~12 s on 16 threads), itself pinned here to the
+        reference's fp32 step at B = 16 (image 0's logits 1e-4, logits checksums, loss);
+      * the bf16 bar of bf16_bar_check -- logits within max(1e-2, the reference's own CPU bf16
+        autocast error at B = 16, tests/golden/cfg2b16_bf16.npz), loss / IoU / Dice 1e-2, confident
+        pixels identical;
+      * the gradient / SGD-update / BatchNorm bar of test_cfg2_geometry_bf16_train_step_vs_reference_
+        autocast against the reference autocast's distances AT B = 16 (same fixture): weight tensors
+        per tensor, small tensors as one vector, whole gradient no worse than autocast.
+    Reference: utils/trainer.py:115-151, models/unet_dfc_sa_res.py:161-204, train.py:73-78."""
+    from oracle import dfcsa_oracle as O
+    fb = load("cfg2b16_bf16.npz")
+    B = int(fb["B"])
+    assert B == 16 and int(fb["pool"]) == 4
+    g = torch.Generator().manual_seed(int(fb["bseed"]))
+    x = torch.randn(B, 3, 224, 224, generator=g)
+    t = (torch.rand(B, 1, 224, 224, generator=g) > 0.5).float()
+    assert abs(x.double().sum().item() - float(fb["x_sum"])) <= 1e-9 * float(fb["x_sqsum"])
+    assert abs((x.double() ** 2).sum().item() - float(fb["x_sqsum"])) <= 1e-12 * float(fb["x_sqsum"])
+    assert t.double().sum().item() == float(fb["t_sum"])
+    m = seeded_model("bf16", 4, int(fb["seed"]), fb)
+    sd0, pre, sd, x, t, logits, met = _bf16_step(m, fb, (x, t))
+    torch.set_num_threads(max(1, min(16, len(os.sched_getaffinity(0)))))
+    orc = O.forward_backward(sd0, x.cpu(), t.cpu(), 4, LP)
+    lref, mref = orc[0], orc[1]
+    # the oracle against the reference's own fp32 step at B = 16
+    assert rel(lref[0], fb["logits0"]) < 1e-4, rel(lref[0], fb["logits0"])
+    assert abs(lref.double().norm().item() - float(fb["logits_norm"])) <= 1e-4 * float(fb["logits_norm"])
+    assert abs(float(mref["loss"]) - float(fb["loss"])) <= 1e-4 * abs(float(fb["loss"]))
+    r, bar = bf16_bar_check(logits, met["loss"].item(), met["stats"], lref.numpy(), fb["loss"], fb["iou"], fb["dice"],
+                            fb["ac_logits_rel"], None)
+    print(f"timed config B=16 bf16 logits rel {r:.4e} (bar {bar:.4e}; reference autocast "
+          f"{float(fb['ac_logits_rel']):.4e})")
+    _check_bf16_step_vs_autocast("b16", fb, 4, sd0, pre, sd, x, t, fb, oracle=orc)
 
 
 # ----------------------------------------------------------------------------- checkpoint interop

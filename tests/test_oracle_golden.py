@@ -385,3 +385,38 @@ def test_zoo_oracle_matches_reference(golden, name):
             continue
         ref = torch.from_numpy(ref)
         assert ((g - ref).norm() / (ref.norm() + 1e-12)).item() < 1e-4 or (g - ref).abs().max().item() < 1e-7, n
+
+
+def test_oracle_timed_config_b16_forward():
+    """The oracle at the configuration bench.py times (64..512, 224^2, P = 4, B = 16), against the
+    reference's own fp32 step of tests/golden/cfg2b16_bf16.npz (make_golden.py (12d)): the seeded init
+    (state-dict checksums), the regenerated batch (checksums), image 0's logits, the logits norm and
+    the loss.  Forward only (a few seconds on the CPU); the GPU test runs the full step."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(GOLDEN), "..", "dfc-sa-unet_amd"))
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    fx = dict(np.load(os.path.join(GOLDEN, "cfg2b16_bf16.npz")))
+    B = int(fx["B"])
+    torch.manual_seed(int(fx["seed"]))
+    m = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=4, ablation_on_qk_channels=8)
+    sd = {}
+    for k, v in m.state_dict().items():
+        v = v.detach().clone()
+        if k.endswith("gamma"):
+            v.fill_(0.5)
+        if v.is_floating_point():
+            ref = float(fx["init_sum." + k])
+            assert abs(v.double().sum().item() - ref) <= 1e-6 * max(1.0, abs(ref)), k
+        sd[k] = v
+    g = torch.Generator().manual_seed(int(fx["bseed"]))
+    x = torch.randn(B, 3, 224, 224, generator=g)
+    t = (torch.rand(B, 1, 224, 224, generator=g) > 0.5).float()
+    assert abs(x.double().sum().item() - float(fx["x_sum"])) <= 1e-9 * float(fx["x_sqsum"])
+    assert t.double().sum().item() == float(fx["t_sum"])
+    with torch.no_grad():
+        logits = O.unet_dfc_sa_res(x, sd, pool_size=4, training=True, bufs={})
+        met = O.calculate_metrics(torch.sigmoid(logits), t, "bce_dice", {"bce_weight": 0.5, "dice_weight": 0.5})
+    close(logits[0], fx["logits0"], rtol=1e-4, atol=1e-4)
+    assert abs(logits.double().norm().item() - float(fx["logits_norm"])) <= 1e-5 * float(fx["logits_norm"])
+    assert abs(float(met["loss"]) - float(fx["loss"])) <= 1e-5 * abs(float(fx["loss"]))
+    assert abs(float(met["dice"]) - float(fx["dice"])) <= 1e-5
