@@ -205,6 +205,44 @@ def val_dice_leg(cfg, dev, steps=600, batch=16, img=224, n_train=512, n_val=64):
             "seconds": round(time.perf_counter() - t0, 1)}
 
 
+# v_exp_f32 issue: 8 cycles per 64-lane wave-instruction on one SIMD (MI355X_MICROARCH.md, constants table
+# row 'vector-instruction ISSUE cost') -> 8 exp / clk / SIMD x 4 SIMDs x 256 CUs x 2.4 GHz
+EXP_PEAK_PER_S = 256 * 4 * 64 / 8 * 2.4e9
+
+
+def fra_exp_roofline(roof, fra_cls, args, B, L):
+    """Config 5's full-resolution attention is transcendental-bound (d_qk = C/8 = 8 at level 1: one
+    v_exp_f32 per score element against 144 MFMA flops), so its roofline is in exp/s, not MFMA flop/s.
+    Executed exps per step: forward N^2 per attention; backward recomputes P from the saved row
+    log-sum-exp twice (dK/dV pass and dQ pass), and the C > 256 levels once per 128-wide value chunk
+    and pass (dfcsa_fra_bwd_wide).  Attention blocks: 4 encoder + 4 decoder at img / 2^l, l = 0..3,
+    and the bottleneck at img / 16 (models/unet_dfc_sa_ablation_attention.py)."""
+    feats = [64, 128, 256, 512]
+    blocks = [(args.img >> l, feats[l], 2) for l in range(4)] + [(args.img >> 4, 1024, 1)]
+    fwd = bwd = 0.0
+    for hw, C, nb in blocks:
+        n2 = float(hw * hw) ** 2
+        path = L.LIB.dfcsa_fra_path(1 if args.precision == "bf16" else 0, C, C // 8, 2 * (C // 8) + C, 1)
+        fwd += nb * n2
+        bwd += nb * n2 * (2 * (C // 128) if path == 2 else 2)
+    name, ms, n, _, _, _ = fra_cls
+    sec = ms * 1e-3 / args.steps
+    executed = B * (fwd + bwd)
+    ach = executed / sec
+    return {"bound": "exp", "kernel": name, "achieved": round(ach / 1e12, 3), "peak": round(EXP_PEAK_PER_S / 1e12, 3),
+            "unit": "Texp/s", "frac": round(ach / EXP_PEAK_PER_S, 4),
+            "executed_exps_per_step": executed, "forward_exps_per_img": fwd,
+            "algorithmic_frac": round(B * fwd / sec / EXP_PEAK_PER_S, 4),
+            "note": "peak = v_exp_f32 issue rate (8 clk per wave-instruction per SIMD, 2.4 GHz, 256 CUs); achieved = "
+                    "every exp the kernels execute (forward N^2 + two backward recomputations of P) / the fra class's "
+                    "time; algorithmic_frac counts the forward N^2 only (the reference stores P instead of recomputing, "
+                    "which at 512^2 is 274.9 GB per image)",
+            "mfma_view": {k: roof[k] for k in ("achieved", "peak", "unit", "frac")},
+            "timing": roof["timing"], "launches_per_step": roof["launches_per_step"],
+            "avg_launch_ms": roof["avg_launch_ms"], "ms_per_step": roof["ms_per_step"],
+            "share_of_step": roof["share_of_step"], "traffic": None, "other_class": {}}
+
+
 def main():
     # stdout carries exactly ONE JSON line (rank 0).  RCCL prints its version banner to stdout when a
     # communicator comes up, and other libraries may print too: keep a private handle on the real
@@ -400,6 +438,8 @@ def main():
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "ms_per_step": round(ms / args.steps, 3), "share_of_step": round(ms / (el * 1e3), 3),
                 "other_class": {}}
+        if args.model == "fullres" and 3 in cls:
+            roof = fra_exp_roofline(roof, cls[3], args, B, L)
         for v in cls.values():
             if v is dom:
                 continue

@@ -822,21 +822,6 @@ constexpr int kRedScr = 1 << 20;           // hand-off doubles (8 MiB)
 __device__ unsigned g_red_cnt[kRedRing];
 __device__ double g_red_scr[kRedScr];
 
-__device__ __forceinline__ void st_sc1_d(double* p, double v) {
-  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-// three sc1 8-byte loads in flight, one wait
-__device__ __forceinline__ void ld_sc1_d3(const double* p0, const double* p1, const double* p2, double& v0,
-                                          double& v1, double& v2) {
-  asm volatile(
-      "global_load_dwordx2 %0, %3, off sc1\n\t"
-      "global_load_dwordx2 %1, %4, off sc1\n\t"
-      "global_load_dwordx2 %2, %5, off sc1\n\t"
-      "s_waitcnt vmcnt(0)"
-      : "=&v"(v0), "=&v"(v1), "=&v"(v2)
-      : "v"(p0), "v"(p1), "v"(p2)
-      : "memory");
-}
 // twelve sc1 8-byte loads in flight, one wait
 __device__ __forceinline__ void ld_sc1_d12(const double* const (&p)[12], double (&v)[12]) {
   asm volatile(

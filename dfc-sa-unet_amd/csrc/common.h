@@ -153,6 +153,37 @@ __device__ __forceinline__ float ld_sc1_f(const float* p) {
   asm volatile("global_load_dword %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
   return v;
 }
+__device__ __forceinline__ void st_sc1_d(double* p, double v) {
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+// three sc1 8-byte loads in flight, one wait
+__device__ __forceinline__ void ld_sc1_d3(const double* p0, const double* p1, const double* p2, double& v0,
+                                          double& v1, double& v2) {
+  asm volatile(
+      "global_load_dwordx2 %0, %3, off sc1\n\t"
+      "global_load_dwordx2 %1, %4, off sc1\n\t"
+      "global_load_dwordx2 %2, %5, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v0), "=&v"(v1), "=&v"(v2)
+      : "v"(p0), "v"(p1), "v"(p2)
+      : "memory");
+}
+// eight sc1 4-byte loads in flight, one wait (a last arriver's batched read of hand-off rows)
+__device__ __forceinline__ void ld_sc1_f8(const float* const (&p)[8], float (&v)[8]) {
+  asm volatile(
+      "global_load_dword %0, %8, off sc1\n\t"
+      "global_load_dword %1, %9, off sc1\n\t"
+      "global_load_dword %2, %10, off sc1\n\t"
+      "global_load_dword %3, %11, off sc1\n\t"
+      "global_load_dword %4, %12, off sc1\n\t"
+      "global_load_dword %5, %13, off sc1\n\t"
+      "global_load_dword %6, %14, off sc1\n\t"
+      "global_load_dword %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
 // true in the workgroup that arrives last of `n` sharing *cnt (which it re-zeroes for the next
 // launch); every thread calls it (contains barriers)
 __device__ __forceinline__ bool wg_last_of(unsigned* cnt, unsigned n, int* flag_smem) {

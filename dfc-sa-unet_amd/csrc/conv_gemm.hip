@@ -678,6 +678,8 @@ thread_local int64_t* t_dry_work = nullptr;   // dfcsa_conv_work_floats: the spl
 // Few tiles (< 150: the 14^2 bottleneck dgrad) with a long K (>= 64 stages) get ~600 workgroups of
 // >= 12 stages each.
 int g_splitk = 1;   // knob 25: 0 = never split
+int g_splitk_min_nk = 64;     // knob 37: fewest 64-deep K stages a split launch may have
+int g_splitk_target = 600;    // knob 38: workgroups a split launch aims for
 void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
   *ksplit = 1;
   *kper = a.Kpad / 64;
@@ -685,8 +687,8 @@ void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
   const int nk = a.Kpad / 64;
   // measured (profiles/r03b_splitk.jsonl): the 14^2 3x3 dgrad (100 tiles, 176 stages) 93 -> 63 us;
   // at 200 tiles / 72 stages (the 14^2 forward) the 64x64 tile stays faster (50 vs 57 us)
-  if (!g_splitk || tiles >= 150 || nk < 64) return;
-  int s = (600 + tiles - 1) / tiles;
+  if (!g_splitk || tiles >= 150 || nk < g_splitk_min_nk) return;
+  int s = (g_splitk_target + tiles - 1) / tiles;
   s = std::min(s, nk / 12);
   if (s < 2) return;
   int per = (nk + s - 1) / s;
@@ -2716,6 +2718,8 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 34: return g_stream_shuf;
     case 35: return g_lsa_cols_nt;
     case 36: return g_gate_grid_div;
+    case 37: return g_splitk_min_nk;
+    case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
 }
@@ -2749,6 +2753,8 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
   if (knob == 36) { g_gate_grid_div = value; return 0; }
+  if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 64; return 0; }
+  if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }
   if (knob == 18) { g_wgrad_wide_small = value; return 0; }

@@ -96,14 +96,32 @@ class GNState:
     __slots__ = ("mr", "scsh", "G", "S")
 
 
+# GroupNorm with the reductions finished inside the stats / backward-reduce launches (no separate
+# finalize launches; dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused, C <= 1024).  DFCSA_GN_FUSED=0
+# restores the four-launch path.
+GN_FUSED = [os.environ.get("DFCSA_GN_FUSED", "1") == "1"]
+
+
+def _gn_fused(C, G):
+    return GN_FUSED[0] and C <= 1024 and G <= 256 and C % G == 0
+
+
 def gn_forward(dtype, y, gn):
     B, H, W, C = y.shape
-    G, S = gn.num_groups, LIB.dfcsa_gn_nslices(H * W, C)
+    G = gn.num_groups
+    st = GNState()
+    st.mr, st.scsh = _f32((B * 2 * G,), y.device), _f32((B * 2 * C,), y.device)
+    if _gn_fused(C, G):
+        S = LIB.dfcsa_gn_nslices_fused(B, H * W, C)
+        rows = _f32((B * S * 2 * C,), y.device)
+        call("dfcsa_gn_stats_fused", dt(dtype), B, H * W, C, G, S, P(y), P(rows), P(gn.weight), P(gn.bias),
+             float(gn.eps), P(st.mr), P(st.scsh), stream())
+        st.G, st.S = G, S
+        return st
+    S = LIB.dfcsa_gn_nslices(H * W, C)
     part = _f32((B * S * 2 * C,), y.device)
     call("dfcsa_gn_stats", dt(dtype), B, H * W, C, S, P(y), P(part), stream())
-    st = GNState()
     st.G, st.S = G, S
-    st.mr, st.scsh = _f32((B * 2 * G,), y.device), _f32((B * 2 * C,), y.device)
     call("dfcsa_gn_finalize", B, H * W, C, G, S, P(part), P(gn.weight), P(gn.bias), float(gn.eps), P(st.mr),
          P(st.scsh), stream())
     return st
@@ -120,12 +138,19 @@ def gn_apply(dtype, y, st, act, res=None, st_res=None):
 def gn_backward(dtype, dout, mask, y, st, gn, dz_out=None):
     """dy for y -> GroupNorm(gn) given dL/d(out) where out = relu(...) is `mask` (None: no ReLU)."""
     B, H, W, C = y.shape
-    part = _f32((B * st.S * 2 * C,), y.device)
-    call("dfcsa_gn_bwd_reduce", dt(dtype), B, H * W, C, st.G, st.S, P(dout), P(mask), P(y), P(st.mr), P(part),
-         stream())
     coef = _f32((B * 2 * st.G,), y.device)
-    call("dfcsa_gn_bwd_finalize", B, H * W, C, st.G, st.S, P(part), P(gn.weight), P(coef), P(grad_of(gn.weight)),
-         P(grad_of(gn.bias)), stream())
+    if _gn_fused(C, st.G):
+        S = LIB.dfcsa_gn_nslices_fused(B, H * W, C)
+        rows = _f32((B * S * 2 * C + B * 4 * C,), y.device)   # hand-off rows + [B][2][C] doubles
+        call("dfcsa_gn_bwd_reduce_fused", dt(dtype), B, H * W, C, st.G, S, P(dout), P(mask), P(y), P(st.mr),
+             P(gn.weight), P(rows), P(rows) + B * S * 2 * C * 4, P(coef), P(grad_of(gn.weight)),
+             P(grad_of(gn.bias)), stream())
+    else:
+        part = _f32((B * st.S * 2 * C,), y.device)
+        call("dfcsa_gn_bwd_reduce", dt(dtype), B, H * W, C, st.G, st.S, P(dout), P(mask), P(y), P(st.mr), P(part),
+             stream())
+        call("dfcsa_gn_bwd_finalize", B, H * W, C, st.G, st.S, P(part), P(gn.weight), P(coef),
+             P(grad_of(gn.weight)), P(grad_of(gn.bias)), stream())
     dy = torch.empty_like(y)
     call("dfcsa_gn_bwd_apply", dt(dtype), B, H * W, C, st.G, P(dout), P(mask), P(y), P(st.mr), P(gn.weight), P(coef),
          P(dy), P(dz_out), stream())

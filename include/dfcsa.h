@@ -607,6 +607,18 @@ int dfcsa_gn_bwd_finalize(int B, int HW, int C, int G, int S, const float* parti
 int dfcsa_gn_bwd_apply(int dtype, int B, int HW, int C, int G, const void* dout, const void* mask, const void* y,
                        const float* mean_rstd, const float* gamma, const float* coef, void* dy, void* dz_out,
                        void* stream);
+/* GroupNorm with the reductions finished inside the launch (round 5; replaces stats + finalize and
+ * bwd_reduce + bwd_finalize, same outputs, C <= 1024, G <= 256): grid (S, B), S =
+ * dfcsa_gn_nslices_fused(B, HW, C); rows [B][S][2][C] floats of hand-off scratch; the last
+ * workgroup of each image finalises it.  bwd: work [B][2][C] doubles (the images' channel sums,
+ * summed in image order by the last image into dgamma / dbeta). */
+int dfcsa_gn_nslices_fused(int B, int HW, int C);
+int dfcsa_gn_stats_fused(int dtype, int B, int HW, int C, int G, int S, const void* y, float* rows,
+                         const float* gamma, const float* beta, float eps, float* mean_rstd, float* scale_shift,
+                         void* stream);
+int dfcsa_gn_bwd_reduce_fused(int dtype, int B, int HW, int C, int G, int S, const void* dout, const void* mask,
+                              const void* y, const float* mean_rstd, const float* gamma, float* rows, double* work,
+                              float* coef, float* dgamma, float* dbeta, void* stream);
 /* MaxPool2d(kernel 3, stride 2, padding 1) (:101): out [B][Ho][Wo][C], Ho = (H-1)/2 + 1; idx
  * uint8 [B][Ho][Wo][C] = tap (kh*3 + kw) of the first maximum; bwd writes every dx element. */
 int dfcsa_maxpool3s2_fwd(int dtype, int B, int H, int W, int C, const void* x, void* out, void* idx, void* stream);
@@ -787,6 +799,8 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 35: threads of the LightSelfAttention upsample-backward column kernel at C <= 128.
  * knob 36: 0 = one slot-sized grid per column block in the fused gate dgrad kernels (default 1:
  *          the C / 64 column blocks share the resident slots, grid.x = slots / (C / 64)).
+ * knob 37: fewest 64-deep K stages a split-K conv launch may have (default 64).
+ * knob 38: workgroups a split-K conv launch aims for (default 600).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -39,30 +39,48 @@ def lib():
 
 
 # ----------------------------------------------------------------------------- kernels
+@pytest.mark.parametrize("fused", [True, False])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
-@pytest.mark.parametrize("C,G,H,eps", [(64, 32, 14, 1e-6), (256, 32, 7, 1e-6), (64, 64, 9, 1e-5), (32, 32, 5, 1e-6)])
-def test_groupnorm_fwd_bwd(C, G, H, eps, dtype, tol):
-    """gn_stats/finalize/apply(+ReLU) and gn_bwd_* against F.group_norm + ReLU autograd."""
+@pytest.mark.parametrize("B,C,G,H,eps", [(3, 64, 32, 14, 1e-6), (3, 256, 32, 7, 1e-6), (3, 64, 64, 9, 1e-5),
+                                         (3, 32, 32, 5, 1e-6), (8, 1024, 32, 14, 1e-6), (8, 256, 32, 56, 1e-6),
+                                         (8, 64, 32, 112, 1e-6)])
+def test_groupnorm_fwd_bwd(B, C, G, H, eps, dtype, tol, fused):
+    """GroupNorm fwd (+ReLU) and bwd against F.group_norm + ReLU autograd: the fused launches
+    (dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused: the finalisation by each image's last
+    workgroup, dgamma / dbeta by the last image) and the four-launch path, at the test sizes and the
+    TransUNet bench's (B = 8: 14^2 x 1024, 56^2 x 256, 112^2 x 64); the fused path twice, bitwise."""
     from dfcsa import transunet_ops as TU
     torch.manual_seed(C + G + H)
     gn = torch.nn.GroupNorm(G, C, eps=eps).cuda()
     with torch.no_grad():
         gn.weight.uniform_(0.5, 1.5)
         gn.bias.uniform_(-0.5, 0.5)
-    x = (torch.randn(3, H, H + 1, C, device="cuda") * 2 + 0.3).to(dtype)
+    x = (torch.randn(B, H, H + 1, C, device="cuda") * 2 + 0.3).to(dtype)
     xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
     yr = F.relu(F.group_norm(xr, G, gn.weight, gn.bias, eps))
     g = torch.randn_like(yr)
     gw, gb = torch.autograd.grad(yr, [xr, gn.weight, gn.bias], g)[1:]
     dxr = torch.autograd.grad(F.relu(F.group_norm(xr, G, gn.weight, gn.bias, eps)), xr, g)[0]
-    st = TU.gn_forward(dtype, x.contiguous(), gn)
-    out = TU.gn_apply(dtype, x.contiguous(), st, 1)
+    saved = TU.GN_FUSED[0]
+    TU.GN_FUSED[0] = fused
+    try:
+        runs = []
+        for _ in range(2 if fused else 1):
+            st = TU.gn_forward(dtype, x.contiguous(), gn)
+            out = TU.gn_apply(dtype, x.contiguous(), st, 1)
+            gn.weight.grad = torch.zeros_like(gn.weight)
+            gn.bias.grad = torch.zeros_like(gn.bias)
+            dy = TU.gn_backward(dtype, g.permute(0, 2, 3, 1).contiguous().to(dtype), out, x.contiguous(), st, gn)
+            torch.cuda.synchronize()
+            runs.append((out.clone(), dy.clone(), gn.weight.grad.clone(), gn.bias.grad.clone()))
+    finally:
+        TU.GN_FUSED[0] = saved
+    out, dy, gwo, gbo = runs[0]
     assert rel(out.float().permute(0, 3, 1, 2), yr) < tol
-    gn.weight.grad = torch.zeros_like(gn.weight)
-    gn.bias.grad = torch.zeros_like(gn.bias)
-    dy = TU.gn_backward(dtype, g.permute(0, 2, 3, 1).contiguous().to(dtype), out, x.contiguous(), st, gn)
     assert rel(dy.float().permute(0, 3, 1, 2), dxr) < 5 * tol
-    assert rel(gn.weight.grad, gw) < 5 * tol and rel(gn.bias.grad, gb) < 5 * tol
+    assert rel(gwo, gw) < 5 * tol and rel(gbo, gb) < 5 * tol
+    if fused:
+        assert all(torch.equal(a, b) for a, b in zip(runs[0], runs[1])), "fused GroupNorm is not bitwise repeatable"
 
 
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
