@@ -1269,6 +1269,9 @@ static int red_mem(unsigned** ring, double** scr) {
   return acq;
 }
 
+// next free word of the hand-off scratch ring (shared by red_plan and dfcsa_scratch_alloc)
+static int64_t g_scr_next = 0;
+
 static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
   int R = (T + 127) / 128;
   if (R > 64) R = 64;
@@ -1299,12 +1302,11 @@ static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
     next += need;
   }
   if (R > 1) {
-    static int64_t snext = 0;
     const int64_t words = (int64_t)nblk * R * ns * 64;
     if (words > kRedScr) return DFCSA_EINVAL;
-    if (snext + words > kRedScr) snext = 0;
-    p->scr = scr + snext;
-    snext += words;
+    if (g_scr_next + words > kRedScr) g_scr_next = 0;
+    p->scr = scr + g_scr_next;
+    g_scr_next += words;
   }
   return 0;
 }
@@ -1313,6 +1315,16 @@ static int red_plan(int T, int nblk, int ns, int extra, RedPlan* p) {
 unsigned* dfcsa_ticket_alloc(int n) {
   RedPlan rp;
   return red_plan(1, 0, 0, n, &rp) ? nullptr : rp.cnt;
+}
+
+double* dfcsa_scratch_alloc(int64_t n) {
+  unsigned* ring = nullptr;
+  double* scr = nullptr;
+  if (n <= 0 || n > kRedScr || red_mem(&ring, &scr) < 0) return nullptr;
+  if (g_scr_next + n > kRedScr) g_scr_next = 0;
+  double* p = scr + g_scr_next;
+  g_scr_next += n;
+  return p;
 }
 
 extern "C" int dfcsa_ew_ntiles(int M, int C) { return (M + tile_px(C) - 1) / tile_px(C); }

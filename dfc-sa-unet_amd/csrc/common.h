@@ -168,6 +168,22 @@ __device__ __forceinline__ void ld_sc1_d3(const double* p0, const double* p1, co
       : "v"(p0), "v"(p1), "v"(p2)
       : "memory");
 }
+// eight sc1 8-byte loads in flight, one wait
+__device__ __forceinline__ void ld_sc1_d8(const double* const (&p)[8], double (&v)[8]) {
+  asm volatile(
+      "global_load_dwordx2 %0, %8, off sc1\n\t"
+      "global_load_dwordx2 %1, %9, off sc1\n\t"
+      "global_load_dwordx2 %2, %10, off sc1\n\t"
+      "global_load_dwordx2 %3, %11, off sc1\n\t"
+      "global_load_dwordx2 %4, %12, off sc1\n\t"
+      "global_load_dwordx2 %5, %13, off sc1\n\t"
+      "global_load_dwordx2 %6, %14, off sc1\n\t"
+      "global_load_dwordx2 %7, %15, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
+      : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
 // eight sc1 4-byte loads in flight, one wait (a last arriver's batched read of hand-off rows)
 __device__ __forceinline__ void ld_sc1_f8(const float* const (&p)[8], float (&v)[8]) {
   asm volatile(
@@ -182,6 +198,36 @@ __device__ __forceinline__ void ld_sc1_f8(const float* const (&p)[8], float (&v)
       "s_waitcnt vmcnt(0)"
       : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7])
       : "v"(p[0]), "v"(p[1]), "v"(p[2]), "v"(p[3]), "v"(p[4]), "v"(p[5]), "v"(p[6]), "v"(p[7])
+      : "memory");
+}
+typedef float f4v_t __attribute__((ext_vector_type(4)));
+// sixteen sc1 16-byte loads in flight, one wait: rows r = 0..7 of a [row][ld] float matrix at p,
+// 8 consecutive floats each (v[2r], v[2r + 1])
+__device__ __forceinline__ void ld_sc1_f4x16(const float* p, int ld, f4v_t (&v)[16]) {
+  const float* q[8];
+#pragma unroll
+  for (int r = 0; r < 8; ++r) q[r] = p + (size_t)r * ld;
+  asm volatile(
+      "global_load_dwordx4 %0, %16, off sc1\n\t"
+      "global_load_dwordx4 %1, %16, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %2, %17, off sc1\n\t"
+      "global_load_dwordx4 %3, %17, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %4, %18, off sc1\n\t"
+      "global_load_dwordx4 %5, %18, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %6, %19, off sc1\n\t"
+      "global_load_dwordx4 %7, %19, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %8, %20, off sc1\n\t"
+      "global_load_dwordx4 %9, %20, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %10, %21, off sc1\n\t"
+      "global_load_dwordx4 %11, %21, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %12, %22, off sc1\n\t"
+      "global_load_dwordx4 %13, %22, off offset:16 sc1\n\t"
+      "global_load_dwordx4 %14, %23, off sc1\n\t"
+      "global_load_dwordx4 %15, %23, off offset:16 sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3]), "=&v"(v[4]), "=&v"(v[5]), "=&v"(v[6]), "=&v"(v[7]),
+        "=&v"(v[8]), "=&v"(v[9]), "=&v"(v[10]), "=&v"(v[11]), "=&v"(v[12]), "=&v"(v[13]), "=&v"(v[14]), "=&v"(v[15])
+      : "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]), "v"(q[4]), "v"(q[5]), "v"(q[6]), "v"(q[7])
       : "memory");
 }
 // true in the workgroup that arrives last of `n` sharing *cnt (which it re-zeroes for the next

@@ -65,6 +65,110 @@ __device__ __forceinline__ void mma(f32x4_t& acc, const Frag<float>& a, const Fr
   for (int s = 0; s < 8; ++s) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.v[s], b.v[s], acc, 0, 0, 0);
 }
 
+// BatchNorm finalisation in a producer's tail (dfcsa_conv_gemm_bn).  Every workgroup has just written
+// (write-through) its statistics row `row` of [T][2][N] for the columns of its column block cb (the
+// launch's N tile, cw columns).  Level 1: the workgroups of row group g (GS consecutive rows) take
+// ticket (cb, g); the last one sums the group's rows per column in a fixed order (P = NT / cw parts of
+// rows p, p + P, ..., combined in part order; fp64) and hands the two sums over (write-through).
+// Level 2: the level-1 finishers take ticket cb; the last one sums the ng group sums in the same
+// fixed order and finalises the block's channels (< f.C) exactly as bn_finalize_kernel (training):
+// scale / shift / mean / invstd, running statistics with the unbiased variance, num_batches_tracked
+// (block 0).  Deterministic; no separate finalize launch.
+template <int NT, int CW>
+__device__ void bn_fold_tail(const BnFold& f, const float* stats, int N, int row, int T, int n0, char* smem) {
+  static_assert(CW <= NT, "fold: at most one column per thread");
+  constexpr int P = NT / CW;   // parts (threads past P * CW idle)
+  const int cb = n0 / CW;
+  if (n0 >= f.C) return;   // columns past the BatchNorm's channels (e.g. a fused residual conv)
+  double* red = (double*)smem;            // [2][NT]
+  int* flag = (int*)(red + 2 * NT);
+  __syncthreads();                        // smem is reused (the output tile staging is done)
+  const int g = row / f.GS, g0 = g * f.GS, g1 = min(T, g0 + f.GS);
+  if (!wg_last_of(f.cnt + cb * f.ng + g, (unsigned)(g1 - g0), flag)) return;
+  const int cl = threadIdx.x % CW, part = threadIdx.x / CW, c = n0 + cl;
+  const bool live = c < f.C && part < P;
+  double s0 = 0.0, s1 = 0.0;
+  if (live) {
+    int r = g0 + part;
+    for (; r + 3 * P < g1; r += 4 * P) {
+      const float* pp[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pp[2 * j] = stats + (size_t)(r + j * P) * 2 * N + c;
+        pp[2 * j + 1] = pp[2 * j] + N;
+      }
+      float v[8];
+      ld_sc1_f8(pp, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s0 += (double)v[2 * j]; s1 += (double)v[2 * j + 1]; }
+    }
+    for (; r < g1; r += P) {
+      s0 += (double)ld_sc1_f(stats + (size_t)r * 2 * N + c);
+      s1 += (double)ld_sc1_f(stats + (size_t)r * 2 * N + N + c);
+    }
+  }
+  red[threadIdx.x] = s0;
+  red[NT + threadIdx.x] = s1;
+  __syncthreads();
+  double* slot = f.scr + ((size_t)(cb * f.ng + g) * 2) * CW;
+  if (part == 0 && live) {
+    double a0 = 0.0, a1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) { a0 += red[q * CW + cl]; a1 += red[NT + q * CW + cl]; }
+    st_sc1_d(slot + cl, a0);
+    st_sc1_d(slot + CW + cl, a1);
+  }
+  if (!wg_last_of(f.cnt + f.ncb * f.ng + cb, (unsigned)f.ng, flag)) return;
+  s0 = s1 = 0.0;
+  if (live) {
+    const double* base = f.scr + (size_t)cb * f.ng * 2 * CW + cl;
+    int gg = part;
+    for (; gg + 3 * P < f.ng; gg += 4 * P) {
+      const double* pp[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        pp[2 * j] = base + (size_t)(gg + j * P) * 2 * CW;
+        pp[2 * j + 1] = pp[2 * j] + CW;
+      }
+      double v[8];
+      ld_sc1_d8(pp, v);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) { s0 += v[2 * j]; s1 += v[2 * j + 1]; }
+    }
+    for (; gg < f.ng; gg += P) {
+      double v0, v1, v2;
+      const double* q = base + (size_t)gg * 2 * CW;
+      ld_sc1_d3(q, q + CW, q, v0, v1, v2);
+      s0 += v0;
+      s1 += v1;
+    }
+  }
+  __syncthreads();
+  red[threadIdx.x] = s0;
+  red[NT + threadIdx.x] = s1;
+  __syncthreads();
+  if (part == 0 && live) {
+    double t0 = 0.0, t1 = 0.0;
+#pragma unroll
+    for (int q = 0; q < P; ++q) { t0 += red[q * CW + cl]; t1 += red[NT + q * CW + cl]; }
+    const double n = (double)f.count;
+    const double ma = t0 / n;
+    double v = t1 / n - ma * ma;
+    if (v < 0.0) v = 0.0;
+    const double b = f.bias ? (double)f.bias[c] : 0.0;
+    const float mu = (float)(ma + b), istd = (float)(1.0 / sqrt(v + (double)f.eps));
+    const double unb = f.count > 1 ? v * n / (n - 1.0) : v;
+    f.rmean[c] = (1.f - f.momentum) * f.rmean[c] + f.momentum * mu;
+    f.rvar[c] = (float)((1.0 - f.momentum) * (double)f.rvar[c] + f.momentum * unb);
+    const float sc = f.gamma[c] * istd;
+    f.scale[c] = sc;
+    f.shift[c] = f.beta[c] - mu * sc;
+    f.mean[c] = mu;
+    f.invstd[c] = istd;
+  }
+  if (cb == 0 && threadIdx.x == 0 && f.nbt) *f.nbt += 1;
+}
+
 // Shared epilogue: BN partial statistics of the fp32 accumulator, bias, conversion, LDS-staged
 // coalesced 16-byte stores (plain / 3-way column split / ConvTranspose pixel shuffle), optional
 // accumulate into the destination.  smem must hold max(2*WM*BN floats, BM*(BN*sizeof(T)+16)) B.
@@ -127,8 +231,13 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t 
             if ((w * WTM) / 64 == st) { sm += red[(w * 2) * BN + c]; q += red[(w * 2 + 1) * BN + c]; }
         }
       }
-      args.stats[(size_t)m_tile * 2 * N + n] = sm;
-      args.stats[(size_t)m_tile * 2 * N + N + n] = q;
+      if (args.fold.on) {   // the fold's last workgroups read these rows (write-through)
+        st_sc1_dw(args.stats + (size_t)m_tile * 2 * N + n, sm);
+        st_sc1_dw(args.stats + (size_t)m_tile * 2 * N + N + n, q);
+      } else {
+        args.stats[(size_t)m_tile * 2 * N + n] = sm;
+        args.stats[(size_t)m_tile * 2 * N + N + n] = q;
+      }
     }
     __syncthreads();
   }
@@ -186,6 +295,8 @@ __device__ __forceinline__ void conv_epilogue(const ConvGemmArgs& args, f32x4_t 
     }
     store8<T>(dst, v);
   }
+  static_assert(BN <= NT, "the BatchNorm fold gives each column of the tile a thread");
+  if (args.fold.on && args.stats) bn_fold_tail<NT, BN>(args.fold, args.stats, N, m_tile, (M + BM - 1) / BM, n0, smem);
 }
 
 template <typename T, int BM, int BN, int WM, int WN>
@@ -330,6 +441,9 @@ __device__ __attribute__((aligned(16))) uint4 g_zero_page[64];
 // dfcsa_conv_stats_rows: the launch functions report the statistics rows of the kernel they would
 // launch instead of launching (one row per M tile / per persistent workgroup)
 thread_local int* t_dry_rows = nullptr;
+// dry run (desc_args): the column-block width of the picked kernel when its epilogue can fold the
+// BatchNorm finalisation (conv_epilogue kernels), 0 otherwise
+thread_local int* t_dry_bn = nullptr;
 __device__ __attribute__((aligned(16))) float g_store_sink[4 * 64];   // write-only target of masked stores
 
 typedef __attribute__((address_space(3))) void lds_void;
@@ -665,7 +779,7 @@ conv_gemm_glds32_kernel(const ConvGemmArgs args) {
 
 template <int BM, int BN, int WM, int WN, int NST>
 int launch_glds32(const ConvGemmArgs& a, hipStream_t st) {
-  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; if (t_dry_bn) *t_dry_bn = BN; return 0; }
   dim3 grid(xcd_pad(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM)));
   hipLaunchKernelGGL((conv_gemm_glds32_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -678,7 +792,7 @@ thread_local int64_t* t_dry_work = nullptr;   // dfcsa_conv_work_floats: the spl
 // Few tiles (< 150: the 14^2 bottleneck dgrad) with a long K (>= 64 stages) get ~600 workgroups of
 // >= 12 stages each.
 int g_splitk = 1;   // knob 25: 0 = never split
-int g_splitk_min_nk = 64;     // knob 37: fewest 64-deep K stages a split launch may have
+int g_splitk_min_nk = 24;     // knob 37: fewest 64-deep K stages a split launch may have (ViT GEMMs, tools/vit_gemm_bench.py)
 int g_splitk_target = 600;    // knob 38: workgroups a split launch aims for
 void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
   *ksplit = 1;
@@ -700,7 +814,7 @@ void splitk_plan(const ConvGemmArgs& a, int* ksplit, int* kper) {
 int launch_splitk(ConvGemmArgs a, int ksplit, int kper, hipStream_t st) {
   const int tiles = ((a.N + 127) / 128) * ((a.M + 127) / 128);
   const int64_t need = (int64_t)tiles * ksplit * 128 * 128;
-  if (t_dry_rows) { *t_dry_rows = (a.M + 127) / 128; if (t_dry_work) *t_dry_work = need; return 0; }
+  if (t_dry_rows) { *t_dry_rows = (a.M + 127) / 128; if (t_dry_work) *t_dry_work = need; if (t_dry_bn) *t_dry_bn = 128; return 0; }
   if (!a.kwork || a.kwork_floats < need) return DFCSA_EINVAL;
   a.ksplit = ksplit;
   a.kper = kper;
@@ -714,7 +828,7 @@ int launch_splitk(ConvGemmArgs a, int ksplit, int kper, hipStream_t st) {
 
 template <int BM, int BN, int WM, int WN, int NST = 2>
 int launch_glds(const ConvGemmArgs& a, hipStream_t st) {
-  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; if (t_dry_bn) *t_dry_bn = BN; return 0; }
   dim3 grid(xcd_pad(((a.N + BN - 1) / BN) * ((a.M + BM - 1) / BM)));
   hipLaunchKernelGGL((conv_gemm_glds_kernel<BM, BN, WM, WN, NST>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -939,7 +1053,7 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
 
 template <int DEPTH, bool RF, bool BAL>
 int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
-  if (t_dry_rows) { *t_dry_rows = (a.M + 255) / 256; return 0; }
+  if (t_dry_rows) { *t_dry_rows = (a.M + 255) / 256; if (t_dry_bn) *t_dry_bn = 256; return 0; }
   dim3 grid(xcd_pad((a.N / 256) * ((a.M + 255) / 256)));
   hipLaunchKernelGGL((conv_gemm_pp_kernel<DEPTH, RF, BAL>), grid, dim3(512), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -1354,7 +1468,7 @@ bool small_conv_applies(const ConvGemmArgs& a) {
 
 template <typename T, int BM, int BN, int WM, int WN>
 int launch_cfg(const ConvGemmArgs& a, hipStream_t st) {
-  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; return 0; }
+  if (t_dry_rows) { *t_dry_rows = (a.M + BM - 1) / BM; if (t_dry_bn) *t_dry_bn = BN; return 0; }
   dim3 grid((a.N + BN - 1) / BN, (a.M + BM - 1) / BM);
   hipLaunchKernelGGL((conv_gemm_kernel<T, BM, BN, WM, WN>), grid, dim3(WM * WN * 64), 0, st, a);
   DFCSA_CHECK_LAUNCH();
@@ -1625,9 +1739,15 @@ conv1x1_stream_kernel(const ConvGemmArgs args, int mtiles) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
       const int n = n0 + wave * NWC + j * 16 + (lane & 15);
-      if (lane < 32 && n < N)
-        args.stats[(size_t)blockIdx.x * 2 * N + (lane < 16 ? 0 : N) + n] = lane < 16 ? st_s[j] : st_q[j];
+      if (lane < 32 && n < N) {
+        float* p = args.stats + (size_t)blockIdx.x * 2 * N + (lane < 16 ? 0 : N) + n;
+        if (args.fold.on) st_sc1_dw(p, lane < 16 ? st_s[j] : st_q[j]);   // read by the fold's last workgroups
+        else *p = lane < 16 ? st_s[j] : st_q[j];
+      }
     }
+    // BatchNorm finalisation in the launch's tail: one statistics row per workgroup (blockIdx.x) of
+    // column block blockIdx.y
+    if (args.fold.on) bn_fold_tail<256, NWG>(args.fold, args.stats, N, blockIdx.x, gridDim.x, n0, smem);
   }
 }
 
@@ -2234,7 +2354,7 @@ int launch_stream(const ConvGemmArgs& a, hipStream_t st) {
   const int per_cu = g_stream_wgs > 0 ? g_stream_wgs : occ;
   int gx = (256 * per_cu + ny - 1) / ny;
   if (gx > mtiles) gx = mtiles;
-  if (t_dry_rows) { *t_dry_rows = gx; return 0; }   // one statistics row per workgroup column
+  if (t_dry_rows) { *t_dry_rows = gx; if (t_dry_bn) *t_dry_bn = 4 * NWC; return 0; }   // one statistics row per workgroup column
   if (g_debug) fprintf(stderr, "[dfcsa] stream1x1 NWC=%d KP=%d occ=%d grid=%dx%d tiles=%d\n", NWC, KP, occ, gx, ny, mtiles);
   bool shifted = false;
   for (int i = 0; i < a.nseg; ++i) shifted = shifted || a.seg[i].dh || a.seg[i].dw;
@@ -2423,6 +2543,7 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
 }  // namespace
 
 namespace {
+thread_local int t_fold_cw = 0;   // desc_args: the fold block width of the picked kernel (0: no fold)
 // descriptor -> kernel arguments (validated); the statistics row count of the launch in *rows
 int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   if (!d || d->nseg < 1 || d->nseg > DFCSA_MAX_SEG || d->M <= 0 || d->N <= 0) return DFCSA_EINVAL;
@@ -2449,12 +2570,15 @@ int desc_args(const dfcsa_conv_desc* d, ConvGemmArgs& a, int* rows) {
   a.kwork = d->work;
   a.kwork_floats = d->work ? d->work_floats : 0;
   // statistics rows of the kernel launch_t picks (a dry run of the selection)
-  int r = 0;
+  int r = 0, bw = 0;
   t_dry_rows = &r;
+  t_dry_bn = &bw;
   if (d->dtype == DFCSA_DT_BF16) launch_t<bf16_t>(a, nullptr);
   else launch_t<float>(a, nullptr);
   t_dry_rows = nullptr;
+  t_dry_bn = nullptr;
   *rows = r;
+  t_fold_cw = bw;
   return 0;
 }
 }  // namespace
@@ -2476,13 +2600,57 @@ extern "C" int dfcsa_conv_stats_rows(const dfcsa_conv_desc* d) {
   return rc ? rc : rows;
 }
 
+static int conv_launch(const dfcsa_conv_desc* d, const ConvGemmArgs& a, hipStream_t st);
+
 extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
   ConvGemmArgs a;
   int rows = 0;
   if (const int rc = desc_args(d, a, &rows)) return rc;
   // statistics slab: [rows][2][N]
   if (d->stats && (int64_t)rows * 2 * d->N > d->stats_floats) return DFCSA_EINVAL;
+  return conv_launch(d, a, (hipStream_t)stream);
+}
+
+int g_bn_fold = 1;   // knob 39: 0 = never fold the BatchNorm finalisation into the conv epilogue
+
+extern "C" int dfcsa_conv_gemm_bn(const dfcsa_conv_desc* d, const dfcsa_bn_fold* f, void* stream) {
+  if (!d || !f || !d->stats || f->C <= 0 || f->C > d->N || f->count <= 0 || !f->gamma || !f->beta ||
+      !f->running_mean || !f->running_var || !f->scale || !f->shift || !f->mean || !f->invstd)
+    return DFCSA_EINVAL;
+  ConvGemmArgs a;
+  int rows = 0;
+  if (const int rc = desc_args(d, a, &rows)) return rc;
+  if ((int64_t)rows * 2 * d->N > d->stats_floats) return DFCSA_EINVAL;
+  const int cw = t_fold_cw;
   hipStream_t st = (hipStream_t)stream;
+  if (g_bn_fold && cw > 0 && rows > 0) {
+    BnFold& b = a.fold;
+    b.C = f->C;
+    b.cw = cw;
+    b.GS = 1;
+    while ((int64_t)b.GS * b.GS < rows) ++b.GS;          // ~sqrt(T) rows per group, ~sqrt(T) groups
+    b.ng = (rows + b.GS - 1) / b.GS;
+    b.ncb = (f->C + cw - 1) / cw;
+    b.cnt = dfcsa_ticket_alloc(b.ncb * b.ng + b.ncb);
+    b.scr = dfcsa_scratch_alloc((int64_t)b.ncb * b.ng * 2 * cw);
+    if (b.cnt && b.scr) {
+      b.on = 1;
+      b.count = f->count; b.bias = f->conv_bias; b.gamma = f->gamma; b.beta = f->beta;
+      b.rmean = f->running_mean; b.rvar = f->running_var; b.nbt = f->num_batches_tracked;
+      b.momentum = f->momentum; b.eps = f->eps;
+      b.scale = f->scale; b.shift = f->shift; b.mean = f->mean; b.invstd = f->invstd;
+      return conv_launch(d, a, st);
+    }
+    std::memset(&b, 0, sizeof(b));
+  }
+  // the picked kernel cannot fold (streaming / halo-tile kernels): conv, then the finalize launch
+  if (const int rc = conv_launch(d, a, st)) return rc;
+  return dfcsa_bn_finalize(d->stats, rows, f->C, d->N, f->count, f->conv_bias, f->gamma, f->beta, f->running_mean,
+                           f->running_var, f->num_batches_tracked, f->momentum, f->eps, 1, f->scale, f->shift,
+                           f->mean, f->invstd, stream);
+}
+
+static int conv_launch(const dfcsa_conv_desc* d, const ConvGemmArgs& a, hipStream_t st) {
   // profiling classes: the 1x1 streaming GEMMs are HBM-bound (their unit is bytes: A and the
   // weight panel read once, the output written once, read too when accumulating); the tile
   // kernels are MFMA-bound (2*M*N*K flop)
@@ -2719,6 +2887,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 35: return g_lsa_cols_nt;
     case 36: return g_gate_grid_div;
     case 37: return g_splitk_min_nk;
+    case 39: return g_bn_fold;
     case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
@@ -2753,7 +2922,8 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
   if (knob == 36) { g_gate_grid_div = value; return 0; }
-  if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 64; return 0; }
+  if (knob == 39) { g_bn_fold = value; return 0; }
+  if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 24; return 0; }
   if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
   if (knob == 17) { g_wgrad_big = value; return 0; }

@@ -9,6 +9,27 @@ struct ConvSeg {
   int dh, dw;
 };
 
+// BatchNorm finalisation folded into a conv epilogue (dfcsa_conv_gemm_bn): the launch's statistics
+// rows are reduced by its own last workgroups (two ticket levels) and finalised as dfcsa_bn_finalize
+// (training) does.  on == 0: no fold.
+struct BnFold {
+  int on, C, GS, ng, ncb, cw;   // channels finalised, rows per group, groups, column blocks, block width
+  unsigned* cnt;                // ncb * ng level-1 tickets, then ncb level-2 tickets (zero, re-zeroed)
+  double* scr;                  // [ncb][ng][2][cw] group sums (write-through hand-off)
+  int count;
+  const float* bias;
+  const float* gamma;
+  const float* beta;
+  float* rmean;
+  float* rvar;
+  int64_t* nbt;
+  float momentum, eps;
+  float* scale;
+  float* shift;
+  float* mean;
+  float* invstd;
+};
+
 struct ConvGemmArgs {
   int M, N, K, Kpad, Cseg, nseg;
   ConvSeg seg[DFCSA_MAX_SEG];
@@ -27,6 +48,7 @@ struct ConvGemmArgs {
   float* kwork;
   int64_t kwork_floats;
   int ksplit, kper;
+  BnFold fold;
 };
 
 struct WgradArgs {
@@ -88,6 +110,8 @@ extern int g_lsa_cols_nt;  // knob 35: 256 = the 256-thread LightSelfAttention u
 extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)
 unsigned* dfcsa_ticket_alloc(int n);
+// n doubles of last-arriver hand-off scratch (ring in block_ew.hip; nullptr on failure)
+double* dfcsa_scratch_alloc(int64_t n);
 extern int g_fra_generic;
 extern int g_fra_occ;
 extern int g_ew_tile_elems;

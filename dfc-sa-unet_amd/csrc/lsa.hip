@@ -795,7 +795,6 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
 // image (ticket) forms dk = dE^T q and dv = A^T dO for the image's tokens from the published rows;
 // the last of all adds dgamma (partials in token order).  Replaces lsa_up_bwd_cols +
 // lsa_attn_bwd_rows + lsa_attn_bwd_cols (three dependent launches on the backward's critical path).
-typedef float f4v_t __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ float4 ld_sc1_f4(const float* p) {
   f4v_t v;
   asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");

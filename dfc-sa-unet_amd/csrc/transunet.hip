@@ -1583,6 +1583,67 @@ __global__ void __launch_bounds__(256) colsum_partial_kernel(int64_t M, int C, c
   st8f(partial + (size_t)blockIdx.y * C + c0, acc);
 }
 
+// Column sums of x [M][C] added into d0 [0, n0), d1 [n0, n0 + n1), d2 [n0 + n1, C), one launch:
+// the colsum_partial rows are published with write-through (sc1) stores, and the last-arriving
+// workgroup of each 2048-column block sums the block's T rows in row order (eight sc1 loads in
+// flight per column) and adds them -- the result of colsum_partial + slab_colsum3 without the
+// second launch (the Linear bias gradients of the ViT, 49 per TransUNet step).
+template <typename T>
+__global__ void __launch_bounds__(256) colsum_fused_kernel(int64_t M, int C, const T* __restrict__ x, float* partial,
+                                                           unsigned* cnt, int n0, int n1, float* d0, float* d1,
+                                                           float* d2) {
+  __shared__ int flag;
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  const int T_ = gridDim.y;
+  if (c0 < C) {
+    const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+    float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    int64_t r = r0;
+    for (; r + 7 < r1; r += 8) {
+      float v[8][8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) load8<T>(x + (r + u) * C + c0, v[u]);
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) acc[q] += v[u][q];
+    }
+    for (; r < r1; ++r) {
+      float v[8];
+      load8<T>(x + r * C + c0, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += v[q];
+    }
+    float* row = partial + (size_t)blockIdx.y * C + c0;
+#pragma unroll
+    for (int q = 0; q < 8; ++q) st_sc1_dw(row + q, acc[q]);
+  }
+  if (!wg_last_of(cnt + blockIdx.x, T_, &flag)) return;
+  // each thread sums its own 8-column chunk over the T rows in row order: two 16-B sc1 loads per
+  // row, eight rows (16 loads) in flight
+  if (c0 >= C) return;
+  float s[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  int t = 0;
+  for (; t + 7 < T_; t += 8) {
+    f4v_t v[16];
+    ld_sc1_f4x16(partial + (size_t)t * C + c0, C, v);
+#pragma unroll
+    for (int u = 0; u < 8; ++u)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) { s[q] += v[2 * u][q]; s[4 + q] += v[2 * u + 1][q]; }
+  }
+  for (; t < T_; ++t)
+#pragma unroll
+    for (int q = 0; q < 8; ++q) s[q] += ld_sc1_f(partial + (size_t)t * C + c0 + q);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const int c = c0 + q;
+    if (c < n0) d0[c] += s[q];
+    else if (c < n0 + n1) d1[c - n0] += s[q];
+    else d2[c - n0 - n1] += s[q];
+  }
+}
+
 // ------------------------------------------------------------ head-major relayout (bf16)
 // Token-major [B*N][ld] (ld = nparts * heads * dh; part p of head h at columns p*D + h*dh) <->
 // head-major [heads*B][N][nparts*dh] (the layout of the flash-attention kernels of fra.hip, one
@@ -2121,6 +2182,23 @@ extern "C" int dfcsa_head3_bwd(int dtype, int B, int H, int W, int C, int Cout, 
 }
 
 extern "C" int dfcsa_colsum_ntiles(int64_t M) { return (int)((M + COLSUM_ROWS - 1) / COLSUM_ROWS); }
+
+extern "C" int dfcsa_colsum_fused(int dtype, int64_t M, int C, const void* x, float* partial, int n0, int n1,
+                                  float* d0, float* d1, float* d2, void* stream) {
+  if (M <= 0 || C <= 0 || C % 8 || !partial || !d0 || n0 < 0 || n1 < 0 || n0 + n1 > C) return DFCSA_EINVAL;
+  if ((n1 > 0 && !d1) || (n0 + n1 < C && !d2)) return DFCSA_EINVAL;
+  dim3 grid((C / 8 + 255) / 256, dfcsa_colsum_ntiles(M));
+  unsigned* cnt = dfcsa_ticket_alloc(grid.x);
+  if (!cnt) return DFCSA_EINVAL;
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(colsum_fused_kernel<bf16_t>, grid, dim3(256), 0, (hipStream_t)stream, M, C, (const bf16_t*)x,
+                       partial, cnt, n0, n1, d0, d1, d2);
+  else
+    hipLaunchKernelGGL(colsum_fused_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, M, C, (const float*)x,
+                       partial, cnt, n0, n1, d0, d1, d2);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
 
 extern "C" int dfcsa_colsum_partial(int dtype, int64_t M, int C, const void* x, float* partial, void* stream) {
   if (M <= 0 || C <= 0 || C % 8) return DFCSA_EINVAL;

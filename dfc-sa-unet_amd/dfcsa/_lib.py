@@ -68,6 +68,15 @@ class ConvDesc(ctypes.Structure):
                 ("work", ctypes.c_void_p), ("work_floats", ctypes.c_int64)]
 
 
+class BnFold(ctypes.Structure):
+    """dfcsa_bn_fold: the train-mode BatchNorm finalisation dfcsa_conv_gemm_bn folds into a conv."""
+    _fields_ = [("C", ctypes.c_int), ("count", ctypes.c_int), ("conv_bias", ctypes.c_void_p),
+                ("gamma", ctypes.c_void_p), ("beta", ctypes.c_void_p), ("running_mean", ctypes.c_void_p),
+                ("running_var", ctypes.c_void_p), ("num_batches_tracked", ctypes.c_void_p),
+                ("momentum", ctypes.c_float), ("eps", ctypes.c_float), ("scale", ctypes.c_void_p),
+                ("shift", ctypes.c_void_p), ("mean", ctypes.c_void_p), ("invstd", ctypes.c_void_p)]
+
+
 class WgradDesc(ctypes.Structure):
     _fields_ = [("dtype", ctypes.c_int), ("M", ctypes.c_int), ("ng", ctypes.c_int), ("Cg", ctypes.c_int),
                 ("g_ptr", ctypes.c_void_p * 3), ("nseg", ctypes.c_int), ("Cseg", ctypes.c_int),

@@ -135,20 +135,26 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     branch = not fullres and ops._SYNC_BN is None
     entry_on_branch = H * W >= ENTRY_ON_BRANCH_HW[0]
 
+    fold = ops.bn_fold_ok(training)   # BatchNorm finalisations inside the producing conv launches
+
     def entry_conv():
         y2_ = torch.empty((B, H, W, C), dtype=dtype, device=dev)
         res_ = torch.empty((B, H, W, C), dtype=dtype, device=dev) if has_res else xs[0]
         st2_ = stats(N2)
-        nt2_ = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
-                             [y2_, res_] if has_res else [y2_], C, bias=b2, stats=st2_)
-        return y2_, res_, st2_, nt2_
+        r = ops.conv_gemm(dtype, [(x, 0, 0) for x in xs], Cs, (B, H, W), (H, W), W2p, Kp2, N2,
+                          [y2_, res_] if has_res else [y2_], C, bias=b2, stats=st2_,
+                          bn=(bn2m, conv2.bias, C) if fold else None)
+        return y2_, res_, st2_, r
 
     if not entry_on_branch:
         y2, res, st2, nt2 = entry_conv()
     with on_branch(dev, branch, *xs):
         if entry_on_branch:
             y2, res, st2, nt2 = entry_conv()
-        bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
+        if fold:
+            nt2, bn2 = nt2
+        else:
+            bn2 = ops.bn_finalize(bn2m, conv2.bias, st2, nt2 if training else nt, C, N2, M, training)
         if not fullres:
             Pp = pool_size
             lsa_saved = lsa_core_forward(lsa, y2, bn2.scale, bn2.shift, True, Pp, dtype, pk,
@@ -156,8 +162,12 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     y1 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st1 = stats(C)
     nt1 = ops.conv_gemm(dtype, _conv3x3_segments(xs), Cs, (B, H, W), (H, W), W1p, Kp1, C, [y1], C,
-                        bias=conv1.bias, stats=st1)   # (3x3 halo tiles: one statistics row per 2-D tile)
-    bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt1 if training else nt, C, C, M, training)
+                        bias=conv1.bias, stats=st1,   # (3x3 halo tiles: one statistics row per 2-D tile)
+                        bn=(bn1m, conv1.bias, C) if fold else None)
+    if fold:
+        nt1, bn1 = nt1
+    else:
+        bn1 = ops.bn_finalize(bn1m, conv1.bias, st1, nt1 if training else nt, C, C, M, training)
     join_branch(dev, branch, bn2, None if fullres else lsa_saved, y2, res if has_res else None)
 
     if fullres:
@@ -193,8 +203,11 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
                  P(bn2.scale), P(bn2.shift), P(o), Pp, P(lsa.gamma), 1, P(local), P(attn), stream())
         # ---- gate conv ----
         nt3 = ops.conv_gemm(dtype, [(local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W3p, Kp3, C, [y3], C,
-                            bias=conv3.bias, stats=st3) or nt
-    bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt3, C, C, M, training)
+                            bias=conv3.bias, stats=st3, bn=(bn3m, conv3.bias, C) if fold else None) or nt
+    if isinstance(nt3, tuple):
+        nt3, bn3 = nt3
+    else:
+        bn3 = ops.bn_finalize(bn3m, conv3.bias, st3, nt3, C, C, M, training)
     fused = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     y4 = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     st4 = stats(C)
@@ -209,8 +222,11 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
              stream())
         nt4 = ops.conv_gemm(dtype, [(fused, 0, 0), (local, 0, 0), (attn, 0, 0)], C, (B, H, W), (H, W), W4p, Kp4, C,
-                            [y4], C, bias=conv4.bias, stats=st4) or nt
-    bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt4, C, C, M, training)
+                            [y4], C, bias=conv4.bias, stats=st4, bn=(bn4m, conv4.bias, C) if fold else None) or nt
+    if isinstance(nt4, tuple):
+        nt4, bn4 = nt4
+    else:
+        bn4 = ops.bn_finalize(bn4m, conv4.bias, st4, nt4, C, C, M, training)
     out = torch.empty((B, H, W, C), dtype=dtype, device=dev)
     pooled_out = None
     if pool:

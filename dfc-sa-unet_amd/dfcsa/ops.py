@@ -60,11 +60,18 @@ def ntiles_ew(M, C):
 _SPLITK_MAX_M = 65536   # split-K applies to few-tile launches only (dfcsa_conv_work_floats decides)
 
 
+# the train-mode BatchNorm finalisation folded into the producing conv's launch (dfcsa_conv_gemm_bn;
+# the finalize is launched separately when the picked kernel cannot fold); DFCSA_BN_FOLD=0 disables
+BN_FOLD = [os.environ.get("DFCSA_BN_FOLD", "1") == "1"]
+
+
 def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=None, stride=1,
-              mode=0, accumulate=False, stats=None, out_hw=(0, 0)):
+              mode=0, accumulate=False, stats=None, out_hw=(0, 0), bn=None):
     """segs: list of (tensor, dh, dw); grid: (B, Ho, Wo) output pixel grid; in_hw: (Hi, Wi).
     With `stats` (>= ceil(M/64) rows of [2][N] fp32) returns the number of statistics rows the
-    launch wrote (ntiles for bn_finalize; the 3x3 halo-tile kernel writes one per 2-D tile)."""
+    launch wrote (ntiles for bn_finalize; the 3x3 halo-tile kernel writes one per 2-D tile).
+    bn = (bn_module, conv_bias, C): the train-mode BatchNorm of output columns [0, C) finalised by the
+    launch itself (dfcsa_conv_gemm_bn); returns (rows, BNState) then."""
     B, Ho, Wo = grid
     d = _lib.ConvDesc()
     d.dtype = dt(dtype)
@@ -96,10 +103,28 @@ def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=N
         if wf > 0:
             work = torch.empty(wf, device=weight.device, dtype=torch.float32)
             d.work, d.work_floats = P(work), wf
+    if bn is not None:
+        bn_mod, conv_bias, C = bn
+        st = BNState(C, bn_mod.weight.device)
+        f = _lib.BnFold()
+        f.C, f.count = C, d.M
+        f.conv_bias, f.gamma, f.beta = P(conv_bias), P(bn_mod.weight), P(bn_mod.bias)
+        f.running_mean, f.running_var = P(bn_mod.running_mean), P(bn_mod.running_var)
+        f.num_batches_tracked = P(bn_mod.num_batches_tracked)
+        f.momentum = float(bn_mod.momentum if bn_mod.momentum is not None else 0.1)
+        f.eps = float(bn_mod.eps)
+        f.scale, f.shift, f.mean, f.invstd = P(st.scale), P(st.shift), P(st.mean), P(st.invstd)
+        call("dfcsa_conv_gemm_bn", ctypes.addressof(d), ctypes.addressof(f), stream())
+        return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d)), st
     call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
     if stats is not None:   # statistics rows written (the ntiles of bn_finalize)
         return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d))
     return None
+
+
+def bn_fold_ok(training):
+    """whether a BatchNorm after a conv is finalised inside the conv's launch (conv_gemm(bn=...))"""
+    return training and BN_FOLD[0] and _SYNC_BN is None and not _SKIP_FIN
 
 
 def _wgrad_desc(dtype, gs, Cg, segs, Cseg, grid, in_hw, stride, layout=0):

@@ -33,6 +33,20 @@ PRIO_SIDE = int(os.environ.get("DFCSA_PRIO_SIDE", "0"))
 PRIO_BRANCH = int(os.environ.get("DFCSA_PRIO_BRANCH", "0"))
 
 
+# The TransUNet (config 4) and plain UNet (config 1) backward passes issue their weight gradients
+# through side_or_main: measured slower on the side stream there (config 4 bf16, same box: 559-563
+# vs 568 img/s with everything on one stream -- its small M = 1568 ViT GEMMs fill the chip on
+# their own), so DFCSA_SIDE_STREAM_TU=1 opts in.
+SIDE_TU = [os.environ.get("DFCSA_SIDE_STREAM_TU", "0") == "1"]
+
+
+def side_or_main(device, *tensors):
+    """on_side for the TransUNet / UNet weight gradients when SIDE_TU is set, else the current stream."""
+    if SIDE_TU[0]:
+        return on_side(device, *tensors)
+    return contextlib.nullcontext()
+
+
 def side_stream(device):
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(idx)

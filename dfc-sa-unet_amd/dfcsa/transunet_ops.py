@@ -24,12 +24,13 @@ import os
 
 import torch
 
-from . import _lib, ops
+from . import _lib, ops, streams
 from ._lib import LIB, call
 from .block import grad_of
 from .ddp import notify_grads_ready
 from .ops import P, dt, rup, stream
 from .packs import get_packset, param_key
+from .streams import side_or_main
 from .unet_ops import ConvBNReLU  # noqa: F401  (decoder convs: Conv2dReLU = conv + BN + ReLU)
 
 KA = ops.KALIGN
@@ -100,6 +101,8 @@ class GNState:
 # finalize launches; dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused, C <= 1024).  DFCSA_GN_FUSED=0
 # restores the four-launch path.
 GN_FUSED = [os.environ.get("DFCSA_GN_FUSED", "1") == "1"]
+# the Linear bias gradients (column sums) in one launch (dfcsa_colsum_fused); DFCSA_COLSUM_FUSED=0: two
+COLSUM_FUSED = [os.environ.get("DFCSA_COLSUM_FUSED", "0") == "1"]
 
 
 def _gn_fused(C, G):
@@ -180,6 +183,9 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
     M, C = x.numel() // x.shape[-1], x.shape[-1]
     nt = LIB.dfcsa_colsum_ntiles(M)
     part = _f32((nt * C,), x.device)
+    if COLSUM_FUSED[0] and nt <= 64:   # one launch: the launch's last workgroup sums the (<= 64) partial rows
+        call("dfcsa_colsum_fused", dt(dtype), M, C, P(x), P(part), n0, n1, P(d0), P(d1), P(d2), stream())
+        return
     call("dfcsa_colsum_partial", dt(dtype), M, C, P(x), P(part), stream())
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
 
@@ -241,8 +247,11 @@ class RootStem(torch.autograd.Function):
         B, Ho, Wo, C, k, Cin, Kpad = ctx.geo
         dtype, conv, gn = ctx.dtype, ctx.root.conv, ctx.root.gn
         dy = gn_backward(dtype, dout.contiguous(), ctx.out, ctx.y, ctx.st, gn)
-        ops.conv_wgrad_into(dtype, [dy], C, [(ctx.cols, 0, 0)], Kpad, (B, Ho, Wo), (Ho, Wo), [conv._dwhat], k * k,
-                            Cin, Cin)
+        with side_or_main(dy.device, dy, ctx.cols):
+            ops.conv_wgrad_into(dtype, [dy], C, [(ctx.cols, 0, 0)], Kpad, (B, Ho, Wo), (Ho, Wo), [conv._dwhat], k * k,
+                                Cin, Cin)
+        # every StdConv2d's dL/d(w_hat) (side-stream weight gradients) is final: map them to dL/dw
+        streams.join()
         ctx.model._stdw.backward()
         notify_grads_ready(ctx.model)
         ctx.cols = ctx.y = ctx.out = None
@@ -346,20 +355,22 @@ class Bottleneck(torch.autograd.Function):
         st1, st2, st3, std = ctx.st
         dev = x.device
         dout = dout.contiguous()
-        dres = None
+        dres = dyd = None
         if ds:
             dyd = gn_backward(dtype, dout, out, yd, std, unit.gn_proj)
             dy3 = gn_backward(dtype, dout, out, y3, st3, unit.gn3)
         else:
             dres = torch.empty_like(out)   # relu'(out) * dout: the identity path's gradient
             dy3 = gn_backward(dtype, dout, out, y3, st3, unit.gn3, dz_out=dres)
-        _wgrad_1x1(dtype, dy3, a2, (B, Ho, Wo), (Ho, Wo), unit.conv3._dwhat)
+        with side_or_main(dev, dy3, a2):
+            _wgrad_1x1(dtype, dy3, a2, (B, Ho, Wo), (Ho, Wo), unit.conv3._dwhat)
         da2 = _gemm_1x1(dtype, dy3, pk["W3t"], rup(cout, KA), cmid,
                         torch.empty((B, Ho, Wo, cmid), dtype=dtype, device=dev))
         dy2 = gn_backward(dtype, da2, a2, y2, st2, unit.gn2)
         del da2
-        ops.conv_wgrad_into(dtype, [dy2], cmid, _taps3(a1), cmid, (B, Ho, Wo), (H, W), [unit.conv2._dwhat], 9, cmid,
-                            cmid, stride=s)
+        with side_or_main(dev, dy2, a1):
+            ops.conv_wgrad_into(dtype, [dy2], cmid, _taps3(a1), cmid, (B, Ho, Wo), (H, W), [unit.conv2._dwhat], 9,
+                                cmid, cmid, stride=s)
         da1 = torch.empty((B, H, W, cmid), dtype=dtype, device=dev)
         if s == 1:
             segs = [(dy2, 1 - kh, 1 - kw) for kh in range(3) for kw in range(3)]
@@ -371,9 +382,10 @@ class Bottleneck(torch.autograd.Function):
             del dcols
         dy1 = gn_backward(dtype, da1, a1, y1, st1, unit.gn1)
         del da1
-        _wgrad_1x1(dtype, dy1, x, (B, H, W), (H, W), unit.conv1._dwhat)
-        if ds:
-            _wgrad_1x1(dtype, dyd, x, (B, Ho, Wo), (H, W), unit.downsample._dwhat, stride=s)
+        with side_or_main(dev, dy1, x, dyd):
+            _wgrad_1x1(dtype, dy1, x, (B, H, W), (H, W), unit.conv1._dwhat)
+            if ds:
+                _wgrad_1x1(dtype, dyd, x, (B, Ho, Wo), (H, W), unit.downsample._dwhat, stride=s)
         dx = None
         if ctx.needs_input_grad[0]:
             if ds:
@@ -428,8 +440,9 @@ class PatchEmbed(torch.autograd.Function):
         call("dfcsa_drop_bwd", dt(dtype), de.numel(), P(dout.contiguous()), float(ctx.p), P(ctx.rng), SITE_EMBED,
              P(de), stream())
         call("dfcsa_batch_sum", dt(dtype), B, h * w * D, P(de), P(grad_of(pos)), stream())
-        bias_grad_into(dtype, de, conv.bias)
-        _wgrad_1x1(dtype, de, x, (B, h, w), (h, w), grad_of(conv.weight))
+        with side_or_main(de.device, de, x):
+            bias_grad_into(dtype, de, conv.bias)
+            _wgrad_1x1(dtype, de, x, (B, h, w), (h, w), grad_of(conv.weight))
         dx = None
         if ctx.needs_input_grad[0]:
             dx = _gemm_1x1(dtype, de, ctx.pk["Wt"], rup(D, KA), Cin, torch.empty_like(x))
@@ -573,23 +586,26 @@ class ViTBlock(torch.autograd.Function):
         # ---- MLP half: out = drop(fc2(drop(gelu(fc1(LN2 h1))))) + h1
         dm = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
         call("dfcsa_drop_bwd", dt(dtype), dm.numel(), P(dout), float(p), P(rng), site + 2, P(dm), stream())
-        _wgrad_1x1(dtype, dm, g, grid, hw, grad_of(mlp.fc2.weight))
-        bias_grad_into(dtype, dm, mlp.fc2.bias)
+        with side_or_main(dev, dm, g):
+            _wgrad_1x1(dtype, dm, g, grid, hw, grad_of(mlp.fc2.weight))
+            bias_grad_into(dtype, dm, mlp.fc2.bias)
         dg = _gemm_1x1(dtype, dm, pk["W2t"], KD, F, torch.empty_like(f))
         del dm
         df = torch.empty_like(f)
         call("dfcsa_gelu_drop_bwd", dt(dtype), f.numel(), P(f), P(dg), float(p), P(rng), site + 1, P(df), stream())
         del dg
-        _wgrad_1x1(dtype, df, y2, grid, hw, grad_of(mlp.fc1.weight))
-        bias_grad_into(dtype, df, mlp.fc1.bias)
+        with side_or_main(dev, df, y2):
+            _wgrad_1x1(dtype, df, y2, grid, hw, grad_of(mlp.fc1.weight))
+            bias_grad_into(dtype, df, mlp.fc1.bias)
         dy2 = _gemm_1x1(dtype, df, pk["W1t"], KF, D, torch.empty((B, gh, gw, D), dtype=dtype, device=dev))
         del df
         dh1 = _ln_backward(dtype, dy2, h1, mr2, blk.ffn_norm, dout)
         # ---- attention half: h1 = drop(out_proj(MHA(qkv(LN1 h)))) + h
         da = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
         call("dfcsa_drop_bwd", dt(dtype), da.numel(), P(dh1), float(p_attn), P(rng), site, P(da), stream())
-        _wgrad_1x1(dtype, da, cx, grid, hw, grad_of(att.out.weight))
-        bias_grad_into(dtype, da, att.out.bias)
+        with side_or_main(dev, da, cx):
+            _wgrad_1x1(dtype, da, cx, grid, hw, grad_of(att.out.weight))
+            bias_grad_into(dtype, da, att.out.bias)
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
         if ctx.probs is not None:
@@ -608,11 +624,12 @@ class ViTBlock(torch.autograd.Function):
             call("dfcsa_mha_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(dcx), P(lse), P(dvec),
                  P(dqkv), stream())
         del dcx
-        ops.conv_wgrad_into(dtype, [dqkv], 3 * D, [(y1, 0, 0)], D, grid, hw,
-                            [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],
-                            1, D, D, layout=2)
-        channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
-                          grad_of(att.value.bias))
+        with side_or_main(dev, dqkv, y1):
+            ops.conv_wgrad_into(dtype, [dqkv], 3 * D, [(y1, 0, 0)], D, grid, hw,
+                                [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],
+                                1, D, D, layout=2)
+            channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
+                              grad_of(att.value.bias))
         dy1 = _gemm_1x1(dtype, dqkv, pk["Wqkvt"], rup(3 * D, KA), D, torch.empty((B, gh, gw, D), dtype=dtype,
                                                                                   device=dev))
         del dqkv

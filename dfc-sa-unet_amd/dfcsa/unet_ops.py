@@ -13,6 +13,7 @@ from .block import grad_of, raise_eval_backward
 from .ddp import notify_grads_ready
 from .ops import P, S, dt, rup, stream
 from .packs import get_packset, param_key
+from .streams import side_or_main
 
 
 def _taps(xs, k=3):
@@ -60,9 +61,13 @@ class ConvBNReLU(torch.autograd.Function):
         nt = ops.ntiles_gemm(M)
         st = torch.empty(nt * 2 * C, device=dev, dtype=torch.float32) if training else None
         y = torch.empty((B, H, W, C), dtype=dtype, device=dev)
+        fold = ops.bn_fold_ok(training)
         ntw = ops.conv_gemm(dtype, _taps(xs, k), Cs, (B, H, W), (H, W), pk["Wf"], rup(k * k * Cin_p, ops.KALIGN), C,
-                            [y], C, bias=conv.bias, stats=st)
-        bnst = ops.bn_finalize(bn, conv.bias, st, ntw if training else nt, C, C, M, training)
+                            [y], C, bias=conv.bias, stats=st, bn=(bn, conv.bias, C) if fold else None)
+        if fold:
+            ntw, bnst = ntw
+        else:
+            bnst = ops.bn_finalize(bn, conv.bias, st, ntw if training else nt, C, C, M, training)
         out = ops.bn_act(dtype, y, bnst, 1)
         ctx.conv, ctx.bn, ctx.dtype, ctx.nsrc, ctx.np = conv, bn, dtype, nsrc, len(args) - nsrc
         ctx.xs, ctx.y, ctx.bnst, ctx.pk = xs, y, bnst, pk
@@ -88,8 +93,10 @@ class ConvBNReLU(torch.autograd.Function):
         del dz
         grid, hw = (B, H, W), (H, W)
         k = conv.kernel_size[0]
-        ops.conv_wgrad_into(dtype, [dy], C, _taps(xs, k), Cs, grid, hw, [grad_of(conv.weight)], k * k, ctx.nsrc * Cs,
-                            conv.in_channels)
+        # the weight gradient on the side stream beside the input-gradient GEMM (dfcsa.streams)
+        with side_or_main(y.device, dy, *xs):
+            ops.conv_wgrad_into(dtype, [dy], C, _taps(xs, k), Cs, grid, hw, [grad_of(conv.weight)], k * k,
+                                ctx.nsrc * Cs, conv.in_channels)
         notify_grads_ready(conv)
         dxs = [None] * ctx.nsrc
         if any(ctx.needs_input_grad[4:4 + ctx.nsrc]):

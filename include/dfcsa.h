@@ -68,6 +68,29 @@ typedef struct {
   int64_t work_floats;  /* splits its K range over workgroups when work holds dfcsa_conv_work_floats(d) */
 } dfcsa_conv_desc;
 int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream);
+/* The conv of *d (stats required) followed by the train-mode BatchNorm finalisation of its first C
+ * output columns -- the result of dfcsa_conv_gemm + dfcsa_bn_finalize(training = 1) over the
+ * launch's statistics rows (scale/shift/mean/invstd, running statistics, num_batches_tracked).  When
+ * the picked kernel's epilogue can (the tile kernels) the finalisation runs in the launch's own tail:
+ * its last workgroups reduce the statistics rows in two fixed-order ticket levels (no finalize
+ * launch, reference models/unet_dfc_sa_res.py:58-59 + nn.BatchNorm2d); otherwise the finalize is
+ * launched after the conv. */
+typedef struct {
+  int C;                      /* channels finalised: output columns [0, C) (C <= N) */
+  int count;                  /* elements per channel (M) */
+  const float* conv_bias;     /* optional: the conv bias, added to the batch mean (stats exclude it) */
+  const float* gamma;
+  const float* beta;
+  float* running_mean;
+  float* running_var;
+  int64_t* num_batches_tracked;   /* optional */
+  float momentum, eps;
+  float* scale;
+  float* shift;
+  float* mean;
+  float* invstd;
+} dfcsa_bn_fold;
+int dfcsa_conv_gemm_bn(const dfcsa_conv_desc* d, const dfcsa_bn_fold* f, void* stream);
 int dfcsa_conv_gemm_mtile(int N); /* rows per stats tile of the row-tile kernels */
 /* statistics rows the launch of *d writes (and dfcsa_bn_finalize reads as ntiles): one per M tile
  * of the row-tile kernels (ceil(M / BM), BM = 64..256), one per workgroup of the persistent 1x1
@@ -686,6 +709,11 @@ int dfcsa_copy_cols(int dtype, int64_t M, int ncols, const void* src, int ld_src
  * any C % 8 == 0) */
 int dfcsa_colsum_ntiles(int64_t M);
 int dfcsa_colsum_partial(int dtype, int64_t M, int C, const void* x, float* partial, void* stream);
+/* the same sums reduced inside the launch (last workgroup per 2048-column block, row order) and
+ * added into d0 [0, n0), d1 [n0, n0 + n1), d2 [n0 + n1, C) -- colsum_partial + slab_colsum3 in one
+ * launch; partial: [dfcsa_colsum_ntiles(M)][C] floats of hand-off scratch */
+int dfcsa_colsum_fused(int dtype, int64_t M, int C, const void* x, float* partial, int n0, int n1, float* d0,
+                       float* d1, float* d2, void* stream);
 /* SegmentationHead 3x3 conv + bias (:272-276): logits NCHW fp32 [B][Cout][H][W] from x NHWC
  * [B][H][W][C] (C <= 64, Cout <= 4), w fp32 [Cout][C][3][3]; bwd: dx, partial_w
  * [ntiles][Cout*C*9], partial_b [ntiles][Cout], ntiles = dfcsa_head3_ntiles */
@@ -799,8 +827,9 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 35: threads of the LightSelfAttention upsample-backward column kernel at C <= 128.
  * knob 36: 0 = one slot-sized grid per column block in the fused gate dgrad kernels (default 1:
  *          the C / 64 column blocks share the resident slots, grid.x = slots / (C / 64)).
- * knob 37: fewest 64-deep K stages a split-K conv launch may have (default 64).
+ * knob 37: fewest 64-deep K stages a split-K conv launch may have (default 24).
  * knob 38: workgroups a split-K conv launch aims for (default 600).
+ * knob 39: 0 = dfcsa_conv_gemm_bn always launches the separate finalize (no epilogue fold).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -44,7 +44,9 @@ def test_descriptor_layouts_match_c(tmp_path):
               ("dfcsa_wstd_entry", _lib.WstdEntry, ("K", "pad")),
               ("dfcsa_resample_desc", _lib.ResampleDesc, ("kk", "row0")),
               ("dfcsa_aug_desc", _lib.AugDesc, ("m", "fix", "rotate", "mask_w")),
-              ("dfcsa_pool_contract", _lib.PoolContract, ("rows", "H", "P"))]
+              ("dfcsa_pool_contract", _lib.PoolContract, ("rows", "H", "P")),
+              ("dfcsa_bn_fold", _lib.BnFold, ("conv_bias", "num_batches_tracked", "momentum", "eps", "scale",
+                                              "invstd"))]
     exprs = []
     want = []
     for cname, py, names in fields:

@@ -1,0 +1,73 @@
+"""BatchNorm finalisation folded into the producing conv launch (dfcsa_conv_gemm_bn, round 5): the
+launch's last workgroups reduce its statistics rows in two fixed-order ticket levels and finalise the
+BatchNorm as dfcsa_bn_finalize does.  Checked against conv + separate finalize (knob 39 = 0) on
+shapes that pick every conv kernel family (the 128x128 / 256x64 / 128x64 / 64x64 LDS-DMA tiles, the
+256x256 ping-pong tile, split-K + its epilogue launch, the fp32 register tile, and the streaming 1x1
+kernel, which falls back to the separate finalize), a column count past the BatchNorm's channels
+(the fused entry + residual conv), and bitwise repeatability."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(dtype, B, H, Cs, taps, N, C, fold, seed=0):
+    import dfcsa
+    from dfcsa import ops
+    torch.manual_seed(seed)
+    x = (torch.randn(B, H, H, Cs, device="cuda") * 0.5).to(dtype)
+    segs = [(x, kh - 1, kw - 1) for kh in range(3) for kw in range(3)] if taps == 9 else [(x, 0, 0)]
+    K = len(segs) * Cs
+    Kp = ops.rup(K, 64 if dtype == torch.bfloat16 else 32)
+    w = (torch.randn(N, Kp, device="cuda") * 0.05).to(dtype)
+    bias = torch.randn(N, device="cuda") * 0.1
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.1, 0.1)
+        bn.running_var.uniform_(0.9, 1.1)
+    y = torch.empty((B, H, H, N), device="cuda", dtype=dtype)
+    M = B * H * H
+    stats = torch.empty(((M + 63) // 64) * 2 * N, device="cuda")
+    saved = dfcsa._lib.LIB.dfcsa_get_tuning(39)
+    dfcsa.set_tuning(39, 1 if fold else 0)
+    try:
+        rows, st = ops.conv_gemm(dtype, segs, Cs, (B, H, H), (H, H), w, Kp, N, [y], N, bias=bias, stats=stats,
+                                 bn=(bn, bias, C))
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(39, saved)
+    return (st.scale.clone(), st.shift.clone(), st.mean.clone(), st.invstd.clone(), bn.running_mean.clone(),
+            bn.running_var.clone(), bn.num_batches_tracked.clone(), y)
+
+
+@pytest.mark.parametrize("dtype,B,H,Cs,taps,N,C", [
+    (torch.bfloat16, 16, 28, 256, 9, 512, 512),     # 28^2 3x3: 128x128 tile
+    (torch.bfloat16, 16, 56, 256, 9, 256, 256),     # 56^2 3x3, K = 2304: 128x128 / ping-pong
+    (torch.bfloat16, 8, 56, 256, 9, 512, 512),      # ping-pong 256x256 (N % 256, K >= 2048, >= 150 tiles)
+    (torch.bfloat16, 16, 14, 512, 9, 1024, 1024),   # 14^2 bottleneck: 64x64 tile
+    (torch.bfloat16, 16, 14, 1024, 9, 512, 512),    # split-K (few tiles, long K) + epilogue launch
+    (torch.bfloat16, 16, 112, 64, 9, 64, 64),       # N = 64: 256x64 tile
+    (torch.bfloat16, 4, 28, 64, 9, 64, 64),         # N = 64, small M: 128x64 tile
+    (torch.bfloat16, 16, 28, 512, 1, 1024, 512),    # entry + residual conv: N = 2C, BatchNorm on C
+    (torch.bfloat16, 16, 112, 64, 1, 128, 64),      # 1x1 at 112^2: streaming kernel
+    (torch.bfloat16, 16, 224, 8, 9, 64, 64),        # first layer: streaming kernel over shifted segments
+    (torch.float32, 2, 20, 32, 9, 48, 48),          # fp32 register tile, ragged N
+])
+def test_bn_fold_equals_separate_finalize(dtype, B, H, Cs, taps, N, C):
+    ref = _run(dtype, B, H, Cs, taps, N, C, fold=False)
+    got = _run(dtype, B, H, Cs, taps, N, C, fold=True)
+    again = _run(dtype, B, H, Cs, taps, N, C, fold=True)
+    names = ("scale", "shift", "mean", "invstd", "running_mean", "running_var", "num_batches_tracked", "y")
+    for n, a, b, c in zip(names, ref, got, again):
+        assert torch.equal(b, c), f"{n}: folded finalize not bitwise repeatable"
+        if n == "num_batches_tracked":
+            assert int(a) == int(b) == 1
+            continue
+        if n == "y":
+            assert torch.equal(a, b)
+            continue
+        # the two reductions sum the same fp32 rows in different (fixed) orders in fp64
+        err = (a.double() - b.double()).abs().max().item()
+        assert err <= 1e-6 * max(1.0, a.double().abs().max().item()), (n, err)

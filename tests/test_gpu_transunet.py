@@ -453,3 +453,26 @@ def test_transunet_full_factory_bf16_train_steps():
         losses.append(met["loss"].item())
     assert all(np.isfinite(losses)), losses
     assert losses[-1] < losses[0], losses
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("M,C,n0,n1", [(1568, 768, 768, 0), (1568, 2304, 768, 768), (1568, 3072, 3072, 0),
+                                       (37, 64, 16, 16), (4096, 4104, 4000, 100)])
+def test_colsum_fused(M, C, n0, n1, dtype):
+    """dfcsa_colsum_fused (the Linear bias gradients in one launch, last workgroup per column block)
+    against the column sums in float64, added into three destinations; bitwise repeatable."""
+    call, P, dt, stream = lib()
+    from dfcsa._lib import LIB
+    torch.manual_seed(M + C)
+    x = torch.randn(M, C, device="cuda").to(dtype)
+    ref = x.double().sum(0)
+    outs = []
+    for _ in range(2):
+        d = [torch.full((n,), 0.5, device="cuda") for n in (n0, n1, C - n0 - n1)]
+        part = torch.empty(LIB.dfcsa_colsum_ntiles(M) * C, device="cuda")
+        call("dfcsa_colsum_fused", dt(dtype), M, C, P(x), P(part), n0, n1, P(d[0]), P(d[1]) if n1 else None,
+             P(d[2]) if C - n0 - n1 else None, stream())
+        torch.cuda.synchronize()
+        outs.append(torch.cat(d))
+    assert (outs[0].double() - 0.5 - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
+    assert torch.equal(outs[0], outs[1])
