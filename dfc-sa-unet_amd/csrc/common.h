@@ -230,6 +230,28 @@ __device__ __forceinline__ void ld_sc1_f4x16(const float* p, int ld, f4v_t (&v)[
       : "v"(q[0]), "v"(q[1]), "v"(q[2]), "v"(q[3]), "v"(q[4]), "v"(q[5]), "v"(q[6]), "v"(q[7])
       : "memory");
 }
+__device__ __forceinline__ float4 ld_sc1_f4(const float* p) {
+  f4v_t v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
+  return make_float4(v[0], v[1], v[2], v[3]);
+}
+__device__ __forceinline__ void st_sc1_f4(float* p, float a, float b, float c, float d) {
+  f4v_t v = {a, b, c, d};
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+
+// four sc1 16-byte loads in flight, one wait: p, p + ld, p + 2 ld, p + 3 ld
+__device__ __forceinline__ void ld_sc1_f4x4(const float* p, int ld, f4v_t (&v)[4]) {
+  asm volatile(
+      "global_load_dwordx4 %0, %4, off sc1\n\t"
+      "global_load_dwordx4 %1, %5, off sc1\n\t"
+      "global_load_dwordx4 %2, %6, off sc1\n\t"
+      "global_load_dwordx4 %3, %7, off sc1\n\t"
+      "s_waitcnt vmcnt(0)"
+      : "=&v"(v[0]), "=&v"(v[1]), "=&v"(v[2]), "=&v"(v[3])
+      : "v"(p), "v"(p + ld), "v"(p + 2 * ld), "v"(p + 3 * ld)
+      : "memory");
+}
 // true in the workgroup that arrives last of `n` sharing *cnt (which it re-zeroes for the next
 // launch); every thread calls it (contains barriers)
 __device__ __forceinline__ bool wg_last_of(unsigned* cnt, unsigned n, int* flag_smem) {

@@ -860,6 +860,24 @@ __device__ __forceinline__ void raw_barrier() {
   __builtin_amdgcn_sched_barrier(0);
 }
 
+// Stream-K work decomposition (SK = true; round 5): the launch has G <= 256 workgroups (one per CU)
+// and workgroup g walks iterations [g I / G, (g + 1) I / G) of the tile-major space of I = tiles x nk
+// 64-deep K-tiles, so every CU does the same number of K-tiles whatever the tile count (the 28^2 /
+// 56^2 grids of 98 / 196 / 392 tiles leave a quarter or more of a wave idle as whole tiles).  A
+// segment that covers a whole tile runs the epilogue directly.  Otherwise the workgroup publishes
+// its fp32 partial tile (write-through, accumulator fragment order) into its slot (two per
+// workgroup: the first and the last tile it touches), takes the tile's ticket, and the tile's last
+// arriving segment sums the tile's partials in SEGMENT order -- its own from registers -- and runs
+// the epilogue (deterministic: the order does not depend on which segment arrives last).
+__device__ __forceinline__ int sk_lo(int g, int I, int G) { return (int)(((int64_t)g * I) / G); }
+// logical workgroup whose iteration range contains iteration i
+__device__ __forceinline__ int sk_owner(int i, int I, int G) {
+  int g = (int)(((int64_t)i * G) / I);
+  while (g + 1 < G && sk_lo(g + 1, I, G) <= i) ++g;
+  while (g > 0 && sk_lo(g, I, G) > i) --g;
+  return g;
+}
+
 template <int DEPTH, bool RF, bool BAL>
 __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs args) {
   using T = bf16_t;
@@ -1052,10 +1070,298 @@ __global__ void __launch_bounds__(512, 1) conv_gemm_pp_kernel(const ConvGemmArgs
 }
 
 template <int DEPTH, bool RF, bool BAL>
+__global__ void __launch_bounds__(512, 1) conv_gemm_ppsk_kernel(const ConvGemmArgs args) {
+  constexpr bool SK = true;
+  using T = bf16_t;
+  constexpr int BM = 256, BN = 256, WM = 2, WN = 4;
+  constexpr int HALF = 128 * 128, BUF = 4 * HALF;
+  constexpr int OSTR = BN * (int)sizeof(T) + 16;
+  constexpr int SMEM = (2 * BUF > BM * OSTR) ? 2 * BUF : BM * OSTR;
+  constexpr int LEAD = DEPTH == 1 ? 4 : 6;   // issue slot of half-tile s = s - LEAD
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+  const int nN = args.N / BN;
+  const int ntiles = nN * ((args.M + BM - 1) / BM);
+  const int nk = args.Kpad / 64;
+  const int M = args.M;
+  const int cchunk = (lane & 7) ^ ((4 * (wave & 1) + (lane >> 4)) & 7);
+  const int rsub = lane >> 3;
+  const int lane_ch = cchunk * 8;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const rsrc_t rb = buf_rsrc(args.Bw);
+
+  // this workgroup's iterations: SK, a contiguous range of the (tile, K-tile) space (logical index
+  // g: consecutive g share an XCD); else one whole tile
+  int it, it_end, g = 0, G = 1, I = 0;
+  if constexpr (SK) {
+    G = gridDim.x;
+    I = ntiles * nk;
+    g = xcd_remap(blockIdx.x, G);
+    if (g < 0) return;
+    it = sk_lo(g, I, G);
+    it_end = sk_lo(g + 1, I, G);
+  } else {
+    const int L = xcd_remap(blockIdx.x, ntiles);
+    if (L < 0) return;  // whole workgroup: no barrier is left unmatched
+    it = L * nk;
+    it_end = it + nk;
+  }
+  const int first_tile = it / nk;
+
+  f32x4_t acc[8][4];
+  Frag<T> fa[4][2], fb0[2][2], fb1[2][2];
+
+  while (it < it_end) {
+    const int L = it / nk, k0 = it - L * nk, k1 = min(nk, k0 + (it_end - it));
+    it += k1 - k0;
+    const int n_tile = L % nN, m_tile = L / nN;
+    const int m0 = m_tile * BM, n0 = n_tile * BN;
+
+    // the 4 A rows and 4 B rows this lane fetches: index q = half*2 + instruction; byte offsets for
+    // the buffer-descriptor LDS-DMA (blds16: the stage's shift goes into the scalar base)
+    unsigned a_off[4], a_tap[4], b_off[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int h = q >> 1, j = q & 1;
+      const int hr = (j * 8 + wave) * 8 + rsub;            // row of the half-tile image
+      const int m = m0 + (hr >> 6) * 128 + h * 64 + (hr & 63);
+      a_off[q] = 0;
+      a_tap[q] = 0;
+      if (m < M) {
+        const int b = dm_div(args.dm_hw, m);
+        const int rem = m - b * args.dm_hw.d;
+        const int oh = dm_div(args.dm_w, rem);
+        const int ow = rem - oh * args.dm_w.d;
+        const int ih = oh * args.stride, iw = ow * args.stride;
+        a_off[q] = 2u * (unsigned)(((b * args.Hi + ih) * args.Wi + iw) * args.Cseg + lane_ch);
+        unsigned t = 0;
+#pragma unroll
+        for (int dh = -1; dh <= 1; ++dh)
+#pragma unroll
+          for (int dw = -1; dw <= 1; ++dw)
+            t |= (unsigned)(ih + dh >= 0 && ih + dh < args.Hi && iw + dw >= 0 && iw + dw < args.Wi) << ((dh + 1) * 3 + dw + 1);
+        a_tap[q] = t;
+      }
+      const int n = n0 + (hr >> 5) * 64 + h * 32 + (hr & 31);
+      b_off[q] = 2u * (unsigned)(n * args.Kpad + lane_ch);
+    }
+    const int nks = k1 - k0;
+    const int slast = 4 * nks - 1;
+
+    // half-tile s = 4 * (local K-tile) + {0: A0, 1: B0, 2: B1, 3: A1} into buffer (local K-tile & 1)
+    auto issue = [&](int sq) {
+      if (sq > slast) return;
+      const int lkt = sq >> 2, i = sq & 3, kt = k0 + lkt;
+      char* bufp = smem + (lkt & 1) * BUF;
+      if (i == 0 || i == 3) {
+        const int h = i == 0 ? 0 : 1;
+        char* dst = bufp + h * HALF;
+        const int kk = kt * 64;
+        const int seg = dm_div(args.dm_cseg, kk);
+        const int ch0 = kk - seg * args.Cseg;
+        const ConvSeg sg = args.seg[seg];
+        const int delta = (sg.dh * args.Wi + sg.dw) * args.Cseg + ch0;
+        const int tb = (sg.dh + 1) * 3 + sg.dw + 1;
+        const rsrc_t ra = buf_rsrc((const T*)sg.ptr + delta);
+#pragma unroll
+        for (int j = 0; j < 2; ++j) blds16(ra, sel_oob(a_tap[h * 2 + j], tb, a_off[h * 2 + j]), 0, dst + (j * 8 + wv) * 1024);
+      } else {
+        const int h = i == 1 ? 0 : 1;
+        char* dst = bufp + (2 + h) * HALF;
+#pragma unroll
+        for (int j = 0; j < 2; ++j) blds16(rb, b_off[h * 2 + j], (unsigned)kt * 128u, dst + (j * 8 + wv) * 1024);
+      }
+    };
+
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = {0.f, 0.f, 0.f, 0.f};
+
+    auto read_a = [&](const char* img) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) read_frag<T>(img, wr * 64 + i * 16 + (lane & 15), gq, lane, fa[i][gq]);
+    };
+    auto read_b = [&](const char* img, Frag<T> (&fb)[2][2]) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int gq = 0; gq < 2; ++gq) read_frag<T>(img, wc * 32 + j * 16 + (lane & 15), gq, lane, fb[j][gq]);
+    };
+    auto quad = [&](int ms, int ns, const Frag<T> (&fb)[2][2]) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int gq = 0; gq < 2; ++gq)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) mma(acc[ms * 4 + i][ns * 2 + j], fa[i][gq], fb[j][gq]);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    // The wait of slot q (= 4 * K-tile + phase) must retire every half read in slot q + 1:
+    // A0 (q+1) and -- unless pre-read in phase 4 -- B0 (q+2) before phase 1; B1 (q+2) before
+    // phase 2; A1 (q+2) before phase 3; with BAL the next B0 (q+3) before phase 4.
+    auto vwait = [&](int q) {
+      const int p = q & 3;
+      const int need = p == 2 ? (BAL ? q + 3 : q + 1) : (p == 3 ? (BAL ? q + 1 : q + 2) : q + 2);
+      const int r = min(q + LEAD, slast) - min(need, slast);
+      if (r >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (r == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (r == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    };
+
+    for (int sq = 0; sq < LEAD; ++sq) issue(sq);
+    {
+      const int r = min(LEAD - 1, slast) - 1;   // halves 0 and 1 needed first
+      if (r >= 4) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else if (r == 3) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      else if (r == 2) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else if (r == 1) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    raw_barrier();
+    if (BAL) read_b(smem + 2 * HALF, fb0);   // B0 of K-tile 0 (later ones: pre-read in phase 4)
+    if (wr == 1) raw_barrier();   // G1 runs one barrier behind G0
+
+    // one K-tile; fbp holds (BAL) or receives its B0, fbq receives B1 (and with BAL the next B0)
+    auto ktile = [&](int lkt, Frag<T> (&fbp)[2][2], Frag<T> (&fbq)[2][2]) {
+      const char* buf = smem + (lkt & 1) * BUF;
+      const char* nbuf = smem + ((lkt + 1) & 1) * BUF;
+      const int q = 4 * lkt;
+      // phase 1: quadrant (0,0) [A0 + B0]
+      if (!RF) issue(q + LEAD);
+      read_a(buf);
+      if (!BAL) read_b(buf + 2 * HALF, fbp);
+      if (RF) issue(q + LEAD);
+      vwait(q);
+      raw_barrier();
+      quad(0, 0, fbp);
+      raw_barrier();
+      // phase 2: quadrant (0,1) [A0 + B1]
+      if (!RF) issue(q + 1 + LEAD);
+      read_b(buf + 3 * HALF, fbq);
+      if (RF) issue(q + 1 + LEAD);
+      vwait(q + 1);
+      raw_barrier();
+      quad(0, 1, fbq);
+      raw_barrier();
+      // phase 3: quadrant (1,1) [A1 + B1]
+      if (!RF) issue(q + 2 + LEAD);
+      read_a(buf + HALF);
+      if (RF) issue(q + 2 + LEAD);
+      vwait(q + 2);
+      raw_barrier();
+      quad(1, 1, fbq);
+      raw_barrier();
+      // phase 4: quadrant (1,0) [A1 + B0]
+      if (!RF) issue(q + 3 + LEAD);
+      if (BAL && lkt + 1 < nks) read_b(nbuf + 2 * HALF, fbq);
+      if (RF) issue(q + 3 + LEAD);
+      vwait(q + 3);
+      raw_barrier();
+      quad(1, 0, fbp);
+      raw_barrier();
+    };
+    if (BAL) {
+      for (int kt = 0; kt < nks; kt += 2) {
+        ktile(kt, fb0, fb1);
+        if (kt + 1 < nks) ktile(kt + 1, fb1, fb0);
+      }
+    } else {
+      for (int kt = 0; kt < nks; ++kt) ktile(kt, fb0, fb1);
+    }
+    if (wr == 0) raw_barrier();   // re-align the groups before the epilogue reuses the LDS
+    __syncthreads();
+    if constexpr (SK) {
+      if (k0 != 0 || k1 != nk) {
+        // partial tile: publish, take the tile's ticket; the last segment combines and stores
+        const int gf = sk_owner(L * nk, I, G), gl = sk_owner(L * nk + nk - 1, I, G);
+        const int mine = g - gf;
+        auto slot_of = [&](int gg) {   // the partial slot of the segment of tile L done by gg
+          return 2 * gg + (L == sk_lo(gg, I, G) / nk ? 0 : 1);
+        };
+        constexpr int PT = 8 * 64 * 32 * 4;   // floats per partial tile (8 waves x 32 fragments x 64 lanes x 4)
+        float* own = args.kwork + (size_t)slot_of(g) * PT + (wave * 32) * 256 + lane * 4;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const f32x4_t v = acc[i][j];
+            st_sc1_f4(own + (i * 4 + j) * 256, v[0], v[1], v[2], v[3]);
+          }
+        int* flag = (int*)smem;
+        if (!wg_last_of(args.kcnt + L, (unsigned)(gl - gf + 1), flag)) continue;
+        // sum the tile's segments in segment order, every one (this workgroup's too) read back from
+        // its slot: no second accumulator set in registers
+        (void)mine;
+        for (int sgm = 0; sgm <= gl - gf; ++sgm) {
+          const float* src = args.kwork + (size_t)slot_of(gf + sgm) * PT + (wave * 32) * 256 + lane * 4;
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            f4v_t v[4];
+            ld_sc1_f4x4(src + (i * 4) * 256, 256, v);
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              const f32x4_t w = {v[j][0], v[j][1], v[j][2], v[j][3]};
+              acc[i][j] = sgm == 0 ? w : acc[i][j] + w;
+            }
+          }
+        }
+      }
+    }
+    conv_epilogue<T, BM, BN, WM, WN>(args, acc, smem, m0, n0, m_tile, tid, lane, wr, wc);
+    if constexpr (SK) __syncthreads();   // the next segment's DMA must not overwrite the staging tile
+  }
+  (void)first_tile;
+}
+
+template <int DEPTH, bool RF, bool BAL>
 int launch_pp(const ConvGemmArgs& a, hipStream_t st) {
   if (t_dry_rows) { *t_dry_rows = (a.M + 255) / 256; if (t_dry_bn) *t_dry_bn = 256; return 0; }
   dim3 grid(xcd_pad((a.N / 256) * ((a.M + 255) / 256)));
   hipLaunchKernelGGL((conv_gemm_pp_kernel<DEPTH, RF, BAL>), grid, dim3(512), 0, st, a);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+// stream-K ping-pong launch (see conv_gemm_pp_kernel): G = 256 persistent workgroups (one per CU);
+// workspace: 2 partial tiles (256 KB each) per workgroup; tickets: one per tile
+int g_ppsk = 0;   // knob 40: 1 = the stream-K ping-pong decomposition where it applies (measured slower: opt-in)
+constexpr int kPpskG = 256;
+int64_t ppsk_work_floats() { return (int64_t)2 * kPpskG * 256 * 256; }
+bool ppsk_applies(const ConvGemmArgs& a) {
+  if (!g_ppsk || a.N % 256 || a.K < 2048) return false;
+  const int tiles = (a.N / 256) * ((a.M + 255) / 256);
+  const int nk = a.Kpad / 64;
+  const int64_t I = (int64_t)tiles * nk;
+  if (tiles >= 2 * kPpskG || I < 8 * kPpskG) return false;
+  // whole waves of tiles fill the chip already (>= 90 %)
+  const int waves = (tiles + kPpskG - 1) / kPpskG;
+  if (tiles * 10 >= waves * kPpskG * 9) return false;
+  // at most ~3 segments per tile (the last arriver reads the others' 256 KB partials serially)
+  return I / kPpskG >= nk / 3;
+}
+int launch_ppsk(ConvGemmArgs a, hipStream_t st) {
+  if (t_dry_rows) {
+    *t_dry_rows = (a.M + 255) / 256;
+    if (t_dry_bn) *t_dry_bn = 256;
+    if (t_dry_work) *t_dry_work = ppsk_work_floats();
+    return 0;
+  }
+  if (!a.kwork || a.kwork_floats < ppsk_work_floats()) return DFCSA_EINVAL;
+  const int tiles = (a.N / 256) * ((a.M + 255) / 256);
+  a.kcnt = dfcsa_ticket_alloc(tiles);
+  if (!a.kcnt) return DFCSA_EINVAL;
+  hipLaunchKernelGGL((conv_gemm_ppsk_kernel<2, true, false>), dim3(kPpskG), dim3(512), 0, st, a);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -2470,6 +2776,8 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
         case 23: if (a.N % 256 == 0) return launch_pp<2, false, true>(a, st); break;
         case 24: if (a.N % 256 == 0) return launch_pp<1, false, false>(a, st); break;
         case 25: if (a.N % 256 == 0) return launch_pp<2, true, true>(a, st); break;
+        case 41: if ((a.kwork || t_dry_work) && a.N % 256 == 0) { const int gg = g_ppsk; g_ppsk = 1;
+                   const bool ok = ppsk_applies(a); g_ppsk = gg; if (ok) return launch_ppsk(a, st); } break;
         case 29: { int ks, kp; const int g = g_splitk; g_splitk = 1; splitk_plan(a, &ks, &kp); g_splitk = g;
                    if (ks > 1 && (a.kwork || t_dry_work)) return launch_splitk(a, ks, kp, st); break; }
         case 30: return launch_glds32<128, 128, 4, 2, 4>(a, st);
@@ -2500,6 +2808,9 @@ int launch_t(const ConvGemmArgs& a, hipStream_t st) {
       splitk_plan(a, &ks, &kp);
       if (ks > 1) return launch_splitk(a, ks, kp, st);
     }
+    // stream-K ping-pong tiles where whole 256x256 tiles leave a partial wave (the 28^2 / 56^2
+    // grids of 98 / 196 / 392 tiles): every CU runs the same number of K-tiles
+    if ((a.kwork || t_dry_work) && ppsk_applies(a)) return launch_ppsk(a, st);
     // N <= 64 with many rows: 256x64 / 8 waves (wave tile 32x64, twice the rows per B panel);
     // fewer than one workgroup of 128x128 per CU (the 14^2 level, 28^2 with N <= 256): 128x64 doubles the
     // workgroup count (gemm_bench: bottleneck dgrad 123 -> 108 us, bottleneck fwd 59 -> 52 us).
@@ -2888,6 +3199,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 36: return g_gate_grid_div;
     case 37: return g_splitk_min_nk;
     case 39: return g_bn_fold;
+    case 40: return g_ppsk;
     case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
@@ -2923,6 +3235,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
   if (knob == 36) { g_gate_grid_div = value; return 0; }
   if (knob == 39) { g_bn_fold = value; return 0; }
+  if (knob == 40) { g_ppsk = value; return 0; }
   if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 24; return 0; }
   if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }

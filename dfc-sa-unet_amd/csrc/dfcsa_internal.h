@@ -48,6 +48,7 @@ struct ConvGemmArgs {
   float* kwork;
   int64_t kwork_floats;
   int ksplit, kper;
+  unsigned* kcnt;   // stream-K ping-pong launch: one ticket per output tile (zero, re-zeroed)
   BnFold fold;
 };
 

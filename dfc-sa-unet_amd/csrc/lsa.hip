@@ -795,16 +795,6 @@ extern "C" int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, cons
 // image (ticket) forms dk = dE^T q and dv = A^T dO for the image's tokens from the published rows;
 // the last of all adds dgamma (partials in token order).  Replaces lsa_up_bwd_cols +
 // lsa_attn_bwd_rows + lsa_attn_bwd_cols (three dependent launches on the backward's critical path).
-__device__ __forceinline__ float4 ld_sc1_f4(const float* p) {
-  f4v_t v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1\n\ts_waitcnt vmcnt(0)" : "=&v"(v) : "v"(p) : "memory");
-  return make_float4(v[0], v[1], v[2], v[3]);
-}
-__device__ __forceinline__ void st_sc1_f4(float* p, float a, float b, float c, float d) {
-  f4v_t v = {a, b, c, d};
-  asm volatile("global_store_dwordx4 %0, %1, off sc1\n\ts_nop 1" ::"v"(p), "v"(v) : "memory");
-}
-
 __global__ void __launch_bounds__(256) lsa_core_bwd_kernel(int H, int C, int Cq, int P, const float* __restrict__ rows,
                                                            const float* __restrict__ o, const float* gamma,
                                                            const float* __restrict__ qkv, const float* __restrict__ A,

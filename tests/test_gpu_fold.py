@@ -71,3 +71,69 @@ def test_bn_fold_equals_separate_finalize(dtype, B, H, Cs, taps, N, C):
         # the two reductions sum the same fp32 rows in different (fixed) orders in fp64
         err = (a.double() - b.double()).abs().max().item()
         assert err <= 1e-6 * max(1.0, a.double().abs().max().item()), (n, err)
+
+
+@pytest.mark.parametrize("B,H,Cs,nsrc,N,taps", [
+    (16, 28, 512, 2, 512, 9),      # dec4 3x3 forward: 98 tiles x 144 K-tiles (~3 segments per tile)
+    (16, 28, 512, 1, 1024, 11),    # dec4 fused 3x3 + 1x1 dgrad shape (K = 5632): 196 tiles
+    (16, 56, 256, 2, 256, 9),      # dec3 3x3 forward: 196 tiles x 72
+    (16, 56, 256, 1, 512, 11),     # dec3 dgrad (K = 2816): 392 tiles = 1.53 waves
+    (16, 28, 256, 1, 512, 9),      # enc4 3x3 forward (K = 2304)
+])
+def test_stream_k_pingpong_conv(B, H, Cs, nsrc, N, taps):
+    """The stream-K ping-pong conv (knob 40, round 5): output vs torch fp32 conv of the same bf16
+    operands, BatchNorm statistics rows vs the fp32 column sums, the folded BatchNorm vs the
+    non-stream-K launch, and bitwise repeatability (the partial tiles are summed in segment order,
+    whichever segment arrives last)."""
+    import ctypes
+
+    import torch.nn.functional as F
+
+    import dfcsa
+    from dfcsa import _lib, ops
+    dtype = torch.bfloat16
+    torch.manual_seed(B + H + N)
+    xs = [(torch.randn(B, Cs, H, H) * 0.5).to(dtype).float() for _ in range(nsrc)]
+    x = torch.cat(xs, 1)
+    if taps == 9:
+        w = (torch.randn(N, nsrc * Cs, 3, 3) * 0.03).to(dtype).float()
+        ref = F.conv2d(x, w, padding=1)
+        segs_t = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)]
+        wmat = w.permute(0, 2, 3, 1).reshape(N, -1)            # k = tap * Cin + ci
+    else:   # 9 taps + 2 extra 1x1 segments over the same input (the block-input dgrad's K layout)
+        w3 = (torch.randn(N, Cs, 3, 3) * 0.03).to(dtype).float()
+        w1 = (torch.randn(N, 2 * Cs) * 0.03).to(dtype).float()
+        ref = F.conv2d(x, w3, padding=1) + F.conv2d(torch.cat([x, x], 1), w1.view(N, 2 * Cs, 1, 1))
+        segs_t = [(kh - 1, kw - 1) for kh in range(3) for kw in range(3)] + [(0, 0), (0, 0)]
+        wmat = torch.cat([w3.permute(0, 2, 3, 1).reshape(N, -1), w1], 1)
+    K = wmat.shape[1]
+    Kp = ops.rup(K, 64)
+    wp = torch.zeros(N, Kp, dtype=dtype, device="cuda")
+    wp[:, :K] = wmat.to(dtype).cuda()
+    xh = [t.permute(0, 2, 3, 1).contiguous().to(dtype).cuda() for t in xs]
+    segs = [(xh[i % nsrc] if taps == 9 else xh[0], dh, dw) for j, (dh, dw) in enumerate(segs_t)
+            for i in range(nsrc if taps == 9 else 1)]
+    M = B * H * H
+    outs = []
+    for sk in (1, 1, 0):   # (opt-in: knob 40 is 0 by default, measured slower than the tile choice)
+        saved = _lib.LIB.dfcsa_get_tuning(40)
+        dfcsa.set_tuning(40, sk)
+        try:
+            y = torch.empty((B, H, H, N), dtype=dtype, device="cuda")
+            stats = torch.empty(((M + 63) // 64) * 2 * N, device="cuda")
+            bn = torch.nn.BatchNorm2d(N).cuda()
+            rows, st = ops.conv_gemm(dtype, segs, Cs, (B, H, H), (H, H), wp, Kp, N, [y], N, stats=stats,
+                                     bn=(bn, None, N))
+            torch.cuda.synchronize()
+            outs.append((y.clone(), stats[:rows * 2 * N].clone(), st.scale.clone(), st.shift.clone(), rows))
+        finally:
+            dfcsa.set_tuning(40, saved)
+    (y1, s1, sc1, sh1, r1), (y2, s2, sc2, sh2, _), (y0, s0, sc0, sh0, r0) = outs
+    assert torch.equal(y1, y2) and torch.equal(s1, s2) and torch.equal(sc1, sc2) and torch.equal(sh1, sh2)
+    yr = y1.float().permute(0, 3, 1, 2).cpu()
+    assert ((yr - ref).norm() / ref.norm()).item() < 1e-2
+    assert ((y1.float() - y0.float()).norm() / y0.float().norm()).item() < 1e-2
+    st = s1.view(-1, 2, N).sum(0).cpu().double()
+    assert ((st[0] - ref.double().sum((0, 2, 3))).norm() / ref.double().sum((0, 2, 3)).norm()).item() < 1e-4
+    assert ((sc1 - sc0).abs().max() / sc0.abs().max()).item() < 1e-4
+    assert ((sh1 - sh0).abs().max() / sh0.abs().max().clamp_min(1e-6)).item() < 1e-3
