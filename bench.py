@@ -79,6 +79,20 @@ def pmc_traffic(cls):
         return None, None
 
 
+def replayed_classes():
+    """Kernel time per step of each roofline class in the replayed HIP-graph step, every stream
+    concurrent, from the newest committed kernel trace of this benchmark
+    (profiles/rNN_replay_classes.json, tools/rocpd_export.py replay)."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_replay_classes.json")))
+    if not files:
+        return None, None
+    try:
+        return json.load(open(files[-1]))["classes"], os.path.relpath(files[-1], ROOT)
+    except (KeyError, ValueError, OSError):
+        return None, None
+
+
 def cpu_model_name():
     try:
         out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
@@ -438,6 +452,17 @@ def main():
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "ms_per_step": round(ms / args.steps, 3), "share_of_step": round(ms / (el * 1e3), 3),
                 "other_class": {}}
+        rep, rsrc = replayed_classes() if headline else (None, None)
+        if rep and dom_key in rep and rep[dom_key]["ms_per_step"] > 0:
+            # the same class's FLOPs per step over its kernel time in the replayed step (streams
+            # concurrent, so a launch also counts the CUs it shares): the figure the step runs at
+            r = rep[dom_key]
+            a_rep = fl / args.steps / (r["ms_per_step"] * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9)
+            roof["replayed"] = {"achieved": round(a_rep, 2), "frac": round(a_rep / peak, 4),
+                                "ms_per_step": round(r["ms_per_step"], 3),
+                                "launches_per_step": r["launches_per_step"], "source": rsrc,
+                                "timing": "rocprofv3 kernel trace of the timed HIP-graph replays (side and "
+                                          "branch streams concurrent), this run's class FLOPs per step"}
         if args.model == "fullres" and 3 in cls:
             roof = fra_exp_roofline(roof, cls[3], args, B, L)
         for v in cls.values():

@@ -7,6 +7,11 @@
   python tools/rocpd_export.py step <FETCH_SIZE db> <WRITE_SIZE db> <out.json>
       HBM bytes of ONE whole training step (the dispatches after the second-to-last clip_sgd
       launch up to the last one) in total and per kernel group (bench.py's step_roofline.hbm_frac)
+  python tools/rocpd_export.py replay <kernel-trace db> <out.json> [steps]
+      per roofline class and per kernel group: launches and kernel time per step over the LAST
+      `steps` (default 5) complete steps of the trace, split at the clip_sgd launches -- with
+      `bench.py --no-kernel-timing ...` under rocprofv3 these are the timed HIP-graph replays, every
+      stream concurrent (bench.py's roofline.replayed reads it)
   python tools/rocpd_export.py sq <SQ/GRBM counter db> <out.json>
       per kernel group: SQ_VALU_MFMA_BUSY_CYCLES, SQ_INSTS_MFMA, SQ_LDS_BANK_CONFLICT, SQ_LDS_IDX_ACTIVE,
       GRBM_GUI_ACTIVE and the MFMA-busy fraction = MFMA busy cycles / (GUI_ACTIVE / 8 XCDs x 1024 SIMDs)
@@ -50,6 +55,34 @@ def classes(db, out):
     print(json.dumps(res, indent=1))
 
 
+def replay(db, out, steps=5):
+    """Class and group kernel time of the replayed step (last `steps` steps, clip_sgd-delimited)."""
+    c = sqlite3.connect(db)
+    rows = list(c.execute("select name, start, end from kernels order by start"))
+    ends = [i for i, r in enumerate(rows) if "clip_sgd" in r[0]]
+    if len(ends) < steps + 1:
+        raise SystemExit(f"need >= {steps + 1} clip_sgd launches in the trace, found {len(ends)}")
+    sel = rows[ends[-steps - 1] + 1: ends[-1] + 1]
+    wall = (sel[-1][2] - sel[0][1]) / 1e6 / steps
+    res = {"steps": steps, "launches_per_step": len(sel) / steps, "first_to_last_kernel_ms_per_step": wall,
+           "definition": "kernel durations (end - start) summed per class / group over the last `steps` "
+                         "clip_sgd-delimited steps, divided by `steps`; concurrent streams overlap, so the "
+                         "sum over groups exceeds the wall time", "classes": {}, "groups": {}}
+    for cls, pats in CLASSES.items():
+        ks = [r for r in sel if any(p in r[0] for p in pats)]
+        res["classes"][cls] = {"launches_per_step": len(ks) / steps,
+                               "ms_per_step": sum(r[2] - r[1] for r in ks) / 1e6 / steps}
+    grp = defaultdict(lambda: [0, 0])
+    for n, s_, e_ in sel:
+        g = grp[group_of(n)]
+        g[0] += 1
+        g[1] += e_ - s_
+    res["groups"] = {k: {"launches_per_step": v[0] / steps, "ms_per_step": v[1] / 1e6 / steps}
+                     for k, v in sorted(grp.items(), key=lambda kv: -kv[1][1])}
+    json.dump(res, open(out, "w"), indent=1)
+    print(json.dumps(res["classes"]), round(wall, 3), "ms first-to-last kernel per step")
+
+
 def _per_dispatch(db, counter):
     c = sqlite3.connect(db)
     out = {}
@@ -60,7 +93,7 @@ def _per_dispatch(db, counter):
 
 
 CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
-                         "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel"),
+                         "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel", "conv_gemm_ppsk_kernel"),
            "conv_wgrad": ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
            # bench.py's class 4 (DFCSA_PROF_CONV_STREAM) times the streaming 1x1 GEMMs AND the fused
            # block GEMMs (dfcsa_dgrad_gate*, dfcsa_gate_fusion_fwd, dfcsa_local_attn_gate_fwd): the
@@ -107,7 +140,8 @@ def traffic_all(fdb, wdb, out):
 
 
 GROUPS = (("conv_gemm", ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
-                         "small_conv_f32_kernel", "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel")),
+                         "small_conv_f32_kernel", "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel",
+                         "conv_gemm_ppsk_kernel")),
           ("conv_wgrad", ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel",
                           "wgrad_reduce", "small_wgrad_f32_kernel", "small_wgrad_dgrad_f32_kernel")),
           ("conv1x1_stream", ("conv1x1_stream_kernel",)),
@@ -207,6 +241,8 @@ if __name__ == "__main__":
         classes(sys.argv[2], sys.argv[3])
     elif sys.argv[1] == "step":
         step(sys.argv[2], sys.argv[3], sys.argv[4])
+    elif sys.argv[1] == "replay":
+        replay(sys.argv[2], sys.argv[3], *(int(a) for a in sys.argv[4:5]))
     elif sys.argv[1] == "sq":
         sq(sys.argv[2], sys.argv[3])
     else:
