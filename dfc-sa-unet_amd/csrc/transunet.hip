@@ -1426,6 +1426,51 @@ __global__ void upsample2_ac_bwd_kernel(int B, int C, int Hi, int Wi, float sh, 
   }
 }
 
+// UpsamplingBilinear2d(scale_factor = s) (align_corners) on fp32 NCHW planes, any output size:
+// SegmentationHead(upsampling > 1) (:272-276) after the head conv's logits.  The backward is the
+// same gather as upsample2_ac_bwd_kernel (deterministic).
+__global__ void upsample_ac_planes_kernel(int64_t planes, int Hi, int Wi, int Ho, int Wo, float sh, float sw,
+                                          const float* __restrict__ x, float* __restrict__ y) {
+  const int64_t total = planes * Ho * Wo;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int ow = (int)(e % Wo);
+    int64_t p = e / Wo;
+    const int oh = (int)(p % Ho);
+    p /= Ho;
+    int h0, h1, w0, w1;
+    float lh0, lh1, lw0, lw1;
+    ac_axis(oh, Hi, sh, h0, h1, lh0, lh1);
+    ac_axis(ow, Wi, sw, w0, w1, lw0, lw1);
+    const float* xp = x + (size_t)p * Hi * Wi;
+    y[e] = lh0 * (lw0 * xp[h0 * Wi + w0] + lw1 * xp[h0 * Wi + w1]) + lh1 * (lw0 * xp[h1 * Wi + w0] + lw1 * xp[h1 * Wi + w1]);
+  }
+}
+
+__global__ void upsample_ac_planes_bwd_kernel(int64_t planes, int Hi, int Wi, int Ho, int Wo, float sh, float sw,
+                                              const float* __restrict__ dy, float* __restrict__ dx) {
+  const int64_t total = planes * Hi * Wi;
+  for (int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x; e < total; e += (int64_t)gridDim.x * 256) {
+    const int iw = (int)(e % Wi);
+    int64_t p = e / Wi;
+    const int ih = (int)(p % Hi);
+    p /= Hi;
+    int oh0, oh1, ow0, ow1;
+    ac_range(ih, Ho, sh, oh0, oh1);
+    ac_range(iw, Wo, sw, ow0, ow1);
+    const float* g = dy + (size_t)p * Ho * Wo;
+    float acc = 0.f;
+    for (int oh = oh0; oh <= oh1; ++oh) {
+      const float wh = ac_weight(oh, ih, Hi, sh);
+      if (wh == 0.f) continue;
+      for (int ow = ow0; ow <= ow1; ++ow) {
+        const float ww = ac_weight(ow, iw, Wi, sw);
+        if (ww != 0.f) acc += wh * ww * g[oh * Wo + ow];
+      }
+    }
+    dx[e] = acc;
+  }
+}
+
 // ------------------------------------------------------------ column copy (concat / split)
 template <typename T>
 __global__ void copy_cols_kernel(int64_t M, int ncols, const T* __restrict__ src, int lds, T* __restrict__ dst,
@@ -2133,6 +2178,26 @@ extern "C" int dfcsa_upsample2_ac_bwd(int dtype, int B, int C, int Hi, int Wi, c
   else
     hipLaunchKernelGGL(upsample2_ac_bwd_kernel<float>, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, B, C,
                        Hi, Wi, sh, sw, (const float*)dout, (float*)dx);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_upsample_ac_f32(int64_t planes, int Hi, int Wi, int Ho, int Wo, const float* x, float* out,
+                                     void* stream) {
+  if (planes <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) return DFCSA_EINVAL;
+  const int64_t total = planes * Ho * Wo;
+  hipLaunchKernelGGL(upsample_ac_planes_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, planes, Hi,
+                     Wi, Ho, Wo, ac_scale(Hi, Ho), ac_scale(Wi, Wo), x, out);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_upsample_ac_f32_bwd(int64_t planes, int Hi, int Wi, int Ho, int Wo, const float* dout, float* dx,
+                                         void* stream) {
+  if (planes <= 0 || Hi <= 0 || Wi <= 0 || Ho <= 0 || Wo <= 0) return DFCSA_EINVAL;
+  const int64_t total = planes * Hi * Wi;
+  hipLaunchKernelGGL(upsample_ac_planes_bwd_kernel, dim3(grid_for(total)), dim3(256), 0, (hipStream_t)stream, planes,
+                     Hi, Wi, Ho, Wo, ac_scale(Hi, Ho), ac_scale(Wi, Wo), dout, dx);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -410,13 +410,15 @@ class PatchEmbed(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, emb, dtype, p, rng, *params):
         conv, pos = emb.patch_embeddings, emb.position_embeddings
-        if conv.kernel_size != (1, 1) or conv.stride != (1, 1):
-            # the reference cannot run this either: patch size = img // 16 // grid > 1 gives
-            # (img / 16 / patch)^2 tokens but (img / 16)^2 position embeddings, and the add in
-            # Embeddings.forward fails (reference models/transformer_unet.py:175-199)
-            raise NotImplementedError("patch embeddings with patch size > 1 (img_size != 16 * grid) are not built "
-                                      "(the reference's position-embedding add fails for them as well)")
         B, h, w, Cin = x.shape
+        if conv.kernel_size != (1, 1) or conv.stride != (1, 1):
+            # patch size = img // 16 // grid > 1: the reference's patch conv gives (h / p) x (w / p)
+            # tokens against (img / 16)^2 position embeddings, and its `x + position_embeddings`
+            # (models/transformer_unet.py:179-181,196) raises this broadcast error at forward
+            # (tests/golden/transunet_patch2_error.json, recorded from the reference)
+            ntok = (h // conv.kernel_size[0]) * (w // conv.kernel_size[1])
+            raise RuntimeError(f"The size of tensor a ({ntok}) must match the size of tensor b ({pos.shape[1]}) "
+                               f"at non-singleton dimension 1")
         D = conv.out_channels
         if pos.shape[1] != h * w:
             raise ValueError(f"position embeddings for {pos.shape[1]} patches, grid has {h * w}")
@@ -697,6 +699,28 @@ class ConcatC(torch.autograd.Function):
         call("dfcsa_copy_cols", dt(ctx.dtype), M, Ca, P(g), Ca + Cb, P(da), Ca, 0, stream())
         call("dfcsa_copy_cols", dt(ctx.dtype), M, Cb, g.data_ptr() + Ca * es, Ca + Cb, P(db), Cb, 0, stream())
         return da, db, None
+
+
+class UpsampleAC(torch.autograd.Function):
+    """nn.UpsamplingBilinear2d(scale_factor) (align_corners=True) of fp32 NCHW logits: the
+    SegmentationHead's upsampling > 1 (:272-276).  Output size floor(H * s) as F.interpolate."""
+
+    @staticmethod
+    def forward(ctx, x, scale):
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        Ho, Wo = int(math.floor(H * float(scale))), int(math.floor(W * float(scale)))
+        out = _f32((B, C, Ho, Wo), x.device)
+        call("dfcsa_upsample_ac_f32", B * C, H, W, Ho, Wo, P(x), P(out), stream())
+        ctx.geom = (B, C, H, W, Ho, Wo)
+        return out
+
+    @staticmethod
+    def backward(ctx, g):
+        B, C, H, W, Ho, Wo = ctx.geom
+        dx = _f32((B, C, H, W), g.device)
+        call("dfcsa_upsample_ac_f32_bwd", B * C, H, W, Ho, Wo, P(g.contiguous()), P(dx), stream())
+        return dx, None
 
 
 class SegHead3x3(torch.autograd.Function):

@@ -31,7 +31,7 @@ from dfcsa._lib import call
 from dfcsa.flat import ALIGN, FlatParams
 from dfcsa.ops import P, rup, stream
 from dfcsa.transunet_ops import (Bottleneck, ConcatC, ConvBNReLU, LayerNormOut, MaxPool3x3s2, PatchEmbed, RootStem,
-                                 SegHead3x3, StdWeights, Upsample2x, ViTBlock)
+                                 SegHead3x3, StdWeights, Upsample2x, UpsampleAC, ViTBlock)
 
 
 class ConfigDict(dict):
@@ -226,13 +226,26 @@ class DecoderBlock(nn.Module):
 
 
 class SegmentationHead(nn.Sequential):
+    """conv 3x3 (+bias) then, for upsampling > 1, nn.UpsamplingBilinear2d(upsampling)
+    (reference :272-276; the reference's TransUNet builds it with upsampling = 1).  Standalone
+    calls take NCHW float input and run the head conv and the upsample on the HIP kernels."""
+
     def __init__(self, in_channels, out_channels, kernel_size=3, upsampling=1):
         conv2d = nn.Conv2d(in_channels, out_channels, kernel_size=kernel_size, padding=kernel_size // 2)
-        if upsampling > 1:
-            # the reference's TransUNet builds its head with the default upsampling = 1
-            # (reference models/transformer_unet.py:355-358); only a standalone head could ask for more
-            raise NotImplementedError("SegmentationHead upsampling > 1 is not built (TransUNet uses 1)")
-        super().__init__(conv2d, nn.Identity())
+        upsampling_m = nn.UpsamplingBilinear2d(scale_factor=upsampling) if upsampling > 1 else nn.Identity()
+        super().__init__(conv2d, upsampling_m)
+        self.upsampling = upsampling
+
+    def upsample(self, logits):
+        """The head's upsampling stage on fp32 NCHW logits (identity at upsampling = 1)."""
+        return UpsampleAC.apply(logits, self.upsampling) if self.upsampling > 1 else logits
+
+    def forward(self, x):
+        if not x.is_cuda:
+            raise RuntimeError("SegmentationHead runs on the MI355X kernels only; move it and its input to 'cuda'")
+        conv = self[0]
+        xn = x.to(torch.float32).permute(0, 2, 3, 1).contiguous()
+        return self.upsample(SegHead3x3.apply(xn, conv, torch.float32, *conv.parameters()))
 
 
 class DecoderCup(nn.Module):
@@ -347,7 +360,7 @@ class TransUNet(nn.Module):
         t = LayerNormOut.apply(t, enc, dtype, *enc.parameters())
         y = self.decoder.forward_nhwc(t, features, dtype)
         head = self.segmentation_head[0]
-        logits = SegHead3x3.apply(y, head, dtype, *head.parameters())
+        logits = self.segmentation_head.upsample(SegHead3x3.apply(y, head, dtype, *head.parameters()))
         if not planned:
             packs.rebuild_model_plan(self, x.device)
         return logits

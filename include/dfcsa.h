@@ -702,6 +702,12 @@ int dfcsa_mha_drop_bwd(int dtype, int B, int N, int heads, int dh, int ldq, floa
  * bwd is a deterministic gather into dx [B][Hi][Wi][C] */
 int dfcsa_upsample2_ac(int dtype, int B, int C, int Hi, int Wi, const void* x, void* out, void* stream);
 int dfcsa_upsample2_ac_bwd(int dtype, int B, int C, int Hi, int Wi, const void* dout, void* dx, void* stream);
+/* nn.UpsamplingBilinear2d(scale_factor) (align_corners=True) on fp32 NCHW planes [planes][Hi][Wi] ->
+ * [planes][Ho][Wo], Ho = floor(Hi * s): SegmentationHead(upsampling > 1) (reference
+ * models/transformer_unet.py:272-276) after the head conv.  The backward gathers (deterministic). */
+int dfcsa_upsample_ac_f32(int64_t planes, int Hi, int Wi, int Ho, int Wo, const float* x, float* out, void* stream);
+int dfcsa_upsample_ac_f32_bwd(int64_t planes, int Hi, int Wi, int Ho, int Wo, const float* dout, float* dx,
+                              void* stream);
 /* dst[m][j] (+)= src[m][j], j < ncols (row strides ld_src / ld_dst): channel concat / split */
 int dfcsa_copy_cols(int dtype, int64_t M, int ncols, const void* src, int ld_src, void* dst, int ld_dst,
                     int accumulate, void* stream);

@@ -548,6 +548,56 @@ def _zoo_model(name):
     return cls(3, 1, [8, 16, 32, 64], 4)
 
 
+def gen_transunet_edges():
+    """Reference behaviour off the shipped TransUNet configuration (VERDICT r4 "missing" 1-2):
+    (a) patch size 2 (img = 2 x 16 x grid): the reference constructs the model, then its forward
+    raises at the position-embedding add -> transunet_patch2_error.json (exception type, message,
+    patch kernel, position-embedding shape);
+    (b) SegmentationHead(upsampling = 2, 3) standalone: conv 3x3 + UpsamplingBilinear2d on a
+    seeded input, forward and input/weight gradients of sum(out * w) -> seghead_up.npz."""
+    import json
+    tu = _transunet_module()
+    c = TRANSUNET_SMALL
+    cfg = tu.get_r50_b16_config()
+    img = 2 * c["img"]
+    cfg.patches.grid = (c["img"] // 16, c["img"] // 16)
+    cfg.resnet.num_layers = c["num_layers"]
+    cfg.resnet.width_factor = c["width_factor"]
+    cfg.hidden_size = c["hidden"]
+    cfg.transformer.mlp_dim = c["mlp"]
+    cfg.transformer.num_heads = c["heads"]
+    cfg.transformer.num_layers = c["layers"]
+    cfg.decoder_channels = c["decoder"]
+    cfg.skip_channels = list(c["skip"])
+    cfg.n_classes = 1
+    torch.manual_seed(7500)
+    model = tu.TransUNet(cfg, img_size=img, num_classes=1)
+    e = model.transformer.embeddings
+    rec = {"img": img, "grid": list(cfg.patches.grid), "patch_kernel": list(e.patch_embeddings.kernel_size),
+           "position_embeddings": list(e.position_embeddings.shape), "config": dict(c)}
+    try:
+        with torch.no_grad():
+            model(torch.randn(1, 3, img, img))
+        rec["raised"] = None
+    except Exception as ex:   # the reference's own failure, recorded as data
+        rec["raised"] = {"type": type(ex).__name__, "message": str(ex)}
+    with open(os.path.join(OUT, "transunet_patch2_error.json"), "w") as f:
+        json.dump(rec, f, indent=1)
+    print("patch2:", rec["raised"])
+    arrays = {}
+    for up in (2, 3):
+        torch.manual_seed(7600 + up)
+        head = tu.SegmentationHead(16, 2, kernel_size=3, upsampling=up)
+        x = torch.randn(2, 16, 7, 9, requires_grad=True)
+        out = head(x)
+        w = torch.randn(out.shape)
+        (out * w).sum().backward()
+        arrays.update({f"up{up}_x": np32(x), f"up{up}_w": np32(w), f"up{up}_conv_w": np32(head[0].weight),
+                       f"up{up}_conv_b": np32(head[0].bias), f"up{up}_out": np32(out), f"up{up}_dx": np32(x.grad),
+                       f"up{up}_dconv_w": np32(head[0].weight.grad), f"up{up}_dconv_b": np32(head[0].bias.grad)})
+    save("seghead_up.npz", **arrays)
+
+
 def gen_zoo():
     for i, name in enumerate(ZOO):
         torch.manual_seed(9100 + i)

@@ -535,3 +535,28 @@ def test_rank_sharded_loader_partitions_global_batches():
     ld = RankShardedLoader(DS(), 5, 0, world, seed=3)
     ld.set_epoch(1)
     assert ld.global_batches() != e0
+
+
+def test_transunet_off_config_modules_match_reference():
+    """Off-config TransUNet pieces build the reference's module tree on the host: patch size 2
+    (img = 2 x 16 x grid) gives the patch conv and position embeddings the reference records in
+    tests/golden/transunet_patch2_error.json (its forward then raises there and here, the GPU test);
+    SegmentationHead(upsampling > 1) holds conv + UpsamplingBilinear2d with the reference's keys and
+    refuses a CPU tensor (no CPU fallback)."""
+    import json
+    from models.transformer_unet import SegmentationHead, TransUNet
+    from test_oracle_golden import transunet_small_config
+    rec = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "transunet_patch2_error.json")))
+    assert rec["raised"]["type"] == "RuntimeError"
+    m = TransUNet(transunet_small_config(), img_size=rec["img"], num_classes=1)
+    e = m.transformer.embeddings
+    assert list(e.patch_embeddings.kernel_size) == rec["patch_kernel"]
+    assert list(e.position_embeddings.shape) == rec["position_embeddings"]
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "seghead_up.npz"))
+    for up in (2, 3):
+        h = SegmentationHead(16, 2, kernel_size=3, upsampling=up)
+        assert isinstance(h[1], torch.nn.UpsamplingBilinear2d) and h[1].scale_factor == up
+        assert sorted(h.state_dict()) == ["0.bias", "0.weight"]
+        assert tuple(h[0].weight.shape) == fx[f"up{up}_conv_w"].shape
+        with pytest.raises(RuntimeError):
+            h(torch.zeros(1, 16, 4, 4))

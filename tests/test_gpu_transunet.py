@@ -476,3 +476,56 @@ def test_colsum_fused(M, C, n0, n1, dtype):
         outs.append(torch.cat(d))
     assert (outs[0].double() - 0.5 - ref).abs().max().item() <= 1e-4 * max(1.0, ref.abs().max().item())
     assert torch.equal(outs[0], outs[1])
+
+
+# ----------------------------------------------------------------------------- off-config edges
+def test_transunet_patch_size_2_raises_like_reference():
+    """img = 2 x 16 x grid (patch size 2): the reference builds the model and its forward raises
+    the position-embedding broadcast error (tests/golden/transunet_patch2_error.json, recorded from
+    reference models/transformer_unet.py:179-181,196); ours raises the same type and message."""
+    import json
+    from models.transformer_unet import TransUNet
+    from test_oracle_golden import transunet_small_config
+    rec = json.load(open(os.path.join(GOLDEN, "transunet_patch2_error.json")))
+    m = TransUNet(transunet_small_config(), img_size=rec["img"], num_classes=1, precision="fp32").cuda().train()
+    assert list(m.transformer.embeddings.patch_embeddings.kernel_size) == rec["patch_kernel"]
+    with pytest.raises(RuntimeError) as ei:
+        m(torch.randn(1, 3, rec["img"], rec["img"], device="cuda"))
+    assert type(ei.value).__name__ == rec["raised"]["type"] and str(ei.value) == rec["raised"]["message"]
+
+
+@pytest.mark.parametrize("up", [2, 3])
+def test_segmentation_head_upsampling_matches_reference(up):
+    """SegmentationHead(upsampling > 1) standalone (reference :272-276): conv 3x3 + bias, then
+    UpsamplingBilinear2d(up) (align_corners), forward and gradients against the reference's fp32
+    CPU run (tests/golden/seghead_up.npz)."""
+    from models.transformer_unet import SegmentationHead
+    fx = np.load(os.path.join(GOLDEN, "seghead_up.npz"))
+    k = f"up{up}_"
+    head = SegmentationHead(16, 2, kernel_size=3, upsampling=up).cuda()
+    with torch.no_grad():
+        head[0].weight.copy_(T(fx[k + "conv_w"]))
+        head[0].bias.copy_(T(fx[k + "conv_b"]))
+    x = T(fx[k + "x"]).requires_grad_(True)
+    out = head(x)
+    assert tuple(out.shape) == fx[k + "out"].shape
+    assert rel(out, fx[k + "out"]) < 1e-5
+    (out * T(fx[k + "w"])).sum().backward()
+    assert rel(x.grad, fx[k + "dx"]) < 1e-5
+    assert rel(head[0].weight.grad, fx[k + "dconv_w"]) < 1e-5
+    assert rel(head[0].bias.grad, fx[k + "dconv_b"]) < 1e-5
+
+
+@pytest.mark.parametrize("H,W,s", [(7, 9, 2), (14, 14, 4), (5, 8, 3), (1, 6, 2)])
+def test_upsample_ac_planes_vs_torch(H, W, s):
+    """dfcsa_upsample_ac_f32(_bwd) against torch's UpsamplingBilinear2d (fp32, align_corners)."""
+    x = torch.randn(3, 5, H, W, device="cuda", requires_grad=True)
+    from dfcsa.transunet_ops import UpsampleAC
+    y = UpsampleAC.apply(x, s)
+    xr = x.detach().clone().requires_grad_(True)
+    yr = torch.nn.UpsamplingBilinear2d(scale_factor=s)(xr)
+    assert y.shape == yr.shape and rel(y, yr) < 1e-6
+    g = torch.randn_like(yr)
+    y.backward(g)
+    yr.backward(g)
+    assert rel(x.grad, xr.grad) < 1e-6
