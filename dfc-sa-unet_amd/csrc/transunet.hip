@@ -1495,6 +1495,7 @@ __global__ void copy_cols_kernel(int64_t M, int ncols, const T* __restrict__ src
 // ------------------------------------------------------------ 3x3 segmentation head (+bias)
 // logits NCHW fp32 [B][Cout][H][W] = bias + conv3x3(x) (x NHWC dtype [B][H][W][C], C <= 64, Cout <= 4)
 constexpr int HEAD3_MAXW = 4 * 64 * 9;
+constexpr int HEAD3_XS = 12288;  // staged halo floats of head3_bwd (48 KB: 16 channels x 768 pixels, W <= 255)
 
 template <typename T>
 __global__ void __launch_bounds__(256) head3_fwd_kernel(int B, int H, int W, int C, int Cout,
@@ -1571,20 +1572,60 @@ __global__ void __launch_bounds__(256) head3_bwd_kernel(int B, int H, int W, int
       store8<T>(dx + (size_t)m * C + c0, acc);
     }
   }
-  // weight / bias partials for this tile
+  // weight / bias partials for this tile.  The tile's pixels with their +-(W+1) halo (one linear
+  // range of NHWC rows: an in-image 3x3 neighbour of linear pixel m is m + dh*W + dw) are staged in
+  // LDS as fp32, with each pixel's 9-bit in-image tap mask, so the (o, c, tap) threads walk the 256
+  // pixels from LDS (a strided global load per pixel made this loop the whole kernel's time).
   const int64_t m0 = (int64_t)blockIdx.x * 256;
   const int np = (int)std::min<int64_t>(256, M - m0);
   const int nw = Cout * C * 9;
+  __shared__ float xs[HEAD3_XS];
+  __shared__ unsigned short tmask[256];
+  const int64_t L0 = std::max<int64_t>(0, m0 - W - 1), L1 = std::min<int64_t>(M, m0 + np + W + 1);
+  const bool staged = (L1 - L0) * C <= HEAD3_XS;
+  if (staged) {
+    const int cpp = C >> 3;
+    for (int64_t e = threadIdx.x; e < (L1 - L0) * cpp; e += 256) {
+      float v[8];
+      load8<T>(x + (L0 + e / cpp) * C + (e % cpp) * 8, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) xs[e * 8 + q] = v[q];
+    }
+    if ((int)threadIdx.x < np) {
+      const int64_t mm = m0 + threadIdx.x;
+      const int wq = (int)(mm % W), hq = (int)((mm / W) % H);
+      unsigned t = 0;
+      for (int tap = 0; tap < 9; ++tap) {
+        const int ih = hq + tap / 3 - 1, iw = wq + tap % 3 - 1;
+        t |= (unsigned)(ih >= 0 && ih < H && iw >= 0 && iw < W) << tap;
+      }
+      tmask[threadIdx.x] = (unsigned short)t;
+    }
+    __syncthreads();
+  }
   for (int e = threadIdx.x; e < nw; e += 256) {
     const int o = e / (C * 9), r = e - o * C * 9, c = r / 9, tap = r - c * 9;
     const int dh = tap / 3 - 1, dw = tap % 3 - 1;
     float s = 0.f;
-    for (int pq = 0; pq < np; ++pq) {
-      const int64_t mm = m0 + pq;
-      const int wq = (int)(mm % W), hq = (int)((mm / W) % H), b = (int)(mm / HWn);
-      const int ih = hq + dh, iw = wq + dw;
-      if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
-      s += gs[o][pq] * ElemTraits<T>::to_f(x[(((size_t)b * H + ih) * W + iw) * C + c]);
+    if (staged) {
+      const float* xb = xs + (m0 + dh * W + dw - L0) * C + c;   // in range wherever the tap is in-image
+      float s4[4] = {0.f, 0.f, 0.f, 0.f};
+      int pq = 0;
+      for (; pq + 4 <= np; pq += 4)
+#pragma unroll
+        for (int u = 0; u < 4; ++u)
+          if ((tmask[pq + u] >> tap) & 1) s4[u] += gs[o][pq + u] * xb[(pq + u) * C];
+      for (; pq < np; ++pq)
+        if ((tmask[pq] >> tap) & 1) s4[0] += gs[o][pq] * xb[pq * C];
+      s = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+    } else {
+      for (int pq = 0; pq < np; ++pq) {
+        const int64_t mm = m0 + pq;
+        const int wq = (int)(mm % W), hq = (int)((mm / W) % H), b = (int)(mm / HWn);
+        const int ih = hq + dh, iw = wq + dw;
+        if (ih < 0 || ih >= H || iw < 0 || iw >= W) continue;
+        s += gs[o][pq] * ElemTraits<T>::to_f(x[(((size_t)b * H + ih) * W + iw) * C + c]);
+      }
     }
     pw[(size_t)blockIdx.x * nw + e] = s;
   }

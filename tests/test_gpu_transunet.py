@@ -344,12 +344,15 @@ def test_dropout_masks():
     assert torch.allclose(dx, ref, atol=1e-5)
 
 
+@pytest.mark.parametrize("B,H,W,C,Cout", [(2, 20, 24, 16, 1), (1, 37, 224, 16, 1), (1, 30, 100, 64, 3), (3, 9, 7, 8, 4)])
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
-def test_head3(dtype, tol):
+def test_head3(dtype, tol, B, H, W, C, Cout):
+    """3x3 segmentation head fwd/bwd vs torch fp32; (1, 30, 100, 64, 3) exceeds head3_bwd's LDS halo
+    staging (the global-load weight-partial path), the others take the staged path."""
     from dfcsa.transunet_ops import SegHead3x3
     torch.manual_seed(4)
-    conv = torch.nn.Conv2d(16, 1, 3, padding=1).cuda()
-    x = torch.randn(2, 20, 24, 16, device="cuda").to(dtype)
+    conv = torch.nn.Conv2d(C, Cout, 3, padding=1).cuda()
+    x = torch.randn(B, H, W, C, device="cuda").to(dtype)
     xr = x.float().permute(0, 3, 1, 2).clone().requires_grad_(True)
     yr = conv(xr)
     g = torch.randn_like(yr)
