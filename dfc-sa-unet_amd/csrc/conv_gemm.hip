@@ -2639,8 +2639,15 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
 #pragma unroll
   for (int j = 0; j < FN; ++j) {
     const int n = wave * NWC + j * 16 + (lane & 15);
-    if (lane < 32) args.stats[(size_t)blockIdx.x * 2 * C + (lane < 16 ? 0 : C) + n] = lane < 16 ? st_s[j] : st_q[j];
+    if (lane < 32) {
+      float* sp = args.stats + (size_t)blockIdx.x * 2 * C + (lane < 16 ? 0 : C) + n;
+      if (args.fold.on) st_sc1_dw(sp, lane < 16 ? st_s[j] : st_q[j]);   // read by the fold's last workgroups
+      else *sp = lane < 16 ? st_s[j] : st_q[j];
+    }
   }
+  // the BatchNorm of the C output columns finalised in the launch's tail (round 5): one
+  // statistics row per workgroup, one column block of C
+  if (args.fold.on) bn_fold_tail<256, C>(args.fold, args.stats, C, blockIdx.x, gridDim.x, 0, smem);
 }
 
 int g_stream_wgs = 0;   // workgroups per CU of the streaming kernel (0 = occupancy limit)
@@ -2924,6 +2931,36 @@ extern "C" int dfcsa_conv_gemm(const dfcsa_conv_desc* d, void* stream) {
 
 int g_bn_fold = 1;   // knob 39: 0 = never fold the BatchNorm finalisation into the conv epilogue
 
+// BnFold of a launch with `rows` statistics rows and fold column width cw (tickets and hand-off
+// scratch from the shared rings); false when the fold is off or the rings cannot serve it
+static bool make_fold(const dfcsa_bn_fold* f, int rows, int cw, BnFold& b) {
+  std::memset(&b, 0, sizeof(b));
+  if (!g_bn_fold || cw <= 0 || rows <= 0) return false;
+  b.C = f->C;
+  b.cw = cw;
+  b.GS = 1;
+  while ((int64_t)b.GS * b.GS < rows) ++b.GS;          // ~sqrt(T) rows per group, ~sqrt(T) groups
+  b.ng = (rows + b.GS - 1) / b.GS;
+  b.ncb = (f->C + cw - 1) / cw;
+  b.cnt = dfcsa_ticket_alloc(b.ncb * b.ng + b.ncb);
+  b.scr = dfcsa_scratch_alloc((int64_t)b.ncb * b.ng * 2 * cw);
+  if (!b.cnt || !b.scr) {
+    std::memset(&b, 0, sizeof(b));
+    return false;
+  }
+  b.on = 1;
+  b.count = f->count; b.bias = f->conv_bias; b.gamma = f->gamma; b.beta = f->beta;
+  b.rmean = f->running_mean; b.rvar = f->running_var; b.nbt = f->num_batches_tracked;
+  b.momentum = f->momentum; b.eps = f->eps;
+  b.scale = f->scale; b.shift = f->shift; b.mean = f->mean; b.invstd = f->invstd;
+  return true;
+}
+
+static bool fold_args_ok(const dfcsa_bn_fold* f) {
+  return f && f->C > 0 && f->count > 0 && f->gamma && f->beta && f->running_mean && f->running_var && f->scale &&
+         f->shift && f->mean && f->invstd;
+}
+
 extern "C" int dfcsa_conv_gemm_bn(const dfcsa_conv_desc* d, const dfcsa_bn_fold* f, void* stream) {
   if (!d || !f || !d->stats || f->C <= 0 || f->C > d->N || f->count <= 0 || !f->gamma || !f->beta ||
       !f->running_mean || !f->running_var || !f->scale || !f->shift || !f->mean || !f->invstd)
@@ -2932,28 +2969,8 @@ extern "C" int dfcsa_conv_gemm_bn(const dfcsa_conv_desc* d, const dfcsa_bn_fold*
   int rows = 0;
   if (const int rc = desc_args(d, a, &rows)) return rc;
   if ((int64_t)rows * 2 * d->N > d->stats_floats) return DFCSA_EINVAL;
-  const int cw = t_fold_cw;
   hipStream_t st = (hipStream_t)stream;
-  if (g_bn_fold && cw > 0 && rows > 0) {
-    BnFold& b = a.fold;
-    b.C = f->C;
-    b.cw = cw;
-    b.GS = 1;
-    while ((int64_t)b.GS * b.GS < rows) ++b.GS;          // ~sqrt(T) rows per group, ~sqrt(T) groups
-    b.ng = (rows + b.GS - 1) / b.GS;
-    b.ncb = (f->C + cw - 1) / cw;
-    b.cnt = dfcsa_ticket_alloc(b.ncb * b.ng + b.ncb);
-    b.scr = dfcsa_scratch_alloc((int64_t)b.ncb * b.ng * 2 * cw);
-    if (b.cnt && b.scr) {
-      b.on = 1;
-      b.count = f->count; b.bias = f->conv_bias; b.gamma = f->gamma; b.beta = f->beta;
-      b.rmean = f->running_mean; b.rvar = f->running_var; b.nbt = f->num_batches_tracked;
-      b.momentum = f->momentum; b.eps = f->eps;
-      b.scale = f->scale; b.shift = f->shift; b.mean = f->mean; b.invstd = f->invstd;
-      return conv_launch(d, a, st);
-    }
-    std::memset(&b, 0, sizeof(b));
-  }
+  if (make_fold(f, rows, t_fold_cw, a.fold)) return conv_launch(d, a, st);
   // the picked kernel cannot fold (streaming / halo-tile kernels): conv, then the finalize launch
   if (const int rc = conv_launch(d, a, st)) return rc;
   return dfcsa_bn_finalize(d->stats, rows, f->C, d->N, f->count, f->conv_bias, f->gamma, f->beta, f->running_mean,
@@ -3119,11 +3136,19 @@ int fwd_pro_grid(int M) {
 }
 
 template <int PRO, int C>
-int launch_fwd_pro(const ConvGemmArgs& a, const FwdPro& pro, int64_t stats_cap, hipStream_t st) {
+int launch_fwd_pro(ConvGemmArgs& a, const FwdPro& pro, int64_t stats_cap, hipStream_t st,
+                   const dfcsa_bn_fold* f = nullptr) {
   const int mtiles = (a.M + 63) / 64;
   const int gx = fwd_pro_grid<PRO, C>(a.M);
   // one [2][C] statistics row per workgroup: refuse a slab shorter than the grid
   if ((int64_t)gx * 2 * C > stats_cap) return DFCSA_EINVAL;
+  if (f && !make_fold(f, gx, C, a.fold)) {
+    // fold off or no ring space: the launch, then the finalize
+    if (const int rc = launch_fwd_pro<PRO, C>(a, pro, stats_cap, st)) return rc;
+    return dfcsa_bn_finalize(a.stats, gx, f->C, C, f->count, f->conv_bias, f->gamma, f->beta, f->running_mean,
+                             f->running_var, f->num_batches_tracked, f->momentum, f->eps, 1, f->scale, f->shift,
+                             f->mean, f->invstd, st);
+  }
   const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + (double)C * a.Kpad + moved * a.M * C));
   hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
@@ -3141,9 +3166,10 @@ extern "C" int dfcsa_fwd_pro_parts(int M, int C, int pro) {
   return DFCSA_EINVAL;
 }
 
-extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
-                                     const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
-                                     void* fused, void* y4, float* stats4, int64_t stats4_floats, void* stream) {
+static int gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
+                           const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
+                           float* stats4, int64_t stats4_floats, void* stream, const dfcsa_bn_fold* f) {
+  if (f && (!fold_args_ok(f) || f->C != C)) return DFCSA_EINVAL;
   if (M <= 0 || (C != 64 && C != 128) || Kpad != 3 * C || !y3 || !sc3 || !sh3 || !local || !attn || !w4 || !fused ||
       !y4 || !stats4)
     return DFCSA_EINVAL;
@@ -3155,15 +3181,30 @@ extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* 
   FwdPro pro;
   std::memset(&pro, 0, sizeof(pro));
   pro.sc0 = sc3; pro.sh0 = sh3; pro.out0 = (bf16_t*)fused;
-  return C == 64 ? launch_fwd_pro<PRO_GATE_FUSION, 64>(a, pro, stats4_floats, (hipStream_t)stream)
-                 : launch_fwd_pro<PRO_GATE_FUSION, 128>(a, pro, stats4_floats, (hipStream_t)stream);
+  return C == 64 ? launch_fwd_pro<PRO_GATE_FUSION, 64>(a, pro, stats4_floats, (hipStream_t)stream, f)
+                 : launch_fwd_pro<PRO_GATE_FUSION, 128>(a, pro, stats4_floats, (hipStream_t)stream, f);
 }
 
-extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1,
-                                         const float* sh1, const void* y2, const float* sc2, const float* sh2,
-                                         const float* o, int P, const float* gamma, const void* w3, int Kpad,
-                                         const float* b3, void* local, void* attn, void* y3, float* stats3, int64_t stats3_floats,
-                                         void* stream) {
+extern "C" int dfcsa_gate_fusion_fwd(int M, int C, const void* y3, const float* sc3, const float* sh3,
+                                     const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
+                                     void* fused, void* y4, float* stats4, int64_t stats4_floats, void* stream) {
+  return gate_fusion_fwd(M, C, y3, sc3, sh3, local, attn, w4, Kpad, b4, fused, y4, stats4, stats4_floats, stream,
+                         nullptr);
+}
+
+extern "C" int dfcsa_gate_fusion_fwd_bn(int M, int C, const void* y3, const float* sc3, const float* sh3,
+                                        const void* local, const void* attn, const void* w4, int Kpad, const float* b4,
+                                        void* fused, void* y4, float* stats4, int64_t stats4_floats,
+                                        const dfcsa_bn_fold* f, void* stream) {
+  if (!f) return DFCSA_EINVAL;
+  return gate_fusion_fwd(M, C, y3, sc3, sh3, local, attn, w4, Kpad, b4, fused, y4, stats4, stats4_floats, stream, f);
+}
+
+static int local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
+                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,
+                               const float* gamma, const void* w3, int Kpad, const float* b3, void* local, void* attn,
+                               void* y3, float* stats3, int64_t stats3_floats, void* stream, const dfcsa_bn_fold* f) {
+  if (f && (!fold_args_ok(f) || f->C != C)) return DFCSA_EINVAL;
   const int64_t M = (int64_t)B * H * W;
   if (M <= 0 || M >= (1ll << 31) || (C != 64 && C != 128) || Kpad != 2 * C || P <= 0 || !y1 || !sc1 || !sh1 || !y2 || !sc2 ||
       !sh2 || !o || !gamma || !w3 || !local || !attn || !y3 || !stats3)
@@ -3180,8 +3221,27 @@ extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void*
   pro.dm_hw = make_divmod(H * W); pro.dm_w = make_divmod(W);
   pro.sh = (float)P / (float)H; pro.sw = (float)P / (float)W;
   pro.out0 = (bf16_t*)local; pro.out1 = (bf16_t*)attn;
-  return C == 64 ? launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream)
-                 : launch_fwd_pro<PRO_LOCAL_ATTN, 128>(a, pro, stats3_floats, (hipStream_t)stream);
+  return C == 64 ? launch_fwd_pro<PRO_LOCAL_ATTN, 64>(a, pro, stats3_floats, (hipStream_t)stream, f)
+                 : launch_fwd_pro<PRO_LOCAL_ATTN, 128>(a, pro, stats3_floats, (hipStream_t)stream, f);
+}
+
+extern "C" int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const float* sc1,
+                                         const float* sh1, const void* y2, const float* sc2, const float* sh2,
+                                         const float* o, int P, const float* gamma, const void* w3, int Kpad,
+                                         const float* b3, void* local, void* attn, void* y3, float* stats3, int64_t stats3_floats,
+                                         void* stream) {
+  return local_attn_gate_fwd(B, H, W, C, y1, sc1, sh1, y2, sc2, sh2, o, P, gamma, w3, Kpad, b3, local, attn, y3,
+                             stats3, stats3_floats, stream, nullptr);
+}
+
+extern "C" int dfcsa_local_attn_gate_fwd_bn(int B, int H, int W, int C, const void* y1, const float* sc1,
+                                            const float* sh1, const void* y2, const float* sc2, const float* sh2,
+                                            const float* o, int P, const float* gamma, const void* w3, int Kpad,
+                                            const float* b3, void* local, void* attn, void* y3, float* stats3,
+                                            int64_t stats3_floats, const dfcsa_bn_fold* f, void* stream) {
+  if (!f) return DFCSA_EINVAL;
+  return local_attn_gate_fwd(B, H, W, C, y1, sc1, sh1, y2, sc2, sh2, o, P, gamma, w3, Kpad, b3, local, attn, y3,
+                             stats3, stats3_floats, stream, f);
 }
 
 extern "C" int dfcsa_conv_gemm_mtile(int N) { (void)N; return 64; }

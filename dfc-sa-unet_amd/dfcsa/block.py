@@ -19,6 +19,7 @@ Activation flow per block (NHWC, dtype T; M = B*H*W pixels; C = out channels):
   GEMM 1x1            [fused, local, attn] -> y4 (+bias, BN4 stats)
   EW                  out = relu(bn4 y4) + res_scale * res
 """
+import ctypes
 import os
 
 import torch
@@ -194,9 +195,14 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # the local/attention merge runs in the gate conv's A-operand prologue (one statistics row
         # per workgroup)
         nt3 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 1)
-        call("dfcsa_local_attn_gate_fwd", B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2), P(bn2.scale),
-             P(bn2.shift), P(o), Pp, P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), *S(st3),
-             stream())
+        args3 = (B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2), P(bn2.scale), P(bn2.shift), P(o), Pp,
+                 P(lsa.gamma), P(W3p), Kp3, P(conv3.bias), P(local), P(attn), P(y3), *S(st3))
+        if fold:   # BN3 finalised in the launch's tail
+            f3, bn3f = ops.bn_fold_desc(bn3m, conv3.bias, C, M)
+            call("dfcsa_local_attn_gate_fwd_bn", *args3, ctypes.addressof(f3), stream())
+            nt3 = (nt3, bn3f)
+        else:
+            call("dfcsa_local_attn_gate_fwd", *args3, stream())
     else:
         if not fullres:
             call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, P(y1), P(bn1.scale), P(bn1.shift), P(y2),
@@ -216,8 +222,14 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
         # the gate fusion runs in the fusion conv's A-operand prologue (dfcsa_gate_fusion_fwd; one
         # statistics row per workgroup)
         nt4 = _lib.LIB.dfcsa_fwd_pro_parts(M, C, 0)
-        call("dfcsa_gate_fusion_fwd", M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4,
-             P(conv4.bias), P(fused), P(y4), *S(st4), stream())
+        args4 = (M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(W4p), Kp4, P(conv4.bias), P(fused),
+                 P(y4), *S(st4))
+        if fold:   # BN4 finalised in the launch's tail
+            f4, bn4f = ops.bn_fold_desc(bn4m, conv4.bias, C, M)
+            call("dfcsa_gate_fusion_fwd_bn", *args4, ctypes.addressof(f4), stream())
+            nt4 = (nt4, bn4f)
+        else:
+            call("dfcsa_gate_fusion_fwd", *args4, stream())
     else:
         call("dfcsa_gate_fuse", dt(dtype), M, C, P(y3), P(bn3.scale), P(bn3.shift), P(local), P(attn), P(fused),
              stream())

@@ -105,21 +105,28 @@ def conv_gemm(dtype, segs, Cseg, grid, in_hw, weight, Kpad, N, dests, Nd, bias=N
             d.work, d.work_floats = P(work), wf
     if bn is not None:
         bn_mod, conv_bias, C = bn
-        st = BNState(C, bn_mod.weight.device)
-        f = _lib.BnFold()
-        f.C, f.count = C, d.M
-        f.conv_bias, f.gamma, f.beta = P(conv_bias), P(bn_mod.weight), P(bn_mod.bias)
-        f.running_mean, f.running_var = P(bn_mod.running_mean), P(bn_mod.running_var)
-        f.num_batches_tracked = P(bn_mod.num_batches_tracked)
-        f.momentum = float(bn_mod.momentum if bn_mod.momentum is not None else 0.1)
-        f.eps = float(bn_mod.eps)
-        f.scale, f.shift, f.mean, f.invstd = P(st.scale), P(st.shift), P(st.mean), P(st.invstd)
+        f, st = bn_fold_desc(bn_mod, conv_bias, C, d.M)
         call("dfcsa_conv_gemm_bn", ctypes.addressof(d), ctypes.addressof(f), stream())
         return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d)), st
     call("dfcsa_conv_gemm", ctypes.addressof(d), stream())
     if stats is not None:   # statistics rows written (the ntiles of bn_finalize)
         return _lib.LIB.dfcsa_conv_stats_rows(ctypes.addressof(d))
     return None
+
+
+def bn_fold_desc(bn_mod, conv_bias, C, count):
+    """(dfcsa_bn_fold, BNState): the train-mode BatchNorm of C channels over `count` values that a
+    producing launch finalises in its tail (dfcsa_conv_gemm_bn, dfcsa_*_fwd_bn)."""
+    st = BNState(C, bn_mod.weight.device)
+    f = _lib.BnFold()
+    f.C, f.count = C, count
+    f.conv_bias, f.gamma, f.beta = P(conv_bias), P(bn_mod.weight), P(bn_mod.bias)
+    f.running_mean, f.running_var = P(bn_mod.running_mean), P(bn_mod.running_var)
+    f.num_batches_tracked = P(bn_mod.num_batches_tracked)
+    f.momentum = float(bn_mod.momentum if bn_mod.momentum is not None else 0.1)
+    f.eps = float(bn_mod.eps)
+    f.scale, f.shift, f.mean, f.invstd = P(st.scale), P(st.shift), P(st.mean), P(st.invstd)
+    return f, st
 
 
 def bn_fold_ok(training):

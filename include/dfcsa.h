@@ -354,6 +354,18 @@ int dfcsa_local_attn_gate_fwd(int B, int H, int W, int C, const void* y1, const 
                               const void* y2, const float* sc2, const float* sh2, const float* o, int P,
                               const float* gamma, const void* w3, int Kpad, const float* b3, void* local,
                               void* attn, void* y3, float* stats3, int64_t stats3_floats, void* stream);
+/* The two prologue GEMMs above with their BatchNorm finalised in the launch's tail (round 5; the
+ * fold of dfcsa_conv_gemm_bn: f->C == C, the statistics rows are the workgroups).  With the fold
+ * off (tuning knob 39) or no ticket space they launch dfcsa_bn_finalize after the GEMM instead.
+ * Outputs f->scale/shift/mean/invstd and the running statistics as dfcsa_bn_finalize (training). */
+int dfcsa_gate_fusion_fwd_bn(int M, int C, const void* y3, const float* sc3, const float* sh3, const void* local,
+                             const void* attn, const void* w4, int Kpad, const float* b4, void* fused, void* y4,
+                             float* stats4, int64_t stats4_floats, const dfcsa_bn_fold* f, void* stream);
+int dfcsa_local_attn_gate_fwd_bn(int B, int H, int W, int C, const void* y1, const float* sc1, const float* sh1,
+                                 const void* y2, const float* sc2, const float* sh2, const float* o, int P,
+                                 const float* gamma, const void* w3, int Kpad, const float* b3, void* local,
+                                 void* attn, void* y3, float* stats3, int64_t stats3_floats,
+                                 const dfcsa_bn_fold* f, void* stream);
 /* dfcsa_dgrad_gate / dfcsa_dgrad_acc_relu_bn at C == 64 with the BatchNorm-backward apply of their
  * A operand in a prologue: dy4 = gamma4*invstd4*(dz4 - coef4[0] - xh4*coef4[1]) with dz4 =
  * dout*(y4*sc4+sh4 > 0) (dfcsa_bn_bwd_apply_relu; sc4 = sh4 = NULL: dz4 = dout) and dy3 likewise from

@@ -137,3 +137,75 @@ def test_stream_k_pingpong_conv(B, H, Cs, nsrc, N, taps):
     assert ((st[0] - ref.double().sum((0, 2, 3))).norm() / ref.double().sum((0, 2, 3)).norm()).item() < 1e-4
     assert ((sc1 - sc0).abs().max() / sc0.abs().max()).item() < 1e-4
     assert ((sh1 - sh0).abs().max() / sh0.abs().max().clamp_min(1e-6)).item() < 1e-3
+
+
+def _bn_module(C):
+    bn = torch.nn.BatchNorm2d(C).cuda()
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-0.1, 0.1)
+        bn.running_var.uniform_(0.9, 1.1)
+    return bn
+
+
+def _run_pro(pro, B, H, C, fold, seed=0):
+    """dfcsa_gate_fusion_fwd_bn (pro 0) / dfcsa_local_attn_gate_fwd_bn (pro 1) with knob 39 = fold."""
+    import ctypes
+
+    import dfcsa
+    from dfcsa import _lib, ops
+    from dfcsa._lib import call
+    from dfcsa.ops import P, S, stream
+    torch.manual_seed(seed)
+    bf = torch.bfloat16
+    M = B * H * H
+    r = lambda *s: (torch.randn(*s, device="cuda") * 0.5).to(bf)   # noqa: E731
+    f = lambda *s: torch.randn(*s, device="cuda") * 0.3            # noqa: E731
+    nsrc = 3 if pro == 0 else 2
+    w = (torch.randn(C, nsrc * C, device="cuda") * 0.05).to(bf)
+    b = f(C)
+    bn = _bn_module(C)
+    rows = _lib.LIB.dfcsa_fwd_pro_parts(M, C, pro)
+    stats = torch.empty(rows * 2 * C, device="cuda")
+    y = torch.empty((B, H, H, C), device="cuda", dtype=bf)
+    o0 = torch.empty_like(y)
+    o1 = torch.empty_like(y)
+    fd, st = ops.bn_fold_desc(bn, b, C, M)
+    saved = _lib.LIB.dfcsa_get_tuning(39)
+    dfcsa.set_tuning(39, 1 if fold else 0)
+    try:
+        if pro == 0:
+            call("dfcsa_gate_fusion_fwd_bn", M, C, P(r(B, H, H, C)), P(f(C)), P(f(C)), P(r(B, H, H, C)),
+                 P(r(B, H, H, C)), P(w), 3 * C, P(b), P(o0), P(y), *S(stats), ctypes.addressof(fd), stream())
+        else:
+            Pp = 4
+            call("dfcsa_local_attn_gate_fwd_bn", B, H, H, C, P(r(B, H, H, C)), P(f(C)), P(f(C)), P(r(B, H, H, C)),
+                 P(f(C)), P(f(C)), P(f(B, Pp, Pp, C)), Pp, P(f(1)), P(w), 2 * C, P(b), P(o0), P(o1), P(y),
+                 *S(stats), ctypes.addressof(fd), stream())
+        torch.cuda.synchronize()
+    finally:
+        dfcsa.set_tuning(39, saved)
+    return (st.scale.clone(), st.shift.clone(), st.mean.clone(), st.invstd.clone(), bn.running_mean.clone(),
+            bn.running_var.clone(), bn.num_batches_tracked.clone(), y)
+
+
+@pytest.mark.parametrize("pro,B,H,C", [(0, 16, 224, 64), (0, 16, 112, 128), (1, 16, 224, 64), (1, 16, 112, 128),
+                                       (0, 2, 30, 64), (1, 3, 17, 128)])
+def test_bn_fold_prologue_gemms(pro, B, H, C):
+    """The forward prologue GEMMs (gate fusion / local-attention merge) with BN4 / BN3 finalised in
+    their tail equal the GEMM + dfcsa_bn_finalize launch (knob 39 = 0), bitwise repeatably."""
+    ref = _run_pro(pro, B, H, C, fold=False)
+    got = _run_pro(pro, B, H, C, fold=True)
+    again = _run_pro(pro, B, H, C, fold=True)
+    names = ("scale", "shift", "mean", "invstd", "running_mean", "running_var", "num_batches_tracked", "y")
+    for n, a, b, c in zip(names, ref, got, again):
+        assert torch.equal(b, c), f"{n}: folded finalize not bitwise repeatable"
+        if n == "num_batches_tracked":
+            assert int(a) == int(b) == 1
+            continue
+        if n == "y":
+            assert torch.equal(a, b)
+            continue
+        err = (a.double() - b.double()).abs().max().item()
+        assert err <= 1e-6 * max(1.0, a.double().abs().max().item()), (n, err)
