@@ -174,15 +174,19 @@ def _run_pro(pro, B, H, C, fold, seed=0):
     fd, st = ops.bn_fold_desc(bn, b, C, M)
     saved = _lib.LIB.dfcsa_get_tuning(39)
     dfcsa.set_tuning(39, 1 if fold else 0)
+    # every input held by a name for the launch (a temporary's memory could be handed to the next
+    # allocation before the kernel reads it)
+    xa, xb, xc = r(B, H, H, C), r(B, H, H, C), r(B, H, H, C)
+    v0, v1, v2, v3 = f(C), f(C), f(C), f(C)
+    Pp = 4
+    o, gam = f(B, Pp, Pp, C), f(1)
     try:
         if pro == 0:
-            call("dfcsa_gate_fusion_fwd_bn", M, C, P(r(B, H, H, C)), P(f(C)), P(f(C)), P(r(B, H, H, C)),
-                 P(r(B, H, H, C)), P(w), 3 * C, P(b), P(o0), P(y), *S(stats), ctypes.addressof(fd), stream())
-        else:
-            Pp = 4
-            call("dfcsa_local_attn_gate_fwd_bn", B, H, H, C, P(r(B, H, H, C)), P(f(C)), P(f(C)), P(r(B, H, H, C)),
-                 P(f(C)), P(f(C)), P(f(B, Pp, Pp, C)), Pp, P(f(1)), P(w), 2 * C, P(b), P(o0), P(o1), P(y),
+            call("dfcsa_gate_fusion_fwd_bn", M, C, P(xa), P(v0), P(v1), P(xb), P(xc), P(w), 3 * C, P(b), P(o0), P(y),
                  *S(stats), ctypes.addressof(fd), stream())
+        else:
+            call("dfcsa_local_attn_gate_fwd_bn", B, H, H, C, P(xa), P(v0), P(v1), P(xb), P(v2), P(v3), P(o), Pp,
+                 P(gam), P(w), 2 * C, P(b), P(o0), P(o1), P(y), *S(stats), ctypes.addressof(fd), stream())
         torch.cuda.synchronize()
     finally:
         dfcsa.set_tuning(39, saved)
