@@ -108,6 +108,7 @@ class Trainer:
         self._weight = 1.0   # this rank's loss-gradient weight for the current batch (shard_weight)
         self._graphs = {} if use_graphs else None
         self._graph_seen = set()
+        self._copy_stream = None   # host batches are uploaded on it, one step ahead (_prefetch)
         print(f"模型將在 {self.device} 上訓練" + (f" (rank {self.rank}/{self.world})" if self.world > 1 else ""))
 
     # ------------------------------------------------------------------ one step
@@ -274,20 +275,51 @@ class Trainer:
             images, masks = images[lo:hi], masks[lo:hi]
         return images, masks, shard_weight(n, self.rank, self.world)
 
+    def _prefetch(self, batch):
+        """(images, masks, weight, event) of a loader batch on the device, or None at the end.  Host
+        (pinned) tensors are uploaded on a copy stream so the upload overlaps the running step; the
+        event marks its completion and the tensors are recorded on the compute stream."""
+        if batch is None:
+            return None
+        images, masks, w = self._local_rows(batch)
+        if images is None or images.shape[0] == 0:
+            return images, masks, w, None
+        dev = torch.device(self.device)
+        if dev.type != "cuda" or images.is_cuda or not torch.cuda.is_available():
+            return images.to(self.device, non_blocking=True), masks.to(self.device, non_blocking=True), w, None
+        if self._copy_stream is None:
+            self._copy_stream = torch.cuda.Stream(device=dev)
+        main = torch.cuda.current_stream(dev)
+        with torch.cuda.stream(self._copy_stream):
+            di = images.to(dev, non_blocking=True)
+            dm = masks.to(dev, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(self._copy_stream)
+        di.record_stream(main)
+        dm.record_stream(main)
+        return di, dm, w, ev
+
     def train_epoch(self, epoch):
         self.model.train()
         if hasattr(self.train_loader, "set_epoch"):   # a rank-sharded loader reshuffles per epoch
             self.train_loader.set_epoch(epoch)
         running_loss = running_iou = running_dice = 0.0
         bar = tqdm(self.train_loader, desc=f"Epoch {epoch + 1}/{self.num_epochs} [Train]")
-        for batch_idx, batch in enumerate(bar):
-            images, masks, self._weight = self._local_rows(batch)
+        it = iter(bar)
+        nxt = self._prefetch(next(it, None))
+        batch_idx = -1
+        while nxt is not None:
+            batch_idx += 1
+            images, masks, self._weight, ready = nxt
             if images is None or images.shape[0] == 0:
                 met = self._null_step()
             else:
-                images = images.to(self.device, non_blocking=True)
-                masks = masks.to(self.device, non_blocking=True)
+                if ready is not None:   # the copy-stream upload of this batch
+                    torch.cuda.current_stream(self.device).wait_event(ready)
                 met = self.train_step(images, masks)
+            # the next batch is fetched and uploaded while this step runs (the reference's loop
+            # uploads it after the .item() below); the results are the same
+            nxt = self._prefetch(next(it, None))
             loss = float(met["stats"][0].item())
             if loss != loss:  # NaN: the device already skipped the update (trainer.py:134-139)
                 print(f"Warning: NaN loss detected at batch {batch_idx}\n  Skipping this batch...")
