@@ -122,27 +122,36 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
       }
     }
   }
-  __shared__ __attribute__((aligned(16))) float red[256 * 8];
+  // lane partials staged element-major, red[q][stride] with stride = 256 + min(cpp, 64): the stores
+  // (lanes consecutive) and the combine's reads (a wave covers chunks kk < cpp of up to 64 / cpp
+  // elements q: banks 8q + kk ... distinct) are free of LDS bank conflicts (the chunk-major
+  // lds_st8 staging measured 33 % conflict cycles)
+  __shared__ float red[8 * (256 + 64)];
+  const int stride = 256 + min(cpp, 64);
   for (int k = 0; k < (WS ? 3 : 1); ++k) {
     if (k) __syncthreads();
     if (lp < pl) {
+      auto stage = [&](const float (&v)[8]) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q) red[q * stride + tid] = v[q];
+      };
       if constexpr (WS) {
-        if (k == 1) lds_st8(red + tid * 8, accr);
-        else if (k == 2) lds_st8(red + tid * 8, accy);
-        else lds_st8(red + tid * 8, acc);
+        if (k == 1) stage(accr);
+        else if (k == 2) stage(accy);
+        else stage(acc);
       } else {
-        lds_st8(red + tid * 8, acc);
+        stage(acc);
       }
     }
     __syncthreads();
     // k = 0: partial [B][N][S][C]; k = 1, 2: wpart [B][N][S][2][C]
     float* out = k == 0 ? partial + (((size_t)b * P * P + n) * S + s) * C
                         : wpart + ((((size_t)b * P * P + n) * S + s) * 2 + (k - 1)) * C;
-    for (int c = tid; c < C; c += 256) {
-      const int kk = c >> 3, q = c & 7;
+    for (int e = tid; e < C; e += 256) {
+      const int kk = e % cpp, q = e / cpp;   // element q of chunk kk: channel kk * 8 + q
       float v = 0.f;
-      for (int p = 0; p < pl; ++p) v += red[(p * cpp + kk) * 8 + q];
-      out[c] = v;
+      for (int p = 0; p < pl; ++p) v += red[q * stride + p * cpp + kk];
+      out[kk * 8 + q] = v;
     }
   }
 }

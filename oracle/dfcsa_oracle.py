@@ -80,16 +80,22 @@ def light_self_attention(a, sd, name, pool_size):
     return sd[name + ".gamma"] * o + a
 
 
-def full_resolution_attention(a, sd, name):
+def full_resolution_attention(a, sd, name, q_chunk=8192):
     """models/unet_dfc_sa_ablation_attention.py:15-26: attention over all H*W positions, q/k with
-    C//8 channels, softmax over keys without a 1/sqrt(d) scale, gamma-scaled residual."""
+    C//8 channels, softmax over keys without a 1/sqrt(d) scale, gamma-scaled residual.  Past
+    q_chunk positions the [N, N] map is formed q_chunk query rows at a time (each row's softmax over
+    every key, as the reference's): at 512^2 the whole map would be 275 GB."""
     B, C, H, W = a.shape
     N = H * W
     q = conv(a, sd, name + ".query_conv").reshape(B, -1, N).permute(0, 2, 1)    # [B,N,C']
     k = conv(a, sd, name + ".key_conv").reshape(B, -1, N)                       # [B,C',N]
-    att = torch.softmax(torch.bmm(q, k), dim=-1)                                # [B,N,N]
     v = conv(a, sd, name + ".value_conv").reshape(B, -1, N)                     # [B,C,N]
-    o = torch.bmm(v, att.permute(0, 2, 1)).reshape(B, C, H, W)
+    if N <= q_chunk:
+        att = torch.softmax(torch.bmm(q, k), dim=-1)                            # [B,N,N]
+        o = torch.bmm(v, att.permute(0, 2, 1)).reshape(B, C, H, W)
+    else:
+        o = torch.cat([torch.bmm(v, torch.softmax(torch.bmm(q[:, i:i + q_chunk], k), dim=-1).permute(0, 2, 1))
+                       for i in range(0, N, q_chunk)], dim=2).reshape(B, C, H, W)
     return sd[name + ".gamma"] * o + a
 
 

@@ -267,8 +267,9 @@ def test_fullres_model_512_bf16_train_step_factory():
     UNet_FullResAttention, features 64..512, 512^2, bf16), built through ModelFactory, B = 1: the
     level-1 / level-9 attention runs over N = 262,144 tokens and level 2 / 8 over 65,536 (the kernels
     at exactly these N and widths are checked against torch fp32 in test_gpu_fra_longn.py).  One train
-    step: logits within 5e-2 of the fp32 mode (generic fp32 attention kernels) on the same weights and
-    batch, loss within 1e-2, every gradient and the clipped norm finite and nonzero, every parameter
+    step: the fp32 mode's logits within 1e-3 of the oracle's fp32 forward of the same weights and batch
+    (tests/golden/fullres512_fwd.npz, oracle/dfcsa_oracle.py with the FRA formed in query chunks; the
+    oracle is pinned to the reference at small N), the bf16 logits within 5e-2 of both, loss within 1e-2, every gradient and the clipped norm finite and nonzero, every parameter
     finite after the SGD step, and the attention gammas' gradients nonzero on every level."""
     from dfcsa.loss import sigmoid
     from dfcsa.optim import FusedSGD
@@ -286,6 +287,11 @@ def test_fullres_model_512_bf16_train_step_factory():
                 p.fill_(0.5)
     m32 = UNet_FullResAttention(3, 1, [64, 128, 256, 512], precision="fp32")
     m32.load_state_dict(m16.state_dict())
+    # the oracle's fp32 forward of these exact weights and batch (tests/golden/make_fullres512.py)
+    fx = np.load(os.path.join(os.path.dirname(__file__), "golden", "fullres512_fwd.npz"))
+    ck = np.array([float(sum(p.detach().double().sum() for p in m32.parameters())),
+                   float(sum(p.detach().double().abs().sum() for p in m32.parameters()))])
+    assert np.allclose(ck, fx["param_checksum"], rtol=1e-12, atol=0), "weights differ from the fixture's"
     m32, m16 = m32.cuda().train(), m16.cuda().train()
     g = torch.Generator().manual_seed(14)
     x = torch.randn(1, 3, 512, 512, generator=g).cuda()
@@ -293,6 +299,10 @@ def test_fullres_model_512_bf16_train_step_factory():
     with torch.no_grad():
         l32 = m32(x)
         ref = calculate_metrics_device(sigmoid(l32), t, "bce_dice", {})["loss"].item()
+    r32 = rel(l32, fx["logits"])
+    print(f"512^2 full-resolution model: fp32 mode vs oracle logits rel {r32:.3e}, loss {ref:.6f} vs "
+          f"{float(fx['loss']):.6f}")
+    assert r32 < 1e-3 and abs(ref - float(fx["loss"])) <= 1e-4 * abs(float(fx["loss"]))
     del m32
     torch.cuda.empty_cache()
     opt = FusedSGD(m16.parameters(), lr=0.01, momentum=0.9, weight_decay=1e-4)
@@ -302,8 +312,10 @@ def test_fullres_model_512_bf16_train_step_factory():
     met["loss"].backward()
     torch.cuda.synchronize()
     r = rel(l16, l32)
-    print(f"512^2 full-resolution model: bf16 vs fp32 logits rel {r:.3e}, loss {met['loss'].item():.6f} vs {ref:.6f}")
-    assert r < 5e-2
+    r16 = rel(l16, fx["logits"])
+    print(f"512^2 full-resolution model: bf16 vs fp32 logits rel {r:.3e}, vs oracle {r16:.3e}, "
+          f"loss {met['loss'].item():.6f} vs {ref:.6f}")
+    assert r < 5e-2 and r16 < 5e-2
     assert abs(met["loss"].item() - ref) <= 1e-2 * abs(ref)
     for n, p in m16.named_parameters():
         assert torch.isfinite(p.grad).all(), n
