@@ -618,8 +618,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
 
 
 # the backward's last block (no input gradient): conv1's weight gradient issued before the attention
-# chain's join (DFCSA_LAST_EARLY=1), and the gate / fusion weight gradients too (=2)
-LAST_EARLY = [int(os.environ.get("DFCSA_LAST_EARLY", "0"))]
+# chain's join (DFCSA_LAST_EARLY=1, the default: same-box A/B 1645.3 / 1645.4 / 1646.0 against
+# 1644.1 / 1642.8 / 1638.7 img/s for 0), and the gate / fusion weight gradients too (=2: 1640.5 /
+# 1636.6 / 1640.9)
+LAST_EARLY = [int(os.environ.get("DFCSA_LAST_EARLY", "1"))]
 
 # the input-side convs' weight gradients of a block issued one block later in the backward (after the
 # next block's input-gradient GEMM) instead of right after its own join: DFCSA_DEFER_WGRAD=1
