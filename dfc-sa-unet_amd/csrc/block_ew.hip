@@ -1468,14 +1468,15 @@ extern "C" int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum,
   if (nsum < 2 || nsum > 3 || C <= 0 || C > 2048 || ntiles <= 0) return DFCSA_EINVAL;
   hipStream_t st = (hipStream_t)stream;
   const int nblk = (C + 63) / 64;
-  // the third per-channel sum (res_scale gradient) is staged in the tail of `coef` ([3][C]) and
-  // reduced to the scalar *extra by the last channel block
-  float* third = (nsum == 3 && extra) ? coef + 2 * C : nullptr;
+  // the third per-channel sum (res_scale gradient) is stored in the tail of `coef` ([3][C]) and, with
+  // `extra`, reduced to the scalar *extra by the last channel block (a second ticket level); without
+  // it the caller sums coef[2C, 3C) off the critical path (dfcsa_sum_into on another stream)
+  float* third = nsum == 3 ? coef + 2 * C : nullptr;
   RedPlan rp;
-  if (red_plan(ntiles, nblk, nsum, third ? 1 : 0, &rp)) return DFCSA_EINVAL;
+  if (red_plan(ntiles, nblk, nsum, extra && third ? 1 : 0, &rp)) return DFCSA_EINVAL;
   if (nsum == 3)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<3>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
-                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, third, third ? extra : nullptr, rp.acq);
+                       rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, third, extra, rp.acq);
   else
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<2>, dim3(nblk, rp.R), dim3(1024), 0, st, partial, ntiles, rp.per,
                        rp.cnt, rp.scr, C, count, coef, dgamma, dbeta, nullptr, nullptr, rp.acq);

@@ -369,8 +369,16 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
         call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean),
              P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), *S(part), stream())
-    coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
-                               extra=grad_of(blk.res_scale))
+    if ops._SYNC_BN is None:
+        # res_scale's gradient (sum over channels of the third sums, left in coef[2C:3C]) is summed on
+        # the side stream: only the optimizer reads it, and the finalize on the critical path then
+        # needs no second ticket level
+        coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias))
+        with on_side(dev, coef):
+            call("dfcsa_sum_into", P(coef) + 8 * C, C, P(grad_of(blk.res_scale)), stream())
+    else:
+        coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
+                                   extra=grad_of(blk.res_scale))
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
     dlocal = torch.empty_like(s.y4)

@@ -398,7 +398,9 @@ int dfcsa_bwd_attn_entry(int dtype, int B, int H, int W, int C, const void* datt
                          int P, const void* y2, const float* sc2, const float* sh2, const float* mean2,
                          const float* invstd2, int relu, void* dz2, float* partial, int64_t partial_floats, void* stream);
 /* from partial sums: coef[0][c] = mean dz, coef[1][c] = mean dz*xh; dgamma += sum dz*xh,
- * dbeta += sum dz; if nsum == 3 and extra != null: *extra += sum over c of the third sum. */
+ * dbeta += sum dz; nsum == 3: coef holds [3][C] floats and coef[2][c] = the third sum, and with
+ * extra != null the launch also adds sum over c of it to *extra (round 5: with extra == null the
+ * caller may sum coef[2][.] itself, e.g. dfcsa_sum_into on another stream). */
 int dfcsa_bn_bwd_finalize(const float* partial, int ntiles, int nsum, int C, int count,
                           float* coef, float* dgamma, float* dbeta, float* extra, void* stream);
 /* dfcsa_bn_bwd_finalize (nsum = 2) for a DFC block's attention entry: `partial` holds the sums of
