@@ -369,7 +369,7 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
         call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean),
              P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), *S(part), stream())
-    if ops._SYNC_BN is None:
+    if ops._SYNC_BN is None and RES_SCALE_SIDE[0]:
         # res_scale's gradient (sum over channels of the third sums, left in coef[2C:3C]) is summed on
         # the side stream: only the optimizer reads it, and the finalize on the critical path then
         # needs no second ticket level
@@ -624,6 +624,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         streams.defer(input_wgrads)
     return dxs
 
+
+# the block output's res_scale gradient summed on the side stream (DFCSA_RES_SCALE_SIDE=0: inside the
+# BN4 finalize, a second ticket level on the critical path)
+RES_SCALE_SIDE = [os.environ.get("DFCSA_RES_SCALE_SIDE", "1") == "1"]
 
 # the backward's last block (no input gradient): conv1's weight gradient issued before the attention
 # chain's join (DFCSA_LAST_EARLY=1, the default: same-box A/B 1645.3 / 1645.4 / 1646.0 against
