@@ -625,9 +625,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     return dxs
 
 
-# the block output's res_scale gradient summed on the side stream (DFCSA_RES_SCALE_SIDE=0: inside the
-# BN4 finalize, a second ticket level on the critical path)
-RES_SCALE_SIDE = [os.environ.get("DFCSA_RES_SCALE_SIDE", "1") == "1"]
+# the block output's res_scale gradient summed on the side stream instead of inside the BN4 finalize
+# (DFCSA_RES_SCALE_SIDE=1).  Off: the extra main -> side edge per block costs far more than the
+# finalize's second ticket level (same-box A/B 1567 / 1578 / 1577 against 1630 / 1629 / 1631 img/s)
+RES_SCALE_SIDE = [os.environ.get("DFCSA_RES_SCALE_SIDE", "0") == "1"]
 
 # the backward's last block (no input gradient): conv1's weight gradient issued before the attention
 # chain's join (DFCSA_LAST_EARLY=1, the default: same-box A/B 1645.3 / 1645.4 / 1646.0 against
