@@ -93,7 +93,8 @@ def _per_dispatch(db, counter):
 
 
 CLASSES = {"conv_gemm": ("conv_gemm_glds_kernel", "conv_gemm_kernel<", "conv_gemm_pp_kernel", "conv_halo_kernel",
-                         "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel", "conv_gemm_ppsk_kernel"),
+                         "conv_gemm_glds32_kernel", "conv_splitk_epi_kernel", "conv_gemm_ppsk_kernel",
+                         "small_conv_f32_kernel"),
            "conv_wgrad": ("wgrad_glds_kernel", "wgrad_bd_kernel", "wgrad_kernel<", "wgrad_halo_kernel"),
            # bench.py's class 4 (DFCSA_PROF_CONV_STREAM) times the streaming 1x1 GEMMs AND the fused
            # block GEMMs (dfcsa_dgrad_gate*, dfcsa_gate_fusion_fwd, dfcsa_local_attn_gate_fwd): the
