@@ -487,9 +487,30 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         ncr = (B * Np + 15) // 16 if rows_in_proj else 0
         part2 = torch.empty((nte + ncr) * 2 * C, device=dev, dtype=f32)
         pool_rows = (wsum, bn2.mean, bn2.invstd, P(part2) + nte * 2 * C * 4, H, W) if rows_in_proj else None
-        with on_branch(dev, branch, dattn, part2, wsum):
-            dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
-                                        pool_rows=pool_rows)
+        if branch and ENTRY_SUMS_BRANCH[0]:
+            # one fork: the dattn part of the entry sums on the branch ahead of the attention backward
+            # (the local branch's BN1 sums then come from the acc GEMM or their own pass on this stream)
+            with on_branch(dev, branch, dattn, part2, wsum):
+                call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
+                     P(bn2.invstd), None, *S(part2), stream())
+                dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
+                                            pool_rows=pool_rows)
+                if rows_in_proj:
+                    coef2 = ops.bn_bwd_finalize(part2, nte + ncr, 2, C, M, grad_of(bn2m.weight),
+                                                grad_of(bn2m.bias))
+                else:
+                    coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias),
+                                                     dpooled, wsum, B, H, W, Pp, bn2)
+                dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
+                                             grad_of(conv2.bias))
+                del dpooled, coef2
+            del part2
+            s.wsum = None
+        else:
+            with on_branch(dev, branch, dattn, part2, wsum):
+                dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
+                                            pool_rows=pool_rows)
+    if s.fra is None and wsum is not None and not (branch and ENTRY_SUMS_BRANCH[0]):
         if fused_bn1:
             call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
                  P(bn2.invstd), None, *S(part2), stream())
@@ -509,6 +530,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             del dpooled, coef2
         del part2
         s.wsum = None
+    elif s.fra is None and wsum is not None:
+        pass   # the one-fork branch above
     else:
         with on_branch(dev, branch, dattn):
             # (dz2 is not materialised: the apply recomputes it from the same inputs)
@@ -624,6 +647,11 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         streams.defer(input_wgrads)
     return dxs
 
+
+# the dattn part of the attention entry's BN2-backward sums on the branch stream ahead of the attention
+# backward (DFCSA_ENTRY_SUMS_BRANCH=1: one branch fork per block backward instead of two; the local
+# branch's BN1 sums then take their own pass where the pair kernel formed them)
+ENTRY_SUMS_BRANCH = [os.environ.get("DFCSA_ENTRY_SUMS_BRANCH", "1") == "1"]
 
 # the block output's res_scale gradient summed on the side stream instead of inside the BN4 finalize
 # (DFCSA_RES_SCALE_SIDE=1).  Off: the extra main -> side edge per block costs far more than the
