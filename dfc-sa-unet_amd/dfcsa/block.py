@@ -650,8 +650,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
 
 # the dattn part of the attention entry's BN2-backward sums on the branch stream ahead of the attention
 # backward (DFCSA_ENTRY_SUMS_BRANCH=1: one branch fork per block backward instead of two; the local
-# branch's BN1 sums then take their own pass where the pair kernel formed them)
-ENTRY_SUMS_BRANCH = [os.environ.get("DFCSA_ENTRY_SUMS_BRANCH", "1") == "1"]
+# branch's BN1 sums then take their own pass where the pair kernel formed them).  Off: the pass is
+# worth more beside the attention backward than the saved fork (same-box A/B 1575 / 1570 / 1578
+# against 1591 / 1589 / 1587 img/s)
+ENTRY_SUMS_BRANCH = [os.environ.get("DFCSA_ENTRY_SUMS_BRANCH", "0") == "1"]
 
 # the block output's res_scale gradient summed on the side stream instead of inside the BN4 finalize
 # (DFCSA_RES_SCALE_SIDE=1).  Off: the extra main -> side edge per block costs far more than the
