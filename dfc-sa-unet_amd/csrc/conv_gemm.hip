@@ -3260,6 +3260,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 37: return g_splitk_min_nk;
     case 39: return g_bn_fold;
     case 40: return g_ppsk;
+    case 42: return g_wgrad_bd_nst;
     case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
@@ -3296,6 +3297,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 36) { g_gate_grid_div = value; return 0; }
   if (knob == 39) { g_bn_fold = value; return 0; }
   if (knob == 40) { g_ppsk = value; return 0; }
+  if (knob == 42) { g_wgrad_bd_nst = (value == 3 || value == 4) ? value : 2; return 0; }
   if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 24; return 0; }
   if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }

@@ -103,6 +103,7 @@ extern int g_wgrad_halo;
 extern int g_wgrad_reduce_old;
 extern int g_wgrad_nst64;
 extern int g_wgrad_bd;
+extern int g_wgrad_bd_nst;
 extern int g_wgrad_coop_launches;
 extern int g_wgrad_coop;   // knob 31: cooperative in-launch split-K reduction (0 = separate reduction launch)
 extern int g_small8;

@@ -791,8 +791,13 @@ __global__ void __launch_bounds__(512) wgrad_bd_kernel(const WgradArgs args, int
   for (int s = 0; s < NST - 1; ++s)
     if (s < nk) issue(s, s);
   for (int kt = 0; kt < nk; ++kt) {
+    // stages issued behind this one: their DMAs may stay in flight
     const int after = min(NST - 2, nk - 1 - kt);
-    if constexpr (NST >= 3) {
+    if constexpr (NST >= 4) {
+      if (after >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * OPS) : "memory");
+      else if (after == 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (NST == 3) {
       if (after >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(OPS) : "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
@@ -1491,8 +1496,19 @@ int launch_wgrad(const WgradArgs& a, int splits, hipStream_t st, bool want_coop,
       // buffer-descriptor kernel on 64-channel sub-images (knob 26 = 0: the pointer-DMA kernel)
       if (g_wgrad_bd && a.simple && a.Cseg % 64 == 0 && a.Cg % 64 == 0 && !wide_j(a) &&
           (int64_t)a.M * a.Cseg * 2 < (1ll << 31) && (int64_t)a.M * a.Cg * 2 < (1ll << 31))
+      {
+        // knob 42: LDS-DMA ring depth of this kernel (2 = two workgroups per CU, the default; 3 / 4 =
+        // one workgroup per CU with two / three stages in flight)
+        const int bnst = g_wgrad_bd_nst;
+        if (bnst == 4)
+          return launch_wg(wgrad_bd_kernel<BI, 4>, xcd_pad(grid.x * grid.y * splits), 512, BI, BJ, a, splits,
+                           want_coop, coop_used, st);
+        if (bnst == 3)
+          return launch_wg(wgrad_bd_kernel<BI, 3>, xcd_pad(grid.x * grid.y * splits), 512, BI, BJ, a, splits,
+                           want_coop, coop_used, st);
         return launch_wg(wgrad_bd_kernel<BI, 2>, xcd_pad(grid.x * grid.y * splits), 512, BI, BJ, a, splits, want_coop,
                          coop_used, st);
+      }
       // 1-D grid (x = padded tile count): see the XCD remap in the kernel
       if (BI == 64 && wide_j(a))
         return launch_wg(wgrad_glds_kernel<64, 256, 2, 4, 2>, xcd_pad(((a.NJ + 255) / 256) * ((a.NI + BI - 1) / BI) * splits),
@@ -1535,6 +1551,7 @@ int g_wgrad_waves = 0;     // waves per wgrad workgroup (dfcsa_set_tuning knob 6
 int g_wgrad_noglds = 0;    // 1 = register-staged bf16 wgrad (dfcsa_set_tuning knob 7)
 int g_wgrad_narrow = 1;    // 0 = allow the 64x256 wgrad tile (dfcsa_set_tuning knob 8; measured slower on the L1 3x3)
 int g_wgrad_target = 512;  // workgroups per wgrad launch (dfcsa_set_tuning knob 2)
+int g_wgrad_bd_nst = 2;    // knob 42: LDS-DMA ring depth of the buffer-descriptor wgrad kernel (2, 3, 4)
 int g_wgrad_nst = 2;       // knob 14: LDS-DMA ring depth of the bf16 wgrad kernel (2, 3, 4)
 int g_wgrad_fuse_all = 0;  // knob 12: 1 = reduce in-kernel at any split count, -1 = never (separate launch)
 // knob 13: most splits reduced in-kernel.  Default 0 = never: measured on the headline step
