@@ -1557,18 +1557,27 @@ __global__ void __launch_bounds__(256) head3_bwd_kernel(int B, int H, int W, int
   __syncthreads();
   if (m < M) {
     const int wq = (int)(m % W), hq = (int)((m / W) % H), b = (int)(m / HWn);
-    for (int c0 = 0; c0 < C; c0 += 8) {
-      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    // the pixel's 9 x Cout logit gradients, loaded together (independent loads in flight) and kept in
+    // registers across the channel chunks
+    float gv[4][9];
+#pragma unroll
+    for (int o = 0; o < 4; ++o)
+#pragma unroll
       for (int tap = 0; tap < 9; ++tap) {
         const int oh = hq - (tap / 3 - 1), ow = wq - (tap % 3 - 1);
-        if (oh < 0 || oh >= H || ow < 0 || ow >= W) continue;
+        const bool in = o < Cout && oh >= 0 && oh < H && ow >= 0 && ow < W;
+        gv[o][tap] = in ? dl[((size_t)b * Cout + o) * HWn + (size_t)oh * W + ow] : 0.f;
+      }
+    for (int c0 = 0; c0 < C; c0 += 8) {
+      float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap)
         for (int o = 0; o < Cout; ++o) {
-          const float g = dl[((size_t)b * Cout + o) * HWn + (size_t)oh * W + ow];
+          const float g = gv[o][tap];
           const float* wr = ws + (o * 9 + tap) * C + c0;
 #pragma unroll
           for (int q = 0; q < 8; ++q) acc[q] += g * wr[q];
         }
-      }
       store8<T>(dx + (size_t)m * C + c0, acc);
     }
   }
