@@ -1572,7 +1572,9 @@ __global__ void __launch_bounds__(256) head3_bwd_kernel(int B, int H, int W, int
       float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
       for (int tap = 0; tap < 9; ++tap)
-        for (int o = 0; o < Cout; ++o) {
+#pragma unroll
+        for (int o = 0; o < 4; ++o) {
+          if (o >= Cout) break;
           const float g = gv[o][tap];
           const float* wr = ws + (o * 9 + tap) * C + c0;
 #pragma unroll
