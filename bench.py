@@ -79,12 +79,13 @@ def pmc_traffic(cls):
         return None, None
 
 
-def replayed_classes():
-    """Kernel time per step of each roofline class in the replayed HIP-graph step, every stream
-    concurrent, from the newest committed kernel trace of this benchmark
-    (profiles/rNN_replay_classes.json, tools/rocpd_export.py replay)."""
+def replayed_classes(kind="replay"):
+    """Kernel time per step of each roofline class from the newest committed kernel trace of this
+    benchmark (tools/rocpd_export.py replay): kind "replay" = the timed HIP-graph replays, every
+    stream concurrent (profiles/rNN_replay_classes.json); "serial" = the class-timing pass, streams
+    serialised (profiles/rNN_serial_classes.json)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_replay_classes.json")))
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_classes.json")))
     if not files:
         return None, None
     try:
@@ -463,6 +464,18 @@ def main():
                                 "launches_per_step": r["launches_per_step"], "source": rsrc,
                                 "timing": "rocprofv3 kernel trace of the timed HIP-graph replays (side and "
                                           "branch streams concurrent), this run's class FLOPs per step"}
+        ser, ssrc = replayed_classes("serial") if headline else (None, None)
+        if ser and dom_key in ser and ser[dom_key]["ms_per_step"] > 0:
+            # the same pass's kernels as rocprofv3 times them (kernel start to end): the HIP events
+            # around each launch also count its dispatch gap
+            r = ser[dom_key]
+            a_s = fl / args.steps / (r["ms_per_step"] * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9)
+            roof["serialised_trace"] = {"achieved": round(a_s, 2), "frac": round(a_s / peak, 4),
+                                        "avg_launch_ms": round(r["ms_per_step"] / max(r["launches_per_step"], 1), 4),
+                                        "launches_per_step": r["launches_per_step"], "source": ssrc,
+                                        "timing": "rocprofv3 kernel trace of this command's class-timing pass "
+                                                  "(kernel durations; the events above also count each launch's "
+                                                  "dispatch gap)"}
         if args.model == "fullres" and 3 in cls:
             roof = fra_exp_roofline(roof, cls[3], args, B, L)
         for v in cls.values():
