@@ -1402,17 +1402,6 @@ extern "C" int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, cons
   return launch_red<EW_BWD_SUM_OUT>(dtype, e, (hipStream_t)stream);
 }
 
-// a HIP stream restricted to the CUs set in mask[0..n) (32 CUs per word; hipExtStreamCreateWithCUMask):
-// the weight-gradient side stream of an A/B (streams.py DFCSA_SIDE_CU_MASK)
-extern "C" int dfcsa_stream_create_cu_mask(const unsigned* mask, int n, void** out) {
-  if (!mask || n <= 0 || !out) return DFCSA_EINVAL;
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)n, mask);
-  if (e != hipSuccess) return -(int)e;
-  *out = (void*)s;
-  return 0;
-}
-
 extern "C" int dfcsa_sum_into(const float* x, int n, float* out, void* stream) {
   if (!x || !out || n <= 0) return DFCSA_EINVAL;
   launch_sum_scalar(x, n, out, (hipStream_t)stream);

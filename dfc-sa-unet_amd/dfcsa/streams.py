@@ -52,33 +52,13 @@ def side_or_main(device, *tensors):
 SIDE_IS_BRANCH = [os.environ.get("DFCSA_SIDE_IS_BRANCH", "0") == "1"]
 
 
-# DFCSA_SIDE_CU_MASK=<k>: the side stream may use only every k-th CU (a CU-masked HIP stream, A/B)
-SIDE_CU_MASK = [int(os.environ.get("DFCSA_SIDE_CU_MASK", "0"))]
-
-
-def _cu_masked_stream(idx, every):
-    import ctypes
-
-    from ._lib import LIB
-    words = (ctypes.c_uint * 8)(*[sum(1 << b for b in range(32) if (w * 32 + b) % every == 0) for w in range(8)])
-    out = ctypes.c_void_p()
-    with torch.cuda.device(idx):
-        rc = LIB.dfcsa_stream_create_cu_mask(ctypes.addressof(words), 8, ctypes.addressof(out))
-    if rc != 0:
-        raise RuntimeError(f"dfcsa_stream_create_cu_mask failed ({rc})")
-    return torch.cuda.ExternalStream(out.value, device=torch.device("cuda", idx))
-
-
 def side_stream(device):
     if SIDE_IS_BRANCH[0]:
         return branch_stream(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(idx)
     if s is None:
-        if SIDE_CU_MASK[0] > 1:
-            s = _cu_masked_stream(idx, SIDE_CU_MASK[0])
-        else:
-            s = torch.cuda.Stream(device=idx, priority=PRIO_SIDE)
+        s = torch.cuda.Stream(device=idx, priority=PRIO_SIDE)
         _SIDE[idx] = s
     return s
 

@@ -753,9 +753,6 @@ int dfcsa_sum_out(int dtype, int M, int C, const void* a, const void* b, const v
                   void* out, void* stream);
 int dfcsa_bwd_sum_out(int dtype, int M, int C, const void* dout, const void* res, const float* res_scale, void* dres,
                       float* partial, int64_t partial_floats, void* stream);
-/* a HIP stream restricted to the CUs whose bits are set in mask[0..n) (32 CUs per word): the
- * weight-gradient side stream of an A/B (dfcsa/streams.py, DFCSA_SIDE_CU_MASK) */
-int dfcsa_stream_create_cu_mask(const unsigned* mask, int n, void** out);
 int dfcsa_sum_into(const float* x, int n, float* out, void* stream);
 
 /* ------------------------------------------------------------------------------------------
