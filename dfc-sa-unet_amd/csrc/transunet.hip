@@ -958,6 +958,59 @@ __global__ void gelu_drop_bwd_kernel(int64_t n, const T* __restrict__ x, const T
   }
 }
 
+constexpr int COLSUM_ROWS = 64;   // rows per column-sum tile (colsum_partial, the *_cs passes)
+
+// drop_bwd / gelu_drop_bwd over a [M][C] matrix with the column sums of their (stored) output per
+// COLSUM_ROWS-row tile: partial[tile][C] for dfcsa_slab_colsum3 -- the Linear bias gradient of the
+// GEMM whose dY this is (fc2 / out-projection: drop_bwd; fc1: gelu_drop_bwd), without the
+// colsum_partial pass over dY.  The element index of the dropout mask is the flat one (r*C + c), as
+// the flat kernels'; the sums add the values as stored (bf16-rounded), as colsum_partial reads them.
+template <typename T, bool GELU>
+__global__ void __launch_bounds__(256) drop_bwd_cs_kernel(int64_t M, int C, const T* __restrict__ x,
+                                                          const void* __restrict__ dout, float p,
+                                                          const int64_t* __restrict__ rng, int site,
+                                                          T* __restrict__ out, float* __restrict__ partial) {
+  const int c0 = (blockIdx.x * 256 + threadIdx.x) * 8;
+  if (c0 >= C) return;
+  const uint64_t key = p > 0.f ? drop_key(rng, site) : 0;
+  const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t r = r0; r < r1; r += 4) {
+    const int nr = (int)min((int64_t)4, r1 - r);
+    float d[4][8], v[4][8];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int64_t rr = r + min(u, nr - 1);   // rows past the tile re-load the last one (unused)
+      if constexpr (GELU) {
+        load8<T>((const T*)dout + rr * C + c0, d[u]);
+        load8<T>(x + rr * C + c0, v[u]);
+      } else {
+        ld8f((const float*)dout + rr * C + c0, d[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (u >= nr) break;
+      const int64_t i0 = (r + u) * C + c0;
+      float o[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        float g = GELU ? d[u][q] * gelu_grad(v[u][q]) : d[u][q];
+        if (p > 0.f) g = keep_elem(key, i0 + q, p) ? g * scale : 0.f;
+        o[q] = g;
+      }
+      store8<T>(out + i0, o);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {   // the stored (rounded) value
+        if constexpr (sizeof(T) == 2) acc[q] += bf2f(f2bf(o[q]));
+        else acc[q] += o[q];
+      }
+    }
+  }
+  st8f(partial + (size_t)blockIdx.y * C + c0, acc);
+}
+
 // out[j] += sum_b x[b*L + j]  (position-embedding gradient; fp64 over the batch)
 template <typename T>
 __global__ void batch_sum_kernel(int B, int64_t L, const T* __restrict__ x, float* __restrict__ out) {
@@ -1651,7 +1704,6 @@ __global__ void __launch_bounds__(256) head3_bwd_kernel(int B, int H, int W, int
 // ------------------------------------------------------------ wide column sums (bias gradients)
 // partial[t][c] = sum over rows [t*64, min(M, t*64 + 64)) of x[row][c]; any C % 8 == 0 (the Linear
 // layers of the ViT reach C = 3072, beyond the 2048-channel elementwise reductions)
-constexpr int COLSUM_ROWS = 64;
 
 template <typename T>
 __global__ void __launch_bounds__(256) colsum_partial_kernel(int64_t M, int C, const T* __restrict__ x,
@@ -2103,6 +2155,37 @@ extern "C" int dfcsa_gelu_drop_bwd(int dtype, int64_t n, const void* x, const vo
                        (const float*)dout, p, rng, site, (float*)dx);
   DFCSA_CHECK_LAUNCH();
   return 0;
+}
+
+template <bool GELU>
+static int launch_drop_cs(int dtype, int64_t M, int C, const void* x, const void* dout, float p, const int64_t* rng,
+                          int site, void* out, float* partial, int64_t partial_floats, hipStream_t st) {
+  if (M <= 0 || C <= 0 || C % 8 || p < 0.f || p >= 1.f || (p > 0.f && !rng) || !dout || !out || !partial ||
+      (GELU && !x))
+    return DFCSA_EINVAL;
+  const int64_t nt = (M + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  if (nt * C > partial_floats) return DFCSA_EINVAL;
+  dim3 grid((C / 8 + 255) / 256, (unsigned)nt);
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL((drop_bwd_cs_kernel<bf16_t, GELU>), grid, dim3(256), 0, st, M, C, (const bf16_t*)x, dout, p,
+                       rng, site, (bf16_t*)out, partial);
+  else
+    hipLaunchKernelGGL((drop_bwd_cs_kernel<float, GELU>), grid, dim3(256), 0, st, M, C, (const float*)x, dout, p, rng,
+                       site, (float*)out, partial);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_drop_bwd_cs(int dtype, int64_t M, int C, const float* dout, float p, const int64_t* rng, int site,
+                                 void* da, float* partial, int64_t partial_floats, void* stream) {
+  return launch_drop_cs<false>(dtype, M, C, nullptr, dout, p, rng, site, da, partial, partial_floats,
+                               (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_gelu_drop_bwd_cs(int dtype, int64_t M, int C, const void* x, const void* dout, float p,
+                                      const int64_t* rng, int site, void* dx, float* partial, int64_t partial_floats,
+                                      void* stream) {
+  return launch_drop_cs<true>(dtype, M, C, x, dout, p, rng, site, dx, partial, partial_floats, (hipStream_t)stream);
 }
 
 extern "C" int dfcsa_batch_sum(int dtype, int B, int64_t L, const void* x, float* out, void* stream) {

@@ -190,6 +190,24 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
 
 
+def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
+    """dropout backward (x given: GELU + dropout backward) of dout [M][C] into out, returning the
+    per-64-row column partials of out (the bias gradient of the GEMM whose dY out is)."""
+    part = _f32((LIB.dfcsa_colsum_ntiles(M) * C,), out.device)
+    if x is None:
+        call("dfcsa_drop_bwd_cs", dt(dtype), M, C, P(dout), float(p), P(rng), site, P(out), P(part), part.numel(),
+             stream())
+    else:
+        call("dfcsa_gelu_drop_bwd_cs", dt(dtype), M, C, P(x), P(dout), float(p), P(rng), site, P(out), P(part),
+             part.numel(), stream())
+    return part
+
+
+def _colsum_rows_into(part, M, C, out):
+    """out[c] += the sum of the column-partial rows of _drop_bwd_cs."""
+    call("dfcsa_slab_colsum3", P(part), LIB.dfcsa_colsum_ntiles(M), C, C, 0, P(out), None, None, stream())
+
+
 def bias_grad_into(dtype, dy, bias):
     channel_sum3_into(dtype, dy, dy.shape[-1], 0, grad_of(bias))
 
@@ -586,28 +604,30 @@ class ViTBlock(torch.autograd.Function):
         KD, KF = rup(D, KA), rup(F, KA)
         dout = dout.contiguous()
         # ---- MLP half: out = drop(fc2(drop(gelu(fc1(LN2 h1))))) + h1
+        M = B * N
         dm = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
-        call("dfcsa_drop_bwd", dt(dtype), dm.numel(), P(dout), float(p), P(rng), site + 2, P(dm), stream())
-        with side_or_main(dev, dm, g):
+        # the dropout backward also forms the fc2 bias gradient's column partials (dfcsa_drop_bwd_cs)
+        pm = _drop_bwd_cs(dtype, M, D, dout, p, rng, site + 2, dm)
+        with side_or_main(dev, dm, g, pm):
             _wgrad_1x1(dtype, dm, g, grid, hw, grad_of(mlp.fc2.weight))
-            bias_grad_into(dtype, dm, mlp.fc2.bias)
+            _colsum_rows_into(pm, M, D, grad_of(mlp.fc2.bias))
         dg = _gemm_1x1(dtype, dm, pk["W2t"], KD, F, torch.empty_like(f))
         del dm
         df = torch.empty_like(f)
-        call("dfcsa_gelu_drop_bwd", dt(dtype), f.numel(), P(f), P(dg), float(p), P(rng), site + 1, P(df), stream())
+        pf = _drop_bwd_cs(dtype, M, F, dg, p, rng, site + 1, df, x=f)
         del dg
-        with side_or_main(dev, df, y2):
+        with side_or_main(dev, df, y2, pf):
             _wgrad_1x1(dtype, df, y2, grid, hw, grad_of(mlp.fc1.weight))
-            bias_grad_into(dtype, df, mlp.fc1.bias)
+            _colsum_rows_into(pf, M, F, grad_of(mlp.fc1.bias))
         dy2 = _gemm_1x1(dtype, df, pk["W1t"], KF, D, torch.empty((B, gh, gw, D), dtype=dtype, device=dev))
         del df
         dh1 = _ln_backward(dtype, dy2, h1, mr2, blk.ffn_norm, dout)
         # ---- attention half: h1 = drop(out_proj(MHA(qkv(LN1 h)))) + h
         da = torch.empty((B, gh, gw, D), dtype=dtype, device=dev)
-        call("dfcsa_drop_bwd", dt(dtype), da.numel(), P(dh1), float(p_attn), P(rng), site, P(da), stream())
-        with side_or_main(dev, da, cx):
+        pa = _drop_bwd_cs(dtype, M, D, dh1, p_attn, rng, site, da)
+        with side_or_main(dev, da, cx, pa):
             _wgrad_1x1(dtype, da, cx, grid, hw, grad_of(att.out.weight))
-            bias_grad_into(dtype, da, att.out.bias)
+            _colsum_rows_into(pa, M, D, grad_of(att.out.bias))
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
         if ctx.probs is not None:

@@ -686,6 +686,15 @@ int dfcsa_gelu_drop_fwd(int dtype, int64_t n, const void* x, float p, const int6
                         void* stream);
 int dfcsa_gelu_drop_bwd(int dtype, int64_t n, const void* x, const void* dout, float p, const int64_t* rng, int site,
                         void* dx, void* stream);
+/* dfcsa_drop_bwd / dfcsa_gelu_drop_bwd over [M][C] (C % 8 == 0) that also write the column sums of
+ * their output per 64-row tile: partial [ceil(M / 64)][C] (capacity partial_floats), reduced by
+ * dfcsa_slab_colsum3 -- the Linear bias gradient of the GEMM whose dY the output is, without a
+ * dfcsa_colsum_partial pass (round 5).  The outputs equal the flat kernels'. */
+int dfcsa_drop_bwd_cs(int dtype, int64_t M, int C, const float* dout, float p, const int64_t* rng, int site,
+                      void* da, float* partial, int64_t partial_floats, void* stream);
+int dfcsa_gelu_drop_bwd_cs(int dtype, int64_t M, int C, const void* x, const void* dout, float p,
+                           const int64_t* rng, int site, void* dx, float* partial, int64_t partial_floats,
+                           void* stream);
 /* out[j] += sum_b x[b*L + j] (position-embedding gradient) */
 int dfcsa_batch_sum(int dtype, int B, int64_t L, const void* x, float* out, void* stream);
 int dfcsa_rng_advance(int64_t* state, void* stream);

@@ -532,3 +532,36 @@ def test_upsample_ac_planes_vs_torch(H, W, s):
     y.backward(g)
     yr.backward(g)
     assert rel(x.grad, xr.grad) < 1e-6
+
+
+@pytest.mark.parametrize("gelu", [False, True])
+@pytest.mark.parametrize("M,C,p", [(1568, 768, 0.1), (1568, 3072, 0.1), (200, 64, 0.0), (77, 136, 0.3)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_drop_bwd_column_partials(M, C, p, gelu, dtype):
+    """dfcsa_(gelu_)drop_bwd_cs: the same output as the flat dropout / GELU-dropout backward, and the
+    same per-64-row column partials as dfcsa_colsum_partial over that output (bitwise)."""
+    call, P, dt, stream = lib()
+    from dfcsa._lib import LIB
+    torch.manual_seed(M + C)
+    rng = torch.tensor([12345, 0], dtype=torch.int64, device="cuda")
+    x = torch.randn(M, C, device="cuda").to(dtype)
+    dout = torch.randn(M, C, device="cuda")
+    if gelu:
+        dout = dout.to(dtype)
+    ref = torch.empty(M, C, device="cuda", dtype=dtype)
+    got = torch.empty_like(ref)
+    nt = LIB.dfcsa_colsum_ntiles(M)
+    pref = torch.empty(nt * C, device="cuda")
+    pgot = torch.empty(nt * C, device="cuda")
+    if gelu:
+        call("dfcsa_gelu_drop_bwd", dt(dtype), M * C, P(x), P(dout), float(p), P(rng), 7, P(ref), stream())
+        call("dfcsa_gelu_drop_bwd_cs", dt(dtype), M, C, P(x), P(dout), float(p), P(rng), 7, P(got), P(pgot),
+             pgot.numel(), stream())
+    else:
+        call("dfcsa_drop_bwd", dt(dtype), M * C, P(dout), float(p), P(rng), 7, P(ref), stream())
+        call("dfcsa_drop_bwd_cs", dt(dtype), M, C, P(dout), float(p), P(rng), 7, P(got), P(pgot), pgot.numel(),
+             stream())
+    call("dfcsa_colsum_partial", dt(dtype), M, C, P(ref), P(pref), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
+    assert torch.equal(pref, pgot)
