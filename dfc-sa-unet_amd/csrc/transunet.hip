@@ -1824,6 +1824,37 @@ __global__ void __launch_bounds__(256) heads_relayout_kernel(int unpack, int B, 
   }
 }
 
+// unpack (head-major -> token-major) of dfcsa_heads_relayout with the column sums of the token-major
+// output per COLSUM_ROWS-row tile (partial [tile][ld]): the q / k / v bias gradients of the
+// attention backward without a colsum pass over dqkv.  Thread = one 8-element chunk column of a
+// row tile; the sums add the stored (bf16) values in row order, as colsum_partial does.
+__global__ void __launch_bounds__(256) heads_unpack_cs_kernel(int B, int N, int heads, int dh, int nparts,
+                                                              float scale0, const bf16_t* __restrict__ src,
+                                                              bf16_t* __restrict__ dst, float* __restrict__ partial) {
+  const int D = heads * dh, ld = nparts * D, cpr = ld / 8;
+  const int ck = blockIdx.x * 256 + threadIdx.x;
+  if (ck >= cpr) return;
+  const int col = ck * 8;
+  const int p = col / D, rem = col - p * D, h = rem / dh, j = rem - h * dh;
+  const int64_t M = (int64_t)B * N;
+  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+  const float sc = p == 0 ? scale0 : 1.f;
+  float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  for (int64_t m = r0; m < r1; ++m) {
+    const int b = (int)(m / N), n = (int)(m - (int64_t)b * N);
+    const int64_t hm = ((int64_t)(h * B + b) * N + n) * (nparts * dh) + p * dh + j;
+    float v[8];
+    load8<bf16_t>(src + hm, v);
+    if (sc != 1.f)
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[q] *= sc;
+    store8<bf16_t>(dst + m * ld + col, v);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) acc[q] += bf2f(f2bf(v[q]));
+  }
+  st8f(partial + (size_t)blockIdx.y * ld + col, acc);
+}
+
 // ------------------------------------------------------------ attention launch helpers
 template <typename T, int DH>
 int mha_launch(int B, int N, int heads, int ldq, float scale, const void* qkv, const void* ctx, const void* dctx,
@@ -2213,6 +2244,20 @@ extern "C" int dfcsa_heads_relayout(int unpack, int B, int N, int heads, int dh,
   const int64_t chunks = (int64_t)B * N * nparts * heads * dh / 8;
   hipLaunchKernelGGL(heads_relayout_kernel, dim3(grid_for(chunks)), dim3(256), 0, (hipStream_t)stream, unpack, B, N,
                      heads, dh, nparts, scale0, (const bf16_t*)src, (bf16_t*)dst);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_heads_unpack_cs(int B, int N, int heads, int dh, int nparts, float scale0, const void* src,
+                                     void* dst, float* partial, int64_t partial_floats, void* stream) {
+  if (B <= 0 || N <= 0 || heads <= 0 || dh <= 0 || dh % 8 || nparts <= 0 || !src || !dst || !partial)
+    return DFCSA_EINVAL;
+  const int64_t M = (int64_t)B * N, ld = (int64_t)nparts * heads * dh;
+  const int64_t nt = (M + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  if (nt * ld > partial_floats) return DFCSA_EINVAL;
+  dim3 grid((unsigned)((ld / 8 + 255) / 256), (unsigned)nt);
+  hipLaunchKernelGGL(heads_unpack_cs_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, N, heads, dh, nparts, scale0,
+                     (const bf16_t*)src, (bf16_t*)dst, partial);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -513,8 +513,9 @@ def mha_flash_forward(dtype, qkv, B, N, heads, dh):
     return cx, (qkv_h, o_h, one, lse)
 
 
-def mha_flash_backward(dtype, saved, dcx, B, N, heads, dh):
-    """d(qkv) [B*N][3*heads*dh] from d(ctx) (the dQ and dK/dV flash kernels; dq rescaled)."""
+def mha_flash_backward(dtype, saved, dcx, B, N, heads, dh, col_partial=None):
+    """d(qkv) [B*N][3*heads*dh] from d(ctx) (the dQ and dK/dV flash kernels; dq rescaled).  With
+    col_partial (fp32 [ceil(B*N/64)][3*heads*dh]) the unpack also writes dqkv's column partials."""
     qkv_h, o_h, one, lse = saved
     dev = o_h.device
     Bh, scale = heads * B, 1.0 / math.sqrt(dh)
@@ -526,7 +527,11 @@ def mha_flash_backward(dtype, saved, dcx, B, N, heads, dh):
     call("dfcsa_fra_bwd", dt(dtype), Bh, N, dh, dh, 3 * dh, P(qkv_h), P(dcx_h), P(one), P(lse), P(rvec), P(dqkv_h),
          stream())
     dqkv = torch.empty((B * N, 3 * heads * dh), dtype=dtype, device=dev)
-    call("dfcsa_heads_relayout", 1, B, N, heads, dh, 3, float(scale), P(dqkv_h), P(dqkv), stream())
+    if col_partial is not None:
+        call("dfcsa_heads_unpack_cs", B, N, heads, dh, 3, float(scale), P(dqkv_h), P(dqkv), P(col_partial),
+             col_partial.numel(), stream())
+    else:
+        call("dfcsa_heads_relayout", 1, B, N, heads, dh, 3, float(scale), P(dqkv_h), P(dqkv), stream())
     return dqkv
 
 
@@ -630,6 +635,7 @@ class ViTBlock(torch.autograd.Function):
             _colsum_rows_into(pa, M, D, grad_of(att.out.bias))
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
+        pq = None
         if ctx.probs is not None:
             dqkv = torch.empty_like(qkv)
             dscores = _f32((B * heads * N * N,), dev)
@@ -638,7 +644,8 @@ class ViTBlock(torch.autograd.Function):
             ctx.probs = None
             del dscores
         elif ctx.flash is not None:
-            dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh).view_as(qkv)
+            pq = _f32((LIB.dfcsa_colsum_ntiles(M) * 3 * D,), dev)   # dqkv's column partials (q/k/v biases)
+            dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh, col_partial=pq).view_as(qkv)
             ctx.flash = None
         else:
             dqkv = torch.empty_like(qkv)
@@ -646,12 +653,16 @@ class ViTBlock(torch.autograd.Function):
             call("dfcsa_mha_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(dcx), P(lse), P(dvec),
                  P(dqkv), stream())
         del dcx
-        with side_or_main(dev, dqkv, y1):
+        with side_or_main(dev, dqkv, y1, pq):
             ops.conv_wgrad_into(dtype, [dqkv], 3 * D, [(y1, 0, 0)], D, grid, hw,
                                 [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],
                                 1, D, D, layout=2)
-            channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
-                              grad_of(att.value.bias))
+            if pq is not None:
+                call("dfcsa_slab_colsum3", P(pq), LIB.dfcsa_colsum_ntiles(M), 3 * D, D, D,
+                     P(grad_of(att.query.bias)), P(grad_of(att.key.bias)), P(grad_of(att.value.bias)), stream())
+            else:
+                channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
+                                  grad_of(att.value.bias))
         dy1 = _gemm_1x1(dtype, dqkv, pk["Wqkvt"], rup(3 * D, KA), D, torch.empty((B, gh, gw, D), dtype=dtype,
                                                                                   device=dev))
         del dqkv

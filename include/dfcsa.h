@@ -707,6 +707,11 @@ int dfcsa_rng_advance(int64_t* state, void* stream);
  * gamma = 1, x = 0) run the ViT's multi-head attention with q pre-scaled by 1/sqrt(dh). */
 int dfcsa_heads_relayout(int unpack, int B, int N, int heads, int dh, int nparts, float scale0, const void* src,
                          void* dst, void* stream);
+/* dfcsa_heads_relayout(unpack = 1) (bf16) that also writes the column sums of the token-major output
+ * per 64-row tile: partial [ceil(B*N / 64)][nparts*heads*dh] for dfcsa_slab_colsum3 (the q / k / v
+ * bias gradients; round 5). */
+int dfcsa_heads_unpack_cs(int B, int N, int heads, int dh, int nparts, float scale0, const void* src, void* dst,
+                          float* partial, int64_t partial_floats, void* stream);
 int dfcsa_mha_fwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv, void* ctx,
                   float* lse, void* stream);
 int dfcsa_mha_bwd(int dtype, int B, int N, int heads, int dh, int ldq, float scale, const void* qkv,

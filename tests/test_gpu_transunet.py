@@ -565,3 +565,26 @@ def test_drop_bwd_column_partials(M, C, p, gelu, dtype):
     torch.cuda.synchronize()
     assert torch.equal(ref, got)
     assert torch.equal(pref, pgot)
+
+
+@pytest.mark.parametrize("B,N,heads,dh", [(8, 196, 12, 64), (2, 50, 3, 16)])
+def test_heads_unpack_column_partials(B, N, heads, dh):
+    """dfcsa_heads_unpack_cs: the token-major unpack of dfcsa_heads_relayout (dq scaled) and the
+    per-64-row column partials of dfcsa_colsum_partial over it, bitwise."""
+    call, P, dt, stream = lib()
+    from dfcsa._lib import LIB
+    torch.manual_seed(B * N)
+    src = torch.randn(heads * B, N, 3 * dh, device="cuda").to(torch.bfloat16)
+    M, ld = B * N, 3 * heads * dh
+    ref = torch.empty(M, ld, device="cuda", dtype=torch.bfloat16)
+    got = torch.empty_like(ref)
+    nt = LIB.dfcsa_colsum_ntiles(M)
+    pref = torch.empty(nt * ld, device="cuda")
+    pgot = torch.empty(nt * ld, device="cuda")
+    scale = 1.0 / math.sqrt(dh)
+    call("dfcsa_heads_relayout", 1, B, N, heads, dh, 3, float(scale), P(src), P(ref), stream())
+    call("dfcsa_heads_unpack_cs", B, N, heads, dh, 3, float(scale), P(src), P(got), P(pgot), pgot.numel(), stream())
+    call("dfcsa_colsum_partial", dt(torch.bfloat16), M, ld, P(ref), P(pref), stream())
+    torch.cuda.synchronize()
+    assert torch.equal(ref, got)
+    assert torch.equal(pref, pgot)
