@@ -958,7 +958,9 @@ __global__ void gelu_drop_bwd_kernel(int64_t n, const T* __restrict__ x, const T
   }
 }
 
-constexpr int COLSUM_ROWS = 64;   // rows per column-sum tile (colsum_partial, the *_cs passes)
+constexpr int COLSUM_ROWS = 64;   // rows per column-sum tile of colsum_partial
+constexpr int CS_ROWS = 16;       // rows per tile of the passes that also emit column partials (*_cs):
+                                  // at the ViT's M = 1568 a 64-row tile left 25 row tiles, too few workgroups
 
 // drop_bwd / gelu_drop_bwd over a [M][C] matrix with the column sums of their (stored) output per
 // COLSUM_ROWS-row tile: partial[tile][C] for dfcsa_slab_colsum3 -- the Linear bias gradient of the
@@ -974,7 +976,7 @@ __global__ void __launch_bounds__(256) drop_bwd_cs_kernel(int64_t M, int C, cons
   if (c0 >= C) return;
   const uint64_t key = p > 0.f ? drop_key(rng, site) : 0;
   const float scale = p > 0.f ? 1.f / (1.f - p) : 1.f;
-  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   for (int64_t r = r0; r < r1; r += 4) {
     const int nr = (int)min((int64_t)4, r1 - r);
@@ -1837,20 +1839,28 @@ __global__ void __launch_bounds__(256) heads_unpack_cs_kernel(int B, int N, int 
   const int col = ck * 8;
   const int p = col / D, rem = col - p * D, h = rem / dh, j = rem - h * dh;
   const int64_t M = (int64_t)B * N;
-  const int64_t r0 = (int64_t)blockIdx.y * COLSUM_ROWS, r1 = min(M, r0 + COLSUM_ROWS);
+  const int64_t r0 = (int64_t)blockIdx.y * CS_ROWS, r1 = min(M, r0 + CS_ROWS);
   const float sc = p == 0 ? scale0 : 1.f;
   float acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  for (int64_t m = r0; m < r1; ++m) {
-    const int b = (int)(m / N), n = (int)(m - (int64_t)b * N);
-    const int64_t hm = ((int64_t)(h * B + b) * N + n) * (nparts * dh) + p * dh + j;
-    float v[8];
-    load8<bf16_t>(src + hm, v);
-    if (sc != 1.f)
+  for (int64_t m0 = r0; m0 < r1; m0 += 4) {
+    const int nr = (int)min((int64_t)4, r1 - m0);
+    float v[4][8];
 #pragma unroll
-      for (int q = 0; q < 8; ++q) v[q] *= sc;
-    store8<bf16_t>(dst + m * ld + col, v);
+    for (int u = 0; u < 4; ++u) {   // 4 rows' loads in flight (rows past the tile re-load the last)
+      const int64_t m = m0 + min(u, nr - 1);
+      const int b = (int)(m / N), n = (int)(m - (int64_t)b * N);
+      load8<bf16_t>(src + ((int64_t)(h * B + b) * N + n) * (nparts * dh) + p * dh + j, v[u]);
+    }
 #pragma unroll
-    for (int q = 0; q < 8; ++q) acc[q] += bf2f(f2bf(v[q]));
+    for (int u = 0; u < 4; ++u) {
+      if (u >= nr) break;
+      if (sc != 1.f)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) v[u][q] *= sc;
+      store8<bf16_t>(dst + (m0 + u) * ld + col, v[u]);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) acc[q] += bf2f(f2bf(v[u][q]));
+    }
   }
   st8f(partial + (size_t)blockIdx.y * ld + col, acc);
 }
@@ -2194,7 +2204,7 @@ static int launch_drop_cs(int dtype, int64_t M, int C, const void* x, const void
   if (M <= 0 || C <= 0 || C % 8 || p < 0.f || p >= 1.f || (p > 0.f && !rng) || !dout || !out || !partial ||
       (GELU && !x))
     return DFCSA_EINVAL;
-  const int64_t nt = (M + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  const int64_t nt = (M + CS_ROWS - 1) / CS_ROWS;
   if (nt * C > partial_floats) return DFCSA_EINVAL;
   dim3 grid((C / 8 + 255) / 256, (unsigned)nt);
   if (dtype == DFCSA_DT_BF16)
@@ -2206,6 +2216,8 @@ static int launch_drop_cs(int dtype, int64_t M, int C, const void* x, const void
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
+
+extern "C" int dfcsa_cs_ntiles(int64_t M) { return (int)((M + CS_ROWS - 1) / CS_ROWS); }
 
 extern "C" int dfcsa_drop_bwd_cs(int dtype, int64_t M, int C, const float* dout, float p, const int64_t* rng, int site,
                                  void* da, float* partial, int64_t partial_floats, void* stream) {
@@ -2253,7 +2265,7 @@ extern "C" int dfcsa_heads_unpack_cs(int B, int N, int heads, int dh, int nparts
   if (B <= 0 || N <= 0 || heads <= 0 || dh <= 0 || dh % 8 || nparts <= 0 || !src || !dst || !partial)
     return DFCSA_EINVAL;
   const int64_t M = (int64_t)B * N, ld = (int64_t)nparts * heads * dh;
-  const int64_t nt = (M + COLSUM_ROWS - 1) / COLSUM_ROWS;
+  const int64_t nt = (M + CS_ROWS - 1) / CS_ROWS;
   if (nt * ld > partial_floats) return DFCSA_EINVAL;
   dim3 grid((unsigned)((ld / 8 + 255) / 256), (unsigned)nt);
   hipLaunchKernelGGL(heads_unpack_cs_kernel, grid, dim3(256), 0, (hipStream_t)stream, B, N, heads, dh, nparts, scale0,

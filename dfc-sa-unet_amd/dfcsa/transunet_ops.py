@@ -193,7 +193,7 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
 def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
     """dropout backward (x given: GELU + dropout backward) of dout [M][C] into out, returning the
     per-64-row column partials of out (the bias gradient of the GEMM whose dY out is)."""
-    part = _f32((LIB.dfcsa_colsum_ntiles(M) * C,), out.device)
+    part = _f32((LIB.dfcsa_cs_ntiles(M) * C,), out.device)
     if x is None:
         call("dfcsa_drop_bwd_cs", dt(dtype), M, C, P(dout), float(p), P(rng), site, P(out), P(part), part.numel(),
              stream())
@@ -205,7 +205,7 @@ def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
 
 def _colsum_rows_into(part, M, C, out):
     """out[c] += the sum of the column-partial rows of _drop_bwd_cs."""
-    call("dfcsa_slab_colsum3", P(part), LIB.dfcsa_colsum_ntiles(M), C, C, 0, P(out), None, None, stream())
+    call("dfcsa_slab_colsum3", P(part), LIB.dfcsa_cs_ntiles(M), C, C, 0, P(out), None, None, stream())
 
 
 def bias_grad_into(dtype, dy, bias):
@@ -644,7 +644,7 @@ class ViTBlock(torch.autograd.Function):
             ctx.probs = None
             del dscores
         elif ctx.flash is not None:
-            pq = _f32((LIB.dfcsa_colsum_ntiles(M) * 3 * D,), dev)   # dqkv's column partials (q/k/v biases)
+            pq = _f32((LIB.dfcsa_cs_ntiles(M) * 3 * D,), dev)   # dqkv's column partials (q/k/v biases)
             dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh, col_partial=pq).view_as(qkv)
             ctx.flash = None
         else:
@@ -658,7 +658,7 @@ class ViTBlock(torch.autograd.Function):
                                 [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],
                                 1, D, D, layout=2)
             if pq is not None:
-                call("dfcsa_slab_colsum3", P(pq), LIB.dfcsa_colsum_ntiles(M), 3 * D, D, D,
+                call("dfcsa_slab_colsum3", P(pq), LIB.dfcsa_cs_ntiles(M), 3 * D, D, D,
                      P(grad_of(att.query.bias)), P(grad_of(att.key.bias)), P(grad_of(att.value.bias)), stream())
             else:
                 channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),

@@ -687,9 +687,10 @@ int dfcsa_gelu_drop_fwd(int dtype, int64_t n, const void* x, float p, const int6
 int dfcsa_gelu_drop_bwd(int dtype, int64_t n, const void* x, const void* dout, float p, const int64_t* rng, int site,
                         void* dx, void* stream);
 /* dfcsa_drop_bwd / dfcsa_gelu_drop_bwd over [M][C] (C % 8 == 0) that also write the column sums of
- * their output per 64-row tile: partial [ceil(M / 64)][C] (capacity partial_floats), reduced by
+ * their output per 16-row tile: partial [dfcsa_cs_ntiles(M)][C] (capacity partial_floats), reduced by
  * dfcsa_slab_colsum3 -- the Linear bias gradient of the GEMM whose dY the output is, without a
  * dfcsa_colsum_partial pass (round 5).  The outputs equal the flat kernels'. */
+int dfcsa_cs_ntiles(int64_t M);   /* ceil(M / 16): partial rows of the *_cs passes */
 int dfcsa_drop_bwd_cs(int dtype, int64_t M, int C, const float* dout, float p, const int64_t* rng, int site,
                       void* da, float* partial, int64_t partial_floats, void* stream);
 int dfcsa_gelu_drop_bwd_cs(int dtype, int64_t M, int C, const void* x, const void* dout, float p,
@@ -708,7 +709,7 @@ int dfcsa_rng_advance(int64_t* state, void* stream);
 int dfcsa_heads_relayout(int unpack, int B, int N, int heads, int dh, int nparts, float scale0, const void* src,
                          void* dst, void* stream);
 /* dfcsa_heads_relayout(unpack = 1) (bf16) that also writes the column sums of the token-major output
- * per 64-row tile: partial [ceil(B*N / 64)][nparts*heads*dh] for dfcsa_slab_colsum3 (the q / k / v
+ * per 16-row tile: partial [dfcsa_cs_ntiles(B*N)][nparts*heads*dh] for dfcsa_slab_colsum3 (the q / k / v
  * bias gradients; round 5). */
 int dfcsa_heads_unpack_cs(int B, int N, int heads, int dh, int nparts, float scale0, const void* src, void* dst,
                           float* partial, int64_t partial_floats, void* stream);
