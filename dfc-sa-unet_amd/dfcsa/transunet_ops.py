@@ -190,9 +190,24 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
 
 
+# the Linear bias gradients from column partials formed by the pass that writes dY (dropout / GELU
+# backward, the dqkv unpack: DFCSA_TU_CS=1) instead of a column-sum pass over dY
+TU_CS = [os.environ.get("DFCSA_TU_CS", "1") == "1"]
+
+
 def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
     """dropout backward (x given: GELU + dropout backward) of dout [M][C] into out, returning the
-    per-64-row column partials of out (the bias gradient of the GEMM whose dY out is)."""
+    per-16-row column partials of out (the bias gradient of the GEMM whose dY out is); without TU_CS
+    the flat pass + dfcsa_colsum_partial (64-row partials: returned as (part, rows))."""
+    if not TU_CS[0]:
+        if x is None:
+            call("dfcsa_drop_bwd", dt(dtype), M * C, P(dout), float(p), P(rng), site, P(out), stream())
+        else:
+            call("dfcsa_gelu_drop_bwd", dt(dtype), M * C, P(x), P(dout), float(p), P(rng), site, P(out), stream())
+        nt = LIB.dfcsa_colsum_ntiles(M)
+        part = _f32((nt * C,), out.device)
+        call("dfcsa_colsum_partial", dt(dtype), M, C, P(out), P(part), stream())
+        return part
     part = _f32((LIB.dfcsa_cs_ntiles(M) * C,), out.device)
     if x is None:
         call("dfcsa_drop_bwd_cs", dt(dtype), M, C, P(dout), float(p), P(rng), site, P(out), P(part), part.numel(),
@@ -205,7 +220,7 @@ def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
 
 def _colsum_rows_into(part, M, C, out):
     """out[c] += the sum of the column-partial rows of _drop_bwd_cs."""
-    call("dfcsa_slab_colsum3", P(part), LIB.dfcsa_cs_ntiles(M), C, C, 0, P(out), None, None, stream())
+    call("dfcsa_slab_colsum3", P(part), part.numel() // C, C, C, 0, P(out), None, None, stream())
 
 
 def bias_grad_into(dtype, dy, bias):
@@ -644,7 +659,7 @@ class ViTBlock(torch.autograd.Function):
             ctx.probs = None
             del dscores
         elif ctx.flash is not None:
-            pq = _f32((LIB.dfcsa_cs_ntiles(M) * 3 * D,), dev)   # dqkv's column partials (q/k/v biases)
+            pq = _f32((LIB.dfcsa_cs_ntiles(M) * 3 * D,), dev) if TU_CS[0] else None   # dqkv's column partials
             dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh, col_partial=pq).view_as(qkv)
             ctx.flash = None
         else:
