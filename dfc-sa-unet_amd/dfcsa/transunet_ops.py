@@ -191,8 +191,10 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
 
 
 # the Linear bias gradients from column partials formed by the pass that writes dY (dropout / GELU
-# backward, the dqkv unpack: DFCSA_TU_CS=1) instead of a column-sum pass over dY
-TU_CS = [os.environ.get("DFCSA_TU_CS", "1") == "1"]
+# backward, the dqkv unpack: DFCSA_TU_CS=1) instead of a column-sum pass over dY.  Off: the row-tiled
+# passes give the per-element dropout hash to a quarter of the threads of the flat kernels, which
+# costs more than the column-sum launch they save (config 4 bf16, same box: 600 vs 609 img/s)
+TU_CS = [os.environ.get("DFCSA_TU_CS", "0") == "1"]
 
 
 def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
