@@ -2423,7 +2423,10 @@ struct FwdPro {
   float sh, sw;       // bilinear source scales P / H, P / W
 };
 
-template <int PRO, int C>
+// SB (single buffer, C = 128; knob 43): one A-image slot instead of two, so two workgroups fit per
+// CU (65 instead of 113 KiB of LDS); the next tile's DMA is issued once every wave has finished its
+// MFMA reads of the slot and flies during the epilogue
+template <int PRO, int C, bool SB = false>
 __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
   using T = bf16_t;
   static_assert(C == 64 || C == 128, "prologue GEMM widths");
@@ -2437,7 +2440,7 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   constexpr int IMG = 64 * 128, SLOT = KS * IMG;
   constexpr int OSTR = NWG * 2 + 16;
   constexpr int NSTORE = (64 * (NWG / 8)) / 256, OCH = NWG / 8;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[(SB ? 1 : 2) * SLOT];
   __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -2499,7 +2502,7 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
   issue(t, 0);
   int slot = 0;
   bool first_iter = true;
-  for (; t < mtiles; t += gridDim.x, slot ^= 1) {
+  for (; t < mtiles; t += gridDim.x, slot ^= (SB ? 0 : 1)) {
     const int tn = t + gridDim.x;
     // LightSelfAttention taps of this tile's pixels, loaded before the next tile's DMA
     float ov[NITEM][4][8], lw[NITEM][4];
@@ -2522,7 +2525,10 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
     }
     // outstanding, in issue order: DMA(t), [o taps], the previous tile's prologue + FN stats +
     // NSTORE output stores (no stats stores: kept in registers), DMA(tn): the counted wait retires DMA(t)
-    if constexpr (PRO == PRO_GATE_FUSION) {   // no loads besides the DMAs: leave the stores in flight
+    if constexpr (SB) {
+      // this tile's DMA was issued during the previous tile's epilogue (or before the loop)
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if constexpr (PRO == PRO_GATE_FUSION) {   // no loads besides the DMAs: leave the stores in flight
       if (tn < mtiles) {
         issue(tn, slot ^ 1);
         if (first_iter) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * KS) : "memory");
@@ -2595,6 +2601,10 @@ __global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs
 #pragma unroll
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (SB) {
+      lds_barrier();   // every wave's fragment reads of the slot are done
+      if (tn < mtiles) issue(tn, 0);
     }
     const int m0 = t * 64;
     // BatchNorm partial sums of this workgroup's tiles, kept in registers (one slab row per
@@ -3126,13 +3136,23 @@ extern "C" int dfcsa_dgrad_apply_parts(int M, int epi) {
 }
 
 namespace {
-template <int PRO, int C>
-int fwd_pro_grid(int M) {
+int g_pro_sb = 0;   // knob 43: 1 = the single-buffer C = 128 prologue GEMMs (two workgroups per CU)
+
+template <int PRO, int C, bool SB = false>
+int fwd_pro_grid_t(int M) {
   static int occ = 0;
   if (!occ &&
-      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO, C>, 256, 0) != hipSuccess || occ < 1))
+      (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, gate_fusion_fwd_kernel<PRO, C, SB>, 256, 0) != hipSuccess ||
+       occ < 1))
     occ = 1;
   return std::min(256 * occ, (M + 63) / 64);
+}
+template <int PRO, int C>
+int fwd_pro_grid(int M) {
+  if constexpr (C == 128) {
+    if (g_pro_sb) return fwd_pro_grid_t<PRO, C, true>(M);
+  }
+  return fwd_pro_grid_t<PRO, C>(M);
 }
 
 template <int PRO, int C>
@@ -3151,6 +3171,13 @@ int launch_fwd_pro(ConvGemmArgs& a, const FwdPro& pro, int64_t stats_cap, hipStr
   }
   const double moved = PRO == PRO_GATE_FUSION ? 2.0 : 3.0;   // prologue stores + the output
   ProfScope prof(DFCSA_PROF_CONV_STREAM, st, 2.0 * ((double)a.M * a.Kpad + (double)C * a.Kpad + moved * a.M * C));
+  if constexpr (C == 128) {
+    if (g_pro_sb) {
+      hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C, true>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
+      DFCSA_CHECK_LAUNCH();
+      return 0;
+    }
+  }
   hipLaunchKernelGGL((gate_fusion_fwd_kernel<PRO, C>), dim3(gx), dim3(256), 0, st, a, pro, mtiles);
   DFCSA_CHECK_LAUNCH();
   return 0;
@@ -3261,6 +3288,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 39: return g_bn_fold;
     case 40: return g_ppsk;
     case 42: return g_wgrad_bd_nst;
+    case 43: return g_pro_sb;
     case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
@@ -3298,6 +3326,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 39) { g_bn_fold = value; return 0; }
   if (knob == 40) { g_ppsk = value; return 0; }
   if (knob == 42) { g_wgrad_bd_nst = (value == 3 || value == 4) ? value : 2; return 0; }
+  if (knob == 43) { g_pro_sb = value ? 1 : 0; return 0; }
   if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 24; return 0; }
   if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }
