@@ -2124,7 +2124,9 @@ enum { EPI_GATE = 0, EPI_ACC_RELU_BN = 1 };
 template <int KP, int EPI, bool APRO>
 constexpr int gate_wpe() { return (KP == 64 || (KP == 128 && EPI == 0)) ? 2 : 1; }
 
-template <int KP, int EPI, bool APRO = false>
+// SB (single buffer, KP = 256; knob 44): one A-image slot, two workgroups per CU; the next tile's
+// DMA is issued once every wave has finished its MFMA reads and flies during the epilogue
+template <int KP, int EPI, bool APRO = false, bool SB = false>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gate_wpe<KP, EPI, APRO>())))
 dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const ApplyPro ap) {
   using T = bf16_t;
@@ -2134,9 +2136,10 @@ dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const Ap
   constexpr int KSD = APRO ? 2 * KS : KS;   // K stages DMA'd per tile ([src | y] with the prologue)
   constexpr int IMG = 64 * 128, SLOT = KSD * IMG;
   constexpr int OSTR = NWG * 2 + 16;
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  __shared__ __attribute__((aligned(16))) char smem[(SB ? 1 : 2) * SLOT];
   __shared__ __attribute__((aligned(16))) char otile[64 * OSTR];
   __shared__ __attribute__((aligned(16))) float red[4][2][64];
+  static_assert(!SB || (!APRO && KP == 256), "single buffer: the non-prologue KP = 256 variants");
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int M = args.M, C = args.Nd, K = args.K;
@@ -2229,10 +2232,12 @@ dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const Ap
     if constexpr (PIPE) load_pin(t, pin);
   }
   int slot = 0;
-  for (; t < mtiles; t += gridDim.x, slot ^= 1) {
+  for (; t < mtiles; t += gridDim.x, slot ^= (SB ? 0 : 1)) {
     const int tn = t + gridDim.x;
     if constexpr (!PIPE) load_pin(t, pin);
-    if (tn < mtiles) {
+    if constexpr (SB) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // DMA(t) was issued in the previous epilogue
+    } else if (tn < mtiles) {
       issue(tn, slot ^ 1);
       if constexpr (PIPE) {
         load_pin(tn, pnx);
@@ -2281,6 +2286,10 @@ dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const Ap
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i].v, bfr[j][g], acc[i][j], 0, 0, 0);
+    }
+    if constexpr (SB) {
+      lds_barrier();   // every wave's fragment reads of the slot are done
+      if (tn < mtiles) issue(tn, 0);
     }
 #pragma unroll
     for (int j = 0; j < FN; ++j) {
@@ -2365,10 +2374,10 @@ dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const Ap
   }
 }
 
-template <int KP, int EPI, bool APRO = false>
+template <int KP, int EPI, bool APRO = false, bool SB = false>
 int gate_occ() {
   static int occ = 0;
-  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP, EPI, APRO>, 256, 0) !=
+  if (!occ && (hipOccupancyMaxActiveBlocksPerMultiprocessor(&occ, dgrad_gate_kernel<KP, EPI, APRO, SB>, 256, 0) !=
                    hipSuccess ||
                occ < 1))
     occ = 1;
@@ -2382,11 +2391,13 @@ int gate_occ() {
 // Same-box A/B (tools/gpu_r04_gate36.sh): the C = 256 kernels 105 -> 88 and 68 -> 51 us, C = 128
 // acc 60 -> 54 us; step 1587 / 1597 / 1602 -> 1604 / 1607 / 1609 img/s.
 int g_gate_grid_div = 1;   // knob 36
+int g_gate_sb = 0;   // knob 44: 1 = the single-buffer KP = 256 gate dgrad kernels (two workgroups per CU)
 template <int EPI>
 int dgrad_gate_grid(int M, int C, bool apro = false) {
   const int kp = (C + 63) / 64 * 64;
   const int occ = apro ? gate_occ<64, EPI, true>() : kp == 64 ? gate_occ<64, EPI>() : kp == 128 ? gate_occ<128, EPI>()
-                  : kp == 192 ? gate_occ<192, EPI>() : gate_occ<256, EPI>();
+                  : kp == 192 ? gate_occ<192, EPI>() : g_gate_sb ? gate_occ<256, EPI, false, true>()
+                                                                 : gate_occ<256, EPI>();
   const int mtiles = (M + 63) / 64;
   int gx = 256 * occ;
   if (g_gate_grid_div) gx = std::max(1, gx / ((C + 63) / 64));
@@ -3023,6 +3034,8 @@ int launch_gate_epi(const ConvGemmArgs& a, const GateEpi& e, int64_t part_cap, h
   else if (Kpad == 64) hipLaunchKernelGGL((dgrad_gate_kernel<64, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
   else if (Kpad == 128) hipLaunchKernelGGL((dgrad_gate_kernel<128, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
   else if (Kpad == 192) hipLaunchKernelGGL((dgrad_gate_kernel<192, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
+  else if (g_gate_sb)
+    hipLaunchKernelGGL((dgrad_gate_kernel<256, EPI, false, true>), grid, dim3(256), 0, st, a, e, mtiles, none);
   else hipLaunchKernelGGL((dgrad_gate_kernel<256, EPI>), grid, dim3(256), 0, st, a, e, mtiles, none);
   DFCSA_CHECK_LAUNCH();
   return 0;
@@ -3136,7 +3149,8 @@ extern "C" int dfcsa_dgrad_apply_parts(int M, int epi) {
 }
 
 namespace {
-int g_pro_sb = 0;   // knob 43: 1 = the single-buffer C = 128 prologue GEMMs (two workgroups per CU)
+int g_pro_sb = 1;   // knob 43: 1 = the single-buffer C = 128 prologue GEMMs (two workgroups per CU;
+                    // same-box A/B 1644 / 1652 / 1638 vs 1630 / 1632 / 1628 img/s with 0)
 
 template <int PRO, int C, bool SB = false>
 int fwd_pro_grid_t(int M) {
@@ -3289,6 +3303,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 40: return g_ppsk;
     case 42: return g_wgrad_bd_nst;
     case 43: return g_pro_sb;
+    case 44: return g_gate_sb;
     case 38: return g_splitk_target;
     default: return DFCSA_EINVAL;
   }
@@ -3327,6 +3342,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 40) { g_ppsk = value; return 0; }
   if (knob == 42) { g_wgrad_bd_nst = (value == 3 || value == 4) ? value : 2; return 0; }
   if (knob == 43) { g_pro_sb = value ? 1 : 0; return 0; }
+  if (knob == 44) { g_gate_sb = value ? 1 : 0; return 0; }
   if (knob == 37) { g_splitk_min_nk = value > 0 ? value : 24; return 0; }
   if (knob == 38) { g_splitk_target = value > 0 ? value : 600; return 0; }
   if (knob == 16) { g_wgrad_noglds_f32small = value; return 0; }

@@ -867,6 +867,8 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 39: 0 = dfcsa_conv_gemm_bn always launches the separate finalize (no epilogue fold).
  * knob 40: 1 = stream-K decomposition of the 256x256 ping-pong conv tile (default 0: measured slower).
  * knob 42: LDS-DMA ring depth of the buffer-descriptor weight-gradient kernel (2 = default, 3, 4).
+ * knob 43: 1 = single-buffer C = 128 forward prologue GEMMs (two workgroups per CU; default 1).
+ * knob 44: 1 = single-buffer KP = 256 fused gate dgrad kernels (two workgroups per CU).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);
