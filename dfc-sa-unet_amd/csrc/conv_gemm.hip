@@ -2121,13 +2121,13 @@ enum { EPI_GATE = 0, EPI_ACC_RELU_BN = 1 };
 // waves per SIMD the compiler budgets registers for: 2 for the variants whose allocation lands just
 // above 256 VGPR+AGPR (one resident workgroup per CU otherwise): the 224^2 gate and acc/apply
 // variants (280 and 264) and the 112^2 gate variant (272)
-template <int KP, int EPI, bool APRO>
-constexpr int gate_wpe() { return (KP == 64 || (KP == 128 && EPI == 0)) ? 2 : 1; }
+template <int KP, int EPI, bool APRO, bool SB = false>
+constexpr int gate_wpe() { return (KP == 64 || (KP == 128 && EPI == 0) || SB) ? 2 : 1; }
 
 // SB (single buffer, KP = 256; knob 44): one A-image slot, two workgroups per CU; the next tile's
 // DMA is issued once every wave has finished its MFMA reads and flies during the epilogue
 template <int KP, int EPI, bool APRO = false, bool SB = false>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gate_wpe<KP, EPI, APRO>())))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(gate_wpe<KP, EPI, APRO, SB>())))
 dgrad_gate_kernel(const ConvGemmArgs args, const GateEpi e, int mtiles, const ApplyPro ap) {
   using T = bf16_t;
   static_assert(!APRO || KP == 64, "A prologue: C = 64");
@@ -2437,8 +2437,14 @@ struct FwdPro {
 // SB (single buffer, C = 128; knob 43): one A-image slot instead of two, so two workgroups fit per
 // CU (65 instead of 113 KiB of LDS); the next tile's DMA is issued once every wave has finished its
 // MFMA reads of the slot and flies during the epilogue
+// waves per SIMD the compiler budgets registers for (knob-free): 2 for the single-buffer C = 128 gate
+// fusion (284 VGPR+AGPR unconstrained: one wave per SIMD, one workgroup per CU whatever its LDS)
+template <int PRO, int C, bool SB>
+constexpr int pro_wpe() { return (SB && PRO == 0 && C == 128) ? 2 : 1; }
+
 template <int PRO, int C, bool SB = false>
-__global__ void __launch_bounds__(256) gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(pro_wpe<PRO, C, SB>())))
+gate_fusion_fwd_kernel(const ConvGemmArgs args, const FwdPro pr_, int mtiles) {
   using T = bf16_t;
   static_assert(C == 64 || C == 128, "prologue GEMM widths");
   constexpr int NSEG = PRO == PRO_GATE_FUSION ? 3 : 2;
