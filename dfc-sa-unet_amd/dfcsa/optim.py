@@ -15,7 +15,7 @@ import ctypes
 
 import torch
 
-from . import streams
+from . import chanpad, streams
 from ._lib import LIB, call
 from .ops import P, stream
 
@@ -111,6 +111,16 @@ class FusedSGD(torch.optim.Optimizer):
         self._grads_zeroed = bool(self.zero_after_step)
         return loss
 
+    def state_dict(self):
+        """torch.optim.SGD's format; momentum buffers of channel-padded parameters (dfcsa.chanpad)
+        in their reference shapes."""
+        sd = super().state_dict()
+        for i, p in enumerate(self.param_groups[0]["params"]):
+            st = sd["state"].get(i)
+            if st is not None and st.get("momentum_buffer") is not None and hasattr(p, "_dfcsa_pad"):
+                sd["state"][i] = dict(st, momentum_buffer=chanpad.logical(p, st["momentum_buffer"]).clone())
+        return sd
+
     def load_state_dict(self, state_dict):
         """torch.optim.SGD state (e.g. a reference checkpoint's optimizer_state_dict): the loaded
         momentum buffers are copied into the flat momentum storage -- now if it exists, otherwise
@@ -126,7 +136,7 @@ class FusedSGD(torch.optim.Optimizer):
                 self._mom.zero_()
             return
         flat = getattr(params[0], "_dfcsa_flat", None)
-        self._pending_mom = {id(p): b.detach().clone() for p, b in zip(params, bufs)}
+        self._pending_mom = {id(p): chanpad.padded(p, b.detach()).clone() for p, b in zip(params, bufs)}
         self._flat = None
         if flat is not None and flat.valid():
             self._resolve()

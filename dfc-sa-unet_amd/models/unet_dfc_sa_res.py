@@ -16,7 +16,7 @@ import torch
 import torch.nn as nn
 
 import dfcsa
-from dfcsa import packs
+from dfcsa import chanpad, packs
 from dfcsa.block import DFCBlockFunction, DFCBlockPoolFunction, LSAFunction
 from dfcsa.flat import FlatParams
 from dfcsa.functions import ConvTranspose2x2, Head1x1, InputToNHWC, MaxPoolFork, ResizeBilinear
@@ -110,9 +110,6 @@ class UNetDFCSA(nn.Module):
                  ablation_on_qk_channels=8, precision=None):
         super().__init__()
         f = list(features)
-        for c in f:
-            if c % 8:
-                raise ValueError(f"feature widths must be multiples of 8 for the NHWC kernels, got {f}")
         blk = lambda i, o: self._make_block(i, o, pool_size, ablation_on_qk_channels)  # noqa: E731
         self.pool_size = pool_size
         self.in_channels = in_channels
@@ -136,6 +133,10 @@ class UNetDFCSA(nn.Module):
         self.final_conv = nn.Conv2d(f[0], out_channels, kernel_size=1)
         self.compute_dtype = dfcsa.resolve_dtype(precision)
         self._flat = None
+        if any(c % 8 for c in f):
+            # widths the 16-byte channel chunks cannot address: zero-pad every channel dimension
+            # after the reference's construction (same init); state_dict stays logical (chanpad)
+            chanpad.pad_model(self, f, in_channels, out_channels)
 
     def _make_block(self, in_channels, out_channels, pool_size, ablation_on_qk_channels):
         """Block factory (AblationUNetBase's block_func, unet_dfc_sa_ablation_branches.py:105)."""

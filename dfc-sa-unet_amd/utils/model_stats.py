@@ -29,12 +29,14 @@ import os
 import torch
 import yaml
 
+from dfcsa import chanpad
+
 
 def count_parameters(model):
     """Parameter totals (reference model_stats.py:15-36)."""
     rows, total, trainable = [], 0, 0
     for name, p in model.named_parameters():
-        n = p.numel()
+        n = chanpad.numel(p)   # reference shape for channel-padded widths (dfcsa/chanpad.py)
         rows.append((name, n))
         total += n
         if p.requires_grad:
@@ -68,7 +70,8 @@ def _conv_mod(m, h, w):
     """FLOPs and output size of an nn.Conv2d at input h x w (flop_counter: 2 * out * Cin/g * k^2)."""
     kh, kw = m.kernel_size
     ho, wo = _out(h, kh, m.stride[0], m.padding[0]), _out(w, kw, m.stride[1], m.padding[1])
-    return 2.0 * ho * wo * m.out_channels * (m.in_channels // m.groups) * kh * kw, ho, wo
+    cin, cout = chanpad.io_channels(m)
+    return 2.0 * ho * wo * cout * (cin // m.groups) * kh * kw, ho, wo
 
 
 def _block_flops(blk, h, w):
@@ -82,10 +85,10 @@ def _block_flops(blk, h, w):
         f += _conv_mod(conv_branch[0], h, w)[0]        # local 3x3 branch
     if attn_branch is not None:
         entry = attn_branch[0]
-        c = entry.out_channels
-        f += _conv(entry.in_channels, c, 1, h, w)       # attention entry 1x1
+        cin, c = chanpad.io_channels(entry)
+        f += _conv(cin, c, 1, h, w)                     # attention entry 1x1
         att = attn_branch[3]
-        cq = att.query_conv.out_channels
+        cq = chanpad.io_channels(att.query_conv)[1]
         if getattr(att, "full_resolution", False):
             n, hp, wp = h * w, h, w                     # unet_dfc_sa_ablation_attention.py:15-26
         else:
@@ -114,11 +117,11 @@ def _dfc_unet_flops(model, h, w):
     for up, blk, (sh, sw) in zip((model.up4, model.up3, model.up2, model.up1),
                                  (model.up_conv4, model.up_conv3, model.up_conv2, model.up_conv1),
                                  reversed(sizes)):
-        f += 2.0 * h * w * up.in_channels * up.out_channels * 4   # ConvTranspose2d(k2, s2)
+        f += 2.0 * h * w * chanpad.io_channels(up)[0] * chanpad.io_channels(up)[1] * 4   # ConvTranspose2d(k2, s2)
         h, w = sh, sw                                    # (bilinear fix to the skip size)
         f += _block_flops(blk, h, w)
     fc = model.final_conv
-    f += _conv(fc.in_channels, fc.out_channels, 1, h, w)
+    f += _conv(*chanpad.io_channels(fc), 1, h, w)
     return f
 
 
