@@ -708,7 +708,9 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     J = 2 * Cq + C
     S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
-    ws = window_sums and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
+    # the window sums feed the projection backward's extra rows (B*N <= 4096) or the pool-fused
+    # finalize (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
+    ws = window_sums and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C) and (N <= 256 or B * N <= 4096)
     wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
     wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
     call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), P(wpart),
