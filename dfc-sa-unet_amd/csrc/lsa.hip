@@ -765,6 +765,47 @@ extern "C" int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const fl
   return 0;
 }
 
+// Row softmax in place over E [rows][N] (fp32): the pooled attention on the opt-in GEMM path,
+// whose energy / output / gradient products run as batched library GEMMs (block.py).
+__global__ void __launch_bounds__(256) softmax_rows_kernel(int N, float* __restrict__ E) {
+  __shared__ float red[8];
+  float* e = E + (size_t)blockIdx.x * N;
+  float mx = -INFINITY;
+  for (int m = threadIdx.x; m < N; m += 256) mx = fmaxf(mx, e[m]);
+  mx = block_reduce_max(mx, red);
+  float sum = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) sum += __expf(e[m] - mx);
+  sum = block_reduce_sum(sum, red + 4);
+  const float inv = 1.f / sum;
+  for (int m = threadIdx.x; m < N; m += 256) e[m] = __expf(e[m] - mx) * inv;
+}
+
+// Softmax backward in place: dA [rows][N] -> dE = A * (dA - sum_m A dA)
+__global__ void __launch_bounds__(256) softmax_bwd_rows_kernel(int N, const float* __restrict__ A,
+                                                               float* __restrict__ dA) {
+  __shared__ float red[4];
+  const float* a = A + (size_t)blockIdx.x * N;
+  float* d = dA + (size_t)blockIdx.x * N;
+  float s = 0.f;
+  for (int m = threadIdx.x; m < N; m += 256) s += a[m] * d[m];
+  s = block_reduce_sum(s, red);
+  for (int m = threadIdx.x; m < N; m += 256) d[m] = a[m] * (d[m] - s);
+}
+
+extern "C" int dfcsa_softmax_rows_f32(int64_t rows, int N, float* E, void* stream) {
+  if (rows <= 0 || rows > 0x7fffffff || N <= 0 || !E) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, N, E);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_softmax_bwd_rows_f32(int64_t rows, int N, const float* A, float* dA, void* stream) {
+  if (rows <= 0 || rows > 0x7fffffff || N <= 0 || !A || !dA) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(softmax_bwd_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, N, A, dA);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
 extern "C" int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream) {
   size_t shm = (size_t)(Cq + N + 8) * sizeof(float);
   hipLaunchKernelGGL(lsa_attn_kernel, dim3(N, B), dim3(256), shm, (hipStream_t)stream, N, C, Cq, qkv, A, o);

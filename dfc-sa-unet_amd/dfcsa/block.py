@@ -689,6 +689,15 @@ WGRAD_LATE = [os.environ.get("DFCSA_WGRAD_LATE", "1") == "1"]
 ENTRY_WS = [os.environ.get("DFCSA_ENTRY_WS", "1") == "1"]
 
 
+# pooled attention above this many tokens: the N x N products as batched fp32 library GEMMs (the
+# one-workgroup-per-query-row kernels are sized for P <= 8; at P = 32 they were 68 of 79 ms/step).
+# Measured at 224^2, B = 16 with DFCSA_LSA_GEMM_MIN_N=64: P = 16 981 -> 1173 img/s, P = 32 201 -> 858.
+# OFF by default: the model-level gradients against the float64 oracle at P = 16 came out ~1e-2
+# relative on some tensors with it against ~1e-5 on the per-row kernels (tools/pool_path_diag2.py),
+# not yet explained (the batched GEMMs themselves are fp32-exact, tools/bmm_precision_check.py)
+LSA_GEMM_MIN_N = int(os.environ.get("DFCSA_LSA_GEMM_MIN_N", str(1 << 30)))
+
+
 def _lsa_gemm_ok(C, J):
     return C % 8 == 0 and J % 8 == 0 and C >= 64
 
@@ -730,7 +739,13 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
         call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
     A = torch.empty((B, N, N), device=dev, dtype=f32)
     o = torch.empty((B, N, C), device=dev, dtype=f32)
-    call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
+    if N > LSA_GEMM_MIN_N:
+        # q k^T and A v as batched fp32 library GEMMs, the row softmax in place between them
+        torch.bmm(qkv[:, :, :Cq], qkv[:, :, Cq:2 * Cq].transpose(1, 2), out=A)
+        call("dfcsa_softmax_rows_f32", ctypes.c_int64(B * N), N, P(A), stream())
+        torch.bmm(A, qkv[:, :, 2 * Cq:], out=o)
+    else:
+        call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
     if window_sums:
         return pooled, qkv, A, o, Wqkv, wsum
     return pooled, qkv, A, o, Wqkv
@@ -764,8 +779,17 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
         gpart = torch.empty(B * N, device=dev, dtype=f32)
         call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
              P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
-        dE = torch.empty((B, N, N), device=dev, dtype=f32)
-        call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
+        if N > LSA_GEMM_MIN_N:
+            # dA = dO v^T; dE = A (dA - rowsum(A dA)) in place; dq = dE k, dk = dE^T q, dv = A^T dO
+            q, k, v = qkv[:, :, :Cq], qkv[:, :, Cq:2 * Cq], qkv[:, :, 2 * Cq:]
+            dE = torch.bmm(dO, v.transpose(1, 2))
+            call("dfcsa_softmax_bwd_rows_f32", ctypes.c_int64(B * N), N, P(A), P(dE), stream())
+            dqkv[:, :, :Cq] = torch.bmm(dE, k)
+            dqkv[:, :, Cq:2 * Cq] = torch.bmm(dE.transpose(1, 2), q)
+            dqkv[:, :, 2 * Cq:] = torch.bmm(A.transpose(1, 2), dO)
+        else:
+            dE = torch.empty((B, N, N), device=dev, dtype=f32)
+            call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
     dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
     qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
     if _lsa_gemm_ok(C, J):

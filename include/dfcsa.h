@@ -468,6 +468,11 @@ int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partia
                   const float* bias, float* pooled, float* qkv, void* stream);
 /* A = softmax_rows(q k^T) [B][N][N]; o[n][c] = sum_m A[n][m] v[m][c]  [B][N][C] */
 int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream);
+/* Pooled attention on the opt-in GEMM path (DFCSA_LSA_GEMM_MIN_N): the energy q k^T, the output A v and the gradient
+ * products run as batched library GEMMs; these two do the row softmax in place over E [rows][N] and
+ * its backward in place over dA (dE = A * (dA - sum_m A dA)). */
+int dfcsa_softmax_rows_f32(int64_t rows, int N, float* E, void* stream);
+int dfcsa_softmax_bwd_rows_f32(int64_t rows, int N, const float* A, float* dA, void* stream);
 /* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
 int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, const void* dattn, int P, float* rows,
                           void* stream);
