@@ -741,9 +741,11 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     o = torch.empty((B, N, C), device=dev, dtype=f32)
     if N > LSA_GEMM_MIN_N:
         # q k^T and A v as batched fp32 library GEMMs, the row softmax in place between them
-        torch.bmm(qkv[:, :, :Cq], qkv[:, :, Cq:2 * Cq].transpose(1, 2), out=A)
+        # (contiguous q / k / v: the column slices of qkv start at arbitrary 4-byte offsets)
+        q, k, v = qkv[:, :, :Cq].contiguous(), qkv[:, :, Cq:2 * Cq].contiguous(), qkv[:, :, 2 * Cq:].contiguous()
+        torch.bmm(q, k.transpose(1, 2), out=A)
         call("dfcsa_softmax_rows_f32", ctypes.c_int64(B * N), N, P(A), stream())
-        torch.bmm(A, qkv[:, :, 2 * Cq:], out=o)
+        torch.bmm(A, v, out=o)
     else:
         call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
     if window_sums:
@@ -781,7 +783,7 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
              P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
         if N > LSA_GEMM_MIN_N:
             # dA = dO v^T; dE = A (dA - rowsum(A dA)) in place; dq = dE k, dk = dE^T q, dv = A^T dO
-            q, k, v = qkv[:, :, :Cq], qkv[:, :, Cq:2 * Cq], qkv[:, :, 2 * Cq:]
+            q, k, v = qkv[:, :, :Cq].contiguous(), qkv[:, :, Cq:2 * Cq].contiguous(), qkv[:, :, 2 * Cq:].contiguous()
             dE = torch.bmm(dO, v.transpose(1, 2))
             call("dfcsa_softmax_bwd_rows_f32", ctypes.c_int64(B * N), N, P(A), P(dE), stream())
             dqkv[:, :, :Cq] = torch.bmm(dE, k)

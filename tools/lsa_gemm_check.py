@@ -15,8 +15,9 @@ def rel(a, b):
     return ((a.double().cpu() - b.double().cpu()).norm() / b.double().cpu().norm()).item()
 
 
+import os
 torch.manual_seed(0)
-C, P = 64, 16
+C, P = int(os.environ.get("C", 64)), 16
 m = LightSelfAttention(C, pool_size=P)
 with torch.no_grad():
     m.gamma.fill_(0.7)
