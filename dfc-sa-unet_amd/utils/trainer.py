@@ -42,6 +42,7 @@ the captured graphs, which hold RCCL kernels referencing the communicator.
 import csv
 import os
 import time
+import weakref
 
 import torch
 import torch.distributed as dist
@@ -58,6 +59,15 @@ try:
 except ImportError:  # pragma: no cover
     def tqdm(it, **kw):
         return it
+
+_LIVE = weakref.WeakSet()   # constructed Trainers (close_all)
+
+
+def close_all():
+    """Trainer.close() on every Trainer still alive (e.g. before dist.destroy_process_group() or at the
+    end of a test): captured graphs and copy streams are released now, in order, not by a finalizer."""
+    for tr in list(_LIVE):
+        tr.close()
 
 
 class Trainer:
@@ -109,6 +119,7 @@ class Trainer:
         self._graphs = {} if use_graphs else None
         self._graph_seen = set()
         self._copy_stream = None   # host batches are uploaded on it, one step ahead (_prefetch)
+        _LIVE.add(self)
         print(f"模型將在 {self.device} 上訓練" + (f" (rank {self.rank}/{self.world})" if self.world > 1 else ""))
 
     # ------------------------------------------------------------------ one step
@@ -127,12 +138,17 @@ class Trainer:
         return self._eager_step(images, masks)
 
     def close(self):
-        """Release the captured step graphs (call before dist.destroy_process_group())."""
+        """Release the captured step graphs and the upload stream (call before
+        dist.destroy_process_group()).  Idempotent; the Trainer can keep training afterwards (it
+        captures again)."""
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
         if self._graphs:
             for g in self._graphs.values():
                 g[0].reset()
             self._drop_graphs()
-        if torch.cuda.is_available():
+        self._copy_stream = None
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
             torch.cuda.synchronize()
 
     def _storage(self):

@@ -1,3 +1,4 @@
+import gc
 import os
 import sys
 
@@ -14,6 +15,41 @@ GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP kernels)")
+    # The GPU tests' torch reference convolutions run on ATen's own kernels, not MIOpen: on the
+    # round-5/6 boxes MIOpen's find step for the 1x1 / stride-2 backward-data of
+    # test_col2im_matches_conv_input_grad failed ("Error setting device", "Empty code object path")
+    # and left the HIP context with an illegal-address error, which then aborted the process when a
+    # tensor was freed at session end (GPUTEST_r05, DESIGN.md "GPU suite abort").  The product path
+    # never calls MIOpen; only the test references did.
+    try:
+        import torch
+        torch.backends.cudnn.enabled = False
+    except ImportError:   # pragma: no cover
+        pass
+
+
+@pytest.fixture(autouse=True)
+def _close_trainers():
+    """Every Trainer a test built releases its captured graphs and copy stream when the test ends."""
+    yield
+    tr = sys.modules.get("utils.trainer")
+    if tr is not None:
+        tr.close_all()
+
+
+@pytest.fixture(autouse=True, scope="module")
+def _release_device_objects():
+    """Free what a test module created (trainers, captured graphs, copy streams, loader iterators)
+    before the next module starts, and surface any asynchronous device error here, attributed to the
+    module that caused it, instead of in a finalizer at interpreter exit."""
+    yield
+    gc.collect()
+    try:
+        import torch
+        if torch.cuda.is_available() and torch.cuda.is_initialized():
+            torch.cuda.synchronize()
+    except ImportError:   # pragma: no cover
+        pass
 
 
 @pytest.fixture

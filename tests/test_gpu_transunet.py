@@ -296,11 +296,13 @@ def test_col2im_matches_conv_input_grad(k, s, p, H):
     call, P, dt, stream = lib()
     torch.manual_seed(k * 10 + H)
     C, Co = 16, 8
-    w = torch.randn(Co, C, k, k, device="cuda")
-    x = torch.randn(2, C, H, H + 1, device="cuda", requires_grad=True)
+    # reference on the host in float64 (ATen's CPU convolution)
+    w = torch.randn(Co, C, k, k, dtype=torch.float64)
+    x = torch.randn(2, C, H, H + 1, dtype=torch.float64, requires_grad=True)
     y = F.conv2d(x, w, None, s, p)
     g = torch.randn_like(y)
-    dxr = torch.autograd.grad(y, x, g)[0]
+    dxr = torch.autograd.grad(y, x, g)[0].float().cuda()
+    w, g = w.float().cuda(), g.float().cuda()
     Ho, Wo = y.shape[2], y.shape[3]
     # dcols[b, oh, ow, (kh*k + kw)*C + c] = sum_o g[b, o, oh, ow] * w[o, c, kh, kw]
     dcols = torch.einsum("bohw,ocij->bhwijc", g, w).reshape(2, Ho, Wo, k * k * C).contiguous()
