@@ -11,9 +11,11 @@ from fixed seeds and sharded by rank, resident in HBM before timing.
 Launch: `python bench.py` (N=1) or, for N > 1, `python -m torch.distributed.run --nproc-per-node N
 ... bench.py --gpus N`.  Rank 0 prints ONE JSON line.  The line carries:
   roofline      the dominant kernel class (implicit-GEMM conv or weight-gradient GEMM): its
-                algorithmic FLOPs (2*M*N*K per launch) / its summed launch time, timed with HIP
-                events on its own stream inside the timed region, vs the 2.5 PFLOP/s dense bf16
-                MFMA peak;
+                algorithmic FLOPs (2*M*N*K per launch, counted by the library in an eager pass) / its
+                kernel time per step in the timed HIP-graph replays, from a rocprofv3 kernel trace of
+                this benchmark run as a child process before the timed run (live_replay_classes), vs
+                the 2.5 PFLOP/s dense bf16 MFMA peak; the HIP-event timing of the eager pass with the
+                streams serialised is kept as roofline.serialised_events;
   cpu_baseline  the CPU oracle (oracle/dfcsa_oracle.py, fp32 eager PyTorch = the reference
                 algorithm) timed on this host on the same B=16 workload (rank 0, N = 1 only);
   step_roofline whole-step fractions: mfma_frac = model FLOP/s / dense bf16
@@ -79,19 +81,58 @@ def pmc_traffic(cls):
         return None, None
 
 
-def replayed_classes(kind="replay"):
-    """Kernel time per step of each roofline class from the newest committed kernel trace of this
-    benchmark (tools/rocpd_export.py replay): kind "replay" = the timed HIP-graph replays, every
-    stream concurrent (profiles/rNN_replay_classes.json); "serial" = the class-timing pass, streams
-    serialised (profiles/rNN_serial_classes.json)."""
+def live_replay_classes(args, timeout_s=420):
+    """Kernel time per step of each roofline class in the timed HIP-graph replays of THIS build on
+    THIS box: this benchmark's own timed loop (same workload, streams concurrent) run under
+    `rocprofv3 --kernel-trace` as a child process, started before this process touches the GPU
+    (no exec from a GPU-initialised process), classified by tools/rocpd_export.py.  Returns
+    (classes, info) or (None, reason)."""
     import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_{kind}_classes.json")))
-    if not files:
-        return None, None
+    import shutil
+    import sqlite3
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
     try:
-        return json.load(open(files[-1]))["classes"], os.path.relpath(files[-1], ROOT)
-    except (KeyError, ValueError, OSError):
-        return None, None
+        import rocpd_export as R
+    finally:
+        sys.path.pop(0)
+    if any(k.startswith(("ROCPROF", "ROCP_")) for k in os.environ):
+        return None, "this command already runs under a profiler"
+    prof = shutil.which("rocprofv3") or "/opt/rocm/bin/rocprofv3"
+    if not os.path.exists(prof):
+        return None, "rocprofv3 not found"
+    steps = max(args.steps, 6)
+    with tempfile.TemporaryDirectory(dir="/tmp") as tmp:
+        cmd = [prof, "--kernel-trace", "-d", tmp, "-o", "run", "--", sys.executable, os.path.join(ROOT, "bench.py"),
+               "--steps", str(steps), "--warmup", str(args.warmup), "--batch", str(args.batch), "--img", str(args.img),
+               "--pool", str(args.pool), "--precision", args.precision, "--no-cpu-baseline", "--no-val-dice",
+               "--no-trainer-faithful", "--no-kernel-timing", "--no-live-trace"]
+        env = dict(os.environ, TMPDIR="/tmp")
+        t0 = time.perf_counter()
+        try:
+            r = subprocess.run(cmd, cwd="/tmp", env=env, capture_output=True, text=True, timeout=timeout_s)
+        except (OSError, subprocess.SubprocessError) as e:
+            return None, f"rocprofv3 child failed: {e}"
+        if r.returncode != 0:
+            return None, f"rocprofv3 child rc={r.returncode}: {r.stderr[-400:]}"
+        dbs = sorted(glob.glob(os.path.join(tmp, "**", "*.db"), recursive=True))
+        if not dbs:
+            return None, "rocprofv3 wrote no trace database"
+        out = os.path.join(tmp, "replay.json")
+        try:
+            R.replay(dbs[-1], out, steps=min(5, steps - 1))
+            res = json.load(open(out))
+        except (SystemExit, sqlite3.Error, OSError, ValueError, KeyError) as e:
+            return None, f"trace parse failed: {e}"
+        try:
+            child = json.loads(r.stdout.strip().splitlines()[-1])
+            child_ms = child.get("ms_per_step")
+        except (ValueError, IndexError):
+            child_ms = None
+    info = {"steps": res["steps"], "launches_per_step": res["launches_per_step"],
+            "first_to_last_kernel_ms_per_step": round(res["first_to_last_kernel_ms_per_step"], 3),
+            "child_ms_per_step_under_profiler": child_ms, "seconds": round(time.perf_counter() - t0, 1),
+            "groups": {k: {kk: round(vv, 4) for kk, vv in v.items()} for k, v in res["groups"].items()}}
+    return res["classes"], info
 
 
 def cpu_model_name():
@@ -287,11 +328,21 @@ def main():
                     help="one GPU: run the N > 1 code path (RCCL group of world size 1, bucket reducer, "
                          "graph-captured collectives, teardown) -- the multi-GPU path's test on a one-GPU box")
     ap.add_argument("--bucket-mb", type=float, default=32.0)
+    ap.add_argument("--no-live-trace", action="store_true",
+                    help="skip the rocprofv3 kernel trace of the timed replay (roofline.frac then falls back to "
+                         "the serialised HIP-event timing)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    live = (None, None)
+    if (world == 1 and args.model == "dfc" and not args.no_kernel_timing and not args.no_live_trace
+            and not args.ddp_rehearsal and not args.no_graph):
+        # before this process initialises the GPU: the child owns the device while it runs
+        log("[rank 0] kernel trace of the timed replay (rocprofv3 child) ...")
+        live = live_replay_classes(args)
+        log(f"[rank 0] live replay trace: {live[1] if live[0] is None else 'ok'}")
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ddp = world > 1 or args.ddp_rehearsal
@@ -453,29 +504,27 @@ def main():
                 "launches_per_step": n // args.steps, "avg_launch_ms": round(ms / max(n, 1), 4),
                 "ms_per_step": round(ms / args.steps, 3), "share_of_step": round(ms / (el * 1e3), 3),
                 "other_class": {}}
-        rep, rsrc = replayed_classes() if headline else (None, None)
+        rep, rinfo = live
         if rep and dom_key in rep and rep[dom_key]["ms_per_step"] > 0:
-            # the same class's FLOPs per step over its kernel time in the replayed step (streams
-            # concurrent, so a launch also counts the CUs it shares): the figure the step runs at
+            # the headline figure: the class's FLOPs per step over its kernel time in the timed HIP-graph
+            # replays of this build on this box (streams concurrent, so a launch also counts the CUs
+            # it shares) -- where the step runs.  The serialised HIP-event timing stays as secondary.
             r = rep[dom_key]
             a_rep = fl / args.steps / (r["ms_per_step"] * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9)
-            roof["replayed"] = {"achieved": round(a_rep, 2), "frac": round(a_rep / peak, 4),
-                                "ms_per_step": round(r["ms_per_step"], 3),
-                                "launches_per_step": r["launches_per_step"], "source": rsrc,
-                                "timing": "rocprofv3 kernel trace of the timed HIP-graph replays (side and "
-                                          "branch streams concurrent), this run's class FLOPs per step"}
-        ser, ssrc = replayed_classes("serial") if headline else (None, None)
-        if ser and dom_key in ser and ser[dom_key]["ms_per_step"] > 0:
-            # the same pass's kernels as rocprofv3 times them (kernel start to end): the HIP events
-            # around each launch also count its dispatch gap
-            r = ser[dom_key]
-            a_s = fl / args.steps / (r["ms_per_step"] * 1e-3) / (1e12 if unit == "TFLOP/s" else 1e9)
-            roof["serialised_trace"] = {"achieved": round(a_s, 2), "frac": round(a_s / peak, 4),
-                                        "avg_launch_ms": round(r["ms_per_step"] / max(r["launches_per_step"], 1), 4),
-                                        "launches_per_step": r["launches_per_step"], "source": ssrc,
-                                        "timing": "rocprofv3 kernel trace of this command's class-timing pass "
-                                                  "(kernel durations; the events above also count each launch's "
-                                                  "dispatch gap)"}
+            roof["serialised_events"] = {"achieved": roof["achieved"], "frac": roof["frac"],
+                                         "avg_launch_ms": roof["avg_launch_ms"], "ms_per_step": roof["ms_per_step"],
+                                         "timing": roof["timing"]}
+            roof.update({"achieved": round(a_rep, 2), "frac": round(a_rep / peak, 4),
+                         "ms_per_step": round(r["ms_per_step"], 3),
+                         "launches_per_step": r["launches_per_step"],
+                         "avg_launch_ms": round(r["ms_per_step"] / max(r["launches_per_step"], 1), 4),
+                         "share_of_step": round(r["ms_per_step"] / (el * 1e3 / args.steps), 3),
+                         "timing": "rocprofv3 --kernel-trace of this benchmark's timed HIP-graph replays, run as a "
+                                   "child process of this command on this box (side and branch streams concurrent); "
+                                   "FLOPs per step from this run's per-launch 2*M*N*K counts"})
+            roof["replay_trace"] = rinfo
+        elif headline:
+            roof["replay_trace"] = {"error": rinfo}
         if args.model == "fullres" and 3 in cls:
             roof = fra_exp_roofline(roof, cls[3], args, B, L)
         for v in cls.values():

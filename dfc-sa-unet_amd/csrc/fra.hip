@@ -91,7 +91,7 @@ __global__ void __launch_bounds__(256) fra_fwd_generic(int N, int C, int Cq, int
       }
     }
   }
-  const float inv = 1.f / l, gm = *gamma;
+  const float inv = 1.f / l, gm = y ? *gamma : 0.f;
   const size_t row = (size_t)b * N + n;
 #pragma unroll
   for (int i = 0; i < MAXR; ++i) {
@@ -99,7 +99,7 @@ __global__ void __launch_bounds__(256) fra_fwd_generic(int N, int C, int Cq, int
     if (c < C) {
       const float ov = acc[i] * inv;
       o[row * C + c] = E::from_f(ov);
-      y[row * C + c] = E::from_f(gm * ov + E::to_f(x[row * C + c]));
+      if (y) y[row * C + c] = E::from_f(gm * ov + E::to_f(x[row * C + c]));
     }
   }
   if (lane == 0) lse[row] = m + __logf(l);
@@ -381,11 +381,13 @@ __device__ __forceinline__ void zero_pad_cols(char* smem, int tile_bytes, int ro
 // ---------------------------------------------------------------------------- forward
 // Workgroup: 4 waves x QB 16-query blocks; value columns [c0, c0 + DV) of grid.y; KT = 64 keys
 // per LDS tile (double-buffered, register-staged).  grid (ceil(N / (64 QB)), C/DV, B).
-template <int CQ, int DV, int QB, int WPE>
+// OT: the type of o (bf16_t; float for the pooled attention, dfcsa_lsa_flash_fwd).  y == nullptr:
+// only o and lse are written (x and gamma are not read).
+template <int CQ, int DV, int QB, int WPE, typename OT>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
                                                     const bf16_t* __restrict__ x, const float* __restrict__ gamma,
-                                                    bf16_t* __restrict__ o, bf16_t* __restrict__ y,
+                                                    OT* __restrict__ o, bf16_t* __restrict__ y,
                                                     float* __restrict__ lse) {
   constexpr int KT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
@@ -511,7 +513,7 @@ fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
     __syncthreads();
   }
 
-  const float gm = *gamma;
+  const float gm = y ? *gamma : 0.f;
 #pragma unroll
   for (int qb = 0; qb < QB; ++qb) {
     const float lt = acc[qb][NCB][0];
@@ -522,10 +524,14 @@ fra_fwd_mfma(int N, int C, int ldq, const bf16_t* __restrict__ qkv,
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) {
       const size_t off = row * C + c0 + cb * 16 + 4 * g;
-      const uint2 xv = *(const uint2*)(x + off);
       const float ov0 = acc[qb][cb][0] * inv, ov1 = acc[qb][cb][1] * inv;
       const float ov2 = acc[qb][cb][2] * inv, ov3 = acc[qb][cb][3] * inv;
-      *(uint2*)(o + off) = make_uint2(pack2bf(ov0, ov1), pack2bf(ov2, ov3));
+      if constexpr (sizeof(OT) == 4)
+        *(float4*)(o + off) = make_float4(ov0, ov1, ov2, ov3);
+      else
+        *(uint2*)(o + off) = make_uint2(pack2bf(ov0, ov1), pack2bf(ov2, ov3));
+      if (!y) continue;
+      const uint2 xv = *(const uint2*)(x + off);
       const float x0 = __uint_as_float(xv.x << 16), x1 = __uint_as_float(xv.x & 0xffff0000u);
       const float x2 = __uint_as_float(xv.y << 16), x3 = __uint_as_float(xv.y & 0xffff0000u);
       *(uint2*)(y + off) = make_uint2(pack2bf(fmaf(gm, ov0, x0), fmaf(gm, ov1, x1)),
@@ -859,14 +865,14 @@ bool mfma_bwd_ok(int dtype, int C, int Cq, int ldq) {
          (Cq == 8 || Cq == 16 || Cq == 32 || (Cq == 64 && C == 64));
 }
 
-template <int CQ, int DV, int QB, int WPE>
+template <int CQ, int DV, int QB, int WPE, typename OT>
 void launch_fwd_w(dim3 grid, int N, int C, int ldq, const void* qkv, const void* x, const float* gamma, void* o,
                   void* y, float* lse, hipStream_t st) {
-  hipLaunchKernelGGL((fra_fwd_mfma<CQ, DV, QB, WPE>), grid, dim3(256), 0, st, N, C, ldq, (const bf16_t*)qkv,
-                     (const bf16_t*)x, gamma, (bf16_t*)o, (bf16_t*)y, lse);
+  hipLaunchKernelGGL((fra_fwd_mfma<CQ, DV, QB, WPE, OT>), grid, dim3(256), 0, st, N, C, ldq, (const bf16_t*)qkv,
+                     (const bf16_t*)x, gamma, (OT*)o, (bf16_t*)y, lse);
 }
 
-template <int CQ, int DV>
+template <int CQ, int DV, typename OT>
 void launch_fwd(int B, int N, int C, int ldq, const void* qkv, const void* x, const float* gamma, void* o, void* y,
                 float* lse, hipStream_t st) {
   constexpr int QB = DV <= 128 ? 2 : 1;
@@ -874,22 +880,22 @@ void launch_fwd(int B, int N, int C, int ldq, const void* qkv, const void* x, co
   // waves-per-SIMD budgets (knob 10): without one the compiler sizes these kernels for 1-2 waves
   const int occ = fra_occ_tuned();
   if constexpr (DV == 64 && CQ <= 16) {
-    if (occ & 8) return launch_fwd_w<CQ, DV, QB, 4>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
-    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 3>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+    if (occ & 8) return launch_fwd_w<CQ, DV, QB, 4, OT>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 3, OT>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
   }
   if constexpr (DV == 128 && CQ <= 16) {
-    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 2>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+    if (occ & 1) return launch_fwd_w<CQ, DV, QB, 2, OT>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
   }
-  launch_fwd_w<CQ, DV, QB, 1>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
+  launch_fwd_w<CQ, DV, QB, 1, OT>(grid, N, C, ldq, qkv, x, gamma, o, y, lse, st);
 }
 
-template <int CQ>
+template <int CQ, typename OT = bf16_t>
 void launch_fwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* x, const float* gamma, void* o,
                    void* y, float* lse, hipStream_t st) {
   switch (fwd_dv(C)) {
-    case 64: launch_fwd<CQ, 64>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
-    case 128: launch_fwd<CQ, 128>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
-    default: launch_fwd<CQ, 256>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
+    case 64: launch_fwd<CQ, 64, OT>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
+    case 128: launch_fwd<CQ, 128, OT>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
+    default: launch_fwd<CQ, 256, OT>(B, N, C, ldq, qkv, x, gamma, o, y, lse, st); break;
   }
 }
 
@@ -1075,6 +1081,176 @@ extern "C" int dfcsa_fra_bwd(int dtype, int B, int N, int C, int Cq, int ldq, co
                          (const float*)dy, gamma, lse, r, (float*)dqkv);
     }
   }
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+// ============================================================================ pooled attention
+// LightSelfAttention's core at P >= 8 (reference models/unet_dfc_sa_res.py:28-33, the
+// config_dfc-sa-res-block-p16 / -p32 pool sizes: N = P*P = 256 / 1024 pooled tokens) on the flash
+// kernels above, with gamma = 1: the LSA applies gamma after the bilinear upsample (:36-38), and its
+// backward hands over dO = gamma * U^T dattn (dfcsa_lsa_up_bwd_cols).  qkv [B][N][ldq], ldq = 2Cq + C,
+// is the fp32 projection output (fp32 mode: the generic fp32 kernels read it directly) or its bf16
+// copy (bf16 mode: the bf16 MFMA kernels).  o, dO and dqkv are fp32 in both modes (what the pooled
+// path's other kernels consume).
+namespace {
+
+constexpr size_t kLsaAlign = 256;
+size_t lsa_al(size_t b) { return (b + kLsaAlign - 1) / kLsaAlign * kLsaAlign; }
+
+bool lsa_mfma_ok(int C, int Cq, int ldq) {
+  return mfma_fwd_ok(DFCSA_DT_BF16, C, Cq, ldq) &&
+         (mfma_bwd_ok(DFCSA_DT_BF16, C, Cq, ldq) || wide_bwd_ok(DFCSA_DT_BF16, C, Cq, ldq));
+}
+
+// wave per row: r[row] = sum_c dO * o (fp32); bf16 mode also writes dO16 = bf16(dO); block 0 writes
+// one[0] = 1 (the gamma the flash kernels read)
+__global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, const float* __restrict__ dO,
+                                                             const float* __restrict__ o, float* __restrict__ r,
+                                                             bf16_t* __restrict__ dO16, float* __restrict__ one) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *one = 1.f;
+  if (row >= rows) return;
+  const float* a = dO + (size_t)row * C;
+  const float* v = o + (size_t)row * C;
+  float s = 0.f;
+  for (int c = lane * 4; c < C; c += 256) {
+    const float4 x = *(const float4*)(a + c), y = *(const float4*)(v + c);
+    s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+    if (dO16) *(uint2*)(dO16 + (size_t)row * C + c) = make_uint2(pack2bf(x.x, x.y), pack2bf(x.z, x.w));
+  }
+  s = wave_sum(s);
+  if (lane == 0) r[row] = s;
+}
+
+// dqkv (fp32) = dq16 (bf16), 8 elements per thread
+__global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const bf16_t* __restrict__ src,
+                                                              float* __restrict__ dst) {
+  const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (e >= n8) return;
+  const uint4 u = *(const uint4*)(src + 8 * e);
+  float4 lo, hi;
+  lo.x = __uint_as_float(u.x << 16); lo.y = __uint_as_float(u.x & 0xffff0000u);
+  lo.z = __uint_as_float(u.y << 16); lo.w = __uint_as_float(u.y & 0xffff0000u);
+  hi.x = __uint_as_float(u.z << 16); hi.y = __uint_as_float(u.z & 0xffff0000u);
+  hi.z = __uint_as_float(u.w << 16); hi.w = __uint_as_float(u.w & 0xffff0000u);
+  *(float4*)(dst + 8 * e) = lo;
+  *(float4*)(dst + 8 * e + 4) = hi;
+}
+
+// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | dq16 [B*N][ldq] | wide partials
+struct LsaWork {
+  size_t one, r, dO16, dq16, part, total;
+};
+LsaWork lsa_work(int dtype, int B, int N, int C, int Cq, int ldq) {
+  LsaWork w{};
+  const size_t rows = (size_t)B * N;
+  w.one = 0;
+  w.r = lsa_al(sizeof(float));
+  size_t e = w.r + lsa_al(rows * sizeof(float));
+  if (dtype == DFCSA_DT_BF16) {
+    w.dO16 = e;
+    e += lsa_al(rows * C * 2);
+    w.dq16 = e;
+    e += lsa_al(rows * ldq * 2);
+    if (!mfma_bwd_ok(dtype, C, Cq, ldq)) {
+      w.part = e;
+      e += lsa_al((size_t)2 * (C / kWideChunk) * rows * Cq * sizeof(float));
+    }
+  }
+  w.total = e;
+  return w;
+}
+
+bool lsa_shape_ok(int dtype, int B, int N, int C, int Cq, int ldq) {
+  if (B <= 0 || N <= 0 || C <= 0 || C % 4 || C > 1024 || Cq <= 0 || Cq > 128 || ldq != 2 * Cq + C) return false;
+  if (dtype == DFCSA_DT_BF16) return !g_fra_generic && lsa_mfma_ok(C, Cq, ldq);
+  return dtype == DFCSA_DT_F32;
+}
+
+}  // namespace
+
+extern "C" int dfcsa_lsa_flash_path(int C, int Cq, int ldq) {
+  return (!g_fra_generic && ldq == 2 * Cq + C && C <= 1024 && lsa_mfma_ok(C, Cq, ldq)) ? 1 : 0;
+}
+
+extern "C" int dfcsa_lsa_flash_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, float* o,
+                                   float* lse, void* stream) {
+  if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !qkv || !o || !lse) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_ATTN, st, 2.0 * B * (double)N * N * (Cq + C));
+  if (dtype == DFCSA_DT_BF16) {
+    switch (Cq) {
+      case 8: launch_fwd_cq<8, float>(B, N, C, ldq, qkv, nullptr, nullptr, o, nullptr, lse, st); break;
+      case 16: launch_fwd_cq<16, float>(B, N, C, ldq, qkv, nullptr, nullptr, o, nullptr, lse, st); break;
+      case 32: launch_fwd_cq<32, float>(B, N, C, ldq, qkv, nullptr, nullptr, o, nullptr, lse, st); break;
+      case 64: launch_fwd_cq<64, float>(B, N, C, ldq, qkv, nullptr, nullptr, o, nullptr, lse, st); break;
+      default: launch_fwd_cq<128, float>(B, N, C, ldq, qkv, nullptr, nullptr, o, nullptr, lse, st); break;
+    }
+  } else {
+    hipLaunchKernelGGL(fra_fwd_generic<float>, dim3((N + 3) / 4, B), dim3(256), (size_t)4 * Cq * sizeof(float), st,
+                       N, C, Cq, ldq, (const float*)qkv, nullptr, nullptr, o, nullptr, lse);
+  }
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq, int ldq, int64_t* bytes) {
+  if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !bytes) return DFCSA_EINVAL;
+  *bytes = (int64_t)lsa_work(dtype, B, N, C, Cq, ldq).total;
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const float* dO,
+                                   const float* o, const float* lse, float* dqkv, void* work, int64_t work_bytes,
+                                   void* stream) {
+  if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !qkv || !dO || !o || !lse || !dqkv || !work) return DFCSA_EINVAL;
+  const LsaWork w = lsa_work(dtype, B, N, C, Cq, ldq);
+  if (work_bytes < (int64_t)w.total || ((uintptr_t)work & 15)) return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  ProfScope prof(DFCSA_PROF_ATTN, st, 4.0 * B * (double)N * N * (Cq + C));
+  char* wb = (char*)work;
+  float* one = (float*)(wb + w.one);
+  float* r = (float*)(wb + w.r);
+  const int rows = B * N;
+  const bool bf = dtype == DFCSA_DT_BF16;
+  bf16_t* dO16 = bf ? (bf16_t*)(wb + w.dO16) : nullptr;
+  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, rows, C, dO, o, r, dO16, one);
+  DFCSA_CHECK_LAUNCH();
+  if (!bf) {
+    dim3 grid((N + 3) / 4, B);
+    const size_t shm = (size_t)4 * (Cq + C) * sizeof(float);
+    hipLaunchKernelGGL(fra_bwd_dq_generic<float>, grid, dim3(256), shm, st, N, C, Cq, ldq, (const float*)qkv, dO, one,
+                       lse, r, dqkv);
+    hipLaunchKernelGGL(fra_bwd_dkv_generic<float>, grid, dim3(256), shm, st, N, C, Cq, ldq, (const float*)qkv, dO,
+                       one, lse, r, dqkv);
+    DFCSA_CHECK_LAUNCH();
+    return 0;
+  }
+  bf16_t* dq16 = (bf16_t*)(wb + w.dq16);
+  if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
+    switch (Cq) {
+      case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
+      case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
+      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
+      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, nullptr, st); break;
+    }
+  } else {
+    float* part = (float*)(wb + w.part);
+    switch (Cq) {
+      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+    }
+    const int64_t threads = 2 * (int64_t)rows * (Cq / 4);
+    hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (int64_t)rows, Cq,
+                       C / kWideChunk, ldq, part, one, dq16);
+  }
+  DFCSA_CHECK_LAUNCH();
+  const int64_t n8 = (int64_t)rows * ldq / 8;
+  hipLaunchKernelGGL(lsa_flash_widen_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, n8, dq16, dqkv);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -16,7 +16,13 @@ from ._lib import version  # noqa: F401
 
 
 def set_tuning(knob, value):
-    """Benchmark-only kernel selection overrides (include/dfcsa.h, dfcsa_set_tuning)."""
+    """Benchmark-only kernel selection overrides (include/dfcsa.h, dfcsa_set_tuning).  Knob 31 (the
+    cooperative split-K weight-gradient reduction) is refused while the side or branch stream is on:
+    it assumes every workgroup of its grid is co-resident, which concurrent streams do not guarantee."""
+    if int(knob) == 31 and int(value):
+        from . import streams
+        if streams.ENABLED[0] or streams.BRANCH_ENABLED[0]:
+            raise ValueError("tuning knob 31 needs DFCSA_SIDE_STREAM=0 and DFCSA_BRANCH_STREAM=0")
     if _LIB.dfcsa_set_tuning(int(knob), int(value)) != 0:
         raise ValueError(f"unknown tuning knob {knob}")
 

@@ -369,16 +369,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         part = torch.empty(nte * 3 * C, device=dev, dtype=f32)
         call("dfcsa_bwd_block_out", T, M, C, P(dout), P(s.y4), P(bn4.scale), P(bn4.shift), P(bn4.mean),
              P(bn4.invstd), P(s.res), P(blk.res_scale), None, P(dres), *S(part), stream())
-    if ops._SYNC_BN is None and RES_SCALE_SIDE[0]:
-        # res_scale's gradient (sum over channels of the third sums, left in coef[2C:3C]) is summed on
-        # the side stream: only the optimizer reads it, and the finalize on the critical path then
-        # needs no second ticket level
-        coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias))
-        with on_side(dev, coef):
-            call("dfcsa_sum_into", P(coef) + 8 * C, C, P(grad_of(blk.res_scale)), stream())
-    else:
-        coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
-                                   extra=grad_of(blk.res_scale))
+    coef = ops.bn_bwd_finalize(part, nbo, 3, C, M, grad_of(bn4m.weight), grad_of(bn4m.bias),
+                               extra=grad_of(blk.res_scale))
     KpC = rup(C, ops.KALIGN)
     W4t = s.pk["W4t"]
     dlocal = torch.empty_like(s.y4)
@@ -487,30 +479,10 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         ncr = (B * Np + 15) // 16 if rows_in_proj else 0
         part2 = torch.empty((nte + ncr) * 2 * C, device=dev, dtype=f32)
         pool_rows = (wsum, bn2.mean, bn2.invstd, P(part2) + nte * 2 * C * 4, H, W) if rows_in_proj else None
-        if branch and ENTRY_SUMS_BRANCH[0]:
-            # one fork: the dattn part of the entry sums on the branch ahead of the attention backward
-            # (the local branch's BN1 sums then come from the acc GEMM or their own pass on this stream)
-            with on_branch(dev, branch, dattn, part2, wsum):
-                call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
-                     P(bn2.invstd), None, *S(part2), stream())
-                dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
-                                            pool_rows=pool_rows)
-                if rows_in_proj:
-                    coef2 = ops.bn_bwd_finalize(part2, nte + ncr, 2, C, M, grad_of(bn2m.weight),
-                                                grad_of(bn2m.bias))
-                else:
-                    coef2 = ops.bn_bwd_finalize_pool(part2, nte, C, M, grad_of(bn2m.weight), grad_of(bn2m.bias),
-                                                     dpooled, wsum, B, H, W, Pp, bn2)
-                dy2 = ops.bn_bwd_apply_entry(dtype, dattn, dpooled, Pp, s.y2, bn2, 1, bn2m.weight, coef2,
-                                             grad_of(conv2.bias))
-                del dpooled, coef2
-            del part2
-            s.wsum = None
-        else:
-            with on_branch(dev, branch, dattn, part2, wsum):
-                dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
-                                            pool_rows=pool_rows)
-    if s.fra is None and wsum is not None and not (branch and ENTRY_SUMS_BRANCH[0]):
+        with on_branch(dev, branch, dattn, part2, wsum):
+            dpooled = lsa_core_backward(lsa, (s.pooled, s.qkv, s.A, s.o, s.Wqkv), dattn, Pp, dtype, s.pk,
+                                        pool_rows=pool_rows)
+    if s.fra is None and wsum is not None:
         if fused_bn1:
             call("dfcsa_bwd_relu_bn", T, M, C, P(dattn), P(s.y2), P(bn2.scale), P(bn2.shift), P(bn2.mean),
                  P(bn2.invstd), None, *S(part2), stream())
@@ -530,8 +502,6 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
             del dpooled, coef2
         del part2
         s.wsum = None
-    elif s.fra is None and wsum is not None:
-        pass   # the one-fork branch above
     else:
         with on_branch(dev, branch, dattn):
             # (dz2 is not materialised: the apply recomputes it from the same inputs)
@@ -648,18 +618,6 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
     return dxs
 
 
-# the dattn part of the attention entry's BN2-backward sums on the branch stream ahead of the attention
-# backward (DFCSA_ENTRY_SUMS_BRANCH=1: one branch fork per block backward instead of two; the local
-# branch's BN1 sums then take their own pass where the pair kernel formed them).  Off: the pass is
-# worth more beside the attention backward than the saved fork (same-box A/B 1575 / 1570 / 1578
-# against 1591 / 1589 / 1587 img/s)
-ENTRY_SUMS_BRANCH = [os.environ.get("DFCSA_ENTRY_SUMS_BRANCH", "0") == "1"]
-
-# the block output's res_scale gradient summed on the side stream instead of inside the BN4 finalize
-# (DFCSA_RES_SCALE_SIDE=1).  Off: the extra main -> side edge per block costs far more than the
-# finalize's second ticket level (same-box A/B 1567 / 1578 / 1577 against 1630 / 1629 / 1631 img/s)
-RES_SCALE_SIDE = [os.environ.get("DFCSA_RES_SCALE_SIDE", "0") == "1"]
-
 # the backward's last block (no input gradient): conv1's weight gradient issued before the attention
 # chain's join (DFCSA_LAST_EARLY=1, the default: same-box A/B 1645.3 / 1645.4 / 1646.0 against
 # 1644.1 / 1642.8 / 1638.7 img/s for 0), and the gate / fusion weight gradients too (=2: 1640.5 /
@@ -696,6 +654,28 @@ ENTRY_WS = [os.environ.get("DFCSA_ENTRY_WS", "1") == "1"]
 # relative on some tensors with it against ~1e-5 on the per-row kernels (tools/pool_path_diag2.py),
 # not yet explained (the batched GEMMs themselves are fp32-exact, tools/bmm_precision_check.py)
 LSA_GEMM_MIN_N = int(os.environ.get("DFCSA_LSA_GEMM_MIN_N", str(1 << 30)))
+
+# pooled attention above this many tokens (N = P*P) on the flash kernels (dfcsa_lsa_flash_fwd / _bwd:
+# bf16 MFMA in bf16 mode where the widths allow, the generic fp32 kernels otherwise; nothing N x N is
+# stored); at and below it, the per-row fp32 kernels (dfcsa_lsa_attn / dfcsa_lsa_attn_bwd) sized for
+# the shipped P = 4 / 8.  DFCSA_LSA_FLASH_MIN_N
+LSA_FLASH_MIN_N = [int(os.environ.get("DFCSA_LSA_FLASH_MIN_N", "64"))]
+
+
+class FlashSaved:
+    """What the flash path keeps for the backward in place of A: the row log-sum-exp and the bf16 copy
+    of qkv the MFMA kernels read (None on the fp32 kernels)."""
+    __slots__ = ("lse", "qkv16")
+
+    def __init__(self, lse, qkv16):
+        self.lse, self.qkv16 = lse, qkv16
+
+
+def _flash_dtype(dtype, C, Cq, J):
+    """(storage dtype code, bf16?) of the flash kernels for this layer."""
+    if dtype == torch.bfloat16 and _lib.LIB.dfcsa_lsa_flash_path(C, Cq, J) == 1:
+        return _lib.DT_BF16, True
+    return _lib.DT_F32, False
 
 
 def _lsa_gemm_ok(C, J):
@@ -737,8 +717,23 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     else:
         Wqkv, WqkvT = pk["Wqkv"], pk["WqkvT"]
         call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
-    A = torch.empty((B, N, N), device=dev, dtype=f32)
     o = torch.empty((B, N, C), device=dev, dtype=f32)
+    if N > LSA_FLASH_MIN_N[0] and N <= LSA_GEMM_MIN_N:
+        # softmax(q k^T) v on the flash kernels; the backward recomputes P from the row log-sum-exp
+        T, bf = _flash_dtype(dtype, C, Cq, J)
+        qkv16 = None
+        src = qkv
+        if bf:
+            qkv16 = torch.empty((B, N, J), device=dev, dtype=torch.bfloat16)
+            call("dfcsa_cast_f32", _lib.DT_BF16, ctypes.c_int64(B * N * J), P(qkv), P(qkv16), 0, stream())
+            src = qkv16
+        lse = torch.empty(B * N, device=dev, dtype=f32)
+        call("dfcsa_lsa_flash_fwd", T, B, N, C, Cq, J, P(src), P(o), P(lse), stream())
+        A = FlashSaved(lse, qkv16)
+        if window_sums:
+            return pooled, qkv, A, o, Wqkv, wsum
+        return pooled, qkv, A, o, Wqkv
+    A = torch.empty((B, N, N), device=dev, dtype=f32)
     if N > LSA_GEMM_MIN_N:
         # q k^T and A v as batched fp32 library GEMMs, the row softmax in place between them
         # (contiguous q / k / v: the column slices of qkv start at arbitrary 4-byte offsets)
@@ -781,7 +776,15 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
         gpart = torch.empty(B * N, device=dev, dtype=f32)
         call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
              P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
-        if N > LSA_GEMM_MIN_N:
+        if isinstance(A, FlashSaved):
+            T, bf = _flash_dtype(dtype, C, Cq, J)
+            nb = ctypes.c_int64()
+            call("dfcsa_lsa_flash_bwd_bytes", T, B, N, C, Cq, J, ctypes.byref(nb))
+            work = torch.empty((nb.value + 15) // 16 * 4, device=dev, dtype=f32)
+            call("dfcsa_lsa_flash_bwd", T, B, N, C, Cq, J, P(A.qkv16 if bf else qkv), P(dO), P(o), P(A.lse),
+                 P(dqkv), P(work), ctypes.c_int64(work.numel() * 4), stream())
+            del work
+        elif N > LSA_GEMM_MIN_N:
             # dA = dO v^T; dE = A (dA - rowsum(A dA)) in place; dq = dE k, dk = dE^T q, dv = A^T dO
             q, k, v = qkv[:, :, :Cq].contiguous(), qkv[:, :, Cq:2 * Cq].contiguous(), qkv[:, :, 2 * Cq:].contiguous()
             dE = torch.bmm(dO, v.transpose(1, 2))

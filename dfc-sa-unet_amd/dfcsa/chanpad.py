@@ -27,12 +27,39 @@ logical shapes, ``load_state_dict`` accepts them (and padded ones), the FusedSGD
 an optimizer state dict is logical-shaped.  ``named_parameters()`` and ``.grad`` hold the padded
 storage; ``logical(p, t)`` slices a tensor of a parameter's padded shape back.
 """
+import contextlib
+
 import torch
 import torch.nn as nn
 
 
 def rup8(n):
     return (n + 7) // 8 * 8
+
+
+# construction depth of the modules that pad their children themselves (the U-Net pads every block
+# after the reference's construction, pad_model): a block or attention module built at depth 0 is
+# standalone and pads itself (pad_standalone)
+_BUILD = [0]
+
+
+@contextlib.contextmanager
+def building():
+    _BUILD[0] += 1
+    try:
+        yield
+    finally:
+        _BUILD[0] -= 1
+
+
+def standalone():
+    return _BUILD[0] == 0
+
+
+def build_inside(fn, *args, **kw):
+    """fn(*args, **kw) with its blocks / attention modules marked as parts of a larger model."""
+    with building():
+        return fn(*args, **kw)
 
 
 class Segs:
@@ -174,6 +201,19 @@ def pad_block(block, in_segs, C):
             _pad_bn(mod, out)
         elif isinstance(mod, nn.ConvTranspose2d):
             raise NotImplementedError(f"channel padding: unexpected {name!r} in {type(block).__name__}")
+
+
+def pad_standalone(mod, cin, cout):
+    """A DFC block (cin -> cout) or a LightSelfAttention / FullResolutionAttention (cin = cout = C)
+    built on its own, outside a U-Net (reference models/unet_dfc_sa_res.py:5-116 accepts any
+    width): zero-pad it like pad_block when cout is not a multiple of 8.  Its standalone forward
+    takes the logical NCHW input (padded to a multiple of 8 on the way in) and returns the logical
+    cout channels (``mod._dfcsa_out``).  cout % 8 == 0 needs nothing: the input side's padding is the
+    NCHW -> NHWC pack's."""
+    if cout % 8 == 0:
+        return
+    pad_block(mod, Segs([cin]), cout)
+    mod._dfcsa_out = cout
 
 
 def pad_model(model, features, in_channels, out_channels):

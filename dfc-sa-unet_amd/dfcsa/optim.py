@@ -39,6 +39,11 @@ class FusedSGD(torch.optim.Optimizer):
         self.zero_after_step = zero_after_step
         self._grads_zeroed = False  # the last step() zeroed the gradients (zero_after_step)
 
+    def add_param_group(self, param_group):
+        if getattr(self, "_flat", "init") != "init" or self.param_groups:
+            raise NotImplementedError("FusedSGD supports a single parameter group (the model's flat buffer)")
+        super().add_param_group(param_group)
+
     @classmethod
     def from_torch_sgd(cls, opt):
         """The fused equivalent of a ``torch.optim.SGD`` built as in the reference's train.py:73-78
@@ -115,7 +120,9 @@ class FusedSGD(torch.optim.Optimizer):
         """torch.optim.SGD's format; momentum buffers of channel-padded parameters (dfcsa.chanpad)
         in their reference shapes."""
         sd = super().state_dict()
-        for i, p in enumerate(self.param_groups[0]["params"]):
+        # torch numbers the state by a running index over every group's parameters
+        params = [p for g in self.param_groups for p in g["params"]]
+        for i, p in enumerate(params):
             st = sd["state"].get(i)
             if st is not None and st.get("momentum_buffer") is not None and hasattr(p, "_dfcsa_pad"):
                 sd["state"][i] = dict(st, momentum_buffer=chanpad.logical(p, st["momentum_buffer"]).clone())

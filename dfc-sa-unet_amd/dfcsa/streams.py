@@ -47,14 +47,7 @@ def side_or_main(device, *tensors):
     return contextlib.nullcontext()
 
 
-# DFCSA_SIDE_IS_BRANCH=1: the weight gradients share the branch stream (two streams in the step
-# instead of three; A/B of the graph's queue mapping)
-SIDE_IS_BRANCH = [os.environ.get("DFCSA_SIDE_IS_BRANCH", "0") == "1"]
-
-
 def side_stream(device):
-    if SIDE_IS_BRANCH[0]:
-        return branch_stream(device)
     idx = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(idx)
     if s is None:
@@ -89,8 +82,6 @@ def _join():
     for s in _SIDE.values():
         if s.device == cur.device:
             cur.wait_stream(s)
-    if SIDE_IS_BRANCH[0] and ENABLED[0]:
-        cur.wait_stream(branch_stream(cur.device))
 
 
 def join():

@@ -101,8 +101,6 @@ class GNState:
 # finalize launches; dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused, C <= 1024).  DFCSA_GN_FUSED=0
 # restores the four-launch path.
 GN_FUSED = [os.environ.get("DFCSA_GN_FUSED", "1") == "1"]
-# the Linear bias gradients (column sums) in one launch (dfcsa_colsum_fused); DFCSA_COLSUM_FUSED=0: two
-COLSUM_FUSED = [os.environ.get("DFCSA_COLSUM_FUSED", "0") == "1"]
 
 
 def _gn_fused(C, G):
@@ -183,40 +181,22 @@ def channel_sum3_into(dtype, x, n0, n1, d0, d1=None, d2=None):
     M, C = x.numel() // x.shape[-1], x.shape[-1]
     nt = LIB.dfcsa_colsum_ntiles(M)
     part = _f32((nt * C,), x.device)
-    if COLSUM_FUSED[0] and nt <= 64:   # one launch: the launch's last workgroup sums the (<= 64) partial rows
-        call("dfcsa_colsum_fused", dt(dtype), M, C, P(x), P(part), n0, n1, P(d0), P(d1), P(d2), stream())
-        return
     call("dfcsa_colsum_partial", dt(dtype), M, C, P(x), P(part), stream())
     call("dfcsa_slab_colsum3", P(part), nt, C, n0, n1, P(d0), P(d1), P(d2), stream())
 
 
-# the Linear bias gradients from column partials formed by the pass that writes dY (dropout / GELU
-# backward, the dqkv unpack: DFCSA_TU_CS=1) instead of a column-sum pass over dY.  Off: the row-tiled
-# passes give the per-element dropout hash to a quarter of the threads of the flat kernels, which
-# costs more than the column-sum launch they save (config 4 bf16, same box: 600 vs 609 img/s)
-TU_CS = [os.environ.get("DFCSA_TU_CS", "0") == "1"]
-
-
 def _drop_bwd_cs(dtype, M, C, dout, p, rng, site, out, x=None):
     """dropout backward (x given: GELU + dropout backward) of dout [M][C] into out, returning the
-    per-16-row column partials of out (the bias gradient of the GEMM whose dY out is); without TU_CS
-    the flat pass + dfcsa_colsum_partial (64-row partials: returned as (part, rows))."""
-    if not TU_CS[0]:
-        if x is None:
-            call("dfcsa_drop_bwd", dt(dtype), M * C, P(dout), float(p), P(rng), site, P(out), stream())
-        else:
-            call("dfcsa_gelu_drop_bwd", dt(dtype), M * C, P(x), P(dout), float(p), P(rng), site, P(out), stream())
-        nt = LIB.dfcsa_colsum_ntiles(M)
-        part = _f32((nt * C,), out.device)
-        call("dfcsa_colsum_partial", dt(dtype), M, C, P(out), P(part), stream())
-        return part
-    part = _f32((LIB.dfcsa_cs_ntiles(M) * C,), out.device)
+    64-row column partials of out (the bias gradient of the GEMM whose dY out is; dfcsa_colsum_partial).
+    (Round 5 measured partials formed inside the dropout pass, dfcsa_drop_bwd_cs: slower, 600 vs 609
+    img/s on config 4 bf16, and dropped.)"""
     if x is None:
-        call("dfcsa_drop_bwd_cs", dt(dtype), M, C, P(dout), float(p), P(rng), site, P(out), P(part), part.numel(),
-             stream())
+        call("dfcsa_drop_bwd", dt(dtype), M * C, P(dout), float(p), P(rng), site, P(out), stream())
     else:
-        call("dfcsa_gelu_drop_bwd_cs", dt(dtype), M, C, P(x), P(dout), float(p), P(rng), site, P(out), P(part),
-             part.numel(), stream())
+        call("dfcsa_gelu_drop_bwd", dt(dtype), M * C, P(x), P(dout), float(p), P(rng), site, P(out), stream())
+    nt = LIB.dfcsa_colsum_ntiles(M)
+    part = _f32((nt * C,), out.device)
+    call("dfcsa_colsum_partial", dt(dtype), M, C, P(out), P(part), stream())
     return part
 
 
@@ -652,7 +632,6 @@ class ViTBlock(torch.autograd.Function):
             _colsum_rows_into(pa, M, D, grad_of(att.out.bias))
         dcx = _gemm_1x1(dtype, da, pk["Wot"], KD, D, torch.empty_like(cx))
         del da
-        pq = None
         if ctx.probs is not None:
             dqkv = torch.empty_like(qkv)
             dscores = _f32((B * heads * N * N,), dev)
@@ -661,8 +640,7 @@ class ViTBlock(torch.autograd.Function):
             ctx.probs = None
             del dscores
         elif ctx.flash is not None:
-            pq = _f32((LIB.dfcsa_cs_ntiles(M) * 3 * D,), dev) if TU_CS[0] else None   # dqkv's column partials
-            dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh, col_partial=pq).view_as(qkv)
+            dqkv = mha_flash_backward(dtype, ctx.flash, dcx, B, N, heads, dh).view_as(qkv)
             ctx.flash = None
         else:
             dqkv = torch.empty_like(qkv)
@@ -670,16 +648,12 @@ class ViTBlock(torch.autograd.Function):
             call("dfcsa_mha_bwd", dt(dtype), B, N, heads, dh, 3 * D, scale, P(qkv), P(cx), P(dcx), P(lse), P(dvec),
                  P(dqkv), stream())
         del dcx
-        with side_or_main(dev, dqkv, y1, pq):
+        with side_or_main(dev, dqkv, y1):
             ops.conv_wgrad_into(dtype, [dqkv], 3 * D, [(y1, 0, 0)], D, grid, hw,
                                 [grad_of(att.query.weight), grad_of(att.key.weight), grad_of(att.value.weight)],
                                 1, D, D, layout=2)
-            if pq is not None:
-                call("dfcsa_slab_colsum3", P(pq), LIB.dfcsa_cs_ntiles(M), 3 * D, D, D,
-                     P(grad_of(att.query.bias)), P(grad_of(att.key.bias)), P(grad_of(att.value.bias)), stream())
-            else:
-                channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
-                                  grad_of(att.value.bias))
+            channel_sum3_into(dtype, dqkv, D, D, grad_of(att.query.bias), grad_of(att.key.bias),
+                              grad_of(att.value.bias))
         dy1 = _gemm_1x1(dtype, dqkv, pk["Wqkvt"], rup(3 * D, KA), D, torch.empty((B, gh, gw, D), dtype=dtype,
                                                                                   device=dev))
         del dqkv

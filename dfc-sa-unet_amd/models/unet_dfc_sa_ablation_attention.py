@@ -15,6 +15,7 @@ is stored.
 import torch
 import torch.nn as nn
 
+from dfcsa import chanpad
 from dfcsa.fra import FRAFunction
 from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock, UNetDFCSA, _nchw_to_nhwc, _nhwc_to_nchw
 
@@ -30,13 +31,13 @@ class FullResolutionAttention(nn.Module):
         self.value_conv = nn.Conv2d(channels, channels, kernel_size=1)
         self.gamma = nn.Parameter(torch.zeros(1))
         self.compute_dtype = torch.bfloat16
+        if chanpad.standalone():   # any width on its own (inside a block or U-Net: padded with it)
+            chanpad.pad_standalone(self, channels, channels)
 
     def forward(self, x):
         """x: [B, C, H, W] -> gamma * attention(x) + x, NCHW fp32."""
-        if x.shape[1] % 8:
-            raise ValueError("the full-resolution attention kernels need channels % 8 == 0")
         y = FRAFunction.apply(self, self.compute_dtype, _nchw_to_nhwc(x, self.compute_dtype), *self.parameters())
-        return _nhwc_to_nchw(y)
+        return _nhwc_to_nchw(y, self)
 
 
 class FullResAttnDFCBlock(DynamicFusionConvAttnBlock):

@@ -27,8 +27,12 @@ def _nchw_to_nhwc(x, dtype):
     return InputToNHWC.apply(x, dtype, rup(x.shape[1], 8))
 
 
-def _nhwc_to_nchw(y):
-    return y.permute(0, 3, 1, 2).float()
+def _nhwc_to_nchw(y, mod=None):
+    """NCHW fp32 view of an NHWC output; a standalone module padded by chanpad.pad_standalone returns
+    its logical channels only."""
+    y = y.permute(0, 3, 1, 2).float()
+    c = getattr(mod, "_dfcsa_out", None)
+    return y if c is None else y[:, :c]
 
 
 class LightSelfAttention(nn.Module):
@@ -44,12 +48,14 @@ class LightSelfAttention(nn.Module):
         self.value_conv = nn.Conv2d(channels, channels, kernel_size=1)
         self.gamma = nn.Parameter(torch.zeros(1))
         self.compute_dtype = torch.bfloat16
+        if chanpad.standalone():
+            chanpad.pad_standalone(self, channels, channels)
 
     def forward(self, x):
         """x: [B, C, H, W] (any values) -> gamma * up(attn(pool(x))) + x, NCHW fp32."""
         xh = _nchw_to_nhwc(x, self.compute_dtype)
         y = LSAFunction.apply(self, self.pool_size, self.compute_dtype, xh, *self.parameters())
-        return _nhwc_to_nchw(y)
+        return _nhwc_to_nchw(y, self)
 
 
 class DynamicFusionConvAttnBlock(nn.Module):
@@ -61,6 +67,12 @@ class DynamicFusionConvAttnBlock(nn.Module):
         super().__init__()
         if kernel_size != 3 or stride != 1 or padding != 1:
             raise NotImplementedError("the DFC block kernels implement the reference's 3x3/s1/p1 local branch")
+        with chanpad.building():   # the attention module is padded with the block
+            self._build(in_channels, out_channels, pool_size, ablation_on_qk_channels)
+        if chanpad.standalone():
+            chanpad.pad_standalone(self, in_channels, out_channels)
+
+    def _build(self, in_channels, out_channels, pool_size, ablation_on_qk_channels):
         self.pool_size = pool_size
         self.conv_branch = nn.Sequential(
             nn.Conv2d(in_channels, out_channels, kernel_size=3, stride=1, padding=1),
@@ -98,7 +110,7 @@ class DynamicFusionConvAttnBlock(nn.Module):
     def forward(self, x):
         """Standalone use on NCHW fp32 input (returns NCHW fp32)."""
         y = self.forward_nhwc([_nchw_to_nhwc(x, self.compute_dtype)], self.compute_dtype)
-        return _nhwc_to_nchw(y)
+        return _nhwc_to_nchw(y, self)
 
 
 class UNetDFCSA(nn.Module):
@@ -110,7 +122,8 @@ class UNetDFCSA(nn.Module):
                  ablation_on_qk_channels=8, precision=None):
         super().__init__()
         f = list(features)
-        blk = lambda i, o: self._make_block(i, o, pool_size, ablation_on_qk_channels)  # noqa: E731
+        # blocks built here are padded by pad_model below, not by themselves (chanpad.pad_standalone)
+        blk = lambda i, o: chanpad.build_inside(self._make_block, i, o, pool_size, ablation_on_qk_channels)  # noqa: E731
         self.pool_size = pool_size
         self.in_channels = in_channels
         self.down1 = blk(in_channels, f[0])

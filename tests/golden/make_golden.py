@@ -670,6 +670,51 @@ def gen_oddwidth():
              **bufs, **noise, **grad_arrays(m64, "grad64."), **mom)
 
 
+def gen_oddwidth_standalone():
+    """LightSelfAttention / DynamicFusionConvAttnBlock built ON THEIR OWN at widths that are not
+    multiples of 8 (reference :5-116 accepts any): the initial state dict under a seed (the build's
+    construction must consume the RNG identically), one train-mode forward + backward in fp32 and
+    the same run in float64 (grad64.*, the gradient reference; noise.* = the fp32 run's distance)."""
+    for C, H, P in ((12, 17, 4), (20, 13, 8), (27, 9, 16)):
+        torch.manual_seed(9700 + C)
+        m = ref_res.LightSelfAttention(C, pool_size=P, ablation_on_qk_channels=8)
+        sd0 = sd_arrays(m, "sd0.")
+        with torch.no_grad():
+            m.gamma.fill_(0.6)
+        m64 = fp64_twin(m)
+        gen = torch.Generator().manual_seed(9800 + C)
+        x = torch.randn(2, C, H, H + 2, generator=gen)
+        g = torch.randn(2, C, H, H + 2, generator=gen)
+        xr = x.clone().requires_grad_(True)
+        y = m(xr)
+        y.backward(g)
+        x64 = x.double().requires_grad_(True)
+        y64 = m64(x64)
+        y64.backward(g.double())
+        save(f"oddw_lsa_C{C}_P{P}.npz", x=np32(x), g=np32(g), y=np32(y), dx=np32(xr.grad), y64=y64.detach().numpy(),
+             dx64=x64.grad.numpy(), **sd0, **grad_arrays(m64, "grad64."), **fp64_noise(m, m64))
+    for cin, cout, H, P in ((5, 12, 12, 4), (12, 20, 10, 8), (16, 27, 8, 4)):
+        torch.manual_seed(9900 + cin * 10 + cout)
+        blk = ref_res.DynamicFusionConvAttnBlock(cin, cout, pool_size=P, ablation_on_qk_channels=8)
+        sd0 = sd_arrays(blk, "sd0.")
+        with torch.no_grad():
+            blk.attn_branch[3].gamma.fill_(0.5)
+        blk.train()
+        b64 = fp64_twin(blk)
+        gen = torch.Generator().manual_seed(9950 + cout)
+        x = torch.randn(2, cin, H, H + 1, generator=gen)
+        g = torch.randn(2, cout, H, H + 1, generator=gen)
+        xr = x.clone().requires_grad_(True)
+        y = blk(xr)
+        y.backward(g)
+        x64 = x.double().requires_grad_(True)
+        y64 = b64(x64)
+        y64.backward(g.double())
+        save(f"oddw_block_{cin}to{cout}_P{P}.npz", x=np32(x), g=np32(g), y=np32(y), dx=np32(xr.grad),
+             y64=y64.detach().numpy(), dx64=x64.grad.numpy(), **sd0, **grad_arrays(b64, "grad64."),
+             **fp64_noise(blk, b64), **sd_arrays(blk, "sd1."))
+
+
 def _zoo_full(name):
     m = _zoo_model(name)
     cls = type(m)

@@ -85,3 +85,27 @@ def test_odd_width_optimizer_state_translation(golden):
         b = chanpad.padded(p, mom[n])
         assert b.shape == p.shape, n
         assert torch.equal(chanpad.logical(p, b), mom[n]), n
+
+
+@pytest.mark.parametrize("fname", ["oddw_lsa_C12_P4.npz", "oddw_lsa_C20_P8.npz", "oddw_lsa_C27_P16.npz",
+                                   "oddw_block_5to12_P4.npz", "oddw_block_12to20_P8.npz", "oddw_block_16to27_P4.npz"])
+def test_standalone_odd_width_init_and_storage(golden, fname):
+    """A block / attention module built on its own at a width that is not a multiple of 8: the fresh
+    state dict equals the reference's under the same seed (key, shape and value); the stored
+    parameters are padded to multiples of 8 (zeros outside the logical channels); load_state_dict of
+    the reference's shapes round-trips bitwise."""
+    from test_gpu_oddwidth import standalone_module
+    fx = golden(fname)
+    ref = sd_of(fx, "sd0.")
+    m = standalone_module(fname)
+    got = m.state_dict()
+    assert list(got) == list(ref)
+    for k, v in ref.items():
+        assert tuple(got[k].shape) == tuple(v.shape), k
+        assert torch.equal(got[k], v.to(got[k].dtype)), k
+    for n, p in m.named_parameters():
+        if p.dim() > 1:
+            assert p.shape[0] % 8 == 0 and (p.shape[1] % 8 == 0 or n.endswith("conv_branch.0.weight")
+                                           or n.endswith("attn_branch.0.weight") or n.endswith("residual_conv.weight")), n
+    m.load_state_dict(ref)
+    assert all(torch.equal(a, ref[k].to(a.dtype)) for k, a in m.state_dict().items())

@@ -161,9 +161,14 @@ def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
     gh = nhwc(g, dtype)
     segs = ([(t, kh - 1, kw - 1) for kh in range(3) for kw in range(3) for t in xh] if taps == 9
             else [(t, 0, 0) for t in xh])
+    from dfcsa import streams
     LIB.dfcsa_wgrad_coop_errors(1)
     outs = {}
     saved = LIB.dfcsa_get_tuning(31)   # restore the library's setting (default 0), not a fixed value
+    # knob 31 is refused while the side / branch streams are on (dfcsa.set_tuning): this standalone
+    # launch runs alone on the device
+    sstate = (streams.ENABLED[0], streams.BRANCH_ENABLED[0])
+    streams.ENABLED[0] = streams.BRANCH_ENABLED[0] = False
     try:
         for coop in (1, 0, 1):
             dfcsa.set_tuning(31, coop)
@@ -175,6 +180,7 @@ def test_wgrad_cooperative_reduction(B, Cs, nsrc, C, H, W, taps):
             outs.setdefault(coop, []).append((gw, used))
     finally:
         dfcsa.set_tuning(31, saved)
+        streams.ENABLED[0], streams.BRANCH_ENABLED[0] = sstate
     assert LIB.dfcsa_wgrad_coop_errors(1) == 0
     (a, ua), (b, _) = outs[1]
     (c, uc), = outs[0]

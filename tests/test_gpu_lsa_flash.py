@@ -1,0 +1,114 @@
+"""Pooled attention for large pools (configs/config_dfc-sa-res-block-p16.yaml / -p32.yaml: N = 256 /
+1024 tokens) on the flash kernels (dfcsa_lsa_flash_fwd / _bwd, csrc/fra.hip).
+
+fp32 mode is pinned by the reference's own LightSelfAttention fixtures at P = 16 / 32
+(tests/test_gpu_model.py::test_lsa_fp32, lsa_C*_P16/P32.npz, 1e-5) and by the model-level float64
+oracle checks (tests/test_gpu_qk_ratio.py::test_large_pool_model_matches_oracle).  Here: the bf16 MFMA
+kernels at the widths the model uses (C = 64 .. 1024, q/k width C / 8; C >= 512 takes the
+value-chunked backward) against the oracle's LightSelfAttention (oracle/dfcsa_oracle.py:68-81) in
+float64 on the same bf16-rounded input.  Tolerance per quantity: max(2e-2, 2x the reference's own
+error under CPU bf16 autocast on the same layer and input, 1.5x the bf16 rounding of the output
+itself) -- the reference's bmm q k^T / v A^T run in bf16 there too, as do our MFMA kernels
+(tools/lsa_flash_err.py: at C = 256 .. 1024 the flash kernels are 2-3x closer to float64 than the
+reference's autocast; at C = 64 the bf16 storage of y dominates both our paths alike).
+"""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def rel(a, b):
+    a, b = a.detach().double().cpu(), b.detach().double().cpu()
+    return ((a - b).norm() / (b.norm() + 1e-30)).item()
+
+
+def _module(C, P, seed):
+    from models.unet_dfc_sa_res import LightSelfAttention
+    torch.manual_seed(seed)
+    m = LightSelfAttention(C, pool_size=P)
+    with torch.no_grad():
+        m.gamma.fill_(0.7)
+        for conv in (m.query_conv, m.key_conv, m.value_conv):
+            conv.weight.mul_(2.0)   # sharper softmax rows than the default init
+    return m
+
+
+@pytest.mark.parametrize("C,P,H,B", [(64, 16, 28, 2), (128, 16, 14, 3), (256, 32, 14, 2), (512, 32, 28, 2),
+                                     (1024, 32, 14, 1), (512, 16, 7, 2)])
+def test_flash_bf16_matches_oracle(C, P, H, B):
+    from dfcsa import _lib
+    from oracle import dfcsa_oracle as O
+    assert _lib.LIB.dfcsa_lsa_flash_path(C, C // 8, 2 * (C // 8) + C) == 1
+    m = _module(C, P, 100 + C + P)
+    g0 = torch.Generator().manual_seed(7 + C)
+    x = torch.randn(B, C, H, H + 1, generator=g0).bfloat16().float()
+    gy = torch.randn(B, C, H, H + 1, generator=g0)
+    # oracle in float64: y = gamma * up(attn(pool(x))) + x and its gradients
+    sd = {"a." + k: v.detach().double().clone().requires_grad_(True) for k, v in m.state_dict().items()}
+    xr = x.double().clone().requires_grad_(True)
+    yr = O.light_self_attention(xr, sd, "a", P)
+    yr.backward(gy.double())
+    # the reference's own bf16-autocast error on this layer (fp32 weights, CPU autocast)
+    sa = {k: v.detach().float().clone().requires_grad_(True) for k, v in sd.items()}
+    xa = x.clone().requires_grad_(True)
+    with torch.autocast("cpu", dtype=torch.bfloat16):
+        ya = O.light_self_attention(xa, sa, "a", P)
+    ya.float().backward(gy)
+    # bf16 mode stores y and dx in bf16: where the attention term is small against x (dx against
+    # the residual's gy) that rounding alone is a large part of the term -- 1.5x of it is admitted
+    bf = lambda t: t.bfloat16().double()   # noqa: E731
+    floor_y = rel(bf(yr.detach()) - xr.detach(), (yr - xr).detach())
+    floor_dx = rel(bf(xr.grad) - gy.double(), xr.grad - gy.double())
+    bar_y = max(2e-2, 2 * rel(ya.float() - x, (yr - xr).detach()), 1.5 * floor_y)
+    bar_dx = max(2e-2, 2 * rel(xa.grad - gy, xr.grad - gy.double()), 1.5 * floor_dx)
+    mg = m.cuda()
+    mg.compute_dtype = torch.bfloat16
+    xg = x.cuda().requires_grad_(True)
+    y = mg(xg)
+    y.backward(gy.cuda())
+    torch.cuda.synchronize()
+    # the attention term alone (y - x), where the bf16 error lives
+    assert rel(y.float().cpu() - x, (yr - xr).detach()) < bar_y, bar_y
+    assert rel(xg.grad - gy.cuda(), xr.grad - gy.double()) < bar_dx, bar_dx
+    for n, p in mg.named_parameters():
+        if n == "key_conv.bias":   # true gradient 0 (softmax is shift-invariant over keys)
+            continue
+        bar = max(2e-2, 2 * rel(sa["a." + n].grad, sd["a." + n].grad))
+        assert rel(p.grad, sd["a." + n].grad) < bar, (n, bar)
+
+
+@pytest.mark.parametrize("P", [16, 32])
+def test_flash_fp32_equals_per_row_kernels(P, monkeypatch):
+    """fp32 mode: the flash (generic fp32) kernels and the per-row kernels the pool sizes <= 8 use
+    agree on the same layer to fp32 rounding."""
+    from dfcsa import block
+    C, H, B = 64, 14, 2
+    outs = []
+    for min_n in (1 << 30, 64):
+        monkeypatch.setattr(block, "LSA_FLASH_MIN_N", [min_n])
+        m = _module(C, P, 5).cuda()
+        m.compute_dtype = torch.float32
+        g0 = torch.Generator().manual_seed(11)
+        x = torch.randn(B, C, H, H, generator=g0).cuda().requires_grad_(True)
+        y = m(x)
+        y.backward(torch.randn(B, C, H, H, generator=g0).cuda())
+        outs.append((y.detach(), x.grad.detach(), {n: p.grad.detach().clone() for n, p in m.named_parameters()}))
+    (ya, dxa, ga), (yb, dxb, gb) = outs
+    assert rel(yb, ya) < 1e-5 and rel(dxb, dxa) < 1e-5
+    for n in ga:
+        if n != "key_conv.bias":
+            assert rel(gb[n], ga[n]) < 1e-4, n
+
+
+def test_flash_rejects_bad_shapes():
+    from dfcsa import _lib
+    import ctypes
+    nb = ctypes.c_int64()
+    L = _lib.LIB
+    assert L.dfcsa_lsa_flash_path(48, 6, 60) == 0            # q/k width not a power of two: fp32 kernels
+    assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_BF16, 2, 256, 48, 6, 60, ctypes.byref(nb)) != 0
+    assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_F32, 2, 256, 48, 6, 61, ctypes.byref(nb)) != 0   # ldq != 2Cq + C
+    assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_F32, 2, 256, 48, 6, 60, ctypes.byref(nb)) == 0 and nb.value > 0
+    assert np.isfinite(nb.value)

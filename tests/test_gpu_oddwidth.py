@@ -90,3 +90,60 @@ def test_odd_width_model_bf16_near_reference(golden, name):
     assert rel(logits, fx["logits"]) < 5e-2
     assert abs(met["loss"].item() - float(fx["loss"])) < 5e-2 * abs(float(fx["loss"]))
     assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+
+STANDALONE = ("oddw_lsa_C12_P4.npz", "oddw_lsa_C20_P8.npz", "oddw_lsa_C27_P16.npz", "oddw_block_5to12_P4.npz",
+              "oddw_block_12to20_P8.npz", "oddw_block_16to27_P4.npz")
+
+
+def standalone_module(fname):
+    """The module of a standalone odd-width fixture, built as the reference built it (same seed)."""
+    from models.unet_dfc_sa_res import DynamicFusionConvAttnBlock, LightSelfAttention
+    parts = fname[:-4].split("_")
+    P = int(parts[-1][1:])
+    if parts[1] == "lsa":
+        C = int(parts[2][1:])
+        torch.manual_seed(9700 + C)
+        return LightSelfAttention(C, pool_size=P, ablation_on_qk_channels=8)
+    cin, cout = (int(v) for v in parts[2].split("to"))
+    torch.manual_seed(9900 + cin * 10 + cout)
+    return DynamicFusionConvAttnBlock(cin, cout, pool_size=P, ablation_on_qk_channels=8)
+
+
+@pytest.mark.parametrize("fname", STANDALONE)
+def test_standalone_odd_width_matches_reference(golden, fname):
+    """A LightSelfAttention / DynamicFusionConvAttnBlock built on its own at a width that is not a
+    multiple of 8 (reference models/unet_dfc_sa_res.py:5-116 accepts any; chanpad.pad_standalone pads
+    it at construction, the NCHW forward returns the logical channels) against the reference's own
+    run (tests/golden/oddw_lsa_* / oddw_block_*, make_golden.gen_oddwidth_standalone): fp32 mode,
+    train-mode forward + backward; y 1e-5 relative, dx 1e-4 against the float64 reference, parameter
+    gradients by check_grads (tol 2e-3, scaled by the reference's own fp32 noise); the padded
+    channels' gradients exactly zero."""
+    from dfcsa import chanpad
+    fx = golden(fname)
+    m = standalone_module(fname)
+    m.load_state_dict(sd_of(fx, "sd0."))
+    with torch.no_grad():
+        (m.gamma if hasattr(m, "gamma") else m.attn_branch[3].gamma).fill_(0.6 if hasattr(m, "gamma") else 0.5)
+    m = m.cuda().train()
+    m.compute_dtype = torch.float32
+    x = T(fx["x"]).requires_grad_(True)
+    y = m(x)
+    assert tuple(y.shape) == tuple(fx["y"].shape)
+    y.backward(T(fx["g"]))
+    torch.cuda.synchronize()
+    assert rel(y, fx["y64"]) < 1e-5
+    assert rel(x.grad, fx["dx64"]) < 1e-4
+    named = []
+    for n, p in m.named_parameters():
+        g = chanpad.logical(p, p.grad)
+        if hasattr(p, "_dfcsa_pad"):
+            assert torch.equal(p._dfcsa_pad.pad(g), p.grad), f"{n}: nonzero gradient in a padded channel"
+        named.append((n, types.SimpleNamespace(grad=g)))
+    check_grads(named, fx, prefix="grad64.", tol=2e-3)
+    if "sd1.running_mean" in str(list(fx)):
+        sd = m.state_dict()
+        for k in fx:
+            if k.startswith("sd1.") and "running" in k:
+                assert rel(sd[k[4:]], fx[k]) < 1e-4, k

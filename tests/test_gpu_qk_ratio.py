@@ -9,7 +9,7 @@ from the state-dict shapes) run in float64 on the CPU on the same weights and ba
 forward + backward of UNetDFCSARes at features 16, 32, 48, 64, pool 4, 32x32, batch 2, fp32 mode.
 Tolerances as for the model fixtures: logits 1e-4 relative, loss 1e-4, gradients by check_grads
 (tol 2e-3, scaled by the oracle's own fp32 distance to its float64 run) against the float64 run,
-with an absolute floor of 1e-4 of the whole gradient's norm per tensor (see _fixture).
+with an absolute floor of 1e-5 of the whole gradient's norm per tensor (see _fixture).
 """
 import numpy as np
 import pytest
@@ -23,11 +23,12 @@ pytestmark = pytest.mark.gpu
 def _fixture(sd, x, t, pool, grads64):
     """check_grads' fixture layout from the float64 oracle run.  noise.<name> is the oracle's own
     fp32 distance to its float64 run (as make_golden.fp64_noise records the reference's), floored
-    at 2e-5 |g_all| / |g_name|: check_grads then admits an error of 1e-4 of the whole gradient's
-    norm on any tensor.  That floor matters for the block scalars (gamma, res_scale) and the
-    attention biases, one cancelling sum each, whose fp32 error swings by 100x with the batch's
-    composition (measured: the oracle's own fp32 error on one gamma is 3e-2 at B = 15 and 4e-4 at
-    B = 17 of the same images; tools/pool_path_diag2.py)."""
+    at 2e-6 |g_all| / |g_name|: check_grads then admits an error of 1e-5 of the whole gradient's
+    norm on any tensor (round 6: 10x tighter than round 5's 2e-5 floor, which let a small-norm
+    tensor -- gamma, res_scale, an attention bias -- be off by several percent).  The
+    floor still matters for those block scalars, one cancelling sum each, whose fp32 error swings
+    by 100x with the batch's composition (measured: the oracle's own fp32 error on one gamma is
+    3e-2 at B = 15 and 4e-4 at B = 17 of the same images; tools/pool_path_diag2.py)."""
     from oracle import dfcsa_oracle as O
     _, _, grads32, _ = O.forward_backward(sd, x, t, pool, LP)
     fx, a, b = {}, [], []
@@ -35,7 +36,7 @@ def _fixture(sd, x, t, pool, grads64):
     for k, g in grads64.items():
         fx["grad." + k] = g.float().numpy()
         fx["grad64." + k] = g.numpy()
-        fx["noise." + k] = max(rel(grads32[k], g), 2e-5 * gall / max(g.norm().item(), 1e-30))
+        fx["noise." + k] = max(rel(grads32[k], g), 2e-6 * gall / max(g.norm().item(), 1e-30))
         a.append(grads32[k].double().reshape(-1))
         b.append(g.reshape(-1))
     fx["noise.all"] = rel(torch.cat(a), torch.cat(b))
