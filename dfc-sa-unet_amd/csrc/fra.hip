@@ -553,7 +553,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                         const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                         const float* __restrict__ lse, const float* __restrict__ rr,
-                                                        bf16_t* __restrict__ dqkv, float* __restrict__ part) {
+                                                        bf16_t* __restrict__ dqkv, float* __restrict__ part,
+                                                        int64_t rstride) {
   constexpr int QT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
   constexpr int QBy = QT * KC * 2, DBy = QT * C * 2, LBy = QT * 4 * 2;
@@ -600,7 +601,9 @@ fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     if (tid < QT) {
       const int q = qt0 + tid;
       ls[tid] = q < N ? lseb[q] * kL2E : 0.f;
-      ls[QT + tid] = (q < N && ch == 0) ? -rrb[q] : 0.f;  // -r enters dP once, in chunk 0
+      // -r enters dP once, in chunk 0; rstride > 0: each chunk subtracts its own share r_ch (the
+      // chunk's columns of rowsum(dy * o), dfcsa_lsa_flash_bwd), so every chunk's dS stays centred
+      ls[QT + tid] = (q < N && (ch == 0 || rstride)) ? -rrb[q + ch * rstride] : 0.f;
     }
   };
   const int ntiles = (N + QT - 1) / QT;
@@ -721,7 +724,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                        const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                        const float* __restrict__ lse, const float* __restrict__ rr,
-                                                       bf16_t* __restrict__ dqkv, float* __restrict__ part) {
+                                                       bf16_t* __restrict__ dqkv, float* __restrict__ part,
+                                                       int64_t rstride) {
   constexpr int KT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
   constexpr int KBy = KT * KC * 2, VBy = KT * C * 2, TB = KBy + VBy;
@@ -748,7 +752,7 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     for (int dc = 0; dc < NDC; ++dc)
       df[qb][dc] = ok ? *(const bf16x8_t*)(dyb + (size_t)q * ldd + 32 * dc + 8 * g) : bf16x8_t{0, 0, 0, 0, 0, 0, 0, 0};
     Lq[qb] = ok ? -lse[(size_t)b * N + q] * kL2E : 0.f;
-    const float nr = (ok && ch == 0) ? -rr[(size_t)b * N + q] : 0.f;  // -r enters dP once, in chunk 0
+    const float nr = (ok && (ch == 0 || rstride)) ? -rr[(size_t)b * N + q + ch * rstride] : 0.f;  // (see dK/dV)
     nR[qb] = f32x4_t{nr, nr, nr, nr};
   }
   f32x4_t dqa[2][NDB];
@@ -904,7 +908,7 @@ void launch_fwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* x,
 // shares) for fra_wide_finish.
 template <int CQ, int C>
 void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy, const float* gamma,
-                const float* lse, const float* rr, void* dqkv, float* part, hipStream_t st) {
+                const float* lse, const float* rr, void* dqkv, float* part, hipStream_t st, int64_t rstride = 0) {
   dim3 grid((N + 127) / 128, Ctot / C, B);
   float* pk = part;
   float* pq = part ? part + (size_t)(Ctot / C) * B * N * CQ : nullptr;
@@ -913,16 +917,16 @@ void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy
   constexpr int WKV = C == 64 ? 3 : 2, WQ = C == 64 ? 4 : 3;
   if (narrow && (occ & 2))
     hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, narrow ? WKV : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk);
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk, rstride);
   else
     hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk);
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk, rstride);
   if (narrow && (occ & 4))
     hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq);
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride);
   else
     hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq);
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride);
 }
 
 template <int CQ>
@@ -1103,9 +1107,15 @@ bool lsa_mfma_ok(int C, int Cq, int ldq) {
          (mfma_bwd_ok(DFCSA_DT_BF16, C, Cq, ldq) || wide_bwd_ok(DFCSA_DT_BF16, C, Cq, ldq));
 }
 
-// wave per row: r[row] = sum_c dO * o (fp32); bf16 mode also writes dO16 = bf16(dO); block 0 writes
-// one[0] = 1 (the gamma the flash kernels read)
-__global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, const float* __restrict__ dO,
+// wave per row: r[row] = sum_c dO * o (fp32); bf16 mode also writes dO16 = bf16(dO) and forms r from
+// the ROUNDED dO16, the same operand the MFMA dP = dO16 V^T uses: dS = P (dP - r) then holds
+// sum_c dO16_c (V_jc - o_c), in which the rounding error of dO (nearly the same for every key when the
+// value rows are alike, as pooled features after BatchNorm + ReLU are) cancels instead of entering
+// dS as P * sum_c (dO16 - dO)_c V_c -- a coherent error along P that swamped dq / dk at the model's
+// P = 8 layers (cos 0.44 against float64 on down1's query weight gradient with fp32 r).  Block 0
+// writes one[0] = 1 (the gamma the flash kernels read).
+// nch > 1 (value-chunked backward): r holds one share per 128-column chunk, r[ch * rows + row]
+__global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, int nch, const float* __restrict__ dO,
                                                              const float* __restrict__ o, float* __restrict__ r,
                                                              bf16_t* __restrict__ dO16, float* __restrict__ one) {
   const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -1113,17 +1123,43 @@ __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, co
   if (row >= rows) return;
   const float* a = dO + (size_t)row * C;
   const float* v = o + (size_t)row * C;
+  if (nch > 1) {   // C = 128 nch: lanes 0-31 cover the first 128 columns of each 256, lanes 32-63 the next
+    for (int c0 = 0; c0 < C; c0 += 256) {
+      const int c = c0 + lane * 4;
+      float s = 0.f;
+      if (c < C) {   // (C = 384: the last 256-column step is half full)
+        float4 x = *(const float4*)(a + c);
+        const float4 y = *(const float4*)(v + c);
+        const uint2 u = make_uint2(pack2bf(x.x, x.y), pack2bf(x.z, x.w));
+        *(uint2*)(dO16 + (size_t)row * C + c) = u;
+        x.x = __uint_as_float(u.x << 16); x.y = __uint_as_float(u.x & 0xffff0000u);
+        x.z = __uint_as_float(u.y << 16); x.w = __uint_as_float(u.y & 0xffff0000u);
+        s = x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
+      }
+#pragma unroll
+      for (int off = 1; off < 32; off <<= 1) s += __shfl_xor(s, off, 64);   // within each 32-lane half
+      const int ch = c0 / 128 + (lane >> 5);
+      if ((lane & 31) == 0 && ch < nch) r[(size_t)ch * rows + row] = s;
+    }
+    return;
+  }
   float s = 0.f;
   for (int c = lane * 4; c < C; c += 256) {
-    const float4 x = *(const float4*)(a + c), y = *(const float4*)(v + c);
+    float4 x = *(const float4*)(a + c);
+    const float4 y = *(const float4*)(v + c);
+    if (dO16) {
+      const uint2 u = make_uint2(pack2bf(x.x, x.y), pack2bf(x.z, x.w));
+      *(uint2*)(dO16 + (size_t)row * C + c) = u;
+      x.x = __uint_as_float(u.x << 16); x.y = __uint_as_float(u.x & 0xffff0000u);
+      x.z = __uint_as_float(u.y << 16); x.w = __uint_as_float(u.y & 0xffff0000u);
+    }
     s += x.x * y.x + x.y * y.y + x.z * y.z + x.w * y.w;
-    if (dO16) *(uint2*)(dO16 + (size_t)row * C + c) = make_uint2(pack2bf(x.x, x.y), pack2bf(x.z, x.w));
   }
   s = wave_sum(s);
   if (lane == 0) r[row] = s;
 }
 
-// dqkv (fp32) = dq16 (bf16), 8 elements per thread
+// dst (fp32) = src (bf16), 8 elements per thread (dfcsa_bf16_to_f32)
 __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const bf16_t* __restrict__ src,
                                                               float* __restrict__ dst) {
   const int64_t e = (int64_t)blockIdx.x * 256 + threadIdx.x;
@@ -1138,24 +1174,24 @@ __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const 
   *(float4*)(dst + 8 * e + 4) = hi;
 }
 
-// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | dq16 [B*N][ldq] | wide partials
+// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | wide partials
 struct LsaWork {
-  size_t one, r, dO16, dq16, part, total;
+  size_t one, r, dO16, part, total;
 };
 LsaWork lsa_work(int dtype, int B, int N, int C, int Cq, int ldq) {
   LsaWork w{};
   const size_t rows = (size_t)B * N;
+  const bool wide = dtype == DFCSA_DT_BF16 && !mfma_bwd_ok(dtype, C, Cq, ldq);
+  const int nch = wide ? C / kWideChunk : 1;   // r: one share per 128-column chunk on wide layers
   w.one = 0;
   w.r = lsa_al(sizeof(float));
-  size_t e = w.r + lsa_al(rows * sizeof(float));
+  size_t e = w.r + lsa_al((size_t)nch * rows * sizeof(float));
   if (dtype == DFCSA_DT_BF16) {
     w.dO16 = e;
     e += lsa_al(rows * C * 2);
-    w.dq16 = e;
-    e += lsa_al(rows * ldq * 2);
-    if (!mfma_bwd_ok(dtype, C, Cq, ldq)) {
+    if (wide) {
       w.part = e;
-      e += lsa_al((size_t)2 * (C / kWideChunk) * rows * Cq * sizeof(float));
+      e += lsa_al((size_t)2 * nch * rows * Cq * sizeof(float));
     }
   }
   w.total = e;
@@ -1202,7 +1238,7 @@ extern "C" int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq,
 }
 
 extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const float* dO,
-                                   const float* o, const float* lse, float* dqkv, void* work, int64_t work_bytes,
+                                   const float* o, const float* lse, void* dqkv, void* work, int64_t work_bytes,
                                    void* stream) {
   if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !qkv || !dO || !o || !lse || !dqkv || !work) return DFCSA_EINVAL;
   const LsaWork w = lsa_work(dtype, B, N, C, Cq, ldq);
@@ -1215,19 +1251,21 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
   const int rows = B * N;
   const bool bf = dtype == DFCSA_DT_BF16;
   bf16_t* dO16 = bf ? (bf16_t*)(wb + w.dO16) : nullptr;
-  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, rows, C, dO, o, r, dO16, one);
+  const int nch = (bf && !mfma_bwd_ok(dtype, C, Cq, ldq)) ? C / kWideChunk : 1;
+  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, rows, C, nch, dO, o, r, dO16,
+                     one);
   DFCSA_CHECK_LAUNCH();
   if (!bf) {
     dim3 grid((N + 3) / 4, B);
     const size_t shm = (size_t)4 * (Cq + C) * sizeof(float);
     hipLaunchKernelGGL(fra_bwd_dq_generic<float>, grid, dim3(256), shm, st, N, C, Cq, ldq, (const float*)qkv, dO, one,
-                       lse, r, dqkv);
+                       lse, r, (float*)dqkv);
     hipLaunchKernelGGL(fra_bwd_dkv_generic<float>, grid, dim3(256), shm, st, N, C, Cq, ldq, (const float*)qkv, dO,
-                       one, lse, r, dqkv);
+                       one, lse, r, (float*)dqkv);
     DFCSA_CHECK_LAUNCH();
     return 0;
   }
-  bf16_t* dq16 = (bf16_t*)(wb + w.dq16);
+  bf16_t* dq16 = (bf16_t*)dqkv;
   if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
     switch (Cq) {
       case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
@@ -1238,19 +1276,25 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
   } else {
     float* part = (float*)(wb + w.part);
     switch (Cq) {
-      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
-      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
-      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
-      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
-      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st); break;
+      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
+      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
+      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
+      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
+      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
     }
     const int64_t threads = 2 * (int64_t)rows * (Cq / 4);
     hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (int64_t)rows, Cq,
                        C / kWideChunk, ldq, part, one, dq16);
   }
   DFCSA_CHECK_LAUNCH();
-  const int64_t n8 = (int64_t)rows * ldq / 8;
-  hipLaunchKernelGGL(lsa_flash_widen_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, n8, dq16, dqkv);
+  return 0;
+}
+
+extern "C" int dfcsa_bf16_to_f32(int64_t n, const void* src, float* dst, void* stream) {
+  if (n <= 0 || n % 8 || !src || !dst || ((uintptr_t)src & 15) || ((uintptr_t)dst & 15)) return DFCSA_EINVAL;
+  const int64_t n8 = n / 8;
+  hipLaunchKernelGGL(lsa_flash_widen_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, (hipStream_t)stream, n8,
+                     (const bf16_t*)src, dst);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -401,28 +401,34 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
   }
 }
 
-// grid (N, B): du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du.
+// grid (ceil(N / npw), B): tokens n = blockIdx.x * npw + t, t < npw, each:
+// du = sum_h wy(pi, h) rows[b][h][pj]; dO = gamma * du; gpart = sum_c o * du.
 // Channels x NSL slices of the h range (all 256 threads busy at C = 64), combined in LDS.
 // NT = 1024 for C <= 128: four times the row slices per output (the 224^2 level's ~84 source rows
 // per pooled row were ~21 dependent loads per lane with 256 threads)
+// npw > 1 (fused dgamma only: gpart then holds one partial per workgroup): large pools (P = 32: 16 k
+// one-token workgroups) spent most of the launch in the dgamma ticket, one atomic per workgroup
 template <int NT>
-__global__ void __launch_bounds__(NT) lsa_up_bwd_cols_kernel(int H, int C, int P, const float* __restrict__ rows,
+__global__ void __launch_bounds__(NT) lsa_up_bwd_cols_kernel(int H, int C, int P, int npw, const float* __restrict__ rows,
                                                              const float* __restrict__ o, const float* gamma,
                                                              float* __restrict__ dO, float* __restrict__ gpart,
                                                              unsigned* cnt, float* gamma_grad) {
   __shared__ float red[NT + 32];
   __shared__ double rd[NT];
   __shared__ int flag;
-  const int n = blockIdx.x, b = blockIdx.y, N = P * P;
-  const int pi = n / P, pj = n - pi * P;
+  const int b = blockIdx.y, N = P * P;
   const float gm = *gamma;
   const float bsc = (float)P / (float)H;   // bilinear source scale along H
   const int nsl = C >= NT ? 1 : NT / C;
   const int cw = nsl == 1 ? NT : C;
   const int sl = threadIdx.x / cw, cl = threadIdx.x - sl * cw;
+  float gsum = 0.f;
+  for (int t = 0; t < npw; ++t) {
+  const int n = blockIdx.x * npw + t;
+  if (n >= N) break;
+  const int pi = n / P, pj = n - pi * P;
   int lo, hi;
   contrib_range(pi, P, H, lo, hi);
-  float gsum = 0.f;
   for (int cb = 0; cb < C; cb += cw) {
     const int c = cb + cl;
     float s = 0.f;
@@ -458,13 +464,15 @@ __global__ void __launch_bounds__(NT) lsa_up_bwd_cols_kernel(int H, int C, int P
       dO[idx] = gm * s;
     }
   }
+  }
   gsum = block_reduce_sum(gsum, red + NT);
+  const size_t gi = (size_t)b * gridDim.x + blockIdx.x;   // = b * N + n when npw == 1
   if (!gamma_grad) {
-    if (threadIdx.x == 0) gpart[(size_t)b * N + n] = gsum;
+    if (threadIdx.x == 0) gpart[gi] = gsum;
     return;
   }
   // fused dgamma: the last workgroup sums gpart in index order (per thread), then a fixed tree
-  if (threadIdx.x == 0) st_sc1_dw(gpart + (size_t)b * N + n, gsum);
+  if (threadIdx.x == 0) st_sc1_dw(gpart + gi, gsum);
   if (!wg_last_of(cnt, gridDim.x * gridDim.y, &flag)) return;
   double v = 0.0;
   const int total = gridDim.x * gridDim.y;
@@ -765,47 +773,6 @@ extern "C" int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const fl
   return 0;
 }
 
-// Row softmax in place over E [rows][N] (fp32): the pooled attention on the opt-in GEMM path,
-// whose energy / output / gradient products run as batched library GEMMs (block.py).
-__global__ void __launch_bounds__(256) softmax_rows_kernel(int N, float* __restrict__ E) {
-  __shared__ float red[8];
-  float* e = E + (size_t)blockIdx.x * N;
-  float mx = -INFINITY;
-  for (int m = threadIdx.x; m < N; m += 256) mx = fmaxf(mx, e[m]);
-  mx = block_reduce_max(mx, red);
-  float sum = 0.f;
-  for (int m = threadIdx.x; m < N; m += 256) sum += __expf(e[m] - mx);
-  sum = block_reduce_sum(sum, red + 4);
-  const float inv = 1.f / sum;
-  for (int m = threadIdx.x; m < N; m += 256) e[m] = __expf(e[m] - mx) * inv;
-}
-
-// Softmax backward in place: dA [rows][N] -> dE = A * (dA - sum_m A dA)
-__global__ void __launch_bounds__(256) softmax_bwd_rows_kernel(int N, const float* __restrict__ A,
-                                                               float* __restrict__ dA) {
-  __shared__ float red[4];
-  const float* a = A + (size_t)blockIdx.x * N;
-  float* d = dA + (size_t)blockIdx.x * N;
-  float s = 0.f;
-  for (int m = threadIdx.x; m < N; m += 256) s += a[m] * d[m];
-  s = block_reduce_sum(s, red);
-  for (int m = threadIdx.x; m < N; m += 256) d[m] = a[m] * (d[m] - s);
-}
-
-extern "C" int dfcsa_softmax_rows_f32(int64_t rows, int N, float* E, void* stream) {
-  if (rows <= 0 || rows > 0x7fffffff || N <= 0 || !E) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(softmax_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, N, E);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
-}
-
-extern "C" int dfcsa_softmax_bwd_rows_f32(int64_t rows, int N, const float* A, float* dA, void* stream) {
-  if (rows <= 0 || rows > 0x7fffffff || N <= 0 || !A || !dA) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(softmax_bwd_rows_kernel, dim3((unsigned)rows), dim3(256), 0, (hipStream_t)stream, N, A, dA);
-  DFCSA_CHECK_LAUNCH();
-  return 0;
-}
-
 extern "C" int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream) {
   size_t shm = (size_t)(Cq + N + 8) * sizeof(float);
   hipLaunchKernelGGL(lsa_attn_kernel, dim3(N, B), dim3(256), shm, (hipStream_t)stream, N, C, Cq, qkv, A, o);
@@ -998,12 +965,14 @@ extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* ro
                                      void* stream) {
   unsigned* cnt = nullptr;
   if (gamma_grad && !(cnt = dfcsa_ticket_alloc(1))) return DFCSA_EINVAL;
-if (C <= 128 && g_lsa_cols_nt > 256)
-    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<1024>, dim3(P * P, B), dim3(1024), 0, (hipStream_t)stream, H, C, P, rows, o,
-                     gamma, dO, gpart, cnt, gamma_grad);
+  // fused dgamma: at most ~64 workgroups per image (one ticket atomic each)
+  const int N = P * P, npw = gamma_grad ? (N + 63) / 64 : 1, gx = (N + npw - 1) / npw;
+  if (C <= 128 && g_lsa_cols_nt > 256)
+    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<1024>, dim3(gx, B), dim3(1024), 0, (hipStream_t)stream, H, C, P, npw, rows,
+                       o, gamma, dO, gpart, cnt, gamma_grad);
   else
-    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<256>, dim3(P * P, B), dim3(256), 0, (hipStream_t)stream, H, C, P, rows, o,
-                     gamma, dO, gpart, cnt, gamma_grad);
+    hipLaunchKernelGGL(lsa_up_bwd_cols_kernel<256>, dim3(gx, B), dim3(256), 0, (hipStream_t)stream, H, C, P, npw, rows,
+                       o, gamma, dO, gpart, cnt, gamma_grad);
   DFCSA_CHECK_LAUNCH();
   if (ngpart) *ngpart = B * P * P;
   return 0;

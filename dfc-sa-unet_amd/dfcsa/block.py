@@ -118,7 +118,7 @@ def block_forward(blk, xs, pool_size, training, dtype, pool=False):
     N2 = 2 * C if has_res else C
     Kp1, Kp2 = rup(9 * Cin_p, ops.KALIGN), rup(Cin_p, ops.KALIGN)
     Kp3, Kp4 = rup(2 * C, ops.KALIGN), rup(3 * C, ops.KALIGN)
-    pk = get_packset(blk, (dtype, nsrc, Cs, param_key(blk)),
+    pk = get_packset(blk, (dtype, nsrc, Cs, LSA_FLASH_MIN_N[0], param_key(blk)),
                      lambda ps: _build_block_packs(ps, blk, dtype, Cin_p, C, has_res))
     W1p, W2p, W3p, W4p = pk["W1p"], pk["W2p"], pk["W3p"], pk["W4p"]
     b2 = pk["b2"] if has_res else conv2.bias
@@ -305,10 +305,10 @@ def _build_block_packs(ps, blk, dtype, Cin_p, C, has_res):
     if getattr(att, "full_resolution", False):
         fra.build_packs(ps, att, dtype)
     else:
-        _build_lsa_packs(ps, att)
+        _build_lsa_packs(ps, att, dtype, blk.pool_size)
 
 
-def _build_lsa_packs(ps, lsa):
+def _build_lsa_packs(ps, lsa, dtype=None, pool_size=None):
     f32 = torch.float32
     C = lsa.value_conv.out_channels
     Cq = lsa.query_conv.out_channels
@@ -320,6 +320,11 @@ def _build_lsa_packs(ps, lsa):
         for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
             Wp = ps.rows("Wp", f32, w, C, Kp, row0=off, rows=J)
         ps.transpose(Wp, 0, 0, J, C, "WT", (C, rup(J, ops.KALIGN)))
+        if pool_size is not None and flash16_layer(dtype, C, Cq, pool_size):
+            # the bf16 projection operands of a flash layer (forward rows, dgrad transposes)
+            for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
+                Wp16 = ps.rows("Wp16", torch.bfloat16, w, C, Kp, row0=off, rows=J)
+            ps.transpose(Wp16, 0, 0, J, C, "WT16", (C, rup(J, ops.KALIGN)))
     else:
         for w, off in ((qw, 0), (kw, Cq), (vw, 2 * Cq)):
             Wq = ps.rows("Wqkv", f32, w, C, C, row0=off, rows=J)
@@ -475,7 +480,8 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         # the pool part as extra partial rows written by the projection backward (B*P*P <= 4096: the
         # one-launch small kernel), else by the finalize (dfcsa_bn_bwd_finalize_pool)
         Np = Pp * Pp
-        rows_in_proj = B * Np <= 4096 and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
+        rows_in_proj = (B * Np <= 4096 and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
+                        and not (isinstance(s.A, FlashSaved) and s.A.qkv16 is not None))
         ncr = (B * Np + 15) // 16 if rows_in_proj else 0
         part2 = torch.empty((nte + ncr) * 2 * C, device=dev, dtype=f32)
         pool_rows = (wsum, bn2.mean, bn2.invstd, P(part2) + nte * 2 * C * 4, H, W) if rows_in_proj else None
@@ -647,35 +653,44 @@ WGRAD_LATE = [os.environ.get("DFCSA_WGRAD_LATE", "1") == "1"]
 ENTRY_WS = [os.environ.get("DFCSA_ENTRY_WS", "1") == "1"]
 
 
-# pooled attention above this many tokens: the N x N products as batched fp32 library GEMMs (the
-# one-workgroup-per-query-row kernels are sized for P <= 8; at P = 32 they were 68 of 79 ms/step).
-# Measured at 224^2, B = 16 with DFCSA_LSA_GEMM_MIN_N=64: P = 16 981 -> 1173 img/s, P = 32 201 -> 858.
-# OFF by default: the model-level gradients against the float64 oracle at P = 16 came out ~1e-2
-# relative on some tensors with it against ~1e-5 on the per-row kernels (tools/pool_path_diag2.py),
-# not yet explained (the batched GEMMs themselves are fp32-exact, tools/bmm_precision_check.py)
-LSA_GEMM_MIN_N = int(os.environ.get("DFCSA_LSA_GEMM_MIN_N", str(1 << 30)))
-
-# pooled attention above this many tokens (N = P*P) on the flash kernels (dfcsa_lsa_flash_fwd / _bwd:
-# bf16 MFMA in bf16 mode where the widths allow, the generic fp32 kernels otherwise; nothing N x N is
-# stored); at and below it, the per-row fp32 kernels (dfcsa_lsa_attn / dfcsa_lsa_attn_bwd) sized for
-# the shipped P = 4 / 8.  DFCSA_LSA_FLASH_MIN_N
-LSA_FLASH_MIN_N = [int(os.environ.get("DFCSA_LSA_FLASH_MIN_N", "64"))]
+# pooled attention above this many tokens (N = P*P) in bf16 mode on the flash kernels
+# (dfcsa_lsa_flash_fwd / _bwd: bf16 MFMA, online softmax, P recomputed from the row log-sum-exp in the
+# backward, nothing N x N stored); at and below it, and in fp32 (parity) mode, the per-row fp32 kernels
+# (dfcsa_lsa_attn / dfcsa_lsa_attn_bwd).  DFCSA_LSA_FLASH_MIN_N; same-box bench at 224^2, B = 16: P = 8
+# 1484 -> 1533 img/s with its 64 tokens on the flash kernels, P = 4 1620 -> 1600 (profiles/r06g_pools.jsonl)
+LSA_FLASH_MIN_N = [int(os.environ.get("DFCSA_LSA_FLASH_MIN_N", "32"))]
+# the flash kernels' fp32 variant (generic, one wave per row) for fp32 mode and for the widths the
+# MFMA kernels do not take: off by default (the per-row kernels are the fp32 path); tests switch it on
+LSA_FLASH_FP32 = [os.environ.get("DFCSA_LSA_FLASH_FP32", "0") == "1"]
 
 
 class FlashSaved:
-    """What the flash path keeps for the backward in place of A: the row log-sum-exp and the bf16 copy
-    of qkv the MFMA kernels read (None on the fp32 kernels)."""
-    __slots__ = ("lse", "qkv16")
+    """What the flash path keeps for the backward in place of A: the row log-sum-exp and, on the bf16
+    MFMA kernels, qkv and the pooled map in bf16 (the projection GEMMs' operands; None on the fp32
+    kernels)."""
+    __slots__ = ("lse", "qkv16", "pooled16")
 
-    def __init__(self, lse, qkv16):
-        self.lse, self.qkv16 = lse, qkv16
+    def __init__(self, lse, qkv16=None, pooled16=None):
+        self.lse, self.qkv16, self.pooled16 = lse, qkv16, pooled16
 
 
-def _flash_dtype(dtype, C, Cq, J):
-    """(storage dtype code, bf16?) of the flash kernels for this layer."""
+def flash16_layer(dtype, C, Cq, pool_size):
+    """True when this layer's pooled attention runs on the bf16 flash kernels (with bf16 q/k/v
+    projection GEMMs)."""
+    J = 2 * Cq + C
+    return (dtype == torch.bfloat16 and pool_size * pool_size > LSA_FLASH_MIN_N[0] and _lsa_gemm_ok(C, J)
+            and _lib.LIB.dfcsa_lsa_flash_path(C, Cq, J) == 1)
+
+
+def _flash_mode(dtype, C, Cq, J, N):
+    """None (per-row kernels) or (storage dtype code, bf16?) of the flash kernels for this layer."""
+    if N <= LSA_FLASH_MIN_N[0]:
+        return None
     if dtype == torch.bfloat16 and _lib.LIB.dfcsa_lsa_flash_path(C, Cq, J) == 1:
         return _lib.DT_BF16, True
-    return _lib.DT_F32, False
+    if LSA_FLASH_FP32[0] and C <= 1024 and C % 4 == 0:
+        return _lib.DT_F32, False
+    return None
 
 
 def _lsa_gemm_ok(C, J):
@@ -697,52 +712,51 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     J = 2 * Cq + C
     S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
-    # the window sums feed the projection backward's extra rows (B*N <= 4096) or the pool-fused
-    # finalize (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
-    ws = window_sums and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C) and (N <= 256 or B * N <= 4096)
+    fm = _flash_mode(dtype, C, Cq, J, N)
+    f16 = fm is not None and fm[1]
+    # the window sums feed the projection backward's extra rows (B*N <= 4096, fp32 projections) or the
+    # pool-fused finalize (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
+    ws = window_sums and _lsa_gemm_ok(C, J) and (N <= 256 or (B * N <= 4096 and not f16))
     wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
     wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
     call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), P(wpart),
          stream())
     bqkv = pk["bqkv"]
     pooled = torch.empty((B, N, C), device=dev, dtype=f32)
-    qkv = torch.empty((B, N, J), device=dev, dtype=f32)
-    if _lsa_gemm_ok(C, J):
-        # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
-        call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
-        Kp = rup(C, ops.KALIGN)
-        Wp = pk["Wp"]
-        ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), Wp, Kp, J, [qkv], J, bias=bqkv)
-        Wqkv = None
-    else:
-        Wqkv, WqkvT = pk["Wqkv"], pk["WqkvT"]
-        call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
     o = torch.empty((B, N, C), device=dev, dtype=f32)
-    if N > LSA_FLASH_MIN_N[0] and N <= LSA_GEMM_MIN_N:
-        # softmax(q k^T) v on the flash kernels; the backward recomputes P from the row log-sum-exp
-        T, bf = _flash_dtype(dtype, C, Cq, J)
-        qkv16 = None
-        src = qkv
-        if bf:
-            qkv16 = torch.empty((B, N, J), device=dev, dtype=torch.bfloat16)
-            call("dfcsa_cast_f32", _lib.DT_BF16, ctypes.c_int64(B * N * J), P(qkv), P(qkv16), 0, stream())
-            src = qkv16
+    Wqkv = None
+    if f16:
+        # bf16 mode, large pools: the q/k/v projections as one bf16 implicit GEMM (the reference's 1x1
+        # convs under bf16 autocast) whose output feeds the bf16 flash kernels directly; the backward
+        # recomputes P from the row log-sum-exp (nothing N x N is stored)
+        bf = torch.bfloat16
+        call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
+        pooled16 = torch.empty((B, N, C), device=dev, dtype=bf)
+        call("dfcsa_cast_f32", _lib.DT_BF16, ctypes.c_int64(B * N * C), P(pooled), P(pooled16), 0, stream())
+        qkv16 = torch.empty((B, N, J), device=dev, dtype=bf)
+        ops.conv_gemm(bf, [(pooled16, 0, 0)], C, (1, B * N, 1), (B * N, 1), pk["Wp16"], rup(C, ops.KALIGN), J,
+                      [qkv16], J, bias=bqkv)
         lse = torch.empty(B * N, device=dev, dtype=f32)
-        call("dfcsa_lsa_flash_fwd", T, B, N, C, Cq, J, P(src), P(o), P(lse), stream())
-        A = FlashSaved(lse, qkv16)
-        if window_sums:
-            return pooled, qkv, A, o, Wqkv, wsum
-        return pooled, qkv, A, o, Wqkv
-    A = torch.empty((B, N, N), device=dev, dtype=f32)
-    if N > LSA_GEMM_MIN_N:
-        # q k^T and A v as batched fp32 library GEMMs, the row softmax in place between them
-        # (contiguous q / k / v: the column slices of qkv start at arbitrary 4-byte offsets)
-        q, k, v = qkv[:, :, :Cq].contiguous(), qkv[:, :, Cq:2 * Cq].contiguous(), qkv[:, :, 2 * Cq:].contiguous()
-        torch.bmm(q, k.transpose(1, 2), out=A)
-        call("dfcsa_softmax_rows_f32", ctypes.c_int64(B * N), N, P(A), stream())
-        torch.bmm(A, v, out=o)
+        call("dfcsa_lsa_flash_fwd", _lib.DT_BF16, B, N, C, Cq, J, P(qkv16), P(o), P(lse), stream())
+        A = FlashSaved(lse, qkv16, pooled16)
+        qkv = None
     else:
-        call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
+        qkv = torch.empty((B, N, J), device=dev, dtype=f32)
+        if _lsa_gemm_ok(C, J):
+            # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
+            call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
+            ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), pk["Wp"], rup(C, ops.KALIGN), J, [qkv],
+                          J, bias=bqkv)
+        else:
+            Wqkv, WqkvT = pk["Wqkv"], pk["WqkvT"]
+            call("dfcsa_lsa_qkv", B, H, W, C, Cq, Pp, P(part), P(WqkvT), P(bqkv), P(pooled), P(qkv), stream())
+        if fm is not None:   # the flash kernels' fp32 variant (opt-in: LSA_FLASH_FP32)
+            lse = torch.empty(B * N, device=dev, dtype=f32)
+            call("dfcsa_lsa_flash_fwd", _lib.DT_F32, B, N, C, Cq, J, P(qkv), P(o), P(lse), stream())
+            A = FlashSaved(lse)
+        else:
+            A = torch.empty((B, N, N), device=dev, dtype=f32)
+            call("dfcsa_lsa_attn", B, N, C, Cq, P(qkv), P(A), P(o), stream())
     if window_sums:
         return pooled, qkv, A, o, Wqkv, wsum
     return pooled, qkv, A, o, Wqkv
@@ -777,21 +791,18 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
         call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
              P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
         if isinstance(A, FlashSaved):
-            T, bf = _flash_dtype(dtype, C, Cq, J)
+            f16 = A.qkv16 is not None
+            T = _lib.DT_BF16 if f16 else _lib.DT_F32
             nb = ctypes.c_int64()
             call("dfcsa_lsa_flash_bwd_bytes", T, B, N, C, Cq, J, ctypes.byref(nb))
             work = torch.empty((nb.value + 15) // 16 * 4, device=dev, dtype=f32)
-            call("dfcsa_lsa_flash_bwd", T, B, N, C, Cq, J, P(A.qkv16 if bf else qkv), P(dO), P(o), P(A.lse),
+            if f16:
+                dqkv = torch.empty((B, N, J), device=dev, dtype=torch.bfloat16)
+            call("dfcsa_lsa_flash_bwd", T, B, N, C, Cq, J, P(A.qkv16 if f16 else qkv), P(dO), P(o), P(A.lse),
                  P(dqkv), P(work), ctypes.c_int64(work.numel() * 4), stream())
             del work
-        elif N > LSA_GEMM_MIN_N:
-            # dA = dO v^T; dE = A (dA - rowsum(A dA)) in place; dq = dE k, dk = dE^T q, dv = A^T dO
-            q, k, v = qkv[:, :, :Cq].contiguous(), qkv[:, :, Cq:2 * Cq].contiguous(), qkv[:, :, 2 * Cq:].contiguous()
-            dE = torch.bmm(dO, v.transpose(1, 2))
-            call("dfcsa_softmax_bwd_rows_f32", ctypes.c_int64(B * N), N, P(A), P(dE), stream())
-            dqkv[:, :, :Cq] = torch.bmm(dE, k)
-            dqkv[:, :, Cq:2 * Cq] = torch.bmm(dE.transpose(1, 2), q)
-            dqkv[:, :, 2 * Cq:] = torch.bmm(A.transpose(1, 2), dO)
+            if f16:
+                return _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
         else:
             dE = torch.empty((B, N, N), device=dev, dtype=f32)
             call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())
@@ -813,6 +824,28 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
     return dpooled
 
 
+def _lsa_proj_bwd_bf16(lsa, pooled16, dqkv16, B, N, C, Cq, pk):
+    """Backward of the bf16 q/k/v projections of a flash layer: dW = dqkv^T pooled (bf16 weight-gradient
+    GEMM into the fp32 gradients, stacked q/k/v rows -> three tensors), db = column sums of dqkv,
+    dpooled = dqkv Wqkv (bf16 implicit GEMM, widened to fp32 for the attention-entry backward)."""
+    dev = dqkv16.device
+    f32, bf = torch.float32, torch.bfloat16
+    J, BN = 2 * Cq + C, B * N
+    qw, kw, vw = lsa.query_conv.weight, lsa.key_conv.weight, lsa.value_conv.weight
+    ops.conv_wgrad_into(bf, [dqkv16], J, [(pooled16, 0, 0)], C, (1, BN, 1), (BN, 1),
+                        [grad_of(qw), grad_of(kw), grad_of(vw)], 1, Cq, C, layout=2)
+    nt = ops.ntiles_ew(BN, J)
+    part = torch.empty(nt * J, device=dev, dtype=f32)
+    call("dfcsa_channel_sum", _lib.DT_BF16, BN, J, P(dqkv16), *S(part), stream())
+    call("dfcsa_slab_colsum3", P(part), nt, J, Cq, Cq, P(grad_of(lsa.query_conv.bias)),
+         P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)), stream())
+    dp16 = torch.empty((B, N, C), device=dev, dtype=bf)
+    ops.conv_gemm(bf, [(dqkv16, 0, 0)], J, (1, BN, 1), (BN, 1), pk["WT16"], rup(J, ops.KALIGN), C, [dp16], C)
+    dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
+    call("dfcsa_bf16_to_f32", ctypes.c_int64(BN * C), P(dp16), P(dpooled), stream())
+    return dpooled
+
+
 class LSAFunction(torch.autograd.Function):
     """Standalone LightSelfAttention on an NHWC tensor (no BatchNorm/ReLU in front)."""
 
@@ -822,7 +855,8 @@ class LSAFunction(torch.autograd.Function):
         dev = x.device
         one = torch.ones(C, device=dev)
         zero = torch.zeros(C, device=dev)
-        pk = get_packset(lsa, ("lsa", param_key(lsa)), lambda ps: _build_lsa_packs(ps, lsa))
+        pk = get_packset(lsa, ("lsa", dtype, pool_size, LSA_FLASH_MIN_N[0], param_key(lsa)),
+                         lambda ps: _build_lsa_packs(ps, lsa, dtype, pool_size))
         saved = lsa_core_forward(lsa, x, one, zero, False, pool_size, dtype, pk)
         out = torch.empty_like(x)
         call("dfcsa_block_local_attn", dt(dtype), B, H, W, C, None, None, None, P(x), P(one), P(zero),

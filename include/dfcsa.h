@@ -468,26 +468,24 @@ int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partia
                   const float* bias, float* pooled, float* qkv, void* stream);
 /* A = softmax_rows(q k^T) [B][N][N]; o[n][c] = sum_m A[n][m] v[m][c]  [B][N][C] */
 int dfcsa_lsa_attn(int B, int N, int C, int Cq, const float* qkv, float* A, float* o, void* stream);
-/* Pooled attention on the opt-in GEMM path (DFCSA_LSA_GEMM_MIN_N): the energy q k^T, the output A v and the gradient
- * products run as batched library GEMMs; these two do the row softmax in place over E [rows][N] and
- * its backward in place over dA (dE = A * (dA - sum_m A dA)). */
-int dfcsa_softmax_rows_f32(int64_t rows, int N, float* E, void* stream);
-int dfcsa_softmax_bwd_rows_f32(int64_t rows, int N, const float* A, float* dA, void* stream);
 /* Pooled attention for large pools (P >= 8: configs/config_dfc-sa-res-block-p16.yaml / -p32.yaml,
  * N = 256 / 1024 tokens; replaces the bmm -> softmax -> bmm of unet_dfc_sa_res.py:30-33 and their
  * autograd backward) on the flash kernels of fra.hip with gamma = 1: nothing N x N is stored.
  *   fwd: o [B][N][C] fp32 = softmax_rows(q k^T) v, lse [B*N] = log-sum-exp of each score row.
- *   bwd: dqkv [B][N][ldq] fp32 from dO [B][N][C] fp32 (= gamma * U^T dattn) and the saved o / lse;
- *        work: dfcsa_lsa_flash_bwd_bytes bytes of device scratch (16-byte aligned).
+ *   bwd: dqkv [B][N][ldq] (the dtype of qkv) from dO [B][N][C] fp32 (= gamma * U^T dattn) and the
+ *        saved o / lse; work: dfcsa_lsa_flash_bwd_bytes bytes of device scratch (16-byte aligned).
  * qkv [B][N][ldq], ldq = 2Cq + C, C <= 1024, is fp32 (dtype DFCSA_DT_F32: the generic fp32 kernels)
- * or its bf16 copy (DFCSA_DT_BF16: bf16 MFMA kernels, only where dfcsa_lsa_flash_path(C, Cq, ldq)
- * returns 1: C % 64 == 0, Cq a power of two in [8, 128]). */
+ * or bf16 (DFCSA_DT_BF16: bf16 MFMA kernels, only where dfcsa_lsa_flash_path(C, Cq, ldq) returns 1:
+ * C % 64 == 0, Cq a power of two in [8, 128]; the q/k/v projections then run as bf16 GEMMs too, as
+ * the reference's 1x1 convs do under bf16 autocast). */
 int dfcsa_lsa_flash_path(int C, int Cq, int ldq);
 int dfcsa_lsa_flash_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, float* o, float* lse,
                         void* stream);
 int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq, int ldq, int64_t* bytes);
 int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const float* dO,
-                        const float* o, const float* lse, float* dqkv, void* work, int64_t work_bytes, void* stream);
+                        const float* o, const float* lse, void* dqkv, void* work, int64_t work_bytes, void* stream);
+/* dst[i] = src[i] (bf16 -> fp32), n % 8 == 0, 16-byte aligned pointers */
+int dfcsa_bf16_to_f32(int64_t n, const void* src, float* dst, void* stream);
 /* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
 int dfcsa_lsa_up_bwd_rows(int dtype, int B, int H, int W, int C, const void* dattn, int P, float* rows,
                           void* stream);

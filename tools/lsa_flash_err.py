@@ -60,6 +60,7 @@ report("ref-amp", ya.float(), xa.grad, {k[2:]: v.grad for k, v in sa.items()})
 for tag, dtype, min_n in (("flash-bf16", torch.bfloat16, 64), ("row-bf16", torch.bfloat16, 1 << 30),
                           ("flash-fp32", torch.float32, 64), ("row-fp32", torch.float32, 1 << 30)):
     block.LSA_FLASH_MIN_N[0] = min_n
+    block.LSA_FLASH_FP32[0] = True
     mg = LightSelfAttention(C, pool_size=P)
     mg.load_state_dict(m.state_dict())
     mg = mg.cuda()
