@@ -3303,6 +3303,8 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 33: return g_stream_min_m;
     case 34: return g_stream_shuf;
     case 35: return g_lsa_cols_nt;
+    case 45: return g_lsa_pool_wpb;
+    case 46: return g_lsa_pool_one_slice;
     case 36: return g_gate_grid_div;
     case 37: return g_splitk_min_nk;
     case 39: return g_bn_fold;
@@ -3343,6 +3345,8 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 33) { g_stream_min_m = value; return 0; }
   if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
+  if (knob == 45) { g_lsa_pool_wpb = value ? 1 : 0; return 0; }
+  if (knob == 46) { g_lsa_pool_one_slice = value ? 1 : 0; return 0; }
   if (knob == 36) { g_gate_grid_div = value; return 0; }
   if (knob == 39) { g_bn_fold = value; return 0; }
   if (knob == 40) { g_ppsk = value; return 0; }

@@ -18,6 +18,8 @@
 
 int g_lsa_rows_old = 0;
 int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
+int g_lsa_pool_wpb = 0;     // knob 45: 1 = several pool windows per workgroup at P >= 16 (measured slower: off)
+int g_lsa_pool_one_slice = 1;   // knob 46: 0 = split the <= 8-row windows of P >= 16 pools into row slices (old)
 
 namespace {
 
@@ -76,14 +78,19 @@ __device__ __forceinline__ float block_reduce_max(float v, float* sh) {
 
 int pool_splits(int H, int P) {
   int maxwh = (H + P - 1) / P + 1;
+  // large pools' small windows (P >= 16, <= 8 rows: P = 32 on 224^2 is 7 x 7) in one slice: 3 slices of
+  // ~16 pixels per workgroup left the launch to workgroup overheads (114 us per launch at P = 32 with
+  // the window sums); P * P windows per image are plenty of workgroups without the split
+  if (P >= 16 && maxwh <= 8 && g_lsa_pool_one_slice) return 1;
   int s = (maxwh + 3) / 4;
   return s < 1 ? 1 : s;
 }
 
 // grid (S, ceil(N / wpb), B): row slice s of windows n = blockIdx.y * wpb + t (t < wpb) of image b.
 // One load in flight per lane at 45 VGPRs: occupancy hides the latency (an eight-loads-in-flight
-// variant at 108 VGPRs measured slower, profiles/r03c_lsa_bench.jsonl).  wpb > 1 for large pools,
-// whose small windows (7 x 7 at P = 32 on 224^2) left most of a one-window workgroup idle
+// variant at 108 VGPRs measured slower, profiles/r03c_lsa_bench.jsonl).  wpb > 1 (knob 45, off): large
+// pools' small windows (7 x 7 at P = 32 on 224^2) leave most of a one-window workgroup idle, but
+// batching windows serialises them per workgroup -- measured slower (614 -> 690 us per step at P = 32)
 template <typename T, bool WS = false>
 __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, const T* __restrict__ y2,
                                                        const float* __restrict__ sc, const float* __restrict__ sh,
@@ -732,7 +739,7 @@ extern "C" int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const vo
   // windows per workgroup: enough pixels per slice to fill the 256 / (C / 8) pixel lanes a few times
   const int wpx = ((H + P - 1) / P) * ((W + P - 1) / P) / S;
   const int lanes = 256 / std::max(1, C / 8);
-  const int wpb = P >= 16 ? std::max(1, std::min(8, (2 * lanes) / std::max(1, wpx))) : 1;
+  const int wpb = (P >= 16 && g_lsa_pool_wpb) ? std::max(1, std::min(8, (2 * lanes) / std::max(1, wpx))) : 1;
   dim3 grid(S, (P * P + wpb - 1) / wpb, B);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DFCSA_DT_BF16) {
@@ -1020,6 +1027,61 @@ extern "C" int dfcsa_lsa_proj_bwd(int B, int N, int C, int Cq, const float* dqkv
   DFCSA_CHECK_LAUNCH();
   hipLaunchKernelGGL(lsa_proj_dx_kernel, dim3((C + 255) / 256, BN), dim3(256), (size_t)J * sizeof(float), st, C, Cq,
                      dqkv, w, dpooled);
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+// The attention entry's pool-backward BatchNorm sums as partial rows (the pool term of
+// dfcsa_bwd_attn_entry's statistics, as dfcsa_conv_wgrad_dgrad1x1_pool's epilogue forms them for the
+// fp32 projections): for the 16 tokens m of row block bx and channel c,
+//   rows[bx][0][c] = sum_m dpooled[m][c] / area(m) * wsum[m][0][c]
+//   rows[bx][1][c] = sum_m dpooled[m][c] / area(m) * invstd[c] * (wsum[m][1][c] - mean[c] * wsum[m][0][c])
+// grid (ceil(BN / 16), ceil(C / 64)), 256 threads: 4 token phases x 64 channels, fixed-order combine.
+namespace {
+__global__ void __launch_bounds__(256) lsa_pool_rows_kernel(int BN, int C, int P, int H, int W,
+                                                            const float* __restrict__ dpooled,
+                                                            const float* __restrict__ wsum,
+                                                            const float* __restrict__ mean,
+                                                            const float* __restrict__ invstd,
+                                                            float* __restrict__ rows) {
+  __shared__ float red[2][4][64];
+  const int bx = blockIdx.x, cl = threadIdx.x & 63, ph = threadIdx.x >> 6;
+  const int c = blockIdx.y * 64 + cl, NP = P * P;
+  float s0 = 0.f, s1 = 0.f;
+  if (c < C) {
+    const float mu = mean[c], is = invstd[c];
+    for (int k = 0; k < 4; ++k) {
+      const int m = bx * 16 + ph + 4 * k;
+      if (m >= BN) break;
+      const int n = m % NP, pi = n / P, pj = n - pi * P;
+      const float area = (float)(((pi + 1) * H + P - 1) / P - (pi * H) / P) *
+                         (float)(((pj + 1) * W + P - 1) / P - (pj * W) / P);
+      const float dd = dpooled[(size_t)m * C + c] / area;
+      const float R = wsum[((size_t)m * 2) * C + c], Y = wsum[((size_t)m * 2 + 1) * C + c];
+      s0 += dd * R;
+      s1 += dd * is * (Y - mu * R);
+    }
+  }
+  red[0][ph][cl] = s0;
+  red[1][ph][cl] = s1;
+  __syncthreads();
+  if (ph < 2 && c < C) {
+    const float v = (red[ph][0][cl] + red[ph][1][cl]) + (red[ph][2][cl] + red[ph][3][cl]);
+    rows[((size_t)bx * 2 + ph) * C + c] = v;
+  }
+}
+}  // namespace
+
+extern "C" int dfcsa_lsa_pool_rows(int BN, int C, int P, int H, int W, const float* dpooled, const float* wsum,
+                                   const float* mean, const float* invstd, float* rows, int64_t rows_floats,
+                                   void* stream) {
+  if (BN <= 0 || C <= 0 || P <= 0 || H <= 0 || W <= 0 || BN % (P * P) || !dpooled || !wsum || !mean || !invstd ||
+      !rows)
+    return DFCSA_EINVAL;
+  const int nb = (BN + 15) / 16;
+  if (rows_floats < (int64_t)nb * 2 * C) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(lsa_pool_rows_kernel, dim3(nb, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, BN, C, P, H, W,
+                     dpooled, wsum, mean, invstd, rows);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -478,10 +478,11 @@ def block_backward(blk, s, dout, need_dx, dtype, pool_grads=None):
         # pool part is a [B][N][C] contraction with the forward pool's window sums, inside the
         # finalize (dfcsa_bn_bwd_finalize_pool)
         # the pool part as extra partial rows written by the projection backward (B*P*P <= 4096: the
-        # one-launch small kernel), else by the finalize (dfcsa_bn_bwd_finalize_pool)
+        # one-launch small kernel) or after the bf16 projection backward of a flash layer
+        # (dfcsa_lsa_pool_rows), else by the finalize (dfcsa_bn_bwd_finalize_pool)
         Np = Pp * Pp
-        rows_in_proj = (B * Np <= 4096 and _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C)
-                        and not (isinstance(s.A, FlashSaved) and s.A.qkv16 is not None))
+        flash16 = isinstance(s.A, FlashSaved) and s.A.qkv16 is not None
+        rows_in_proj = _lsa_gemm_ok(C, 2 * lsa.query_conv.out_channels + C) and (B * Np <= 4096 or flash16)
         ncr = (B * Np + 15) // 16 if rows_in_proj else 0
         part2 = torch.empty((nte + ncr) * 2 * C, device=dev, dtype=f32)
         pool_rows = (wsum, bn2.mean, bn2.invstd, P(part2) + nte * 2 * C * 4, H, W) if rows_in_proj else None
@@ -664,6 +665,12 @@ LSA_FLASH_MIN_N = [int(os.environ.get("DFCSA_LSA_FLASH_MIN_N", "32"))]
 LSA_FLASH_FP32 = [os.environ.get("DFCSA_LSA_FLASH_FP32", "0") == "1"]
 
 
+# pooled attention with N > 64 tokens: dgamma of the upsample backward as a separate sum over per-token
+# partials instead of the in-kernel ticket (DFCSA_LSA_DGAMMA_SPLIT=0: in-kernel, N / 64 tokens per
+# workgroup)
+LSA_DGAMMA_SPLIT = [os.environ.get("DFCSA_LSA_DGAMMA_SPLIT", "1") == "1"]
+
+
 class FlashSaved:
     """What the flash path keeps for the backward in place of A: the row log-sum-exp and, on the bf16
     MFMA kernels, qkv and the pooled map in bf16 (the projection GEMMs' operands; None on the fp32
@@ -714,9 +721,10 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     part = torch.empty(B * N * S * C, device=dev, dtype=f32)
     fm = _flash_mode(dtype, C, Cq, J, N)
     f16 = fm is not None and fm[1]
-    # the window sums feed the projection backward's extra rows (B*N <= 4096, fp32 projections) or the
-    # pool-fused finalize (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
-    ws = window_sums and _lsa_gemm_ok(C, J) and (N <= 256 or (B * N <= 4096 and not f16))
+    # the window sums feed the projection backward's extra rows (B*N <= 4096, fp32 projections), the
+    # pool-rows kernel (bf16 flash layers, dfcsa_lsa_pool_rows) or the pool-fused finalize
+    # (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
+    ws = window_sums and _lsa_gemm_ok(C, J) and (f16 or N <= 256 or B * N <= 4096)
     wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
     wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
     call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), P(wpart),
@@ -788,8 +796,15 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
     else:
         dO = torch.empty((B, N, C), device=dev, dtype=f32)
         gpart = torch.empty(B * N, device=dev, dtype=f32)
-        call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
-             P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
+        if N > 64 and LSA_DGAMMA_SPLIT[0]:
+            # large pools: one workgroup per token (full parallelism) and dgamma as a separate fixed-order
+            # sum -- the in-kernel last-arriver sum takes one ticket atomic per workgroup
+            call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None, None,
+                 stream())
+            call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
+        else:
+            call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
+                 P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
         if isinstance(A, FlashSaved):
             f16 = A.qkv16 is not None
             T = _lib.DT_BF16 if f16 else _lib.DT_F32
@@ -802,7 +817,12 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
                  P(dqkv), P(work), ctypes.c_int64(work.numel() * 4), stream())
             del work
             if f16:
-                return _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
+                dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
+                if pool_rows is not None:   # the attention entry's pool-backward BatchNorm rows
+                    wsum, mean, invstd, rows_ptr, Hh, Ww = pool_rows
+                    call("dfcsa_lsa_pool_rows", B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum), P(mean), P(invstd),
+                         rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
+                return dpooled
         else:
             dE = torch.empty((B, N, N), device=dev, dtype=f32)
             call("dfcsa_lsa_attn_bwd", B, N, C, Cq, P(qkv), P(A), P(dO), P(dE), P(dqkv), stream())

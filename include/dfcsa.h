@@ -484,6 +484,12 @@ int dfcsa_lsa_flash_fwd(int dtype, int B, int N, int C, int Cq, int ldq, const v
 int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq, int ldq, int64_t* bytes);
 int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const float* dO,
                         const float* o, const float* lse, void* dqkv, void* work, int64_t work_bytes, void* stream);
+/* The attention entry's pool-backward BatchNorm sums as ceil(BN/16) partial rows [row][2][C] (the rows
+ * dfcsa_conv_wgrad_dgrad1x1_pool's epilogue adds for the fp32 projections), from dpooled [BN][C] and the
+ * forward's window sums wsum [BN][2][C]: for the bf16 projections of the flash layers.  rows_floats:
+ * capacity of rows in floats. */
+int dfcsa_lsa_pool_rows(int BN, int C, int P, int H, int W, const float* dpooled, const float* wsum,
+                        const float* mean, const float* invstd, float* rows, int64_t rows_floats, void* stream);
 /* dst[i] = src[i] (bf16 -> fp32), n % 8 == 0, 16-byte aligned pointers */
 int dfcsa_bf16_to_f32(int64_t n, const void* src, float* dst, void* stream);
 /* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
@@ -887,6 +893,8 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 42: LDS-DMA ring depth of the buffer-descriptor weight-gradient kernel (2 = default, 3, 4).
  * knob 43: 1 = single-buffer C = 128 forward prologue GEMMs (two workgroups per CU; default 1).
  * knob 44: 1 = single-buffer KP = 256 fused gate dgrad kernels (two workgroups per CU).
+ * knob 45: 1 = several LightSelfAttention pool windows per workgroup at P >= 16 (default 0: measured slower).
+ * knob 46: 0 = LightSelfAttention pool windows of <= 8 rows split into row slices too (default 1: one slice).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -119,3 +119,66 @@ def test_flash_rejects_bad_shapes():
     assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_F32, 2, 256, 48, 6, 61, ctypes.byref(nb)) != 0   # ldq != 2Cq + C
     assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_F32, 2, 256, 48, 6, 60, ctypes.byref(nb)) == 0 and nb.value > 0
     assert np.isfinite(nb.value)
+
+
+def _cos(a, b):
+    a, b = a.reshape(-1).double().cpu(), b.reshape(-1).double().cpu()
+    return (a @ b / (a.norm() * b.norm() + 1e-300)).item()
+
+
+@pytest.mark.parametrize("P", [8, 16, 32])
+def test_flash_model_bf16_step_vs_float64(P, monkeypatch):
+    """The whole bf16 train step at pool size P (64..512 features, 64 x 64, B = 2) with the pooled
+    attention on the flash kernels (bf16 projections, the entry's pool-backward BatchNorm rows from
+    dfcsa_lsa_pool_rows), against the float64 oracle (oracle/dfcsa_oracle.py) beside the same bf16 step
+    with the per-row fp32 attention kernels: logits and loss within the per-row path's own distance to
+    float64 plus 1e-2; the whole gradient's cosine distance to float64 at most 1.5x the per-row path's
+    + 2e-3; every non-scalar attention-branch tensor's at most 2x + 1e-2.  (At 64 x 64 with pools as
+    large as the maps the bf16 step itself is far from float64 -- whole-gradient cosine ~0.96 on both
+    paths -- so the bar is relative to the per-row path, not absolute.)"""
+    from dfcsa import block
+    from dfcsa.loss import sigmoid
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    from oracle import dfcsa_oracle as O
+    from utils.metrics import calculate_metrics
+    torch.manual_seed(500 + P)
+    m0 = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=P, precision="bf16")
+    with torch.no_grad():
+        for i, (n, p) in enumerate(sorted(m0.named_parameters())):
+            if n.endswith("gamma"):
+                p.fill_(0.3 + 0.05 * (i % 5))
+    sd = {k: v.detach().clone() for k, v in m0.state_dict().items()}
+    g0 = torch.Generator().manual_seed(600 + P)
+    x = torch.randn(2, 3, 64, 64, generator=g0)
+    t = (torch.rand(2, 1, 64, 64, generator=g0) > 0.5).float()
+    sd64 = {k: (v.double() if v.is_floating_point() else v) for k, v in sd.items()}
+    logits64, met64, g64, _ = O.forward_backward(sd64, x.double(), t.double(), P, {})
+    runs = {}
+    for tag, min_n in (("row", 1 << 30), ("flash", 32)):
+        monkeypatch.setattr(block, "LSA_FLASH_MIN_N", [min_n])
+        m = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=P, precision="bf16")
+        m.load_state_dict(sd)
+        m = m.cuda().train()
+        logits = m(x.cuda())
+        met = calculate_metrics(sigmoid(logits), t.cuda(), "bce_dice", {})
+        met["loss"].backward()
+        torch.cuda.synchronize()
+        runs[tag] = (logits.float(), met["loss"].item(), {n: p.grad.detach() for n, p in m.named_parameters()})
+    names = [n for n in g64 if not n.endswith(("conv_branch.0.bias", "attn_branch.0.bias", "gate.0.bias",
+                                                  "fusion_conv.0.bias", "key_conv.bias"))]
+    ref = torch.cat([g64[n].reshape(-1) for n in names])
+    dist = {}
+    for tag, (lg, loss, gr) in runs.items():
+        whole = 1 - _cos(torch.cat([gr[n].reshape(-1).double().cpu() for n in names]), ref)
+        # non-scalar attention-branch tensors (a scalar's "cosine" is its sign: gamma's gradient is one
+        # cancelling sum whose sign bf16 noise can flip on either path)
+        attn = {n: 1 - _cos(gr[n], g64[n]) for n in names
+                if ".attn_branch." in n and g64[n].numel() > 1 and g64[n].norm() > 0}
+        dist[tag] = (rel(lg, logits64), abs(loss - met64["loss"].item()) / abs(met64["loss"].item()), whole, attn)
+        print(f"P={P} {tag}: logits {dist[tag][0]:.3e} loss {dist[tag][1]:.3e} whole-gradient 1-cos {whole:.3e} "
+              f"worst attention tensor 1-cos {max(attn.values()):.3e}")
+    (lr, sr, wr, ar), (lf, sf, wf, af) = dist["row"], dist["flash"]
+    assert lf <= lr + 1e-2 and sf <= sr + 1e-2
+    assert wf <= 1.5 * wr + 2e-3, (wf, wr)
+    for n in af:
+        assert af[n] <= 2 * ar[n] + 1e-2, (n, af[n], ar[n])
