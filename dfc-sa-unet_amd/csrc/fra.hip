@@ -719,13 +719,18 @@ fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
 //   S^T = K Q^T, dPy'^T = V dy^T - r_q (the MFMA chain starts from -r_q), dS^T / gamma = P^T dPy'^T,
 //   dQ^T[d][q] += K^T[d][k] (dS / gamma)^T[k][q], scaled by gamma at the end.  Keys past N are
 //   masked on the last tile only (tile-uniform branch).
+// kbar != nullptr ([B][CQ] fp32, the image's mean key): dQ = sum_k dS16 (K_k - kbar).  Exact dS rows
+//   sum to zero (softmax), so subtracting any fixed key changes nothing -- but the bf16-ROUNDED dS16 rows
+//   do not, and their rounding residue times the mean key is a coherent error that dominates dQ (and
+//   the query bias gradient, sum over queries) when the keys are alike, as pooled features are.  The
+//   row sums come from one more MFMA against a ones fragment, so the subtraction is exact in fp32.
 template <int CQ, int C, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                        const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
                                                        const float* __restrict__ lse, const float* __restrict__ rr,
                                                        bf16_t* __restrict__ dqkv, float* __restrict__ part,
-                                                       int64_t rstride) {
+                                                       int64_t rstride, const float* __restrict__ kbar) {
   constexpr int KT = 64;
   constexpr int KC = CQ < 16 ? 16 : CQ;
   constexpr int KBy = KT * KC * 2, VBy = KT * C * 2, TB = KBy + VBy;
@@ -755,11 +760,15 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     const float nr = (ok && (ch == 0 || rstride)) ? -rr[(size_t)b * N + q + ch * rstride] : 0.f;  // (see dK/dV)
     nR[qb] = f32x4_t{nr, nr, nr, nr};
   }
-  f32x4_t dqa[2][NDB];
+  f32x4_t dqa[2][NDB], rsum[2];
 #pragma unroll
-  for (int qb = 0; qb < 2; ++qb)
+  for (int qb = 0; qb < 2; ++qb) {
+    rsum[qb] = zero4();
 #pragma unroll
     for (int db = 0; db < NDB; ++db) dqa[qb][db] = zero4();
+  }
+  const short b1 = 0x3F80;   // bf16 1.0
+  const bf16x8_t ones = {b1, b1, b1, b1, b1, b1, b1, b1};
   const float gm = *gamma;
 
   Stage<KT, CQ / 8> sk;
@@ -818,6 +827,10 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) dqa[qb][db] = mfma32(a, sb[qb], dqa[qb][db]);
       }
+      if (kbar) {   // column sums of the rounded dS^T tile (every row of rsum holds them)
+#pragma unroll
+        for (int qb = 0; qb < 2; ++qb) rsum[qb] = mfma32(ones, sb[qb], rsum[qb]);
+      }
     }
     if (t + 1 < ntiles) {
       char* nx = smem + ((t + 1) & 1) * TB;
@@ -835,6 +848,12 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
       if (d < CQ) {
+        if (kbar) {
+          const float4 kb = *(const float4*)(kbar + (size_t)b * CQ + d);
+          const float rs = rsum[qb][0];
+          dqa[qb][db][0] -= rs * kb.x; dqa[qb][db][1] -= rs * kb.y;
+          dqa[qb][db][2] -= rs * kb.z; dqa[qb][db][3] -= rs * kb.w;
+        }
         if (part) {  // wide layers: this chunk's share of dQ (fp32, unscaled)
           float* pp = part + (((size_t)ch * gridDim.z + b) * N + q) * CQ + d;
           *(float4*)pp = make_float4(dqa[qb][db][0], dqa[qb][db][1], dqa[qb][db][2], dqa[qb][db][3]);
@@ -908,7 +927,8 @@ void launch_fwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* x,
 // shares) for fra_wide_finish.
 template <int CQ, int C>
 void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy, const float* gamma,
-                const float* lse, const float* rr, void* dqkv, float* part, hipStream_t st, int64_t rstride = 0) {
+                const float* lse, const float* rr, void* dqkv, float* part, hipStream_t st, int64_t rstride = 0,
+                const float* kbar = nullptr) {
   dim3 grid((N + 127) / 128, Ctot / C, B);
   float* pk = part;
   float* pq = part ? part + (size_t)(Ctot / C) * B * N * CQ : nullptr;
@@ -923,18 +943,18 @@ void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy
                        (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk, rstride);
   if (narrow && (occ & 4))
     hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride);
+                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
   else
     hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride);
+                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
 }
 
 template <int CQ>
 void launch_bwd_cq(int B, int N, int C, int ldq, const void* qkv, const void* dy, const float* gamma,
-                   const float* lse, const float* rr, void* dqkv, hipStream_t st) {
-  if (C == 64) launch_bwd<CQ, 64>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
-  else if (C == 128) launch_bwd<CQ, 128>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
-  else launch_bwd<CQ, 256>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st);
+                   const float* lse, const float* rr, void* dqkv, hipStream_t st, const float* kbar = nullptr) {
+  if (C == 64) launch_bwd<CQ, 64>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st, 0, kbar);
+  else if (C == 128) launch_bwd<CQ, 128>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st, 0, kbar);
+  else launch_bwd<CQ, 256>(B, N, ldq, C, qkv, dy, gamma, lse, rr, dqkv, nullptr, st, 0, kbar);
 }
 
 // Wide layers (C > 256: the 64^2 / 32^2 levels of config 5): value columns in chunks of kWideChunk.
@@ -1159,6 +1179,34 @@ __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, in
   if (lane == 0) r[row] = s;
 }
 
+// kbar[b][c] = mean over the image's N keys of the bf16 key column c (fp32, fixed order): the centre
+// fra_bwd_dq_mfma subtracts.  grid (B, ceil(Cq / cw)), cw = min(Cq, 64) columns x 256 / cw key slices.
+__global__ void __launch_bounds__(256) lsa_key_mean_kernel(int N, int Cq, int ldq, const bf16_t* __restrict__ qkv,
+                                                           float* __restrict__ kbar) {
+  __shared__ float red[256];
+  const int b = blockIdx.x, cw = Cq < 64 ? Cq : 64, nsl = 256 / cw;
+  const int sl = threadIdx.x / cw, c = blockIdx.y * cw + threadIdx.x % cw;
+  float s = 0.f;
+  if (c < Cq) {
+    const bf16_t* k = qkv + (size_t)b * N * ldq + Cq + c;
+    float a[4] = {0.f, 0.f, 0.f, 0.f};
+    int n = sl;
+    for (; n + 3 * nsl < N; n += 4 * nsl) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) a[u] += bf2f(k[(size_t)(n + u * nsl) * ldq]);
+    }
+    for (; n < N; n += nsl) a[0] += bf2f(k[(size_t)n * ldq]);
+    s = (a[0] + a[1]) + (a[2] + a[3]);
+  }
+  red[threadIdx.x] = s;
+  __syncthreads();
+  if (threadIdx.x < cw && c < Cq) {
+    float t = 0.f;
+    for (int i = 0; i < nsl; ++i) t += red[i * cw + threadIdx.x];
+    kbar[(size_t)b * Cq + c] = t / (float)N;
+  }
+}
+
 // dst (fp32) = src (bf16), 8 elements per thread (dfcsa_bf16_to_f32)
 __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const bf16_t* __restrict__ src,
                                                               float* __restrict__ dst) {
@@ -1174,9 +1222,9 @@ __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const 
   *(float4*)(dst + 8 * e + 4) = hi;
 }
 
-// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | wide partials
+// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | kbar [B][Cq] | wide partials
 struct LsaWork {
-  size_t one, r, dO16, part, total;
+  size_t one, r, dO16, kbar, part, total;
 };
 LsaWork lsa_work(int dtype, int B, int N, int C, int Cq, int ldq) {
   LsaWork w{};
@@ -1189,6 +1237,8 @@ LsaWork lsa_work(int dtype, int B, int N, int C, int Cq, int ldq) {
   if (dtype == DFCSA_DT_BF16) {
     w.dO16 = e;
     e += lsa_al(rows * C * 2);
+    w.kbar = e;
+    e += lsa_al((size_t)B * Cq * sizeof(float));
     if (wide) {
       w.part = e;
       e += lsa_al((size_t)2 * nch * rows * Cq * sizeof(float));
@@ -1266,21 +1316,28 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
     return 0;
   }
   bf16_t* dq16 = (bf16_t*)dqkv;
+  float* kb = nullptr;   // the mean key (dQ centring, fra_bwd_dq_mfma); knob 48 = 0 leaves dQ uncentred
+  if (g_lsa_key_centre) {
+    kb = (float*)(wb + w.kbar);
+    const int cw = Cq < 64 ? Cq : 64;
+    hipLaunchKernelGGL(lsa_key_mean_kernel, dim3(B, (Cq + cw - 1) / cw), dim3(256), 0, st, N, Cq, ldq,
+                       (const bf16_t*)qkv, kb);
+  }
   if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
     switch (Cq) {
-      case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
-      case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
-      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st); break;
-      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, nullptr, st); break;
+      case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, nullptr, st, 0, kb); break;
     }
   } else {
     float* part = (float*)(wb + w.part);
     switch (Cq) {
-      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
-      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
-      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
-      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
-      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows); break;
+      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
     }
     const int64_t threads = 2 * (int64_t)rows * (Cq / 4);
     hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (int64_t)rows, Cq,

@@ -19,6 +19,7 @@
 int g_lsa_rows_old = 0;
 int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
 int g_lsa_pool_wpb = 0;     // knob 45: 1 = several pool windows per workgroup at P >= 16 (measured slower: off)
+int g_lsa_key_centre = 1;   // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
 int g_lsa_pool_one_slice = 1;   // knob 46: 0 = split the <= 8-row windows of P >= 16 pools into row slices (old)
 
 namespace {

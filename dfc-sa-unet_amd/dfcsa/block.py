@@ -795,14 +795,15 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
              P(gpart), P(grad_of(lsa.gamma)), stream())
     else:
         dO = torch.empty((B, N, C), device=dev, dtype=f32)
-        gpart = torch.empty(B * N, device=dev, dtype=f32)
         if N > 64 and LSA_DGAMMA_SPLIT[0]:
-            # large pools: one workgroup per token (full parallelism) and dgamma as a separate fixed-order
-            # sum -- the in-kernel last-arriver sum takes one ticket atomic per workgroup
+            # large pools: dgamma as a separate fixed-order sum of the column pass's partials (the
+            # in-kernel last-arriver sum takes one ticket atomic per workgroup)
+            gpart = torch.empty(B * N, device=dev, dtype=f32)
             call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None, None,
                  stream())
             call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
         else:
+            gpart = torch.empty(B * N, device=dev, dtype=f32)
             call("dfcsa_lsa_up_bwd_cols", B, H, C, Pp, P(rows), P(o), P(lsa.gamma), P(dO), P(gpart), None,
                  P(grad_of(lsa.gamma)), stream())    # dgamma summed in-kernel
         if isinstance(A, FlashSaved):

@@ -895,6 +895,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 44: 1 = single-buffer KP = 256 fused gate dgrad kernels (two workgroups per CU).
  * knob 45: 1 = several LightSelfAttention pool windows per workgroup at P >= 16 (default 0: measured slower).
  * knob 46: 0 = LightSelfAttention pool windows of <= 8 rows split into row slices too (default 1: one slice).
+ * knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (default 1: dQ = sum_k dS (K_k - mean key)).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -19,14 +19,4 @@ for args in "--model unet --img 64 --batch 2 --precision fp32 --steps 50 --warmu
             "--model fullres --img 512 --batch 2 --steps 4 --warmup 2"; do
   timeout -k 10 400 python bench.py $args $S >> gpurun_out/${T}_bench_secondary.jsonl 2>> gpurun_out/${T}_bench_secondary.err || exit 1
 done
-cd /tmp && export TMPDIR=/tmp
-rm -rf $R/gpurun_out/p_trace $R/gpurun_out/p_fetch $R/gpurun_out/p_write $R/gpurun_out/p_sq
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_trace -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-kernel-timing $S > $R/gpurun_out/p_trace.log 2>&1 || exit 1
-# the bench command with its class-timing pass: the last 20 steps of this trace are the serialised
-# eager pass whose HIP-event class times the line reports (rocpd_export.py replay ... -> *_serial_classes.json)
-rm -rf $R/gpurun_out/p_trace_timing
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/p_trace_timing -o run -- python3 $R/bench.py --steps 20 --warmup 5 --no-live-trace $S > $R/gpurun_out/p_trace_timing.log 2>&1 || exit 1
-timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d $R/gpurun_out/p_fetch -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-kernel-timing --no-graph $S > $R/gpurun_out/p_fetch.log 2>&1 || exit 1
-timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d $R/gpurun_out/p_write -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-kernel-timing --no-graph $S > $R/gpurun_out/p_write.log 2>&1 || exit 1
-timeout -s KILL 300 rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_INSTS_MFMA SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_VALU SQ_WAIT_ANY GRBM_GUI_ACTIVE -d $R/gpurun_out/p_sq -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-kernel-timing --no-graph $S > $R/gpurun_out/p_sq.log 2>&1 || exit 1
-echo profile done
+echo part1 done
