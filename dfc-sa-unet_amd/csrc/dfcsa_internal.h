@@ -108,6 +108,7 @@ extern int g_wgrad_coop_launches;
 extern int g_wgrad_coop;   // knob 31: cooperative in-launch split-K reduction (0 = separate reduction launch)
 extern int g_small8;
 extern int g_lsa_rows_old;  // knob 28: 1 = the item-owner LightSelfAttention upsample-backward row kernel
+extern int g_lsa_pool_direct;  // knob 47: one wave per window for P >= 16 (dfcsa_lsa_pool_direct, default 1)
 extern int g_lsa_key_centre;  // knob 48: mean-key centred dQ in the bf16 pooled-attention backward (default 1)
 extern int g_lsa_pool_one_slice;  // knob 46: small pool windows in one row slice (default 1)
 extern int g_lsa_pool_wpb;  // knob 45: several pool windows per workgroup at P >= 16 (off)

@@ -19,7 +19,8 @@
 int g_lsa_rows_old = 0;
 int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
 int g_lsa_pool_wpb = 0;     // knob 45: 1 = several pool windows per workgroup at P >= 16 (measured slower: off)
-int g_lsa_key_centre = 1;   // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
+int g_lsa_key_centre = 1;
+int g_lsa_pool_direct = 1;   // knob 47: 0 = large pools on the sliced pool + pooled launches (old)   // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
 int g_lsa_pool_one_slice = 1;   // knob 46: 0 = split the <= 8-row windows of P >= 16 pools into row slices (old)
 
 namespace {
@@ -169,6 +170,85 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
       out[kk * 8 + q] = v;
     }
   }
+  }
+}
+
+// Large pools (P >= 16: 7 x 7 / 14 x 14 windows at 224^2): ONE WAVE per window, 4 windows (consecutive
+// pj of one pooled row) per workgroup, and the pooled values / window sums written directly -- no
+// partial slices, no block barrier, no separate dfcsa_lsa_pooled_ws launch (which at P = 32 was one
+// ~34 us launch of 16 k single-token workgroups per layer).  Lanes: cw = min(C / 8, 64) channel chunks
+// x 64 / cw pixel lanes (C / 8 a power of two or a multiple of 64, host-checked); the pixel lanes are
+// combined by xor shuffles.  Writes pooled [B][N][C] = window mean (fp32), optional pooled16 (bf16
+// copy, the projection GEMM's operand) and optional wsum [B][N][2][C] (sum r, sum r*y; see
+// lsa_pool_kernel).
+template <typename T, bool WS>
+__global__ void __launch_bounds__(256) lsa_pool_direct_kernel(int H, int W, int C, int P, const T* __restrict__ y2,
+                                                              const float* __restrict__ sc,
+                                                              const float* __restrict__ sh, int relu,
+                                                              float* __restrict__ pooled, bf16_t* __restrict__ pooled16,
+                                                              float* __restrict__ wsum) {
+  const int lane = threadIdx.x & 63, b = blockIdx.y, N = P * P;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int pi = n / P, pj = n - pi * P;
+  const int hs = win_lo(pi, H, P), he = win_hi(pi, H, P);
+  const int ws = win_lo(pj, W, P), we = win_hi(pj, W, P);
+  const int ww = we - ws, npx = (he - hs) * ww;
+  const float inv = 1.f / (float)npx;
+  const int cpp = C >> 3, cw = cpp < 64 ? cpp : 64, plw = 64 / cw;
+  const int pl = lane / cw, kl = lane - pl * cw;
+  const size_t orow = (size_t)b * N + n;
+  for (int cb = 0; cb < cpp; cb += cw) {
+    const int c0 = (cb + kl) * 8;
+    float a[8], bb[8], acc[8], accr[WS ? 8 : 1], accy[WS ? 8 : 1];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      a[q] = sc[c0 + q]; bb[q] = sh[c0 + q]; acc[q] = 0.f;
+      if constexpr (WS) { accr[q] = 0.f; accy[q] = 0.f; }
+    }
+    for (int i = pl; i < npx; i += plw) {
+      const int h = hs + i / ww, w = ws + i % ww;
+      float v[8];
+      load8<T>(y2 + ((size_t)(b * H + h) * W + w) * C + c0, v);
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const float t = v[q] * a[q] + bb[q];
+        acc[q] += relu ? fmaxf(t, 0.f) : t;
+        if constexpr (WS) {
+          const float r = (!relu || t > 0.f) ? 1.f : 0.f;
+          accr[q] += r;
+          accy[q] += r * v[q];
+        }
+      }
+    }
+    for (int off = cw; off < 64; off <<= 1) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        acc[q] += __shfl_xor(acc[q], off, 64);
+        if constexpr (WS) {
+          accr[q] += __shfl_xor(accr[q], off, 64);
+          accy[q] += __shfl_xor(accy[q], off, 64);
+        }
+      }
+    }
+    if (pl == 0) {
+      float m[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) m[q] = acc[q] * inv;
+      float* po = pooled + orow * C + c0;
+      *(float4*)po = make_float4(m[0], m[1], m[2], m[3]);
+      *(float4*)(po + 4) = make_float4(m[4], m[5], m[6], m[7]);
+      if (pooled16)
+        *(uint4*)(pooled16 + orow * C + c0) =
+            make_uint4(pack2bf(m[0], m[1]), pack2bf(m[2], m[3]), pack2bf(m[4], m[5]), pack2bf(m[6], m[7]));
+      if constexpr (WS) {
+        float* wr = wsum + orow * 2 * C + c0;
+        *(float4*)wr = make_float4(accr[0], accr[1], accr[2], accr[3]);
+        *(float4*)(wr + 4) = make_float4(accr[4], accr[5], accr[6], accr[7]);
+        *(float4*)(wr + C) = make_float4(accy[0], accy[1], accy[2], accy[3]);
+        *(float4*)(wr + C + 4) = make_float4(accy[4], accy[5], accy[6], accy[7]);
+      }
+    }
   }
 }
 
@@ -758,6 +838,37 @@ extern "C" int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const vo
       hipLaunchKernelGGL((lsa_pool_kernel<float, false>), grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2,
                          P, S, wpb, relu, partial, wpart);
   }
+  DFCSA_CHECK_LAUNCH();
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_pool_direct_ok(int C, int P) {
+  const int cpp = C / 8;
+  return (g_lsa_pool_direct && P >= 16 && C % 8 == 0 && C <= 2048 && cpp > 0 &&
+          ((cpp & (cpp - 1)) == 0 || cpp % 64 == 0)) ? 1 : 0;
+}
+
+extern "C" int dfcsa_lsa_pool_direct(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                                     const float* sh2, int P, int relu, float* pooled, void* pooled16, float* wsum,
+                                     void* stream) {
+  if (!dfcsa_lsa_pool_direct_ok(C, P) || B <= 0 || H <= 0 || W <= 0 || !y2 || !sc2 || !sh2 || !pooled ||
+      ((uintptr_t)pooled & 15) || ((uintptr_t)pooled16 & 15) || ((uintptr_t)wsum & 15))
+    return DFCSA_EINVAL;
+  if (pooled16 && dtype != DFCSA_DT_BF16 && dtype != DFCSA_DT_F32) return DFCSA_EINVAL;
+  dim3 grid((P * P + 3) / 4, B);
+  hipStream_t st = (hipStream_t)stream;
+  bf16_t* p16 = (bf16_t*)pooled16;
+#define DFCSA_POOL_DIRECT(TT, WSV)                                                                              \
+  hipLaunchKernelGGL((lsa_pool_direct_kernel<TT, WSV>), grid, dim3(256), 0, st, H, W, C, P, (const TT*)y2, sc2, \
+                     sh2, relu, pooled, p16, wsum)
+  if (dtype == DFCSA_DT_BF16) {
+    if (wsum) DFCSA_POOL_DIRECT(bf16_t, true);
+    else DFCSA_POOL_DIRECT(bf16_t, false);
+  } else {
+    if (wsum) DFCSA_POOL_DIRECT(float, true);
+    else DFCSA_POOL_DIRECT(float, false);
+  }
+#undef DFCSA_POOL_DIRECT
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -717,20 +717,28 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     N = Pp * Pp
     Cq = lsa.query_conv.out_channels
     J = 2 * Cq + C
-    S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
-    part = torch.empty(B * N * S * C, device=dev, dtype=f32)
     fm = _flash_mode(dtype, C, Cq, J, N)
     f16 = fm is not None and fm[1]
     # the window sums feed the projection backward's extra rows (B*N <= 4096, fp32 projections), the
     # pool-rows kernel (bf16 flash layers, dfcsa_lsa_pool_rows) or the pool-fused finalize
     # (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
     ws = window_sums and _lsa_gemm_ok(C, J) and (f16 or N <= 256 or B * N <= 4096)
-    wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
     wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
-    call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part), P(wpart),
-         stream())
-    bqkv = pk["bqkv"]
     pooled = torch.empty((B, N, C), device=dev, dtype=f32)
+    pooled16 = torch.empty((B, N, C), device=dev, dtype=torch.bfloat16) if f16 else None
+    # large pools on the projection-GEMM path: one wave per window, pooled (+ its bf16 copy, + the window
+    # sums) written by the pool launch itself (dfcsa_lsa_pool_direct)
+    direct = _lsa_gemm_ok(C, J) and _lib.LIB.dfcsa_lsa_pool_direct_ok(C, Pp) == 1
+    if direct:
+        call("dfcsa_lsa_pool_direct", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(pooled),
+             P(pooled16), P(wsum), stream())
+    else:
+        S = ops._lib.LIB.dfcsa_lsa_pool_splits(H, Pp)
+        part = torch.empty(B * N * S * C, device=dev, dtype=f32)
+        wpart = torch.empty(B * N * S * 2 * C, device=dev, dtype=f32) if ws else None
+        call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(part),
+             P(wpart), stream())
+    bqkv = pk["bqkv"]
     o = torch.empty((B, N, C), device=dev, dtype=f32)
     Wqkv = None
     if f16:
@@ -738,9 +746,9 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
         # convs under bf16 autocast) whose output feeds the bf16 flash kernels directly; the backward
         # recomputes P from the row log-sum-exp (nothing N x N is stored)
         bf = torch.bfloat16
-        call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
-        pooled16 = torch.empty((B, N, C), device=dev, dtype=bf)
-        call("dfcsa_cast_f32", _lib.DT_BF16, ctypes.c_int64(B * N * C), P(pooled), P(pooled16), 0, stream())
+        if not direct:
+            call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
+            call("dfcsa_cast_f32", _lib.DT_BF16, ctypes.c_int64(B * N * C), P(pooled), P(pooled16), 0, stream())
         qkv16 = torch.empty((B, N, J), device=dev, dtype=bf)
         ops.conv_gemm(bf, [(pooled16, 0, 0)], C, (1, B * N, 1), (B * N, 1), pk["Wp16"], rup(C, ops.KALIGN), J,
                       [qkv16], J, bias=bqkv)
@@ -752,7 +760,8 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
         qkv = torch.empty((B, N, J), device=dev, dtype=f32)
         if _lsa_gemm_ok(C, J):
             # projections on the MFMA implicit GEMM (fp32 operands, f32 MFMA): [B*N, C] x [C, J]
-            call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
+            if not direct:
+                call("dfcsa_lsa_pooled_ws", B, H, W, C, Pp, P(part), P(pooled), P(wpart), P(wsum), stream())
             ops.conv_gemm(f32, [(pooled, 0, 0)], C, (1, B * N, 1), (B * N, 1), pk["Wp"], rup(C, ops.KALIGN), J, [qkv],
                           J, bias=bqkv)
         else:

@@ -463,6 +463,14 @@ int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const void* y2, con
                       const float* sh2, int P, int relu, float* partial, float* wpart, void* stream);
 int dfcsa_lsa_pooled_ws(int B, int H, int W, int C, int P, const float* partial, float* pooled,
                         const float* wpart, float* wsum, void* stream);
+/* Large pools (P >= 16, C / 8 a power of two or a multiple of 64: dfcsa_lsa_pool_direct_ok): the pool in
+ * ONE launch, one wave per window -- pooled [B][N][C] fp32 = window mean of act(y2*sc2+sh2); pooled16
+ * (optional, bf16 [B][N][C]) the same values rounded; wsum (optional, [B][N][2][C]) the window sums of
+ * dfcsa_lsa_pooled_ws.  Replaces dfcsa_lsa_pool_ws + dfcsa_lsa_pooled_ws (+ the bf16 cast) there. */
+int dfcsa_lsa_pool_direct_ok(int C, int P);
+int dfcsa_lsa_pool_direct(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
+                          const float* sh2, int P, int relu, float* pooled, void* pooled16, float* wsum,
+                          void* stream);
 /* pooled = partial sums / window area; qkv = pooled @ wT + b  (wT: [C][2Cq+C] fp32) */
 int dfcsa_lsa_qkv(int B, int H, int W, int C, int Cq, int P, const float* partial, const float* wT,
                   const float* bias, float* pooled, float* qkv, void* stream);
@@ -895,6 +903,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 44: 1 = single-buffer KP = 256 fused gate dgrad kernels (two workgroups per CU).
  * knob 45: 1 = several LightSelfAttention pool windows per workgroup at P >= 16 (default 0: measured slower).
  * knob 46: 0 = LightSelfAttention pool windows of <= 8 rows split into row slices too (default 1: one slice).
+ * knob 47: 0 = large pools (P >= 16) on the sliced pool + pooled launches (default 1: dfcsa_lsa_pool_direct).
  * knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (default 1: dQ = sum_k dS (K_k - mean key)).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);

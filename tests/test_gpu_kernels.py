@@ -1071,6 +1071,45 @@ def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
     assert abs(g1.item() - g2.item()) <= 1e-5 * max(1.0, abs(g2.item()))
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("B,H,W,C,P,relu", [(2, 224, 224, 64, 32, 1), (2, 112, 112, 128, 16, 1), (3, 28, 28, 512, 32, 1),
+                                            (2, 14, 14, 1024, 32, 0), (2, 30, 17, 256, 16, 1), (1, 9, 13, 16, 16, 1),
+                                            (2, 56, 56, 8, 16, 0)])
+def test_lsa_pool_direct_matches_sliced_pool(B, H, W, C, P, relu, dtype):
+    """dfcsa_lsa_pool_direct (one wave per window, P >= 16) against the sliced pool + pooled launches
+    (dfcsa_lsa_pool_ws + dfcsa_lsa_pooled_ws) and an fp64 adaptive average pool: the window means,
+    their bf16 copy, and the window sums (sum r exactly: a pixel count)."""
+    from dfcsa._lib import LIB, call
+    from dfcsa.ops import P as ptr, dt, stream
+    assert LIB.dfcsa_lsa_pool_direct_ok(C, P) == 1
+    torch.manual_seed(B + H + C + P)
+    y = torch.randn(B, H, W, C, device="cuda").to(dtype)
+    sc = torch.rand(C, device="cuda") + 0.5
+    sh = torch.randn(C, device="cuda") * 0.3
+    N = P * P
+    pooled = torch.full((B, N, C), float("nan"), device="cuda")
+    p16 = torch.empty((B, N, C), device="cuda", dtype=torch.bfloat16)
+    wsum = torch.full((B, N, 2, C), float("nan"), device="cuda")
+    call("dfcsa_lsa_pool_direct", dt(dtype), B, H, W, C, ptr(y), ptr(sc), ptr(sh), P, relu, ptr(pooled), ptr(p16),
+         ptr(wsum), stream())
+    S = LIB.dfcsa_lsa_pool_splits(H, P)
+    part = torch.empty(B * N * S * C, device="cuda")
+    wpart = torch.empty(B * N * S * 2 * C, device="cuda")
+    pooled2 = torch.empty((B, N, C), device="cuda")
+    wsum2 = torch.empty((B, N, 2, C), device="cuda")
+    call("dfcsa_lsa_pool_ws", dt(dtype), B, H, W, C, ptr(y), ptr(sc), ptr(sh), P, relu, ptr(part), ptr(wpart), stream())
+    call("dfcsa_lsa_pooled_ws", B, H, W, C, P, ptr(part), ptr(pooled2), ptr(wpart), ptr(wsum2), stream())
+    torch.cuda.synchronize()
+    t = y.double() * sc.double() + sh.double()
+    a = t.clamp_min(0) if relu else t
+    ref = F.adaptive_avg_pool2d(a.permute(0, 3, 1, 2).cpu(), (P, P)).permute(0, 2, 3, 1).reshape(B, N, C)
+    assert rel(pooled.cpu(), ref) < 1e-6
+    assert rel(pooled, pooled2) < 1e-6
+    assert torch.equal(p16, pooled.bfloat16())
+    assert torch.equal(wsum[:, :, 0], wsum2[:, :, 0])
+    assert rel(wsum[:, :, 1], wsum2[:, :, 1]) < 1e-6
+
+
 def _bilinear_matrix(out, inp):
     """[out][inp] weights of F.interpolate(bilinear, align_corners=False) along one axis."""
     eye = torch.eye(inp, dtype=torch.float64).view(inp, 1, inp, 1)
