@@ -719,11 +719,13 @@ fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
 //   S^T = K Q^T, dPy'^T = V dy^T - r_q (the MFMA chain starts from -r_q), dS^T / gamma = P^T dPy'^T,
 //   dQ^T[d][q] += K^T[d][k] (dS / gamma)^T[k][q], scaled by gamma at the end.  Keys past N are
 //   masked on the last tile only (tile-uniform branch).
-// kbar != nullptr ([B][CQ] fp32, the image's mean key): dQ = sum_k dS16 (K_k - kbar).  Exact dS rows
+// kbar != nullptr ([B][kKeySlices][CQ] fp32: partial key sums, the image's mean key is their sum / N):
+//   dQ = sum_k dS16 (K_k - mean key).  Exact dS rows
 //   sum to zero (softmax), so subtracting any fixed key changes nothing -- but the bf16-ROUNDED dS16 rows
 //   do not, and their rounding residue times the mean key is a coherent error that dominates dQ (and
 //   the query bias gradient, sum over queries) when the keys are alike, as pooled features are.  The
 //   row sums come from one more MFMA against a ones fragment, so the subtraction is exact in fp32.
+constexpr int kKeySlices = 8;   // key-sum partials per image (lsa_flash_prep_kernel)
 template <int CQ, int C, int WPE>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
@@ -848,8 +850,15 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
       if (d < CQ) {
-        if (kbar) {
-          const float4 kb = *(const float4*)(kbar + (size_t)b * CQ + d);
+        if (kbar) {   // kbar: kKeySlices partial key sums per image, [B][kKeySlices][CQ]
+          float4 kb = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int ks = 0; ks < kKeySlices; ++ks) {
+            const float4 v = *(const float4*)(kbar + ((size_t)b * kKeySlices + ks) * CQ + d);
+            kb.x += v.x; kb.y += v.y; kb.z += v.z; kb.w += v.w;
+          }
+          const float invn = 1.f / (float)N;
+          kb.x *= invn; kb.y *= invn; kb.z *= invn; kb.w *= invn;
           const float rs = rsum[qb][0];
           dqa[qb][db][0] -= rs * kb.x; dqa[qb][db][1] -= rs * kb.y;
           dqa[qb][db][2] -= rs * kb.z; dqa[qb][db][3] -= rs * kb.w;
@@ -1135,9 +1144,37 @@ bool lsa_mfma_ok(int C, int Cq, int ldq) {
 // P = 8 layers (cos 0.44 against float64 on down1's query weight gradient with fp32 r).  Block 0
 // writes one[0] = 1 (the gamma the flash kernels read).
 // nch > 1 (value-chunked backward): r holds one share per 128-column chunk, r[ch * rows + row]
+// kpart != nullptr: the workgroups past the row blocks (B * kKeySlices of them) also form the key sums
+// the centred dQ needs, kpart[b][s][c] = sum of the bf16 key column c over tokens [s N/8, (s+1) N/8) of
+// image b (fixed order: thread (row lane, c) strided sums, then the row lanes in order)
 __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, int nch, const float* __restrict__ dO,
                                                              const float* __restrict__ o, float* __restrict__ r,
-                                                             bf16_t* __restrict__ dO16, float* __restrict__ one) {
+                                                             bf16_t* __restrict__ dO16, float* __restrict__ one,
+                                                             int N, int Cq, int ldq, const bf16_t* __restrict__ qkv,
+                                                             float* __restrict__ kpart) {
+  const int rblocks = (rows + 3) / 4;
+  if ((int)blockIdx.x >= rblocks) {
+    __shared__ float red[256];
+    const int kb = blockIdx.x - rblocks, b = kb / kKeySlices, sl = kb - b * kKeySlices;
+    const int t0 = (int)(((int64_t)sl * N) / kKeySlices), t1 = (int)(((int64_t)(sl + 1) * N) / kKeySlices);
+    const int c = threadIdx.x % Cq, rl = threadIdx.x / Cq, nrl = 256 / Cq;   // Cq divides 256 (host-checked)
+    const bf16_t* k = qkv + (size_t)b * N * ldq + Cq + c;
+    float a0 = 0.f, a1 = 0.f;
+    int t = t0 + rl;
+    for (; t + nrl < t1; t += 2 * nrl) {
+      a0 += bf2f(k[(size_t)t * ldq]);
+      a1 += bf2f(k[(size_t)(t + nrl) * ldq]);
+    }
+    if (t < t1) a0 += bf2f(k[(size_t)t * ldq]);
+    red[threadIdx.x] = a0 + a1;
+    __syncthreads();
+    if ((int)threadIdx.x < Cq) {
+      float v = 0.f;
+      for (int i = 0; i < nrl; ++i) v += red[i * Cq + threadIdx.x];
+      kpart[((size_t)b * kKeySlices + sl) * Cq + threadIdx.x] = v;
+    }
+    return;
+  }
   const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (blockIdx.x == 0 && threadIdx.x == 0) *one = 1.f;
   if (row >= rows) return;
@@ -1179,34 +1216,6 @@ __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, in
   if (lane == 0) r[row] = s;
 }
 
-// kbar[b][c] = mean over the image's N keys of the bf16 key column c (fp32, fixed order): the centre
-// fra_bwd_dq_mfma subtracts.  grid (B, ceil(Cq / cw)), cw = min(Cq, 64) columns x 256 / cw key slices.
-__global__ void __launch_bounds__(256) lsa_key_mean_kernel(int N, int Cq, int ldq, const bf16_t* __restrict__ qkv,
-                                                           float* __restrict__ kbar) {
-  __shared__ float red[256];
-  const int b = blockIdx.x, cw = Cq < 64 ? Cq : 64, nsl = 256 / cw;
-  const int sl = threadIdx.x / cw, c = blockIdx.y * cw + threadIdx.x % cw;
-  float s = 0.f;
-  if (c < Cq) {
-    const bf16_t* k = qkv + (size_t)b * N * ldq + Cq + c;
-    float a[4] = {0.f, 0.f, 0.f, 0.f};
-    int n = sl;
-    for (; n + 3 * nsl < N; n += 4 * nsl) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) a[u] += bf2f(k[(size_t)(n + u * nsl) * ldq]);
-    }
-    for (; n < N; n += nsl) a[0] += bf2f(k[(size_t)n * ldq]);
-    s = (a[0] + a[1]) + (a[2] + a[3]);
-  }
-  red[threadIdx.x] = s;
-  __syncthreads();
-  if (threadIdx.x < cw && c < Cq) {
-    float t = 0.f;
-    for (int i = 0; i < nsl; ++i) t += red[i * cw + threadIdx.x];
-    kbar[(size_t)b * Cq + c] = t / (float)N;
-  }
-}
-
 // dst (fp32) = src (bf16), 8 elements per thread (dfcsa_bf16_to_f32)
 __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const bf16_t* __restrict__ src,
                                                               float* __restrict__ dst) {
@@ -1222,7 +1231,7 @@ __global__ void __launch_bounds__(256) lsa_flash_widen_kernel(int64_t n8, const 
   *(float4*)(dst + 8 * e + 4) = hi;
 }
 
-// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | kbar [B][Cq] | wide partials
+// work layout: one (1 float) | r [B*N] | bf16 mode: dO16 [B*N][C] | key sums [B][kKeySlices][Cq] | wide partials
 struct LsaWork {
   size_t one, r, dO16, kbar, part, total;
 };
@@ -1238,7 +1247,7 @@ LsaWork lsa_work(int dtype, int B, int N, int C, int Cq, int ldq) {
     w.dO16 = e;
     e += lsa_al(rows * C * 2);
     w.kbar = e;
-    e += lsa_al((size_t)B * Cq * sizeof(float));
+    e += lsa_al((size_t)B * kKeySlices * Cq * sizeof(float));
     if (wide) {
       w.part = e;
       e += lsa_al((size_t)2 * nch * rows * Cq * sizeof(float));
@@ -1302,8 +1311,10 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
   const bool bf = dtype == DFCSA_DT_BF16;
   bf16_t* dO16 = bf ? (bf16_t*)(wb + w.dO16) : nullptr;
   const int nch = (bf && !mfma_bwd_ok(dtype, C, Cq, ldq)) ? C / kWideChunk : 1;
-  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3((rows + 3) / 4), dim3(256), 0, st, rows, C, nch, dO, o, r, dO16,
-                     one);
+  // the key sums of the centred dQ (bf16, knob 48; knob 0 leaves dQ uncentred) ride on the prep launch
+  float* kb = (bf && g_lsa_key_centre && 256 % Cq == 0) ? (float*)(wb + w.kbar) : nullptr;
+  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3((rows + 3) / 4 + (kb ? B * kKeySlices : 0)), dim3(256), 0, st, rows,
+                     C, nch, dO, o, r, dO16, one, N, Cq, ldq, (const bf16_t*)qkv, kb);
   DFCSA_CHECK_LAUNCH();
   if (!bf) {
     dim3 grid((N + 3) / 4, B);
@@ -1316,13 +1327,6 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
     return 0;
   }
   bf16_t* dq16 = (bf16_t*)dqkv;
-  float* kb = nullptr;   // the mean key (dQ centring, fra_bwd_dq_mfma); knob 48 = 0 leaves dQ uncentred
-  if (g_lsa_key_centre) {
-    kb = (float*)(wb + w.kbar);
-    const int cw = Cq < 64 ? Cq : 64;
-    hipLaunchKernelGGL(lsa_key_mean_kernel, dim3(B, (Cq + cw - 1) / cw), dim3(256), 0, st, N, Cq, ldq,
-                       (const bf16_t*)qkv, kb);
-  }
   if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
     switch (Cq) {
       case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;

@@ -178,7 +178,7 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
 // partial slices, no block barrier, no separate dfcsa_lsa_pooled_ws launch (which at P = 32 was one
 // ~34 us launch of 16 k single-token workgroups per layer).  Lanes: cw = min(C / 8, 64) channel chunks
 // x 64 / cw pixel lanes (C / 8 a power of two or a multiple of 64, host-checked); the pixel lanes are
-// combined by xor shuffles.  Writes pooled [B][N][C] = window mean (fp32), optional pooled16 (bf16
+// combined by xor shuffles.  Writes pooled [B][N][C] = window mean (fp32, optional), pooled16 (bf16
 // copy, the projection GEMM's operand) and optional wsum [B][N][2][C] (sum r, sum r*y; see
 // lsa_pool_kernel).
 template <typename T, bool WS>
@@ -235,9 +235,11 @@ __global__ void __launch_bounds__(256) lsa_pool_direct_kernel(int H, int W, int 
       float m[8];
 #pragma unroll
       for (int q = 0; q < 8; ++q) m[q] = acc[q] * inv;
-      float* po = pooled + orow * C + c0;
-      *(float4*)po = make_float4(m[0], m[1], m[2], m[3]);
-      *(float4*)(po + 4) = make_float4(m[4], m[5], m[6], m[7]);
+      if (pooled) {
+        float* po = pooled + orow * C + c0;
+        *(float4*)po = make_float4(m[0], m[1], m[2], m[3]);
+        *(float4*)(po + 4) = make_float4(m[4], m[5], m[6], m[7]);
+      }
       if (pooled16)
         *(uint4*)(pooled16 + orow * C + c0) =
             make_uint4(pack2bf(m[0], m[1]), pack2bf(m[2], m[3]), pack2bf(m[4], m[5]), pack2bf(m[6], m[7]));
@@ -851,7 +853,7 @@ extern "C" int dfcsa_lsa_pool_direct_ok(int C, int P) {
 extern "C" int dfcsa_lsa_pool_direct(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
                                      const float* sh2, int P, int relu, float* pooled, void* pooled16, float* wsum,
                                      void* stream) {
-  if (!dfcsa_lsa_pool_direct_ok(C, P) || B <= 0 || H <= 0 || W <= 0 || !y2 || !sc2 || !sh2 || !pooled ||
+  if (!dfcsa_lsa_pool_direct_ok(C, P) || B <= 0 || H <= 0 || W <= 0 || !y2 || !sc2 || !sh2 || (!pooled && !pooled16) ||
       ((uintptr_t)pooled & 15) || ((uintptr_t)pooled16 & 15) || ((uintptr_t)wsum & 15))
     return DFCSA_EINVAL;
   if (pooled16 && dtype != DFCSA_DT_BF16 && dtype != DFCSA_DT_F32) return DFCSA_EINVAL;

@@ -724,11 +724,12 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     # (dfcsa_bn_bwd_finalize_pool: N <= 256); otherwise the entry pass computes them
     ws = window_sums and _lsa_gemm_ok(C, J) and (f16 or N <= 256 or B * N <= 4096)
     wsum = torch.empty((B, N, 2, C), device=dev, dtype=f32) if ws else None
-    pooled = torch.empty((B, N, C), device=dev, dtype=f32)
     pooled16 = torch.empty((B, N, C), device=dev, dtype=torch.bfloat16) if f16 else None
     # large pools on the projection-GEMM path: one wave per window, pooled (+ its bf16 copy, + the window
-    # sums) written by the pool launch itself (dfcsa_lsa_pool_direct)
+    # sums) written by the pool launch itself (dfcsa_lsa_pool_direct); the bf16 flash layers keep only
+    # the bf16 copy (their backward reads pooled16)
     direct = _lsa_gemm_ok(C, J) and _lib.LIB.dfcsa_lsa_pool_direct_ok(C, Pp) == 1
+    pooled = None if (direct and f16) else torch.empty((B, N, C), device=dev, dtype=f32)
     if direct:
         call("dfcsa_lsa_pool_direct", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(pooled),
              P(pooled16), P(wsum), stream())
