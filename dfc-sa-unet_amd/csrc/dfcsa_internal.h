@@ -109,7 +109,8 @@ extern int g_wgrad_coop;   // knob 31: cooperative in-launch split-K reduction (
 extern int g_small8;
 extern int g_lsa_rows_old;  // knob 28: 1 = the item-owner LightSelfAttention upsample-backward row kernel
 extern int g_lsa_pool_direct;  // knob 47: one wave per window for P >= 16 (dfcsa_lsa_pool_direct, default 1)
-extern int g_lsa_key_centre;  // knob 48: mean-key centred dQ in the bf16 pooled-attention backward (default 1)
+extern int g_lsa_key_centre;
+extern int g_lsa_cols_flash;   // knob 49: fused column pass + prep for the bf16 flash layers (default 1)  // knob 48: mean-key centred dQ in the bf16 pooled-attention backward (default 1)
 extern int g_lsa_pool_one_slice;  // knob 46: small pool windows in one row slice (default 1)
 extern int g_lsa_pool_wpb;  // knob 45: several pool windows per workgroup at P >= 16 (off)
 extern int g_lsa_cols_nt;  // knob 35: 256 = the 256-thread LightSelfAttention upsample-backward column kernel
@@ -125,3 +126,10 @@ extern int g_ew_tile_elems;
 // DFCSA_SHAPELOG=1: one stderr line per conv / wgrad launch (shape analysis against a kernel
 // trace, tools/shape_trace.py); off by default
 bool dfcsa_shapelog();
+
+// bf16 pooled-attention backward pieces shared by fra.hip and lsa.hip (dfcsa_lsa_flash_bwd_up): the
+// work pointers plus the one / key-sum launch, and the MFMA kernels after the prep step
+int lsa_flash_prepare_ext(int B, int N, int C, int Cq, int ldq, const void* qkv, void* work, int64_t work_bytes,
+                          bf16_t** dO16, float** r, int* nch, const float** kb, hipStream_t st);
+void lsa_flash_bwd_core(int B, int N, int C, int Cq, int ldq, const void* qkv, const float* lse, void* dqkv, void* work,
+                        const float* kb, hipStream_t st);

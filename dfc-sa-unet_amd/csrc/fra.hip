@@ -1153,6 +1153,7 @@ __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, in
                                                              int N, int Cq, int ldq, const bf16_t* __restrict__ qkv,
                                                              float* __restrict__ kpart) {
   const int rblocks = (rows + 3) / 4;
+  if (blockIdx.x == 0 && threadIdx.x == 0) *one = 1.f;
   if ((int)blockIdx.x >= rblocks) {
     __shared__ float red[256];
     const int kb = blockIdx.x - rblocks, b = kb / kKeySlices, sl = kb - b * kKeySlices;
@@ -1176,7 +1177,6 @@ __global__ void __launch_bounds__(256) lsa_flash_prep_kernel(int rows, int C, in
     return;
   }
   const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (blockIdx.x == 0 && threadIdx.x == 0) *one = 1.f;
   if (row >= rows) return;
   const float* a = dO + (size_t)row * C;
   const float* v = o + (size_t)row * C;
@@ -1290,6 +1290,62 @@ extern "C" int dfcsa_lsa_flash_fwd(int dtype, int B, int N, int C, int Cq, int l
   return 0;
 }
 
+// The bf16 flash backward's kernels after the prep step (dO16, r and one already in `work`; kb: the key
+// sums of the centred dQ, or nullptr): dfcsa_lsa_flash_bwd and the fused column pass of lsa.hip
+// (dfcsa_lsa_flash_bwd_up) share it.
+void lsa_flash_bwd_core(int B, int N, int C, int Cq, int ldq, const void* qkv, const float* lse, void* dqkv, void* work,
+                        const float* kb, hipStream_t st) {
+  const int dtype = DFCSA_DT_BF16;
+  const LsaWork w = lsa_work(dtype, B, N, C, Cq, ldq);
+  char* wb = (char*)work;
+  const float* one = (const float*)(wb + w.one);
+  const float* r = (const float*)(wb + w.r);
+  const bf16_t* dO16 = (const bf16_t*)(wb + w.dO16);
+  const int rows = B * N;
+  bf16_t* dq16 = (bf16_t*)dqkv;
+  if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
+    switch (Cq) {
+      case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
+      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, nullptr, st, 0, kb); break;
+    }
+  } else {
+    float* part = (float*)(wb + w.part);
+    switch (Cq) {
+      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
+    }
+    const int64_t threads = 2 * (int64_t)rows * (Cq / 4);
+    hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (int64_t)rows, Cq,
+                       C / kWideChunk, ldq, part, one, dq16);
+  }
+}
+
+
+// work pointers of the bf16 flash backward for a caller that forms dO16 / r itself (r: nch shares of
+// 128 value columns on wide layers, else 1) and the key-sum / one launch; 0 or DFCSA_EINVAL
+int lsa_flash_prepare_ext(int B, int N, int C, int Cq, int ldq, const void* qkv, void* work, int64_t work_bytes,
+                          bf16_t** dO16, float** r, int* nch, const float** kb, hipStream_t st) {
+  const int dtype = DFCSA_DT_BF16;
+  if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !qkv || !work) return DFCSA_EINVAL;
+  const LsaWork w = lsa_work(dtype, B, N, C, Cq, ldq);
+  if (work_bytes < (int64_t)w.total || ((uintptr_t)work & 15)) return DFCSA_EINVAL;
+  char* wb = (char*)work;
+  *dO16 = (bf16_t*)(wb + w.dO16);
+  *r = (float*)(wb + w.r);
+  *nch = mfma_bwd_ok(dtype, C, Cq, ldq) ? 1 : C / kWideChunk;
+  float* k = (g_lsa_key_centre && 256 % Cq == 0) ? (float*)(wb + w.kbar) : nullptr;
+  *kb = k;
+  // one = 1 (the gamma the kernels read) and the key sums: the prep kernel with no dO rows
+  hipLaunchKernelGGL(lsa_flash_prep_kernel, dim3(k ? B * kKeySlices : 1), dim3(256), 0, st, 0, C, *nch, nullptr,
+                     nullptr, nullptr, nullptr, (float*)(wb + w.one), N, Cq, ldq, (const bf16_t*)qkv, k);
+  return 0;
+}
+
 extern "C" int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq, int ldq, int64_t* bytes) {
   if (!lsa_shape_ok(dtype, B, N, C, Cq, ldq) || !bytes) return DFCSA_EINVAL;
   *bytes = (int64_t)lsa_work(dtype, B, N, C, Cq, ldq).total;
@@ -1326,27 +1382,7 @@ extern "C" int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int l
     DFCSA_CHECK_LAUNCH();
     return 0;
   }
-  bf16_t* dq16 = (bf16_t*)dqkv;
-  if (mfma_bwd_ok(dtype, C, Cq, ldq)) {
-    switch (Cq) {
-      case 8: launch_bwd_cq<8>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
-      case 16: launch_bwd_cq<16>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
-      case 32: launch_bwd_cq<32>(B, N, C, ldq, qkv, dO16, one, lse, r, dq16, st, kb); break;
-      default: launch_bwd<64, 64>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, nullptr, st, 0, kb); break;
-    }
-  } else {
-    float* part = (float*)(wb + w.part);
-    switch (Cq) {
-      case 8: launch_bwd<8, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
-      case 16: launch_bwd<16, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
-      case 32: launch_bwd<32, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
-      case 64: launch_bwd<64, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
-      default: launch_bwd<128, kWideChunk>(B, N, ldq, C, qkv, dO16, one, lse, r, dq16, part, st, rows, kb); break;
-    }
-    const int64_t threads = 2 * (int64_t)rows * (Cq / 4);
-    hipLaunchKernelGGL(fra_wide_finish, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, (int64_t)rows, Cq,
-                       C / kWideChunk, ldq, part, one, dq16);
-  }
+  lsa_flash_bwd_core(B, N, C, Cq, ldq, qkv, lse, dqkv, work, kb, st);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -19,8 +19,9 @@
 int g_lsa_rows_old = 0;
 int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
 int g_lsa_pool_wpb = 0;     // knob 45: 1 = several pool windows per workgroup at P >= 16 (measured slower: off)
-int g_lsa_key_centre = 1;
-int g_lsa_pool_direct = 1;   // knob 47: 0 = large pools on the sliced pool + pooled launches (old)   // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
+int g_lsa_key_centre = 1;    // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
+int g_lsa_pool_direct = 1;   // knob 47: 0 = large pools on the sliced pool + pooled launches (old)
+int g_lsa_cols_flash = 1;    // knob 49: 0 = the bf16 flash layers' column pass + separate prep (old)
 int g_lsa_pool_one_slice = 1;   // knob 46: 0 = split the <= 8-row windows of P >= 16 pools into row slices (old)
 
 namespace {
@@ -584,6 +585,90 @@ __global__ void __launch_bounds__(NT) lsa_up_bwd_cols_kernel(int H, int C, int P
   if (threadIdx.x == 0) *gamma_grad += (float)rd[0];
 }
 
+// bf16 flash layers (dfcsa_lsa_flash_bwd_up): the upsample-backward column pass fused with the flash
+// backward's prep.  ONE WAVE per token n = (pi, pj) of image b, lanes over channels (64 per step):
+//   du[c] = sum_h wy(pi, h) rows[b][h][pj][c]   (the source rows with a non-zero weight, found once per
+//           wave by a ballot over h = lo + lane; weights fetched by readlane),
+//   dO16 = bf16(gamma du), r = sum_c dO16 * o (per 128-column share when nch > 1, as the prep kernel's),
+//   gpart[b N + n] = sum_c o du (the dgamma partial).
+// The fp32 dO never exists: the separate pass (dfcsa_lsa_up_bwd_cols + the prep kernel) wrote it and
+// read it back with o.  hi - lo <= 64 is host-checked (H <= 29 P).
+__global__ void __launch_bounds__(256) lsa_up_bwd_cols_flash_kernel(int H, int C, int P, int nch,
+                                                                    const float* __restrict__ rows,
+                                                                    const float* __restrict__ o, const float* gamma,
+                                                                    bf16_t* __restrict__ dO16, float* __restrict__ r,
+                                                                    float* __restrict__ gpart) {
+  const int lane = threadIdx.x & 63, b = blockIdx.y, N = P * P;
+  const int n = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (n >= N) return;
+  const int pi = n / P, pj = n - pi * P;
+  int lo, hi;
+  contrib_range(pi, P, H, lo, hi);
+  const float bsc = (float)P / (float)H;
+  float wl = 0.f;
+  {
+    const int h = lo + lane;
+    if (h < hi) {
+      int i0, i1;
+      float l0, l1;
+      bilin_axis_s(h, P, bsc, i0, i1, l0, l1);
+      wl = (i0 == pi ? l0 : 0.f) + (i1 == pi ? l1 : 0.f);
+    }
+  }
+  const unsigned long long hm = __ballot(wl != 0.f);
+  const int wli = __float_as_int(wl);
+  const float gm = *gamma;
+  const int PC = P * C;
+  const float* rb = rows + ((size_t)b * H * P + pj) * C;   // rows[b][h][pj][c] = rb[h * PC + c]
+  const size_t row = (size_t)b * N + n, rows_tot = (size_t)gridDim.y * N;
+  float g = 0.f, rs = 0.f;
+  for (int c0 = 0; c0 < C; c0 += 64) {
+    const int c = c0 + lane;
+    const int cc = c < C ? c : C - 1;
+    float s = 0.f;
+    unsigned long long m = hm;
+    while (m) {   // 4 source rows in flight (the tail repeats the last row at weight 0)
+      int hh[4];
+      float wv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        if (m) {
+          const int j = __builtin_ctzll(m);
+          m &= m - 1;
+          hh[u] = lo + j;
+          wv[u] = __int_as_float(__builtin_amdgcn_readlane(wli, j));
+        } else {
+          hh[u] = hh[0];
+          wv[u] = 0.f;
+        }
+      }
+      float v[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) v[u] = rb[(size_t)hh[u] * PC + cc];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) s += wv[u] * v[u];
+    }
+    if (c < C) {
+      const float ov = o[row * C + c];
+      g += ov * s;
+      const bf16_t d16 = f2bf(gm * s);
+      dO16[row * C + c] = d16;
+      rs += bf2f(d16) * ov;
+    }
+    if (nch > 1 && ((c0 + 64) % 128 == 0 || c0 + 64 >= C)) {   // end of a 128-column share
+      const float t = wave_sum(rs);
+      if (lane == 0) r[(size_t)(c0 / 128) * rows_tot + row] = t;
+      rs = 0.f;
+    }
+  }
+  if (nch <= 1) {
+    const float t = wave_sum(rs);
+    if (lane == 0) r[row] = t;
+  }
+  g = wave_sum(g);
+  if (lane == 0) gpart[row] = g;
+}
+
 // grid (N, B): query row n -> dE[b][n][:], dq[b][n][:]
 __global__ void __launch_bounds__(256) lsa_attn_bwd_rows_kernel(int N, int C, int Cq, const float* __restrict__ qkv,
                                                                 const float* __restrict__ A,
@@ -1108,6 +1193,27 @@ extern "C" int dfcsa_lsa_up_bwd_cols(int B, int H, int C, int P, const float* ro
                        o, gamma, dO, gpart, cnt, gamma_grad);
   DFCSA_CHECK_LAUNCH();
   if (ngpart) *ngpart = B * P * P;
+  return 0;
+}
+
+extern "C" int dfcsa_lsa_flash_bwd_up(int B, int H, int C, int Cq, int P, const float* rows, const float* o,
+                                      const float* gamma, const void* qkv16, const float* lse, void* dqkv16,
+                                      float* gpart, void* work, int64_t work_bytes, void* stream) {
+  const int N = P * P, ldq = 2 * Cq + C;
+  if (!g_lsa_cols_flash || B <= 0 || H <= 0 || P <= 0 || H > 29 * P || !rows || !o || !gamma || !qkv16 || !lse ||
+      !dqkv16 || !gpart)
+    return DFCSA_EINVAL;
+  hipStream_t st = (hipStream_t)stream;
+  bf16_t* dO16 = nullptr;
+  float* r = nullptr;
+  int nch = 1;
+  const float* kb = nullptr;
+  if (lsa_flash_prepare_ext(B, N, C, Cq, ldq, qkv16, work, work_bytes, &dO16, &r, &nch, &kb, st)) return DFCSA_EINVAL;
+  hipLaunchKernelGGL(lsa_up_bwd_cols_flash_kernel, dim3((N + 3) / 4, B), dim3(256), 0, st, H, C, P, nch, rows, o,
+                     gamma, dO16, r, gpart);
+  DFCSA_CHECK_LAUNCH();
+  lsa_flash_bwd_core(B, N, C, Cq, ldq, qkv16, lse, dqkv16, work, kb, st);
+  DFCSA_CHECK_LAUNCH();
   return 0;
 }
 

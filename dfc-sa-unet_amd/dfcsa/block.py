@@ -803,6 +803,25 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
         gpart = torch.empty(B * N, device=dev, dtype=f32)
         call("dfcsa_lsa_core_bwd", B, H, C, Cq, Pp, P(rows), P(o), P(lsa.gamma), P(qkv), P(A), P(dqkv), P(dO), P(dE),
              P(gpart), P(grad_of(lsa.gamma)), stream())
+    elif (isinstance(A, FlashSaved) and A.qkv16 is not None and H <= 29 * Pp
+          and _lib.LIB.dfcsa_get_tuning(49) == 1):
+        # bf16 flash layer: the column pass writes the bf16 dO and r of the flash backward itself (one
+        # wave per token; no fp32 dO, no prep pass), then the MFMA kernels (dfcsa_lsa_flash_bwd_up)
+        gpart = torch.empty(B * N, device=dev, dtype=f32)
+        nb = ctypes.c_int64()
+        call("dfcsa_lsa_flash_bwd_bytes", _lib.DT_BF16, B, N, C, Cq, J, ctypes.byref(nb))
+        work = torch.empty((nb.value + 15) // 16 * 4, device=dev, dtype=f32)
+        dqkv = torch.empty((B, N, J), device=dev, dtype=torch.bfloat16)
+        call("dfcsa_lsa_flash_bwd_up", B, H, C, Cq, Pp, P(rows), P(o), P(lsa.gamma), P(A.qkv16), P(A.lse), P(dqkv),
+             P(gpart), P(work), ctypes.c_int64(work.numel() * 4), stream())
+        del work
+        call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
+        dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
+        if pool_rows is not None:   # the attention entry's pool-backward BatchNorm rows
+            wsum, mean, invstd, rows_ptr, Hh, Ww = pool_rows
+            call("dfcsa_lsa_pool_rows", B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum), P(mean), P(invstd),
+                 rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
+        return dpooled
     else:
         dO = torch.empty((B, N, C), device=dev, dtype=f32)
         if N > 64 and LSA_DGAMMA_SPLIT[0]:

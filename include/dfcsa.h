@@ -498,6 +498,14 @@ int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const v
  * capacity of rows in floats. */
 int dfcsa_lsa_pool_rows(int BN, int C, int P, int H, int W, const float* dpooled, const float* wsum,
                         const float* mean, const float* invstd, float* rows, int64_t rows_floats, void* stream);
+/* bf16 flash layers: dfcsa_lsa_up_bwd_cols (gamma_grad NULL) + dfcsa_lsa_flash_bwd in one call, the
+ * column pass writing the flash backward's bf16 dO and r itself (one wave per token; the fp32 dO is never
+ * formed): rows [B][H][P][C] (dfcsa_lsa_up_bwd_rows), o [B][N][C] fp32, qkv16 / lse / dqkv16 / work as
+ * dfcsa_lsa_flash_bwd (work sized by dfcsa_lsa_flash_bwd_bytes with dtype bf16), gpart [B*N] the
+ * per-token dgamma partials (sum them: dfcsa_sum_to_scalar).  H <= 29 P; knob 49 = 0 refuses. */
+int dfcsa_lsa_flash_bwd_up(int B, int H, int C, int Cq, int P, const float* rows, const float* o,
+                           const float* gamma, const void* qkv16, const float* lse, void* dqkv16,
+                           float* gpart, void* work, int64_t work_bytes, void* stream);
 /* dst[i] = src[i] (bf16 -> fp32), n % 8 == 0, 16-byte aligned pointers */
 int dfcsa_bf16_to_f32(int64_t n, const void* src, float* dst, void* stream);
 /* backward through the bilinear upsample: rows[b][h][pj][c] = sum_w wx(pj,w) dattn[b,h,w,c] */
@@ -905,6 +913,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 46: 0 = LightSelfAttention pool windows of <= 8 rows split into row slices too (default 1: one slice).
  * knob 47: 0 = large pools (P >= 16) on the sliced pool + pooled launches (default 1: dfcsa_lsa_pool_direct).
  * knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (default 1: dQ = sum_k dS (K_k - mean key)).
+ * knob 49: 0 = the bf16 flash layers' column pass + separate prep (default 1: dfcsa_lsa_flash_bwd_up).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

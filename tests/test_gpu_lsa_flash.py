@@ -241,3 +241,45 @@ def test_flash_bwd_centred_dq_on_alike_keys(C, N, B):
     assert errs[1][0] < 3e-2 and errs[1][0] <= errs[0][0]
     assert errs[1][1] == pytest.approx(errs[0][1], rel=1e-6, abs=1e-7)
     assert errs[1][2] == pytest.approx(errs[0][2], rel=1e-6, abs=1e-7)
+
+
+@pytest.mark.parametrize("C,P,H,B", [(64, 16, 224, 2), (128, 32, 112, 2), (512, 32, 28, 2), (1024, 32, 14, 1),
+                                     (256, 8, 56, 3), (64, 8, 224, 1)])
+def test_flash_bwd_up_matches_separate_passes(C, P, H, B):
+    """dfcsa_lsa_flash_bwd_up (column pass writing the bf16 dO / r itself) against dfcsa_lsa_up_bwd_cols +
+    dfcsa_lsa_flash_bwd on the same rows / o / q,k,v: the q/k/v gradients (bf16 outputs: the fp32 du may
+    differ in its last bits between the two summation orders, so a bf16 dO element can round the other
+    way) and the dgamma partials."""
+    import ctypes
+    from dfcsa import _lib
+    from dfcsa.ops import P as ptr, stream
+    L = _lib.LIB
+    N, Cq = P * P, C // 8
+    J = 2 * Cq + C
+    g0 = torch.Generator().manual_seed(C + P + H)
+    rows = torch.randn(B * H * P * C, generator=g0).cuda()
+    o = torch.randn(B, N, C, generator=g0).cuda()
+    gamma = torch.tensor([0.7]).cuda()
+    qkv16 = (torch.randn(B, N, J, generator=g0) * 0.5).bfloat16().cuda()
+    lse = torch.empty(B * N, device="cuda")
+    o2 = torch.empty(B, N, C, device="cuda")
+    assert L.dfcsa_lsa_flash_fwd(_lib.DT_BF16, B, N, C, Cq, J, ptr(qkv16), ptr(o2), ptr(lse), stream()) == 0
+    nb = ctypes.c_int64()
+    assert L.dfcsa_lsa_flash_bwd_bytes(_lib.DT_BF16, B, N, C, Cq, J, ctypes.byref(nb)) == 0
+    work = torch.empty(nb.value, dtype=torch.uint8, device="cuda")
+    d1 = torch.full((B, N, J), float("nan"), device="cuda").bfloat16()
+    gp1 = torch.full((B * N,), float("nan"), device="cuda")
+    assert L.dfcsa_lsa_flash_bwd_up(B, H, C, Cq, P, ptr(rows), ptr(o), ptr(gamma), ptr(qkv16), ptr(lse), ptr(d1),
+                                    ptr(gp1), ptr(work), nb.value, stream()) == 0
+    dO = torch.empty(B, N, C, device="cuda")
+    gp2 = torch.empty(B * N, device="cuda")
+    assert L.dfcsa_lsa_up_bwd_cols(B, H, C, P, ptr(rows), ptr(o), ptr(gamma), ptr(dO), ptr(gp2), None, None,
+                                   stream()) == 0
+    d2 = torch.full((B, N, J), float("nan"), device="cuda").bfloat16()
+    assert L.dfcsa_lsa_flash_bwd(_lib.DT_BF16, B, N, C, Cq, J, ptr(qkv16), ptr(dO), ptr(o), ptr(lse), ptr(d2),
+                                 ptr(work), nb.value, stream()) == 0
+    torch.cuda.synchronize()
+    assert torch.isfinite(d1.float()).all()
+    assert rel(gp1, gp2) < 1e-5
+    for a, b_ in zip(d1.float().split([Cq, Cq, C], -1), d2.float().split([Cq, Cq, C], -1)):
+        assert rel(a, b_) < 5e-3
