@@ -929,16 +929,20 @@ extern "C" int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const vo
   return 0;
 }
 
-extern "C" int dfcsa_lsa_pool_direct_ok(int C, int P) {
+extern "C" int dfcsa_lsa_pool_direct_ok(int C, int P, int H, int W) {
   const int cpp = C / 8;
-  return (g_lsa_pool_direct && P >= 16 && C % 8 == 0 && C <= 2048 && cpp > 0 &&
+  // large pools, or P = 8 windows of at most 8 x 8 pixels (below 224^2): a wave per window has the
+  // whole window in a few loads per lane; larger windows keep the row-sliced launches.  (P = 4's deep
+  // levels measured 0.6 % slower on it, profiles/r06z_ab.txt: P = 4 keeps the sliced launches.)
+  const bool small = P >= 16 || (P >= 8 && (H + P - 1) / P <= 8 && (W + P - 1) / P <= 8);
+  return (g_lsa_pool_direct && small && P > 0 && C % 8 == 0 && C <= 2048 && cpp > 0 &&
           ((cpp & (cpp - 1)) == 0 || cpp % 64 == 0)) ? 1 : 0;
 }
 
 extern "C" int dfcsa_lsa_pool_direct(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
                                      const float* sh2, int P, int relu, float* pooled, void* pooled16, float* wsum,
                                      void* stream) {
-  if (!dfcsa_lsa_pool_direct_ok(C, P) || B <= 0 || H <= 0 || W <= 0 || !y2 || !sc2 || !sh2 || (!pooled && !pooled16) ||
+  if (!dfcsa_lsa_pool_direct_ok(C, P, H, W) || B <= 0 || H <= 0 || W <= 0 || !y2 || !sc2 || !sh2 || (!pooled && !pooled16) ||
       ((uintptr_t)pooled & 15) || ((uintptr_t)pooled16 & 15) || ((uintptr_t)wsum & 15))
     return DFCSA_EINVAL;
   if (pooled16 && dtype != DFCSA_DT_BF16 && dtype != DFCSA_DT_F32) return DFCSA_EINVAL;

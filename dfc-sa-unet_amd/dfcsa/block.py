@@ -728,7 +728,7 @@ def lsa_core_forward(lsa, y, scale, shift, relu, pool_size, dtype, pk, window_su
     # large pools on the projection-GEMM path: one wave per window, pooled (+ its bf16 copy, + the window
     # sums) written by the pool launch itself (dfcsa_lsa_pool_direct); the bf16 flash layers keep only
     # the bf16 copy (their backward reads pooled16)
-    direct = _lsa_gemm_ok(C, J) and _lib.LIB.dfcsa_lsa_pool_direct_ok(C, Pp) == 1
+    direct = _lsa_gemm_ok(C, J) and _lib.LIB.dfcsa_lsa_pool_direct_ok(C, Pp, H, W) == 1
     pooled = None if (direct and f16) else torch.empty((B, N, C), device=dev, dtype=f32)
     if direct:
         call("dfcsa_lsa_pool_direct", dt(dtype), B, H, W, C, P(y), P(scale), P(shift), Pp, int(relu), P(pooled),

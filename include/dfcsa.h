@@ -463,11 +463,12 @@ int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const void* y2, con
                       const float* sh2, int P, int relu, float* partial, float* wpart, void* stream);
 int dfcsa_lsa_pooled_ws(int B, int H, int W, int C, int P, const float* partial, float* pooled,
                         const float* wpart, float* wsum, void* stream);
-/* Large pools (P >= 16, C / 8 a power of two or a multiple of 64: dfcsa_lsa_pool_direct_ok): the pool in
+/* Large pools or small windows (P >= 16, or P >= 8 with windows of <= 8 x 8 pixels; C / 8 a power of two or a multiple
+ * of 64: dfcsa_lsa_pool_direct_ok): the pool in
  * ONE launch, one wave per window -- pooled [B][N][C] fp32 = window mean of act(y2*sc2+sh2); pooled16
  * (bf16 [B][N][C]) the same values rounded (either may be NULL, not both); wsum (optional, [B][N][2][C]) the window sums of
  * dfcsa_lsa_pooled_ws.  Replaces dfcsa_lsa_pool_ws + dfcsa_lsa_pooled_ws (+ the bf16 cast) there. */
-int dfcsa_lsa_pool_direct_ok(int C, int P);
+int dfcsa_lsa_pool_direct_ok(int C, int P, int H, int W);
 int dfcsa_lsa_pool_direct(int dtype, int B, int H, int W, int C, const void* y2, const float* sc2,
                           const float* sh2, int P, int relu, float* pooled, void* pooled16, float* wsum,
                           void* stream);

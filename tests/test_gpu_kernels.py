@@ -1074,14 +1074,15 @@ def test_lsa_core_bwd_fused_matches_three_launches(B, H, C, P):
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("B,H,W,C,P,relu", [(2, 224, 224, 64, 32, 1), (2, 112, 112, 128, 16, 1), (3, 28, 28, 512, 32, 1),
                                             (2, 14, 14, 1024, 32, 0), (2, 30, 17, 256, 16, 1), (1, 9, 13, 16, 16, 1),
-                                            (2, 56, 56, 8, 16, 0)])
+                                            (2, 56, 56, 8, 16, 0), (3, 56, 56, 256, 8, 1), (2, 28, 30, 512, 8, 1),
+                                            (2, 14, 14, 1024, 8, 1)])
 def test_lsa_pool_direct_matches_sliced_pool(B, H, W, C, P, relu, dtype):
-    """dfcsa_lsa_pool_direct (one wave per window, P >= 16) against the sliced pool + pooled launches
+    """dfcsa_lsa_pool_direct (one wave per window: P >= 16, or P = 8 with windows of <= 8 x 8) against the sliced pool + pooled launches
     (dfcsa_lsa_pool_ws + dfcsa_lsa_pooled_ws) and an fp64 adaptive average pool: the window means,
     their bf16 copy, and the window sums (sum r exactly: a pixel count)."""
     from dfcsa._lib import LIB, call
     from dfcsa.ops import P as ptr, dt, stream
-    assert LIB.dfcsa_lsa_pool_direct_ok(C, P) == 1
+    assert LIB.dfcsa_lsa_pool_direct_ok(C, P, H, W) == 1
     torch.manual_seed(B + H + C + P)
     y = torch.randn(B, H, W, C, device="cuda").to(dtype)
     sc = torch.rand(C, device="cuda") + 0.5
