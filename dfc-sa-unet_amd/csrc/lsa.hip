@@ -207,6 +207,7 @@ __global__ void __launch_bounds__(256) lsa_pool_direct_kernel(int H, int W, int 
       a[q] = sc[c0 + q]; bb[q] = sh[c0 + q]; acc[q] = 0.f;
       if constexpr (WS) { accr[q] = 0.f; accy[q] = 0.f; }
     }
+#pragma unroll 4
     for (int i = pl; i < npx; i += plw) {
       const int h = hs + i / ww, w = ws + i % ww;
       float v[8];
@@ -454,29 +455,26 @@ __global__ void __launch_bounds__(256) lsa_up_bwd_rows_kernel(int H, int W, int 
       c0 = (e - pj * cpp) * 8;
       int lo, hi;
       contrib_range(pj, P, W, lo, hi);
-      // 4 source columns per step: independent loads in flight (zero weights load nothing)
+      // 4 source columns per step, loaded unconditionally (columns past the range clamped, weight 0):
+      // a load under a (lane-divergent) zero-weight branch was waited for before the branch joined,
+      // which serialised the four loads (the clamped / zero-weight columns are the row this workgroup
+      // reads anyway: L1 / L2 hits)
       for (int w0 = lo + sl; w0 < hi; w0 += 4 * nsl) {
         float wt[4], v[4][8];
 #pragma unroll
         for (int u = 0; u < 4; ++u) {
           const int w = w0 + u * nsl;
-          wt[u] = 0.f;
-          if (w < hi) {
-            int i0, i1;
-            float l0, l1;
-            bilin_axis_s(w, P, bsc, i0, i1, l0, l1);
-            wt[u] = (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f);
-          }
-          if (wt[u] != 0.f) load8<T>(row + (size_t)w * C + c0, v[u]);
-          else
-#pragma unroll
-            for (int q = 0; q < 8; ++q) v[u][q] = 0.f;
+          const int wc = w < hi ? w : hi - 1;
+          int i0, i1;
+          float l0, l1;
+          bilin_axis_s(wc, P, bsc, i0, i1, l0, l1);
+          wt[u] = w < hi ? (i0 == pj ? l0 : 0.f) + (i1 == pj ? l1 : 0.f) : 0.f;
+          load8<T>(row + (size_t)wc * C + c0, v[u]);
         }
 #pragma unroll
         for (int u = 0; u < 4; ++u)
-          if (wt[u] != 0.f)
 #pragma unroll
-            for (int q = 0; q < 8; ++q) acc[q] += wt[u] * v[u][q];
+          for (int q = 0; q < 8; ++q) acc[q] += wt[u] * v[u][q];
       }
     }
     if (nsl == 1) {
