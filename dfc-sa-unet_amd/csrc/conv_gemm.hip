@@ -3308,6 +3308,7 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 47: return g_lsa_pool_direct;
     case 48: return g_lsa_key_centre;
     case 49: return g_lsa_cols_flash;
+    case 50: return g_gn_chunk;
     case 36: return g_gate_grid_div;
     case 37: return g_splitk_min_nk;
     case 39: return g_bn_fold;
@@ -3353,6 +3354,7 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 47) { g_lsa_pool_direct = value ? 1 : 0; return 0; }
   if (knob == 48) { g_lsa_key_centre = value ? 1 : 0; return 0; }
   if (knob == 49) { g_lsa_cols_flash = value ? 1 : 0; return 0; }
+  if (knob == 50) { g_gn_chunk = value ? 1 : 0; return 0; }
   if (knob == 36) { g_gate_grid_div = value; return 0; }
   if (knob == 39) { g_bn_fold = value; return 0; }
   if (knob == 40) { g_ppsk = value; return 0; }

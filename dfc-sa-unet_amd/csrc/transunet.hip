@@ -452,8 +452,11 @@ __device__ __forceinline__ void gn_publish_row(const float (&acc)[NS][8], int C,
 
 // statistics + finalize: mr[b][0][g] = mean, mr[b][1][g] = rstd; scsh[b][0][c] = gamma_c*rstd,
 // scsh[b][1][c] = beta_c - mean*gamma_c*rstd (as gn_finalize_kernel)
+// Channel chunks (grid.z, CW = gn_chunk(C, G) channels each, whole groups): the last-arriver sums
+// S rows of 2 CW values instead of 2 C -- at C = 1024 its serial column sum was 24 rows x 2048 values
+// of write-through loads per image, most of a 23 us launch.  Rows [B][nck][S][2][CW].
 template <typename T>
-__global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G, int S, const T* __restrict__ y,
+__global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int CW, int G, int S, const T* __restrict__ y,
                                                            float* rows, unsigned* cnt, const float* __restrict__ gamma,
                                                            const float* __restrict__ beta, float eps, float* mr,
                                                            float* scsh) {
@@ -462,8 +465,8 @@ __global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G,
   __shared__ float grp[2 * 256];
   __shared__ int flag;
   double* tmp = (double*)red;
-  const int sl = blockIdx.x, b = blockIdx.y;
-  const int cpp = C >> 3, pl = 256 / cpp;
+  const int sl = blockIdx.x, b = blockIdx.y, kc = blockIdx.z, nck = gridDim.z, c0 = kc * CW;
+  const int cpp = CW >> 3, pl = 256 / cpp;
   const int lane_px = threadIdx.x / cpp, ck = threadIdx.x - lane_px * cpp;
   const bool active = lane_px < pl;
   const int per = (HW + S - 1) / S, p0 = sl * per, p1 = min(HW, p0 + per);
@@ -471,7 +474,7 @@ __global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G,
 #pragma unroll
   for (int q = 0; q < 8; ++q) acc[0][q] = acc[1][q] = 0.f;
   if (active) {
-    const T* yb = y + (size_t)b * HW * C + ck * 8;
+    const T* yb = y + (size_t)b * HW * C + c0 + ck * 8;
 #pragma unroll 4
     for (int p = p0 + lane_px; p < p1; p += pl) {
       float v[8];
@@ -483,15 +486,15 @@ __global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G,
       }
     }
   }
-  float* img = rows + (size_t)b * S * 2 * C;
-  gn_publish_row<2>(acc, C, cpp, pl, lane_px, ck, active, red, img + (size_t)sl * 2 * C);
-  if (!wg_last_of(cnt + b, S, &flag)) return;
-  gn_rows_colsum(img, S, C, ch, tmp);
-  const int Cg = C / G;
+  float* img = rows + ((size_t)b * nck + kc) * S * 2 * CW;
+  gn_publish_row<2>(acc, CW, cpp, pl, lane_px, ck, active, red, img + (size_t)sl * 2 * CW);
+  if (!wg_last_of(cnt + b * nck + kc, S, &flag)) return;
+  gn_rows_colsum(img, S, CW, ch, tmp);   // ch[k * CW + (c - c0)]
+  const int Cg = C / G, g0 = c0 / Cg, g1 = (c0 + CW) / Cg;
   const double n = (double)HW * Cg;
-  for (int g = threadIdx.x; g < G; g += 256) {
+  for (int g = g0 + (int)threadIdx.x; g < g1; g += 256) {
     double s0 = 0.0, q0 = 0.0;
-    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { s0 += ch[c]; q0 += ch[C + c]; }
+    for (int c = g * Cg; c < (g + 1) * Cg; ++c) { s0 += ch[c - c0]; q0 += ch[CW + c - c0]; }
     const double mean = s0 / n;
     double var = q0 / n - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -502,7 +505,7 @@ __global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G,
     grp[G + g] = rstd;
   }
   __syncthreads();
-  for (int c = threadIdx.x; c < C; c += 256) {
+  for (int c = c0 + (int)threadIdx.x; c < c0 + CW; c += 256) {
     const int g = c / Cg;
     const float sc = gamma[c] * grp[G + g];
     scsh[(size_t)b * 2 * C + c] = sc;
@@ -515,15 +518,15 @@ __global__ void __launch_bounds__(256) gn_stats_fin_kernel(int HW, int C, int G,
 // sum_b sum dz (last image, image order).  work: [B][2][C] doubles (hand-off of the images' sums).
 template <typename T>
 __global__ void __launch_bounds__(256) gn_bwd_reduce_fin_kernel(
-    int HW, int C, int G, int S, const T* __restrict__ dout, const T* __restrict__ mask, const T* __restrict__ y,
+    int HW, int C, int CW, int G, int S, const T* __restrict__ dout, const T* __restrict__ mask, const T* __restrict__ y,
     const float* __restrict__ mr, const float* __restrict__ gamma, float* rows, double* work, unsigned* cnt,
     float* coef, float* dgamma, float* dbeta) {
   __shared__ __attribute__((aligned(16))) float red[256 * 8];   // (also the colsum's [2][256] doubles)
   __shared__ double ch[2 * 1024];
   __shared__ int flag;
   double* tmp = (double*)red;
-  const int sl = blockIdx.x, b = blockIdx.y, B = gridDim.y;
-  const int cpp = C >> 3, pl = 256 / cpp;
+  const int sl = blockIdx.x, b = blockIdx.y, B = gridDim.y, kc = blockIdx.z, nck = gridDim.z, c0 = kc * CW;
+  const int cpp = CW >> 3, pl = 256 / cpp;
   const int lane_px = threadIdx.x / cpp, ck = threadIdx.x - lane_px * cpp;
   const bool active = lane_px < pl;
   const int per = (HW + S - 1) / S, p0 = sl * per, p1 = min(HW, p0 + per);
@@ -532,12 +535,12 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_fin_kernel(
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
     acc[0][q] = acc[1][q] = 0.f;
-    const int g = (ck * 8 + q) / Cg;
+    const int g = (c0 + ck * 8 + q) / Cg;
     mu[q] = active ? mr[(size_t)b * 2 * G + g] : 0.f;
     rs[q] = active ? mr[(size_t)b * 2 * G + G + g] : 0.f;
   }
   if (active) {
-    const size_t base = (size_t)b * HW * C + ck * 8;
+    const size_t base = (size_t)b * HW * C + c0 + ck * 8;
 #pragma unroll 4
     for (int p = p0 + lane_px; p < p1; p += pl) {
       const size_t off = base + (size_t)p * C;
@@ -557,30 +560,30 @@ __global__ void __launch_bounds__(256) gn_bwd_reduce_fin_kernel(
       }
     }
   }
-  float* img = rows + (size_t)b * S * 2 * C;
-  gn_publish_row<2>(acc, C, cpp, pl, lane_px, ck, active, red, img + (size_t)sl * 2 * C);
-  if (!wg_last_of(cnt + b, S, &flag)) return;
-  gn_rows_colsum(img, S, C, ch, tmp);
-  // this image's channel sums -> work[b] (hand-off to the last image); group coefficients
+  float* img = rows + ((size_t)b * nck + kc) * S * 2 * CW;
+  gn_publish_row<2>(acc, CW, cpp, pl, lane_px, ck, active, red, img + (size_t)sl * 2 * CW);
+  if (!wg_last_of(cnt + b * nck + kc, S, &flag)) return;
+  gn_rows_colsum(img, S, CW, ch, tmp);   // ch[k * CW + (c - c0)]
+  // this image's channel sums (of the chunk) -> work[b] (hand-off to the last image); group coefficients
   double* wb = work + (size_t)b * 2 * C;
-  for (int c = threadIdx.x; c < C; c += 256) {
-    st_sc1_d(wb + c, ch[c]);
-    st_sc1_d(wb + C + c, ch[C + c]);
+  for (int c = c0 + (int)threadIdx.x; c < c0 + CW; c += 256) {
+    st_sc1_d(wb + c, ch[c - c0]);
+    st_sc1_d(wb + C + c, ch[CW + c - c0]);
   }
   const double n = (double)HW * Cg;
-  for (int g = threadIdx.x; g < G; g += 256) {
+  for (int g = c0 / Cg + (int)threadIdx.x; g < (c0 + CW) / Cg; g += 256) {
     double a0 = 0.0, a1 = 0.0;
     for (int c = g * Cg; c < (g + 1) * Cg; ++c) {
       const double gm = (double)gamma[c];
-      a0 += gm * ch[c];
-      a1 += gm * ch[C + c];
+      a0 += gm * ch[c - c0];
+      a1 += gm * ch[CW + c - c0];
     }
     coef[(size_t)b * 2 * G + g] = (float)(a0 / n);
     coef[(size_t)b * 2 * G + G + g] = (float)(a1 / n);
   }
   if (!dgamma && !dbeta) return;
-  if (!wg_last_of(cnt + B, B, &flag)) return;
-  for (int c = threadIdx.x; c < C; c += 256) {
+  if (!wg_last_of(cnt + B * nck + kc, B, &flag)) return;
+  for (int c = c0 + (int)threadIdx.x; c < c0 + CW; c += 256) {
     double tb = 0.0, tg = 0.0;
     for (int bb = 0; bb < B; ++bb) {
       double v0, v1, v2;
@@ -2016,10 +2019,22 @@ extern "C" int dfcsa_gn_bwd_apply(int dtype, int B, int HW, int C, int G, const 
   return 0;
 }
 
+// channel chunk of the fused GroupNorm reductions: 128 channels (whole groups) when C > 128 splits so
+// (knob 50 = 0: one chunk, the round-5 layout), else all C
+int g_gn_chunk = 1;
+static int gn_chunk_w(int C) { return (g_gn_chunk && C > 128 && C % 128 == 0) ? 128 : C; }
+static int gn_chunk(int C, int G) {
+  const int Cg = (G > 0 && C % G == 0) ? C / G : 0;
+  const int cw = gn_chunk_w(C);
+  return (Cg > 0 && cw % Cg == 0) ? cw : C;
+}
+
 extern "C" int dfcsa_gn_nslices_fused(int B, int HW, int C) {
-  // about 512 workgroups over the batch, at least 4 pixels per pixel-lane, at most 64 slices
-  const int cpp = C / 8 > 0 ? C / 8 : 1, pl = std::max(1, 256 / cpp);
-  int s = (512 + std::max(1, B) - 1) / std::max(1, B);
+  // about 512 workgroups over the batch and the channel chunks, at least 4 pixels per pixel-lane, at
+  // most 64 slices (any S is valid for the launch: the rows buffer is B * S * 2C floats either way)
+  const int CW = gn_chunk_w(C), nck = C / CW;
+  const int cpp = CW / 8 > 0 ? CW / 8 : 1, pl = std::max(1, 256 / cpp);
+  int s = (512 + std::max(1, B * nck) - 1) / std::max(1, B * nck);
   s = std::min(s, 64);
   s = std::min(s, std::max(1, HW / (4 * pl)));
   return std::max(1, s);
@@ -2033,14 +2048,15 @@ extern "C" int dfcsa_gn_stats_fused(int dtype, int B, int HW, int C, int G, int 
                                     const float* gamma, const float* beta, float eps, float* mean_rstd,
                                     float* scale_shift, void* stream) {
   if (!gn_fused_ok(B, HW, C, G, S) || !rows) return DFCSA_EINVAL;
-  unsigned* cnt = dfcsa_ticket_alloc(B);
+  const int CW = gn_chunk(C, G), nck = C / CW;
+  unsigned* cnt = dfcsa_ticket_alloc(B * nck);
   if (!cnt) return DFCSA_EINVAL;
   if (dtype == DFCSA_DT_BF16)
-    hipLaunchKernelGGL(gn_stats_fin_kernel<bf16_t>, dim3(S, B), dim3(256), 0, (hipStream_t)stream, HW, C, G, S,
-                       (const bf16_t*)y, rows, cnt, gamma, beta, eps, mean_rstd, scale_shift);
+    hipLaunchKernelGGL(gn_stats_fin_kernel<bf16_t>, dim3(S, B, nck), dim3(256), 0, (hipStream_t)stream, HW, C, CW, G,
+                       S, (const bf16_t*)y, rows, cnt, gamma, beta, eps, mean_rstd, scale_shift);
   else
-    hipLaunchKernelGGL(gn_stats_fin_kernel<float>, dim3(S, B), dim3(256), 0, (hipStream_t)stream, HW, C, G, S,
-                       (const float*)y, rows, cnt, gamma, beta, eps, mean_rstd, scale_shift);
+    hipLaunchKernelGGL(gn_stats_fin_kernel<float>, dim3(S, B, nck), dim3(256), 0, (hipStream_t)stream, HW, C, CW, G,
+                       S, (const float*)y, rows, cnt, gamma, beta, eps, mean_rstd, scale_shift);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }
@@ -2050,14 +2066,17 @@ extern "C" int dfcsa_gn_bwd_reduce_fused(int dtype, int B, int HW, int C, int G,
                                          float* rows, double* work, float* coef, float* dgamma, float* dbeta,
                                          void* stream) {
   if (!gn_fused_ok(B, HW, C, G, S) || !rows || !work) return DFCSA_EINVAL;
-  unsigned* cnt = dfcsa_ticket_alloc(B + 1);
+  const int CW = gn_chunk(C, G), nck = C / CW;
+  unsigned* cnt = dfcsa_ticket_alloc((B + 1) * nck);
   if (!cnt) return DFCSA_EINVAL;
   if (dtype == DFCSA_DT_BF16)
-    hipLaunchKernelGGL(gn_bwd_reduce_fin_kernel<bf16_t>, dim3(S, B), dim3(256), 0, (hipStream_t)stream, HW, C, G, S,
+    hipLaunchKernelGGL(gn_bwd_reduce_fin_kernel<bf16_t>, dim3(S, B, nck), dim3(256), 0, (hipStream_t)stream, HW, C,
+                       CW, G, S,
                        (const bf16_t*)dout, (const bf16_t*)mask, (const bf16_t*)y, mean_rstd, gamma, rows, work, cnt,
                        coef, dgamma, dbeta);
   else
-    hipLaunchKernelGGL(gn_bwd_reduce_fin_kernel<float>, dim3(S, B), dim3(256), 0, (hipStream_t)stream, HW, C, G, S,
+    hipLaunchKernelGGL(gn_bwd_reduce_fin_kernel<float>, dim3(S, B, nck), dim3(256), 0, (hipStream_t)stream, HW, C,
+                       CW, G, S,
                        (const float*)dout, (const float*)mask, (const float*)y, mean_rstd, gamma, rows, work, cnt,
                        coef, dgamma, dbeta);
   DFCSA_CHECK_LAUNCH();

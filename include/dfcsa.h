@@ -686,9 +686,9 @@ int dfcsa_gn_bwd_apply(int dtype, int B, int HW, int C, int G, const void* dout,
                        const float* mean_rstd, const float* gamma, const float* coef, void* dy, void* dz_out,
                        void* stream);
 /* GroupNorm with the reductions finished inside the launch (round 5; replaces stats + finalize and
- * bwd_reduce + bwd_finalize, same outputs, C <= 1024, G <= 256): grid (S, B), S =
- * dfcsa_gn_nslices_fused(B, HW, C); rows [B][S][2][C] floats of hand-off scratch; the last
- * workgroup of each image finalises it.  bwd: work [B][2][C] doubles (the images' channel sums,
+ * bwd_reduce + bwd_finalize, same outputs, C <= 1024, G <= 256): grid (S, B, C / CW), S =
+ * dfcsa_gn_nslices_fused(B, HW, C), CW = 128 channels (whole groups) for C > 128, else C (round 6);
+ * rows: B * S * 2C floats of hand-off scratch; the last workgroup of each (image, chunk) finalises it.  bwd: work [B][2][C] doubles (the images' channel sums,
  * summed in image order by the last image into dgamma / dbeta). */
 int dfcsa_gn_nslices_fused(int B, int HW, int C);
 int dfcsa_gn_stats_fused(int dtype, int B, int HW, int C, int G, int S, const void* y, float* rows,
@@ -915,6 +915,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 47: 0 = large pools (P >= 16) on the sliced pool + pooled launches (default 1: dfcsa_lsa_pool_direct).
  * knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (default 1: dQ = sum_k dS (K_k - mean key)).
  * knob 49: 0 = the bf16 flash layers' column pass + separate prep (default 1: dfcsa_lsa_flash_bwd_up).
+ * knob 50: 0 = one channel chunk in the fused GroupNorm reductions (default 1: 128-channel chunks for C > 128).
  * dfcsa_get_tuning returns a knob's current value (DFCSA_EINVAL for an unknown knob). */
 int dfcsa_set_tuning(int knob, int value);
 int dfcsa_get_tuning(int knob);

@@ -43,12 +43,14 @@ def lib():
 @pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1e-2)])
 @pytest.mark.parametrize("B,C,G,H,eps", [(3, 64, 32, 14, 1e-6), (3, 256, 32, 7, 1e-6), (3, 64, 64, 9, 1e-5),
                                          (3, 32, 32, 5, 1e-6), (8, 1024, 32, 14, 1e-6), (8, 256, 32, 56, 1e-6),
-                                         (8, 64, 32, 112, 1e-6)])
+                                         (8, 64, 32, 112, 1e-6), (3, 256, 1, 7, 1e-6), (2, 512, 2, 9, 1e-6),
+                                         (2, 512, 16, 11, 1e-6)])
 def test_groupnorm_fwd_bwd(B, C, G, H, eps, dtype, tol, fused):
     """GroupNorm fwd (+ReLU) and bwd against F.group_norm + ReLU autograd: the fused launches
-    (dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused: the finalisation by each image's last
-    workgroup, dgamma / dbeta by the last image) and the four-launch path, at the test sizes and the
-    TransUNet bench's (B = 8: 14^2 x 1024, 56^2 x 256, 112^2 x 64); the fused path twice, bitwise."""
+    (dfcsa_gn_stats_fused / dfcsa_gn_bwd_reduce_fused: the finalisation by the last workgroup of each
+    image and 128-channel chunk, dgamma / dbeta by the last image) and the four-launch path, at the test
+    sizes and the TransUNet bench's (B = 8: 14^2 x 1024, 56^2 x 256, 112^2 x 64), plus groups wider than a
+    chunk (G = 1; C = 512, G = 2: one chunk); the fused path twice, bitwise."""
     from dfcsa import transunet_ops as TU
     torch.manual_seed(C + G + H)
     gn = torch.nn.GroupNorm(G, C, eps=eps).cuda()
