@@ -726,7 +726,9 @@ fra_bwd_dkv_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
 //   the query bias gradient, sum over queries) when the keys are alike, as pooled features are.  The
 //   row sums come from one more MFMA against a ones fragment, so the subtraction is exact in fp32.
 constexpr int kKeySlices = 8;   // key-sum partials per image (lsa_flash_prep_kernel)
-template <int CQ, int C, int WPE>
+// KCEN: the centred variant (kbar non-null); the other keeps the row-sum registers out of the
+// full-resolution attention's dQ kernel (config 5: 12 -> 40 spilled bytes per lane with them)
+template <int CQ, int C, int WPE, bool KCEN>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WPE)))
 fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
                                                        const bf16_t* __restrict__ dy, const float* __restrict__ gamma,
@@ -829,7 +831,7 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) dqa[qb][db] = mfma32(a, sb[qb], dqa[qb][db]);
       }
-      if (kbar) {   // column sums of the rounded dS^T tile (every row of rsum holds them)
+      if (KCEN) {   // column sums of the rounded dS^T tile (every row of rsum holds them)
 #pragma unroll
         for (int qb = 0; qb < 2; ++qb) rsum[qb] = mfma32(ones, sb[qb], rsum[qb]);
       }
@@ -850,7 +852,7 @@ fra_bwd_dq_mfma(int N, int ldq, int ldd, const bf16_t* __restrict__ qkv,
     for (int db = 0; db < NDB; ++db) {
       const int d = db * 16 + 4 * g;
       if (d < CQ) {
-        if (kbar) {   // kbar: kKeySlices partial key sums per image, [B][kKeySlices][CQ]
+        if (KCEN) {   // kbar: kKeySlices partial key sums per image, [B][kKeySlices][CQ]
           float4 kb = make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
           for (int ks = 0; ks < kKeySlices; ++ks) {
@@ -950,12 +952,21 @@ void launch_bwd(int B, int N, int ldq, int Ctot, const void* qkv, const void* dy
   else
     hipLaunchKernelGGL((fra_bwd_dkv_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
                        (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pk, rstride);
-  if (narrow && (occ & 4))
-    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1>), grid, dim3(256), 0, st, N, ldq, Ctot,
-                       (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
-  else
-    hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
-                       (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
+  if (narrow && (occ & 4)) {
+    if (kbar)
+      hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1, true>), grid, dim3(256), 0, st, N, ldq, Ctot,
+                         (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
+    else
+      hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, narrow ? WQ : 1, false>), grid, dim3(256), 0, st, N, ldq, Ctot,
+                         (const bf16_t*)qkv, (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
+  } else {
+    if (kbar)
+      hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1, true>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
+                         (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
+    else
+      hipLaunchKernelGGL((fra_bwd_dq_mfma<CQ, C, 1, false>), grid, dim3(256), 0, st, N, ldq, Ctot, (const bf16_t*)qkv,
+                         (const bf16_t*)dy, gamma, lse, rr, (bf16_t*)dqkv, pq, rstride, kbar);
+  }
 }
 
 template <int CQ>
