@@ -3303,7 +3303,6 @@ extern "C" int dfcsa_get_tuning(int knob) {
     case 33: return g_stream_min_m;
     case 34: return g_stream_shuf;
     case 35: return g_lsa_cols_nt;
-    case 45: return g_lsa_pool_wpb;
     case 46: return g_lsa_pool_one_slice;
     case 47: return g_lsa_pool_direct;
     case 48: return g_lsa_key_centre;
@@ -3349,7 +3348,6 @@ extern "C" int dfcsa_set_tuning(int knob, int value) {
   if (knob == 33) { g_stream_min_m = value; return 0; }
   if (knob == 34) { g_stream_shuf = value; return 0; }
   if (knob == 35) { g_lsa_cols_nt = value; return 0; }
-  if (knob == 45) { g_lsa_pool_wpb = value ? 1 : 0; return 0; }
   if (knob == 46) { g_lsa_pool_one_slice = value ? 1 : 0; return 0; }
   if (knob == 47) { g_lsa_pool_direct = value ? 1 : 0; return 0; }
   if (knob == 48) { g_lsa_key_centre = value ? 1 : 0; return 0; }

@@ -113,7 +113,6 @@ extern int g_lsa_key_centre;
 extern int g_lsa_cols_flash;
 extern int g_gn_chunk;   // knob 50: 128-channel chunks in the fused GroupNorm reductions (default 1)   // knob 49: fused column pass + prep for the bf16 flash layers (default 1)  // knob 48: mean-key centred dQ in the bf16 pooled-attention backward (default 1)
 extern int g_lsa_pool_one_slice;  // knob 46: small pool windows in one row slice (default 1)
-extern int g_lsa_pool_wpb;  // knob 45: several pool windows per workgroup at P >= 16 (off)
 extern int g_lsa_cols_nt;  // knob 35: 256 = the 256-thread LightSelfAttention upsample-backward column kernel
 extern int g_wgrad_nosimple;
 // n ticket counters for a last-arriver hand-off (ring in block_ew.hip; nullptr on failure)

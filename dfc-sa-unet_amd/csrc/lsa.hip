@@ -18,7 +18,6 @@
 
 int g_lsa_rows_old = 0;
 int g_lsa_cols_nt = 256;    // knob 35: threads of the upsample-backward column kernel at C <= 128 (256 = old)
-int g_lsa_pool_wpb = 0;     // knob 45: 1 = several pool windows per workgroup at P >= 16 (measured slower: off)
 int g_lsa_key_centre = 1;    // knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (old)
 int g_lsa_pool_direct = 1;   // knob 47: 0 = large pools on the sliced pool + pooled launches (old)
 int g_lsa_cols_flash = 1;    // knob 49: 0 = the bf16 flash layers' column pass + separate prep (old)
@@ -89,21 +88,17 @@ int pool_splits(int H, int P) {
   return s < 1 ? 1 : s;
 }
 
-// grid (S, ceil(N / wpb), B): row slice s of windows n = blockIdx.y * wpb + t (t < wpb) of image b.
-// One load in flight per lane at 45 VGPRs: occupancy hides the latency (an eight-loads-in-flight
-// variant at 108 VGPRs measured slower, profiles/r03c_lsa_bench.jsonl).  wpb > 1 (knob 45, off): large
-// pools' small windows (7 x 7 at P = 32 on 224^2) leave most of a one-window workgroup idle, but
-// batching windows serialises them per workgroup -- measured slower (614 -> 690 us per step at P = 32)
+// grid (S, N, B): row slice s of window n of image b.  One load in flight per lane at 45 VGPRs:
+// occupancy hides the latency (an eight-loads-in-flight variant at 108 VGPRs measured slower,
+// profiles/r03c_lsa_bench.jsonl).  Large pools' small windows take dfcsa_lsa_pool_direct (one wave per
+// window); batching several windows per workgroup here measured slower (614 -> 690 us per step at
+// P = 32, round 6) and was removed.
 template <typename T, bool WS = false>
 __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, const T* __restrict__ y2,
                                                        const float* __restrict__ sc, const float* __restrict__ sh,
-                                                       int P, int S, int wpb, int relu, float* __restrict__ partial,
+                                                       int P, int S, int relu, float* __restrict__ partial,
                                                        float* __restrict__ wpart) {
-  const int s = blockIdx.x, b = blockIdx.z;
-  for (int t = 0; t < wpb; ++t) {
-  const int n = blockIdx.y * wpb + t;
-  if (n >= P * P) break;
-  if (t) __syncthreads();   // the previous window's combine has read `red`
+  const int s = blockIdx.x, n = blockIdx.y, b = blockIdx.z;
   const int pi = n / P, pj = n - pi * P;
   const int hs = win_lo(pi, H, P), he = win_hi(pi, H, P);
   const int ws = win_lo(pj, W, P), we = win_hi(pj, W, P);
@@ -170,7 +165,6 @@ __global__ void __launch_bounds__(256) lsa_pool_kernel(int H, int W, int C, cons
       for (int p = 0; p < pl; ++p) v += red[q * stride + p * cpp + kk];
       out[kk * 8 + q] = v;
     }
-  }
   }
 }
 
@@ -902,26 +896,22 @@ extern "C" int dfcsa_lsa_pool_ws(int dtype, int B, int H, int W, int C, const vo
                                  const float* sh2, int P, int relu, float* partial, float* wpart, void* stream) {
   if (C % 8 || C > 2048 || P <= 0) return DFCSA_EINVAL;
   const int S = pool_splits(H, P);
-  // windows per workgroup: enough pixels per slice to fill the 256 / (C / 8) pixel lanes a few times
-  const int wpx = ((H + P - 1) / P) * ((W + P - 1) / P) / S;
-  const int lanes = 256 / std::max(1, C / 8);
-  const int wpb = (P >= 16 && g_lsa_pool_wpb) ? std::max(1, std::min(8, (2 * lanes) / std::max(1, wpx))) : 1;
-  dim3 grid(S, (P * P + wpb - 1) / wpb, B);
+  dim3 grid(S, P * P, B);
   hipStream_t st = (hipStream_t)stream;
   if (dtype == DFCSA_DT_BF16) {
     if (wpart)
       hipLaunchKernelGGL((lsa_pool_kernel<bf16_t, true>), grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2,
-                         sh2, P, S, wpb, relu, partial, wpart);
+                         sh2, P, S, relu, partial, wpart);
     else
       hipLaunchKernelGGL((lsa_pool_kernel<bf16_t, false>), grid, dim3(256), 0, st, H, W, C, (const bf16_t*)y2, sc2,
-                         sh2, P, S, wpb, relu, partial, wpart);
+                         sh2, P, S, relu, partial, wpart);
   } else {
     if (wpart)
       hipLaunchKernelGGL((lsa_pool_kernel<float, true>), grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2,
-                         P, S, wpb, relu, partial, wpart);
+                         P, S, relu, partial, wpart);
     else
       hipLaunchKernelGGL((lsa_pool_kernel<float, false>), grid, dim3(256), 0, st, H, W, C, (const float*)y2, sc2, sh2,
-                         P, S, wpb, relu, partial, wpart);
+                         P, S, relu, partial, wpart);
   }
   DFCSA_CHECK_LAUNCH();
   return 0;

@@ -910,7 +910,7 @@ int dfcsa_prof_read(int kernel_class, double* total_ms, int64_t* launches, doubl
  * knob 42: LDS-DMA ring depth of the buffer-descriptor weight-gradient kernel (2 = default, 3, 4).
  * knob 43: 1 = single-buffer C = 128 forward prologue GEMMs (two workgroups per CU; default 1).
  * knob 44: 1 = single-buffer KP = 256 fused gate dgrad kernels (two workgroups per CU).
- * knob 45: 1 = several LightSelfAttention pool windows per workgroup at P >= 16 (default 0: measured slower).
+ * knob 45: (removed in round 6: several pool windows per workgroup, measured slower).
  * knob 46: 0 = LightSelfAttention pool windows of <= 8 rows split into row slices too (default 1: one slice).
  * knob 47: 0 = large pools (P >= 16) on the sliced pool + pooled launches (default 1: dfcsa_lsa_pool_direct).
  * knob 48: 0 = uncentred dQ in the bf16 pooled-attention backward (default 1: dQ = sum_k dS (K_k - mean key)).
