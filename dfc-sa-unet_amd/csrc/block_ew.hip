@@ -70,6 +70,7 @@ struct EwArgs {
   // multiply-shift division; pool_exact: P divides H and W (one window per pixel, area pool_inv)
   DivMod dm_hw, dm_w, dm_ph, dm_pw;
   int pool_exact;
+  int tbl16;     // tbl holds bf16 values (the bf16 flash layers' dpooled), else fp32
   float pool_inv;
   float bil_sh, bil_sw;   // bilinear upsample source scales P / H, P / W (host-computed quotients)
 };
@@ -348,6 +349,18 @@ template <> struct NSums<EW_BWD_SUM_OUT> { static constexpr int v = 1; };
 // Attention-entry gradient of pixel m (channels c0..c0+7): the adaptive-avg-pool backward of
 // dpooled ([B][P][P][C] fp32), i.e. the sum over the pooling windows containing (h, w) of
 // dpooled / window size (windows rows [floor(i*H/P), ceil((i+1)*H/P)) as torch's adaptive pool).
+__device__ __forceinline__ void ld8_tbl(const EwArgs& a, size_t off, float (&v)[8]) {
+  if (a.tbl16) {
+    const uint4 u = *(const uint4*)((const bf16_t*)(const void*)a.tbl + off);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+    v[4] = __uint_as_float(u.z << 16); v[5] = __uint_as_float(u.z & 0xffff0000u);
+    v[6] = __uint_as_float(u.w << 16); v[7] = __uint_as_float(u.w & 0xffff0000u);
+  } else {
+    ld8f(a.tbl + off, v);
+  }
+}
+
 __device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, float (&add)[8]) {
   const int b = dm_div(a.dm_hw, m), rem = m - b * a.dm_hw.d, h = dm_div(a.dm_w, rem), w = rem - h * a.W;
   const int P = a.P;
@@ -356,7 +369,7 @@ __device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, flo
     // 1 / area as the general path below
     const int pi = dm_div(a.dm_ph, h), pj = dm_div(a.dm_pw, w);
     float v[8];
-    ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
+    ld8_tbl(a, ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
 #pragma unroll
     for (int q = 0; q < 8; ++q) add[q] = v[q] * a.pool_inv;
     return;
@@ -371,7 +384,7 @@ __device__ __forceinline__ void pool_bwd_add(const EwArgs& a, int m, int c0, flo
       const int ws = (pj * a.W) / P, we = ((pj + 1) * a.W + P - 1) / P;
       const float inv = 1.f / (float)((he - hs) * (we - ws));
       float v[8];
-      ld8f(a.tbl + ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
+      ld8_tbl(a, ((size_t)(b * P + pi) * P + pj) * a.C + c0, v);
 #pragma unroll
       for (int q = 0; q < 8; ++q) add[q] += v[q] * inv;
     }
@@ -1529,6 +1542,23 @@ extern "C" int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, c
   EwArgs a = zargs(B * H * W, C);
   a.B = B; a.H = H; a.W = W; a.P = P;
   a.a0 = dattn; a.a1 = y; a.tbl = dpooled; a.sc = sc; a.sh = sh; a.mean = mean; a.invstd = invstd; a.act = relu;
+  a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial; a.partial_cap = bias_partial_floats;
+  set_pool_geom(a);
+  return launch_red<EW_BN_BWD_APPLY_ENTRY>(dtype, a, (hipStream_t)stream);
+}
+
+extern "C" int dfcsa_bn_bwd_apply_entry16(int dtype, int B, int H, int W, int C, const void* dattn,
+                                          const void* dpooled16, int P, const void* y, const float* sc,
+                                          const float* sh, const float* mean, const float* invstd, int relu,
+                                          const float* gamma, const float* coef, void* dy, float* bias_partial,
+                                          int64_t bias_partial_floats, void* stream) {
+  if (!dattn || !dpooled16 || P <= 0 || !y || !sc || !sh || !mean || !invstd || !gamma || !coef || !dy ||
+      ((uintptr_t)dpooled16 & 15))
+    return DFCSA_EINVAL;
+  EwArgs a = zargs(B * H * W, C);
+  a.B = B; a.H = H; a.W = W; a.P = P;
+  a.a0 = dattn; a.a1 = y; a.tbl = (const float*)dpooled16; a.tbl16 = 1; a.sc = sc; a.sh = sh; a.mean = mean;
+  a.invstd = invstd; a.act = relu;
   a.gamma = gamma; a.coef = coef; a.o0 = dy; a.partial = bias_partial; a.partial_cap = bias_partial_floats;
   set_pool_geom(a);
   return launch_red<EW_BN_BWD_APPLY_ENTRY>(dtype, a, (hipStream_t)stream);

@@ -1250,8 +1250,9 @@ extern "C" int dfcsa_lsa_proj_bwd(int B, int N, int C, int Cq, const float* dqkv
 //   rows[bx][1][c] = sum_m dpooled[m][c] / area(m) * invstd[c] * (wsum[m][1][c] - mean[c] * wsum[m][0][c])
 // grid (ceil(BN / 16), ceil(C / 64)), 256 threads: 4 token phases x 64 channels, fixed-order combine.
 namespace {
+template <typename T>
 __global__ void __launch_bounds__(256) lsa_pool_rows_kernel(int BN, int C, int P, int H, int W,
-                                                            const float* __restrict__ dpooled,
+                                                            const T* __restrict__ dpooled,
                                                             const float* __restrict__ wsum,
                                                             const float* __restrict__ mean,
                                                             const float* __restrict__ invstd,
@@ -1268,7 +1269,7 @@ __global__ void __launch_bounds__(256) lsa_pool_rows_kernel(int BN, int C, int P
       const int n = m % NP, pi = n / P, pj = n - pi * P;
       const float area = (float)(((pi + 1) * H + P - 1) / P - (pi * H) / P) *
                          (float)(((pj + 1) * W + P - 1) / P - (pj * W) / P);
-      const float dd = dpooled[(size_t)m * C + c] / area;
+      const float dd = ElemTraits<T>::to_f(dpooled[(size_t)m * C + c]) / area;
       const float R = wsum[((size_t)m * 2) * C + c], Y = wsum[((size_t)m * 2 + 1) * C + c];
       s0 += dd * R;
       s1 += dd * is * (Y - mu * R);
@@ -1284,16 +1285,20 @@ __global__ void __launch_bounds__(256) lsa_pool_rows_kernel(int BN, int C, int P
 }
 }  // namespace
 
-extern "C" int dfcsa_lsa_pool_rows(int BN, int C, int P, int H, int W, const float* dpooled, const float* wsum,
-                                   const float* mean, const float* invstd, float* rows, int64_t rows_floats,
-                                   void* stream) {
+extern "C" int dfcsa_lsa_pool_rows(int dtype, int BN, int C, int P, int H, int W, const void* dpooled,
+                                   const float* wsum, const float* mean, const float* invstd, float* rows,
+                                   int64_t rows_floats, void* stream) {
   if (BN <= 0 || C <= 0 || P <= 0 || H <= 0 || W <= 0 || BN % (P * P) || !dpooled || !wsum || !mean || !invstd ||
       !rows)
     return DFCSA_EINVAL;
   const int nb = (BN + 15) / 16;
   if (rows_floats < (int64_t)nb * 2 * C) return DFCSA_EINVAL;
-  hipLaunchKernelGGL(lsa_pool_rows_kernel, dim3(nb, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, BN, C, P, H, W,
-                     dpooled, wsum, mean, invstd, rows);
+  if (dtype == DFCSA_DT_BF16)
+    hipLaunchKernelGGL(lsa_pool_rows_kernel<bf16_t>, dim3(nb, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, BN, C,
+                       P, H, W, (const bf16_t*)dpooled, wsum, mean, invstd, rows);
+  else
+    hipLaunchKernelGGL(lsa_pool_rows_kernel<float>, dim3(nb, (C + 63) / 64), dim3(256), 0, (hipStream_t)stream, BN, C,
+                       P, H, W, (const float*)dpooled, wsum, mean, invstd, rows);
   DFCSA_CHECK_LAUNCH();
   return 0;
 }

@@ -665,6 +665,11 @@ LSA_FLASH_MIN_N = [int(os.environ.get("DFCSA_LSA_FLASH_MIN_N", "32"))]
 LSA_FLASH_FP32 = [os.environ.get("DFCSA_LSA_FLASH_FP32", "0") == "1"]
 
 
+# bf16 flash layers on the window-sum path: the projection dgrad's bf16 dpooled is read as it is by the
+# entry's pool rows and BatchNorm apply (DFCSA_LSA_DP16=0: widened to fp32 first; same-box +0.4-0.7 % at
+# P = 8 / 16 / 32, profiles/r06dp16_ab.txt; gradients bitwise equal)
+LSA_DP16 = [os.environ.get("DFCSA_LSA_DP16", "1") == "1"]
+
 # pooled attention with N > 64 tokens: dgamma of the upsample backward as a separate sum over per-token
 # partials instead of the in-kernel ticket (DFCSA_LSA_DGAMMA_SPLIT=0: in-kernel, N / 64 tokens per
 # workgroup)
@@ -816,11 +821,14 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
              P(gpart), P(work), ctypes.c_int64(work.numel() * 4), stream())
         del work
         call("dfcsa_sum_to_scalar", P(gpart), B * N, P(grad_of(lsa.gamma)), stream())
-        dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
+        # with the entry's pool rows (the window-sum path) the bf16 dpooled is consumed as it is (the
+        # rows kernel here, dfcsa_bn_bwd_apply_entry16 after the finalize): no fp32 widening pass
+        dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk,
+                                     widen=pool_rows is None or not LSA_DP16[0])
         if pool_rows is not None:   # the attention entry's pool-backward BatchNorm rows
             wsum, mean, invstd, rows_ptr, Hh, Ww = pool_rows
-            call("dfcsa_lsa_pool_rows", B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum), P(mean), P(invstd),
-                 rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
+            call("dfcsa_lsa_pool_rows", dt(dpooled.dtype), B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum), P(mean),
+                 P(invstd), rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
         return dpooled
     else:
         dO = torch.empty((B, N, C), device=dev, dtype=f32)
@@ -847,11 +855,12 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
                  P(dqkv), P(work), ctypes.c_int64(work.numel() * 4), stream())
             del work
             if f16:
-                dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk)
+                dpooled = _lsa_proj_bwd_bf16(lsa, A.pooled16, dqkv, B, N, C, Cq, pk,
+                                             widen=pool_rows is None or not LSA_DP16[0])
                 if pool_rows is not None:   # the attention entry's pool-backward BatchNorm rows
                     wsum, mean, invstd, rows_ptr, Hh, Ww = pool_rows
-                    call("dfcsa_lsa_pool_rows", B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum), P(mean), P(invstd),
-                         rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
+                    call("dfcsa_lsa_pool_rows", dt(dpooled.dtype), B * N, C, Pp, Hh, Ww, P(dpooled), P(wsum),
+                         P(mean), P(invstd), rows_ptr, ctypes.c_int64((B * N + 15) // 16 * 2 * C), stream())
                 return dpooled
         else:
             dE = torch.empty((B, N, N), device=dev, dtype=f32)
@@ -874,10 +883,11 @@ def lsa_core_backward(lsa, saved, dattn, pool_size, dtype, pk, pool_rows=None):
     return dpooled
 
 
-def _lsa_proj_bwd_bf16(lsa, pooled16, dqkv16, B, N, C, Cq, pk):
+def _lsa_proj_bwd_bf16(lsa, pooled16, dqkv16, B, N, C, Cq, pk, widen=True):
     """Backward of the bf16 q/k/v projections of a flash layer: dW = dqkv^T pooled (bf16 weight-gradient
     GEMM into the fp32 gradients, stacked q/k/v rows -> three tensors), db = column sums of dqkv,
-    dpooled = dqkv Wqkv (bf16 implicit GEMM, widened to fp32 for the attention-entry backward)."""
+    dpooled = dqkv Wqkv (bf16 implicit GEMM; widened to fp32 for the attention-entry backward unless
+    widen is False -- the window-sum path's consumers read the bf16 values as they are)."""
     dev = dqkv16.device
     f32, bf = torch.float32, torch.bfloat16
     J, BN = 2 * Cq + C, B * N
@@ -891,6 +901,8 @@ def _lsa_proj_bwd_bf16(lsa, pooled16, dqkv16, B, N, C, Cq, pk):
          P(grad_of(lsa.key_conv.bias)), P(grad_of(lsa.value_conv.bias)), stream())
     dp16 = torch.empty((B, N, C), device=dev, dtype=bf)
     ops.conv_gemm(bf, [(dqkv16, 0, 0)], J, (1, BN, 1), (BN, 1), pk["WT16"], rup(J, ops.KALIGN), C, [dp16], C)
+    if not widen:
+        return dp16
     dpooled = torch.empty((B, N, C), device=dev, dtype=f32)
     call("dfcsa_bf16_to_f32", ctypes.c_int64(BN * C), P(dp16), P(dpooled), stream())
     return dpooled

@@ -418,7 +418,9 @@ def bn_bwd_apply_entry(dtype, dattn, dpooled, P_, y, bn, relu, gamma, coef, bias
     if bias_grad is not None and NUMERIC_BN_BIAS_GRAD:
         nt = ntiles_ew(M, C)
         part = torch.empty(nt * C, device=dattn.device, dtype=torch.float32)
-    call("dfcsa_bn_bwd_apply_entry", dt(dtype), B, H, W, C, P(dattn), P(dpooled), P_, P(y), P(bn.scale),
+    # dpooled in bf16: the flash layers' projection dgrad output, read as it is
+    fn = "dfcsa_bn_bwd_apply_entry16" if dpooled.dtype == torch.bfloat16 else "dfcsa_bn_bwd_apply_entry"
+    call(fn, dt(dtype), B, H, W, C, P(dattn), P(dpooled), P_, P(y), P(bn.scale),
          P(bn.shift), P(bn.mean), P(bn.invstd), int(relu), P(gamma), P(coef), P(dy), *S(part), stream())
     if part is not None:
         colsum_into(part, nt, C, bias_grad)

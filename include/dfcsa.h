@@ -432,6 +432,11 @@ int dfcsa_bn_bwd_apply_entry(int dtype, int B, int H, int W, int C, const void* 
                              const void* y, const float* sc, const float* sh, const float* mean,
                              const float* invstd, int relu, const float* gamma, const float* coef, void* dy,
                              float* bias_partial, int64_t bias_partial_floats, void* stream);
+/* the same with dpooled in bf16 (the bf16 flash layers' projection dgrad output as it is; 16-B aligned) */
+int dfcsa_bn_bwd_apply_entry16(int dtype, int B, int H, int W, int C, const void* dattn, const void* dpooled16, int P,
+                               const void* y, const float* sc, const float* sh, const float* mean,
+                               const float* invstd, int relu, const float* gamma, const float* coef, void* dy,
+                               float* bias_partial, int64_t bias_partial_floats, void* stream);
 /* Two-stage reduction helper for per-tile slabs: dst[g][j] = sum of rows t in group g of
  * src[t][j] (T rows of rowlen floats, G groups of ceil(T/G) consecutive rows).  The finalize
  * entry points then reduce G rows instead of T.  dst: [G][rowlen] fp32 (caller scratch). */
@@ -494,10 +499,10 @@ int dfcsa_lsa_flash_bwd_bytes(int dtype, int B, int N, int C, int Cq, int ldq, i
 int dfcsa_lsa_flash_bwd(int dtype, int B, int N, int C, int Cq, int ldq, const void* qkv, const float* dO,
                         const float* o, const float* lse, void* dqkv, void* work, int64_t work_bytes, void* stream);
 /* The attention entry's pool-backward BatchNorm sums as ceil(BN/16) partial rows [row][2][C] (the rows
- * dfcsa_conv_wgrad_dgrad1x1_pool's epilogue adds for the fp32 projections), from dpooled [BN][C] and the
- * forward's window sums wsum [BN][2][C]: for the bf16 projections of the flash layers.  rows_floats:
- * capacity of rows in floats. */
-int dfcsa_lsa_pool_rows(int BN, int C, int P, int H, int W, const float* dpooled, const float* wsum,
+ * dfcsa_conv_wgrad_dgrad1x1_pool's epilogue adds for the fp32 projections), from dpooled [BN][C] (dtype:
+ * fp32, or bf16 -- the flash layers' projection dgrad output as it is) and the forward's window sums
+ * wsum [BN][2][C]: for the bf16 projections of the flash layers.  rows_floats: capacity of rows in floats. */
+int dfcsa_lsa_pool_rows(int dtype, int BN, int C, int P, int H, int W, const void* dpooled, const float* wsum,
                         const float* mean, const float* invstd, float* rows, int64_t rows_floats, void* stream);
 /* bf16 flash layers: dfcsa_lsa_up_bwd_cols (gamma_grad NULL) + dfcsa_lsa_flash_bwd in one call, the
  * column pass writing the flash backward's bf16 dO and r itself (one wave per token; the fp32 dO is never

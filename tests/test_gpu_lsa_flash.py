@@ -283,3 +283,36 @@ def test_flash_bwd_up_matches_separate_passes(C, P, H, B):
     assert rel(gp1, gp2) < 1e-5
     for a, b_ in zip(d1.float().split([Cq, Cq, C], -1), d2.float().split([Cq, Cq, C], -1)):
         assert rel(a, b_) < 5e-3
+
+
+@pytest.mark.parametrize("P", [8, 32])
+def test_bf16_dpooled_path_is_bitwise_the_widened_one(P, monkeypatch):
+    """The window-sum path of a bf16 flash layer reads the projection dgrad's bf16 dpooled as it is
+    (dfcsa_lsa_pool_rows with dtype bf16, dfcsa_bn_bwd_apply_entry16) instead of widening it to fp32 first
+    (DFCSA_LSA_DP16=0): bf16 -> fp32 is exact, so the whole train step's gradients are bitwise equal."""
+    from dfcsa import block
+    from dfcsa.loss import sigmoid
+    from models.unet_dfc_sa_res import UNetDFCSARes
+    from utils.metrics import calculate_metrics
+    torch.manual_seed(900 + P)
+    m0 = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=P, precision="bf16")
+    with torch.no_grad():
+        for n, p in m0.named_parameters():
+            if n.endswith("gamma"):
+                p.fill_(0.4)
+    sd = {k: v.detach().clone() for k, v in m0.state_dict().items()}
+    g0 = torch.Generator().manual_seed(910 + P)
+    x = torch.randn(2, 3, 64, 64, generator=g0)
+    t = (torch.rand(2, 1, 64, 64, generator=g0) > 0.5).float()
+    grads = []
+    for on in (True, False):
+        monkeypatch.setattr(block, "LSA_DP16", [on])
+        m = UNetDFCSARes(3, 1, [64, 128, 256, 512], pool_size=P, precision="bf16")
+        m.load_state_dict(sd)
+        m = m.cuda().train()
+        met = calculate_metrics(sigmoid(m(x.cuda())), t.cuda(), "bce_dice", {})
+        met["loss"].backward()
+        torch.cuda.synchronize()
+        grads.append({n: p.grad.detach().clone() for n, p in m.named_parameters()})
+    for n in grads[0]:
+        assert torch.equal(grads[0][n], grads[1][n]), n
